@@ -1,0 +1,16 @@
+"""Native MapReduce ops: the HIP/CDNA4 engine (map / shuffle / reduce kernels), CPU paths."""
+from .engine import (  # noqa: F401
+    Comm,
+    Engine,
+    Result,
+    cpu_count,
+    cpu_count_compat,
+    default_options,
+    device_count,
+    format_output,
+    loopback_count,
+    shard_range,
+    shard_range_file,
+    synth_host,
+)
+from ._lib import LIB_PATH, WcError  # noqa: F401

@@ -1,0 +1,221 @@
+"""Python face of the native engine (src/engine/engine.cpp) and CPU paths.
+
+Reference parity: the whole reference pipeline is ``runMapReduce``
+(/root/reference/main.cu:133-162) fed by the host tokenizer (main.cu:181-206);
+``Engine.count_*`` + ``Engine.result`` are its MI355X-native equivalent.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from ._lib import Options, check, check_ptr, lib
+
+_P8 = ctypes.POINTER(ctypes.c_uint8)
+_P64 = ctypes.POINTER(ctypes.c_uint64)
+
+
+def _u8ptr(buf) -> "ctypes._Pointer":
+    arr = np.frombuffer(buf, dtype=np.uint8) if not isinstance(buf, np.ndarray) else buf
+    return arr.ctypes.data_as(_P8), arr
+
+
+@dataclass
+class Result:
+    """Distinct words in first-occurrence order with their counts."""
+
+    words: List[bytes] = field(default_factory=list)
+    counts: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint64))
+    first_off: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint64))
+    total: int = 0
+
+    def __len__(self) -> int:
+        return len(self.words)
+
+    def as_dict(self) -> dict:
+        return {w: int(c) for w, c in zip(self.words, self.counts)}
+
+    def rows(self):
+        return list(zip(self.words, (int(c) for c in self.counts)))
+
+    @classmethod
+    def _from_native(cls, p) -> "Result":
+        try:
+            n = lib.wc_result_size(p)
+            nb = lib.wc_result_bytes(p)
+            counts = np.zeros(n, np.uint64)
+            first = np.zeros(n, np.uint64)
+            offs = np.zeros(n + 1, np.uint64)
+            blob = ctypes.create_string_buffer(max(nb, 1))
+            lib.wc_result_export(p, counts.ctypes.data_as(_P64), first.ctypes.data_as(_P64), offs.ctypes.data_as(_P64), blob)
+            raw = blob.raw
+            words = [raw[int(offs[i]) : int(offs[i + 1])] for i in range(n)]
+            res = cls(words, counts, first, int(lib.wc_result_total(p)))
+            return res
+        finally:
+            lib.wc_result_free(p)
+
+
+def format_output(res: Result, echo: Optional[bytes] = None, list_rows: bool = True, top_k: int = 0) -> bytes:
+    """Reference-identical framing (/root/reference/main.cu:166-218)."""
+    out = bytearray(b"Input Data:\n")
+    if echo:
+        out += echo
+    out += b"-" * 26 + b"\n"
+    if list_rows:
+        idx = range(len(res))
+        if top_k and top_k < len(res):
+            order = sorted(range(len(res)), key=lambda i: (-int(res.counts[i]), int(res.first_off[i])))
+            idx = order[:top_k]
+        for i in idx:
+            out += res.words[i] + b"\t" + str(int(res.counts[i])).encode() + b"\n"
+    out += b"-" * 26 + b"\n"
+    out += b"Total Count:" + str(res.total).encode() + b"\n"
+    return bytes(out)
+
+
+def default_options(**kw) -> Options:
+    o = Options()
+    lib.wc_default_options(ctypes.byref(o))
+    for k, v in kw.items():
+        if not hasattr(o, k):
+            raise TypeError(f"unknown engine option {k!r}")
+        setattr(o, k, v)
+    return o
+
+
+def device_count() -> int:
+    return int(lib.wc_device_count())
+
+
+class Comm:
+    """RCCL communicator owned by the native engine (one rank per GPU)."""
+
+    def __init__(self, unique_id: bytes, rank: int, size: int, device: int):
+        buf = ctypes.create_string_buffer(unique_id, 128)
+        self._p = check_ptr(lib.wc_comm_rccl_create(buf, rank, size, device))
+        self.rank, self.size = rank, size
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(128)
+        check(lib.wc_rccl_unique_id(buf))
+        return buf.raw
+
+    def close(self) -> None:
+        if getattr(self, "_p", None):
+            lib.wc_comm_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        self.close()
+
+
+class Engine:
+    """One GPU's MapReduce engine: count text, then merge / order / download."""
+
+    def __init__(self, device: int = 0, **opts):
+        self.options = default_options(device=device, **opts)
+        self._p = check_ptr(lib.wc_engine_create(ctypes.byref(self.options)))
+        self._resident = 0
+
+    def close(self) -> None:
+        if getattr(self, "_p", None):
+            lib.wc_engine_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def reset(self) -> None:
+        check(lib.wc_engine_reset(self._p))
+
+    def count_bytes(self, data: bytes, global_base: int = 0) -> None:
+        """Host text, streamed through the pinned ring (H2D overlapped)."""
+        ptr, keep = _u8ptr(data)
+        check(lib.wc_count_host(self._p, ptr, len(keep), global_base))
+
+    def count_file(self, path: str, begin: int = 0, end: Optional[int] = None, global_base: Optional[int] = None) -> None:
+        import os
+
+        if end is None:
+            end = os.path.getsize(path)
+        check(lib.wc_count_file(self._p, path.encode(), begin, end, begin if global_base is None else global_base))
+
+    def count_replay(self, pool: np.ndarray, total: int, global_base: int = 0) -> None:
+        """Replay a host pool of self-contained chunks until `total` bytes (host-staged config)."""
+        ptr, keep = _u8ptr(pool)
+        check(lib.wc_count_replay(self._p, ptr, len(keep), total, global_base))
+
+    def synth_device(self, nbytes: int, first_segment: int = 0, seed: int = 1, vocab: int = 100000, zipf_s: float = 1.0) -> None:
+        """Generate synthetic text directly in HBM (no host/PCIe involvement)."""
+        check(lib.wc_synth_device(self._p, nbytes, first_segment, seed, vocab, zipf_s))
+        self._resident = nbytes
+
+    def count_resident(self, nbytes: Optional[int] = None, global_base: int = 0) -> None:
+        check(lib.wc_count_resident(self._p, self._resident if nbytes is None else nbytes, global_base))
+
+    def finalize_device(self, comm: Optional[Comm] = None) -> int:
+        n = ctypes.c_uint64(0)
+        check(lib.wc_finalize_device(self._p, comm._p if comm else None, ctypes.byref(n)))
+        return int(n.value)
+
+    def result(self, comm: Optional[Comm] = None, all_ranks: bool = False) -> Result:
+        return Result._from_native(check_ptr(lib.wc_engine_result(self._p, comm._p if comm else None, int(all_ranks))))
+
+    def stats(self) -> dict:
+        buf = ctypes.create_string_buffer(2048)
+        lib.wc_engine_stats_json(self._p, buf, len(buf))
+        return json.loads(buf.value.decode())
+
+
+# ---------------------------------------------------------------- CPU paths --
+def cpu_count(data: bytes, global_base: int = 0) -> Result:
+    """Single-thread CPU oracle (BASELINE config 1)."""
+    ptr, keep = _u8ptr(data)
+    return Result._from_native(check_ptr(lib.wc_cpu_count(ptr, len(keep), global_base)))
+
+
+def cpu_count_compat(data: bytes) -> Result:
+    """The reference program's exact quirks."""
+    ptr, keep = _u8ptr(data)
+    return Result._from_native(check_ptr(lib.wc_cpu_count_compat(ptr, len(keep))))
+
+
+def synth_host(nbytes: int, first_segment: int = 0, seed: int = 1, vocab: int = 100000, zipf_s: float = 1.0) -> bytes:
+    """Host copy of the synthetic stream (bit-identical to the device generator)."""
+    out = np.zeros(nbytes, np.uint8)
+    check(lib.wc_synth_host(out.ctypes.data_as(_P8), nbytes, first_segment, seed, vocab, zipf_s))
+    return out.tobytes()
+
+
+def shard_range(data: bytes, rank: int, world: int):
+    """Ownership-adjusted [begin, end) of shard `rank` (token owned by its first byte)."""
+    ptr, keep = _u8ptr(data)
+    b, e = ctypes.c_uint64(), ctypes.c_uint64()
+    check(lib.wc_shard_range_mem(ptr, len(keep), rank, world, ctypes.byref(b), ctypes.byref(e)))
+    return int(b.value), int(e.value)
+
+
+def shard_range_file(path: str, rank: int, world: int):
+    b, e = ctypes.c_uint64(), ctypes.c_uint64()
+    check(lib.wc_shard_range_file(path.encode(), rank, world, ctypes.byref(b), ctypes.byref(e)))
+    return int(b.value), int(e.value)
+
+
+def loopback_count(data: bytes, ranks: int, devices: Optional[Sequence[int]] = None, **opts) -> Result:
+    """`ranks` virtual ranks (threads) on `devices` count shards and merge in-process."""
+    ptr, keep = _u8ptr(data)
+    devs = (ctypes.c_int * ranks)(*(devices if devices is not None else [0] * ranks))
+    o = default_options(**opts)
+    return Result._from_native(check_ptr(lib.wc_loopback_count(ptr, len(keep), ranks, devs, ctypes.byref(o))))

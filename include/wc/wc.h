@@ -1,0 +1,79 @@
+/* wc.h — C ABI of libwc (used by the Python package through ctypes).
+ * Every function returning int returns 0 on success and -1 on error; the
+ * message is available from wc_last_error() (thread-local). */
+#ifndef WC_C_API_H
+#define WC_C_API_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct wc_engine wc_engine;
+typedef struct wc_result wc_result;
+typedef struct wc_comm wc_comm;
+
+typedef struct wc_options {
+  int32_t device;
+  uint32_t log2_rec_buckets;
+  uint32_t log2_tab_buckets;
+  uint32_t max_log2_tab_buckets;
+  uint32_t map_blocks;
+  uint32_t staging_buffers;
+  uint64_t chunk_bytes;
+  uint64_t arena_bytes;
+  uint64_t min_records;
+  double records_per_byte;
+} wc_options;
+
+const char* wc_last_error(void);
+const char* wc_version(void);
+int wc_device_count(void);
+void wc_default_options(wc_options* o);
+
+wc_engine* wc_engine_create(const wc_options* o);
+void wc_engine_destroy(wc_engine* e);
+int wc_engine_reset(wc_engine* e);
+int wc_count_host(wc_engine* e, const uint8_t* text, uint64_t n, uint64_t global_base);
+int wc_count_file(wc_engine* e, const char* path, uint64_t begin, uint64_t end, uint64_t global_base);
+int wc_count_replay(wc_engine* e, const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t global_base);
+/* Generate synthetic text into the engine's device text buffer ... */
+int wc_synth_device(wc_engine* e, uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double zipf_s);
+/* ... and count [0, n) of it. */
+int wc_count_resident(wc_engine* e, uint64_t n, uint64_t global_base);
+int wc_finalize_device(wc_engine* e, wc_comm* comm, uint64_t* n_keys);
+wc_result* wc_engine_result(wc_engine* e, wc_comm* comm, int all_ranks);
+/* JSON object with the engine's Stats. Returns required length. */
+int wc_engine_stats_json(wc_engine* e, char* buf, int cap);
+int wc_engine_sync(wc_engine* e);
+
+/* results */
+uint64_t wc_result_size(const wc_result* r);
+uint64_t wc_result_total(const wc_result* r);
+uint64_t wc_result_bytes(const wc_result* r);
+void wc_result_export(const wc_result* r, uint64_t* counts, uint64_t* first_off, uint64_t* word_off, char* bytes);
+void wc_result_free(wc_result* r);
+/* reference output framing; *out must be released with wc_free */
+int wc_format(const wc_result* r, const uint8_t* echo, uint64_t echo_len, int echo_input, int list_rows,
+              uint64_t top_k, char** out, uint64_t* out_len);
+void wc_free(void* p);
+
+/* CPU paths */
+wc_result* wc_cpu_count(const uint8_t* text, uint64_t n, uint64_t global_base);
+wc_result* wc_cpu_count_compat(const uint8_t* text, uint64_t n);
+int wc_synth_host(uint8_t* out, uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double zipf_s);
+int wc_shard_range_mem(const uint8_t* text, uint64_t n, int rank, int world, uint64_t* begin, uint64_t* end);
+int wc_shard_range_file(const char* path, int rank, int world, uint64_t* begin, uint64_t* end);
+
+/* communicators */
+int wc_rccl_unique_id(char out[128]);
+wc_comm* wc_comm_rccl_create(const char* unique_id, int rank, int size, int device);
+void wc_comm_destroy(wc_comm* c);
+/* N virtual ranks on `devices` (one thread each) count shards of `text` and
+ * merge through the loopback communicator; returns rank 0's result. */
+wc_result* wc_loopback_count(const uint8_t* text, uint64_t n, int ranks, const int* devices, const wc_options* o);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,120 @@
+// wc.hpp — public C++ API of the MI355X-native MapReduce word-count engine.
+//
+// Capability parity with the reference (/root/reference/main.cu): count
+// whitespace-delimited words of a text and report `word<TAB>count` in
+// first-occurrence order plus the total (main.cu:208-218).  Semantics are the
+// reference's on its safe envelope, without its limits.
+#pragma once
+#include <stdint.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace wc {
+
+// Final result: one row per distinct word, ordered by first occurrence.
+struct KeyTable {
+  std::vector<std::string> words;
+  std::vector<uint64_t> counts;
+  std::vector<uint64_t> first_off;  // global byte offset of the first occurrence
+  uint64_t total = 0;               // sum of counts == number of tokens
+  size_t size() const { return words.size(); }
+};
+
+struct Stats {
+  uint64_t bytes = 0;     // text bytes ingested
+  uint64_t tokens = 0;    // words counted (device counter)
+  uint64_t keys = 0;      // distinct words (local, before merge)
+  uint32_t chunks = 0;    // map/reduce chunk passes
+  uint32_t map_reruns = 0;     // shuffle-region overflow -> chunk halved
+  uint32_t table_splits = 0;   // running table grew B -> 2B
+  uint32_t log2_buckets = 0;   // final table buckets
+  double h2d_ms = 0, map_reduce_ms = 0, finalize_ms = 0, merge_ms = 0;
+};
+
+struct Options {
+  int device = 0;
+  uint64_t chunk_bytes = 1ull << 30;   // device chunk (<= 4 GiB: records carry u32 offsets)
+  uint32_t log2_rec_buckets = 8;       // shuffle partitions
+  uint32_t log2_tab_buckets = 8;       // initial running-table buckets (x4096 slots)
+  uint32_t max_log2_tab_buckets = 16;
+  uint64_t min_records = 1ull << 21;   // floor of shuffle record capacity per chunk
+  double records_per_byte = 0.25;      // shuffle record capacity per chunk byte
+  uint64_t arena_bytes = 256ull << 20; // key arena for >8-byte words
+  uint32_t map_blocks = 0;             // 0 = 2 per CU
+  uint32_t staging_buffers = 3;        // pinned host ring depth (host-staged path)
+};
+
+// Synthetic text spec (see src/kernels/synth.hpp).
+struct SynthSpec {
+  uint64_t seed = 1;
+  uint32_t vocab = 100000;
+  double zipf_s = 1.0;
+};
+
+// Supplies host text chunks for the streaming (host-staged) path.
+class ChunkSource {
+ public:
+  virtual ~ChunkSource() = default;
+  // Fill up to `cap` bytes; return bytes written (0 = end).  The engine cuts
+  // chunks at the last delimiter and carries the remainder forward.
+  virtual uint64_t read(uint8_t* dst, uint64_t cap) = 0;
+};
+
+class Comm;  // dist/comm.hpp
+
+class Engine {
+ public:
+  explicit Engine(const Options& opt);
+  ~Engine();
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+
+  const Options& options() const;
+  Stats& stats();
+  void reset();  // empty the running table (keeps allocations)
+
+  // Text already resident in HBM (16-B aligned).  Tokens owned by this call are
+  // those starting in [0, n); bytes in [n, avail) may be read to finish them.
+  void count_device(const uint8_t* d_text, uint64_t n, uint64_t avail, uint64_t global_base, int prev_byte = ' ');
+  // Host text: staged through a pinned ring, H2D overlapped with compute.
+  void count_host(const uint8_t* h_text, uint64_t n, uint64_t global_base);
+  // Streaming source (files larger than HBM, replayed synthetic chunks).
+  void count_source(ChunkSource& src, uint64_t global_base);
+
+  // Device-resident synthetic text: allocates (or reuses) a buffer of n bytes
+  // holding segments [first_segment, ...) of the spec's stream.
+  const uint8_t* synth_device(uint64_t n, uint64_t first_segment, const SynthSpec& spec);
+
+  // Merge with other ranks (comm may be null), order by first occurrence and
+  // download.  Only rank 0 receives rows unless all_ranks.
+  KeyTable result(Comm* comm = nullptr, bool all_ranks = false);
+
+  // Device-side finalisation only (no download): returns distinct keys.  Used
+  // by the benchmark to time the full pipeline to an ordered device table.
+  uint64_t finalize_device(Comm* comm = nullptr);
+
+  struct Impl;
+
+ private:
+  std::unique_ptr<Impl> p_;
+};
+
+// ---- host components ----------------------------------------------------------
+namespace cpu {
+// Single-thread oracle (BASELINE config 1): hash map keyed by the word bytes.
+KeyTable count(const uint8_t* text, uint64_t n, uint64_t global_base = 0);
+// The reference program's exact quirks (prefix compare, 99-byte fgets records,
+// blank line stops input, ...) for differential tests.
+KeyTable count_reference_compat(const uint8_t* text, uint64_t n);
+}  // namespace cpu
+
+// Host copy of the synthetic stream (bit-identical to the device generator).
+std::vector<uint8_t> synth_host(uint64_t n, uint64_t first_segment, const SynthSpec& spec);
+
+// Reference-identical output framing (/root/reference/main.cu:166-218).
+std::string format_output(const KeyTable& t, const uint8_t* echo, uint64_t echo_len, bool echo_input,
+                          bool list_rows, uint64_t top_k = 0);
+
+}  // namespace wc

@@ -1,0 +1,299 @@
+// capi.cpp — C ABI over the C++ engine (ctypes binding of the Python package).
+#include <cstdlib>
+#include <cstring>
+#include <exception>
+#include <thread>
+
+#include "common/hip_util.hpp"
+#include "dist/comm.hpp"
+#include "io/source.hpp"
+#include "wc/wc.h"
+#include "wc/wc.hpp"
+
+struct wc_engine {
+  std::unique_ptr<wc::Engine> e;
+  uint64_t resident = 0;  // bytes of synthetic text resident on device
+  const uint8_t* d_text = nullptr;
+};
+struct wc_result {
+  wc::KeyTable t;
+};
+struct wc_comm {
+  std::unique_ptr<wc::Comm> c;
+};
+
+namespace {
+thread_local std::string g_err;
+
+template <class F>
+int guard(F&& f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+wc::Options to_opts(const wc_options* o) {
+  wc::Options x;
+  if (!o) return x;
+  x.device = o->device;
+  x.log2_rec_buckets = o->log2_rec_buckets;
+  x.log2_tab_buckets = o->log2_tab_buckets;
+  x.max_log2_tab_buckets = o->max_log2_tab_buckets;
+  x.map_blocks = o->map_blocks;
+  x.staging_buffers = o->staging_buffers;
+  x.chunk_bytes = o->chunk_bytes;
+  x.arena_bytes = o->arena_bytes;
+  x.min_records = o->min_records;
+  x.records_per_byte = o->records_per_byte;
+  return x;
+}
+
+wc::SynthSpec spec_of(uint64_t seed, uint32_t vocab, double s) {
+  wc::SynthSpec sp;
+  sp.seed = seed;
+  sp.vocab = vocab;
+  sp.zipf_s = s;
+  return sp;
+}
+}  // namespace
+
+extern "C" {
+
+const char* wc_last_error(void) { return g_err.c_str(); }
+const char* wc_version(void) { return "wc-mi355x 0.1.0"; }
+
+int wc_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+void wc_default_options(wc_options* o) {
+  const wc::Options d;
+  o->device = d.device;
+  o->log2_rec_buckets = d.log2_rec_buckets;
+  o->log2_tab_buckets = d.log2_tab_buckets;
+  o->max_log2_tab_buckets = d.max_log2_tab_buckets;
+  o->map_blocks = d.map_blocks;
+  o->staging_buffers = d.staging_buffers;
+  o->chunk_bytes = d.chunk_bytes;
+  o->arena_bytes = d.arena_bytes;
+  o->min_records = d.min_records;
+  o->records_per_byte = d.records_per_byte;
+}
+
+wc_engine* wc_engine_create(const wc_options* o) {
+  wc_engine* e = nullptr;
+  if (guard([&] {
+        e = new wc_engine;
+        e->e.reset(new wc::Engine(to_opts(o)));
+      }) != 0) {
+    delete e;
+    return nullptr;
+  }
+  return e;
+}
+
+void wc_engine_destroy(wc_engine* e) { delete e; }
+
+int wc_engine_reset(wc_engine* e) { return guard([&] { e->e->reset(); }); }
+
+int wc_count_host(wc_engine* e, const uint8_t* text, uint64_t n, uint64_t base) {
+  return guard([&] { e->e->count_host(text, n, base); });
+}
+
+int wc_count_file(wc_engine* e, const char* path, uint64_t begin, uint64_t end, uint64_t base) {
+  return guard([&] {
+    wc::FileSource src(path, begin, end);
+    e->e->count_source(src, base);
+  });
+}
+
+int wc_count_replay(wc_engine* e, const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t base) {
+  return guard([&] {
+    wc::ReplaySource src(pool, pool_bytes, total);
+    e->e->count_source(src, base);
+  });
+}
+
+int wc_synth_device(wc_engine* e, uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double s) {
+  return guard([&] {
+    e->d_text = e->e->synth_device(n, first_segment, spec_of(seed, vocab, s));
+    e->resident = n;
+  });
+}
+
+int wc_count_resident(wc_engine* e, uint64_t n, uint64_t base) {
+  return guard([&] {
+    WC_CHECK(e->d_text && n <= e->resident, "no resident text of that size (call wc_synth_device first)");
+    e->e->count_device(e->d_text, n, e->resident, base, ' ');
+  });
+}
+
+int wc_finalize_device(wc_engine* e, wc_comm* c, uint64_t* n_keys) {
+  return guard([&] { *n_keys = e->e->finalize_device(c ? c->c.get() : nullptr); });
+}
+
+wc_result* wc_engine_result(wc_engine* e, wc_comm* c, int all_ranks) {
+  wc_result* r = new wc_result;
+  if (guard([&] { r->t = e->e->result(c ? c->c.get() : nullptr, all_ranks != 0); }) != 0) {
+    delete r;
+    return nullptr;
+  }
+  return r;
+}
+
+int wc_engine_stats_json(wc_engine* e, char* buf, int cap) {
+  const wc::Stats& s = e->e->stats();
+  char tmp[1024];
+  const int k = snprintf(tmp, sizeof tmp,
+                         "{\"bytes\": %llu, \"tokens\": %llu, \"keys\": %llu, \"chunks\": %u, \"map_reruns\": %u, "
+                         "\"table_splits\": %u, \"log2_buckets\": %u, \"map_reduce_ms\": %.3f, \"finalize_ms\": %.3f, "
+                         "\"merge_ms\": %.3f}",
+                         (unsigned long long)s.bytes, (unsigned long long)s.tokens, (unsigned long long)s.keys,
+                         s.chunks, s.map_reruns, s.table_splits, s.log2_buckets, s.map_reduce_ms, s.finalize_ms,
+                         s.merge_ms);
+  if (buf && cap > 0) {
+    std::strncpy(buf, tmp, (size_t)cap - 1);
+    buf[cap - 1] = 0;
+  }
+  return k;
+}
+
+int wc_engine_sync(wc_engine* e) { return guard([&] { WC_HIP_CHECK(hipDeviceSynchronize()); (void)e; }); }
+
+uint64_t wc_result_size(const wc_result* r) { return r->t.size(); }
+uint64_t wc_result_total(const wc_result* r) { return r->t.total; }
+uint64_t wc_result_bytes(const wc_result* r) {
+  uint64_t b = 0;
+  for (const auto& w : r->t.words) b += w.size();
+  return b;
+}
+
+void wc_result_export(const wc_result* r, uint64_t* counts, uint64_t* first_off, uint64_t* word_off, char* bytes) {
+  uint64_t o = 0;
+  for (size_t i = 0; i < r->t.size(); ++i) {
+    if (counts) counts[i] = r->t.counts[i];
+    if (first_off) first_off[i] = r->t.first_off[i];
+    if (word_off) word_off[i] = o;
+    if (bytes) std::memcpy(bytes + o, r->t.words[i].data(), r->t.words[i].size());
+    o += r->t.words[i].size();
+  }
+  if (word_off) word_off[r->t.size()] = o;
+}
+
+void wc_result_free(wc_result* r) { delete r; }
+
+int wc_format(const wc_result* r, const uint8_t* echo, uint64_t echo_len, int echo_input, int list_rows,
+              uint64_t top_k, char** out, uint64_t* out_len) {
+  return guard([&] {
+    const std::string s = wc::format_output(r->t, echo, echo_len, echo_input != 0, list_rows != 0, top_k);
+    char* p = static_cast<char*>(std::malloc(s.size() + 1));
+    WC_CHECK(p, "out of memory");
+    std::memcpy(p, s.data(), s.size());
+    p[s.size()] = 0;
+    *out = p;
+    *out_len = s.size();
+  });
+}
+
+void wc_free(void* p) { std::free(p); }
+
+wc_result* wc_cpu_count(const uint8_t* text, uint64_t n, uint64_t base) {
+  wc_result* r = new wc_result;
+  if (guard([&] { r->t = wc::cpu::count(text, n, base); }) != 0) {
+    delete r;
+    return nullptr;
+  }
+  return r;
+}
+
+wc_result* wc_cpu_count_compat(const uint8_t* text, uint64_t n) {
+  wc_result* r = new wc_result;
+  if (guard([&] { r->t = wc::cpu::count_reference_compat(text, n); }) != 0) {
+    delete r;
+    return nullptr;
+  }
+  return r;
+}
+
+int wc_synth_host(uint8_t* out, uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double s) {
+  return guard([&] {
+    const std::vector<uint8_t> v = wc::synth_host(n, first_segment, spec_of(seed, vocab, s));
+    std::memcpy(out, v.data(), n);
+  });
+}
+
+int wc_shard_range_mem(const uint8_t* text, uint64_t n, int rank, int world, uint64_t* begin, uint64_t* end) {
+  return guard([&] {
+    const wc::ShardRange r = wc::shard_range_mem(text, n, rank, world);
+    *begin = r.begin;
+    *end = r.end;
+  });
+}
+
+int wc_shard_range_file(const char* path, int rank, int world, uint64_t* begin, uint64_t* end) {
+  return guard([&] {
+    const wc::ShardRange r = wc::shard_range(path, rank, world);
+    *begin = r.begin;
+    *end = r.end;
+  });
+}
+
+int wc_rccl_unique_id(char out[128]) {
+  return guard([&] {
+    const std::string id = wc::rccl_unique_id();
+    std::memcpy(out, id.data(), id.size());
+  });
+}
+
+wc_comm* wc_comm_rccl_create(const char* unique_id, int rank, int size, int device) {
+  wc_comm* c = new wc_comm;
+  if (guard([&] { c->c = wc::make_rccl_comm(std::string(unique_id, wc::RCCL_ID_BYTES), rank, size, device); }) != 0) {
+    delete c;
+    return nullptr;
+  }
+  return c;
+}
+
+void wc_comm_destroy(wc_comm* c) { delete c; }
+
+wc_result* wc_loopback_count(const uint8_t* text, uint64_t n, int ranks, const int* devices, const wc_options* o) {
+  wc_result* out = new wc_result;
+  std::vector<std::string> errs(ranks);
+  std::vector<std::unique_ptr<wc::Comm>> comms;
+  if (guard([&] { comms = wc::make_loopback_comms(ranks); }) != 0) {
+    delete out;
+    return nullptr;
+  }
+  std::vector<std::thread> th;
+  for (int r = 0; r < ranks; ++r) {
+    th.emplace_back([&, r] {
+      try {
+        wc::Options opt = to_opts(o);
+        opt.device = devices ? devices[r] : 0;
+        wc::Engine eng(opt);
+        const wc::ShardRange sr = wc::shard_range_mem(text, n, r, ranks);
+        if (sr.end > sr.begin) eng.count_host(text + sr.begin, sr.end - sr.begin, sr.begin);
+        wc::KeyTable t = eng.result(comms[r].get(), false);
+        if (r == 0) out->t = std::move(t);
+      } catch (const std::exception& ex) {
+        errs[r] = ex.what();
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int r = 0; r < ranks; ++r)
+    if (!errs[r].empty()) {
+      g_err = "rank " + std::to_string(r) + ": " + errs[r];
+      delete out;
+      return nullptr;
+    }
+  return out;
+}
+
+}  // extern "C"

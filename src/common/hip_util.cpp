@@ -1,0 +1,81 @@
+#include "hip_util.hpp"
+
+#include <rocprofiler-sdk-roctx/roctx.h>
+
+#include <chrono>
+#include <mutex>
+
+namespace wc {
+
+void fail(const std::string& msg) { throw Error(msg); }
+
+DeviceArena::~DeviceArena() {
+  if (base_) (void)hipFree(base_);
+}
+
+void DeviceArena::reserve(size_t bytes) {
+  if (bytes <= cap_) {
+    used_ = 0;
+    return;
+  }
+  if (base_) WC_HIP_CHECK(hipFree(base_));
+  base_ = nullptr;
+  cap_ = used_ = 0;
+  WC_HIP_CHECK(hipMalloc(&base_, bytes));
+  cap_ = bytes;
+}
+
+void* DeviceArena::take(size_t bytes, size_t align) {
+  size_t off = (used_ + align - 1) / align * align;
+  if (off + bytes > cap_)
+    fail("device arena exhausted: need " + std::to_string(off + bytes) + " of " + std::to_string(cap_));
+  used_ = off + bytes;
+  return base_ + off;
+}
+
+PinnedBuffer::~PinnedBuffer() {
+  if (p_) (void)hipHostFree(p_);
+}
+
+PinnedBuffer& PinnedBuffer::operator=(PinnedBuffer&& o) noexcept {
+  if (this != &o) {
+    if (p_) (void)hipHostFree(p_);
+    p_ = o.p_;
+    n_ = o.n_;
+    o.p_ = nullptr;
+    o.n_ = 0;
+  }
+  return *this;
+}
+
+void PinnedBuffer::resize(size_t bytes) {
+  if (bytes <= n_) return;
+  if (p_) WC_HIP_CHECK(hipHostFree(p_));
+  p_ = nullptr;
+  n_ = 0;
+  WC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_), bytes, hipHostMallocDefault));
+  n_ = bytes;
+}
+
+Range::Range(const char* name) { roctxRangePush(name); }
+Range::~Range() { roctxRangePop(); }
+
+double now_seconds() {
+  using clk = std::chrono::steady_clock;
+  return std::chrono::duration<double>(clk::now().time_since_epoch()).count();
+}
+
+int device_cu_count(int device) {
+  static std::mutex mu;
+  static std::vector<int> cache;
+  std::lock_guard<std::mutex> g(mu);
+  if ((int)cache.size() <= device) cache.resize(device + 1, 0);
+  if (!cache[device]) {
+    hipDeviceProp_t p;
+    WC_HIP_CHECK(hipGetDeviceProperties(&p, device));
+    cache[device] = p.multiProcessorCount;
+  }
+  return cache[device];
+}
+
+}  // namespace wc

@@ -1,0 +1,89 @@
+// hip_util.hpp — error checking, device arena, timers, roctx ranges.
+//
+// Reference parity: the reference checks no return code anywhere
+// (/root/reference/main.cu:143-161); every HIP call here goes
+// through WC_HIP_CHECK and throws wc::Error with file:line.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace wc {
+
+struct Error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+[[noreturn]] void fail(const std::string& msg);
+
+#define WC_HIP_CHECK(expr)                                                                     \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess)                                                                       \
+      ::wc::fail(std::string("HIP error ") + hipGetErrorString(e_) + " at " + __FILE__ + ":" + \
+                 std::to_string(__LINE__) + " in " #expr);                                     \
+  } while (0)
+
+#define WC_CHECK(cond, msg)                                                                      \
+  do {                                                                                           \
+    if (!(cond)) ::wc::fail(std::string("check failed: ") + (msg) + " at " + __FILE__ + ":" +   \
+                            std::to_string(__LINE__));                                          \
+  } while (0)
+
+// Bump allocator over ONE hipMalloc: nothing in the hot path allocates
+// (cdna_hip_programming.md Guideline 9).
+class DeviceArena {
+ public:
+  DeviceArena() = default;
+  ~DeviceArena();
+  DeviceArena(const DeviceArena&) = delete;
+  DeviceArena& operator=(const DeviceArena&) = delete;
+  void reserve(size_t bytes);  // (re)allocate backing store; invalidates pointers
+  void* take(size_t bytes, size_t align = 256);
+  template <class T>
+  T* take_n(size_t n) {
+    return static_cast<T*>(take(n * sizeof(T)));
+  }
+  void reset() { used_ = 0; }
+  size_t capacity() const { return cap_; }
+  size_t used() const { return used_; }
+
+ private:
+  uint8_t* base_ = nullptr;
+  size_t cap_ = 0, used_ = 0;
+};
+
+// Pinned host buffer (hipHostMalloc) RAII.
+class PinnedBuffer {
+ public:
+  PinnedBuffer() = default;
+  explicit PinnedBuffer(size_t bytes) { resize(bytes); }
+  ~PinnedBuffer();
+  PinnedBuffer(PinnedBuffer&& o) noexcept : p_(o.p_), n_(o.n_) { o.p_ = nullptr; o.n_ = 0; }
+  PinnedBuffer& operator=(PinnedBuffer&& o) noexcept;
+  PinnedBuffer(const PinnedBuffer&) = delete;
+  void resize(size_t bytes);
+  uint8_t* data() const { return p_; }
+  size_t size() const { return n_; }
+
+ private:
+  uint8_t* p_ = nullptr;
+  size_t n_ = 0;
+};
+
+// Scoped roctx range (no-op when the profiler is not attached).
+class Range {
+ public:
+  explicit Range(const char* name);
+  ~Range();
+};
+
+double now_seconds();
+
+// Number of compute units of the current device (cached per device).
+int device_cu_count(int device);
+
+}  // namespace wc

@@ -1,0 +1,167 @@
+// comm.cpp — RCCL and loopback implementations of wc::Comm.
+#include "comm.hpp"
+
+#include <rccl/rccl.h>
+
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+
+#include "../common/hip_util.hpp"
+
+namespace wc {
+
+void launch_combine_u64(uint64_t* dst, const uint64_t* src, uint64_t n, int op, hipStream_t s);  // sort.hip
+
+#define WC_NCCL_CHECK(expr)                                                                          \
+  do {                                                                                                \
+    ncclResult_t r_ = (expr);                                                                         \
+    if (r_ != ncclSuccess)                                                                            \
+      ::wc::fail(std::string("RCCL error ") + ncclGetErrorString(r_) + " at " + __FILE__ + ":" +     \
+                 std::to_string(__LINE__) + " in " #expr);                                           \
+  } while (0)
+
+namespace {
+
+ncclRedOp_t to_nccl(RedOp op) {
+  switch (op) {
+    case RedOp::Sum: return ncclSum;
+    case RedOp::Min: return ncclMin;
+    default: return ncclMax;
+  }
+}
+
+class RcclComm final : public Comm {
+ public:
+  RcclComm(ncclComm_t c, int rank, int size, int device) : c_(c), rank_(rank), size_(size), dev_(device) {
+    WC_HIP_CHECK(hipSetDevice(device));
+    WC_HIP_CHECK(hipMalloc(&scratch_, 8));
+  }
+  ~RcclComm() override {
+    (void)hipFree(scratch_);
+    (void)ncclCommDestroy(c_);
+  }
+  int rank() const override { return rank_; }
+  int size() const override { return size_; }
+  const char* backend() const override { return "rccl"; }
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    WC_NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, c_, s));
+  }
+  void reduce_scatter_u64(const uint64_t* send, uint64_t* recv, size_t count, RedOp op, hipStream_t s) override {
+    WC_NCCL_CHECK(ncclReduceScatter(send, recv, count, ncclUint64, to_nccl(op), c_, s));
+  }
+  void barrier(hipStream_t s) override {
+    WC_NCCL_CHECK(ncclAllReduce(scratch_, scratch_, 1, ncclUint64, ncclSum, c_, s));
+    WC_HIP_CHECK(hipStreamSynchronize(s));
+  }
+
+ private:
+  ncclComm_t c_;
+  int rank_, size_, dev_;
+  void* scratch_ = nullptr;
+};
+
+// Shared rendezvous for loopback ranks.
+struct Hub {
+  explicit Hub(int n) : n(n), ptrs(n, nullptr) {}
+  int n;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  std::vector<const void*> ptrs;
+  void wait_all() {
+    std::unique_lock<std::mutex> lk(mu);
+    const uint64_t g = gen;
+    if (++arrived == n) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return gen != g; });
+    }
+  }
+};
+
+class LoopbackComm final : public Comm {
+ public:
+  LoopbackComm(std::shared_ptr<Hub> hub, int rank) : hub_(std::move(hub)), rank_(rank) {}
+  int rank() const override { return rank_; }
+  int size() const override { return hub_->n; }
+  const char* backend() const override { return "loopback"; }
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    WC_HIP_CHECK(hipStreamSynchronize(s));
+    hub_->ptrs[rank_] = send;
+    hub_->wait_all();
+    for (int r = 0; r < hub_->n; ++r)
+      WC_HIP_CHECK(hipMemcpyAsync(static_cast<uint8_t*>(recv) + (size_t)r * bytes, hub_->ptrs[r], bytes,
+                                  hipMemcpyDefault, s));
+    WC_HIP_CHECK(hipStreamSynchronize(s));
+    hub_->wait_all();  // senders may reuse their buffers after everyone copied
+  }
+  void reduce_scatter_u64(const uint64_t* send, uint64_t* recv, size_t count, RedOp op, hipStream_t s) override {
+    WC_HIP_CHECK(hipStreamSynchronize(s));
+    hub_->ptrs[rank_] = send;
+    hub_->wait_all();
+    uint64_t* tmp = nullptr;
+    if (count) WC_HIP_CHECK(hipMalloc(&tmp, count * 8));
+    for (int r = 0; r < hub_->n; ++r) {
+      const uint64_t* src = static_cast<const uint64_t*>(hub_->ptrs[r]) + (size_t)rank_ * count;
+      if (!count) break;
+      if (r == 0) {
+        WC_HIP_CHECK(hipMemcpyAsync(recv, src, count * 8, hipMemcpyDefault, s));
+      } else {
+        WC_HIP_CHECK(hipMemcpyAsync(tmp, src, count * 8, hipMemcpyDefault, s));
+        launch_combine_u64(recv, tmp, count, (int)op, s);
+      }
+    }
+    WC_HIP_CHECK(hipStreamSynchronize(s));
+    if (tmp) WC_HIP_CHECK(hipFree(tmp));
+    hub_->wait_all();
+  }
+  void barrier(hipStream_t s) override {
+    WC_HIP_CHECK(hipStreamSynchronize(s));
+    hub_->wait_all();
+  }
+
+ private:
+  std::shared_ptr<Hub> hub_;
+  int rank_;
+};
+
+}  // namespace
+
+std::string rccl_unique_id() {
+  static_assert(sizeof(ncclUniqueId) == RCCL_ID_BYTES, "ncclUniqueId size");
+  ncclUniqueId id;
+  WC_NCCL_CHECK(ncclGetUniqueId(&id));
+  return std::string(reinterpret_cast<const char*>(&id), sizeof id);
+}
+
+std::unique_ptr<Comm> make_rccl_comm(const std::string& unique_id, int rank, int size, int device) {
+  WC_CHECK(unique_id.size() == sizeof(ncclUniqueId), "bad RCCL unique id");
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id.data(), sizeof id);
+  WC_HIP_CHECK(hipSetDevice(device));
+  ncclComm_t c;
+  WC_NCCL_CHECK(ncclCommInitRank(&c, size, id, rank));
+  return std::unique_ptr<Comm>(new RcclComm(c, rank, size, device));
+}
+
+std::vector<std::unique_ptr<Comm>> make_rccl_comms_all(const std::vector<int>& devices) {
+  std::vector<ncclComm_t> cs(devices.size());
+  WC_NCCL_CHECK(ncclCommInitAll(cs.data(), (int)devices.size(), devices.data()));
+  std::vector<std::unique_ptr<Comm>> out;
+  for (size_t i = 0; i < devices.size(); ++i)
+    out.emplace_back(new RcclComm(cs[i], (int)i, (int)devices.size(), devices[i]));
+  return out;
+}
+
+std::vector<std::unique_ptr<Comm>> make_loopback_comms(int n) {
+  auto hub = std::make_shared<Hub>(n);
+  std::vector<std::unique_ptr<Comm>> out;
+  for (int r = 0; r < n; ++r) out.emplace_back(new LoopbackComm(hub, r));
+  return out;
+}
+
+}  // namespace wc

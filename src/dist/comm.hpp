@@ -1,0 +1,45 @@
+// comm.hpp — collective interface used by the cross-GPU merge.
+//
+// The reference has no communication at all.  Backends:
+//  * RcclComm      RCCL over xGMI; either one process per GPU (unique id shared
+//                  by the launcher, e.g. torch.distributed's store) or one
+//                  process driving all GPUs (ncclCommInitAll, the CLI).
+//  * LoopbackComm  N virtual ranks in one process (threads), any devices —
+//                  exercises sharding + merge at N = 1..8 on a single GPU.
+// All buffers are device pointers on the caller's current device and every
+// call is ordered on the given stream.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace wc {
+
+enum class RedOp { Sum, Min, Max };
+
+class Comm {
+ public:
+  virtual ~Comm() = default;
+  virtual int rank() const = 0;
+  virtual int size() const = 0;
+  virtual const char* backend() const = 0;
+  // recv[r * bytes ...] = rank r's send (bytes each).
+  virtual void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
+  // recv[count] = op over ranks of send[rank * count ... + count).
+  virtual void reduce_scatter_u64(const uint64_t* send, uint64_t* recv, size_t count, RedOp op, hipStream_t s) = 0;
+  virtual void barrier(hipStream_t s) = 0;
+};
+
+// RCCL.  unique_id is the 128-byte ncclUniqueId blob.
+constexpr int RCCL_ID_BYTES = 128;
+std::string rccl_unique_id();
+std::unique_ptr<Comm> make_rccl_comm(const std::string& unique_id, int rank, int size, int device);
+std::vector<std::unique_ptr<Comm>> make_rccl_comms_all(const std::vector<int>& devices);
+
+// In-process virtual ranks (call each rank's methods from its own thread).
+std::vector<std::unique_ptr<Comm>> make_loopback_comms(int n);
+
+}  // namespace wc

@@ -1,0 +1,480 @@
+// engine.cpp — per-GPU MapReduce pipeline (host orchestration).
+//
+// Reference: runMapReduce (/root/reference/main.cu:133-162) mallocs, copies,
+// launches map then reduce on the legacy default stream, copies back and
+// frees, once, for <= 891 bytes of input.  Here:
+//  * one preallocated workspace per engine (records, running table, key arena,
+//    counters); nothing is allocated on the per-chunk path;
+//  * text is processed in HBM-sized chunks (default 1 GiB) — either already
+//    resident (count_device), or streamed from host memory / files through a
+//    pinned ring where the H2D of chunk k+1 (copy stream) overlaps the
+//    map/reduce of chunk k (compute stream);
+//  * per chunk ONE host synchronisation reads a 32-byte counter block; shuffle
+//    region overflow re-runs the chunk in halves, running-table overflow
+//    splits the table (B -> 2B) and re-runs only the overflowed buckets.
+#include <algorithm>
+#include <cstring>
+
+#include "engine_impl.hpp"
+#include "../dist/comm.hpp"
+
+namespace wc {
+
+// ---------------------------------------------------------------- TableStore --
+TableStore::~TableStore() {
+  if (mem) (void)hipFree(mem);
+}
+
+void TableStore::alloc(uint32_t log2_buckets) {
+  if (mem && v.log2_buckets == log2_buckets) return;
+  if (mem) WC_HIP_CHECK(hipFree(mem));
+  mem = nullptr;
+  const size_t nb = (size_t)1 << log2_buckets, n = nb * TAB_SLOTS;
+  const size_t bytes = n * (5 * sizeof(uint64_t) + sizeof(uint32_t)) + nb * sizeof(uint32_t) + 1024;
+  WC_HIP_CHECK(hipMalloc(&mem, bytes));
+  uint8_t* p = static_cast<uint8_t*>(mem);
+  auto take = [&](size_t b) {
+    uint8_t* r = p;
+    p += (b + 255) / 256 * 256;
+    return r;
+  };
+  v.k0 = reinterpret_cast<uint64_t*>(take(n * 8));
+  v.k1 = reinterpret_cast<uint64_t*>(take(n * 8));
+  v.cnt = reinterpret_cast<uint64_t*>(take(n * 8));
+  v.first = reinterpret_cast<uint64_t*>(take(n * 8));
+  v.sref_off = reinterpret_cast<uint64_t*>(take(n * 8));
+  v.sref_len = reinterpret_cast<uint32_t*>(take(n * 4));
+  v.occupancy = reinterpret_cast<uint32_t*>(take(nb * 4));
+  v.log2_buckets = log2_buckets;
+}
+
+// ---------------------------------------------------------------------- Impl --
+Engine::Impl::Impl(const Options& o) : opt(o) {
+  dev = opt.device;
+  WC_HIP_CHECK(hipSetDevice(dev));
+  WC_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  WC_HIP_CHECK(hipStreamCreateWithFlags(&copy_s, hipStreamNonBlocking));
+  map_blocks = opt.map_blocks ? opt.map_blocks : 2u * (uint32_t)device_cu_count(dev);
+
+  opt.log2_rec_buckets = std::min<uint32_t>(opt.log2_rec_buckets, MAX_REC_BUCKETS_LOG2);
+  opt.max_log2_tab_buckets = std::min<uint32_t>(std::max<uint32_t>(opt.max_log2_tab_buckets, 1), 20);
+  opt.log2_tab_buckets = std::max(opt.log2_tab_buckets, opt.log2_rec_buckets);
+  opt.log2_tab_buckets = std::min(opt.log2_tab_buckets, opt.max_log2_tab_buckets);
+  const uint64_t max_chunk = (1ull << 32) - 2 * (uint64_t)MAP_TILE;  // records carry u32 offsets
+  opt.chunk_bytes = std::min<uint64_t>(std::max<uint64_t>(opt.chunk_bytes, MAP_TILE), max_chunk);
+  opt.chunk_bytes = opt.chunk_bytes / MAP_TILE * MAP_TILE;
+
+  rec_total = std::max<uint64_t>(opt.min_records, (uint64_t)((double)opt.chunk_bytes * opt.records_per_byte));
+  const size_t region_words = (size_t)MAX_REC_BUCKETS * map_blocks;
+  rec_mem.reserve(rec_total * 3 * sizeof(uint64_t) + region_words * 4 + 4096);
+  rec.k0 = rec_mem.take_n<uint64_t>(rec_total);
+  rec.k1 = rec_mem.take_n<uint64_t>(rec_total);
+  rec.co = rec_mem.take_n<uint64_t>(rec_total);
+  rec.region_count = rec_mem.take_n<uint32_t>(region_words);
+
+  WC_HIP_CHECK(hipMalloc(&d_ctr, sizeof(DevCounters)));
+  WC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_ctr), sizeof(DevCounters), hipHostMallocDefault));
+  const size_t maxb = (size_t)1 << opt.max_log2_tab_buckets;
+  WC_HIP_CHECK(hipMalloc(&d_bucket_ovf, maxb * sizeof(uint32_t)));
+  WC_HIP_CHECK(hipMalloc(&d_bucket_en, maxb));
+  WC_HIP_CHECK(hipMalloc(&d_arena, std::max<uint64_t>(opt.arena_bytes, 16)));
+  WC_HIP_CHECK(hipMalloc(&d_arena_cursor, sizeof(unsigned long long)));
+  for (int i = 0; i < 2; ++i) {
+    WC_HIP_CHECK(hipEventCreateWithFlags(&ev_h2d[i], hipEventDisableTiming));
+    WC_HIP_CHECK(hipEventCreateWithFlags(&ev_done[i], hipEventDisableTiming));
+  }
+  tab[0].alloc(opt.log2_tab_buckets);
+  cur = 0;
+  launch_table_clear(table(), s);
+  WC_HIP_CHECK(hipMemsetAsync(d_bucket_ovf, 0, maxb * sizeof(uint32_t), s));
+  WC_HIP_CHECK(hipMemsetAsync(d_arena_cursor, 0, sizeof(unsigned long long), s));
+  WC_HIP_CHECK(hipStreamSynchronize(s));
+}
+
+Engine::Impl::~Impl() {
+  (void)hipSetDevice(dev);
+  if (s) (void)hipStreamSynchronize(s);
+  if (copy_s) (void)hipStreamSynchronize(copy_s);
+  for (int i = 0; i < 2; ++i) {
+    if (ev_h2d[i]) (void)hipEventDestroy(ev_h2d[i]);
+    if (ev_done[i]) (void)hipEventDestroy(ev_done[i]);
+  }
+  if (d_ctr) (void)hipFree(d_ctr);
+  if (h_ctr) (void)hipHostFree(h_ctr);
+  if (d_bucket_ovf) (void)hipFree(d_bucket_ovf);
+  if (d_bucket_en) (void)hipFree(d_bucket_en);
+  if (d_arena) (void)hipFree(d_arena);
+  if (d_arena_cursor) (void)hipFree(d_arena_cursor);
+  if (s) (void)hipStreamDestroy(s);
+  if (copy_s) (void)hipStreamDestroy(copy_s);
+}
+
+void Engine::Impl::ensure_text(uint64_t n) {
+  const uint64_t need = (n + 4095) / 4096 * 4096 + 4096;
+  if (need > text_cap || !d_text) {
+    text_mem.reserve(need);
+    d_text = static_cast<uint8_t*>(text_mem.take(need));
+    text_cap = need;
+  }
+}
+
+void Engine::Impl::ensure_staging(uint64_t chunk) {
+  if (d_stage[0] && pinned.size() >= 2 && pinned[0].size() >= chunk) return;
+  ensure_text(2 * chunk + 256);
+  d_stage[0] = d_text;
+  d_stage[1] = d_text + (chunk + 255) / 256 * 256;
+  pinned.clear();
+  const uint32_t nring = std::max<uint32_t>(2, opt.staging_buffers);
+  for (uint32_t i = 0; i < nring; ++i) pinned.emplace_back(chunk);
+}
+
+uint32_t Engine::Impl::blocks_for(uint64_t len) const {
+  const uint64_t tiles = (len + MAP_TILE - 1) / MAP_TILE;
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(map_blocks, tiles));
+}
+
+void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev,
+                               uint32_t log2_rb, uint32_t blocks) {
+  WC_CHECK((reinterpret_cast<uintptr_t>(text) & 15) == 0, "chunk text must be 16-byte aligned");
+  WC_HIP_CHECK(hipMemsetAsync(d_ctr, 0, sizeof(DevCounters), s));
+  Records r = rec;
+  r.cap = (uint32_t)std::min<uint64_t>(rec_total / (((uint64_t)1 << log2_rb) * blocks), 0xFFFFFFFFull);
+  MapArgs m{text, len, avail, prev, log2_rb, r, d_ctr->flags, &d_ctr->tokens};
+  launch_map(m, blocks, s);
+  ReduceArgs ra{r,      blocks, log2_rb, table(), text, avail, base, Arena{d_arena, d_arena_cursor, opt.arena_bytes},
+                d_ctr->flags, d_bucket_ovf, nullptr};
+  launch_reduce(ra, s);
+  WC_HIP_CHECK(hipMemcpyAsync(h_ctr, d_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));
+}
+
+void Engine::Impl::split_table() {
+  const uint32_t lg = table().log2_buckets;
+  if (lg >= opt.max_log2_tab_buckets)
+    fail("vocabulary exceeds the key table (" + std::to_string(((size_t)1 << lg) * TAB_MAX_OCC) +
+         " keys); raise max_log2_tab_buckets");
+  TableStore& dst = tab[cur ^ 1];
+  dst.alloc(lg + 1);
+  launch_table_clear(dst.v, s);
+  launch_table_split(table(), dst.v, s);
+  cur ^= 1;
+  st.table_splits++;
+}
+
+void Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev,
+                                 uint32_t log2_rb, uint32_t blocks) {
+  WC_HIP_CHECK(hipStreamSynchronize(s));
+  DevCounters c = *h_ctr;
+  if (c.flags[FLAG_REGION_OVF]) {
+    // Shuffle regions too small for this chunk's record skew: the reduce was
+    // skipped (table untouched), so re-run exactly this chunk, smaller.
+    st.map_reruns++;
+    auto run = [&](const uint8_t* t, uint64_t l, uint64_t av, uint64_t b, int pv, uint32_t rb) {
+      const uint32_t bl = blocks_for(l);
+      launch_pass(t, l, av, b, pv, rb, bl);
+      complete_pass(t, l, av, b, pv, rb, bl);
+    };
+    if (len > (uint64_t)MAP_TILE) {
+      const uint64_t h = std::max<uint64_t>(MAP_TILE, (len / 2) / MAP_TILE * MAP_TILE);
+      run(text, h, avail, base, prev, log2_rb);
+      run(text + h, len - h, avail - h, base + h, -1, log2_rb);
+    } else if (log2_rb > 0) {
+      run(text, len, avail, base, prev, 0);
+    } else {
+      fail("shuffle record capacity too small for a single tile");
+    }
+    return;
+  }
+  const uint64_t tokens = c.tokens;
+  uint32_t max_occ = c.flags[FLAG_MAX_OCC];
+  while (c.flags[FLAG_TABLE_OVF]) {
+    if (c.flags[FLAG_ARENA_OVF]) break;
+    const uint32_t lg = table().log2_buckets;
+    std::vector<uint32_t> ovf((size_t)1 << lg);
+    WC_HIP_CHECK(hipMemcpy(ovf.data(), d_bucket_ovf, ovf.size() * 4, hipMemcpyDeviceToHost));
+    split_table();
+    std::vector<uint8_t> en(ovf.size() * 2);
+    for (size_t b = 0; b < en.size(); ++b) en[b] = ovf[b >> 1] ? 1 : 0;
+    WC_HIP_CHECK(hipMemcpyAsync(d_bucket_en, en.data(), en.size(), hipMemcpyHostToDevice, s));
+    WC_HIP_CHECK(hipMemsetAsync(d_bucket_ovf, 0, en.size() * 4, s));
+    WC_HIP_CHECK(hipMemsetAsync(d_ctr, 0, sizeof(DevCounters), s));
+    Records r = rec;
+    r.cap = (uint32_t)std::min<uint64_t>(rec_total / (((uint64_t)1 << log2_rb) * blocks), 0xFFFFFFFFull);
+    ReduceArgs ra{r,      blocks, log2_rb, table(), text, avail, base, Arena{d_arena, d_arena_cursor, opt.arena_bytes},
+                  d_ctr->flags, d_bucket_ovf, d_bucket_en};
+    launch_reduce(ra, s);
+    WC_HIP_CHECK(hipMemcpyAsync(h_ctr, d_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));
+    WC_HIP_CHECK(hipStreamSynchronize(s));
+    c = *h_ctr;
+    max_occ = std::max(max_occ, c.flags[FLAG_MAX_OCC]);
+  }
+  if (c.flags[FLAG_ARENA_OVF])
+    fail("key arena exhausted (" + std::to_string(opt.arena_bytes) + " bytes); raise arena_bytes");
+  st.tokens += tokens;
+  st.chunks++;
+  max_end = std::max(max_end, base + len);
+  if (max_occ >= (uint32_t)TAB_SPLIT_AT && table().log2_buckets < opt.max_log2_tab_buckets) split_table();
+}
+
+void Engine::Impl::process_chunk(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev) {
+  const uint32_t blocks = blocks_for(len);
+  launch_pass(text, len, avail, base, prev, opt.log2_rec_buckets, blocks);
+  complete_pass(text, len, avail, base, prev, opt.log2_rec_buckets, blocks);
+}
+
+void Engine::Impl::compact_local() {
+  Range r("wc_finalize_compact");
+  const TableView& t = table();
+  const size_t nb = (size_t)1 << t.log2_buckets;
+  std::vector<uint32_t> occ(nb);
+  WC_HIP_CHECK(hipMemcpyAsync(occ.data(), t.occupancy, nb * 4, hipMemcpyDeviceToHost, s));
+  unsigned long long arena_used = 0;
+  WC_HIP_CHECK(hipMemcpyAsync(&arena_used, d_arena_cursor, 8, hipMemcpyDeviceToHost, s));
+  WC_HIP_CHECK(hipStreamSynchronize(s));
+  uint64_t n = 0;
+  for (uint32_t o : occ) n += o;
+  // columns x2 (sorted copy) + sort scratch + hist
+  const size_t per = 5 * 8 + 4;
+  fin_mem.reserve(std::max<size_t>(1 << 20, (n + 1) * per + radix_hist_words(n) * 4 + 64 * 1024));
+  fin_mem.reset();
+  cols = KeyCols{};
+  cols.k0 = fin_mem.take_n<uint64_t>(n + 1);
+  cols.k1 = fin_mem.take_n<uint64_t>(n + 1);
+  cols.cnt = fin_mem.take_n<uint64_t>(n + 1);
+  cols.first = fin_mem.take_n<uint64_t>(n + 1);
+  cols.sref_off = fin_mem.take_n<uint64_t>(n + 1);
+  cols.sref_len = fin_mem.take_n<uint32_t>(n + 1);
+  unsigned long long* d_n = fin_mem.take_n<unsigned long long>(1);
+  WC_HIP_CHECK(hipMemsetAsync(d_n, 0, 8, s));
+  launch_table_compact(t, cols.k0, cols.k1, cols.cnt, cols.first, cols.sref_off, cols.sref_len, d_n, s);
+  cols.n = n;
+  cols_arena = d_arena;
+  cols_arena_bytes = std::min<uint64_t>(arena_used, opt.arena_bytes);
+  st.keys = n;
+  st.log2_buckets = t.log2_buckets;
+}
+
+void Engine::Impl::sort_cols_by_first() {
+  Range r("wc_finalize_sort");
+  const uint64_t n = cols.n;
+  if (n == 0) return;
+  DeviceArena& A = sort_mem;
+  A.reserve(n * (2 * 8 + 2 * 4 + 5 * 8 + 4) + radix_hist_words(n) * 4 + 64 * 1024);
+  A.reset();
+  uint64_t* keys = A.take_n<uint64_t>(n);
+  uint64_t* tkeys = A.take_n<uint64_t>(n);
+  uint32_t* vals = A.take_n<uint32_t>(n);
+  uint32_t* tvals = A.take_n<uint32_t>(n);
+  uint32_t* hist = A.take_n<uint32_t>(radix_hist_words(n));
+  KeyCols o;
+  o.k0 = A.take_n<uint64_t>(n);
+  o.k1 = A.take_n<uint64_t>(n);
+  o.cnt = A.take_n<uint64_t>(n);
+  o.first = A.take_n<uint64_t>(n);
+  o.sref_off = A.take_n<uint64_t>(n);
+  o.sref_len = A.take_n<uint32_t>(n);
+  o.n = n;
+  WC_HIP_CHECK(hipMemcpyAsync(keys, cols.first, n * 8, hipMemcpyDeviceToDevice, s));
+  launch_iota_u32(vals, n, s);
+  int bits = 1;
+  while (bits < 64 && (max_end >> bits) != 0) ++bits;
+  radix_sort_pairs(keys, vals, tkeys, tvals, hist, n, bits, s);
+  launch_gather_u64(cols.k0, vals, o.k0, n, s);
+  launch_gather_u64(cols.k1, vals, o.k1, n, s);
+  launch_gather_u64(cols.cnt, vals, o.cnt, n, s);
+  launch_gather_u64(cols.first, vals, o.first, n, s);
+  launch_gather_u64(cols.sref_off, vals, o.sref_off, n, s);
+  launch_gather_u32(cols.sref_len, vals, o.sref_len, n, s);
+  cols = o;
+}
+
+KeyTable Engine::Impl::download_cols() {
+  Range r("wc_download");
+  const uint64_t n = cols.n;
+  std::vector<uint64_t> k0(n), k1(n), cnt(n), first(n), soff(n);
+  std::vector<uint32_t> slen(n);
+  std::vector<uint8_t> arena(cols_arena_bytes);
+  if (n) {
+    WC_HIP_CHECK(hipMemcpyAsync(k0.data(), cols.k0, n * 8, hipMemcpyDeviceToHost, s));
+    WC_HIP_CHECK(hipMemcpyAsync(k1.data(), cols.k1, n * 8, hipMemcpyDeviceToHost, s));
+    WC_HIP_CHECK(hipMemcpyAsync(cnt.data(), cols.cnt, n * 8, hipMemcpyDeviceToHost, s));
+    WC_HIP_CHECK(hipMemcpyAsync(first.data(), cols.first, n * 8, hipMemcpyDeviceToHost, s));
+    WC_HIP_CHECK(hipMemcpyAsync(soff.data(), cols.sref_off, n * 8, hipMemcpyDeviceToHost, s));
+    WC_HIP_CHECK(hipMemcpyAsync(slen.data(), cols.sref_len, n * 4, hipMemcpyDeviceToHost, s));
+  }
+  if (!arena.empty())
+    WC_HIP_CHECK(hipMemcpyAsync(arena.data(), cols_arena, arena.size(), hipMemcpyDeviceToHost, s));
+  WC_HIP_CHECK(hipStreamSynchronize(s));
+  KeyTable t;
+  t.words.resize(n);
+  t.counts = std::move(cnt);
+  t.first_off = std::move(first);
+  for (uint64_t i = 0; i < n; ++i) {
+    if (key_is_short(k1[i])) {
+      const uint64_t len = k1[i];
+      t.words[i].resize(len);
+      for (uint64_t b = 0; b < len; ++b) t.words[i][b] = (char)((k0[i] >> (8 * b)) & 0xFF);
+    } else {
+      WC_CHECK(soff[i] + slen[i] <= arena.size(), "arena reference out of range");
+      t.words[i].assign(reinterpret_cast<const char*>(arena.data()) + soff[i], slen[i]);
+    }
+    t.total += t.counts[i];
+  }
+  return t;
+}
+
+// -------------------------------------------------------------------- Engine --
+Engine::Engine(const Options& opt) : p_(new Impl(opt)) {}
+Engine::~Engine() = default;
+const Options& Engine::options() const { return p_->opt; }
+Stats& Engine::stats() { return p_->st; }
+
+void Engine::reset() {
+  Impl& im = *p_;
+  WC_HIP_CHECK(hipSetDevice(im.dev));
+  launch_table_clear(im.table(), im.s);
+  WC_HIP_CHECK(hipMemsetAsync(im.d_arena_cursor, 0, sizeof(unsigned long long), im.s));
+  WC_HIP_CHECK(hipStreamSynchronize(im.s));
+  im.st = Stats{};
+  im.max_end = 0;
+}
+
+void Engine::count_device(const uint8_t* d_text, uint64_t n, uint64_t avail, uint64_t global_base, int prev_byte) {
+  Impl& im = *p_;
+  WC_HIP_CHECK(hipSetDevice(im.dev));
+  Range r("wc_count_device");
+  const double t0 = now_seconds();
+  const uint64_t C = im.opt.chunk_bytes;
+  for (uint64_t off = 0; off < n; off += C) {
+    const uint64_t len = std::min<uint64_t>(C, n - off);
+    im.process_chunk(d_text + off, len, avail - off, global_base + off, off == 0 ? prev_byte : -1);
+  }
+  im.st.bytes += n;
+  im.st.map_reduce_ms += (now_seconds() - t0) * 1e3;
+}
+
+namespace {
+struct MemorySource : ChunkSource {
+  const uint8_t* p;
+  uint64_t n, pos = 0;
+  MemorySource(const uint8_t* p_, uint64_t n_) : p(p_), n(n_) {}
+  uint64_t read(uint8_t* dst, uint64_t cap) override {
+    const uint64_t k = std::min(cap, n - pos);
+    std::memcpy(dst, p + pos, k);
+    pos += k;
+    return k;
+  }
+};
+}  // namespace
+
+void Engine::count_host(const uint8_t* h_text, uint64_t n, uint64_t global_base) {
+  MemorySource src(h_text, n);
+  count_source(src, global_base);
+}
+
+void Engine::count_source(ChunkSource& src, uint64_t global_base) {
+  Impl& im = *p_;
+  WC_HIP_CHECK(hipSetDevice(im.dev));
+  Range r("wc_count_stream");
+  const double t0 = now_seconds();
+  const uint64_t C = im.opt.chunk_bytes;
+  im.ensure_staging(C);
+  std::vector<uint8_t> carry;
+  bool eof = false;
+  uint64_t offset = global_base;
+
+  // Fill pinned[k % ring] with carry + fresh bytes, cut at the last delimiter.
+  auto fill = [&](uint64_t k) -> uint64_t {
+    uint8_t* pin = im.pinned[k % im.pinned.size()].data();
+    uint64_t total = carry.size();
+    if (total) std::memcpy(pin, carry.data(), total);
+    carry.clear();
+    while (!eof && total < C) {
+      const uint64_t got = src.read(pin + total, C - total);
+      if (got == 0) eof = true;
+      total += got;
+    }
+    if (total == 0 || eof) return total;
+    uint64_t cut = total;
+    while (cut > 0 && !is_delim(pin[cut - 1])) --cut;
+    if (cut == 0) fail("a single word is longer than the chunk size (" + std::to_string(C) + " bytes)");
+    carry.assign(pin + cut, pin + total);
+    return cut;
+  };
+  auto issue = [&](uint64_t k, uint64_t len) {
+    WC_HIP_CHECK(hipStreamWaitEvent(im.copy_s, im.ev_done[k & 1], 0));
+    WC_HIP_CHECK(hipMemcpyAsync(im.d_stage[k & 1], im.pinned[k % im.pinned.size()].data(), len,
+                                hipMemcpyHostToDevice, im.copy_s));
+    WC_HIP_CHECK(hipEventRecord(im.ev_h2d[k & 1], im.copy_s));
+  };
+  WC_HIP_CHECK(hipEventRecord(im.ev_done[0], im.s));
+  WC_HIP_CHECK(hipEventRecord(im.ev_done[1], im.s));
+  uint64_t len = fill(0);
+  if (len) issue(0, len);
+  for (uint64_t k = 0; len; ++k) {
+    const uint8_t* d = im.d_stage[k & 1];
+    WC_HIP_CHECK(hipStreamWaitEvent(im.s, im.ev_h2d[k & 1], 0));
+    const uint32_t blocks = im.blocks_for(len);
+    im.launch_pass(d, len, len, offset, ' ', im.opt.log2_rec_buckets, blocks);
+    const uint64_t next = fill(k + 1);  // host reads the next chunk while the GPU works
+    if (next) issue(k + 1, next);
+    im.complete_pass(d, len, len, offset, ' ', im.opt.log2_rec_buckets, blocks);
+    WC_HIP_CHECK(hipEventRecord(im.ev_done[k & 1], im.s));
+    offset += len;
+    im.st.bytes += len;
+    len = next;
+  }
+  WC_HIP_CHECK(hipStreamSynchronize(im.copy_s));
+  im.st.map_reduce_ms += (now_seconds() - t0) * 1e3;
+}
+
+const uint8_t* Engine::synth_device(uint64_t n, uint64_t first_segment, const SynthSpec& spec) {
+  Impl& im = *p_;
+  WC_HIP_CHECK(hipSetDevice(im.dev));
+  const uint64_t key = spec.seed * 1000003ull ^ ((uint64_t)spec.vocab << 20) ^ (uint64_t)(spec.zipf_s * 1e6);
+  if (key != im.vocab_key) {
+    const HostVocab hv = build_vocab(spec);
+    im.vocab_mem.reserve(hv.bytes.size() + hv.off.size() * 9 + hv.cdf.size() * 4 + 4096);
+    uint8_t* b = im.vocab_mem.take_n<uint8_t>(hv.bytes.size());
+    uint32_t* off = im.vocab_mem.take_n<uint32_t>(hv.off.size());
+    uint8_t* len = im.vocab_mem.take_n<uint8_t>(hv.len.size());
+    uint32_t* cdf = im.vocab_mem.take_n<uint32_t>(hv.cdf.size());
+    WC_HIP_CHECK(hipMemcpy(b, hv.bytes.data(), hv.bytes.size(), hipMemcpyHostToDevice));
+    WC_HIP_CHECK(hipMemcpy(off, hv.off.data(), hv.off.size() * 4, hipMemcpyHostToDevice));
+    WC_HIP_CHECK(hipMemcpy(len, hv.len.data(), hv.len.size(), hipMemcpyHostToDevice));
+    WC_HIP_CHECK(hipMemcpy(cdf, hv.cdf.data(), hv.cdf.size() * 4, hipMemcpyHostToDevice));
+    im.d_vocab = SynthVocab{b, off, len, cdf, (uint32_t)hv.off.size()};
+    im.vocab_key = key;
+  }
+  im.ensure_text(n);
+  launch_synth(im.d_text, n, first_segment, spec.seed, im.d_vocab, im.s);
+  WC_HIP_CHECK(hipStreamSynchronize(im.s));
+  return im.d_text;
+}
+
+uint64_t Engine::finalize_device(Comm* comm) {
+  Impl& im = *p_;
+  WC_HIP_CHECK(hipSetDevice(im.dev));
+  const double t0 = now_seconds();
+  im.compact_local();
+  if (comm && comm->size() > 1) {
+    const double tm = now_seconds();
+    merge_cols(im, *comm);
+    im.st.merge_ms += (now_seconds() - tm) * 1e3;
+  }
+  im.sort_cols_by_first();
+  WC_HIP_CHECK(hipStreamSynchronize(im.s));
+  im.st.finalize_ms += (now_seconds() - t0) * 1e3;
+  return im.cols.n;
+}
+
+KeyTable Engine::result(Comm* comm, bool all_ranks) {
+  Impl& im = *p_;
+  finalize_device(comm);
+  if (comm && comm->size() > 1 && comm->rank() != 0 && !all_ranks) {
+    KeyTable t;
+    return t;
+  }
+  return im.download_cols();
+}
+
+}  // namespace wc

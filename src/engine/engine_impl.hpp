@@ -1,0 +1,113 @@
+// engine_impl.hpp — private state of wc::Engine (shared with dist/merge.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <memory>
+#include <vector>
+
+#include "../common/hip_util.hpp"
+#include "../io/synth_host.hpp"
+#include "../kernels/kernels.hpp"
+#include "../kernels/keys.hpp"
+#include "wc/wc.hpp"
+
+namespace wc {
+
+// Device counters block, zeroed per map/reduce pass.
+struct DevCounters {
+  uint32_t flags[FLAG_COUNT];
+  unsigned long long tokens;
+  unsigned long long pad;
+};
+
+// Running table storage (own allocation: it grows by splitting).
+struct TableStore {
+  void* mem = nullptr;
+  TableView v{};
+  ~TableStore();
+  void alloc(uint32_t log2_buckets);
+  size_t slots() const { return ((size_t)1 << v.log2_buckets) * TAB_SLOTS; }
+};
+
+// Dense key columns (compact output, merge input/output).
+struct KeyCols {
+  uint64_t *k0 = nullptr, *k1 = nullptr, *cnt = nullptr, *first = nullptr, *sref_off = nullptr;
+  uint32_t* sref_len = nullptr;
+  uint64_t n = 0;
+};
+
+struct Engine::Impl {
+  Options opt;
+  Stats st;
+  int dev = 0;
+  hipStream_t s = nullptr, copy_s = nullptr;
+  uint32_t map_blocks = 0;
+
+  // shuffle records
+  uint64_t rec_total = 0;
+  Records rec{};
+  DeviceArena rec_mem;
+
+  // counters + pinned mirror
+  DevCounters* d_ctr = nullptr;
+  DevCounters* h_ctr = nullptr;
+
+  TableStore tab[2];
+  int cur = 0;
+  uint32_t* d_bucket_ovf = nullptr;
+  uint8_t* d_bucket_en = nullptr;
+
+  // key arena (bytes of >8-byte words)
+  uint8_t* d_arena = nullptr;
+  unsigned long long* d_arena_cursor = nullptr;
+
+  // resident / staging text
+  DeviceArena text_mem;
+  uint8_t* d_text = nullptr;
+  uint64_t text_cap = 0;
+  uint8_t* d_stage[2] = {nullptr, nullptr};
+  std::vector<PinnedBuffer> pinned;
+  hipEvent_t ev_h2d[2] = {}, ev_done[2] = {};
+
+  // synthetic vocabulary on device
+  uint64_t vocab_key = ~0ull;
+  DeviceArena vocab_mem;
+  SynthVocab d_vocab{};
+
+  // finalisation workspace
+  DeviceArena fin_mem;   // compact output
+  DeviceArena merge_mem; // merge buffers (merged columns live here)
+  DeviceArena sort_mem;  // first-occurrence sort + sorted columns
+  KeyCols cols;        // local (compact) or merged, sorted by first after finalize
+  uint8_t* cols_arena = nullptr;   // arena the sref_* of cols point into
+  uint64_t cols_arena_bytes = 0;
+  uint64_t max_end = 0;  // max global byte offset seen (sort key width)
+
+  explicit Impl(const Options& o);
+  ~Impl();
+
+  TableView& table() { return tab[cur].v; }
+  void ensure_text(uint64_t n);
+  void ensure_staging(uint64_t chunk);
+
+  // One chunk: map + reduce with overflow recovery (synchronous).
+  void process_chunk(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev);
+  // Asynchronous part (map + reduce + counters D2H) and the completion check.
+  void launch_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev, uint32_t log2_rb,
+                   uint32_t blocks);
+  void complete_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev, uint32_t log2_rb,
+                     uint32_t blocks);
+  uint32_t blocks_for(uint64_t len) const;
+  void split_table();
+
+  void compact_local();                     // table -> cols (unsorted)
+  void sort_cols_by_first();                // cols ordered by first occurrence
+  KeyTable download_cols();
+};
+
+// Multi-rank merge (dist/merge.cpp): replaces im.cols / cols_arena with the
+// merged global table (identical on every rank).
+void merge_cols(Engine::Impl& im, Comm& comm);
+
+}  // namespace wc

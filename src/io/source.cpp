@@ -1,0 +1,132 @@
+#include "source.hpp"
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstring>
+#include <stdexcept>
+#include <vector>
+
+#include "../common/hip_util.hpp"
+#include "../kernels/keys.hpp"
+
+namespace wc {
+
+uint64_t file_size(const std::string& path) {
+  struct stat st;
+  if (::stat(path.c_str(), &st) != 0) fail("cannot stat " + path + ": " + std::strerror(errno));
+  return (uint64_t)st.st_size;
+}
+
+namespace {
+// Byte accessor abstraction so file and memory shards share one rule.
+template <class Get>
+ShardRange owned_range(uint64_t n, int rank, int world, Get get) {
+  ShardRange r;
+  const uint64_t s = n / world * rank, e = (rank == world - 1) ? n : n / world * (rank + 1);
+  uint64_t b = s;
+  if (s > 0 && !is_delim(get(s - 1)))  // the token straddling s belongs to the previous shard
+    while (b < e && !is_delim(get(b))) ++b;
+  if (b >= e) {  // no token starts in this shard
+    r.begin = r.end = e;
+    return r;
+  }
+  uint64_t x = e;  // finish the last owned token past e
+  if (e > 0 && !is_delim(get(e - 1)))
+    while (x < n && !is_delim(get(x))) ++x;
+  r.begin = b;
+  r.end = x;
+  return r;
+}
+}  // namespace
+
+ShardRange shard_range_mem(const uint8_t* p, uint64_t n, int rank, int world) {
+  return owned_range(n, rank, world, [&](uint64_t i) { return (uint32_t)p[i]; });
+}
+
+ShardRange shard_range(const std::string& path, int rank, int world) {
+  const uint64_t n = file_size(path);
+  const int fd = ::open(path.c_str(), O_RDONLY);
+  if (fd < 0) fail("cannot open " + path + ": " + std::strerror(errno));
+  // small read-through cache for the boundary scans
+  std::vector<uint8_t> buf(1 << 16);
+  uint64_t buf_off = ~0ull, buf_len = 0;
+  auto get = [&](uint64_t i) -> uint32_t {
+    if (i < buf_off || i >= buf_off + buf_len) {
+      buf_off = i;
+      const ssize_t k = ::pread(fd, buf.data(), buf.size(), (off_t)i);
+      buf_len = k > 0 ? (uint64_t)k : 0;
+      if (!buf_len) return ' ';
+    }
+    return buf[i - buf_off];
+  };
+  ShardRange r = owned_range(n, rank, world, get);
+  ::close(fd);
+  return r;
+}
+
+FileSource::FileSource(const std::string& path, uint64_t begin, uint64_t end) : pos_(begin), end_(end) {
+  fd_ = ::open(path.c_str(), O_RDONLY);
+  if (fd_ < 0) fail("cannot open " + path + ": " + std::strerror(errno));
+}
+
+FileSource::~FileSource() {
+  if (fd_ >= 0) ::close(fd_);
+}
+
+uint64_t FileSource::read(uint8_t* dst, uint64_t cap) {
+  uint64_t got = 0;
+  while (got < cap && pos_ < end_) {
+    const uint64_t want = std::min<uint64_t>(cap - got, end_ - pos_);
+    const ssize_t k = ::pread(fd_, dst + got, std::min<uint64_t>(want, 1ull << 30), (off_t)pos_);
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      fail(std::string("read error: ") + std::strerror(errno));
+    }
+    if (k == 0) break;
+    got += (uint64_t)k;
+    pos_ += (uint64_t)k;
+  }
+  return got;
+}
+
+ReplaySource::ReplaySource(const uint8_t* pool, uint64_t pool_bytes, uint64_t total)
+    : pool_(pool), pool_bytes_(pool_bytes), total_(total) {
+  WC_CHECK(pool_bytes > 0 && is_delim(pool[pool_bytes - 1]), "replay pool must end with a delimiter");
+}
+
+uint64_t ReplaySource::read(uint8_t* dst, uint64_t cap) {
+  uint64_t got = 0;
+  while (got < cap && produced_ < total_) {
+    const uint64_t k = std::min({cap - got, pool_bytes_ - pos_, total_ - produced_});
+    std::memcpy(dst + got, pool_ + pos_, k);
+    got += k;
+    produced_ += k;
+    pos_ = (pos_ + k) % pool_bytes_;
+  }
+  return got;
+}
+
+std::string read_file(const std::string& path) {
+  const int fd = ::open(path.c_str(), O_RDONLY);
+  if (fd < 0) fail("cannot open " + path + ": " + std::strerror(errno));
+  std::string out;
+  char buf[1 << 16];
+  for (;;) {
+    const ssize_t k = ::read(fd, buf, sizeof buf);
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      ::close(fd);
+      fail("read error on " + path);
+    }
+    if (k == 0) break;
+    out.append(buf, (size_t)k);
+  }
+  ::close(fd);
+  return out;
+}
+
+}  // namespace wc

@@ -1,0 +1,139 @@
+// kernels.hpp — host-side launch interface of every hand-written CDNA4 kernel.
+//
+// Pipeline per chunk (SURVEY §2.2 replacement column):
+//   wc_map_tokenize   text -> token keys -> LDS pre-aggregation -> bucketed records
+//   wc_reduce_buckets records -> per-bucket LDS hash table -> running key table
+//   wc_table_split    running table B -> 2B buckets (grows with the vocabulary)
+//   wc_table_compact  running table -> dense key list
+//   wc_radix_*        LSD radix sort (first-occurrence order, merge dictionary)
+//   wc_synth_text     device-side synthetic text generator
+// Reference counterparts: mapKernel (/root/reference/main.cu:109-117) and the
+// single-thread reduceKernel (main.cu:119-123).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace wc {
+
+// ---- geometry (gfx950: wave64, 256 CUs, 160 KiB LDS per CU) -------------------
+constexpr int MAP_THREADS = 512;                     // 8 waves
+constexpr int MAP_BPL = 32;                          // text bytes per lane
+constexpr int MAP_TILE = MAP_THREADS * MAP_BPL;      // 16 KiB LDS text tile
+constexpr int MAP_HALO = 256;                        // bytes past the tile kept in LDS
+constexpr int MAP_SLOTS = 2048;                      // LDS pre-aggregation slots
+constexpr int MAP_FLUSH_AT = 1024;                   // flush when this many keys
+constexpr int MAP_MAX_PROBE = 64;
+constexpr int MAX_REC_BUCKETS_LOG2 = 10;             // shuffle partitions <= 1024
+constexpr int MAX_REC_BUCKETS = 1 << MAX_REC_BUCKETS_LOG2;
+
+constexpr int RED_THREADS = 1024;                    // 16 waves, one block per CU
+constexpr int TAB_SLOTS_LOG2 = 12;
+constexpr int TAB_SLOTS = 1 << TAB_SLOTS_LOG2;       // 4096 slots x 32 B = 128 KiB LDS
+constexpr int TAB_MAX_OCC = TAB_SLOTS * 7 / 8;       // overflow -> split the table
+constexpr int TAB_SPLIT_AT = TAB_SLOTS * 5 / 8;      // proactive split threshold
+constexpr int TAB_MAX_PROBE = 512;
+
+// ---- flags word indices ------------------------------------------------------
+enum : int { FLAG_REGION_OVF = 0, FLAG_ARENA_OVF = 1, FLAG_TABLE_OVF = 2, FLAG_MAX_OCC = 3, FLAG_COUNT = 4 };
+
+// Shuffle records, SoA (24 B / record): key words and (count << 32 | chunk offset).
+struct Records {
+  uint64_t* k0;
+  uint64_t* k1;
+  uint64_t* co;
+  uint32_t* region_count;  // [n_rec_buckets * map_blocks]
+  uint32_t cap;            // records per (bucket, map block) region
+};
+
+// Running key table: n_buckets x TAB_SLOTS open-addressing slices.
+struct TableView {
+  uint64_t* k0;
+  uint64_t* k1;
+  uint64_t* cnt;
+  uint64_t* first;     // global byte offset of the first occurrence
+  uint64_t* sref_off;  // arena offset of the word bytes (long words only)
+  uint32_t* sref_len;
+  uint32_t* occupancy;  // [n_buckets]
+  uint32_t log2_buckets;
+};
+
+struct Arena {
+  uint8_t* bytes;
+  unsigned long long* cursor;
+  uint64_t cap;
+};
+
+struct MapArgs {
+  const uint8_t* text;  // chunk start (16-B aligned)
+  uint64_t chunk_len;   // tokens owned: those starting in [0, chunk_len)
+  uint64_t avail_len;   // bytes readable from text (>= chunk_len), for straddling tokens
+  int32_t prev_byte;    // byte before the chunk; -1 = read text[-1]
+  uint32_t log2_rec_buckets;
+  Records rec;
+  uint32_t* flags;
+  unsigned long long* tokens;  // += tokens owned by this chunk
+};
+
+struct ReduceArgs {
+  Records rec;
+  uint32_t map_blocks;
+  uint32_t log2_rec_buckets;
+  TableView tab;
+  const uint8_t* text;  // the same chunk, for copying new long words
+  uint64_t avail_len;
+  uint64_t chunk_base;  // global offset of text[0]
+  Arena arena;
+  uint32_t* flags;
+  uint32_t* bucket_overflow;      // [n_buckets] set when a slice overflowed
+  const uint8_t* bucket_enable;   // nullptr = all
+};
+
+struct SynthVocab {
+  const uint8_t* bytes;
+  const uint32_t* off;
+  const uint8_t* len;
+  const uint32_t* cdf;  // cumulative P(rank <= i) scaled to 2^32
+  uint32_t n;
+};
+
+// ---- launchers (all stream-ordered, no host sync) ----------------------------
+void launch_map(const MapArgs& a, uint32_t map_blocks, hipStream_t s);
+void launch_reduce(const ReduceArgs& a, hipStream_t s);
+void launch_table_split(const TableView& src, const TableView& dst, hipStream_t s);
+void launch_table_clear(const TableView& t, hipStream_t s);
+// Writes occupied entries densely; out_n receives the count.
+void launch_table_compact(const TableView& t, uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first,
+                          uint64_t* sref_off, uint32_t* sref_len, unsigned long long* out_n, hipStream_t s);
+
+// LSD radix sort of (key, value) by the low `bits` bits of key; stable.
+// tmp_* must hold n items; hist must hold radix_hist_words(n) words.
+size_t radix_hist_words(uint64_t n);
+void radix_sort_pairs(uint64_t* keys, uint32_t* vals, uint64_t* tmp_keys, uint32_t* tmp_vals, uint32_t* hist,
+                      uint64_t n, int bits, hipStream_t s);
+
+// out[i] = in[perm[i]] for the six key-table columns.
+void launch_gather_u64(const uint64_t* in, const uint32_t* perm, uint64_t* out, uint64_t n, hipStream_t s);
+void launch_gather_u32(const uint32_t* in, const uint32_t* perm, uint32_t* out, uint64_t n, hipStream_t s);
+void launch_iota_u32(uint32_t* v, uint64_t n, hipStream_t s);
+
+void launch_synth(uint8_t* out, uint64_t n, uint64_t first_segment, uint64_t seed, const SynthVocab& v,
+                  hipStream_t s);
+
+// Merge-protocol helpers (dist/merge.cpp).
+void launch_place_hash(const uint64_t* k0, const uint64_t* k1, uint64_t* ph, uint64_t n, hipStream_t s);
+// Dense scatter: dst_cnt[id[i]] += cnt[i] (ids unique per rank, so plain stores), dst_first min.
+void launch_scatter_dense(const uint32_t* ids, const uint64_t* cnt, const uint64_t* first, uint64_t* dense_cnt,
+                          uint64_t* dense_first, uint64_t n, hipStream_t s);
+void launch_fill_u64(uint64_t* p, uint64_t v, uint64_t n, hipStream_t s);
+// merge.hip
+void launch_union_flags(const uint32_t* pos, const uint64_t* K0, const uint64_t* K1, uint32_t* flag, uint64_t m,
+                        hipStream_t s);
+void launch_union_assign(const uint32_t* pos, const uint32_t* flag, const uint32_t* ex, const uint64_t* K0,
+                         const uint64_t* K1, const uint64_t* SO, const uint32_t* SL, uint64_t m, uint64_t n_max,
+                         uint64_t arena_stride, uint32_t* id_of_pos, uint64_t* ok0, uint64_t* ok1, uint64_t* osoff,
+                         uint32_t* oslen, hipStream_t s);
+void launch_combine_u64(uint64_t* dst, const uint64_t* src, uint64_t n, int op, hipStream_t s);  // 0 sum 1 min 2 max
+void launch_pad_u64(const uint64_t* in, uint64_t n, uint64_t* out, uint64_t m, uint64_t fill, hipStream_t s);
+void launch_exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint64_t m, uint32_t* total, hipStream_t s);
+
+}  // namespace wc

@@ -1,0 +1,82 @@
+// keys.hpp — the word-key contract shared by host (CPU oracle, merge, formatter)
+// and device (map / reduce kernels).  Compiled by hipcc and by g++.
+//
+// Reference parity: the reference identifies a word by a byte-at-a-time *prefix*
+// test (`compare`, /root/reference/main.cu:57-67) over NUL-terminated 30-byte
+// buffers (main.cu:16-22).  Here a word is identified EXACTLY by a packed
+// 128-bit key so every equality test is two 64-bit integer compares:
+//
+//   k0 = the first min(len, 8) bytes, little-endian packed, zero-padded
+//   k1 = len                                   when len <= 8  (exact, no hash)
+//        TAG | fnv1a64(word) & HASH_MASK       when len >  8
+//
+// Words of <= 8 bytes (the vast majority of natural text) are therefore keyed
+// with no hashing at all; longer words collide only if they share their first
+// 8 bytes AND a 62-bit FNV-1a tail hash.  k1 is never 0 (0 marks an empty
+// slot) and never ~0 (PENDING marks a slot being claimed).
+//
+// Delimiters are exactly the reference's set {' ', '\r', '\n'} (main.cu:188);
+// TAB and every other byte, NUL included, are word bytes.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define WC_HD __host__ __device__ __forceinline__
+#else
+#define WC_HD inline
+#endif
+
+namespace wc {
+
+constexpr uint64_t FNV_OFFSET = 0xcbf29ce484222325ull;
+constexpr uint64_t FNV_PRIME = 0x100000001b3ull;
+constexpr uint64_t K1_TAG = 1ull << 63;
+constexpr uint64_t K1_HASH_MASK = (1ull << 62) - 1;
+constexpr uint64_t K1_EMPTY = 0;
+constexpr uint64_t K1_PENDING = ~0ull;
+
+WC_HD bool is_delim(uint32_t c) { return c == 0x20u || c == 0x0Du || c == 0x0Au; }
+
+WC_HD uint64_t fnv1a_step(uint64_t h, uint32_t byte) { return (h ^ (uint64_t)(byte & 0xFFu)) * FNV_PRIME; }
+
+// murmur3 fmix64 finalizer: FNV's low bits are weak, placement needs all 64.
+WC_HD uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+// k1 for a word of `len` bytes whose full-word FNV-1a-64 is `h`.
+WC_HD uint64_t make_k1(uint64_t len, uint64_t h) { return len <= 8 ? len : (K1_TAG | (h & K1_HASH_MASK)); }
+
+// Placement hash: word-wise FNV-1a over the packed key (k0, k1), then fmix64.
+// Top bits select the shuffle bucket, low bits the slot inside the bucket.
+WC_HD uint64_t place_hash(uint64_t k0, uint64_t k1) {
+  uint64_t h = FNV_OFFSET;
+  h = (h ^ k0) * FNV_PRIME;
+  h = (h ^ k1) * FNV_PRIME;
+  return fmix64(h);
+}
+
+WC_HD uint32_t bucket_of(uint64_t ph, uint32_t log2_buckets) {
+  return log2_buckets == 0 ? 0u : (uint32_t)(ph >> (64 - log2_buckets));
+}
+
+// Host helper: key of an explicit byte string.
+WC_HD void key_of(const uint8_t* w, uint64_t len, uint64_t* k0, uint64_t* k1) {
+  uint64_t a = 0, h = FNV_OFFSET;
+  for (uint64_t i = 0; i < len; ++i) {
+    if (i < 8) a |= (uint64_t)w[i] << (8 * i);
+    h = fnv1a_step(h, w[i]);
+  }
+  *k0 = a;
+  *k1 = make_k1(len, h);
+}
+
+// Short words (len <= 8) are recoverable from the key alone.
+WC_HD bool key_is_short(uint64_t k1) { return k1 <= 8; }
+
+}  // namespace wc

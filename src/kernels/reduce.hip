@@ -1,0 +1,210 @@
+// reduce.hip — the REDUCE stage and the running key table.
+//
+// Reference: reducer (/root/reference/main.cu:69-108) is run by ONE GPU thread
+// (reduceKernel, main.cu:119-123) doing a linear scan of at most 10 output
+// keys per pair with a prefix compare.  Here:
+//
+//  wc_reduce_buckets  one 1024-thread block per table bucket (one per CU).
+//                     The bucket's 4096-slot slice of the running table is
+//                     loaded into LDS (128 KiB), the bucket's shuffle records
+//                     are streamed from every map block's region and merged
+//                     with LDS atomics (count +=, first_off = min), and the
+//                     slice is written back.  New long words copy their bytes
+//                     into the key arena so keys outlive streamed chunks.  If a
+//                     slice overflows it is NOT written back; the host splits
+//                     the table and re-runs only the overflowed buckets.
+//  wc_table_split     B -> 2B buckets (rehash into new slices).
+//  wc_table_compact   occupied slots -> dense columns (wave-aggregated atomics).
+#include "kernels.hpp"
+#include "lds_table.hpp"
+
+namespace wc {
+namespace dev {
+
+struct RedLds {
+  uint64_t k0[TAB_SLOTS];
+  uint64_t k1[TAB_SLOTS];
+  uint64_t cnt[TAB_SLOTS];
+  uint64_t first[TAB_SLOTS];
+  uint32_t occupied;
+  uint32_t overflow;
+};
+
+__device__ __forceinline__ void load_slice(RedLds& L, const TableView& t, uint32_t b) {
+  const size_t base = (size_t)b * TAB_SLOTS;
+  for (int s = threadIdx.x; s < TAB_SLOTS; s += blockDim.x) {
+    L.k0[s] = t.k0[base + s];
+    L.k1[s] = t.k1[base + s];
+    L.cnt[s] = t.cnt[base + s];
+    L.first[s] = t.first[base + s];
+  }
+}
+
+__device__ __forceinline__ void store_slice(const RedLds& L, const TableView& t, uint32_t b) {
+  const size_t base = (size_t)b * TAB_SLOTS;
+  for (int s = threadIdx.x; s < TAB_SLOTS; s += blockDim.x) {
+    t.k0[base + s] = L.k0[s];
+    t.k1[base + s] = L.k1[s];
+    t.cnt[base + s] = L.cnt[s];
+    t.first[base + s] = L.first[s];
+  }
+}
+
+// Copy the bytes of a newly seen long word into the key arena.
+__device__ void arena_copy_word(const ReduceArgs& a, uint64_t off, size_t gslot) {
+  uint64_t len = 0;
+  while (off + len < a.avail_len && !is_delim(a.text[off + len])) ++len;
+  const uint64_t p = atomicAdd(a.arena.cursor, (unsigned long long)len);
+  if (p + len > a.arena.cap) {
+    atomicOr(&a.flags[FLAG_ARENA_OVF], 1u);
+    a.tab.sref_off[gslot] = 0;
+    a.tab.sref_len[gslot] = 0;
+    return;
+  }
+  for (uint64_t i = 0; i < len; ++i) a.arena.bytes[p + i] = a.text[off + i];
+  a.tab.sref_off[gslot] = p;
+  a.tab.sref_len[gslot] = (uint32_t)len;
+}
+
+__global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
+  __shared__ RedLds L;
+  const uint32_t b = blockIdx.x;
+  if (a.bucket_enable && !a.bucket_enable[b]) return;
+  if (a.flags[FLAG_REGION_OVF]) return;  // shuffle records incomplete: host re-runs the chunk
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = RED_THREADS / 64;
+  load_slice(L, a.tab, b);
+  if (tid == 0) {
+    L.occupied = a.tab.occupancy[b];
+    L.overflow = 0;
+  }
+  __syncthreads();
+
+  const uint32_t shift = a.tab.log2_buckets - a.log2_rec_buckets;  // table buckets per record bucket
+  const uint32_t rb = b >> shift;
+  const uint32_t P = a.map_blocks;
+  for (uint32_t p = wave; p < P; p += nwaves) {
+    const size_t region = (size_t)rb * P + p;
+    const uint32_t n = a.rec.region_count[region];
+    const size_t base = region * a.rec.cap;
+    for (uint32_t i = lane; i < n; i += 64) {
+      const uint64_t k0 = a.rec.k0[base + i], k1 = a.rec.k1[base + i], co = a.rec.co[base + i];
+      const uint64_t ph = place_hash(k0, k1);
+      if (shift && bucket_of(ph, a.tab.log2_buckets) != b) continue;
+      const uint64_t cnt = co >> 32, first = a.chunk_base + (co & 0xFFFFFFFFull);
+      bool claimed;
+      const int s = lds_find_or_claim(L.k0, L.k1, TAB_SLOTS - 1, k0, k1, (uint32_t)ph & (TAB_SLOTS - 1),
+                                      TAB_MAX_PROBE, claimed);
+      if (s < 0) {
+        L.overflow = 1;
+        continue;
+      }
+      atomicAdd(reinterpret_cast<unsigned long long*>(&L.cnt[s]), (unsigned long long)cnt);
+      atomicMin(reinterpret_cast<unsigned long long*>(&L.first[s]), (unsigned long long)first);
+      if (claimed) {
+        if (atomicAdd(&L.occupied, 1u) + 1 > (uint32_t)TAB_MAX_OCC) L.overflow = 1;
+        if (!key_is_short(k1)) arena_copy_word(a, co & 0xFFFFFFFFull, (size_t)b * TAB_SLOTS + s);
+      }
+    }
+  }
+  __syncthreads();
+  if (L.overflow) {
+    if (tid == 0) {
+      a.bucket_overflow[b] = 1;
+      atomicOr(&a.flags[FLAG_TABLE_OVF], 1u);
+    }
+    return;
+  }
+  store_slice(L, a.tab, b);
+  if (tid == 0) {
+    a.tab.occupancy[b] = L.occupied;
+    atomicMax(&a.flags[FLAG_MAX_OCC], L.occupied);
+  }
+}
+
+// Rehash slice (new_b >> 1) of `src` into slice new_b of `dst` (2x buckets).
+__global__ void __launch_bounds__(RED_THREADS) wc_table_split(TableView src, TableView dst) {
+  __shared__ RedLds L;
+  const uint32_t nb = blockIdx.x, ob = nb >> 1;
+  for (int s = threadIdx.x; s < TAB_SLOTS; s += blockDim.x) {
+    L.k1[s] = K1_EMPTY;
+    L.cnt[s] = 0;
+    L.first[s] = ~0ull;
+  }
+  if (threadIdx.x == 0) L.occupied = 0;
+  __syncthreads();
+  const size_t obase = (size_t)ob * TAB_SLOTS, nbase = (size_t)nb * TAB_SLOTS;
+  for (int s = threadIdx.x; s < TAB_SLOTS; s += blockDim.x) {
+    const uint64_t k1 = src.k1[obase + s];
+    if (k1 == K1_EMPTY) continue;
+    const uint64_t k0 = src.k0[obase + s];
+    const uint64_t ph = place_hash(k0, k1);
+    if (bucket_of(ph, dst.log2_buckets) != nb) continue;
+    bool claimed;
+    const int d = lds_find_or_claim(L.k0, L.k1, TAB_SLOTS - 1, k0, k1, (uint32_t)ph & (TAB_SLOTS - 1), TAB_SLOTS,
+                                    claimed);
+    // d >= 0 always: a child receives at most the parent's occupancy.
+    L.cnt[d] = src.cnt[obase + s];
+    L.first[d] = src.first[obase + s];
+    dst.sref_off[nbase + d] = src.sref_off[obase + s];
+    dst.sref_len[nbase + d] = src.sref_len[obase + s];
+    atomicAdd(&L.occupied, 1u);
+  }
+  __syncthreads();
+  store_slice(L, dst, nb);
+  if (threadIdx.x == 0) dst.occupancy[nb] = L.occupied;
+}
+
+__global__ void wc_table_clear(TableView t, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    t.k1[i] = K1_EMPTY;
+    t.cnt[i] = 0;
+    t.first[i] = ~0ull;
+    if (i < ((size_t)1 << t.log2_buckets)) t.occupancy[i] = 0;
+  }
+}
+
+__global__ void wc_table_compact(TableView t, size_t n, uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first,
+                                 uint64_t* sref_off, uint32_t* sref_len, unsigned long long* out_n) {
+  for (size_t base = blockIdx.x * (size_t)blockDim.x; base < n; base += (size_t)gridDim.x * blockDim.x) {
+    const size_t i = base + threadIdx.x;
+    const bool occ = i < n && t.k1[i] != K1_EMPTY;
+    uint32_t total;
+    const uint32_t r = wave_rank(occ, total);
+    unsigned long long w0 = 0;
+    if (lane_id() == 0 && total) w0 = atomicAdd(out_n, (unsigned long long)total);
+    w0 = __shfl(w0, 0);
+    if (occ) {
+      const size_t o = w0 + r;
+      k0[o] = t.k0[i];
+      k1[o] = t.k1[i];
+      cnt[o] = t.cnt[i];
+      first[o] = t.first[i];
+      sref_off[o] = t.sref_off[i];
+      sref_len[o] = t.sref_len[i];
+    }
+  }
+}
+
+}  // namespace dev
+
+void launch_reduce(const ReduceArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(dev::wc_reduce_buckets, dim3(1u << a.tab.log2_buckets), dim3(RED_THREADS), 0, s, a);
+}
+
+void launch_table_split(const TableView& src, const TableView& dst, hipStream_t s) {
+  hipLaunchKernelGGL(dev::wc_table_split, dim3(1u << dst.log2_buckets), dim3(RED_THREADS), 0, s, src, dst);
+}
+
+void launch_table_clear(const TableView& t, hipStream_t s) {
+  const size_t n = ((size_t)1 << t.log2_buckets) * TAB_SLOTS;
+  hipLaunchKernelGGL(dev::wc_table_clear, dim3(1024), dim3(256), 0, s, t, n);
+}
+
+void launch_table_compact(const TableView& t, uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first,
+                          uint64_t* sref_off, uint32_t* sref_len, unsigned long long* out_n, hipStream_t s) {
+  const size_t n = ((size_t)1 << t.log2_buckets) * TAB_SLOTS;
+  hipLaunchKernelGGL(dev::wc_table_compact, dim3(1024), dim3(256), 0, s, t, n, k0, k1, cnt, first, sref_off,
+                     sref_len, out_n);
+}
+
+}  // namespace wc

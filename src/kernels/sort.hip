@@ -1,0 +1,203 @@
+// sort.hip — stable LSD radix sort of (u64 key, u32 value) pairs + small
+// column kernels used by finalisation and the multi-GPU merge.
+//
+// Used for: first-occurrence output order (the reference gets that order for
+// free from its serial append, /root/reference/main.cu:97-104) and the
+// deterministic dictionary union of the cross-GPU merge.
+//
+// Per 8-bit digit pass: wc_radix_hist (LDS histogram per 2048-item tile) ->
+// wc_radix_scan (exclusive scan, digit-major) -> wc_radix_scatter (stable
+// in-tile ranking with 64-lane ballots: lanes with equal digits are matched
+// with 8 ballots, ranked with popcount, waves combined through LDS).
+#include <utility>
+
+#include "../common/hip_util.hpp"
+#include "kernels.hpp"
+#include "lds_table.hpp"
+
+namespace wc {
+namespace dev {
+
+constexpr int RS_THREADS = 256;
+constexpr int RS_ROUNDS = 8;
+constexpr int RS_TILE = RS_THREADS * RS_ROUNDS;  // 2048 items per block
+constexpr int RS_WAVES = RS_THREADS / 64;
+
+__global__ void __launch_bounds__(RS_THREADS) wc_radix_hist(const uint64_t* keys, uint64_t n, int shift,
+                                                            uint32_t* hist, uint32_t nblocks) {
+  __shared__ uint32_t h[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+  for (int r = 0; r < RS_ROUNDS; ++r) {
+    const uint64_t i = base + (uint64_t)r * RS_THREADS + threadIdx.x;
+    if (i < n) atomicAdd(&h[(keys[i] >> shift) & 0xFF], 1u);
+  }
+  __syncthreads();
+  hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+}
+
+// Single-block exclusive scan of m words (digit-major histogram).
+__global__ void __launch_bounds__(1024) wc_radix_scan(uint32_t* hist, uint64_t m) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (uint64_t base = 0; base < m; base += 1024) {
+    const uint64_t i = base + threadIdx.x;
+    const uint32_t v = i < m ? hist[i] : 0;
+    uint32_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    if (wave == 0) {
+      uint32_t s = lane < 16 ? wsum[lane] : 0;
+      for (int o = 1; o < 16; o <<= 1) {
+        const uint32_t y = __shfl_up(s, o);
+        if (lane >= o) s += y;
+      }
+      if (lane < 16) wsum[lane] = s;
+    }
+    __syncthreads();
+    const uint32_t excl = carry + (wave ? wsum[wave - 1] : 0) + x - v;
+    if (i < m) hist[i] = excl;
+    __syncthreads();
+    if (threadIdx.x == 0) carry += wsum[15];
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(RS_THREADS) wc_radix_scatter(const uint64_t* keys, const uint32_t* vals,
+                                                               uint64_t* okeys, uint32_t* ovals, uint64_t n,
+                                                               int shift, const uint32_t* hist, uint32_t nblocks) {
+  __shared__ uint32_t run[256];             // next output slot per digit
+  __shared__ uint32_t wcnt[RS_WAVES][256];  // per-wave digit counts, then offsets
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  run[tid] = hist[(size_t)tid * nblocks + blockIdx.x];
+  const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  for (int r = 0; r < RS_ROUNDS; ++r) {
+    for (int w = 0; w < RS_WAVES; ++w) wcnt[w][tid] = 0;
+    __syncthreads();
+    const uint64_t i = base + (uint64_t)r * RS_THREADS + tid;
+    const bool valid = i < n;
+    const uint64_t k = valid ? keys[i] : 0;
+    const uint32_t d = (uint32_t)(k >> shift) & 0xFF;
+    uint64_t peers = __ballot(valid);
+    for (int bit = 0; bit < 8; ++bit) {
+      const uint64_t bb = __ballot((d >> bit) & 1);
+      peers &= ((d >> bit) & 1) ? bb : ~bb;
+    }
+    const uint32_t rank = (uint32_t)__popcll(peers & lt);
+    if (valid && rank == 0) wcnt[wave][d] = (uint32_t)__popcll(peers);
+    __syncthreads();
+    {
+      uint32_t acc = run[tid];
+      for (int w = 0; w < RS_WAVES; ++w) {
+        const uint32_t c = wcnt[w][tid];
+        wcnt[w][tid] = acc;
+        acc += c;
+      }
+      run[tid] = acc;
+    }
+    __syncthreads();
+    if (valid) {
+      const uint32_t dst = wcnt[wave][d] + rank;
+      okeys[dst] = k;
+      ovals[dst] = vals[i];
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void wc_gather_u64(const uint64_t* in, const uint32_t* perm, uint64_t* out, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = in[perm[i]];
+}
+__global__ void wc_gather_u32(const uint32_t* in, const uint32_t* perm, uint32_t* out, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = in[perm[i]];
+}
+__global__ void wc_iota_u32(uint32_t* v, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    v[i] = (uint32_t)i;
+}
+__global__ void wc_fill_u64(uint64_t* p, uint64_t v, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+__global__ void wc_place_hash(const uint64_t* k0, const uint64_t* k1, uint64_t* ph, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    ph[i] = place_hash(k0[i], k1[i]);
+}
+__global__ void wc_scatter_dense(const uint32_t* ids, const uint64_t* cnt, const uint64_t* first, uint64_t* dcnt,
+                                 uint64_t* dfirst, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t id = ids[i];
+    dcnt[id] += cnt[i];
+    dfirst[id] = first[i] < dfirst[id] ? first[i] : dfirst[id];
+  }
+}
+
+inline dim3 grid_for(uint64_t n) {
+  uint64_t g = (n + 255) / 256;
+  if (g < 1) g = 1;
+  if (g > 2048) g = 2048;
+  return dim3((unsigned)g);
+}
+
+}  // namespace dev
+
+size_t radix_hist_words(uint64_t n) {
+  const uint64_t nb = (n + dev::RS_TILE - 1) / dev::RS_TILE;
+  return (size_t)256 * (nb ? nb : 1);
+}
+
+void radix_sort_pairs(uint64_t* keys, uint32_t* vals, uint64_t* tmp_keys, uint32_t* tmp_vals, uint32_t* hist,
+                      uint64_t n, int bits, hipStream_t s) {
+  if (n <= 1 || bits <= 0) return;
+  const uint32_t nb = (uint32_t)((n + dev::RS_TILE - 1) / dev::RS_TILE);
+  const int passes = (bits + 7) / 8;
+  uint64_t *ki = keys, *ko = tmp_keys;
+  uint32_t *vi = vals, *vo = tmp_vals;
+  for (int p = 0; p < passes; ++p) {
+    const int shift = 8 * p;
+    hipLaunchKernelGGL(dev::wc_radix_hist, dim3(nb), dim3(dev::RS_THREADS), 0, s, ki, n, shift, hist, nb);
+    hipLaunchKernelGGL(dev::wc_radix_scan, dim3(1), dim3(1024), 0, s, hist, (uint64_t)256 * nb);
+    hipLaunchKernelGGL(dev::wc_radix_scatter, dim3(nb), dim3(dev::RS_THREADS), 0, s, ki, vi, ko, vo, n, shift, hist,
+                       nb);
+    std::swap(ki, ko);
+    std::swap(vi, vo);
+  }
+  if (ki != keys) {  // odd pass count: result lives in tmp
+    WC_HIP_CHECK(hipMemcpyAsync(keys, ki, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+    WC_HIP_CHECK(hipMemcpyAsync(vals, vi, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  }
+}
+
+void launch_gather_u64(const uint64_t* in, const uint32_t* perm, uint64_t* out, uint64_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(dev::wc_gather_u64, dev::grid_for(n), dim3(256), 0, s, in, perm, out, n);
+}
+void launch_gather_u32(const uint32_t* in, const uint32_t* perm, uint32_t* out, uint64_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(dev::wc_gather_u32, dev::grid_for(n), dim3(256), 0, s, in, perm, out, n);
+}
+void launch_iota_u32(uint32_t* v, uint64_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(dev::wc_iota_u32, dev::grid_for(n), dim3(256), 0, s, v, n);
+}
+void launch_fill_u64(uint64_t* p, uint64_t v, uint64_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(dev::wc_fill_u64, dev::grid_for(n), dim3(256), 0, s, p, v, n);
+}
+void launch_place_hash(const uint64_t* k0, const uint64_t* k1, uint64_t* ph, uint64_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(dev::wc_place_hash, dev::grid_for(n), dim3(256), 0, s, k0, k1, ph, n);
+}
+void launch_scatter_dense(const uint32_t* ids, const uint64_t* cnt, const uint64_t* first, uint64_t* dense_cnt,
+                          uint64_t* dense_first, uint64_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(dev::wc_scatter_dense, dev::grid_for(n), dim3(256), 0, s, ids, cnt, first, dense_cnt,
+                            dense_first, n);
+}
+
+}  // namespace wc

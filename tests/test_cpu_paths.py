@@ -1,0 +1,124 @@
+"""CPU-only tests: output contract, reference-quirk emulation, synthetic stream,
+shard ownership.  Run everywhere (no GPU needed)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_OUTPUT, ROOT
+
+ops = pytest.importorskip("cuda_mapreduce_amd.ops")
+
+
+def table(res):
+    return [(w, int(c)) for w, c in zip(res.words, res.counts)]
+
+
+def test_golden_oracle(golden_text):
+    res = ops.cpu_count(golden_text)
+    assert ops.format_output(res, echo=golden_text) == GOLDEN_OUTPUT
+
+
+def test_golden_cli_cpu(tmp_path, golden_text):
+    exe = os.path.join(ROOT, "wordcount")
+    (tmp_path / "test.txt").write_bytes(golden_text)
+    out = subprocess.run([exe, "--cpu"], cwd=tmp_path, capture_output=True, timeout=60)
+    assert out.returncode == 0 and out.stdout == GOLDEN_OUTPUT
+    out = subprocess.run([exe, "--compat=reference"], cwd=tmp_path, capture_output=True, timeout=60)
+    assert out.stdout == GOLDEN_OUTPUT
+
+
+def test_cli_missing_file_matches_reference(tmp_path):
+    # reference: prints the empty framing and exits 0 (main.cu:174)
+    exe = os.path.join(ROOT, "wordcount")
+    out = subprocess.run([exe, "--cpu"], cwd=tmp_path, capture_output=True, timeout=60)
+    assert out.returncode == 0
+    assert out.stdout == b"Input Data:\n" + b"-" * 26 + b"\n" + b"-" * 26 + b"\nTotal Count:0\n"
+
+
+def test_cli_format_tab_and_first_occurrence_order():
+    res = ops.cpu_count(b"b a b c a b\n")
+    assert table(res) == [(b"b", 3), (b"a", 2), (b"c", 1)]
+    assert b"b\t3\n" in ops.format_output(res)
+
+
+# the reference's verified behaviour on its edge cases.
+COMPAT_CASES = [
+    (b"a  b\nb a\n", [(b"a", 3), (b"b", 2)]),
+    (b" a b\n", [(b"a", 1), (b"b", 1)]),
+    (b"x \ny\n", [(b"x", 2), (b"y", 1)]),
+    (b"Good Go\n", [(b"Good", 2)]),
+    (b"Go Good\n", [(b"Go", 1), (b"Good", 1)]),
+    (b"Hello hello, hello\n", [(b"Hello", 1), (b"hello,", 2)]),
+    (b"a\tb a\n", [(b"a\tb", 2)]),
+    (b"a b\r\nb c\r\n", [(b"a", 1), (b"b", 2), (b"c", 1)]),
+    (b"a\rb c\nd\n", [(b"a", 1), (b"d", 1)]),
+    (b"x y\nlast word", [(b"x", 1), (b"y", 1), (b"last", 1)]),
+    (b"a b\n\nc d\n", [(b"a", 1), (b"b", 1)]),
+    (b"a\n" * 9, [(b"a", 9)]),
+]
+
+
+@pytest.mark.parametrize("text,want", COMPAT_CASES)
+def test_reference_compat_quirks(text, want):
+    assert table(ops.cpu_count_compat(text)) == want
+
+
+def test_clean_semantics_differ_from_quirks():
+    assert table(ops.cpu_count(b"Good Go\n")) == [(b"Good", 1), (b"Go", 1)]
+    assert table(ops.cpu_count(b"x y\nlast word")) == [(b"x", 1), (b"y", 1), (b"last", 1), (b"word", 1)]
+    assert table(ops.cpu_count(b"a\rb c\nd\n")) == [(b"a", 1), (b"b", 1), (b"c", 1), (b"d", 1)]
+
+
+def test_compat_equals_clean_inside_envelope(golden_text):
+    rng = np.random.default_rng(0)
+    vocab = [b"alpha", b"beta", b"gamma", b"delta", b"eps"]  # no word is a prefix of another
+    for _ in range(50):
+        lines = []
+        for _ in range(rng.integers(1, 9)):
+            lines.append(b" ".join(vocab[i] for i in rng.integers(0, 5, rng.integers(1, 8))) + b"\n")
+        t = b"".join(lines)
+        assert table(ops.cpu_count_compat(t)) == table(ops.cpu_count(t))
+
+
+def test_synth_is_segment_addressable():
+    full = ops.synth_host(64 * 1024, first_segment=0, seed=3, vocab=1000)
+    part = ops.synth_host(16 * 1024, first_segment=20, seed=3, vocab=1000)
+    assert full[20 * 1024 : 36 * 1024] == part
+    assert all(full[i * 1024 + 1023] in b" \n" for i in range(64))  # segments end on a delimiter
+
+
+def test_synth_zipf_shape():
+    res = ops.cpu_count(ops.synth_host(4 << 20, seed=1, vocab=100000))
+    c = np.sort(res.counts)[::-1]
+    assert res.total > 600_000 and len(res) > 20000, (res.total, len(res))
+    assert c[0] > 20 * c[100]  # heavy head
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 5, 8])
+def test_shard_ownership_partitions_tokens(world):
+    rng = np.random.default_rng(world)
+    a = np.frombuffer(b"ab c\n", np.uint8)
+    text = a[rng.integers(0, 5, 10007)].tobytes()
+    pieces = []
+    for r in range(world):
+        b, e = ops.shard_range(text, r, world)
+        pieces.append(ops.cpu_count(text[b:e], global_base=b))
+    merged = {}
+    for p in pieces:
+        for w, c, f in zip(p.words, p.counts, p.first_off):
+            cnt, first = merged.get(w, (0, 1 << 62))
+            merged[w] = (cnt + int(c), min(first, int(f)))
+    want = ops.cpu_count(text)
+    assert sum(p.total for p in pieces) == want.total
+    assert {w: v for w, v in merged.items()} == {w: (int(c), int(f)) for w, c, f in zip(want.words, want.counts, want.first_off)}
+
+
+def test_shard_range_file_matches_mem(tmp_path):
+    text = ops.synth_host(50_000, seed=9, vocab=300)[:49_999]
+    p = tmp_path / "x.txt"
+    p.write_bytes(text)
+    for world in (2, 4, 7):
+        for r in range(world):
+            assert ops.shard_range_file(str(p), r, world) == ops.shard_range(text, r, world)

@@ -1,0 +1,162 @@
+"""GPU numerics tests of the native engine against the CPU oracle (exact equality).
+
+Every case compares words, first-occurrence order, counts and total with
+``cpu_count`` (a byte-keyed hash map), so the GPU's packed-key scheme, the LDS
+combiner, the shuffle partitioning, the running table, its splits and the
+merge are all checked end to end.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_OUTPUT, ROOT
+
+pytestmark = pytest.mark.gpu
+
+ops = pytest.importorskip("cuda_mapreduce_amd.ops")
+
+
+def assert_same(got, want):
+    assert got.total == want.total
+    assert len(got) == len(want)
+    assert got.words == want.words
+    assert np.array_equal(got.counts, want.counts)
+    assert np.array_equal(got.first_off, want.first_off)
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = ops.Engine(device=0, chunk_bytes=1 << 22)
+    yield e
+    e.close()
+
+
+def run(eng, text):
+    eng.reset()
+    eng.count_bytes(text)
+    return eng.result()
+
+
+def random_text(rng, n, alphabet=b"abcd ,\n\r\tXY", long_words=0):
+    a = np.frombuffer(alphabet, np.uint8)
+    buf = a[rng.integers(0, len(a), n)].copy()
+    for _ in range(long_words):  # plant words longer than lanes / halo / tiles
+        L = int(rng.choice([9, 31, 33, 255, 257, 4000, 20000]))
+        if n > L + 2:
+            p = int(rng.integers(0, n - L))
+            buf[p : p + L] = np.frombuffer(b"q", np.uint8)[0]
+            buf[p + L - 1] = ord("z")
+    return buf.tobytes()
+
+
+def test_golden(eng, golden_text):
+    res = run(eng, golden_text)
+    assert ops.format_output(res, echo=golden_text) == GOLDEN_OUTPUT
+
+
+def test_empty_and_delims(eng):
+    for t in [b"", b" ", b"\n\n\r  \n", b"a", b"a ", b" a", b"\r\na\r\n"]:
+        assert_same(run(eng, t), ops.cpu_count(t))
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_vs_oracle(eng, seed):
+    rng = np.random.default_rng(seed)
+    n = int(rng.choice([1, 17, 1000, 16383, 16384, 16385, 70000, 300000, 2_000_000]))
+    text = random_text(rng, n, long_words=3)
+    assert_same(run(eng, text), ops.cpu_count(text))
+
+
+def test_chunk_and_tile_boundaries():
+    # 32 KiB chunks: words straddle lanes (32 B), tiles (16 KiB), halo and chunks
+    rng = np.random.default_rng(5)
+    text = random_text(rng, 1_000_003, alphabet=b"abcdefgh   \n", long_words=20)
+    with ops.Engine(device=0, chunk_bytes=1 << 15) as e:
+        e.count_bytes(text)
+        got = e.result()
+    assert_same(got, ops.cpu_count(text))
+
+
+def test_synthetic_device_matches_host():
+    n = 8 << 20
+    with ops.Engine(device=0, chunk_bytes=1 << 22) as e:
+        e.synth_device(n, first_segment=3, seed=11, vocab=20000)
+        e.count_resident(n, global_base=0)
+        got = e.result()
+    assert_same(got, ops.cpu_count(ops.synth_host(n, first_segment=3, seed=11, vocab=20000)))
+
+
+def test_table_split_large_vocab():
+    # 2 buckets x 4096 slots to start; ~60k distinct words force several splits
+    words = [f"w{i:x}".encode() for i in range(60000)]
+    rng = np.random.default_rng(3)
+    text = b" ".join(words[i] for i in rng.integers(0, len(words), 300000)) + b"\n"
+    with ops.Engine(device=0, chunk_bytes=1 << 20, log2_rec_buckets=1, log2_tab_buckets=1) as e:
+        e.count_bytes(text)
+        got = e.result()
+        st = e.stats()
+    assert st["table_splits"] >= 3
+    assert_same(got, ops.cpu_count(text))
+
+
+def test_region_overflow_reruns():
+    rng = np.random.default_rng(9)
+    text = b" ".join(f"k{i}".encode() for i in rng.integers(0, 200000, 200000))
+    with ops.Engine(device=0, chunk_bytes=1 << 20, min_records=4096, records_per_byte=0.001) as e:
+        e.count_bytes(text)
+        got = e.result()
+        st = e.stats()
+    assert st["map_reruns"] >= 1
+    assert_same(got, ops.cpu_count(text))
+
+
+@pytest.mark.parametrize("ranks", [1, 2, 3, 4, 8])
+def test_loopback_merge(ranks):
+    rng = np.random.default_rng(ranks)
+    text = random_text(rng, 400_000, alphabet=b"abcdefg  \n", long_words=4) + ops.synth_host(1 << 20, seed=2, vocab=3000)
+    got = ops.loopback_count(text, ranks, chunk_bytes=1 << 20)
+    assert_same(got, ops.cpu_count(text))
+
+
+def test_file_stream(tmp_path):
+    rng = np.random.default_rng(21)
+    text = random_text(rng, 3_000_000, long_words=10)
+    p = tmp_path / "in.txt"
+    p.write_bytes(text)
+    with ops.Engine(device=0, chunk_bytes=1 << 18) as e:
+        e.count_file(str(p))
+        got = e.result()
+    assert_same(got, ops.cpu_count(text))
+
+
+def test_replay_host_staged():
+    pool = np.frombuffer(ops.synth_host(1 << 20, seed=4, vocab=1000), np.uint8)
+    with ops.Engine(device=0, chunk_bytes=1 << 18) as e:
+        e.count_replay(pool, total=5 << 20)
+        got = e.result()
+    one = ops.cpu_count(pool.tobytes())
+    assert got.total == 5 * one.total
+    assert dict(zip(got.words, got.counts.tolist())) == {w: 5 * int(c) for w, c in zip(one.words, one.counts)}
+
+
+def test_rccl_world1():
+    uid = ops.Comm.unique_id()
+    comm = ops.Comm(uid, 0, 1, 0)
+    with ops.Engine(device=0, chunk_bytes=1 << 20) as e:
+        text = ops.synth_host(1 << 18, seed=1, vocab=500)
+        e.count_bytes(text)
+        got = e.result(comm)
+    comm.close()
+    assert_same(got, ops.cpu_count(text))
+
+
+def test_cli_golden(tmp_path, golden_text):
+    exe = os.path.join(ROOT, "wordcount")
+    (tmp_path / "test.txt").write_bytes(golden_text)
+    out = subprocess.run([exe], cwd=tmp_path, capture_output=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout == GOLDEN_OUTPUT
+    out = subprocess.run([exe, str(tmp_path / "test.txt")], capture_output=True, timeout=120)
+    assert out.stdout == GOLDEN_OUTPUT

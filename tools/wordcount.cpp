@@ -1,0 +1,213 @@
+// wordcount — CLI of the MI355X-native MapReduce word count.
+//
+// Reference CLI: the reference binary ignores argv and always reads ./test.txt
+// (/root/reference/main.cu:164-167), printing the framed table of
+// main.cu:166-218.  `wordcount` with no arguments does exactly that;
+// `wordcount <file>` is the north-star form; everything else is opt-in.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../src/common/hip_util.hpp"
+#include "../src/dist/comm.hpp"
+#include "../src/io/source.hpp"
+#include "wc/wc.hpp"
+
+namespace {
+
+const char* kUsage =
+    "usage: wordcount [FILE] [options]\n"
+    "  FILE                    input text (default: test.txt, as the reference)\n"
+    "  --gpus N                shard across N GPUs, merged with RCCL (default 1)\n"
+    "  --cpu                   single-thread CPU oracle (hash map)\n"
+    "  --compat=reference      CPU emulation of the reference program's quirks\n"
+    "  --echo | --no-echo      echo the input after 'Input Data:' (default: echo)\n"
+    "  --no-list               do not print per-word rows\n"
+    "  --top K                 print only the K most frequent words\n"
+    "  --synthetic SIZE[:SEED[:VOCAB[:ZIPF]]]  count generated text instead of FILE\n"
+    "  --chunk-bytes N         device chunk size (default 1G)\n"
+    "  --host-staged           stream FILE through the pinned host ring (no echo)\n"
+    "  --bench-json PATH       write throughput / stage timings as JSON\n";
+
+uint64_t parse_size(const std::string& s) {
+  char* end = nullptr;
+  const double v = std::strtod(s.c_str(), &end);
+  uint64_t mul = 1;
+  if (end && *end) {
+    switch (*end) {
+      case 'k': case 'K': mul = 1ull << 10; break;
+      case 'm': case 'M': mul = 1ull << 20; break;
+      case 'g': case 'G': mul = 1ull << 30; break;
+      case 't': case 'T': mul = 1ull << 40; break;
+      default: wc::fail("bad size: " + s);
+    }
+  }
+  return (uint64_t)(v * (double)mul);
+}
+
+struct Cli {
+  std::string file = "test.txt";
+  int gpus = 1;
+  bool cpu = false, compat = false, echo = true, list = true, host_staged = false;
+  uint64_t top = 0, chunk = 1ull << 30;
+  bool synthetic = false;
+  uint64_t synth_bytes = 0;
+  wc::SynthSpec spec;
+  std::string bench_json;
+};
+
+Cli parse(int argc, char** argv) {
+  Cli c;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto need = [&](const char* what) -> std::string {
+      if (i + 1 >= argc) wc::fail(std::string("missing value for ") + what);
+      return argv[++i];
+    };
+    if (a == "-h" || a == "--help") {
+      std::fputs(kUsage, stdout);
+      std::exit(0);
+    } else if (a == "--gpus") c.gpus = std::stoi(need("--gpus"));
+    else if (a == "--cpu") c.cpu = true;
+    else if (a == "--compat=reference") c.compat = true;
+    else if (a == "--echo") c.echo = true;
+    else if (a == "--no-echo") c.echo = false;
+    else if (a == "--no-list") c.list = false;
+    else if (a == "--top") c.top = std::stoull(need("--top"));
+    else if (a == "--chunk-bytes") c.chunk = parse_size(need("--chunk-bytes"));
+    else if (a == "--host-staged") c.host_staged = true;
+    else if (a == "--bench-json") c.bench_json = need("--bench-json");
+    else if (a == "--synthetic") {
+      std::string v = need("--synthetic");
+      std::vector<std::string> f;
+      size_t p = 0;
+      for (size_t q; (q = v.find(':', p)) != std::string::npos; p = q + 1) f.push_back(v.substr(p, q - p));
+      f.push_back(v.substr(p));
+      c.synthetic = true;
+      c.synth_bytes = parse_size(f[0]);
+      if (f.size() > 1) c.spec.seed = std::stoull(f[1]);
+      if (f.size() > 2) c.spec.vocab = (uint32_t)std::stoul(f[2]);
+      if (f.size() > 3) c.spec.zipf_s = std::stod(f[3]);
+    } else if (!a.empty() && a[0] == '-') wc::fail("unknown option " + a + "\n" + kUsage);
+    else c.file = a;
+  }
+  if (c.synthetic) c.echo = false;
+  return c;
+}
+
+void write_out(const std::string& s) { std::fwrite(s.data(), 1, s.size(), stdout); }
+
+int run(const Cli& c) {
+  wc::KeyTable t;
+  std::string text;  // host copy when echoing / CPU paths
+  bool have_text = false;
+  const double t0 = wc::now_seconds();
+  uint64_t bytes = 0;
+
+  const bool need_host_text = !c.synthetic && (c.echo || c.cpu || c.compat);
+  if (!c.synthetic) {
+    try {
+      if (need_host_text) {
+        text = wc::read_file(c.file);
+        have_text = true;
+      } else {
+        (void)wc::file_size(c.file);
+      }
+    } catch (const wc::Error&) {
+      // Reference behaviour for a missing file: empty framing, exit 0 (main.cu:174).
+      std::fprintf(stderr, "wordcount: cannot open %s\n", c.file.c_str());
+      write_out(wc::format_output(t, nullptr, 0, false, c.list));
+      return 0;
+    }
+  }
+
+  if (c.compat || c.cpu) {
+    std::string host = have_text ? text : std::string();
+    if (c.synthetic) {
+      const std::vector<uint8_t> v = wc::synth_host(c.synth_bytes, 0, c.spec);
+      host.assign(v.begin(), v.end());
+    }
+    const auto* p = reinterpret_cast<const uint8_t*>(host.data());
+    t = c.compat ? wc::cpu::count_reference_compat(p, host.size()) : wc::cpu::count(p, host.size());
+    bytes = host.size();
+  } else {
+    int ndev = 0;
+    WC_HIP_CHECK(hipGetDeviceCount(&ndev));
+    const int g = std::max(1, std::min(c.gpus, ndev));
+    std::vector<int> devs(g);
+    for (int i = 0; i < g; ++i) devs[i] = i;
+    std::vector<std::unique_ptr<wc::Comm>> comms;
+    if (g > 1) comms = wc::make_rccl_comms_all(devs);
+    std::vector<std::string> errs(g);
+    const uint64_t total = c.synthetic ? c.synth_bytes : (have_text ? text.size() : wc::file_size(c.file));
+    bytes = total;
+    auto worker = [&](int r) {
+      try {
+        wc::Options o;
+        o.device = devs[r];
+        o.chunk_bytes = c.chunk;
+        wc::Engine eng(o);
+        if (c.synthetic) {
+          // shard at segment granularity: every segment ends with a delimiter
+          const uint64_t nseg = (total + 1023) / 1024, per = (nseg + g - 1) / g;
+          const uint64_t s0 = std::min<uint64_t>(nseg, per * r), s1 = std::min<uint64_t>(nseg, per * (r + 1));
+          const uint64_t b0 = s0 * 1024, b1 = std::min<uint64_t>(total, s1 * 1024);
+          if (b1 > b0) {
+            const uint8_t* d = eng.synth_device(b1 - b0, s0, c.spec);
+            eng.count_device(d, b1 - b0, b1 - b0, b0, ' ');
+          }
+        } else if (have_text && !c.host_staged) {
+          const auto* p = reinterpret_cast<const uint8_t*>(text.data());
+          const wc::ShardRange sr = wc::shard_range_mem(p, text.size(), r, g);
+          if (sr.end > sr.begin) eng.count_host(p + sr.begin, sr.end - sr.begin, sr.begin);
+        } else {
+          const wc::ShardRange sr = wc::shard_range(c.file, r, g);
+          wc::FileSource src(c.file, sr.begin, sr.end);
+          eng.count_source(src, sr.begin);
+        }
+        wc::KeyTable kt = eng.result(g > 1 ? comms[r].get() : nullptr, false);
+        if (r == 0) t = std::move(kt);
+      } catch (const std::exception& ex) {
+        errs[r] = ex.what();
+      }
+    };
+    if (g == 1) {
+      worker(0);
+    } else {
+      std::vector<std::thread> th;
+      for (int r = 0; r < g; ++r) th.emplace_back(worker, r);
+      for (auto& x : th) x.join();
+    }
+    for (int r = 0; r < g; ++r)
+      if (!errs[r].empty()) wc::fail("GPU " + std::to_string(r) + ": " + errs[r]);
+  }
+  const double secs = wc::now_seconds() - t0;
+  write_out(wc::format_output(t, have_text ? reinterpret_cast<const uint8_t*>(text.data()) : nullptr,
+                              have_text ? text.size() : 0, c.echo && have_text, c.list, c.top));
+  if (!c.bench_json.empty()) {
+    FILE* f = std::fopen(c.bench_json.c_str(), "w");
+    if (!f) wc::fail("cannot write " + c.bench_json);
+    std::fprintf(f,
+                 "{\"bytes\": %llu, \"tokens\": %llu, \"keys\": %zu, \"seconds\": %.6f, \"gb_per_s\": %.3f, "
+                 "\"words_per_s\": %.1f, \"gpus\": %d, \"path\": \"%s\"}\n",
+                 (unsigned long long)bytes, (unsigned long long)t.total, t.size(), secs, bytes / secs / 1e9,
+                 t.total / secs, c.cpu || c.compat ? 0 : c.gpus, c.compat ? "compat" : (c.cpu ? "cpu" : "gpu"));
+    std::fclose(f);
+  }
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  try {
+    return run(parse(argc, argv));
+  } catch (const std::exception& ex) {
+    std::fprintf(stderr, "wordcount: %s\n", ex.what());
+    return 1;
+  }
+}
