@@ -1,0 +1,158 @@
+"""One-process-per-GPU data parallelism.
+
+* Rendezvous and control: torch.distributed (``nccl`` backend = RCCL on ROCm,
+  ``gloo`` on CPU).
+* Data plane on GPUs: the native engine's RCCL communicator (src/dist/comm.cpp),
+  created from a unique id that rank 0 broadcasts through torch.distributed;
+  the merge (src/dist/merge.cpp) then runs reduce-scatter + all-gather over
+  xGMI on device buffers.
+* CPU ranks (tests, hosts without GPUs): the same merge protocol on host data
+  (``host_merge``) over gloo.
+
+Input sharding: rank r owns every token whose first byte lies in its byte
+range (``shard_range``), so shards need no halo exchange.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from ..ops import Comm, Engine, Result, cpu_count, shard_range, shard_range_file
+
+
+@dataclass
+class DistEnv:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+
+
+def init_from_env(backend: Optional[str] = None) -> DistEnv:
+    """Initialise torch.distributed from RANK/WORLD_SIZE/LOCAL_RANK (127.0.0.1 rendezvous)."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world == 1:
+        return DistEnv(rank, world, local, "none")
+    import torch
+    import torch.distributed as dist
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if not dist.is_initialized():
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    return DistEnv(rank, world, local, backend)
+
+
+def rccl_comm(env: DistEnv, device: int) -> Optional[Comm]:
+    """Native RCCL communicator over the ranks of the torch.distributed world."""
+    if env.world == 1:
+        return None
+    import torch.distributed as dist
+
+    uid = [Comm.unique_id() if env.rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    return Comm(uid[0], env.rank, env.world, device)
+
+
+def _reduce_scatter(t, op):
+    """reduce-scatter of a 1-D tensor (len divisible by world); gloo lacks it, so all-reduce + slice."""
+    import torch
+    import torch.distributed as dist
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    n = t.numel() // world
+    if dist.get_backend() == "gloo":
+        dist.all_reduce(t, op=op)
+        return t[rank * n : (rank + 1) * n].clone()
+    out = torch.empty(n, dtype=t.dtype, device=t.device)
+    dist.reduce_scatter_tensor(out, t, op=op)
+    return out
+
+
+def host_merge(local: Result) -> Result:
+    """Merge per-rank results on the host (same protocol as src/dist/merge.cpp).
+
+    1. all-gather every rank's distinct keys
+    2. deterministic union (sorted) -> identical global ids on every rank
+    3. scatter local counts / first offsets into dense vectors
+    4. reduce-scatter (sum / min), 5. all-gather the slices
+    """
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size()
+    keys = [None] * world
+    dist.all_gather_object(keys, list(local.words))
+    union = sorted(set().union(*map(set, keys)))
+    gid = {w: i for i, w in enumerate(union)}
+    vpad = max(world, -(-len(union) // world) * world)
+    cnt = torch.zeros(vpad, dtype=torch.int64)
+    first = torch.full((vpad,), 1 << 62, dtype=torch.int64)
+    for w, c, f in zip(local.words, local.counts, local.first_off):
+        cnt[gid[w]] = int(c)
+        first[gid[w]] = int(f)
+    scnt = _reduce_scatter(cnt, dist.ReduceOp.SUM)
+    sfirst = _reduce_scatter(first, dist.ReduceOp.MIN)
+    full_cnt = [torch.empty_like(scnt) for _ in range(world)]
+    full_first = [torch.empty_like(sfirst) for _ in range(world)]
+    dist.all_gather(full_cnt, scnt)
+    dist.all_gather(full_first, sfirst)
+    c = torch.cat(full_cnt)[: len(union)].numpy()
+    f = torch.cat(full_first)[: len(union)].numpy()
+    order = np.argsort(f, kind="stable")
+    return Result(
+        words=[union[i] for i in order],
+        counts=c[order].astype(np.uint64),
+        first_off=f[order].astype(np.uint64),
+        total=int(c.sum()),
+    )
+
+
+class DistributedWordCount:
+    """Count one logical input across all ranks; rank 0 (or all) gets the result."""
+
+    def __init__(self, env: DistEnv, use_gpu: bool = True, **engine_opts):
+        self.env = env
+        self.use_gpu = use_gpu
+        self.engine = Engine(device=env.local_rank, **engine_opts) if use_gpu else None
+        self.comm = rccl_comm(env, env.local_rank) if use_gpu else None
+
+    def close(self):
+        if self.comm is not None:
+            self.comm.close()
+        if self.engine is not None:
+            self.engine.close()
+
+    def count_bytes(self, data: bytes) -> Result:
+        b, e = shard_range(data, self.env.rank, self.env.world)
+        return self._count(lambda eng: eng.count_bytes(data[b:e], global_base=b), lambda: cpu_count(data[b:e], b))
+
+    def count_file(self, path: str) -> Result:
+        b, e = shard_range_file(path, self.env.rank, self.env.world)
+
+        def host():
+            with open(path, "rb") as fh:
+                fh.seek(b)
+                return cpu_count(fh.read(e - b), b)
+
+        return self._count(lambda eng: eng.count_file(path, b, e), host)
+
+    def _count(self, gpu_fn, cpu_fn) -> Result:
+        if self.use_gpu:
+            self.engine.reset()
+            gpu_fn(self.engine)
+            return self.engine.result(self.comm)
+        local = cpu_fn()
+        if self.env.world == 1:
+            return local
+        return host_merge(local)
