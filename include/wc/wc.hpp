@@ -26,6 +26,7 @@ struct Stats {
   uint64_t bytes = 0;     // text bytes ingested
   uint64_t tokens = 0;    // words counted (device counter)
   uint64_t keys = 0;      // distinct words (local, before merge)
+  uint64_t records = 0;   // shuffle records after the LDS combiner
   uint32_t chunks = 0;    // map/reduce chunk passes
   uint32_t map_reruns = 0;     // shuffle-region overflow -> chunk halved
   uint32_t table_splits = 0;   // running table grew B -> 2B

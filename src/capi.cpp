@@ -151,11 +151,12 @@ int wc_engine_stats_json(wc_engine* e, char* buf, int cap) {
   const wc::Stats& s = e->e->stats();
   char tmp[1024];
   const int k = snprintf(tmp, sizeof tmp,
-                         "{\"bytes\": %llu, \"tokens\": %llu, \"keys\": %llu, \"chunks\": %u, \"map_reruns\": %u, "
+                         "{\"bytes\": %llu, \"tokens\": %llu, \"keys\": %llu, \"records\": %llu, \"chunks\": %u, "
+                         "\"map_reruns\": %u, "
                          "\"table_splits\": %u, \"log2_buckets\": %u, \"map_reduce_ms\": %.3f, \"finalize_ms\": %.3f, "
                          "\"merge_ms\": %.3f}",
                          (unsigned long long)s.bytes, (unsigned long long)s.tokens, (unsigned long long)s.keys,
-                         s.chunks, s.map_reruns, s.table_splits, s.log2_buckets, s.map_reduce_ms, s.finalize_ms,
+                         (unsigned long long)s.records, s.chunks, s.map_reruns, s.table_splits, s.log2_buckets, s.map_reduce_ms, s.finalize_ms,
                          s.merge_ms);
   if (buf && cap > 0) {
     std::strncpy(buf, tmp, (size_t)cap - 1);

@@ -139,7 +139,7 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   WC_HIP_CHECK(hipMemsetAsync(d_ctr, 0, sizeof(DevCounters), s));
   Records r = rec;
   r.cap = (uint32_t)std::min<uint64_t>(rec_total / (((uint64_t)1 << log2_rb) * blocks), 0xFFFFFFFFull);
-  MapArgs m{text, len, avail, prev, log2_rb, r, d_ctr->flags, &d_ctr->tokens};
+  MapArgs m{text, len, avail, prev, log2_rb, r, d_ctr->flags, &d_ctr->tokens, &d_ctr->records};
   launch_map(m, blocks, s);
   ReduceArgs ra{r,      blocks, log2_rb, table(), text, avail, base, Arena{d_arena, d_arena_cursor, opt.arena_bytes},
                 d_ctr->flags, d_bucket_ovf, nullptr};
@@ -185,6 +185,7 @@ void Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
     return;
   }
   const uint64_t tokens = c.tokens;
+  st.records += c.records;
   uint32_t max_occ = c.flags[FLAG_MAX_OCC];
   while (c.flags[FLAG_TABLE_OVF]) {
     if (c.flags[FLAG_ARENA_OVF]) break;

@@ -18,7 +18,7 @@ namespace wc {
 struct DevCounters {
   uint32_t flags[FLAG_COUNT];
   unsigned long long tokens;
-  unsigned long long pad;
+  unsigned long long records;
 };
 
 // Running table storage (own allocation: it grows by splitting).

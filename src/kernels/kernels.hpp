@@ -21,8 +21,8 @@ constexpr int MAP_BPL = 32;                          // text bytes per lane
 constexpr int MAP_TILE = MAP_THREADS * MAP_BPL;      // 16 KiB LDS text tile
 constexpr int MAP_HALO = 256;                        // bytes past the tile kept in LDS
 constexpr int MAP_SLOTS = 2048;                      // LDS pre-aggregation slots
-constexpr int MAP_FLUSH_AT = 1024;                   // flush when this many keys
-constexpr int MAP_MAX_PROBE = 64;
+constexpr int MAP_FLUSH_AT = MAP_SLOTS * 3 / 8;      // flush before a tile when fuller
+constexpr int MAP_MAX_PROBE = 16;
 constexpr int MAX_REC_BUCKETS_LOG2 = 10;             // shuffle partitions <= 1024
 constexpr int MAX_REC_BUCKETS = 1 << MAX_REC_BUCKETS_LOG2;
 
@@ -71,7 +71,8 @@ struct MapArgs {
   uint32_t log2_rec_buckets;
   Records rec;
   uint32_t* flags;
-  unsigned long long* tokens;  // += tokens owned by this chunk
+  unsigned long long* tokens;   // += tokens owned by this chunk
+  unsigned long long* records;  // += shuffle records emitted (combiner efficiency)
 };
 
 struct ReduceArgs {

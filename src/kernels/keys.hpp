@@ -49,8 +49,14 @@ WC_HD uint64_t fmix64(uint64_t k) {
   return k;
 }
 
-// k1 for a word of `len` bytes whose full-word FNV-1a-64 is `h`.
-WC_HD uint64_t make_k1(uint64_t len, uint64_t h) { return len <= 8 ? len : (K1_TAG | (h & K1_HASH_MASK)); }
+// Long-word tail hash: word-wise FNV-1a-64 over the 8-byte little-endian
+// chunks that follow k0 (last chunk zero-padded), folded with the length and
+// finalised with fmix64.  Chunk-at-a-time so the map kernel hashes straight
+// from registers (one fold per 8 bytes instead of one per byte).
+WC_HD uint64_t tail_fold(uint64_t h, uint64_t chunk) { return (h ^ chunk) * FNV_PRIME; }
+WC_HD uint64_t make_k1(uint64_t len, uint64_t h) {
+  return len <= 8 ? len : (K1_TAG | (fmix64(h ^ len) & K1_HASH_MASK));
+}
 
 // Placement hash: word-wise FNV-1a over the packed key (k0, k1), then fmix64.
 // Top bits select the shuffle bucket, low bits the slot inside the bucket.
@@ -67,11 +73,19 @@ WC_HD uint32_t bucket_of(uint64_t ph, uint32_t log2_buckets) {
 
 // Host helper: key of an explicit byte string.
 WC_HD void key_of(const uint8_t* w, uint64_t len, uint64_t* k0, uint64_t* k1) {
-  uint64_t a = 0, h = FNV_OFFSET;
+  uint64_t a = 0, h = FNV_OFFSET, chunk = 0;
   for (uint64_t i = 0; i < len; ++i) {
-    if (i < 8) a |= (uint64_t)w[i] << (8 * i);
-    h = fnv1a_step(h, w[i]);
+    if (i < 8) {
+      a |= (uint64_t)w[i] << (8 * i);
+    } else {
+      chunk |= (uint64_t)w[i] << (8 * (i & 7));
+      if ((i & 7) == 7) {
+        h = tail_fold(h, chunk);
+        chunk = 0;
+      }
+    }
   }
+  if (len > 8 && (len & 7)) h = tail_fold(h, chunk);
   *k0 = a;
   *k1 = make_k1(len, h);
 }
