@@ -13,6 +13,7 @@
 //    region overflow re-runs the chunk in halves, running-table overflow
 //    splits the table (B -> 2B) and re-runs only the overflowed buckets.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "engine_impl.hpp"
@@ -55,6 +56,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   WC_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   WC_HIP_CHECK(hipStreamCreateWithFlags(&copy_s, hipStreamNonBlocking));
   map_blocks = opt.map_blocks ? opt.map_blocks : 2u * (uint32_t)device_cu_count(dev);
+  if (const char* e = std::getenv("WC_ABLATE_MAP")) ablate_map = (uint32_t)std::atoi(e);  // profiling only
 
   opt.log2_rec_buckets = std::min<uint32_t>(opt.log2_rec_buckets, MAX_REC_BUCKETS_LOG2);
   opt.max_log2_tab_buckets = std::min<uint32_t>(std::max<uint32_t>(opt.max_log2_tab_buckets, 1), 20);
@@ -65,12 +67,16 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   opt.chunk_bytes = opt.chunk_bytes / MAP_TILE * MAP_TILE;
 
   rec_total = std::max<uint64_t>(opt.min_records, (uint64_t)((double)opt.chunk_bytes * opt.records_per_byte));
-  const size_t region_words = (size_t)MAX_REC_BUCKETS * map_blocks;
-  rec_mem.reserve(rec_total * 3 * sizeof(uint64_t) + region_words * 4 + 4096);
-  rec.k0 = rec_mem.take_n<uint64_t>(rec_total);
-  rec.k1 = rec_mem.take_n<uint64_t>(rec_total);
-  rec.co = rec_mem.take_n<uint64_t>(rec_total);
-  rec.region_count = rec_mem.take_n<uint32_t>(region_words);
+  // flush directory: at most one flush per tile (+ retries, + the final one)
+  dir_per_block_max = dir_per_block_for(opt.chunk_bytes, map_blocks);
+  const size_t dir_cols = (size_t)map_blocks * dir_per_block_max;
+  const size_t nrb1 = ((size_t)1 << opt.log2_rec_buckets) + 1;
+  rec_mem.reserve(rec_total * sizeof(Rec) + dir_cols * (8 + 4 * nrb1) + map_blocks * 4 + 8192);
+  rec.recs = rec_mem.take_n<Rec>(rec_total);
+  rec.cap = rec_total;
+  rec.dir_base = rec_mem.take_n<uint64_t>(dir_cols);
+  rec.dir_off = rec_mem.take_n<uint32_t>(dir_cols * nrb1);
+  rec.dir_count = rec_mem.take_n<uint32_t>(map_blocks);
 
   WC_HIP_CHECK(hipMalloc(&d_ctr, sizeof(DevCounters)));
   WC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_ctr), sizeof(DevCounters), hipHostMallocDefault));
@@ -137,11 +143,13 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
                                uint32_t log2_rb, uint32_t blocks) {
   WC_CHECK((reinterpret_cast<uintptr_t>(text) & 15) == 0, "chunk text must be 16-byte aligned");
   WC_HIP_CHECK(hipMemsetAsync(d_ctr, 0, sizeof(DevCounters), s));
-  Records r = rec;
-  r.cap = (uint32_t)std::min<uint64_t>(rec_total / (((uint64_t)1 << log2_rb) * blocks), 0xFFFFFFFFull);
-  MapArgs m{text, len, avail, prev, log2_rb, r, d_ctr->flags, &d_ctr->tokens, &d_ctr->records};
+  pass_rec = rec;
+  pass_rec.cursor = &d_ctr->records;
+  pass_rec.dir_per_block = dir_per_block_for(len, blocks);
+  MapArgs m{text, len, avail, prev, log2_rb, pass_rec, d_ctr->flags, &d_ctr->tokens, ablate_map};
   launch_map(m, blocks, s);
-  ReduceArgs ra{r,      blocks, log2_rb, table(), text, avail, base, Arena{d_arena, d_arena_cursor, opt.arena_bytes},
+  ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
+                avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
                 d_ctr->flags, d_bucket_ovf, nullptr};
   launch_reduce(ra, s);
   WC_HIP_CHECK(hipMemcpyAsync(h_ctr, d_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));
@@ -198,9 +206,8 @@ void Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
     WC_HIP_CHECK(hipMemcpyAsync(d_bucket_en, en.data(), en.size(), hipMemcpyHostToDevice, s));
     WC_HIP_CHECK(hipMemsetAsync(d_bucket_ovf, 0, en.size() * 4, s));
     WC_HIP_CHECK(hipMemsetAsync(d_ctr, 0, sizeof(DevCounters), s));
-    Records r = rec;
-    r.cap = (uint32_t)std::min<uint64_t>(rec_total / (((uint64_t)1 << log2_rb) * blocks), 0xFFFFFFFFull);
-    ReduceArgs ra{r,      blocks, log2_rb, table(), text, avail, base, Arena{d_arena, d_arena_cursor, opt.arena_bytes},
+    ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
+                  avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
                   d_ctr->flags, d_bucket_ovf, d_bucket_en};
     launch_reduce(ra, s);
     WC_HIP_CHECK(hipMemcpyAsync(h_ctr, d_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));

@@ -43,10 +43,17 @@ struct Engine::Impl {
   int dev = 0;
   hipStream_t s = nullptr, copy_s = nullptr;
   uint32_t map_blocks = 0;
+  uint32_t ablate_map = 0;  // WC_ABLATE_MAP (profiling ablations, MapArgs::ablate)
 
   // shuffle records
   uint64_t rec_total = 0;
-  Records rec{};
+  Records rec{};       // full-capacity views
+  Records pass_rec{};  // views of the current map/reduce pass
+  uint32_t dir_per_block_max = 0;
+  static uint32_t dir_per_block_for(uint64_t len, uint32_t blocks) {
+    const uint64_t tiles = (len + MAP_TILE - 1) / MAP_TILE;
+    return (uint32_t)(2 * ((tiles + blocks - 1) / blocks) + 8);
+  }
   DeviceArena rec_mem;
 
   // counters + pinned mirror

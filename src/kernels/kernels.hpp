@@ -20,9 +20,10 @@ constexpr int MAP_THREADS = 512;                     // 8 waves
 constexpr int MAP_BPL = 32;                          // text bytes per lane
 constexpr int MAP_TILE = MAP_THREADS * MAP_BPL;      // 16 KiB LDS text tile
 constexpr int MAP_HALO = 256;                        // bytes past the tile kept in LDS
-constexpr int MAP_SLOTS = 2048;                      // LDS pre-aggregation slots
+constexpr int MAP_SLOTS = 2048;                      // LDS combiner slots (groups of 4)
+constexpr int MAP_GROUPS = MAP_SLOTS / 4;
 constexpr int MAP_FLUSH_AT = MAP_SLOTS * 3 / 8;      // flush before a tile when fuller
-constexpr int MAP_MAX_PROBE = 16;
+constexpr int MAP_MAX_GROUP_PROBES = 8;              // then flush and retry the token
 constexpr int MAX_REC_BUCKETS_LOG2 = 10;             // shuffle partitions <= 1024
 constexpr int MAX_REC_BUCKETS = 1 << MAX_REC_BUCKETS_LOG2;
 
@@ -31,18 +32,31 @@ constexpr int TAB_SLOTS_LOG2 = 12;
 constexpr int TAB_SLOTS = 1 << TAB_SLOTS_LOG2;       // 4096 slots x 32 B = 128 KiB LDS
 constexpr int TAB_MAX_OCC = TAB_SLOTS * 7 / 8;       // overflow -> split the table
 constexpr int TAB_SPLIT_AT = TAB_SLOTS * 5 / 8;      // proactive split threshold
-constexpr int TAB_MAX_PROBE = 512;
+constexpr int TAB_GROUPS = TAB_SLOTS / 4;
+constexpr int TAB_MAX_GROUP_PROBES = 64;
 
 // ---- flags word indices ------------------------------------------------------
 enum : int { FLAG_REGION_OVF = 0, FLAG_ARENA_OVF = 1, FLAG_TABLE_OVF = 2, FLAG_MAX_OCC = 3, FLAG_COUNT = 4 };
 
-// Shuffle records, SoA (24 B / record): key words and (count << 32 | chunk offset).
+// One shuffle record: key words and (count << 32 | chunk-relative first offset).
+struct Rec {
+  uint64_t k0, k1, co;
+};
+
+// Shuffle output.  Every combiner flush of map block p writes ONE contiguous,
+// bucket-sorted chunk of records (coalesced stores) and a directory entry j:
+//   dir_base[p * dir_per_block + j]                      first record of the chunk
+//   dir_off[(b * map_blocks + p) * dir_per_block + j]    start of bucket b in it (b = 0..B)
+// Bucket-major directory rows let the reducer of bucket b read its run
+// boundaries for consecutive flushes with coalesced loads.
 struct Records {
-  uint64_t* k0;
-  uint64_t* k1;
-  uint64_t* co;
-  uint32_t* region_count;  // [n_rec_buckets * map_blocks]
-  uint32_t cap;            // records per (bucket, map block) region
+  Rec* recs;
+  unsigned long long* cursor;  // records allocated so far (device counter)
+  uint64_t cap;                // record capacity
+  uint64_t* dir_base;
+  uint32_t* dir_off;
+  uint32_t* dir_count;  // [map_blocks] flushes written per block
+  uint32_t dir_per_block;
 };
 
 // Running key table: n_buckets x TAB_SLOTS open-addressing slices.
@@ -72,12 +86,12 @@ struct MapArgs {
   Records rec;
   uint32_t* flags;
   unsigned long long* tokens;   // += tokens owned by this chunk
-  unsigned long long* records;  // += shuffle records emitted (combiner efficiency)
+  uint32_t ablate;             // profiling: 0 full map; 1 keys only (no combiner); 2 scan only
 };
 
 struct ReduceArgs {
   Records rec;
-  uint32_t map_blocks;
+  uint32_t map_blocks;  // grid of the map pass that wrote `rec`
   uint32_t log2_rec_buckets;
   TableView tab;
   const uint8_t* text;  // the same chunk, for copying new long words

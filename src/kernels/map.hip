@@ -16,28 +16,37 @@
 //     funnel shift + mask, and (> 8 bytes) the tail hash one 8-byte chunk at a
 //     time.  Only tokens longer than the window take a byte loop (LDS halo,
 //     then global).
-//  4. Keys are combined in an LDS open-addressing table (the MapReduce
-//     combiner), kept across tiles while it is sparse, so Zipf text collapses
-//     to one record per hot word per block.  Probing is bounded: a key that
-//     finds no slot within MAP_MAX_PROBE ships as a singleton record.
-//  5. Flush = shuffle write: each record goes to partition
-//     bucket_of(place_hash) in a per-(bucket, block) region, so the reducer
-//     reads its bucket contiguously and no global atomics are needed.
+//  4. Keys are combined in a group-probed LDS hash table (lds_table.hpp): the
+//     MapReduce combiner, kept across tiles while it is sparse, so Zipf text
+//     collapses to one record per hot word per block.  A token that finds no
+//     slot makes the block flush and retry it (no singleton fallback).
+//  5. Flush = shuffle write: occupied slots are counting-sorted by shuffle
+//     bucket (LDS histogram + block scan) and written as ONE contiguous chunk
+//     (coalesced) plus a bucket-offset directory entry; the reducer of bucket
+//     b reads its run of every chunk.
 #include "kernels.hpp"
 #include "lds_table.hpp"
 
 namespace wc {
 namespace dev {
 
+constexpr int MAP_SPT = MAP_SLOTS / MAP_THREADS;  // table slots per thread in a flush
+static_assert(MAP_SLOTS % MAP_THREADS == 0, "flush assumes whole slots per thread");
+
 struct MapLds {
+  uint32_t tags[MAP_SLOTS];  // first: 16-B aligned for the ds_read_b128 group reads
   uint64_t k0[MAP_SLOTS];
   uint64_t k1[MAP_SLOTS];
   uint32_t cnt[MAP_SLOTS];
   uint32_t off[MAP_SLOTS];
-  uint32_t cursor[MAX_REC_BUCKETS];
-  uint8_t tile[MAP_TILE + MAP_HALO];
+  uint32_t boff[MAX_REC_BUCKETS + 4];  // bucket counts -> exclusive offsets (+ total)
+  uint8_t tile[MAP_TILE + MAP_HALO + 16];  // +16: tile8() reads one word past
+  uint32_t wsum[MAP_THREADS / 64];
   uint32_t occupied;
   uint32_t prev;
+  uint32_t flush_ok;
+  uint32_t nflush;  // directory entries written by this block
+  uint64_t flush_base;
   unsigned long long tokens;
 };
 
@@ -49,15 +58,12 @@ __device__ __forceinline__ uint64_t delim_mask8(uint64_t x) {
   return ((m >> 7) * 0x0102040810204080ull) >> 56;
 }
 
-// 8 bytes starting at byte b (0..63) of the 64-byte window w[0..7] (zero past it).
-__device__ __forceinline__ uint64_t window8(const uint64_t (&w)[8], uint32_t b) {
-  const uint32_t q = b >> 3, sh = (b & 7) * 8;
-  uint64_t lo = 0, hi = 0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    lo = (q == (uint32_t)j) ? w[j] : lo;
-    hi = (q + 1 == (uint32_t)j) ? w[j] : hi;
-  }
+// 8 bytes of the LDS tile starting at byte p: two aligned ds_read_b64 + funnel
+// shift (dynamic indexing of a register window would be lowered to scratch).
+__device__ __forceinline__ uint64_t tile8(const uint8_t* tile, uint32_t p) {
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(tile + (p & ~7u));
+  const uint32_t sh = (p & 7) * 8;
+  const uint64_t lo = q[0], hi = q[1];
   return sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
 }
 
@@ -65,35 +71,107 @@ __device__ __forceinline__ uint64_t low_bytes(uint64_t v, uint32_t n) {
   return n >= 8 ? v : (v & ((1ull << (8 * n)) - 1ull));
 }
 
-__device__ __forceinline__ void emit_record(MapLds& L, const MapArgs& a, uint64_t k0, uint64_t k1, uint32_t cnt,
-                                            uint32_t off) {
-  const uint32_t b = bucket_of(place_hash(k0, k1), a.log2_rec_buckets);
-  const uint32_t pos = atomicAdd(&L.cursor[b], 1u);
-  if (pos < a.rec.cap) {
-    const size_t r = ((size_t)b * gridDim.x + blockIdx.x) * a.rec.cap + pos;
-    a.rec.k0[r] = k0;
-    a.rec.k1[r] = k1;
-    a.rec.co[r] = ((uint64_t)cnt << 32) | off;
+// Exclusive scan of a[0..n) in place (n <= MAX_REC_BUCKETS); a[n] = total.
+__device__ void block_exclusive_scan(uint32_t* a, uint32_t n, uint32_t* wsum) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int PER = (MAX_REC_BUCKETS + MAP_THREADS - 1) / MAP_THREADS;
+  uint32_t v[PER], s = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const uint32_t i = tid * PER + k;
+    v[k] = i < n ? a[i] : 0;
+    s += v[k];
   }
+  uint32_t x = s;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  uint32_t before = 0, total = 0;
+  for (int w = 0; w < MAP_THREADS / 64; ++w) {
+    before += w < wave ? wsum[w] : 0;
+    total += wsum[w];
+  }
+  uint32_t run = before + x - s;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const uint32_t i = tid * PER + k;
+    if (i < n) a[i] = run;
+    run += v[k];
+  }
+  if (tid == 0) a[n] = total;
+  __syncthreads();
 }
 
-__device__ __forceinline__ void flush_table(MapLds& L, const MapArgs& a) {
-  for (int s = threadIdx.x; s < MAP_SLOTS; s += MAP_THREADS) {
-    const uint64_t k1 = L.k1[s];
-    if (k1 != K1_EMPTY) {
-      emit_record(L, a, L.k0[s], k1, L.cnt[s], L.off[s]);
-      L.k1[s] = K1_EMPTY;
-      L.cnt[s] = 0;
-      L.off[s] = 0xFFFFFFFFu;
+// Shuffle write of the combiner table: one contiguous bucket-sorted chunk.
+__device__ void flush_table(MapLds& L, const MapArgs& a) {
+  const int tid = threadIdx.x;
+  const uint32_t nb = 1u << a.log2_rec_buckets;
+  for (uint32_t b = tid; b <= nb; b += MAP_THREADS) L.boff[b] = 0;
+  __syncthreads();
+  uint32_t sb[MAP_SPT], sr[MAP_SPT];
+#pragma unroll
+  for (int j = 0; j < MAP_SPT; ++j) {
+    const int s = tid + j * MAP_THREADS;
+    sb[j] = 0xFFFFFFFFu;
+    if (L.tags[s] > TAG_PENDING) {
+      sb[j] = bucket_of(place_hash(L.k0[s], L.k1[s]), a.log2_rec_buckets);
+      sr[j] = atomicAdd(&L.boff[sb[j]], 1u);
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) L.occupied = 0;
+  block_exclusive_scan(L.boff, nb, L.wsum);
+  const uint32_t n = L.boff[nb];
+  if (tid == 0) {
+    uint32_t ok = 0;
+    if (n) {
+      const uint64_t base = atomicAdd(a.rec.cursor, (unsigned long long)n);
+      const uint32_t j = L.nflush;
+      ok = (base + n <= a.rec.cap && j < a.rec.dir_per_block) ? 1u : 0u;
+      if (ok) {
+        L.nflush = j + 1;
+        a.rec.dir_base[(size_t)blockIdx.x * a.rec.dir_per_block + j] = base;
+      } else {
+        atomicOr(&a.flags[FLAG_REGION_OVF], 1u);
+      }
+      L.flush_base = base;
+    }
+    L.flush_ok = ok;
+  }
+  __syncthreads();
+  if (L.flush_ok) {
+    const uint32_t j = L.nflush - 1;
+    const size_t row = (size_t)gridDim.x * a.rec.dir_per_block;
+    for (uint32_t b = tid; b <= nb; b += MAP_THREADS)
+      a.rec.dir_off[b * row + (size_t)blockIdx.x * a.rec.dir_per_block + j] = L.boff[b];
+    const uint64_t base = L.flush_base;
+#pragma unroll
+    for (int k = 0; k < MAP_SPT; ++k) {
+      if (sb[k] == 0xFFFFFFFFu) continue;
+      const int s = tid + k * MAP_THREADS;
+      Rec r;
+      r.k0 = L.k0[s];
+      r.k1 = L.k1[s];
+      r.co = ((uint64_t)L.cnt[s] << 32) | L.off[s];
+      a.rec.recs[base + L.boff[sb[k]] + sr[k]] = r;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < MAP_SPT; ++k) {
+    const int s = tid + k * MAP_THREADS;
+    L.tags[s] = TAG_EMPTY;
+    L.cnt[s] = 0;
+    L.off[s] = 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  if (tid == 0) L.occupied = 0;
   __syncthreads();
 }
 
 // Key of a token that does not end inside the register window.
-__device__ __noinline__ void key_slow(const MapLds& L, const MapArgs& a, uint64_t pos, uint64_t g, uint64_t& k0,
+__device__ __forceinline__ void key_slow(const MapLds& L, const MapArgs& a, uint64_t pos, uint64_t g, uint64_t& k0,
                                       uint64_t& k1) {
   uint64_t len = 0, h = FNV_OFFSET, chunk = 0;
   k0 = 0;
@@ -122,19 +200,19 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_map_tokenize(MapArgs a) {
   __shared__ MapLds L;
   const int tid = threadIdx.x;
   for (int s = tid; s < MAP_SLOTS; s += MAP_THREADS) {
-    L.k1[s] = K1_EMPTY;
+    L.tags[s] = TAG_EMPTY;
     L.cnt[s] = 0;
     L.off[s] = 0xFFFFFFFFu;
   }
-  const uint32_t nb = 1u << a.log2_rec_buckets;
-  for (uint32_t b = tid; b < nb; b += MAP_THREADS) L.cursor[b] = 0;
   if (tid == 0) {
     L.occupied = 0;
     L.tokens = 0;
+    L.nflush = 0;
   }
 
   const uint64_t ntiles = (a.chunk_len + MAP_TILE - 1) / MAP_TILE;
   uint32_t my_tokens = 0;
+  uint64_t sink = 0;  // keeps ablated work alive
 
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const uint64_t t0 = tile * MAP_TILE;
@@ -185,58 +263,67 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_map_tokenize(MapArgs a) {
       starts &= (1u << (uint32_t)(a.chunk_len - lane_base)) - 1u;
     }
     my_tokens += __popc(starts);
+    if (a.ablate == 2) {
+      sink ^= dm;
+      continue;
+    }
 
-    while (starts) {
-      const uint32_t i = __ffs(starts) - 1;
-      starts &= starts - 1;
-      const uint64_t rest = dm >> i;
-      uint64_t k0, k1;
-      if (rest != 0) {
-        const uint32_t len = (uint32_t)__ffsll((unsigned long long)rest) - 1;  // ends inside the window
-        k0 = low_bytes(window8(w, i), len);
-        if (len <= 8) {
-          k1 = len;
+    uint32_t todo = starts;
+    for (;;) {
+      uint32_t failed = 0;
+      while (todo) {
+        const uint32_t i = __ffs(todo) - 1;
+        todo &= todo - 1;
+        const uint64_t rest = dm >> i;
+        uint64_t k0, k1;
+        if (rest != 0) {
+          const uint32_t len = (uint32_t)__ffsll((unsigned long long)rest) - 1;  // ends inside the window
+          const uint32_t p = tid * MAP_BPL + i;
+          k0 = low_bytes(tile8(L.tile, p), len);
+          if (len <= 8) {
+            k1 = len;
+          } else {
+            uint64_t h = FNV_OFFSET;
+            for (uint32_t c = 8; c < len; c += 8) h = tail_fold(h, low_bytes(tile8(L.tile, p + c), len - c));
+            k1 = make_k1(len, h);
+          }
         } else {
-          uint64_t h = FNV_OFFSET;
-          for (uint32_t c = 8; c < len; c += 8) h = tail_fold(h, low_bytes(window8(w, i + c), len - c));
-          k1 = make_k1(len, h);
+          key_slow(L, a, (uint64_t)tid * MAP_BPL + i, lane_base + i, k0, k1);
         }
-      } else {
-        key_slow(L, a, (uint64_t)tid * MAP_BPL + i, lane_base + i, k0, k1);
-      }
-      const uint32_t off = (uint32_t)(lane_base + i);
-      bool claimed;
-      const int s = lds_find_or_claim(L.k0, L.k1, MAP_SLOTS - 1, k0, k1,
-                                      (uint32_t)place_hash(k0, k1) & (MAP_SLOTS - 1), MAP_MAX_PROBE, claimed);
-      if (s >= 0) {
+        const uint32_t off = (uint32_t)(lane_base + i);
+        const uint64_t ph = place_hash(k0, k1);
+        if (a.ablate == 1) {
+          sink ^= ph + off;
+          continue;
+        }
+        bool claimed;
+        const int s = lds_find_or_claim(L.tags, L.k0, L.k1, MAP_GROUPS, ph, k0, k1, MAP_MAX_GROUP_PROBES, claimed);
+        if (s < 0) {
+          failed |= 1u << i;  // neighbourhood full: flush, then retry
+          continue;
+        }
         atomicAdd(&L.cnt[s], 1u);
         atomicMin(&L.off[s], off);
         if (claimed) atomicAdd(&L.occupied, 1u);
-      } else {
-        emit_record(L, a, k0, k1, 1u, off);  // crowded neighbourhood: ship the singleton
       }
+      todo = failed;
+      if (!__syncthreads_or(todo != 0)) break;
+      flush_table(L, a);
     }
   }
   __syncthreads();
-  flush_table(L, a);
+  if (L.occupied) flush_table(L, a);
 
-  unsigned long long recs = 0;
-  for (uint32_t b = tid; b < nb; b += MAP_THREADS) {
-    const uint32_t c = L.cursor[b];
-    recs += c;
-    a.rec.region_count[(size_t)b * gridDim.x + blockIdx.x] = c < a.rec.cap ? c : a.rec.cap;
-    if (c > a.rec.cap) atomicOr(&a.flags[FLAG_REGION_OVF], 1u);
-  }
-  // block totals -> one global atomic each
+  // block totals -> one global atomic
   uint64_t t = my_tokens;
-  for (int o = 32; o > 0; o >>= 1) {
-    t += __shfl_down(t, o);
-    recs += __shfl_down(recs, o);
-  }
+  for (int o = 32; o > 0; o >>= 1) t += __shfl_down(t, o);
   if ((tid & 63) == 0) atomicAdd(&L.tokens, (unsigned long long)t);
-  if ((tid & 63) == 0 && recs) atomicAdd(a.records, recs);
+  if (sink == 0x9E3779B97F4A7C15ull) atomicOr(&a.flags[FLAG_COUNT - 1], 0u);  // never true
   __syncthreads();
-  if (tid == 0) atomicAdd(a.tokens, L.tokens);
+  if (tid == 0) {
+    atomicAdd(a.tokens, L.tokens);
+    a.rec.dir_count[blockIdx.x] = L.nflush;
+  }
 }
 
 }  // namespace dev

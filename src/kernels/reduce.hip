@@ -6,13 +6,14 @@
 //
 //  wc_reduce_buckets  one 1024-thread block per table bucket (one per CU).
 //                     The bucket's 4096-slot slice of the running table is
-//                     loaded into LDS (128 KiB), the bucket's shuffle records
-//                     are streamed from every map block's region and merged
-//                     with LDS atomics (count +=, first_off = min), and the
-//                     slice is written back.  New long words copy their bytes
-//                     into the key arena so keys outlive streamed chunks.  If a
-//                     slice overflows it is NOT written back; the host splits
-//                     the table and re-runs only the overflowed buckets.
+//                     loaded into LDS (144 KiB with tags), the bucket's run of
+//                     every map flush is gathered (directory -> wave scan of
+//                     run lengths -> 64 consecutive records per wave step)
+//                     and merged with LDS atomics (count +=, first = min), and
+//                     the slice is written back.  New long words copy their
+//                     bytes into the key arena so keys outlive streamed chunks.
+//                     If a slice overflows it is NOT written back; the host
+//                     splits the table and re-runs only the overflowed buckets.
 //  wc_table_split     B -> 2B buckets (rehash into new slices).
 //  wc_table_compact   occupied slots -> dense columns (wave-aggregated atomics).
 #include "kernels.hpp"
@@ -22,6 +23,7 @@ namespace wc {
 namespace dev {
 
 struct RedLds {
+  uint32_t tags[TAB_SLOTS];  // first: 16-B aligned group reads
   uint64_t k0[TAB_SLOTS];
   uint64_t k1[TAB_SLOTS];
   uint64_t cnt[TAB_SLOTS];
@@ -33,18 +35,21 @@ struct RedLds {
 __device__ __forceinline__ void load_slice(RedLds& L, const TableView& t, uint32_t b) {
   const size_t base = (size_t)b * TAB_SLOTS;
   for (int s = threadIdx.x; s < TAB_SLOTS; s += blockDim.x) {
-    L.k0[s] = t.k0[base + s];
-    L.k1[s] = t.k1[base + s];
+    const uint64_t k0 = t.k0[base + s], k1 = t.k1[base + s];
+    L.k0[s] = k0;
+    L.k1[s] = k1;
     L.cnt[s] = t.cnt[base + s];
     L.first[s] = t.first[base + s];
+    L.tags[s] = k1 == K1_EMPTY ? TAG_EMPTY : make_tag(place_hash(k0, k1));
   }
 }
 
 __device__ __forceinline__ void store_slice(const RedLds& L, const TableView& t, uint32_t b) {
   const size_t base = (size_t)b * TAB_SLOTS;
   for (int s = threadIdx.x; s < TAB_SLOTS; s += blockDim.x) {
+    const bool occ = L.tags[s] > TAG_PENDING;
     t.k0[base + s] = L.k0[s];
-    t.k1[base + s] = L.k1[s];
+    t.k1[base + s] = occ ? L.k1[s] : K1_EMPTY;
     t.cnt[base + s] = L.cnt[s];
     t.first[base + s] = L.first[s];
   }
@@ -66,11 +71,29 @@ __device__ void arena_copy_word(const ReduceArgs& a, uint64_t off, size_t gslot)
   a.tab.sref_len[gslot] = (uint32_t)len;
 }
 
+__device__ __forceinline__ void merge_record(RedLds& L, const ReduceArgs& a, uint32_t b, const Rec& r, uint32_t shift) {
+  const uint64_t ph = place_hash(r.k0, r.k1);
+  if (shift && bucket_of(ph, a.tab.log2_buckets) != b) return;
+  bool claimed;
+  const int s = lds_find_or_claim(L.tags, L.k0, L.k1, TAB_GROUPS, ph, r.k0, r.k1, TAB_MAX_GROUP_PROBES, claimed);
+  if (s < 0) {
+    L.overflow = 1;
+    return;
+  }
+  atomicAdd(reinterpret_cast<unsigned long long*>(&L.cnt[s]), (unsigned long long)(r.co >> 32));
+  atomicMin(reinterpret_cast<unsigned long long*>(&L.first[s]),
+            (unsigned long long)(a.chunk_base + (r.co & 0xFFFFFFFFull)));
+  if (claimed) {
+    if (atomicAdd(&L.occupied, 1u) + 1 > (uint32_t)TAB_MAX_OCC) L.overflow = 1;
+    if (!key_is_short(r.k1)) arena_copy_word(a, r.co & 0xFFFFFFFFull, (size_t)b * TAB_SLOTS + s);
+  }
+}
+
 __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   __shared__ RedLds L;
   const uint32_t b = blockIdx.x;
   if (a.bucket_enable && !a.bucket_enable[b]) return;
-  if (a.flags[FLAG_REGION_OVF]) return;  // shuffle records incomplete: host re-runs the chunk
+  if (a.flags[FLAG_REGION_OVF]) return;  // shuffle output incomplete: host re-runs the chunk
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = RED_THREADS / 64;
   load_slice(L, a.tab, b);
   if (tid == 0) {
@@ -81,28 +104,42 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
 
   const uint32_t shift = a.tab.log2_buckets - a.log2_rec_buckets;  // table buckets per record bucket
   const uint32_t rb = b >> shift;
-  const uint32_t P = a.map_blocks;
-  for (uint32_t p = wave; p < P; p += nwaves) {
-    const size_t region = (size_t)rb * P + p;
-    const uint32_t n = a.rec.region_count[region];
-    const size_t base = region * a.rec.cap;
-    for (uint32_t i = lane; i < n; i += 64) {
-      const uint64_t k0 = a.rec.k0[base + i], k1 = a.rec.k1[base + i], co = a.rec.co[base + i];
-      const uint64_t ph = place_hash(k0, k1);
-      if (shift && bucket_of(ph, a.tab.log2_buckets) != b) continue;
-      const uint64_t cnt = co >> 32, first = a.chunk_base + (co & 0xFFFFFFFFull);
-      bool claimed;
-      const int s = lds_find_or_claim(L.k0, L.k1, TAB_SLOTS - 1, k0, k1, (uint32_t)ph & (TAB_SLOTS - 1),
-                                      TAB_MAX_PROBE, claimed);
-      if (s < 0) {
-        L.overflow = 1;
-        continue;
+  const uint32_t J = a.rec.dir_per_block;
+  const size_t row = (size_t)a.map_blocks * J;
+  const uint32_t* lo_row = a.rec.dir_off + (size_t)rb * row;
+  const uint32_t* hi_row = lo_row + row;
+  for (uint32_t p = wave; p < a.map_blocks; p += nwaves) {
+    const uint32_t nf = a.rec.dir_count[p];
+    for (uint32_t j0 = 0; j0 < nf; j0 += 64) {
+      // one flush per lane: its run [lo, hi) of bucket rb
+      const uint32_t j = j0 + lane;
+      const size_t col = (size_t)p * J + j;
+      uint32_t len = 0;
+      uint64_t start = 0;
+      if (j < nf) {
+        const uint32_t lo = lo_row[col];
+        len = hi_row[col] - lo;
+        start = a.rec.dir_base[col] + lo;
       }
-      atomicAdd(reinterpret_cast<unsigned long long*>(&L.cnt[s]), (unsigned long long)cnt);
-      atomicMin(reinterpret_cast<unsigned long long*>(&L.first[s]), (unsigned long long)first);
-      if (claimed) {
-        if (atomicAdd(&L.occupied, 1u) + 1 > (uint32_t)TAB_MAX_OCC) L.overflow = 1;
-        if (!key_is_short(k1)) arena_copy_word(a, co & 0xFFFFFFFFull, (size_t)b * TAB_SLOTS + s);
+      // concatenate the 64 runs: inclusive scan of run lengths
+      uint32_t incl = len;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+      }
+      const uint32_t total = __shfl(incl, 63);
+      const uint32_t excl = incl - len;
+      for (uint32_t k = 0; k < total; k += 64) {
+        const uint32_t q = k + lane;
+        // owner lane: the last lane whose exclusive prefix is <= q
+        int o = 0;
+        for (int step = 32; step > 0; step >>= 1) {
+          const uint32_t e = __shfl(excl, o + step);
+          if (o + step < 64 && e <= q) o += step;
+        }
+        const uint64_t ostart = __shfl(start, o);
+        const uint32_t oexcl = __shfl(excl, o);
+        if (q < total) merge_record(L, a, b, a.rec.recs[ostart + (q - oexcl)], shift);
       }
     }
   }
@@ -126,7 +163,7 @@ __global__ void __launch_bounds__(RED_THREADS) wc_table_split(TableView src, Tab
   __shared__ RedLds L;
   const uint32_t nb = blockIdx.x, ob = nb >> 1;
   for (int s = threadIdx.x; s < TAB_SLOTS; s += blockDim.x) {
-    L.k1[s] = K1_EMPTY;
+    L.tags[s] = TAG_EMPTY;
     L.cnt[s] = 0;
     L.first[s] = ~0ull;
   }
@@ -140,8 +177,7 @@ __global__ void __launch_bounds__(RED_THREADS) wc_table_split(TableView src, Tab
     const uint64_t ph = place_hash(k0, k1);
     if (bucket_of(ph, dst.log2_buckets) != nb) continue;
     bool claimed;
-    const int d = lds_find_or_claim(L.k0, L.k1, TAB_SLOTS - 1, k0, k1, (uint32_t)ph & (TAB_SLOTS - 1), TAB_SLOTS,
-                                    claimed);
+    const int d = lds_find_or_claim(L.tags, L.k0, L.k1, TAB_GROUPS, ph, k0, k1, TAB_GROUPS, claimed);
     // d >= 0 always: a child receives at most the parent's occupancy.
     L.cnt[d] = src.cnt[obase + s];
     L.first[d] = src.first[obase + s];
