@@ -151,7 +151,7 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                 avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
                 d_ctr->flags, d_bucket_ovf, nullptr};
-  launch_reduce(ra, s);
+  if (!ablate_map) launch_reduce(ra, s);  // ablated map output is not a valid shuffle
   WC_HIP_CHECK(hipMemcpyAsync(h_ctr, d_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));
 }
 
@@ -202,7 +202,7 @@ void Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
     WC_HIP_CHECK(hipMemcpy(ovf.data(), d_bucket_ovf, ovf.size() * 4, hipMemcpyDeviceToHost));
     split_table();
     std::vector<uint8_t> en(ovf.size() * 2);
-    for (size_t b = 0; b < en.size(); ++b) en[b] = ovf[b >> 1] ? 1 : 0;
+    for (size_t b = 0; b < en.size(); ++b) en[b] = ovf[b & (ovf.size() - 1)] ? 1 : 0;  // parent = b mod B
     WC_HIP_CHECK(hipMemcpyAsync(d_bucket_en, en.data(), en.size(), hipMemcpyHostToDevice, s));
     WC_HIP_CHECK(hipMemsetAsync(d_bucket_ovf, 0, en.size() * 4, s));
     WC_HIP_CHECK(hipMemsetAsync(d_ctr, 0, sizeof(DevCounters), s));

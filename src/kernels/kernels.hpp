@@ -24,7 +24,7 @@ constexpr int MAP_SLOTS = 2048;                      // LDS combiner slots (grou
 constexpr int MAP_GROUPS = MAP_SLOTS / 4;
 constexpr int MAP_FLUSH_AT = MAP_SLOTS * 3 / 8;      // flush before a tile when fuller
 constexpr int MAP_MAX_GROUP_PROBES = 8;              // then flush and retry the token
-constexpr int MAX_REC_BUCKETS_LOG2 = 10;             // shuffle partitions <= 1024
+constexpr int MAX_REC_BUCKETS_LOG2 = 9;              // shuffle partitions <= 512
 constexpr int MAX_REC_BUCKETS = 1 << MAX_REC_BUCKETS_LOG2;
 
 constexpr int RED_THREADS = 1024;                    // 16 waves, one block per CU

@@ -59,7 +59,9 @@ WC_HD uint64_t make_k1(uint64_t len, uint64_t h) {
 }
 
 // Placement hash: word-wise FNV-1a over the packed key (k0, k1), then fmix64.
-// Top bits select the shuffle bucket, low bits the slot inside the bucket.
+// Bits [2, 2+log2 B) select the shuffle / table bucket (they live inside the
+// 32-bit LDS tag, so a flush recovers the bucket without rehashing), bits
+// [32, ..) the slot group inside a bucket's table.
 WC_HD uint64_t place_hash(uint64_t k0, uint64_t k1) {
   uint64_t h = FNV_OFFSET;
   h = (h ^ k0) * FNV_PRIME;
@@ -67,8 +69,9 @@ WC_HD uint64_t place_hash(uint64_t k0, uint64_t k1) {
   return fmix64(h);
 }
 
+// Nested: the bucket under 2B buckets is b or b + B for bucket b under B.
 WC_HD uint32_t bucket_of(uint64_t ph, uint32_t log2_buckets) {
-  return log2_buckets == 0 ? 0u : (uint32_t)(ph >> (64 - log2_buckets));
+  return (uint32_t)(ph >> 2) & ((1u << log2_buckets) - 1u);
 }
 
 // Host helper: key of an explicit byte string.

@@ -2,18 +2,22 @@
 // word key (keys.hpp).  Used by the map kernel (per-block combiner) and the
 // reduce kernel (per-bucket slice of the running table).
 //
-// Layout: slots are grouped by 4; a parallel array of 32-bit tags (derived
-// from the placement hash) lets one ds_read_b128 test a whole group, so a
-// lookup is ONE dependent LDS round trip in the common case even at 80-90%
-// load, instead of a chain of single-slot probes (which made every wave wait
-// for its unluckiest lane).  Groups fill left to right and slots are never
-// freed until the table is cleared, so linear probing over groups is exact.
+// Layout: slots come in groups of 4 stored together (SlotGroup, 80 B): four
+// 32-bit tags derived from the placement hash, then the four k1 and four k0.
+// A lookup reads the whole group with five ds_read_b128 issued back to back —
+// ONE dependent LDS round trip — and compares in registers, so the common
+// case (key present) needs no further LDS reads and no divergent branches.
+// Groups fill left to right and slots are never freed until the table is
+// cleared, so linear probing over groups is exact.
 //
 // Claim protocol (no spin inside a branch, so lanes of one wave can never
 // dead-lock on each other): tag 0 -> PENDING by LDS CAS, the claimer writes
-// k0/k1, then publishes the real tag (never 0 or PENDING).  A prober that sees
-// PENDING in a group re-reads that group on its next loop iteration; the
-// claimer always finishes its publish inside the iteration that won the CAS.
+// k0/k1, waits for them, then publishes the real tag (never 0 or PENDING).
+// The tag is the publish flag: a reader only trusts k0/k1 of a slot whose tag
+// it saw published, and it reads the tags before the keys (LDS executes one
+// wave's reads in order).  A prober that sees PENDING in a group re-reads the
+// group on its next loop iteration; the claimer always finishes its publish
+// inside the iteration that won the CAS.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -25,47 +29,54 @@ namespace dev {
 constexpr uint32_t TAG_EMPTY = 0u;
 constexpr uint32_t TAG_PENDING = 1u;
 
+struct alignas(16) SlotGroup {
+  uint32_t tag[4];
+  uint64_t k1[4];
+  uint64_t k0[4];
+};
+static_assert(sizeof(SlotGroup) == 80, "SlotGroup layout");
+
 __device__ __forceinline__ uint32_t make_tag(uint64_t ph) { return ((uint32_t)ph & ~1u) | 2u; }
 __device__ __forceinline__ uint32_t group_of(uint64_t ph, uint32_t ngroups) {
   return (uint32_t)(ph >> 32) & (ngroups - 1);
 }
 
-// Returns the slot holding (k0,k1) — claiming the first empty slot of the
-// first non-full group if the key is new (claimed = true) — or -1 after
-// `max_groups` full groups.
-__device__ __forceinline__ int lds_find_or_claim(uint32_t* tags, uint64_t* k0s, uint64_t* k1s, uint32_t ngroups,
-                                                 uint64_t ph, uint64_t k0, uint64_t k1, int max_groups,
-                                                 bool& claimed) {
+// Returns the slot (4 * group + lane-in-group) holding (k0,k1) — claiming the
+// first empty slot of the first non-full group if the key is new
+// (claimed = true) — or -1 after `max_groups` full groups.
+__device__ __forceinline__ int lds_find_or_claim(SlotGroup* groups, uint32_t ngroups, uint64_t ph, uint64_t k0,
+                                                 uint64_t k1, int max_groups, bool& claimed) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
   const uint32_t tag = make_tag(ph);
   uint32_t g = group_of(ph, ngroups);
   int steps = 0;
   claimed = false;
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   for (;;) {
-    // Plain (non-volatile) load so it stays a ds_read_b128; the asm barrier
-    // stops the compiler from reusing a previous iteration's value.
+    // Plain loads stay ds_read_b128; the asm barrier stops reuse across iterations.
     asm volatile("" ::: "memory");
-    const u32x4 q = *reinterpret_cast<const u32x4*>(&tags[4 * g]);
-    const uint32_t m_match = (q.x == tag) | (q.y == tag) << 1 | (q.z == tag) << 2 | (q.w == tag) << 3;
-    const uint32_t m_pend = (q.x == TAG_PENDING) | (q.y == TAG_PENDING) << 1 | (q.z == TAG_PENDING) << 2 |
-                            (q.w == TAG_PENDING) << 3;
-    const uint32_t m_empty = (q.x == TAG_EMPTY) | (q.y == TAG_EMPTY) << 1 | (q.z == TAG_EMPTY) << 2 |
-                             (q.w == TAG_EMPTY) << 3;
-    for (uint32_t mm = m_match; mm; mm &= mm - 1) {  // almost always 0 or 1 iteration
-      const int s = 4 * g + (__ffs(mm) - 1);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      if (k0s[s] == k0 && k1s[s] == k1) return s;
-    }
-    if (m_pend) continue;  // someone is publishing in this group: look again
-    if (m_empty) {
-      const int s = 4 * g + (__ffs(m_empty) - 1);
-      if (atomicCAS(&tags[s], TAG_EMPTY, TAG_PENDING) == TAG_EMPTY) {
-        k0s[s] = k0;
-        k1s[s] = k1;
+    SlotGroup& G = groups[g];
+    const u32x4 t = *reinterpret_cast<const u32x4*>(G.tag);
+    const u64x2 a1 = *reinterpret_cast<const u64x2*>(&G.k1[0]);
+    const u64x2 b1 = *reinterpret_cast<const u64x2*>(&G.k1[2]);
+    const u64x2 a0 = *reinterpret_cast<const u64x2*>(&G.k0[0]);
+    const u64x2 b0 = *reinterpret_cast<const u64x2*>(&G.k0[2]);
+    const bool h0 = t.x == tag && a1.x == k1 && a0.x == k0;
+    const bool h1 = t.y == tag && a1.y == k1 && a0.y == k0;
+    const bool h2 = t.z == tag && b1.x == k1 && b0.x == k0;
+    const bool h3 = t.w == tag && b1.y == k1 && b0.y == k0;
+    if (h0 | h1 | h2 | h3) return 4 * (int)g + (h0 ? 0 : (h1 ? 1 : (h2 ? 2 : 3)));
+    if (t.x == TAG_PENDING || t.y == TAG_PENDING || t.z == TAG_PENDING || t.w == TAG_PENDING)
+      continue;  // someone is publishing in this group: look again
+    const int e = t.x == TAG_EMPTY ? 0 : (t.y == TAG_EMPTY ? 1 : (t.z == TAG_EMPTY ? 2 : (t.w == TAG_EMPTY ? 3 : -1)));
+    if (e >= 0) {
+      if (atomicCAS(&G.tag[e], TAG_EMPTY, TAG_PENDING) == TAG_EMPTY) {
+        G.k0[e] = k0;
+        G.k1[e] = k1;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __hip_atomic_store(&tags[s], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&G.tag[e], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         claimed = true;
-        return s;
+        return 4 * (int)g + e;
       }
       continue;  // lost the race for that slot: re-read the group
     }
@@ -73,6 +84,10 @@ __device__ __forceinline__ int lds_find_or_claim(uint32_t* tags, uint64_t* k0s, 
     g = (g + 1) & (ngroups - 1);
   }
 }
+
+__device__ __forceinline__ uint32_t slot_tag(const SlotGroup* groups, int s) { return groups[s >> 2].tag[s & 3]; }
+__device__ __forceinline__ uint64_t slot_k0(const SlotGroup* groups, int s) { return groups[s >> 2].k0[s & 3]; }
+__device__ __forceinline__ uint64_t slot_k1(const SlotGroup* groups, int s) { return groups[s >> 2].k1[s & 3]; }
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 

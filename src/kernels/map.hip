@@ -34,18 +34,18 @@ constexpr int MAP_SPT = MAP_SLOTS / MAP_THREADS;  // table slots per thread in a
 static_assert(MAP_SLOTS % MAP_THREADS == 0, "flush assumes whole slots per thread");
 
 struct MapLds {
-  uint32_t tags[MAP_SLOTS];  // first: 16-B aligned for the ds_read_b128 group reads
-  uint64_t k0[MAP_SLOTS];
-  uint64_t k1[MAP_SLOTS];
+  SlotGroup grp[MAP_GROUPS];  // first: 16-B aligned for the ds_read_b128 group reads
   uint32_t cnt[MAP_SLOTS];
   uint32_t off[MAP_SLOTS];
   uint32_t boff[MAX_REC_BUCKETS + 4];  // bucket counts -> exclusive offsets (+ total)
   uint8_t tile[MAP_TILE + MAP_HALO + 16];  // +16: tile8() reads one word past
+  uint32_t fail[MAP_THREADS];  // per owner lane: token starts to retry after a flush
   uint32_t wsum[MAP_THREADS / 64];
   uint32_t occupied;
   uint32_t prev;
   uint32_t flush_ok;
   uint32_t nflush;  // directory entries written by this block
+  uint64_t used;    // records written into this block's region
   uint64_t flush_base;
   unsigned long long tokens;
 };
@@ -65,6 +65,21 @@ __device__ __forceinline__ uint64_t tile8(const uint8_t* tile, uint32_t p) {
   const uint32_t sh = (p & 7) * 8;
   const uint64_t lo = q[0], hi = q[1];
   return sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
+}
+
+// Position of the k-th (0-based) set bit of m (k < popcount(m)).
+__device__ __forceinline__ uint32_t nth_set_bit(uint32_t m, uint32_t k) {
+  uint32_t b = 0;
+#pragma unroll
+  for (int s = 16; s > 0; s >>= 1) {
+    const uint32_t c = __popc(m & ((1u << s) - 1u));
+    if (k >= c) {
+      k -= c;
+      m >>= s;
+      b += s;
+    }
+  }
+  return b;
 }
 
 __device__ __forceinline__ uint64_t low_bytes(uint64_t v, uint32_t n) {
@@ -109,6 +124,13 @@ __device__ void block_exclusive_scan(uint32_t* a, uint32_t n, uint32_t* wsum) {
 __device__ void flush_table(MapLds& L, const MapArgs& a) {
   const int tid = threadIdx.x;
   const uint32_t nb = 1u << a.log2_rec_buckets;
+  if (a.ablate == 5) {  // profiling: clear only
+    for (int s = tid; s < MAP_SLOTS; s += MAP_THREADS) L.grp[s >> 2].tag[s & 3] = TAG_EMPTY;
+    __syncthreads();
+    if (tid == 0) L.occupied = 0;
+    __syncthreads();
+    return;
+  }
   for (uint32_t b = tid; b <= nb; b += MAP_THREADS) L.boff[b] = 0;
   __syncthreads();
   uint32_t sb[MAP_SPT], sr[MAP_SPT];
@@ -116,8 +138,9 @@ __device__ void flush_table(MapLds& L, const MapArgs& a) {
   for (int j = 0; j < MAP_SPT; ++j) {
     const int s = tid + j * MAP_THREADS;
     sb[j] = 0xFFFFFFFFu;
-    if (L.tags[s] > TAG_PENDING) {
-      sb[j] = bucket_of(place_hash(L.k0[s], L.k1[s]), a.log2_rec_buckets);
+    const uint32_t tag = slot_tag(L.grp, s);
+    if (tag > TAG_PENDING) {
+      sb[j] = (tag >> 2) & (nb - 1u);  // == bucket_of(place_hash): bucket bits live in the tag
       sr[j] = atomicAdd(&L.boff[sb[j]], 1u);
     }
   }
@@ -127,9 +150,12 @@ __device__ void flush_table(MapLds& L, const MapArgs& a) {
   if (tid == 0) {
     uint32_t ok = 0;
     if (n) {
-      const uint64_t base = atomicAdd(a.rec.cursor, (unsigned long long)n);
+      // block-private record region: no global cursor contention
+      const uint64_t region = a.rec.cap / gridDim.x;
+      const uint64_t base = (uint64_t)blockIdx.x * region + L.used;
       const uint32_t j = L.nflush;
-      ok = (base + n <= a.rec.cap && j < a.rec.dir_per_block) ? 1u : 0u;
+      ok = (L.used + n <= region && j < a.rec.dir_per_block) ? 1u : 0u;
+      L.used += n;
       if (ok) {
         L.nflush = j + 1;
         a.rec.dir_base[(size_t)blockIdx.x * a.rec.dir_per_block + j] = base;
@@ -144,16 +170,17 @@ __device__ void flush_table(MapLds& L, const MapArgs& a) {
   if (L.flush_ok) {
     const uint32_t j = L.nflush - 1;
     const size_t row = (size_t)gridDim.x * a.rec.dir_per_block;
-    for (uint32_t b = tid; b <= nb; b += MAP_THREADS)
-      a.rec.dir_off[b * row + (size_t)blockIdx.x * a.rec.dir_per_block + j] = L.boff[b];
+    if (a.ablate != 3)
+      for (uint32_t b = tid; b <= nb; b += MAP_THREADS)
+        a.rec.dir_off[b * row + (size_t)blockIdx.x * a.rec.dir_per_block + j] = L.boff[b];
     const uint64_t base = L.flush_base;
 #pragma unroll
     for (int k = 0; k < MAP_SPT; ++k) {
       if (sb[k] == 0xFFFFFFFFu) continue;
       const int s = tid + k * MAP_THREADS;
       Rec r;
-      r.k0 = L.k0[s];
-      r.k1 = L.k1[s];
+      r.k0 = slot_k0(L.grp, s);
+      r.k1 = slot_k1(L.grp, s);
       r.co = ((uint64_t)L.cnt[s] << 32) | L.off[s];
       a.rec.recs[base + L.boff[sb[k]] + sr[k]] = r;
     }
@@ -161,7 +188,7 @@ __device__ void flush_table(MapLds& L, const MapArgs& a) {
 #pragma unroll
   for (int k = 0; k < MAP_SPT; ++k) {
     const int s = tid + k * MAP_THREADS;
-    L.tags[s] = TAG_EMPTY;
+    L.grp[s >> 2].tag[s & 3] = TAG_EMPTY;
     L.cnt[s] = 0;
     L.off[s] = 0xFFFFFFFFu;
   }
@@ -200,14 +227,16 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_map_tokenize(MapArgs a) {
   __shared__ MapLds L;
   const int tid = threadIdx.x;
   for (int s = tid; s < MAP_SLOTS; s += MAP_THREADS) {
-    L.tags[s] = TAG_EMPTY;
+    L.grp[s >> 2].tag[s & 3] = TAG_EMPTY;
     L.cnt[s] = 0;
     L.off[s] = 0xFFFFFFFFu;
   }
+  L.fail[tid] = 0;
   if (tid == 0) {
     L.occupied = 0;
     L.tokens = 0;
     L.nflush = 0;
+    L.used = 0;
   }
 
   const uint64_t ntiles = (a.chunk_len + MAP_TILE - 1) / MAP_TILE;
@@ -268,17 +297,35 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_map_tokenize(MapArgs a) {
       continue;
     }
 
+    // ---- tokens: redistributed so every lane of the wave takes one per round ----
+    // Lanes own 0..~10 token starts; a wave prefix sum over their counts
+    // numbers the wave's tokens, and lane L of round r handles token r*64+L
+    // (owner lane by binary search over the prefix, bit by k-th-set-bit).
+    const int lane = tid & 63, wbase = tid & ~63;
     uint32_t todo = starts;
     for (;;) {
-      uint32_t failed = 0;
-      while (todo) {
-        const uint32_t i = __ffs(todo) - 1;
-        todo &= todo - 1;
-        const uint64_t rest = dm >> i;
+      const uint32_t cnt = __popc(todo);
+      uint32_t incl = cnt;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+      }
+      const uint32_t total = __shfl(incl, 63), excl = incl - cnt;
+      for (uint32_t r = 0; r < total; r += 64) {
+        const uint32_t q = r + lane;
+        int o = 0;  // owner: last lane whose exclusive prefix is <= q
+        for (int step = 32; step > 0; step >>= 1)
+          if (__shfl(excl, o + step) <= q) o += step;
+        const uint32_t k = q - __shfl(excl, o);
+        const uint32_t om = __shfl(todo, o);
+        const uint64_t odm = ((uint64_t)__shfl((uint32_t)(dm >> 32), o) << 32) | __shfl((uint32_t)dm, o);
+        if (q >= total) continue;
+        const uint32_t bit = nth_set_bit(om, k);
+        const uint32_t p = (uint32_t)(wbase + o) * MAP_BPL + bit;  // tile position of the token
+        const uint64_t rest = odm >> bit;
         uint64_t k0, k1;
         if (rest != 0) {
           const uint32_t len = (uint32_t)__ffsll((unsigned long long)rest) - 1;  // ends inside the window
-          const uint32_t p = tid * MAP_BPL + i;
           k0 = low_bytes(tile8(L.tile, p), len);
           if (len <= 8) {
             k1 = len;
@@ -288,26 +335,30 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_map_tokenize(MapArgs a) {
             k1 = make_k1(len, h);
           }
         } else {
-          key_slow(L, a, (uint64_t)tid * MAP_BPL + i, lane_base + i, k0, k1);
+          key_slow(L, a, p, t0 + p, k0, k1);
         }
-        const uint32_t off = (uint32_t)(lane_base + i);
+        const uint32_t off = (uint32_t)(t0 + p);
         const uint64_t ph = place_hash(k0, k1);
         if (a.ablate == 1) {
           sink ^= ph + off;
           continue;
         }
         bool claimed;
-        const int s = lds_find_or_claim(L.tags, L.k0, L.k1, MAP_GROUPS, ph, k0, k1, MAP_MAX_GROUP_PROBES, claimed);
+        const int s = lds_find_or_claim(L.grp, MAP_GROUPS, ph, k0, k1, MAP_MAX_GROUP_PROBES, claimed);
         if (s < 0) {
-          failed |= 1u << i;  // neighbourhood full: flush, then retry
+          atomicOr(&L.fail[wbase + o], 1u << bit);  // neighbourhood full: flush, then retry
           continue;
         }
-        atomicAdd(&L.cnt[s], 1u);
-        atomicMin(&L.off[s], off);
+        if (a.ablate != 6) {
+          atomicAdd(&L.cnt[s], 1u);
+          atomicMin(&L.off[s], off);
+        }
         if (claimed) atomicAdd(&L.occupied, 1u);
       }
-      todo = failed;
+      __syncthreads();
+      todo = L.fail[tid];
       if (!__syncthreads_or(todo != 0)) break;
+      L.fail[tid] = 0;
       flush_table(L, a);
     }
   }
@@ -322,6 +373,7 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_map_tokenize(MapArgs a) {
   __syncthreads();
   if (tid == 0) {
     atomicAdd(a.tokens, L.tokens);
+    atomicAdd(a.rec.cursor, (unsigned long long)L.used);  // stats: records after the combiner
     a.rec.dir_count[blockIdx.x] = L.nflush;
   }
 }

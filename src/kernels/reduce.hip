@@ -22,10 +22,10 @@
 namespace wc {
 namespace dev {
 
+constexpr int RED_UNROLL = 4;
+
 struct RedLds {
-  uint32_t tags[TAB_SLOTS];  // first: 16-B aligned group reads
-  uint64_t k0[TAB_SLOTS];
-  uint64_t k1[TAB_SLOTS];
+  SlotGroup grp[TAB_GROUPS];  // first: 16-B aligned group reads
   uint64_t cnt[TAB_SLOTS];
   uint64_t first[TAB_SLOTS];
   uint32_t occupied;
@@ -36,20 +36,21 @@ __device__ __forceinline__ void load_slice(RedLds& L, const TableView& t, uint32
   const size_t base = (size_t)b * TAB_SLOTS;
   for (int s = threadIdx.x; s < TAB_SLOTS; s += blockDim.x) {
     const uint64_t k0 = t.k0[base + s], k1 = t.k1[base + s];
-    L.k0[s] = k0;
-    L.k1[s] = k1;
+    SlotGroup& G = L.grp[s >> 2];
+    G.k0[s & 3] = k0;
+    G.k1[s & 3] = k1;
+    G.tag[s & 3] = k1 == K1_EMPTY ? TAG_EMPTY : make_tag(place_hash(k0, k1));
     L.cnt[s] = t.cnt[base + s];
     L.first[s] = t.first[base + s];
-    L.tags[s] = k1 == K1_EMPTY ? TAG_EMPTY : make_tag(place_hash(k0, k1));
   }
 }
 
 __device__ __forceinline__ void store_slice(const RedLds& L, const TableView& t, uint32_t b) {
   const size_t base = (size_t)b * TAB_SLOTS;
   for (int s = threadIdx.x; s < TAB_SLOTS; s += blockDim.x) {
-    const bool occ = L.tags[s] > TAG_PENDING;
-    t.k0[base + s] = L.k0[s];
-    t.k1[base + s] = occ ? L.k1[s] : K1_EMPTY;
+    const bool occ = slot_tag(L.grp, s) > TAG_PENDING;
+    t.k0[base + s] = slot_k0(L.grp, s);
+    t.k1[base + s] = occ ? slot_k1(L.grp, s) : K1_EMPTY;
     t.cnt[base + s] = L.cnt[s];
     t.first[base + s] = L.first[s];
   }
@@ -75,7 +76,7 @@ __device__ __forceinline__ void merge_record(RedLds& L, const ReduceArgs& a, uin
   const uint64_t ph = place_hash(r.k0, r.k1);
   if (shift && bucket_of(ph, a.tab.log2_buckets) != b) return;
   bool claimed;
-  const int s = lds_find_or_claim(L.tags, L.k0, L.k1, TAB_GROUPS, ph, r.k0, r.k1, TAB_MAX_GROUP_PROBES, claimed);
+  const int s = lds_find_or_claim(L.grp, TAB_GROUPS, ph, r.k0, r.k1, TAB_MAX_GROUP_PROBES, claimed);
   if (s < 0) {
     L.overflow = 1;
     return;
@@ -102,8 +103,8 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   }
   __syncthreads();
 
-  const uint32_t shift = a.tab.log2_buckets - a.log2_rec_buckets;  // table buckets per record bucket
-  const uint32_t rb = b >> shift;
+  const uint32_t shift = a.tab.log2_buckets - a.log2_rec_buckets;  // table buckets per record bucket (log2)
+  const uint32_t rb = b & ((1u << a.log2_rec_buckets) - 1u);       // buckets nest on the low bits
   const uint32_t J = a.rec.dir_per_block;
   const size_t row = (size_t)a.map_blocks * J;
   const uint32_t* lo_row = a.rec.dir_off + (size_t)rb * row;
@@ -129,17 +130,21 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
       }
       const uint32_t total = __shfl(incl, 63);
       const uint32_t excl = incl - len;
-      for (uint32_t k = 0; k < total; k += 64) {
-        const uint32_t q = k + lane;
-        // owner lane: the last lane whose exclusive prefix is <= q
-        int o = 0;
-        for (int step = 32; step > 0; step >>= 1) {
-          const uint32_t e = __shfl(excl, o + step);
-          if (o + step < 64 && e <= q) o += step;
+      // RED_UNROLL x 64 records in flight per wave before any is merged
+      for (uint32_t k = 0; k < total; k += RED_UNROLL * 64) {
+        Rec rr[RED_UNROLL];
+#pragma unroll
+        for (int u = 0; u < RED_UNROLL; ++u) {
+          const uint32_t q = min(k + u * 64 + lane, total - 1);  // clamp: always a valid record
+          int o = 0;  // owner lane: the last lane whose exclusive prefix is <= q
+          for (int step = 32; step > 0; step >>= 1)
+            if (__shfl(excl, o + step) <= q) o += step;
+          const uint64_t ostart = ((uint64_t)__shfl((uint32_t)(start >> 32), o) << 32) | __shfl((uint32_t)start, o);
+          rr[u] = a.rec.recs[ostart + (q - __shfl(excl, o))];
         }
-        const uint64_t ostart = __shfl(start, o);
-        const uint32_t oexcl = __shfl(excl, o);
-        if (q < total) merge_record(L, a, b, a.rec.recs[ostart + (q - oexcl)], shift);
+#pragma unroll
+        for (int u = 0; u < RED_UNROLL; ++u)
+          if (k + u * 64 + lane < total) merge_record(L, a, b, rr[u], shift);
       }
     }
   }
@@ -158,12 +163,12 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   }
 }
 
-// Rehash slice (new_b >> 1) of `src` into slice new_b of `dst` (2x buckets).
+// Rehash parent slice (new_b mod B) of `src` into slice new_b of `dst` (2B buckets).
 __global__ void __launch_bounds__(RED_THREADS) wc_table_split(TableView src, TableView dst) {
   __shared__ RedLds L;
-  const uint32_t nb = blockIdx.x, ob = nb >> 1;
+  const uint32_t nb = blockIdx.x, ob = nb & ((1u << src.log2_buckets) - 1u);
   for (int s = threadIdx.x; s < TAB_SLOTS; s += blockDim.x) {
-    L.tags[s] = TAG_EMPTY;
+    L.grp[s >> 2].tag[s & 3] = TAG_EMPTY;
     L.cnt[s] = 0;
     L.first[s] = ~0ull;
   }
@@ -177,7 +182,7 @@ __global__ void __launch_bounds__(RED_THREADS) wc_table_split(TableView src, Tab
     const uint64_t ph = place_hash(k0, k1);
     if (bucket_of(ph, dst.log2_buckets) != nb) continue;
     bool claimed;
-    const int d = lds_find_or_claim(L.tags, L.k0, L.k1, TAB_GROUPS, ph, k0, k1, TAB_GROUPS, claimed);
+    const int d = lds_find_or_claim(L.grp, TAB_GROUPS, ph, k0, k1, TAB_GROUPS, claimed);
     // d >= 0 always: a child receives at most the parent's occupancy.
     L.cnt[d] = src.cnt[obase + s];
     L.first[d] = src.first[obase + s];
