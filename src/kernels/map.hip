@@ -39,7 +39,6 @@ struct MapLds {
   uint32_t off[MAP_SLOTS];
   uint32_t boff[MAX_REC_BUCKETS + 4];  // bucket counts -> exclusive offsets (+ total)
   uint8_t tile[MAP_TILE + MAP_HALO + 16];  // +16: tile8() reads one word past
-  uint32_t fail[MAP_THREADS];  // per owner lane: token starts to retry after a flush
   uint32_t wsum[MAP_THREADS / 64];
   uint32_t occupied;
   uint32_t prev;
@@ -65,21 +64,6 @@ __device__ __forceinline__ uint64_t tile8(const uint8_t* tile, uint32_t p) {
   const uint32_t sh = (p & 7) * 8;
   const uint64_t lo = q[0], hi = q[1];
   return sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
-}
-
-// Position of the k-th (0-based) set bit of m (k < popcount(m)).
-__device__ __forceinline__ uint32_t nth_set_bit(uint32_t m, uint32_t k) {
-  uint32_t b = 0;
-#pragma unroll
-  for (int s = 16; s > 0; s >>= 1) {
-    const uint32_t c = __popc(m & ((1u << s) - 1u));
-    if (k >= c) {
-      k -= c;
-      m >>= s;
-      b += s;
-    }
-  }
-  return b;
 }
 
 __device__ __forceinline__ uint64_t low_bytes(uint64_t v, uint32_t n) {
@@ -125,7 +109,10 @@ __device__ void flush_table(MapLds& L, const MapArgs& a) {
   const int tid = threadIdx.x;
   const uint32_t nb = 1u << a.log2_rec_buckets;
   if (a.ablate == 5) {  // profiling: clear only
-    for (int s = tid; s < MAP_SLOTS; s += MAP_THREADS) L.grp[s >> 2].tag[s & 3] = TAG_EMPTY;
+    for (int s = tid; s < MAP_SLOTS; s += MAP_THREADS) {
+      L.grp[s >> 2].tag[s & 3] = TAG_EMPTY;
+      L.grp[s >> 2].k1[s & 3] = K1_EMPTY;
+    }
     __syncthreads();
     if (tid == 0) L.occupied = 0;
     __syncthreads();
@@ -189,6 +176,7 @@ __device__ void flush_table(MapLds& L, const MapArgs& a) {
   for (int k = 0; k < MAP_SPT; ++k) {
     const int s = tid + k * MAP_THREADS;
     L.grp[s >> 2].tag[s & 3] = TAG_EMPTY;
+    L.grp[s >> 2].k1[s & 3] = K1_EMPTY;
     L.cnt[s] = 0;
     L.off[s] = 0xFFFFFFFFu;
   }
@@ -223,15 +211,129 @@ __device__ __forceinline__ void key_slow(const MapLds& L, const MapArgs& a, uint
   k1 = make_k1(len, h);
 }
 
-__global__ void __launch_bounds__(MAP_THREADS) wc_map_tokenize(MapArgs a) {
+// Key of the token starting at tile position p, given the lane's 64-bit
+// delimiter window mask `rest` shifted to the token start.
+struct TokKey {
+  uint64_t k0, k1, ph;
+  uint32_t off;
+};
+
+__device__ __forceinline__ TokKey token_key(const MapLds& L, const MapArgs& a, uint64_t t0, uint32_t p,
+                                            uint64_t rest) {
+  TokKey t;
+  if (rest != 0) {
+    const uint32_t len = (uint32_t)__ffsll((unsigned long long)rest) - 1;  // ends inside the window
+    t.k0 = low_bytes(tile8(L.tile, p), len);
+    if (len <= 8) {
+      t.k1 = len;
+    } else {
+      uint64_t h = FNV_OFFSET;
+      for (uint32_t c = 8; c < len; c += 8) h = tail_fold(h, low_bytes(tile8(L.tile, p + c), len - c));
+      t.k1 = make_k1(len, h);
+    }
+  } else {
+    key_slow(L, a, p, t0 + p, t.k0, t.k1);
+  }
+  t.off = (uint32_t)(t0 + p);
+  t.ph = place_hash(t.k0, t.k1);
+  return t;
+}
+
+// Combiner insert.  The map's table may hold the same key in two slots (each
+// becomes a record and the reducer sums them), so a claim is ONE CAS from
+// EMPTY straight to the final tag; the claimer then writes k0/k1.  A reader
+// that sees the tag before the keys simply does not match (k1 was cleared to
+// 0 at the last flush, so stale keys never match) and probes on — at worst it
+// claims a duplicate slot.  Returns the slot, or -1 if `max_groups` groups
+// were full.
+__device__ __forceinline__ int combiner_slot(SlotGroup* groups, const TokKey& t) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+  const uint32_t tag = make_tag(t.ph);
+  uint32_t g = group_of(t.ph, MAP_GROUPS);
+  for (int steps = 0; steps < MAP_MAX_GROUP_PROBES;) {
+    asm volatile("" ::: "memory");
+    SlotGroup& G = groups[g];
+    const u32x4 tg = *reinterpret_cast<const u32x4*>(G.tag);
+    const u64x2 a1 = *reinterpret_cast<const u64x2*>(&G.k1[0]);
+    const u64x2 b1 = *reinterpret_cast<const u64x2*>(&G.k1[2]);
+    const u64x2 a0 = *reinterpret_cast<const u64x2*>(&G.k0[0]);
+    const u64x2 b0 = *reinterpret_cast<const u64x2*>(&G.k0[2]);
+    const bool h0 = tg.x == tag && a1.x == t.k1 && a0.x == t.k0;
+    const bool h1 = tg.y == tag && a1.y == t.k1 && a0.y == t.k0;
+    const bool h2 = tg.z == tag && b1.x == t.k1 && b0.x == t.k0;
+    const bool h3 = tg.w == tag && b1.y == t.k1 && b0.y == t.k0;
+    if (h0 | h1 | h2 | h3) return 4 * (int)g + (h0 ? 0 : (h1 ? 1 : (h2 ? 2 : 3)));
+    const int e = tg.x == TAG_EMPTY ? 0 : (tg.y == TAG_EMPTY ? 1 : (tg.z == TAG_EMPTY ? 2 : (tg.w == TAG_EMPTY ? 3 : -1)));
+    if (e < 0) {
+      ++steps;
+      g = (g + 1) & (MAP_GROUPS - 1);
+      continue;
+    }
+    if (atomicCAS(&G.tag[e], TAG_EMPTY, tag) == TAG_EMPTY) {
+      G.k0[e] = t.k0;
+      G.k1[e] = t.k1;
+      return 4 * (int)g + e;
+    }
+    // lost the slot to another lane: re-read this group
+  }
+  return -1;
+}
+
+// Count token t into the combiner; returns false if its neighbourhood is full.
+__device__ __forceinline__ bool combine(MapLds& L, const TokKey& t) {
+  const int s = combiner_slot(L.grp, t);
+  if (s < 0) return false;
+  const uint32_t c = atomicAdd(&L.cnt[s], 1u);
+  atomicMin(&L.off[s], t.off);
+  if (c == 0) atomicAdd(&L.occupied, 1u);
+  return true;
+}
+
+// 32 text bytes at global offset g as two 16-B vectors (' ' past avail).
+__device__ __forceinline__ void load32(const MapArgs& a, uint64_t g, uint4& v0, uint4& v1) {
+  if (g + MAP_BPL <= a.avail_len) {
+    const uint4* src = reinterpret_cast<const uint4*>(a.text + g);
+    v0 = src[0];
+    v1 = src[1];
+  } else {
+    uint32_t w[8];
+    for (int k = 0; k < 8; ++k) {
+      uint32_t x = 0;
+      for (int b = 0; b < 4; ++b) {
+        const uint64_t i = g + 4 * k + b;
+        x |= (uint32_t)(i < a.avail_len ? a.text[i] : 0x20) << (8 * b);
+      }
+      w[k] = x;
+    }
+    v0 = make_uint4(w[0], w[1], w[2], w[3]);
+    v1 = make_uint4(w[4], w[5], w[6], w[7]);
+  }
+}
+
+__device__ __forceinline__ uint4 load16(const MapArgs& a, uint64_t g) {
+  if (g + 16 <= a.avail_len) return *reinterpret_cast<const uint4*>(a.text + g);
+  uint32_t w[4];
+  for (int k = 0; k < 4; ++k) {
+    uint32_t x = 0;
+    for (int b = 0; b < 4; ++b) {
+      const uint64_t i = g + 4 * k + b;
+      x |= (uint32_t)(i < a.avail_len ? a.text[i] : 0x20) << (8 * b);
+    }
+    w[k] = x;
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  // 2 blocks / CU
   __shared__ MapLds L;
   const int tid = threadIdx.x;
   for (int s = tid; s < MAP_SLOTS; s += MAP_THREADS) {
     L.grp[s >> 2].tag[s & 3] = TAG_EMPTY;
+    L.grp[s >> 2].k1[s & 3] = K1_EMPTY;
     L.cnt[s] = 0;
     L.off[s] = 0xFFFFFFFFu;
   }
-  L.fail[tid] = 0;
   if (tid == 0) {
     L.occupied = 0;
     L.tokens = 0;
@@ -243,46 +345,39 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_map_tokenize(MapArgs a) {
   uint32_t my_tokens = 0;
   uint64_t sink = 0;  // keeps ablated work alive
 
+  // Software pipeline: the next tile's 32 B per lane (+ halo) are loaded into
+  // registers while the current tile is being tokenized.
+  uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0, ph16 = p0;
+  uint32_t pprev = 0x20;
+  auto prefetch = [&](uint64_t tile) {
+    if (tile >= ntiles) return;
+    const uint64_t t0 = tile * MAP_TILE;
+    load32(a, t0 + (uint64_t)tid * MAP_BPL, p0, p1);
+    if (tid < MAP_HALO / 16) ph16 = load16(a, t0 + MAP_TILE + (uint64_t)tid * 16);
+    if (tid == 0) pprev = (t0 == 0 && a.prev_byte >= 0) ? (uint32_t)a.prev_byte : a.text[(int64_t)t0 - 1];
+  };
+  prefetch(blockIdx.x);
+
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const uint64_t t0 = tile * MAP_TILE;
     __syncthreads();  // previous tile fully consumed
     if (L.occupied > MAP_FLUSH_AT) flush_table(L, a);
-    // ---- stage tile + halo into LDS (16-B loads; ' ' past avail_len) ----
-    {
-      const uint64_t g = t0 + (uint64_t)tid * MAP_BPL;
-      uint4* dst = reinterpret_cast<uint4*>(&L.tile[tid * MAP_BPL]);
-      if (g + MAP_BPL <= a.avail_len) {
-        const uint4* src = reinterpret_cast<const uint4*>(a.text + g);
-        const uint4 v0 = src[0], v1 = src[1];
-        dst[0] = v0;
-        dst[1] = v1;
-      } else {
-        for (int i = 0; i < MAP_BPL; ++i) L.tile[tid * MAP_BPL + i] = (g + i < a.avail_len) ? a.text[g + i] : 0x20;
-      }
-      if (tid < MAP_HALO / 16) {
-        const uint64_t h = t0 + MAP_TILE + (uint64_t)tid * 16;
-        uint4* hd = reinterpret_cast<uint4*>(&L.tile[MAP_TILE + tid * 16]);
-        if (h + 16 <= a.avail_len) {
-          *hd = *reinterpret_cast<const uint4*>(a.text + h);
-        } else {
-          for (int i = 0; i < 16; ++i) L.tile[MAP_TILE + tid * 16 + i] = (h + i < a.avail_len) ? a.text[h + i] : 0x20;
-        }
-      }
-      if (tid == 0) L.prev = (t0 == 0 && a.prev_byte >= 0) ? (uint32_t)a.prev_byte : a.text[(int64_t)t0 - 1];
-    }
+    // ---- commit the prefetched tile to LDS, start loading the next ----
+    reinterpret_cast<uint4*>(&L.tile[tid * MAP_BPL])[0] = p0;
+    reinterpret_cast<uint4*>(&L.tile[tid * MAP_BPL])[1] = p1;
+    if (tid < MAP_HALO / 16) *reinterpret_cast<uint4*>(&L.tile[MAP_TILE + tid * 16]) = ph16;
+    if (tid == 0) L.prev = pprev;
     __syncthreads();
+    prefetch(tile + gridDim.x);
 
-    // ---- 64-byte register window, delimiter / start masks ----
-    uint64_t w[8];
+    // ---- 64-byte window (own 32 B + next lane's), delimiter / start masks ----
+    uint64_t dm = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint4 v = reinterpret_cast<const uint4*>(&L.tile[tid * MAP_BPL])[j];
-      w[2 * j] = (uint64_t)v.x | ((uint64_t)v.y << 32);
-      w[2 * j + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
+      dm |= delim_mask8((uint64_t)v.x | ((uint64_t)v.y << 32)) << (16 * j);
+      dm |= delim_mask8((uint64_t)v.z | ((uint64_t)v.w << 32)) << (16 * j + 8);
     }
-    uint64_t dm = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dm |= delim_mask8(w[j]) << (8 * j);
     const uint32_t prevb = (tid == 0) ? L.prev : L.tile[tid * MAP_BPL - 1];
     uint32_t starts = (uint32_t)(~dm & ((dm << 1) | (is_delim(prevb) ? 1ull : 0ull)));
     const uint64_t lane_base = t0 + (uint64_t)tid * MAP_BPL;
@@ -297,69 +392,29 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_map_tokenize(MapArgs a) {
       continue;
     }
 
-    // ---- tokens: redistributed so every lane of the wave takes one per round ----
-    // Lanes own 0..~10 token starts; a wave prefix sum over their counts
-    // numbers the wave's tokens, and lane L of round r handles token r*64+L
-    // (owner lane by binary search over the prefix, bit by k-th-set-bit).
-    const int lane = tid & 63, wbase = tid & ~63;
+    // ---- tokens: two per iteration so their LDS round trips overlap ----
+    const uint32_t pbase = tid * MAP_BPL;
     uint32_t todo = starts;
     for (;;) {
-      const uint32_t cnt = __popc(todo);
-      uint32_t incl = cnt;
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-      }
-      const uint32_t total = __shfl(incl, 63), excl = incl - cnt;
-      for (uint32_t r = 0; r < total; r += 64) {
-        const uint32_t q = r + lane;
-        int o = 0;  // owner: last lane whose exclusive prefix is <= q
-        for (int step = 32; step > 0; step >>= 1)
-          if (__shfl(excl, o + step) <= q) o += step;
-        const uint32_t k = q - __shfl(excl, o);
-        const uint32_t om = __shfl(todo, o);
-        const uint64_t odm = ((uint64_t)__shfl((uint32_t)(dm >> 32), o) << 32) | __shfl((uint32_t)dm, o);
-        if (q >= total) continue;
-        const uint32_t bit = nth_set_bit(om, k);
-        const uint32_t p = (uint32_t)(wbase + o) * MAP_BPL + bit;  // tile position of the token
-        const uint64_t rest = odm >> bit;
-        uint64_t k0, k1;
-        if (rest != 0) {
-          const uint32_t len = (uint32_t)__ffsll((unsigned long long)rest) - 1;  // ends inside the window
-          k0 = low_bytes(tile8(L.tile, p), len);
-          if (len <= 8) {
-            k1 = len;
-          } else {
-            uint64_t h = FNV_OFFSET;
-            for (uint32_t c = 8; c < len; c += 8) h = tail_fold(h, low_bytes(tile8(L.tile, p + c), len - c));
-            k1 = make_k1(len, h);
-          }
-        } else {
-          key_slow(L, a, p, t0 + p, k0, k1);
-        }
-        const uint32_t off = (uint32_t)(t0 + p);
-        const uint64_t ph = place_hash(k0, k1);
+      uint32_t failed = 0;
+      while (todo) {
+        const uint32_t i1 = __ffs(todo) - 1;
+        todo &= todo - 1;
+        const bool two = todo != 0;
+        const uint32_t i2 = two ? (uint32_t)__ffs(todo) - 1 : i1;
+        todo &= two ? todo - 1 : todo;
+        const TokKey ta = token_key(L, a, t0, pbase + i1, dm >> i1);
+        const TokKey tb = token_key(L, a, t0, pbase + i2, dm >> i2);
         if (a.ablate == 1) {
-          sink ^= ph + off;
+          sink ^= ta.ph + tb.ph;
           continue;
         }
-        bool claimed;
-        const int s = lds_find_or_claim(L.grp, MAP_GROUPS, ph, k0, k1, MAP_MAX_GROUP_PROBES, claimed);
-        if (s < 0) {
-          atomicOr(&L.fail[wbase + o], 1u << bit);  // neighbourhood full: flush, then retry
-          continue;
-        }
-        if (a.ablate != 6) {
-          atomicAdd(&L.cnt[s], 1u);
-          atomicMin(&L.off[s], off);
-        }
-        if (claimed) atomicAdd(&L.occupied, 1u);
+        if (!combine(L, ta)) failed |= 1u << i1;
+        if (two && !combine(L, tb)) failed |= 1u << i2;
       }
-      __syncthreads();
-      todo = L.fail[tid];
+      todo = failed;
       if (!__syncthreads_or(todo != 0)) break;
-      L.fail[tid] = 0;
-      flush_table(L, a);
+      flush_table(L, a);  // neighbourhood full: flush, then retry those tokens
     }
   }
   __syncthreads();
