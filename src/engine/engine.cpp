@@ -70,7 +70,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   // flush directory: at most one flush per tile (+ retries, + the final one)
   dir_per_block_max = dir_per_block_for(opt.chunk_bytes, map_blocks);
   const size_t dir_cols = (size_t)map_blocks * dir_per_block_max;
-  const size_t nrb1 = ((size_t)1 << opt.log2_rec_buckets) + 1;
+  const size_t nrb1 = (size_t)MAX_REC_BUCKETS + 1;  // partitions follow the table up to the max
   rec_mem.reserve(rec_total * sizeof(Rec) + dir_cols * (8 + 4 * nrb1) + map_blocks * 4 + 8192);
   rec.recs = rec_mem.take_n<Rec>(rec_total);
   rec.cap = rec_total;
@@ -111,6 +111,7 @@ Engine::Impl::~Impl() {
   if (d_bucket_en) (void)hipFree(d_bucket_en);
   if (d_arena) (void)hipFree(d_arena);
   if (d_arena_cursor) (void)hipFree(d_arena_cursor);
+  if (d_newkeys) (void)hipFree(d_newkeys);
   if (s) (void)hipStreamDestroy(s);
   if (copy_s) (void)hipStreamDestroy(copy_s);
 }
@@ -150,9 +151,20 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   launch_map(m, blocks, s);
   ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                 avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
-                d_ctr->flags, d_bucket_ovf, nullptr};
+                d_ctr->flags, d_bucket_ovf, nullptr, newkeys()};
   if (!ablate_map) launch_reduce(ra, s);  // ablated map output is not a valid shuffle
   WC_HIP_CHECK(hipMemcpyAsync(h_ctr, d_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));
+}
+
+uint64_t* Engine::Impl::newkeys() {
+  const size_t nb = (size_t)1 << table().log2_buckets;
+  if (nb > newkeys_buckets) {
+    if (d_newkeys) WC_HIP_CHECK(hipFree(d_newkeys));
+    d_newkeys = nullptr;
+    WC_HIP_CHECK(hipMalloc(&d_newkeys, nb * NEWKEY_CAP * sizeof(uint64_t)));
+    newkeys_buckets = nb;
+  }
+  return d_newkeys;
 }
 
 void Engine::Impl::split_table() {
@@ -208,7 +220,7 @@ void Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
     WC_HIP_CHECK(hipMemsetAsync(d_ctr, 0, sizeof(DevCounters), s));
     ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                   avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
-                  d_ctr->flags, d_bucket_ovf, d_bucket_en};
+                  d_ctr->flags, d_bucket_ovf, d_bucket_en, newkeys()};
     launch_reduce(ra, s);
     WC_HIP_CHECK(hipMemcpyAsync(h_ctr, d_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));
     WC_HIP_CHECK(hipStreamSynchronize(s));
@@ -225,8 +237,9 @@ void Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
 
 void Engine::Impl::process_chunk(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev) {
   const uint32_t blocks = blocks_for(len);
-  launch_pass(text, len, avail, base, prev, opt.log2_rec_buckets, blocks);
-  complete_pass(text, len, avail, base, prev, opt.log2_rec_buckets, blocks);
+  const uint32_t rb = rec_buckets_log2();
+  launch_pass(text, len, avail, base, prev, rb, blocks);
+  complete_pass(text, len, avail, base, prev, rb, blocks);
 }
 
 void Engine::Impl::compact_local() {
@@ -422,10 +435,11 @@ void Engine::count_source(ChunkSource& src, uint64_t global_base) {
     const uint8_t* d = im.d_stage[k & 1];
     WC_HIP_CHECK(hipStreamWaitEvent(im.s, im.ev_h2d[k & 1], 0));
     const uint32_t blocks = im.blocks_for(len);
-    im.launch_pass(d, len, len, offset, ' ', im.opt.log2_rec_buckets, blocks);
+    const uint32_t rb = im.rec_buckets_log2();
+    im.launch_pass(d, len, len, offset, ' ', rb, blocks);
     const uint64_t next = fill(k + 1);  // host reads the next chunk while the GPU works
     if (next) issue(k + 1, next);
-    im.complete_pass(d, len, len, offset, ' ', im.opt.log2_rec_buckets, blocks);
+    im.complete_pass(d, len, len, offset, ' ', rb, blocks);
     WC_HIP_CHECK(hipEventRecord(im.ev_done[k & 1], im.s));
     offset += len;
     im.st.bytes += len;

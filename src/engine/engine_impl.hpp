@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <map>
 #include <memory>
 #include <vector>
@@ -64,6 +65,9 @@ struct Engine::Impl {
   int cur = 0;
   uint32_t* d_bucket_ovf = nullptr;
   uint8_t* d_bucket_en = nullptr;
+  uint64_t* d_newkeys = nullptr;  // [buckets * NEWKEY_CAP], grows with the table
+  size_t newkeys_buckets = 0;
+  uint64_t* newkeys();            // sized for the current table
 
   // key arena (bytes of >8-byte words)
   uint8_t* d_arena = nullptr;
@@ -106,6 +110,11 @@ struct Engine::Impl {
   void complete_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev, uint32_t log2_rb,
                      uint32_t blocks);
   uint32_t blocks_for(uint64_t len) const;
+  // Shuffle partitions track the running table (one reduce block reads only
+  // its own partition) up to MAX_REC_BUCKETS.
+  uint32_t rec_buckets_log2() {
+    return std::min<uint32_t>(std::max(opt.log2_rec_buckets, table().log2_buckets), MAX_REC_BUCKETS_LOG2);
+  }
   void split_table();
 
   void compact_local();                     // table -> cols (unsorted)

@@ -22,7 +22,7 @@ constexpr int MAP_TILE = MAP_THREADS * MAP_BPL;      // 16 KiB LDS text tile
 constexpr int MAP_HALO = 256;                        // bytes past the tile kept in LDS
 constexpr int MAP_SLOTS = 2048;                      // LDS combiner slots (groups of 4)
 constexpr int MAP_GROUPS = MAP_SLOTS / 4;
-constexpr int MAP_FLUSH_AT = MAP_SLOTS * 3 / 8;      // flush before a tile when fuller
+constexpr int MAP_FILL_MAX = MAP_SLOTS * 3 / 4;      // adaptive flush: target max fill
 constexpr int MAP_MAX_GROUP_PROBES = 8;              // then flush and retry the token
 constexpr int MAX_REC_BUCKETS_LOG2 = 9;              // shuffle partitions <= 512
 constexpr int MAX_REC_BUCKETS = 1 << MAX_REC_BUCKETS_LOG2;
@@ -101,7 +101,9 @@ struct ReduceArgs {
   uint32_t* flags;
   uint32_t* bucket_overflow;      // [n_buckets] set when a slice overflowed
   const uint8_t* bucket_enable;   // nullptr = all
+  uint64_t* newkeys;              // [n_buckets * NEWKEY_CAP] (slot << 32 | offset) of new long words
 };
+constexpr int NEWKEY_CAP = 1024;  // per bucket and pass; beyond it words are copied inline
 
 struct SynthVocab {
   const uint8_t* bytes;

@@ -41,6 +41,7 @@ struct MapLds {
   uint8_t tile[MAP_TILE + MAP_HALO + 16];  // +16: tile8() reads one word past
   uint32_t wsum[MAP_THREADS / 64];
   uint32_t occupied;
+  uint32_t occ_before, last_new;  // adaptive flush: keys added by the last tile
   uint32_t prev;
   uint32_t flush_ok;
   uint32_t nflush;  // directory entries written by this block
@@ -336,6 +337,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
   }
   if (tid == 0) {
     L.occupied = 0;
+    L.last_new = 0;
     L.tokens = 0;
     L.nflush = 0;
     L.used = 0;
@@ -361,7 +363,11 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const uint64_t t0 = tile * MAP_TILE;
     __syncthreads();  // previous tile fully consumed
-    if (L.occupied > MAP_FLUSH_AT) flush_table(L, a);
+    // Flush only if the keys the last tile added would not fit again: Zipf
+    // text with a small vocabulary keeps its table across many tiles, large
+    // vocabularies flush before every tile instead of overflowing mid-tile.
+    if (L.occupied + L.last_new > MAP_FILL_MAX) flush_table(L, a);
+    if (tid == 0) L.occ_before = L.occupied;
     // ---- commit the prefetched tile to LDS, start loading the next ----
     reinterpret_cast<uint4*>(&L.tile[tid * MAP_BPL])[0] = p0;
     reinterpret_cast<uint4*>(&L.tile[tid * MAP_BPL])[1] = p1;
@@ -416,6 +422,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
       if (!__syncthreads_or(todo != 0)) break;
       flush_table(L, a);  // neighbourhood full: flush, then retry those tokens
     }
+    if (tid == 0) L.last_new = L.occupied > L.occ_before ? L.occupied - L.occ_before : L.occupied;
   }
   __syncthreads();
   if (L.occupied) flush_table(L, a);

@@ -30,6 +30,9 @@ struct RedLds {
   uint64_t first[TAB_SLOTS];
   uint32_t occupied;
   uint32_t overflow;
+  uint32_t nnew;                 // new long words queued in a.newkeys
+  unsigned long long arena_base;  // this block's arena reservation
+  unsigned long long arena_need;
 };
 
 __device__ __forceinline__ void load_slice(RedLds& L, const TableView& t, uint32_t b) {
@@ -72,6 +75,42 @@ __device__ void arena_copy_word(const ReduceArgs& a, uint64_t off, size_t gslot)
   a.tab.sref_len[gslot] = (uint32_t)len;
 }
 
+// Copy the bytes of this pass's new long words into the key arena: one word
+// per thread, one global arena reservation per block.
+__device__ void copy_new_words(RedLds& L, const ReduceArgs& a, uint32_t b) {
+  const uint32_t n = min(L.nnew, (uint32_t)NEWKEY_CAP);
+  uint64_t len[2], mine[2];
+  unsigned long long off[2];
+  for (int k = 0; k < 2; ++k) {  // up to 2 words per thread (NEWKEY_CAP <= 2 * RED_THREADS)
+    const uint32_t i = threadIdx.x + k * RED_THREADS;
+    len[k] = 0;
+    if (i < n) {
+      mine[k] = a.newkeys[(size_t)b * NEWKEY_CAP + i];
+      const uint64_t o = mine[k] & 0xFFFFFFFFull;
+      while (o + len[k] < a.avail_len && !is_delim(a.text[o + len[k]])) ++len[k];
+      off[k] = atomicAdd(&L.arena_need, (unsigned long long)len[k]);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) L.arena_base = L.arena_need ? atomicAdd(a.arena.cursor, L.arena_need) : 0;
+  __syncthreads();
+  for (int k = 0; k < 2; ++k) {
+    const uint32_t i = threadIdx.x + k * RED_THREADS;
+    if (i >= n) continue;
+    const size_t gslot = (size_t)b * TAB_SLOTS + (mine[k] >> 32);
+    const uint64_t p = L.arena_base + off[k], o = mine[k] & 0xFFFFFFFFull;
+    if (p + len[k] > a.arena.cap) {
+      atomicOr(&a.flags[FLAG_ARENA_OVF], 1u);
+      a.tab.sref_off[gslot] = 0;
+      a.tab.sref_len[gslot] = 0;
+      continue;
+    }
+    for (uint64_t j = 0; j < len[k]; ++j) a.arena.bytes[p + j] = a.text[o + j];
+    a.tab.sref_off[gslot] = p;
+    a.tab.sref_len[gslot] = (uint32_t)len[k];
+  }
+}
+
 __device__ __forceinline__ void merge_record(RedLds& L, const ReduceArgs& a, uint32_t b, const Rec& r, uint32_t shift) {
   const uint64_t ph = place_hash(r.k0, r.k1);
   if (shift && bucket_of(ph, a.tab.log2_buckets) != b) return;
@@ -86,7 +125,11 @@ __device__ __forceinline__ void merge_record(RedLds& L, const ReduceArgs& a, uin
             (unsigned long long)(a.chunk_base + (r.co & 0xFFFFFFFFull)));
   if (claimed) {
     if (atomicAdd(&L.occupied, 1u) + 1 > (uint32_t)TAB_MAX_OCC) L.overflow = 1;
-    if (!key_is_short(r.k1)) arena_copy_word(a, r.co & 0xFFFFFFFFull, (size_t)b * TAB_SLOTS + s);
+    if (!key_is_short(r.k1)) {  // copy its bytes after the merge loop, all threads in parallel
+      const uint32_t q = atomicAdd(&L.nnew, 1u);
+      if (q < (uint32_t)NEWKEY_CAP) a.newkeys[(size_t)b * NEWKEY_CAP + q] = ((uint64_t)s << 32) | (r.co & 0xFFFFFFFFull);
+      else arena_copy_word(a, r.co & 0xFFFFFFFFull, (size_t)b * TAB_SLOTS + s);
+    }
   }
 }
 
@@ -100,6 +143,8 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   if (tid == 0) {
     L.occupied = a.tab.occupancy[b];
     L.overflow = 0;
+    L.nnew = 0;
+    L.arena_need = 0;
   }
   __syncthreads();
 
@@ -156,6 +201,7 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
     }
     return;
   }
+  copy_new_words(L, a, b);
   store_slice(L, a.tab, b);
   if (tid == 0) {
     a.tab.occupancy[b] = L.occupied;
