@@ -34,11 +34,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--gb-per-gpu", type=float, default=1.0, help="GiB of synthetic text per GPU")
-    ap.add_argument("--vocab", type=int, default=100000)
-    ap.add_argument("--zipf", type=float, default=1.0)
-    ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--chunk-gb", type=float, default=1.0)
+    ap.add_argument("--config", default="1gb", help="BASELINE config (cuda_mapreduce_amd.models.CONFIGS)")
+    ap.add_argument("--gb-per-gpu", type=float, default=None, help="override: GiB of synthetic text per GPU")
+    ap.add_argument("--vocab", type=int, default=None)
+    ap.add_argument("--zipf", type=float, default=None)
+    ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--chunk-gb", type=float, default=None)
+    ap.add_argument("--pool-gb", type=float, default=None, help="host-staged: replay pool per GPU")
     ap.add_argument("--json-out", default="")
     return ap.parse_args()
 
@@ -54,7 +56,18 @@ def main() -> int:
     import torch
     import torch.distributed as dist
 
-    from cuda_mapreduce_amd.ops import Comm, Engine
+    from cuda_mapreduce_amd.models import CONFIGS
+    from cuda_mapreduce_amd.ops import Comm, Engine, synth_host
+    import numpy as np
+
+    cfg = CONFIGS[a.config]
+    gib = 1 << 30
+    per_gpu = int(a.gb_per_gpu * gib) if a.gb_per_gpu is not None else cfg.bytes_per_gpu
+    vocab = a.vocab if a.vocab is not None else cfg.vocab
+    zipf = a.zipf if a.zipf is not None else cfg.zipf_s
+    seed = a.seed if a.seed is not None else cfg.seed
+    chunk = int(a.chunk_gb * gib) if a.chunk_gb is not None else cfg.chunk_bytes
+    host_staged = cfg.source == "host-staged"
 
     torch.cuda.set_device(local)
     if world > 1:
@@ -65,10 +78,9 @@ def main() -> int:
         if world > 1:
             dist.barrier()
 
-    nbytes = int(a.gb_per_gpu * (1 << 30))
     seg = 1024
-    nbytes = nbytes // seg * seg
-    chunk = int(a.chunk_gb * (1 << 30))
+    nbytes = per_gpu // seg * seg
+    chunk = min(chunk, nbytes) // seg * seg
     eng = Engine(device=local, chunk_bytes=chunk)
     comm = None
     if world > 1:
@@ -78,12 +90,22 @@ def main() -> int:
 
     # rank r owns segments [r*nseg, (r+1)*nseg) of the logical stream
     first_seg = rank * (nbytes // seg)
-    eng.synth_device(nbytes, first_segment=first_seg, seed=a.seed, vocab=a.vocab, zipf_s=a.zipf)
     base = rank * nbytes
+    if host_staged:
+        # pinned host pool of whole chunks replayed over PCIe (1 TB config: 128 GiB per GPU)
+        pool_bytes = int((a.pool_gb if a.pool_gb is not None else cfg.pool_bytes / gib) * gib)
+        pool_bytes = max(chunk, pool_bytes // chunk * chunk)
+        pool = np.frombuffer(synth_host(pool_bytes, first_segment=first_seg, seed=seed, vocab=vocab, zipf_s=zipf),
+                             np.uint8)
+    else:
+        eng.synth_device(nbytes, first_segment=first_seg, seed=seed, vocab=vocab, zipf_s=zipf)
 
     def step():
         eng.reset()
-        eng.count_resident(nbytes, global_base=base)
+        if host_staged:
+            eng.count_replay_pinned(pool, nbytes, global_base=base)
+        else:
+            eng.count_resident(nbytes, global_base=base)
         return eng.finalize_device(comm)
 
     for _ in range(a.warmup):
@@ -125,11 +147,12 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8 text / u64 counts",
-            "data": f"synthetic (device-generated Zipf({a.zipf}) text, {a.vocab}-word vocabulary, seed {a.seed})",
+            "data": (f"synthetic ({'host pool replayed over PCIe' if host_staged else 'device-generated'} "
+                     f"Zipf({zipf}) text, {vocab}-word vocabulary, seed {seed})"),
             "words_per_s": round(words, 1),
             "distinct_words": keys,
             "config": {
-                "model": "wordcount-mapreduce",
+                "model": f"wordcount-mapreduce/{cfg.name}",
                 "global_batch": total_bytes,
                 "seq_len": nbytes,
                 "parallelism": f"dp{world}",

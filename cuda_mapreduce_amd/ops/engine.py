@@ -157,6 +157,13 @@ class Engine:
         ptr, keep = _u8ptr(pool)
         check(lib.wc_count_replay(self._p, ptr, len(keep), total, global_base))
 
+    def count_replay_pinned(self, pool: np.ndarray, total: int, global_base: int = 0) -> None:
+        """Host-staged path at PCIe speed: the pool (whole chunks, each ending with a
+        delimiter) is page-locked once and DMA'd straight to HBM, overlapped with compute."""
+        ptr, keep = _u8ptr(pool)
+        self._pool = keep  # must stay alive (and registered) while the engine uses it
+        check(lib.wc_count_pinned_replay(self._p, ptr, len(keep), total, global_base))
+
     def synth_device(self, nbytes: int, first_segment: int = 0, seed: int = 1, vocab: int = 100000, zipf_s: float = 1.0) -> None:
         """Generate synthetic text directly in HBM (no host/PCIe involvement)."""
         check(lib.wc_synth_device(self._p, nbytes, first_segment, seed, vocab, zipf_s))

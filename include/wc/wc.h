@@ -37,6 +37,8 @@ int wc_engine_reset(wc_engine* e);
 int wc_count_host(wc_engine* e, const uint8_t* text, uint64_t n, uint64_t global_base);
 int wc_count_file(wc_engine* e, const char* path, uint64_t begin, uint64_t end, uint64_t global_base);
 int wc_count_replay(wc_engine* e, const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t global_base);
+/* Host-staged benchmark path: pool page-locked once, chunks DMA'd directly. */
+int wc_count_pinned_replay(wc_engine* e, const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t global_base);
 /* Generate synthetic text into the engine's device text buffer ... */
 int wc_synth_device(wc_engine* e, uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double zipf_s);
 /* ... and count [0, n) of it. */

@@ -83,6 +83,10 @@ class Engine {
   void count_host(const uint8_t* h_text, uint64_t n, uint64_t global_base);
   // Streaming source (files larger than HBM, replayed synthetic chunks).
   void count_source(ChunkSource& src, uint64_t global_base);
+  // Host-staged benchmark path: `total` bytes replayed from a host pool of
+  // whole chunks (each ending with a delimiter), page-locked once and DMA'd
+  // straight into HBM with H2D of chunk k+1 overlapping compute of chunk k.
+  void count_pinned_replay(const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t global_base);
 
   // Device-resident synthetic text: allocates (or reuses) a buffer of n bytes
   // holding segments [first_segment, ...) of the spec's stream.

@@ -120,6 +120,10 @@ int wc_count_replay(wc_engine* e, const uint8_t* pool, uint64_t pool_bytes, uint
   });
 }
 
+int wc_count_pinned_replay(wc_engine* e, const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t base) {
+  return guard([&] { e->e->count_pinned_replay(pool, pool_bytes, total, base); });
+}
+
 int wc_synth_device(wc_engine* e, uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double s) {
   return guard([&] {
     e->d_text = e->e->synth_device(n, first_segment, spec_of(seed, vocab, s));

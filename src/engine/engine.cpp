@@ -13,6 +13,7 @@
 //    region overflow re-runs the chunk in halves, running-table overflow
 //    splits the table (B -> 2B) and re-runs only the overflowed buckets.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -57,6 +58,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   WC_HIP_CHECK(hipStreamCreateWithFlags(&copy_s, hipStreamNonBlocking));
   map_blocks = opt.map_blocks ? opt.map_blocks : 2u * (uint32_t)device_cu_count(dev);
   if (const char* e = std::getenv("WC_ABLATE_MAP")) ablate_map = (uint32_t)std::atoi(e);  // profiling only
+  if (const char* e = std::getenv("WC_SYNC_DEBUG")) sync_debug = std::atoi(e) != 0;
 
   opt.log2_rec_buckets = std::min<uint32_t>(opt.log2_rec_buckets, MAX_REC_BUCKETS_LOG2);
   opt.max_log2_tab_buckets = std::min<uint32_t>(std::max<uint32_t>(opt.max_log2_tab_buckets, 1), 20);
@@ -112,6 +114,7 @@ Engine::Impl::~Impl() {
   if (d_arena) (void)hipFree(d_arena);
   if (d_arena_cursor) (void)hipFree(d_arena_cursor);
   if (d_newkeys) (void)hipFree(d_newkeys);
+  if (registered) (void)hipHostUnregister(const_cast<uint8_t*>(registered));
   if (s) (void)hipStreamDestroy(s);
   if (copy_s) (void)hipStreamDestroy(copy_s);
 }
@@ -149,10 +152,22 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   pass_rec.dir_per_block = dir_per_block_for(len, blocks);
   MapArgs m{text, len, avail, prev, log2_rb, pass_rec, d_ctr->flags, &d_ctr->tokens, ablate_map};
   launch_map(m, blocks, s);
+  if (sync_debug) {  // WC_SYNC_DEBUG: attribute a device fault to a kernel and a chunk
+    const hipError_t e = hipStreamSynchronize(s);
+    fprintf(stderr, "[wc] map    base=%llu len=%llu avail=%llu blocks=%u J=%u -> %s\n", (unsigned long long)base,
+            (unsigned long long)len, (unsigned long long)avail, blocks, pass_rec.dir_per_block, hipGetErrorString(e));
+    WC_HIP_CHECK(e);
+  }
   ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                 avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
                 d_ctr->flags, d_bucket_ovf, nullptr, newkeys()};
   if (!ablate_map) launch_reduce(ra, s);  // ablated map output is not a valid shuffle
+  if (sync_debug) {
+    const hipError_t e = hipStreamSynchronize(s);
+    fprintf(stderr, "[wc] reduce base=%llu buckets=%u -> %s\n", (unsigned long long)base, 1u << table().log2_buckets,
+            hipGetErrorString(e));
+    WC_HIP_CHECK(e);
+  }
   WC_HIP_CHECK(hipMemcpyAsync(h_ctr, d_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));
 }
 
@@ -444,6 +459,50 @@ void Engine::count_source(ChunkSource& src, uint64_t global_base) {
     offset += len;
     im.st.bytes += len;
     len = next;
+  }
+  WC_HIP_CHECK(hipStreamSynchronize(im.copy_s));
+  im.st.map_reduce_ms += (now_seconds() - t0) * 1e3;
+}
+
+void Engine::count_pinned_replay(const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t global_base) {
+  Impl& im = *p_;
+  WC_HIP_CHECK(hipSetDevice(im.dev));
+  Range r("wc_count_pinned_replay");
+  const double t0 = now_seconds();
+  const uint64_t C = std::min<uint64_t>(im.opt.chunk_bytes, pool_bytes);
+  WC_CHECK(pool_bytes % C == 0, "replay pool must be a whole number of chunks");
+  for (uint64_t c = C; c <= pool_bytes; c += C)
+    WC_CHECK(is_delim(pool[c - 1]), "every replay chunk must end with a delimiter");
+  // Page-lock the caller's pool once: chunks are DMA'd straight from it.
+  if (im.registered != pool) {
+    if (im.registered) (void)hipHostUnregister(const_cast<uint8_t*>(im.registered));
+    im.registered = nullptr;
+    WC_HIP_CHECK(hipHostRegister(const_cast<uint8_t*>(pool), pool_bytes, hipHostRegisterDefault));
+    im.registered = pool;
+  }
+  im.ensure_staging(C);
+  WC_HIP_CHECK(hipEventRecord(im.ev_done[0], im.s));
+  WC_HIP_CHECK(hipEventRecord(im.ev_done[1], im.s));
+  const uint64_t nchunks = (total + C - 1) / C;
+  auto issue = [&](uint64_t k) {
+    const uint64_t len = std::min<uint64_t>(C, total - k * C);
+    WC_HIP_CHECK(hipStreamWaitEvent(im.copy_s, im.ev_done[k & 1], 0));
+    WC_HIP_CHECK(hipMemcpyAsync(im.d_stage[k & 1], pool + (k * C) % pool_bytes, len, hipMemcpyHostToDevice,
+                                im.copy_s));
+    WC_HIP_CHECK(hipEventRecord(im.ev_h2d[k & 1], im.copy_s));
+  };
+  if (nchunks) issue(0);
+  for (uint64_t k = 0; k < nchunks; ++k) {
+    const uint64_t len = std::min<uint64_t>(C, total - k * C);
+    const uint8_t* d = im.d_stage[k & 1];
+    WC_HIP_CHECK(hipStreamWaitEvent(im.s, im.ev_h2d[k & 1], 0));
+    const uint32_t blocks = im.blocks_for(len), rb = im.rec_buckets_log2();
+    // a truncated last chunk may end mid-word: it is the end of the stream
+    im.launch_pass(d, len, len, global_base + k * C, ' ', rb, blocks);
+    if (k + 1 < nchunks) issue(k + 1);  // H2D of chunk k+1 overlaps map/reduce of chunk k
+    im.complete_pass(d, len, len, global_base + k * C, ' ', rb, blocks);
+    WC_HIP_CHECK(hipEventRecord(im.ev_done[k & 1], im.s));
+    im.st.bytes += len;
   }
   WC_HIP_CHECK(hipStreamSynchronize(im.copy_s));
   im.st.map_reduce_ms += (now_seconds() - t0) * 1e3;

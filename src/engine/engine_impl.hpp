@@ -45,6 +45,7 @@ struct Engine::Impl {
   hipStream_t s = nullptr, copy_s = nullptr;
   uint32_t map_blocks = 0;
   uint32_t ablate_map = 0;  // WC_ABLATE_MAP (profiling ablations, MapArgs::ablate)
+  bool sync_debug = false;  // WC_SYNC_DEBUG: sync + log after every kernel
 
   // shuffle records
   uint64_t rec_total = 0;
@@ -79,6 +80,7 @@ struct Engine::Impl {
   uint64_t text_cap = 0;
   uint8_t* d_stage[2] = {nullptr, nullptr};
   std::vector<PinnedBuffer> pinned;
+  const uint8_t* registered = nullptr;  // caller pool page-locked by count_pinned_replay
   hipEvent_t ev_h2d[2] = {}, ev_done[2] = {};
 
   // synthetic vocabulary on device

@@ -160,3 +160,17 @@ def test_cli_golden(tmp_path, golden_text):
     assert out.stdout == GOLDEN_OUTPUT
     out = subprocess.run([exe, str(tmp_path / "test.txt")], capture_output=True, timeout=120)
     assert out.stdout == GOLDEN_OUTPUT
+
+
+def test_pinned_replay_host_staged():
+    pool = np.frombuffer(ops.synth_host(1 << 20, seed=6, vocab=2000), np.uint8).copy()
+    with ops.Engine(device=0, chunk_bytes=1 << 18) as e:
+        e.count_replay_pinned(pool, total=(5 << 20) + (1 << 18))
+        got = e.result()
+    one = ops.cpu_count(pool.tobytes())
+    q = ops.cpu_count(pool[: 1 << 18].tobytes())
+    want = {w: 5 * int(c) for w, c in zip(one.words, one.counts)}
+    for w, c in zip(q.words, q.counts):
+        want[w] = want.get(w, 0) + int(c)
+    assert got.total == 5 * one.total + q.total
+    assert dict(zip(got.words, got.counts.tolist())) == want
