@@ -122,3 +122,25 @@ def test_shard_range_file_matches_mem(tmp_path):
     for world in (2, 4, 7):
         for r in range(world):
             assert ops.shard_range_file(str(p), r, world) == ops.shard_range(text, r, world)
+
+
+def test_cli_synthetic_cpu_matches_python_oracle(tmp_path):
+    exe = os.path.join(ROOT, "wordcount")
+    out = subprocess.run([exe, "--cpu", "--synthetic", "64K:3:500", "--bench-json", str(tmp_path / "b.json")],
+                         capture_output=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    want = ops.format_output(ops.cpu_count(ops.synth_host(64 * 1024, seed=3, vocab=500)))
+    assert out.stdout == want
+    import json
+
+    j = json.loads((tmp_path / "b.json").read_text())
+    assert j["bytes"] == 64 * 1024 and j["path"] == "cpu"
+
+
+def test_cli_top_k(tmp_path):
+    exe = os.path.join(ROOT, "wordcount")
+    p = tmp_path / "t.txt"
+    p.write_bytes(b"a b a c a b d\n")
+    out = subprocess.run([exe, str(p), "--cpu", "--no-echo", "--top", "2"], capture_output=True, timeout=60)
+    assert out.stdout.split(b"-" * 26 + b"\n")[1] == b"a\t3\nb\t2\n"
+    assert out.stdout.endswith(b"Total Count:7\n")
