@@ -31,6 +31,8 @@ class Options(ctypes.Structure):
         ("arena_bytes", c_uint64),
         ("min_records", c_uint64),
         ("records_per_byte", c_double),
+        ("merge_mode", c_uint32),  # 0 shuffle (all-to-all by key owner), 1 dense reduce-scatter
+        ("reserved", c_uint32),
     ]
 
 
@@ -76,7 +78,7 @@ def _load() -> ctypes.CDLL:
         "wc_rccl_unique_id": (c_int, [POINTER(c_char)]),
         "wc_comm_rccl_create": (c_void_p, [POINTER(c_char), c_int, c_int, c_int]),
         "wc_comm_destroy": (None, [c_void_p]),
-        "wc_loopback_count": (c_void_p, [P8, c_uint64, c_int, POINTER(c_int), POINTER(Options)]),
+        "wc_loopback_count": (c_void_p, [P8, c_uint64, c_int, POINTER(c_int), POINTER(Options), c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -24,6 +24,8 @@ typedef struct wc_options {
   uint64_t arena_bytes;
   uint64_t min_records;
   double records_per_byte;
+  uint32_t merge_mode; /* 0 shuffle (all-to-all by key owner), 1 dense reduce-scatter */
+  uint32_t reserved;
 } wc_options;
 
 const char* wc_last_error(void);
@@ -72,8 +74,10 @@ int wc_rccl_unique_id(char out[128]);
 wc_comm* wc_comm_rccl_create(const char* unique_id, int rank, int size, int device);
 void wc_comm_destroy(wc_comm* c);
 /* N virtual ranks on `devices` (one thread each) count shards of `text` and
- * merge through the loopback communicator; returns rank 0's result. */
-wc_result* wc_loopback_count(const uint8_t* text, uint64_t n, int ranks, const int* devices, const wc_options* o);
+ * merge through the loopback communicator; returns rank 0's result.  With
+ * all_ranks every rank receives the merged table and must match rank 0's. */
+wc_result* wc_loopback_count(const uint8_t* text, uint64_t n, int ranks, const int* devices, const wc_options* o,
+                             int all_ranks);
 
 #ifdef __cplusplus
 }

@@ -45,6 +45,10 @@ struct Options {
   uint64_t arena_bytes = 256ull << 20; // key arena for >8-byte words
   uint32_t map_blocks = 0;             // 0 = 2 per CU
   uint32_t staging_buffers = 3;        // pinned host ring depth (host-staged path)
+  // Cross-GPU merge: 0 = shuffle (all-to-all of each key to its hash owner, owner-side
+  // merge, gather to rank 0); 1 = dense (dictionary union on every rank, reduce-scatter of
+  // dense count vectors + all-gather).
+  uint32_t merge_mode = 0;
 };
 
 // Synthetic text spec (see src/kernels/synth.hpp).

@@ -49,6 +49,7 @@ wc::Options to_opts(const wc_options* o) {
   x.arena_bytes = o->arena_bytes;
   x.min_records = o->min_records;
   x.records_per_byte = o->records_per_byte;
+  x.merge_mode = o->merge_mode;
   return x;
 }
 
@@ -84,6 +85,8 @@ void wc_default_options(wc_options* o) {
   o->arena_bytes = d.arena_bytes;
   o->min_records = d.min_records;
   o->records_per_byte = d.records_per_byte;
+  o->merge_mode = d.merge_mode;
+  o->reserved = 0;
 }
 
 wc_engine* wc_engine_create(const wc_options* o) {
@@ -267,9 +270,11 @@ wc_comm* wc_comm_rccl_create(const char* unique_id, int rank, int size, int devi
 
 void wc_comm_destroy(wc_comm* c) { delete c; }
 
-wc_result* wc_loopback_count(const uint8_t* text, uint64_t n, int ranks, const int* devices, const wc_options* o) {
+wc_result* wc_loopback_count(const uint8_t* text, uint64_t n, int ranks, const int* devices, const wc_options* o,
+                             int all_ranks) {
   wc_result* out = new wc_result;
   std::vector<std::string> errs(ranks);
+  std::vector<wc::KeyTable> tables(ranks);
   std::vector<std::unique_ptr<wc::Comm>> comms;
   if (guard([&] { comms = wc::make_loopback_comms(ranks); }) != 0) {
     delete out;
@@ -284,8 +289,12 @@ wc_result* wc_loopback_count(const uint8_t* text, uint64_t n, int ranks, const i
         wc::Engine eng(opt);
         const wc::ShardRange sr = wc::shard_range_mem(text, n, r, ranks);
         if (sr.end > sr.begin) eng.count_host(text + sr.begin, sr.end - sr.begin, sr.begin);
-        wc::KeyTable t = eng.result(comms[r].get(), false);
-        if (r == 0) out->t = std::move(t);
+        wc::KeyTable t = eng.result(comms[r].get(), all_ranks != 0);
+        if (r == 0) {
+          out->t = std::move(t);
+        } else if (all_ranks) {
+          tables[r] = std::move(t);
+        }
       } catch (const std::exception& ex) {
         errs[r] = ex.what();
       }
@@ -298,6 +307,14 @@ wc_result* wc_loopback_count(const uint8_t* text, uint64_t n, int ranks, const i
       delete out;
       return nullptr;
     }
+  for (int r = 1; all_ranks && r < ranks; ++r) {
+    const wc::KeyTable& t = tables[r];
+    if (t.words != out->t.words || t.counts != out->t.counts || t.first_off != out->t.first_off) {
+      g_err = "rank " + std::to_string(r) + ": all_ranks result differs from rank 0";
+      delete out;
+      return nullptr;
+    }
+  }
   return out;
 }
 

@@ -50,6 +50,20 @@ class RcclComm final : public Comm {
   void reduce_scatter_u64(const uint64_t* send, uint64_t* recv, size_t count, RedOp op, hipStream_t s) override {
     WC_NCCL_CHECK(ncclReduceScatter(send, recv, count, ncclUint64, to_nccl(op), c_, s));
   }
+  void alltoallv(const void* send, const size_t* send_off, const size_t* send_bytes, void* recv,
+                 const size_t* recv_off, const size_t* recv_bytes, hipStream_t s) override {
+    WC_NCCL_CHECK(ncclGroupStart());
+    for (int p = 0; p < size_; ++p) {
+      if (send_bytes[p])
+        WC_NCCL_CHECK(ncclSend(static_cast<const uint8_t*>(send) + send_off[p], send_bytes[p], ncclUint8, p, c_, s));
+      if (recv_bytes[p])
+        WC_NCCL_CHECK(ncclRecv(static_cast<uint8_t*>(recv) + recv_off[p], recv_bytes[p], ncclUint8, p, c_, s));
+    }
+    WC_NCCL_CHECK(ncclGroupEnd());
+  }
+  void broadcast(void* buf, size_t bytes, int root, hipStream_t s) override {
+    if (bytes) WC_NCCL_CHECK(ncclBroadcast(buf, buf, bytes, ncclUint8, root, c_, s));
+  }
   void barrier(hipStream_t s) override {
     WC_NCCL_CHECK(ncclAllReduce(scratch_, scratch_, 1, ncclUint64, ncclSum, c_, s));
     WC_HIP_CHECK(hipStreamSynchronize(s));
@@ -63,8 +77,9 @@ class RcclComm final : public Comm {
 
 // Shared rendezvous for loopback ranks.
 struct Hub {
-  explicit Hub(int n) : n(n), ptrs(n, nullptr) {}
+  explicit Hub(int n) : n(n), offs(n, nullptr), ptrs(n, nullptr) {}
   int n;
+  std::vector<const size_t*> offs;  // alltoallv: each rank's send offsets
   std::mutex mu;
   std::condition_variable cv;
   int arrived = 0;
@@ -117,6 +132,28 @@ class LoopbackComm final : public Comm {
     }
     WC_HIP_CHECK(hipStreamSynchronize(s));
     if (tmp) WC_HIP_CHECK(hipFree(tmp));
+    hub_->wait_all();
+  }
+  void alltoallv(const void* send, const size_t* send_off, const size_t* /*send_bytes*/, void* recv,
+                 const size_t* recv_off, const size_t* recv_bytes, hipStream_t s) override {
+    WC_HIP_CHECK(hipStreamSynchronize(s));
+    hub_->ptrs[rank_] = send;
+    hub_->offs[rank_] = send_off;
+    hub_->wait_all();
+    for (int r = 0; r < hub_->n; ++r)
+      if (recv_bytes[r])
+        WC_HIP_CHECK(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[r],
+                                    static_cast<const uint8_t*>(hub_->ptrs[r]) + hub_->offs[r][rank_], recv_bytes[r],
+                                    hipMemcpyDefault, s));
+    WC_HIP_CHECK(hipStreamSynchronize(s));
+    hub_->wait_all();
+  }
+  void broadcast(void* buf, size_t bytes, int root, hipStream_t s) override {
+    WC_HIP_CHECK(hipStreamSynchronize(s));
+    if (rank_ == root) hub_->ptrs[root] = buf;
+    hub_->wait_all();
+    if (rank_ != root && bytes) WC_HIP_CHECK(hipMemcpyAsync(buf, hub_->ptrs[root], bytes, hipMemcpyDefault, s));
+    WC_HIP_CHECK(hipStreamSynchronize(s));
     hub_->wait_all();
   }
   void barrier(hipStream_t s) override {

@@ -30,6 +30,11 @@ class Comm {
   virtual void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
   // recv[count] = op over ranks of send[rank * count ... + count).
   virtual void reduce_scatter_u64(const uint64_t* send, uint64_t* recv, size_t count, RedOp op, hipStream_t s) = 0;
+  // Personalised exchange (the MapReduce shuffle): bytes [send_off[p], +send_bytes[p]) of
+  // `send` go to rank p, which receives them at recv + recv_off[me].  Arrays have size().
+  virtual void alltoallv(const void* send, const size_t* send_off, const size_t* send_bytes, void* recv,
+                         const size_t* recv_off, const size_t* recv_bytes, hipStream_t s) = 0;
+  virtual void broadcast(void* buf, size_t bytes, int root, hipStream_t s) = 0;
   virtual void barrier(hipStream_t s) = 0;
 };
 

@@ -1,7 +1,19 @@
 // merge.cpp — cross-GPU merge of per-rank key tables.
 //
 // Keys are variable-length words, so per-rank tables are not index-aligned.
-// Protocol (all device-side, RCCL over xGMI or loopback):
+// Two protocols (Options::merge_mode), all device-side, RCCL over xGMI or loopback.
+//
+// SHUFFLE (default) — the MapReduce shuffle proper, W-way parallel merge work:
+//  1. owner(key) = high bits of the placement hash; count rows / long-word
+//     bytes per owner, all-gather the W x 2 count matrix (+ max offset)    tiny
+//  2. pack rows (40 B) + long-word bytes by owner, RCCL all-to-all         ~V x 40 B
+//  3. owner merges what it received in a global hash table (row-id claims,
+//     device-scope count / min-offset atomics) and compacts it
+//  4. gather the merged rows + bytes to rank 0 (broadcast for all_ranks)   ~V x 40 B
+// Each rank merges ~V/W keys instead of sorting all W x V, and only rank 0
+// orders the final table; the merge is a few tens of microseconds of xGMI.
+//
+// DENSE (merge_mode 1):
 //  1. allgather per-rank (n_keys, arena bytes, max offset)              tiny
 //  2. allgather the padded key columns (k0, k1, arena refs) + arenas    ~V x 28 B
 //  3. every rank sorts the union by (k0, k1) (stable LSD radix) and
@@ -20,8 +32,8 @@
 
 namespace wc {
 
-void merge_cols(Engine::Impl& im, Comm& comm) {
-  Range rg("wc_merge");
+void merge_cols_dense(Engine::Impl& im, Comm& comm) {
+  Range rg("wc_merge_dense");
   hipStream_t s = im.s;
   const int W = comm.size(), R = comm.rank();
   const uint64_t n = im.cols.n;
@@ -125,6 +137,166 @@ void merge_cols(Engine::Impl& im, Comm& comm) {
   im.cols_arena = AR;
   im.cols_arena_bytes = (uint64_t)W * a_max;
   im.max_end = gmax_end;
+}
+
+
+namespace {
+template <class T>
+T* take_aligned(DeviceArena& A, size_t n) {
+  return A.take_n<T>(n ? n : 1);
+}
+}  // namespace
+
+void merge_cols_shuffle(Engine::Impl& im, Comm& comm, bool all_ranks) {
+  Range rg("wc_merge_shuffle");
+  hipStream_t s = im.s;
+  const int W = comm.size(), R = comm.rank();
+  WC_CHECK(W <= (int)MERGE_MAX_RANKS, "shuffle merge supports at most 64 ranks");
+  const uint64_t n = im.cols.n;
+  const size_t C = 2 * (size_t)W + 1;  // per rank: (rows, bytes) per owner + max offset
+
+  // 1. owner counts, exchanged as a W x C matrix (small buffers: own arena)
+  DeviceArena& S = im.merge_small;
+  S.reserve(((size_t)W * C + 2 * C + 4 * (size_t)W + 16) * 8 + 8 * 1024);
+  unsigned long long* d_cnt = take_aligned<unsigned long long>(S, 2 * C);  // counts | cursor
+  unsigned long long* d_all = take_aligned<unsigned long long>(S, (size_t)W * C);
+  WC_HIP_CHECK(hipMemsetAsync(d_cnt, 0, 2 * C * 8, s));
+  const unsigned long long mx = im.max_end;
+  WC_HIP_CHECK(hipMemcpyAsync(d_cnt + 2 * W, &mx, 8, hipMemcpyHostToDevice, s));
+  launch_owner_count(im.cols.k0, im.cols.k1, im.cols.sref_len, n, (uint32_t)W, d_cnt, s);
+  comm.allgather(d_cnt, d_all, C * 8, s);
+  std::vector<unsigned long long> all((size_t)W * C);
+  WC_HIP_CHECK(hipMemcpyAsync(all.data(), d_all, all.size() * 8, hipMemcpyDeviceToHost, s));
+  WC_HIP_CHECK(hipStreamSynchronize(s));
+  uint64_t gmax_end = 0;
+  for (int r = 0; r < W; ++r) gmax_end = std::max<uint64_t>(gmax_end, all[(size_t)r * C + 2 * W]);
+
+  // 2. pack by owner and exchange
+  std::vector<size_t> so_r(W), sb_r(W), so_b(W), sb_b(W), ro_r(W), rb_r(W), ro_b(W), rb_b(W);
+  size_t tr = 0, tb = 0, rr = 0, rbt = 0;
+  for (int p = 0; p < W; ++p) {
+    const unsigned long long* mine = &all[(size_t)R * C];
+    so_r[p] = tr * sizeof(MRow);
+    sb_r[p] = mine[2 * p] * sizeof(MRow);
+    so_b[p] = tb;
+    sb_b[p] = mine[2 * p + 1];
+    tr += mine[2 * p];
+    tb += mine[2 * p + 1];
+    const unsigned long long* theirs = &all[(size_t)p * C];
+    ro_r[p] = rr * sizeof(MRow);
+    rb_r[p] = theirs[2 * R] * sizeof(MRow);
+    ro_b[p] = rbt;
+    rb_b[p] = theirs[2 * R + 1];
+    rr += theirs[2 * R];
+    rbt += theirs[2 * R + 1];
+  }
+  uint64_t T = 1024;
+  while (T < 2 * rr) T <<= 1;
+  // upper bounds of the gathered table: every row / byte of every rank
+  uint64_t Gmax = 0, GBmax = 0;
+  for (int r = 0; r < W; ++r)
+    for (int p = 0; p < W; ++p) {
+      Gmax += all[(size_t)r * C + 2 * p];
+      GBmax += all[(size_t)r * C + 2 * p + 1];
+    }
+  DeviceArena& A = im.merge_mem;
+  A.reserve((tr + 2 * rr + Gmax) * sizeof(MRow) + tb + 2 * rbt + GBmax + T * (4 + 16) + Gmax * (5 * 8 + 4) +
+            (4 * (size_t)W + 4) * 8 + 32 * 1024);
+  MRow* send_rows = take_aligned<MRow>(A, tr);
+  uint8_t* send_bytes = take_aligned<uint8_t>(A, tb);
+  MRow* recv_rows = take_aligned<MRow>(A, rr);
+  uint8_t* recv_bytes = take_aligned<uint8_t>(A, rbt);
+  launch_owner_scatter(im.cols.k0, im.cols.k1, im.cols.cnt, im.cols.first, im.cols.sref_off, im.cols.sref_len,
+                       im.cols_arena, n, (uint32_t)W, d_cnt, d_cnt + C, send_rows, send_bytes, s);
+  comm.alltoallv(send_rows, so_r.data(), sb_r.data(), recv_rows, ro_r.data(), rb_r.data(), s);
+  comm.alltoallv(send_bytes, so_b.data(), sb_b.data(), recv_bytes, ro_b.data(), rb_b.data(), s);
+
+  // 3. owner-side merge
+  uint32_t* state = take_aligned<uint32_t>(A, T);
+  unsigned long long* tcnt = take_aligned<unsigned long long>(A, T);
+  unsigned long long* tfirst = take_aligned<unsigned long long>(A, T);
+  MRow* merged = take_aligned<MRow>(A, rr);
+  uint64_t* d_base = take_aligned<uint64_t>(A, 2 * (size_t)W + 2);  // row / byte bases per source (then per owner)
+  unsigned long long* d_m = take_aligned<unsigned long long>(A, 1);
+  std::vector<uint64_t> base(2 * (size_t)W + 2);
+  for (int p = 0; p < W; ++p) {
+    base[p] = ro_r[p] / sizeof(MRow);
+    base[W + 1 + p] = ro_b[p];
+  }
+  base[W] = rr;
+  base[2 * W + 1] = rbt;
+  WC_HIP_CHECK(hipMemcpyAsync(d_base, base.data(), base.size() * 8, hipMemcpyHostToDevice, s));
+  WC_HIP_CHECK(hipMemsetAsync(state, 0, T * 4, s));
+  WC_HIP_CHECK(hipMemsetAsync(tcnt, 0, T * 8, s));
+  launch_fill_u64(reinterpret_cast<uint64_t*>(tfirst), ~0ull, T, s);
+  WC_HIP_CHECK(hipMemsetAsync(d_m, 0, 8, s));
+  launch_mrow_insert(recv_rows, rr, state, tcnt, tfirst, T, s);
+  launch_mrow_compact(recv_rows, state, tcnt, tfirst, T, d_base, d_base + W + 1, (uint32_t)W, merged, d_m, s);
+
+  // 4. gather merged rows + bytes to rank 0 (and broadcast for all_ranks)
+  unsigned long long own[2] = {0, rbt};
+  WC_HIP_CHECK(hipMemcpyAsync(&own[0], d_m, 8, hipMemcpyDeviceToHost, s));
+  WC_HIP_CHECK(hipStreamSynchronize(s));  // base[] / own[] are pageable host memory
+  unsigned long long* d_own = take_aligned<unsigned long long>(A, 2);
+  unsigned long long* d_owns = take_aligned<unsigned long long>(A, 2 * (size_t)W);
+  WC_HIP_CHECK(hipMemcpyAsync(d_own, own, 16, hipMemcpyHostToDevice, s));
+  comm.allgather(d_own, d_owns, 16, s);
+  std::vector<unsigned long long> owns(2 * (size_t)W);
+  WC_HIP_CHECK(hipMemcpyAsync(owns.data(), d_owns, owns.size() * 8, hipMemcpyDeviceToHost, s));
+  WC_HIP_CHECK(hipStreamSynchronize(s));
+  std::vector<size_t> go_r(W, 0), gb_r(W, 0), go_b(W, 0), gb_b(W, 0), zs(W, 0);
+  std::vector<size_t> sr(W, 0), sb(W, 0);
+  uint64_t G = 0, GB = 0;
+  std::vector<uint64_t> gbase(2 * (size_t)W + 2);
+  for (int p = 0; p < W; ++p) {
+    gbase[p] = G;
+    gbase[W + 1 + p] = GB;
+    go_r[p] = G * sizeof(MRow);
+    go_b[p] = GB;
+    if (R == 0) {
+      gb_r[p] = owns[2 * p] * sizeof(MRow);
+      gb_b[p] = owns[2 * p + 1];
+    }
+    G += owns[2 * p];
+    GB += owns[2 * p + 1];
+  }
+  gbase[W] = G;
+  gbase[2 * W + 1] = GB;
+  sr[0] = own[0] * sizeof(MRow);
+  sb[0] = own[1];
+  const bool have = R == 0 || all_ranks;
+  MRow* grows = take_aligned<MRow>(A, G);
+  uint8_t* gbytes = take_aligned<uint8_t>(A, GB);
+  comm.alltoallv(merged, zs.data(), sr.data(), grows, go_r.data(), gb_r.data(), s);
+  comm.alltoallv(recv_bytes, zs.data(), sb.data(), gbytes, go_b.data(), gb_b.data(), s);
+  if (all_ranks) {
+    comm.broadcast(grows, G * sizeof(MRow), 0, s);
+    comm.broadcast(gbytes, GB, 0, s);
+  }
+  KeyCols o;
+  o.n = have ? G : 0;
+  if (have) {
+    o.k0 = take_aligned<uint64_t>(A, G);
+    o.k1 = take_aligned<uint64_t>(A, G);
+    o.cnt = take_aligned<uint64_t>(A, G);
+    o.first = take_aligned<uint64_t>(A, G);
+    o.sref_off = take_aligned<uint64_t>(A, G);
+    o.sref_len = take_aligned<uint32_t>(A, G);
+    uint64_t* d_gbase = take_aligned<uint64_t>(A, gbase.size());
+    WC_HIP_CHECK(hipMemcpyAsync(d_gbase, gbase.data(), gbase.size() * 8, hipMemcpyHostToDevice, s));
+    launch_mrow_to_cols(grows, G, d_gbase, d_gbase + W + 1, (uint32_t)W, o.k0, o.k1, o.cnt, o.first, o.sref_off,
+                        o.sref_len, s);
+  }
+  WC_HIP_CHECK(hipStreamSynchronize(s));
+  im.cols = o;
+  im.cols_arena = gbytes;
+  im.cols_arena_bytes = have ? GB : 0;
+  im.max_end = gmax_end;
+}
+
+void merge_cols(Engine::Impl& im, Comm& comm, bool all_ranks) {
+  if (im.opt.merge_mode == 1) merge_cols_dense(im, comm);
+  else merge_cols_shuffle(im, comm, all_ranks);
 }
 
 }  // namespace wc

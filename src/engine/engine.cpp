@@ -59,6 +59,11 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   map_blocks = opt.map_blocks ? opt.map_blocks : 2u * (uint32_t)device_cu_count(dev);
   if (const char* e = std::getenv("WC_ABLATE_MAP")) ablate_map = (uint32_t)std::atoi(e);  // profiling only
   if (const char* e = std::getenv("WC_SYNC_DEBUG")) sync_debug = std::atoi(e) != 0;
+  if (const char* e = std::getenv("WC_MAP_V4")) map_v4 = std::atoi(e) != 0;
+  if (const char* e = std::getenv("WC_MAP_STAMPS"); e && std::atoi(e)) {
+    WC_HIP_CHECK(hipMalloc(&d_stamps, MAP_STAMP_N * 8));
+    WC_HIP_CHECK(hipMemset(d_stamps, 0, MAP_STAMP_N * 8));
+  }
 
   opt.log2_rec_buckets = std::min<uint32_t>(opt.log2_rec_buckets, MAX_REC_BUCKETS_LOG2);
   opt.max_log2_tab_buckets = std::min<uint32_t>(std::max<uint32_t>(opt.max_log2_tab_buckets, 1), 20);
@@ -114,6 +119,17 @@ Engine::Impl::~Impl() {
   if (d_arena) (void)hipFree(d_arena);
   if (d_arena_cursor) (void)hipFree(d_arena_cursor);
   if (d_newkeys) (void)hipFree(d_newkeys);
+  if (d_stamps) {
+    unsigned long long h[MAP_STAMP_N];
+    if (hipMemcpy(h, d_stamps, sizeof h, hipMemcpyDeviceToHost) == hipSuccess && h[MS_TOTAL]) {
+      static const char* names[MAP_STAMP_N] = {"top-barrier", "commit", "mask", "list", "keys",
+                                               "combine",     "retry",  "flush", "total"};
+      fprintf(stderr, "[wc] map phase clock (share of wave lifetime):");
+      for (int i = 0; i < MAP_STAMP_N; ++i) fprintf(stderr, " %s=%.3f", names[i], (double)h[i] / h[MS_TOTAL]);
+      fprintf(stderr, "\n");
+    }
+    (void)hipFree(d_stamps);
+  }
   if (registered) (void)hipHostUnregister(const_cast<uint8_t*>(registered));
   if (s) (void)hipStreamDestroy(s);
   if (copy_s) (void)hipStreamDestroy(copy_s);
@@ -150,8 +166,9 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   pass_rec = rec;
   pass_rec.cursor = &d_ctr->records;
   pass_rec.dir_per_block = dir_per_block_for(len, blocks);
-  MapArgs m{text, len, avail, prev, log2_rb, pass_rec, d_ctr->flags, &d_ctr->tokens, ablate_map};
-  launch_map(m, blocks, s);
+  MapArgs m{text, len, avail, prev, log2_rb, pass_rec, d_ctr->flags, &d_ctr->tokens, ablate_map, d_stamps};
+  if (map_v4) launch_map_v4(m, blocks, s);
+  else launch_map(m, blocks, s);
   if (sync_debug) {  // WC_SYNC_DEBUG: attribute a device fault to a kernel and a chunk
     const hipError_t e = hipStreamSynchronize(s);
     fprintf(stderr, "[wc] map    base=%llu len=%llu avail=%llu blocks=%u J=%u -> %s\n", (unsigned long long)base,
@@ -266,11 +283,15 @@ void Engine::Impl::compact_local() {
   unsigned long long arena_used = 0;
   WC_HIP_CHECK(hipMemcpyAsync(&arena_used, d_arena_cursor, 8, hipMemcpyDeviceToHost, s));
   WC_HIP_CHECK(hipStreamSynchronize(s));
+  std::vector<uint64_t> boff(nb);
   uint64_t n = 0;
-  for (uint32_t o : occ) n += o;
+  for (size_t b = 0; b < nb; ++b) {
+    boff[b] = n;
+    n += occ[b];
+  }
   // columns x2 (sorted copy) + sort scratch + hist
   const size_t per = 5 * 8 + 4;
-  fin_mem.reserve(std::max<size_t>(1 << 20, (n + 1) * per + radix_hist_words(n) * 4 + 64 * 1024));
+  fin_mem.reserve(std::max<size_t>(1 << 20, (n + 1) * per + nb * 8 + radix_hist_words(n) * 4 + 64 * 1024));
   fin_mem.reset();
   cols = KeyCols{};
   cols.k0 = fin_mem.take_n<uint64_t>(n + 1);
@@ -279,9 +300,10 @@ void Engine::Impl::compact_local() {
   cols.first = fin_mem.take_n<uint64_t>(n + 1);
   cols.sref_off = fin_mem.take_n<uint64_t>(n + 1);
   cols.sref_len = fin_mem.take_n<uint32_t>(n + 1);
-  unsigned long long* d_n = fin_mem.take_n<unsigned long long>(1);
-  WC_HIP_CHECK(hipMemsetAsync(d_n, 0, 8, s));
-  launch_table_compact(t, cols.k0, cols.k1, cols.cnt, cols.first, cols.sref_off, cols.sref_len, d_n, s);
+  uint64_t* d_boff = fin_mem.take_n<uint64_t>(nb);
+  WC_HIP_CHECK(hipMemcpyAsync(d_boff, boff.data(), nb * 8, hipMemcpyHostToDevice, s));
+  launch_table_compact(t, d_boff, cols.k0, cols.k1, cols.cnt, cols.first, cols.sref_off, cols.sref_len, s);
+  WC_HIP_CHECK(hipStreamSynchronize(s));  // boff is pageable host memory
   cols.n = n;
   cols_arena = d_arena;
   cols_arena_bytes = std::min<uint64_t>(arena_used, opt.arena_bytes);
@@ -532,14 +554,16 @@ const uint8_t* Engine::synth_device(uint64_t n, uint64_t first_segment, const Sy
   return im.d_text;
 }
 
-uint64_t Engine::finalize_device(Comm* comm) {
-  Impl& im = *p_;
+uint64_t Engine::finalize_device(Comm* comm) { return p_->finalize(comm, false); }
+
+uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
+  Impl& im = *this;
   WC_HIP_CHECK(hipSetDevice(im.dev));
   const double t0 = now_seconds();
   im.compact_local();
   if (comm && comm->size() > 1) {
     const double tm = now_seconds();
-    merge_cols(im, *comm);
+    merge_cols(im, *comm, all_ranks);
     im.st.merge_ms += (now_seconds() - tm) * 1e3;
   }
   im.sort_cols_by_first();
@@ -550,7 +574,7 @@ uint64_t Engine::finalize_device(Comm* comm) {
 
 KeyTable Engine::result(Comm* comm, bool all_ranks) {
   Impl& im = *p_;
-  finalize_device(comm);
+  im.finalize(comm, all_ranks);
   if (comm && comm->size() > 1 && comm->rank() != 0 && !all_ranks) {
     KeyTable t;
     return t;

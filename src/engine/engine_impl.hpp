@@ -46,6 +46,8 @@ struct Engine::Impl {
   uint32_t map_blocks = 0;
   uint32_t ablate_map = 0;  // WC_ABLATE_MAP (profiling ablations, MapArgs::ablate)
   bool sync_debug = false;  // WC_SYNC_DEBUG: sync + log after every kernel
+  bool map_v4 = false;      // WC_MAP_V4: previous map kernel (A/B)
+  unsigned long long* d_stamps = nullptr;  // WC_MAP_STAMPS: map phase clock sums
 
   // shuffle records
   uint64_t rec_total = 0;
@@ -91,6 +93,7 @@ struct Engine::Impl {
   // finalisation workspace
   DeviceArena fin_mem;   // compact output
   DeviceArena merge_mem; // merge buffers (merged columns live here)
+  DeviceArena merge_small;  // merge metadata (count matrices)
   DeviceArena sort_mem;  // first-occurrence sort + sorted columns
   KeyCols cols;        // local (compact) or merged, sorted by first after finalize
   uint8_t* cols_arena = nullptr;   // arena the sref_* of cols point into
@@ -119,13 +122,15 @@ struct Engine::Impl {
   }
   void split_table();
 
+  uint64_t finalize(Comm* comm, bool all_ranks);  // compact [+ merge] + order by first
   void compact_local();                     // table -> cols (unsorted)
   void sort_cols_by_first();                // cols ordered by first occurrence
   KeyTable download_cols();
 };
 
 // Multi-rank merge (dist/merge.cpp): replaces im.cols / cols_arena with the
-// merged global table (identical on every rank).
-void merge_cols(Engine::Impl& im, Comm& comm);
+// merged global table — on rank 0, or on every rank if all_ranks (the dense
+// protocol always leaves it on every rank).
+void merge_cols(Engine::Impl& im, Comm& comm, bool all_ranks);
 
 }  // namespace wc

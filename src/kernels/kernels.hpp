@@ -87,7 +87,10 @@ struct MapArgs {
   uint32_t* flags;
   unsigned long long* tokens;   // += tokens owned by this chunk
   uint32_t ablate;             // profiling: 0 full map; 1 keys only (no combiner); 2 scan only
+  unsigned long long* stamps;  // profiling: per-phase s_memtime sums (MAP_STAMP_N), nullptr = off
 };
+// In-kernel phase stamps of the map (diagnostic build path, WC_MAP_STAMPS=1).
+enum : int { MS_TOP = 0, MS_COMMIT, MS_MASK, MS_LIST, MS_KEYS, MS_COMBINE, MS_RETRY, MS_FLUSH, MS_TOTAL, MAP_STAMP_N };
 
 struct ReduceArgs {
   Records rec;
@@ -115,12 +118,14 @@ struct SynthVocab {
 
 // ---- launchers (all stream-ordered, no host sync) ----------------------------
 void launch_map(const MapArgs& a, uint32_t map_blocks, hipStream_t s);
+void launch_map_v4(const MapArgs& a, uint32_t map_blocks, hipStream_t s);  // A/B baseline
 void launch_reduce(const ReduceArgs& a, hipStream_t s);
 void launch_table_split(const TableView& src, const TableView& dst, hipStream_t s);
 void launch_table_clear(const TableView& t, hipStream_t s);
-// Writes occupied entries densely; out_n receives the count.
-void launch_table_compact(const TableView& t, uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first,
-                          uint64_t* sref_off, uint32_t* sref_len, unsigned long long* out_n, hipStream_t s);
+// Writes occupied entries densely in bucket order; bucket_off[b] = exclusive
+// prefix of the per-bucket occupancy (device array of 2^log2_buckets).
+void launch_table_compact(const TableView& t, const uint64_t* bucket_off, uint64_t* k0, uint64_t* k1, uint64_t* cnt,
+                          uint64_t* first, uint64_t* sref_off, uint32_t* sref_len, hipStream_t s);
 
 // LSD radix sort of (key, value) by the low `bits` bits of key; stable.
 // tmp_* must hold n items; hist must hold radix_hist_words(n) words.
@@ -149,6 +154,27 @@ void launch_union_assign(const uint32_t* pos, const uint32_t* flag, const uint32
                          const uint64_t* K1, const uint64_t* SO, const uint32_t* SL, uint64_t m, uint64_t n_max,
                          uint64_t arena_stride, uint32_t* id_of_pos, uint64_t* ok0, uint64_t* ok1, uint64_t* osoff,
                          uint32_t* oslen, hipStream_t s);
+// ---- shuffle merge (src/kernels/merge.hip) ----
+struct MRow {  // one key row on the wire (40 B)
+  uint64_t k0, k1, cnt, first;
+  uint32_t aoff, alen;  // long word: bytes [aoff, aoff + alen) of the accompanying byte payload
+};
+static_assert(sizeof(MRow) == 40, "MRow layout");
+constexpr uint32_t MERGE_MAX_RANKS = 64;
+void launch_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* slen, uint64_t n, uint32_t W,
+                        unsigned long long* counts, hipStream_t s);
+void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
+                          const uint64_t* soff, const uint32_t* slen, const uint8_t* arena, uint64_t n, uint32_t W,
+                          const unsigned long long* counts, unsigned long long* cursor, MRow* rows, uint8_t* bytes,
+                          hipStream_t s);
+void launch_mrow_insert(const MRow* rows, uint64_t R, uint32_t* state, unsigned long long* cnt,
+                        unsigned long long* first, uint64_t T, hipStream_t s);
+void launch_mrow_compact(const MRow* rows, const uint32_t* state, const unsigned long long* cnt,
+                         const unsigned long long* first, uint64_t T, const uint64_t* rbase, const uint64_t* bbase,
+                         uint32_t W, MRow* out, unsigned long long* out_n, hipStream_t s);
+void launch_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rbase, const uint64_t* bbase, uint32_t W,
+                         uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first, uint64_t* soff, uint32_t* slen,
+                         hipStream_t s);
 void launch_combine_u64(uint64_t* dst, const uint64_t* src, uint64_t n, int op, hipStream_t s);  // 0 sum 1 min 2 max
 void launch_pad_u64(const uint64_t* in, uint64_t n, uint64_t* out, uint64_t m, uint64_t fill, hipStream_t s);
 void launch_exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint64_t m, uint32_t* total, hipStream_t s);

@@ -4,42 +4,64 @@
 // pre-split input record and only copies words the HOST tokenizer
 // (main.cu:181-206) already found.  Here the GPU does the whole map:
 //
-//  1. A persistent grid of ~2 blocks/CU walks 16 KiB text tiles.  Each tile
-//     (+256 B halo) is staged global -> LDS with 16-B loads.
-//  2. Each lane owns 32 bytes and holds a 64-byte register window (its bytes
-//     + the next lane's, four aligned ds_read_b128).  A SWAR packed-byte
-//     compare against {0x20,0x0D,0x0A} gives a 64-bit delimiter mask; token
-//     starts are  ~d & (d << 1 | carry-in)  restricted to the owned 32 bytes,
-//     so a token straddling lanes / tiles / chunks is owned by the unit
-//     holding its FIRST byte.
-//  3. A token that ends inside the window is keyed from registers: k0 by a
-//     funnel shift + mask, and (> 8 bytes) the tail hash one 8-byte chunk at a
-//     time.  Only tokens longer than the window take a byte loop (LDS halo,
-//     then global).
-//  4. Keys are combined in a group-probed LDS hash table (lds_table.hpp): the
-//     MapReduce combiner, kept across tiles while it is sparse, so Zipf text
-//     collapses to one record per hot word per block.  A token that finds no
-//     slot makes the block flush and retry it (no singleton fallback).
-//  5. Flush = shuffle write: occupied slots are counting-sorted by shuffle
+//  1. A persistent grid of 2 blocks/CU walks 16 KiB text tiles.  The next
+//     tile (+256 B halo) is prefetched into registers while the current one is
+//     tokenized, then committed to LDS.
+//  2. Each lane owns 32 bytes and builds a 64-bit delimiter mask over its
+//     bytes and its neighbour's (SWAR zero-byte test against {0x20,0x0D,0x0A}).
+//     Token starts are  ~d & (d << 1 | carry-in)  restricted to the owned 32
+//     bytes, so a token straddling lanes / tiles / chunks / GPU shards is owned
+//     by the unit holding its FIRST byte.
+//  3. Load balance: a wave scan of the per-lane token counts compacts the
+//     wave's tokens into an LDS list of (position, length) entries, and the 64
+//     lanes then take list entries two at a time — every lane keys and combines
+//     the same number of tokens, instead of each lane walking its own (uneven)
+//     tokens while the rest of the wave idles.
+//  4. Keys (keys.hpp) come from two aligned ds_read_b64 per 8 bytes; words
+//     longer than the lane window fall back to a byte loop (LDS halo, then
+//     global memory).
+//  5. Combiner: 2048-slot LDS hash table, 8-slot groups.  A probe reads the
+//     group's eight 32-bit tags (two ds_read_b128) and then only the matching
+//     slot's 16-byte key.  Claims are ONE CAS on the tag (duplicates are
+//     allowed: the reducer merges them), count / first-offset updates are
+//     no-return LDS atomics, occupancy is counted once per wave.
+//  6. A token whose probe sequence is full is marked in a per-tile failure
+//     bitmap; the block flushes and the owning lanes retry those tokens.
+//  7. Flush = shuffle write: occupied slots are counting-sorted by shuffle
 //     bucket (LDS histogram + block scan) and written as ONE contiguous chunk
 //     (coalesced) plus a bucket-offset directory entry; the reducer of bucket
 //     b reads its run of every chunk.
 #include "kernels.hpp"
-#include "lds_table.hpp"
+#include "keys.hpp"
 
 namespace wc {
 namespace dev {
 
-constexpr int MAP_SPT = MAP_SLOTS / MAP_THREADS;  // table slots per thread in a flush
+constexpr int MAP_WAVES = MAP_THREADS / 64;
+constexpr int MAP_LIST = 128;                    // token-list entries per wave per round (2 per lane)
+constexpr int MAP_GS = 8;                        // slots per probe group
+constexpr int MAP_NGROUPS = MAP_SLOTS / MAP_GS;  // 256
+constexpr int MAP_SPT = MAP_SLOTS / MAP_THREADS; // table slots per thread in a flush
+constexpr uint32_t MAP_LONG = 0xFFFFu;           // list entry: token runs past the lane window
 static_assert(MAP_SLOTS % MAP_THREADS == 0, "flush assumes whole slots per thread");
+static_assert(MAP_TILE <= 65536, "list entries hold 16-bit tile positions");
+static_assert((MAP_NGROUPS & (MAP_NGROUPS - 1)) == 0, "group count must be a power of two");
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
 struct MapLds {
-  SlotGroup grp[MAP_GROUPS];  // first: 16-B aligned for the ds_read_b128 group reads
+  u64x2 key[MAP_SLOTS];    // {k0, k1}; k1 = K1_EMPTY after a flush, so a stale key never matches
+  uint32_t tag[MAP_SLOTS];  // group g = tag[8g, 8g+8); 0 = empty
   uint32_t cnt[MAP_SLOTS];
   uint32_t off[MAP_SLOTS];
-  uint32_t boff[MAX_REC_BUCKETS + 4];  // bucket counts -> exclusive offsets (+ total)
+  union {
+    uint32_t list[MAP_WAVES][MAP_LIST];   // token rounds: (tile position | length << 16)
+    uint32_t boff[MAX_REC_BUCKETS + 4];   // flush: bucket counts -> exclusive offsets (+ total)
+  } u;
+  uint32_t fail[MAP_THREADS];  // bit i of word t: token at tile byte 32 t + i must be retried
   uint8_t tile[MAP_TILE + MAP_HALO + 16];  // +16: tile8() reads one word past
-  uint32_t wsum[MAP_THREADS / 64];
+  uint32_t wsum[MAP_WAVES];
   uint32_t occupied;
   uint32_t occ_before, last_new;  // adaptive flush: keys added by the last tile
   uint32_t prev;
@@ -49,6 +71,10 @@ struct MapLds {
   uint64_t flush_base;
   unsigned long long tokens;
 };
+static_assert(sizeof(MapLds) <= 160 * 1024 / 2, "two map blocks must fit one CU's LDS");
+
+__device__ __forceinline__ uint32_t map_tag(uint64_t ph) { return ((uint32_t)ph & ~1u) | 2u; }  // never 0
+__device__ __forceinline__ uint32_t map_group(uint64_t ph) { return (uint32_t)(ph >> 32) & (MAP_NGROUPS - 1); }
 
 // Per-byte "is delimiter" for 8 packed bytes -> 8-bit mask (exact SWAR zero test).
 __device__ __forceinline__ uint64_t delim_mask8(uint64_t x) {
@@ -71,6 +97,12 @@ __device__ __forceinline__ uint64_t low_bytes(uint64_t v, uint32_t n) {
   return n >= 8 ? v : (v & ((1ull << (8 * n)) - 1ull));
 }
 
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Exclusive scan of a[0..n) in place (n <= MAX_REC_BUCKETS); a[n] = total.
 __device__ void block_exclusive_scan(uint32_t* a, uint32_t n, uint32_t* wsum) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -90,7 +122,7 @@ __device__ void block_exclusive_scan(uint32_t* a, uint32_t n, uint32_t* wsum) {
   if (lane == 63) wsum[wave] = x;
   __syncthreads();
   uint32_t before = 0, total = 0;
-  for (int w = 0; w < MAP_THREADS / 64; ++w) {
+  for (int w = 0; w < MAP_WAVES; ++w) {
     before += w < wave ? wsum[w] : 0;
     total += wsum[w];
   }
@@ -105,36 +137,44 @@ __device__ void block_exclusive_scan(uint32_t* a, uint32_t n, uint32_t* wsum) {
   __syncthreads();
 }
 
+__device__ __forceinline__ void clear_slots(MapLds& L) {
+#pragma unroll
+  for (int k = 0; k < MAP_SPT; ++k) {
+    const int s = threadIdx.x + k * MAP_THREADS;
+    L.tag[s] = 0;
+    L.key[s].y = K1_EMPTY;
+    L.cnt[s] = 0;
+    L.off[s] = 0xFFFFFFFFu;
+  }
+}
+
 // Shuffle write of the combiner table: one contiguous bucket-sorted chunk.
 __device__ void flush_table(MapLds& L, const MapArgs& a) {
   const int tid = threadIdx.x;
   const uint32_t nb = 1u << a.log2_rec_buckets;
   if (a.ablate == 5) {  // profiling: clear only
-    for (int s = tid; s < MAP_SLOTS; s += MAP_THREADS) {
-      L.grp[s >> 2].tag[s & 3] = TAG_EMPTY;
-      L.grp[s >> 2].k1[s & 3] = K1_EMPTY;
-    }
+    clear_slots(L);
     __syncthreads();
     if (tid == 0) L.occupied = 0;
     __syncthreads();
     return;
   }
-  for (uint32_t b = tid; b <= nb; b += MAP_THREADS) L.boff[b] = 0;
+  for (uint32_t b = tid; b <= nb; b += MAP_THREADS) L.u.boff[b] = 0;
   __syncthreads();
   uint32_t sb[MAP_SPT], sr[MAP_SPT];
 #pragma unroll
   for (int j = 0; j < MAP_SPT; ++j) {
     const int s = tid + j * MAP_THREADS;
     sb[j] = 0xFFFFFFFFu;
-    const uint32_t tag = slot_tag(L.grp, s);
-    if (tag > TAG_PENDING) {
+    const uint32_t tag = L.tag[s];
+    if (tag != 0) {
       sb[j] = (tag >> 2) & (nb - 1u);  // == bucket_of(place_hash): bucket bits live in the tag
-      sr[j] = atomicAdd(&L.boff[sb[j]], 1u);
+      sr[j] = atomicAdd(&L.u.boff[sb[j]], 1u);
     }
   }
   __syncthreads();
-  block_exclusive_scan(L.boff, nb, L.wsum);
-  const uint32_t n = L.boff[nb];
+  block_exclusive_scan(L.u.boff, nb, L.wsum);
+  const uint32_t n = L.u.boff[nb];
   if (tid == 0) {
     uint32_t ok = 0;
     if (n) {
@@ -160,33 +200,28 @@ __device__ void flush_table(MapLds& L, const MapArgs& a) {
     const size_t row = (size_t)gridDim.x * a.rec.dir_per_block;
     if (a.ablate != 3)
       for (uint32_t b = tid; b <= nb; b += MAP_THREADS)
-        a.rec.dir_off[b * row + (size_t)blockIdx.x * a.rec.dir_per_block + j] = L.boff[b];
+        a.rec.dir_off[b * row + (size_t)blockIdx.x * a.rec.dir_per_block + j] = L.u.boff[b];
     const uint64_t base = L.flush_base;
 #pragma unroll
     for (int k = 0; k < MAP_SPT; ++k) {
       if (sb[k] == 0xFFFFFFFFu) continue;
       const int s = tid + k * MAP_THREADS;
+      const u64x2 kk = L.key[s];
       Rec r;
-      r.k0 = slot_k0(L.grp, s);
-      r.k1 = slot_k1(L.grp, s);
+      r.k0 = kk.x;
+      r.k1 = kk.y;
       r.co = ((uint64_t)L.cnt[s] << 32) | L.off[s];
-      a.rec.recs[base + L.boff[sb[k]] + sr[k]] = r;
+      a.rec.recs[base + L.u.boff[sb[k]] + sr[k]] = r;
     }
   }
-#pragma unroll
-  for (int k = 0; k < MAP_SPT; ++k) {
-    const int s = tid + k * MAP_THREADS;
-    L.grp[s >> 2].tag[s & 3] = TAG_EMPTY;
-    L.grp[s >> 2].k1[s & 3] = K1_EMPTY;
-    L.cnt[s] = 0;
-    L.off[s] = 0xFFFFFFFFu;
-  }
+  __syncthreads();  // boff (aliases the token lists) fully read
+  clear_slots(L);
   __syncthreads();
   if (tid == 0) L.occupied = 0;
   __syncthreads();
 }
 
-// Key of a token that does not end inside the register window.
+// Key of a token that does not end inside the 64-byte lane window.
 __device__ __forceinline__ void key_slow(const MapLds& L, const MapArgs& a, uint64_t pos, uint64_t g, uint64_t& k0,
                                       uint64_t& k1) {
   uint64_t len = 0, h = FNV_OFFSET, chunk = 0;
@@ -212,82 +247,73 @@ __device__ __forceinline__ void key_slow(const MapLds& L, const MapArgs& a, uint
   k1 = make_k1(len, h);
 }
 
-// Key of the token starting at tile position p, given the lane's 64-bit
-// delimiter window mask `rest` shifted to the token start.
-struct TokKey {
-  uint64_t k0, k1, ph;
-  uint32_t off;
-};
-
-__device__ __forceinline__ TokKey token_key(const MapLds& L, const MapArgs& a, uint64_t t0, uint32_t p,
-                                            uint64_t rest) {
-  TokKey t;
-  if (rest != 0) {
-    const uint32_t len = (uint32_t)__ffsll((unsigned long long)rest) - 1;  // ends inside the window
-    t.k0 = low_bytes(tile8(L.tile, p), len);
+// Key of the token at tile position p with known length (< 64) or MAP_LONG.
+__device__ __forceinline__ void token_key(const MapLds& L, const MapArgs& a, uint64_t t0, uint32_t p, uint32_t len,
+                                          uint64_t& k0, uint64_t& k1) {
+  if (len != MAP_LONG) {
+    k0 = low_bytes(tile8(L.tile, p), len);
     if (len <= 8) {
-      t.k1 = len;
+      k1 = len;
     } else {
       uint64_t h = FNV_OFFSET;
       for (uint32_t c = 8; c < len; c += 8) h = tail_fold(h, low_bytes(tile8(L.tile, p + c), len - c));
-      t.k1 = make_k1(len, h);
+      k1 = make_k1(len, h);
     }
   } else {
-    key_slow(L, a, p, t0 + p, t.k0, t.k1);
+    key_slow(L, a, p, t0 + p, k0, k1);
   }
-  t.off = (uint32_t)(t0 + p);
-  t.ph = place_hash(t.k0, t.k1);
-  return t;
 }
 
-// Combiner insert.  The map's table may hold the same key in two slots (each
-// becomes a record and the reducer sums them), so a claim is ONE CAS from
-// EMPTY straight to the final tag; the claimer then writes k0/k1.  A reader
-// that sees the tag before the keys simply does not match (k1 was cleared to
-// 0 at the last flush, so stale keys never match) and probes on — at worst it
-// claims a duplicate slot.  Returns the slot, or -1 if `max_groups` groups
-// were full.
-__device__ __forceinline__ int combiner_slot(SlotGroup* groups, const TokKey& t) {
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-  const uint32_t tag = make_tag(t.ph);
-  uint32_t g = group_of(t.ph, MAP_GROUPS);
+// Combiner slot of (k0, k1) — claiming one if the key is absent — or -1 when
+// MAP_MAX_GROUP_PROBES groups are full.  Claim = ONE CAS of the tag; the
+// claimer then writes k0 before k1 (LDS executes one wave's writes in order,
+// and the reader loads the 16-byte key in one instruction), so a reader that
+// sees the new k1 also sees the new k0; one that sees the tag before the key
+// does not match and may claim a duplicate slot, which the reducer merges.
+__device__ __forceinline__ int combiner_slot(MapLds& L, uint64_t ph, uint64_t k0, uint64_t k1, bool& claimed) {
+  const uint32_t tag = map_tag(ph);
+  uint32_t g = map_group(ph);
+  claimed = false;
   for (int steps = 0; steps < MAP_MAX_GROUP_PROBES;) {
     asm volatile("" ::: "memory");
-    SlotGroup& G = groups[g];
-    const u32x4 tg = *reinterpret_cast<const u32x4*>(G.tag);
-    const u64x2 a1 = *reinterpret_cast<const u64x2*>(&G.k1[0]);
-    const u64x2 b1 = *reinterpret_cast<const u64x2*>(&G.k1[2]);
-    const u64x2 a0 = *reinterpret_cast<const u64x2*>(&G.k0[0]);
-    const u64x2 b0 = *reinterpret_cast<const u64x2*>(&G.k0[2]);
-    const bool h0 = tg.x == tag && a1.x == t.k1 && a0.x == t.k0;
-    const bool h1 = tg.y == tag && a1.y == t.k1 && a0.y == t.k0;
-    const bool h2 = tg.z == tag && b1.x == t.k1 && b0.x == t.k0;
-    const bool h3 = tg.w == tag && b1.y == t.k1 && b0.y == t.k0;
-    if (h0 | h1 | h2 | h3) return 4 * (int)g + (h0 ? 0 : (h1 ? 1 : (h2 ? 2 : 3)));
-    const int e = tg.x == TAG_EMPTY ? 0 : (tg.y == TAG_EMPTY ? 1 : (tg.z == TAG_EMPTY ? 2 : (tg.w == TAG_EMPTY ? 3 : -1)));
-    if (e < 0) {
+    const u32x4 ta = *reinterpret_cast<const u32x4*>(&L.tag[g * MAP_GS]);
+    const u32x4 tb = *reinterpret_cast<const u32x4*>(&L.tag[g * MAP_GS + 4]);
+    uint32_t m = (ta.x == tag ? 1u : 0u) | (ta.y == tag ? 2u : 0u) | (ta.z == tag ? 4u : 0u) |
+                 (ta.w == tag ? 8u : 0u) | (tb.x == tag ? 16u : 0u) | (tb.y == tag ? 32u : 0u) |
+                 (tb.z == tag ? 64u : 0u) | (tb.w == tag ? 128u : 0u);
+    while (m) {
+      const uint32_t i = __ffs(m) - 1;
+      m &= m - 1;
+      const u64x2 kk = L.key[g * MAP_GS + i];
+      if (kk.x == k0 && kk.y == k1) return (int)(g * MAP_GS + i);
+    }
+    const uint32_t e = (ta.x == 0 ? 1u : 0u) | (ta.y == 0 ? 2u : 0u) | (ta.z == 0 ? 4u : 0u) |
+                       (ta.w == 0 ? 8u : 0u) | (tb.x == 0 ? 16u : 0u) | (tb.y == 0 ? 32u : 0u) |
+                       (tb.z == 0 ? 64u : 0u) | (tb.w == 0 ? 128u : 0u);
+    if (!e) {
       ++steps;
-      g = (g + 1) & (MAP_GROUPS - 1);
+      g = (g + 1) & (MAP_NGROUPS - 1);
       continue;
     }
-    if (atomicCAS(&G.tag[e], TAG_EMPTY, tag) == TAG_EMPTY) {
-      G.k0[e] = t.k0;
-      G.k1[e] = t.k1;
-      return 4 * (int)g + e;
+    const uint32_t s = g * MAP_GS + (__ffs(e) - 1);
+    if (atomicCAS(&L.tag[s], 0u, tag) == 0u) {
+      L.key[s].x = k0;
+      asm volatile("" ::: "memory");
+      L.key[s].y = k1;
+      claimed = true;
+      return (int)s;
     }
     // lost the slot to another lane: re-read this group
   }
   return -1;
 }
 
-// Count token t into the combiner; returns false if its neighbourhood is full.
-__device__ __forceinline__ bool combine(MapLds& L, const TokKey& t) {
-  const int s = combiner_slot(L.grp, t);
+// Count one token; false if its probe sequence is full.
+__device__ __forceinline__ bool combine(MapLds& L, uint64_t k0, uint64_t k1, uint32_t off, bool& claimed) {
+  const int s = combiner_slot(L, place_hash(k0, k1), k0, k1, claimed);
   if (s < 0) return false;
-  const uint32_t c = atomicAdd(&L.cnt[s], 1u);
-  atomicMin(&L.off[s], t.off);
-  if (c == 0) atomicAdd(&L.occupied, 1u);
+  atomicAdd(&L.cnt[s], 1u);  // results unused: no-return ds_add / ds_min
+  atomicMin(&L.off[s], off);
   return true;
 }
 
@@ -326,15 +352,30 @@ __device__ __forceinline__ uint4 load16(const MapArgs& a, uint64_t g) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-__global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  // 2 blocks / CU
-  __shared__ MapLds L;
-  const int tid = threadIdx.x;
-  for (int s = tid; s < MAP_SLOTS; s += MAP_THREADS) {
-    L.grp[s >> 2].tag[s & 3] = TAG_EMPTY;
-    L.grp[s >> 2].k1[s & 3] = K1_EMPTY;
-    L.cnt[s] = 0;
-    L.off[s] = 0xFFFFFFFFu;
+// Phase clock for the diagnostic build (ST = true): accumulates s_memtime
+// deltas per wave; the real kernel (ST = false) compiles it away.
+template <bool ST>
+struct PhaseClock {
+  uint64_t acc[MAP_STAMP_N] = {};
+  uint64_t t = 0;
+  __device__ __forceinline__ void start() {
+    if (ST) t = __builtin_amdgcn_s_memtime();
   }
+  __device__ __forceinline__ void lap(int phase) {
+    if (ST) {
+      const uint64_t n = __builtin_amdgcn_s_memtime();
+      acc[phase] += n - t;
+      t = n;
+    }
+  }
+};
+
+template <bool ST>
+__global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  // 2nd arg: waves per SIMD (2 blocks / CU)
+  __shared__ MapLds L;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  clear_slots(L);
+  L.fail[tid] = 0;
   if (tid == 0) {
     L.occupied = 0;
     L.last_new = 0;
@@ -359,14 +400,19 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
     if (tid == 0) pprev = (t0 == 0 && a.prev_byte >= 0) ? (uint32_t)a.prev_byte : a.text[(int64_t)t0 - 1];
   };
   prefetch(blockIdx.x);
+  PhaseClock<ST> clk;
+  clk.start();
+  const uint64_t t_begin = clk.t;
 
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const uint64_t t0 = tile * MAP_TILE;
     __syncthreads();  // previous tile fully consumed
+    clk.lap(MS_TOP);
     // Flush only if the keys the last tile added would not fit again: Zipf
     // text with a small vocabulary keeps its table across many tiles, large
     // vocabularies flush before every tile instead of overflowing mid-tile.
     if (L.occupied + L.last_new > MAP_FILL_MAX) flush_table(L, a);
+    clk.lap(MS_FLUSH);
     if (tid == 0) L.occ_before = L.occupied;
     // ---- commit the prefetched tile to LDS, start loading the next ----
     reinterpret_cast<uint4*>(&L.tile[tid * MAP_BPL])[0] = p0;
@@ -375,6 +421,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
     if (tid == 0) L.prev = pprev;
     __syncthreads();
     prefetch(tile + gridDim.x);
+    clk.lap(MS_COMMIT);
 
     // ---- 64-byte window (own 32 B + next lane's), delimiter / start masks ----
     uint64_t dm = 0;
@@ -392,45 +439,108 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
     } else if (lane_base + MAP_BPL > a.chunk_len) {
       starts &= (1u << (uint32_t)(a.chunk_len - lane_base)) - 1u;
     }
-    my_tokens += __popc(starts);
+    const uint32_t ntok = __popc(starts);
+    my_tokens += ntok;
+    clk.lap(MS_MASK);
     if (a.ablate == 2) {
       sink ^= dm;
       continue;
     }
 
-    // ---- tokens: two per iteration so their LDS round trips overlap ----
-    const uint32_t pbase = tid * MAP_BPL;
-    uint32_t todo = starts;
-    for (;;) {
-      uint32_t failed = 0;
-      while (todo) {
-        const uint32_t i1 = __ffs(todo) - 1;
-        todo &= todo - 1;
-        const bool two = todo != 0;
-        const uint32_t i2 = two ? (uint32_t)__ffs(todo) - 1 : i1;
-        todo &= two ? todo - 1 : todo;
-        const TokKey ta = token_key(L, a, t0, pbase + i1, dm >> i1);
-        const TokKey tb = token_key(L, a, t0, pbase + i2, dm >> i2);
-        if (a.ablate == 1) {
-          sink ^= ta.ph + tb.ph;
-          continue;
-        }
-        if (!combine(L, ta)) failed |= 1u << i1;
-        if (two && !combine(L, tb)) failed |= 1u << i2;
-      }
-      todo = failed;
-      if (!__syncthreads_or(todo != 0)) break;
-      flush_table(L, a);  // neighbourhood full: flush, then retry those tokens
+    // ---- compact the wave's tokens into list rounds of MAP_LIST entries ----
+    uint32_t incl = ntok;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
     }
+    const uint32_t wave_total = __shfl(incl, 63), excl = incl - ntok;
+    const uint32_t pbase = tid * MAP_BPL;
+    uint32_t* list = L.u.list[wave];
+    bool any_fail = false;
+    uint32_t bits = starts, k = excl;  // this lane's next token and its wave index
+    for (uint32_t base = 0; base < wave_total; base += MAP_LIST) {
+      const uint32_t lim = base + MAP_LIST;
+      while (bits && k < lim) {
+        const uint32_t i = __ffs(bits) - 1;
+        bits &= bits - 1;
+        const uint64_t rest = dm >> i;
+        const uint32_t len = rest ? (uint32_t)__ffsll((unsigned long long)rest) - 1 : MAP_LONG;
+        list[k - base] = (pbase + i) | (len << 16);
+        ++k;
+      }
+      wave_sync();
+      clk.lap(MS_LIST);
+      const uint32_t n = min(wave_total - base, (uint32_t)MAP_LIST);
+      const bool h1 = (uint32_t)lane < n, h2 = (uint32_t)lane + 64 < n;
+      const uint32_t e1 = h1 ? list[lane] : 0u, e2 = h2 ? list[lane + 64] : 0u;
+      wave_sync();  // entries read before the next round overwrites them
+      const uint32_t q1 = e1 & 0xFFFFu, q2 = e2 & 0xFFFFu;
+      uint64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+      if (h1) token_key(L, a, t0, q1, e1 >> 16, a0, a1);
+      if (h2) token_key(L, a, t0, q2, e2 >> 16, b0, b1);
+      if (ST) {  // force the keys before the keys/combine boundary stamp
+        asm volatile("" ::"v"(a0), "v"(a1), "v"(b0), "v"(b1));
+      }
+      clk.lap(MS_KEYS);
+      if (a.ablate == 1) {
+        sink ^= place_hash(a0, a1) + place_hash(b0, b1);
+        continue;
+      }
+      bool c1 = false, c2 = false;
+      if (h1 && !combine(L, a0, a1, (uint32_t)(t0 + q1), c1)) {
+        atomicOr(&L.fail[q1 >> 5], 1u << (q1 & 31));
+        any_fail = true;
+      }
+      if (h2 && !combine(L, b0, b1, (uint32_t)(t0 + q2), c2)) {
+        atomicOr(&L.fail[q2 >> 5], 1u << (q2 & 31));
+        any_fail = true;
+      }
+      const uint32_t claims = (uint32_t)__popcll(__ballot(c1)) + (uint32_t)__popcll(__ballot(c2));
+      if (lane == 0 && claims) atomicAdd(&L.occupied, claims);
+      clk.lap(MS_COMBINE);
+    }
+
+    // ---- probe sequences that were full: flush, then the owners retry ----
+    while (__syncthreads_or(any_fail)) {
+      clk.lap(MS_RETRY);
+      flush_table(L, a);
+      clk.lap(MS_FLUSH);
+      uint32_t todo = L.fail[tid];
+      L.fail[tid] = 0;
+      any_fail = false;
+      uint32_t claims = 0;
+      while (todo) {
+        const uint32_t i = __ffs(todo) - 1;
+        todo &= todo - 1;
+        const uint64_t rest = dm >> i;
+        const uint32_t len = rest ? (uint32_t)__ffsll((unsigned long long)rest) - 1 : MAP_LONG;
+        uint64_t k0, k1;
+        token_key(L, a, t0, pbase + i, len, k0, k1);
+        bool c = false;
+        if (!combine(L, k0, k1, (uint32_t)(t0 + pbase + i), c)) {
+          atomicOr(&L.fail[tid], 1u << i);
+          any_fail = true;
+        }
+        claims += c;
+      }
+      if (claims) atomicAdd(&L.occupied, claims);
+    }
+    clk.lap(MS_RETRY);
     if (tid == 0) L.last_new = L.occupied > L.occ_before ? L.occupied - L.occ_before : L.occupied;
   }
   __syncthreads();
+  clk.lap(MS_TOP);
   if (L.occupied) flush_table(L, a);
+  clk.lap(MS_FLUSH);
+  if (ST && lane == 0) {
+    clk.acc[MS_TOTAL] = clk.t - t_begin;
+    for (int i = 0; i < MAP_STAMP_N; ++i) atomicAdd(&a.stamps[i], (unsigned long long)clk.acc[i]);
+  }
 
   // block totals -> one global atomic
   uint64_t t = my_tokens;
   for (int o = 32; o > 0; o >>= 1) t += __shfl_down(t, o);
-  if ((tid & 63) == 0) atomicAdd(&L.tokens, (unsigned long long)t);
+  if (lane == 0) atomicAdd(&L.tokens, (unsigned long long)t);
   if (sink == 0x9E3779B97F4A7C15ull) atomicOr(&a.flags[FLAG_COUNT - 1], 0u);  // never true
   __syncthreads();
   if (tid == 0) {
@@ -443,7 +553,8 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
 }  // namespace dev
 
 void launch_map(const MapArgs& a, uint32_t map_blocks, hipStream_t s) {
-  hipLaunchKernelGGL(dev::wc_map_tokenize, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a);
+  if (a.stamps) hipLaunchKernelGGL(dev::wc_map_tokenize<true>, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a);
+  else hipLaunchKernelGGL(dev::wc_map_tokenize<false>, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a);
 }
 
 }  // namespace wc

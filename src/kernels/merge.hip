@@ -1,7 +1,17 @@
-// merge.hip — device kernels of the cross-GPU merge protocol:
-// dictionary-union head flags, global-id assignment, dense combine, and a
-// single-block exclusive scan.
+// merge.hip — device kernels of the cross-GPU merge protocols.
+//
+// Shuffle merge (default): every key goes to its owner rank (high bits of the
+// placement hash) — owner partition + pack (wc_owner_count / wc_owner_scatter),
+// RCCL all-to-all, owner-side merge in a global open-addressing table whose
+// slots are claimed by the row id of the first inserter (wc_mrow_insert: keys are
+// read from the immutable received rows, so no key publication race), owner
+// compaction (wc_mrow_compact), and rank-0 conversion to key columns
+// (wc_mrow_to_cols).
+//
+// Dense merge (merge_mode 1): dictionary-union head flags, global-id
+// assignment, dense combine, and a single-block exclusive scan.
 #include "kernels.hpp"
+#include "keys.hpp"
 #include "lds_table.hpp"
 
 namespace wc {
@@ -93,7 +103,205 @@ __global__ void __launch_bounds__(1024) wc_exclusive_scan_u32(const uint32_t* in
   if (threadIdx.x == 0) *total = carry;
 }
 
+constexpr int OWN_MAX = 64;       // ranks supported by the shuffle merge
+constexpr int OWN_ROWS_PER_BLOCK = 1024;
+
+__device__ __forceinline__ uint32_t owner_of(uint64_t ph, uint32_t W) {
+  return (uint32_t)(((ph >> 32) * (uint64_t)W) >> 32);  // high hash bits (bucket bits are low)
+}
+
+// counts[2o] += rows owned by o, counts[2o+1] += their long-word bytes.
+__global__ void __launch_bounds__(256) wc_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* slen,
+                                                      uint64_t n, uint32_t W, unsigned long long* counts) {
+  __shared__ unsigned long long h[2 * OWN_MAX];
+  for (uint32_t i = threadIdx.x; i < 2 * W; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t o = owner_of(place_hash(k0[i], k1[i]), W);
+    atomicAdd(&h[2 * o], 1ull);
+    if (!key_is_short(k1[i])) atomicAdd(&h[2 * o + 1], (unsigned long long)slen[i]);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 2 * W; i += blockDim.x)
+    if (h[i]) atomicAdd(&counts[i], h[i]);
+}
+
+// Pack rows (and long-word bytes) contiguously by owner.  Each block reserves
+// one range per owner (one global atomic per owner per block), then places its
+// rows with LDS atomics.  counts = wc_owner_count output; cursor zeroed.
+__global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt,
+                                                        const uint64_t* first, const uint64_t* soff,
+                                                        const uint32_t* slen, const uint8_t* arena, uint64_t n,
+                                                        uint32_t W, const unsigned long long* counts,
+                                                        unsigned long long* cursor, MRow* rows, uint8_t* bytes) {
+  __shared__ unsigned long long base[2 * OWN_MAX], h[2 * OWN_MAX];
+  constexpr int PER = OWN_ROWS_PER_BLOCK / 256;
+  const uint64_t r0 = (uint64_t)blockIdx.x * OWN_ROWS_PER_BLOCK;
+  for (uint32_t i = threadIdx.x; i < 2 * W; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  uint32_t own[PER];
+  unsigned long long lr[PER], lb[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint64_t i = r0 + threadIdx.x + (uint64_t)j * 256;
+    own[j] = OWN_MAX;
+    if (i < n) {
+      own[j] = owner_of(place_hash(k0[i], k1[i]), W);
+      lr[j] = atomicAdd(&h[2 * own[j]], 1ull);
+      lb[j] = key_is_short(k1[i]) ? 0 : atomicAdd(&h[2 * own[j] + 1], (unsigned long long)slen[i]);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long br = 0, bb = 0;  // exclusive prefix of the global per-owner totals
+    for (uint32_t o = 0; o < W; ++o) {
+      base[2 * o] = br + (h[2 * o] ? atomicAdd(&cursor[2 * o], h[2 * o]) : 0);
+      base[2 * o + 1] = bb + (h[2 * o + 1] ? atomicAdd(&cursor[2 * o + 1], h[2 * o + 1]) : 0);
+      br += counts[2 * o];
+      bb += counts[2 * o + 1];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    if (own[j] == OWN_MAX) continue;
+    const uint64_t i = r0 + threadIdx.x + (uint64_t)j * 256;
+    const uint32_t o = own[j];
+    MRow r;
+    r.k0 = k0[i];
+    r.k1 = k1[i];
+    r.cnt = cnt[i];
+    r.first = first[i];
+    r.aoff = 0;
+    r.alen = 0;
+    if (!key_is_short(r.k1)) {
+      const unsigned long long bpos = base[2 * o + 1] + lb[j];
+      for (uint32_t b = 0; b < slen[i]; ++b) bytes[bpos + b] = arena[soff[i] + b];
+      unsigned long long bb = 0;  // offset inside owner o's byte payload
+      for (uint32_t q = 0; q < o; ++q) bb += counts[2 * q + 1];
+      r.aoff = (uint32_t)(bpos - bb);
+      r.alen = slen[i];
+    }
+    rows[base[2 * o] + lr[j]] = r;
+  }
+}
+
+// Owner-side merge: a slot belongs to the first row that CAS-es its id in;
+// later rows of the same key compare against that row (immutable input) and add
+// their counts with device-scope atomics.  T is a power of two >= 2 R.
+__global__ void __launch_bounds__(256) wc_mrow_insert(const MRow* rows, uint64_t R, uint32_t* state,
+                                                      unsigned long long* cnt, unsigned long long* first, uint64_t T) {
+  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < R; r += (uint64_t)gridDim.x * blockDim.x) {
+    const MRow me = rows[r];
+    uint64_t slot = place_hash(me.k0, me.k1) & (T - 1);
+    for (;;) {
+      uint32_t s = __hip_atomic_load(&state[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (s == 0) {
+        s = atomicCAS(&state[slot], 0u, (uint32_t)r + 1u);
+        if (s == 0) break;  // claimed
+      }
+      const MRow& o = rows[s - 1];
+      if (o.k0 == me.k0 && o.k1 == me.k1) break;  // same key
+      slot = (slot + 1) & (T - 1);
+    }
+    atomicAdd(&cnt[slot], (unsigned long long)me.cnt);
+    atomicMin(&first[slot], (unsigned long long)me.first);
+  }
+}
+
+// Occupied slots -> merged rows; aoff becomes absolute in the received byte
+// buffer (rbase/bbase: exclusive prefixes of rows / bytes received per source).
+__global__ void __launch_bounds__(1024) wc_mrow_compact(const MRow* rows, const uint32_t* state,
+                                                        const unsigned long long* cnt,
+                                                        const unsigned long long* first, uint64_t T,
+                                                        const uint64_t* rbase, const uint64_t* bbase, uint32_t W,
+                                                        MRow* out, unsigned long long* out_n) {
+  __shared__ unsigned long long blk;
+  __shared__ uint32_t bcount;
+  constexpr int PER = 16;
+  const uint64_t s0 = (uint64_t)blockIdx.x * 1024 * PER;
+  if (threadIdx.x == 0) bcount = 0;
+  __syncthreads();
+  uint32_t mine = 0, local[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint64_t sl = s0 + threadIdx.x + (uint64_t)j * 1024;
+    local[j] = 0xFFFFFFFFu;
+    if (sl < T && state[sl]) {
+      local[j] = atomicAdd(&bcount, 1u);
+      ++mine;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) blk = bcount ? atomicAdd(out_n, (unsigned long long)bcount) : 0;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    if (local[j] == 0xFFFFFFFFu) continue;
+    const uint64_t sl = s0 + threadIdx.x + (uint64_t)j * 1024;
+    const uint64_t r = state[sl] - 1u;
+    uint32_t src = 0;
+    while (src + 1 < W && rbase[src + 1] <= r) ++src;
+    MRow m = rows[r];
+    m.cnt = cnt[sl];
+    m.first = first[sl];
+    if (m.alen) m.aoff = (uint32_t)(bbase[src] + m.aoff);
+    out[blk + local[j]] = m;
+  }
+  (void)mine;
+}
+
+// Gathered merged rows (grouped by owner) -> key columns; sref_off is made
+// absolute in the gathered byte buffer.
+__global__ void wc_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rbase, const uint64_t* bbase,
+                                uint32_t W, uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first,
+                                uint64_t* soff, uint32_t* slen) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t o = 0;
+    while (o + 1 < W && rbase[o + 1] <= i) ++o;
+    const MRow m = rows[i];
+    k0[i] = m.k0;
+    k1[i] = m.k1;
+    cnt[i] = m.cnt;
+    first[i] = m.first;
+    soff[i] = m.alen ? bbase[o] + m.aoff : 0;
+    slen[i] = m.alen;
+  }
+}
+
 }  // namespace dev
+
+void launch_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* slen, uint64_t n, uint32_t W,
+                        unsigned long long* counts, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(dev::wc_owner_count, dev::mgrid(n), dim3(256), 0, s, k0, k1, slen, n, W, counts);
+}
+void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
+                          const uint64_t* soff, const uint32_t* slen, const uint8_t* arena, uint64_t n, uint32_t W,
+                          const unsigned long long* counts, unsigned long long* cursor, MRow* rows, uint8_t* bytes,
+                          hipStream_t s) {
+  const uint64_t blocks = (n + dev::OWN_ROWS_PER_BLOCK - 1) / dev::OWN_ROWS_PER_BLOCK;
+  if (n)
+    hipLaunchKernelGGL(dev::wc_owner_scatter, dim3((unsigned)blocks), dim3(256), 0, s, k0, k1, cnt, first, soff, slen,
+                       arena, n, W, counts, cursor, rows, bytes);
+}
+void launch_mrow_insert(const MRow* rows, uint64_t R, uint32_t* state, unsigned long long* cnt,
+                        unsigned long long* first, uint64_t T, hipStream_t s) {
+  if (R) hipLaunchKernelGGL(dev::wc_mrow_insert, dev::mgrid(R), dim3(256), 0, s, rows, R, state, cnt, first, T);
+}
+void launch_mrow_compact(const MRow* rows, const uint32_t* state, const unsigned long long* cnt,
+                         const unsigned long long* first, uint64_t T, const uint64_t* rbase, const uint64_t* bbase,
+                         uint32_t W, MRow* out, unsigned long long* out_n, hipStream_t s) {
+  const uint64_t blocks = (T + 1024 * 16 - 1) / (1024 * 16);
+  hipLaunchKernelGGL(dev::wc_mrow_compact, dim3((unsigned)blocks), dim3(1024), 0, s, rows, state, cnt, first, T, rbase,
+                     bbase, W, out, out_n);
+}
+void launch_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rbase, const uint64_t* bbase, uint32_t W,
+                         uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first, uint64_t* soff, uint32_t* slen,
+                         hipStream_t s) {
+  if (n)
+    hipLaunchKernelGGL(dev::wc_mrow_to_cols, dev::mgrid(n), dim3(256), 0, s, rows, n, rbase, bbase, W, k0, k1, cnt,
+                       first, soff, slen);
+}
 
 void launch_union_flags(const uint32_t* pos, const uint64_t* K0, const uint64_t* K1, uint32_t* flag, uint64_t m,
                         hipStream_t s) {

@@ -15,7 +15,7 @@
 //                     If a slice overflows it is NOT written back; the host
 //                     splits the table and re-runs only the overflowed buckets.
 //  wc_table_split     B -> 2B buckets (rehash into new slices).
-//  wc_table_compact   occupied slots -> dense columns (wave-aggregated atomics).
+//  wc_table_compact   occupied slots -> dense columns (per-bucket block scan).
 #include "kernels.hpp"
 #include "lds_table.hpp"
 
@@ -250,25 +250,45 @@ __global__ void wc_table_clear(TableView t, size_t n) {
   }
 }
 
-__global__ void wc_table_compact(TableView t, size_t n, uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first,
-                                 uint64_t* sref_off, uint32_t* sref_len, unsigned long long* out_n) {
-  for (size_t base = blockIdx.x * (size_t)blockDim.x; base < n; base += (size_t)gridDim.x * blockDim.x) {
-    const size_t i = base + threadIdx.x;
-    const bool occ = i < n && t.k1[i] != K1_EMPTY;
-    uint32_t total;
-    const uint32_t r = wave_rank(occ, total);
-    unsigned long long w0 = 0;
-    if (lane_id() == 0 && total) w0 = atomicAdd(out_n, (unsigned long long)total);
-    w0 = __shfl(w0, 0);
-    if (occ) {
-      const size_t o = w0 + r;
-      k0[o] = t.k0[i];
-      k1[o] = t.k1[i];
-      cnt[o] = t.cnt[i];
-      first[o] = t.first[i];
-      sref_off[o] = t.sref_off[i];
-      sref_len[o] = t.sref_len[i];
-    }
+// One 1024-thread block per bucket: thread t owns slots [4t, 4t+4) of the
+// slice; a block scan of the occupied counts places them at bucket_off[b] + rank
+// (bucket order, slot order inside a bucket).  No global atomics: the previous
+// one-counter-per-wave form serialised ~16k waves on one address (~200 us).
+__global__ void __launch_bounds__(1024) wc_table_compact(TableView t, const uint64_t* bucket_off, uint64_t* k0,
+                                                         uint64_t* k1, uint64_t* cnt, uint64_t* first,
+                                                         uint64_t* sref_off, uint32_t* sref_len) {
+  static_assert(TAB_SLOTS == 4 * 1024, "compact: 4 slots per thread");
+  __shared__ uint32_t wsum[16];
+  const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const size_t base = (size_t)b * TAB_SLOTS + 4 * tid;
+  uint64_t kk1[4];
+  uint32_t n = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    kk1[j] = t.k1[base + j];
+    n += kk1[j] != K1_EMPTY;
+  }
+  uint32_t incl = n;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  uint32_t before = 0;
+  for (uint32_t w = 0; w < wave; ++w) before += wsum[w];
+  uint64_t o = bucket_off[b] + before + incl - n;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (kk1[j] == K1_EMPTY) continue;
+    const size_t i = base + j;
+    k0[o] = t.k0[i];
+    k1[o] = kk1[j];
+    cnt[o] = t.cnt[i];
+    first[o] = t.first[i];
+    sref_off[o] = t.sref_off[i];
+    sref_len[o] = t.sref_len[i];
+    ++o;
   }
 }
 
@@ -287,11 +307,10 @@ void launch_table_clear(const TableView& t, hipStream_t s) {
   hipLaunchKernelGGL(dev::wc_table_clear, dim3(1024), dim3(256), 0, s, t, n);
 }
 
-void launch_table_compact(const TableView& t, uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first,
-                          uint64_t* sref_off, uint32_t* sref_len, unsigned long long* out_n, hipStream_t s) {
-  const size_t n = ((size_t)1 << t.log2_buckets) * TAB_SLOTS;
-  hipLaunchKernelGGL(dev::wc_table_compact, dim3(1024), dim3(256), 0, s, t, n, k0, k1, cnt, first, sref_off,
-                     sref_len, out_n);
+void launch_table_compact(const TableView& t, const uint64_t* bucket_off, uint64_t* k0, uint64_t* k1, uint64_t* cnt,
+                          uint64_t* first, uint64_t* sref_off, uint32_t* sref_len, hipStream_t s) {
+  hipLaunchKernelGGL(dev::wc_table_compact, dim3(1u << t.log2_buckets), dim3(1024), 0, s, t, bucket_off, k0, k1, cnt,
+                     first, sref_off, sref_len);
 }
 
 }  // namespace wc
