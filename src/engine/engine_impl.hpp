@@ -46,7 +46,6 @@ struct Engine::Impl {
   uint32_t map_blocks = 0;
   uint32_t ablate_map = 0;  // WC_ABLATE_MAP (profiling ablations, MapArgs::ablate)
   bool sync_debug = false;  // WC_SYNC_DEBUG: sync + log after every kernel
-  bool map_v4 = false;      // WC_MAP_V4: previous map kernel (A/B)
   unsigned long long* d_stamps = nullptr;  // WC_MAP_STAMPS: map phase clock sums
 
   // shuffle records

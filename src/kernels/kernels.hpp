@@ -16,11 +16,12 @@
 namespace wc {
 
 // ---- geometry (gfx950: wave64, 256 CUs, 160 KiB LDS per CU) -------------------
-constexpr int MAP_THREADS = 512;                     // 8 waves
+constexpr int MAP_THREADS = 1024;                    // 16 waves, one block per CU
+constexpr int MAP_BLOCKS_PER_CU = 1;
 constexpr int MAP_BPL = 32;                          // text bytes per lane
-constexpr int MAP_TILE = MAP_THREADS * MAP_BPL;      // 16 KiB LDS text tile
+constexpr int MAP_TILE = MAP_THREADS * MAP_BPL;      // 32 KiB LDS text tile
 constexpr int MAP_HALO = 256;                        // bytes past the tile kept in LDS
-constexpr int MAP_SLOTS = 2048;                      // LDS combiner slots (groups of 4)
+constexpr int MAP_SLOTS = 4096;                      // LDS combiner slots (groups of 8)
 constexpr int MAP_GROUPS = MAP_SLOTS / 4;
 constexpr int MAP_FILL_MAX = MAP_SLOTS * 3 / 4;      // adaptive flush: target max fill
 constexpr int MAP_MAX_GROUP_PROBES = 8;              // then flush and retry the token
@@ -90,7 +91,7 @@ struct MapArgs {
   unsigned long long* stamps;  // profiling: per-phase s_memtime sums (MAP_STAMP_N), nullptr = off
 };
 // In-kernel phase stamps of the map (diagnostic build path, WC_MAP_STAMPS=1).
-enum : int { MS_TOP = 0, MS_COMMIT, MS_MASK, MS_LIST, MS_KEYS, MS_COMBINE, MS_RETRY, MS_FLUSH, MS_TOTAL, MAP_STAMP_N };
+enum : int { MS_TOP = 0, MS_COMMIT, MS_MASK, MS_LIST, MS_KEYS, MS_COMBINE, MS_RETRY, MS_FLUSH, MS_BARRIER, MS_TOTAL, MAP_STAMP_N };
 
 struct ReduceArgs {
   Records rec;
@@ -118,7 +119,6 @@ struct SynthVocab {
 
 // ---- launchers (all stream-ordered, no host sync) ----------------------------
 void launch_map(const MapArgs& a, uint32_t map_blocks, hipStream_t s);
-void launch_map_v4(const MapArgs& a, uint32_t map_blocks, hipStream_t s);  // A/B baseline
 void launch_reduce(const ReduceArgs& a, hipStream_t s);
 void launch_table_split(const TableView& src, const TableView& dst, hipStream_t s);
 void launch_table_clear(const TableView& t, hipStream_t s);

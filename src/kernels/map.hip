@@ -55,10 +55,8 @@ struct MapLds {
   uint32_t tag[MAP_SLOTS];  // group g = tag[8g, 8g+8); 0 = empty
   uint32_t cnt[MAP_SLOTS];
   uint32_t off[MAP_SLOTS];
-  union {
-    uint32_t list[MAP_WAVES][MAP_LIST];   // token rounds: (tile position | length << 16)
-    uint32_t boff[MAX_REC_BUCKETS + 4];   // flush: bucket counts -> exclusive offsets (+ total)
-  } u;
+  uint32_t list[MAP_WAVES][MAP_LIST];  // token rounds: (tile position | length << 16)
+  uint32_t boff[MAX_REC_BUCKETS + 4];  // flush: bucket counts -> exclusive offsets (+ total); 0 between flushes
   uint32_t fail[MAP_THREADS];  // bit i of word t: token at tile byte 32 t + i must be retried
   uint8_t tile[MAP_TILE + MAP_HALO + 16];  // +16: tile8() reads one word past
   uint32_t wsum[MAP_WAVES];
@@ -71,7 +69,7 @@ struct MapLds {
   uint64_t flush_base;
   unsigned long long tokens;
 };
-static_assert(sizeof(MapLds) <= 160 * 1024 / 2, "two map blocks must fit one CU's LDS");
+static_assert(sizeof(MapLds) <= 160 * 1024 / MAP_BLOCKS_PER_CU, "map blocks per CU must fit its LDS");
 
 __device__ __forceinline__ uint32_t map_tag(uint64_t ph) { return ((uint32_t)ph & ~1u) | 2u; }  // never 0
 __device__ __forceinline__ uint32_t map_group(uint64_t ph) { return (uint32_t)(ph >> 32) & (MAP_NGROUPS - 1); }
@@ -103,40 +101,6 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Exclusive scan of a[0..n) in place (n <= MAX_REC_BUCKETS); a[n] = total.
-__device__ void block_exclusive_scan(uint32_t* a, uint32_t n, uint32_t* wsum) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr int PER = (MAX_REC_BUCKETS + MAP_THREADS - 1) / MAP_THREADS;
-  uint32_t v[PER], s = 0;
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const uint32_t i = tid * PER + k;
-    v[k] = i < n ? a[i] : 0;
-    s += v[k];
-  }
-  uint32_t x = s;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) wsum[wave] = x;
-  __syncthreads();
-  uint32_t before = 0, total = 0;
-  for (int w = 0; w < MAP_WAVES; ++w) {
-    before += w < wave ? wsum[w] : 0;
-    total += wsum[w];
-  }
-  uint32_t run = before + x - s;
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const uint32_t i = tid * PER + k;
-    if (i < n) a[i] = run;
-    run += v[k];
-  }
-  if (tid == 0) a[n] = total;
-  __syncthreads();
-}
-
 __device__ __forceinline__ void clear_slots(MapLds& L) {
 #pragma unroll
   for (int k = 0; k < MAP_SPT; ++k) {
@@ -149,76 +113,89 @@ __device__ __forceinline__ void clear_slots(MapLds& L) {
 }
 
 // Shuffle write of the combiner table: one contiguous bucket-sorted chunk.
-__device__ void flush_table(MapLds& L, const MapArgs& a) {
-  const int tid = threadIdx.x;
+// Four block barriers: bucket histogram | wave sums of the scan | offsets +
+// region | records written (then the histogram is re-zeroed).  trailing_sync
+// adds a fifth when inserts follow immediately (retry path).
+__device__ void flush_table(MapLds& L, const MapArgs& a, bool trailing_sync) {
+  static_assert(MAX_REC_BUCKETS < MAP_THREADS, "one bucket per thread in the scan");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t nb = 1u << a.log2_rec_buckets;
-  if (a.ablate == 5) {  // profiling: clear only
-    clear_slots(L);
-    __syncthreads();
-    if (tid == 0) L.occupied = 0;
-    __syncthreads();
-    return;
-  }
-  for (uint32_t b = tid; b <= nb; b += MAP_THREADS) L.u.boff[b] = 0;
-  __syncthreads();
   uint32_t sb[MAP_SPT], sr[MAP_SPT];
+  if (a.ablate != 5) {  // 5 (profiling): flush = clear only
 #pragma unroll
-  for (int j = 0; j < MAP_SPT; ++j) {
-    const int s = tid + j * MAP_THREADS;
-    sb[j] = 0xFFFFFFFFu;
-    const uint32_t tag = L.tag[s];
-    if (tag != 0) {
-      sb[j] = (tag >> 2) & (nb - 1u);  // == bucket_of(place_hash): bucket bits live in the tag
-      sr[j] = atomicAdd(&L.u.boff[sb[j]], 1u);
-    }
-  }
-  __syncthreads();
-  block_exclusive_scan(L.u.boff, nb, L.wsum);
-  const uint32_t n = L.u.boff[nb];
-  if (tid == 0) {
-    uint32_t ok = 0;
-    if (n) {
-      // block-private record region: no global cursor contention
-      const uint64_t region = a.rec.cap / gridDim.x;
-      const uint64_t base = (uint64_t)blockIdx.x * region + L.used;
-      const uint32_t j = L.nflush;
-      ok = (L.used + n <= region && j < a.rec.dir_per_block) ? 1u : 0u;
-      L.used += n;
-      if (ok) {
-        L.nflush = j + 1;
-        a.rec.dir_base[(size_t)blockIdx.x * a.rec.dir_per_block + j] = base;
-      } else {
-        atomicOr(&a.flags[FLAG_REGION_OVF], 1u);
+    for (int j = 0; j < MAP_SPT; ++j) {
+      const int s = tid + j * MAP_THREADS;
+      sb[j] = 0xFFFFFFFFu;
+      const uint32_t tag = L.tag[s];
+      if (tag != 0) {
+        sb[j] = (tag >> 2) & (nb - 1u);  // == bucket_of(place_hash): bucket bits live in the tag
+        sr[j] = atomicAdd(&L.boff[sb[j]], 1u);
       }
-      L.flush_base = base;
     }
-    L.flush_ok = ok;
-  }
-  __syncthreads();
-  if (L.flush_ok) {
-    const uint32_t j = L.nflush - 1;
-    const size_t row = (size_t)gridDim.x * a.rec.dir_per_block;
-    if (a.ablate != 3)
-      for (uint32_t b = tid; b <= nb; b += MAP_THREADS)
-        a.rec.dir_off[b * row + (size_t)blockIdx.x * a.rec.dir_per_block + j] = L.u.boff[b];
-    const uint64_t base = L.flush_base;
+    __syncthreads();
+    // exclusive scan of boff[0, nb): one bucket per thread
+    const uint32_t v = (uint32_t)tid < nb ? L.boff[tid] : 0u;
+    uint32_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) L.wsum[wave] = x;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
 #pragma unroll
-    for (int k = 0; k < MAP_SPT; ++k) {
-      if (sb[k] == 0xFFFFFFFFu) continue;
-      const int s = tid + k * MAP_THREADS;
-      const u64x2 kk = L.key[s];
-      Rec r;
-      r.k0 = kk.x;
-      r.k1 = kk.y;
-      r.co = ((uint64_t)L.cnt[s] << 32) | L.off[s];
-      a.rec.recs[base + L.u.boff[sb[k]] + sr[k]] = r;
+    for (int w = 0; w < MAP_WAVES; ++w) {
+      const uint32_t ws = L.wsum[w];
+      before += w < wave ? ws : 0u;
+      total += ws;
     }
+    if ((uint32_t)tid <= nb) L.boff[tid] = before + x - v;  // boff[nb] = total
+    if (tid == 0) {
+      uint32_t ok = 0;
+      L.occupied = 0;
+      if (total) {
+        // block-private record region: no global cursor contention
+        const uint64_t region = a.rec.cap / gridDim.x;
+        const uint64_t base = (uint64_t)blockIdx.x * region + L.used;
+        const uint32_t j = L.nflush;
+        ok = (L.used + total <= region && j < a.rec.dir_per_block) ? 1u : 0u;
+        L.used += total;
+        if (ok) {
+          L.nflush = j + 1;
+          a.rec.dir_base[(size_t)blockIdx.x * a.rec.dir_per_block + j] = base;
+        } else {
+          atomicOr(&a.flags[FLAG_REGION_OVF], 1u);
+        }
+        L.flush_base = base;
+      }
+      L.flush_ok = ok;
+    }
+    __syncthreads();
+    if (L.flush_ok) {
+      const uint32_t j = L.nflush - 1;
+      const size_t row = (size_t)gridDim.x * a.rec.dir_per_block;
+      if (a.ablate != 3 && (uint32_t)tid <= nb)
+        a.rec.dir_off[(size_t)tid * row + (size_t)blockIdx.x * a.rec.dir_per_block + j] = L.boff[tid];
+      const uint64_t base = L.flush_base;
+#pragma unroll
+      for (int k = 0; k < MAP_SPT; ++k) {
+        if (sb[k] == 0xFFFFFFFFu) continue;
+        const int s = tid + k * MAP_THREADS;
+        const u64x2 kk = L.key[s];
+        Rec r;
+        r.k0 = kk.x;
+        r.k1 = kk.y;
+        r.co = ((uint64_t)L.cnt[s] << 32) | L.off[s];
+        a.rec.recs[base + L.boff[sb[k]] + sr[k]] = r;
+      }
+    }
+  } else if (tid == 0) {
+    L.occupied = 0;
   }
-  __syncthreads();  // boff (aliases the token lists) fully read
-  clear_slots(L);
-  __syncthreads();
-  if (tid == 0) L.occupied = 0;
-  __syncthreads();
+  clear_slots(L);   // own slots only: no barrier needed before
+  __syncthreads();  // every thread done reading boff (and the slots cleared)
+  if ((uint32_t)tid <= nb) L.boff[tid] = 0;
+  if (trailing_sync) __syncthreads();
 }
 
 // Key of a token that does not end inside the 64-byte lane window.
@@ -371,11 +348,12 @@ struct PhaseClock {
 };
 
 template <bool ST>
-__global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  // 2nd arg: waves per SIMD (2 blocks / CU)
+__global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  // 2nd arg: waves per SIMD
   __shared__ MapLds L;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   clear_slots(L);
   L.fail[tid] = 0;
+  for (uint32_t b = tid; b < MAX_REC_BUCKETS + 4; b += MAP_THREADS) L.boff[b] = 0;
   if (tid == 0) {
     L.occupied = 0;
     L.last_new = 0;
@@ -411,7 +389,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
     // Flush only if the keys the last tile added would not fit again: Zipf
     // text with a small vocabulary keeps its table across many tiles, large
     // vocabularies flush before every tile instead of overflowing mid-tile.
-    if (L.occupied + L.last_new > MAP_FILL_MAX) flush_table(L, a);
+    if (L.occupied + L.last_new > MAP_FILL_MAX) flush_table(L, a, false);  // the commit barrier follows
     clk.lap(MS_FLUSH);
     if (tid == 0) L.occ_before = L.occupied;
     // ---- commit the prefetched tile to LDS, start loading the next ----
@@ -455,7 +433,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
     }
     const uint32_t wave_total = __shfl(incl, 63), excl = incl - ntok;
     const uint32_t pbase = tid * MAP_BPL;
-    uint32_t* list = L.u.list[wave];
+    uint32_t* list = L.list[wave];
     bool any_fail = false;
     uint32_t bits = starts, k = excl;  // this lane's next token and its wave index
     for (uint32_t base = 0; base < wave_total; base += MAP_LIST) {
@@ -503,7 +481,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
     // ---- probe sequences that were full: flush, then the owners retry ----
     while (__syncthreads_or(any_fail)) {
       clk.lap(MS_RETRY);
-      flush_table(L, a);
+      flush_table(L, a, true);
       clk.lap(MS_FLUSH);
       uint32_t todo = L.fail[tid];
       L.fail[tid] = 0;
@@ -530,7 +508,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
   }
   __syncthreads();
   clk.lap(MS_TOP);
-  if (L.occupied) flush_table(L, a);
+  if (L.occupied) flush_table(L, a, false);
   clk.lap(MS_FLUSH);
   if (ST && lane == 0) {
     clk.acc[MS_TOTAL] = clk.t - t_begin;

@@ -104,7 +104,7 @@ def test_table_split_large_vocab():
 def test_region_overflow_reruns():
     rng = np.random.default_rng(9)
     text = b" ".join(f"k{i}".encode() for i in rng.integers(0, 200000, 200000))
-    with ops.Engine(device=0, chunk_bytes=1 << 20, min_records=4096, records_per_byte=0.001) as e:
+    with ops.Engine(device=0, chunk_bytes=1 << 20, min_records=16384, records_per_byte=0.001) as e:
         e.count_bytes(text)
         got = e.result()
         st = e.stats()
