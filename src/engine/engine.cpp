@@ -121,11 +121,12 @@ Engine::Impl::~Impl() {
   if (d_stamps) {
     unsigned long long h[MAP_STAMP_N];
     if (hipMemcpy(h, d_stamps, sizeof h, hipMemcpyDeviceToHost) == hipSuccess && h[MS_TOTAL]) {
-      static const char* names[MAP_STAMP_N] = {"top-barrier", "commit", "mask", "list", "keys",
-                                               "combine",     "retry",  "flush", "barrier", "total"};
+      static const char* names[MS_TOTAL] = {"top-barrier", "commit", "mask", "list", "keys",
+                                               "combine",     "retry",  "flush", "barrier"};
       fprintf(stderr, "[wc] map phase clock (share of wave lifetime):");
-      for (int i = 0; i < MAP_STAMP_N; ++i) fprintf(stderr, " %s=%.3f", names[i], (double)h[i] / h[MS_TOTAL]);
-      fprintf(stderr, "\n");
+      for (int i = 0; i < MS_TOTAL; ++i) fprintf(stderr, " %s=%.3f", names[i], (double)h[i] / h[MS_TOTAL]);
+      fprintf(stderr, "; slowest-wave token phase / mean = %.3f\n",
+              h[MS_TOKSUM] ? (double)h[MS_TOKMAX] * MAP_THREADS / 64 / (double)h[MS_TOKSUM] : 0.0);
     }
     (void)hipFree(d_stamps);
   }
@@ -176,7 +177,7 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                 avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
                 d_ctr->flags, d_bucket_ovf, nullptr, newkeys()};
-  if (!ablate_map) launch_reduce(ra, s);  // ablated map output is not a valid shuffle
+  if (ablate_map == 0 || ablate_map >= 7) launch_reduce(ra, s);  // modes 1-6 leave no valid shuffle
   if (sync_debug) {
     const hipError_t e = hipStreamSynchronize(s);
     fprintf(stderr, "[wc] reduce base=%llu buckets=%u -> %s\n", (unsigned long long)base, 1u << table().log2_buckets,

@@ -333,15 +333,18 @@ __device__ __forceinline__ uint4 load16(const MapArgs& a, uint64_t g) {
 // deltas per wave; the real kernel (ST = false) compiles it away.
 template <bool ST>
 struct PhaseClock {
-  uint64_t acc[MAP_STAMP_N] = {};
+  unsigned long long* acc = nullptr;  // block accumulators in LDS (lane 0 of each wave adds)
   uint64_t t = 0;
-  __device__ __forceinline__ void start() {
-    if (ST) t = __builtin_amdgcn_s_memtime();
+  __device__ __forceinline__ void start(unsigned long long* lds_acc) {
+    if (ST) {
+      acc = lds_acc;
+      t = __builtin_amdgcn_s_memtime();
+    }
   }
   __device__ __forceinline__ void lap(int phase) {
     if (ST) {
       const uint64_t n = __builtin_amdgcn_s_memtime();
-      acc[phase] += n - t;
+      if (__lane_id() == 0) atomicAdd(&acc[phase], (unsigned long long)(n - t));
       t = n;
     }
   }
@@ -350,7 +353,9 @@ struct PhaseClock {
 template <bool ST>
 __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  // 2nd arg: waves per SIMD
   __shared__ MapLds L;
+  __shared__ unsigned long long st_acc[ST ? MAP_STAMP_N : 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (ST && tid < MAP_STAMP_N) st_acc[tid] = 0;
   clear_slots(L);
   L.fail[tid] = 0;
   for (uint32_t b = tid; b < MAX_REC_BUCKETS + 4; b += MAP_THREADS) L.boff[b] = 0;
@@ -379,7 +384,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
   };
   prefetch(blockIdx.x);
   PhaseClock<ST> clk;
-  clk.start();
+  clk.start(st_acc);
   const uint64_t t_begin = clk.t;
 
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -419,6 +424,8 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
     }
     const uint32_t ntok = __popc(starts);
     my_tokens += ntok;
+    uint64_t t_tok = 0;
+    if constexpr (ST) t_tok = __builtin_amdgcn_s_memtime();
     clk.lap(MS_MASK);
     if (a.ablate == 2) {
       sink ^= dm;
@@ -478,6 +485,13 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
       clk.lap(MS_COMBINE);
     }
 
+    if constexpr (ST) {  // spread of the waves' token-phase times (diagnostic)
+      const uint64_t dt = __builtin_amdgcn_s_memtime() - t_tok;
+      if (lane == 0) {
+        atomicAdd(&st_acc[MS_TOKSUM], (unsigned long long)dt);
+        atomicMax(&st_acc[MS_TOKMAX_TILE], (unsigned long long)dt);
+      }
+    }
     // ---- probe sequences that were full: flush, then the owners retry ----
     while (__syncthreads_or(any_fail)) {
       clk.lap(MS_RETRY);
@@ -505,14 +519,19 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
     }
     clk.lap(MS_RETRY);
     if (tid == 0) L.last_new = L.occupied > L.occ_before ? L.occupied - L.occ_before : L.occupied;
+    if constexpr (ST) {
+      if (tid == 0) {  // all waves passed __syncthreads_or: the tile's max is final
+        st_acc[MS_TOKMAX] += st_acc[MS_TOKMAX_TILE];
+        st_acc[MS_TOKMAX_TILE] = 0;
+      }
+    }
   }
   __syncthreads();
   clk.lap(MS_TOP);
   if (L.occupied) flush_table(L, a, false);
   clk.lap(MS_FLUSH);
-  if (ST && lane == 0) {
-    clk.acc[MS_TOTAL] = clk.t - t_begin;
-    for (int i = 0; i < MAP_STAMP_N; ++i) atomicAdd(&a.stamps[i], (unsigned long long)clk.acc[i]);
+  if constexpr (ST) {
+    if (lane == 0) atomicAdd(&st_acc[MS_TOTAL], (unsigned long long)(clk.t - t_begin));
   }
 
   // block totals -> one global atomic
@@ -521,6 +540,9 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
   if (lane == 0) atomicAdd(&L.tokens, (unsigned long long)t);
   if (sink == 0x9E3779B97F4A7C15ull) atomicOr(&a.flags[FLAG_COUNT - 1], 0u);  // never true
   __syncthreads();
+  if constexpr (ST) {
+    if (tid < MAP_STAMP_N) atomicAdd(&a.stamps[tid], st_acc[tid]);
+  }
   if (tid == 0) {
     atomicAdd(a.tokens, L.tokens);
     atomicAdd(a.rec.cursor, (unsigned long long)L.used);  // stats: records after the combiner
