@@ -58,15 +58,17 @@ WC_HD uint64_t make_k1(uint64_t len, uint64_t h) {
   return len <= 8 ? len : (K1_TAG | (fmix64(h ^ len) & K1_HASH_MASK));
 }
 
-// Placement hash: word-wise FNV-1a over the packed key (k0, k1), then fmix64.
-// Bits [2, 2+log2 B) select the shuffle / table bucket (they live inside the
-// 32-bit LDS tag, so a flush recovers the bucket without rehashing), bits
-// [32, ..) the slot group inside a bucket's table.
+// Placement hash of the packed key: (k0 ^ rotl(k1, 56)) through a two-multiply
+// xor-shift mixer (splitmix64-style finaliser).  Two full 64-bit multiplies —
+// the map computes it once per token, so it is kept cheaper than a byte-wise
+// FNV.  Bits [2, 2+log2 B) select the shuffle / table bucket (they live inside
+// the 32-bit LDS tag, so a flush recovers the bucket without rehashing), bits
+// [32, ..) the slot group inside a table, the top bits the merge owner rank.
 WC_HD uint64_t place_hash(uint64_t k0, uint64_t k1) {
-  uint64_t h = FNV_OFFSET;
-  h = (h ^ k0) * FNV_PRIME;
-  h = (h ^ k1) * FNV_PRIME;
-  return fmix64(h);
+  uint64_t h = (k0 ^ ((k1 << 56) | (k1 >> 8))) * 0x9E3779B97F4A7C15ull;
+  h ^= h >> 29;
+  h *= 0xBF58476D1CE4E5B9ull;
+  return h ^ (h >> 32);
 }
 
 // Nested: the bucket under 2B buckets is b or b + B for bucket b under B.
