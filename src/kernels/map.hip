@@ -38,11 +38,13 @@ namespace wc {
 namespace dev {
 
 constexpr int MAP_WAVES = MAP_THREADS / 64;
-constexpr int MAP_LIST = 128;                    // token-list entries per wave per round (2 per lane)
+constexpr int MAP_LIST = 256;                    // token-list entries per wave per round (u16)
 constexpr int MAP_GS = 8;                        // slots per probe group
 constexpr int MAP_NGROUPS = MAP_SLOTS / MAP_GS;  // 256
 constexpr int MAP_SPT = MAP_SLOTS / MAP_THREADS; // table slots per thread in a flush
-constexpr uint32_t MAP_LONG = 0xFFFFu;           // list entry: token runs past the lane window
+constexpr uint32_t MAP_LONG = 31u;               // list length field: >= 31 bytes or past the lane window
+constexpr int MAP_WAVE_BYTES = 64 * MAP_BPL;     // text bytes owned by one wave (list positions are relative)
+static_assert(MAP_WAVE_BYTES <= 2048, "list entries hold 11-bit wave-relative positions");
 static_assert(MAP_SLOTS % MAP_THREADS == 0, "flush assumes whole slots per thread");
 static_assert(MAP_TILE <= 65536, "list entries hold 16-bit tile positions");
 static_assert((MAP_NGROUPS & (MAP_NGROUPS - 1)) == 0, "group count must be a power of two");
@@ -55,7 +57,7 @@ struct MapLds {
   uint32_t tag[MAP_SLOTS];  // group g = tag[8g, 8g+8); 0 = empty
   uint32_t cnt[MAP_SLOTS];
   uint32_t off[MAP_SLOTS];
-  uint32_t list[MAP_WAVES][MAP_LIST];  // token rounds: (tile position | length << 16)
+  uint16_t list[MAP_WAVES][MAP_LIST];  // token rounds: wave-relative position | min(length, 31) << 11
   uint32_t boff[MAX_REC_BUCKETS + 4];  // flush: bucket counts -> exclusive offsets (+ total); 0 between flushes
   uint32_t fail[MAP_THREADS];  // bit i of word t: token at tile byte 32 t + i must be retried
   uint8_t tile[MAP_TILE + MAP_HALO + 16];  // +16: tile8() reads one word past
@@ -224,7 +226,7 @@ __device__ __forceinline__ void key_slow(const MapLds& L, const MapArgs& a, uint
   k1 = make_k1(len, h);
 }
 
-// Key of the token at tile position p with known length (< 64) or MAP_LONG.
+// Key of the token at tile position p with known length (< 31) or MAP_LONG.
 __device__ __forceinline__ void token_key(const MapLds& L, const MapArgs& a, uint64_t t0, uint32_t p, uint32_t len,
                                           uint64_t& k0, uint64_t& k1) {
   if (len != MAP_LONG) {
@@ -440,7 +442,8 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
     }
     const uint32_t wave_total = __shfl(incl, 63), excl = incl - ntok;
     const uint32_t pbase = tid * MAP_BPL;
-    uint32_t* list = L.list[wave];
+    uint16_t* list = L.list[wave];
+    const uint32_t wbase = wave * MAP_WAVE_BYTES;
     bool any_fail = false;
     uint32_t bits = starts, k = excl;  // this lane's next token and its wave index
     for (uint32_t base = 0; base < wave_total; base += MAP_LIST) {
@@ -449,20 +452,20 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
         const uint32_t i = __ffs(bits) - 1;
         bits &= bits - 1;
         const uint64_t rest = dm >> i;
-        const uint32_t len = rest ? (uint32_t)__ffsll((unsigned long long)rest) - 1 : MAP_LONG;
-        list[k - base] = (pbase + i) | (len << 16);
+        const uint32_t len = rest ? min((uint32_t)__ffsll((unsigned long long)rest) - 1, MAP_LONG) : MAP_LONG;
+        list[k - base] = (uint16_t)((pbase + i - wbase) | (len << 11));
         ++k;
       }
       wave_sync();
       clk.lap(MS_LIST);
       const uint32_t n = min(wave_total - base, (uint32_t)MAP_LIST);
-      const bool h1 = (uint32_t)lane < n, h2 = (uint32_t)lane + 64 < n;
-      const uint32_t e1 = h1 ? list[lane] : 0u, e2 = h2 ? list[lane + 64] : 0u;
-      wave_sync();  // entries read before the next round overwrites them
-      const uint32_t q1 = e1 & 0xFFFFu, q2 = e2 & 0xFFFFu;
+      for (uint32_t j = 0; j < n; j += 128) {
+      const bool h1 = j + lane < n, h2 = j + 64 + lane < n;
+      const uint32_t e1 = h1 ? list[j + lane] : 0u, e2 = h2 ? list[j + 64 + lane] : 0u;
+      const uint32_t q1 = wbase + (e1 & 0x7FFu), q2 = wbase + (e2 & 0x7FFu);
       uint64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
-      if (h1) token_key(L, a, t0, q1, e1 >> 16, a0, a1);
-      if (h2) token_key(L, a, t0, q2, e2 >> 16, b0, b1);
+      if (h1) token_key(L, a, t0, q1, e1 >> 11, a0, a1);
+      if (h2) token_key(L, a, t0, q2, e2 >> 11, b0, b1);
       if (ST) {  // force the keys before the keys/combine boundary stamp
         asm volatile("" ::"v"(a0), "v"(a1), "v"(b0), "v"(b1));
       }
@@ -483,6 +486,8 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
       const uint32_t claims = (uint32_t)__popcll(__ballot(c1)) + (uint32_t)__popcll(__ballot(c2));
       if (lane == 0 && claims) atomicAdd(&L.occupied, claims);
       clk.lap(MS_COMBINE);
+      }
+      wave_sync();  // entries read before the next round overwrites them
     }
 
     if constexpr (ST) {  // spread of the waves' token-phase times (diagnostic)
@@ -505,7 +510,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
         const uint32_t i = __ffs(todo) - 1;
         todo &= todo - 1;
         const uint64_t rest = dm >> i;
-        const uint32_t len = rest ? (uint32_t)__ffsll((unsigned long long)rest) - 1 : MAP_LONG;
+        const uint32_t len = rest ? min((uint32_t)__ffsll((unsigned long long)rest) - 1, MAP_LONG) : MAP_LONG;
         uint64_t k0, k1;
         token_key(L, a, t0, pbase + i, len, k0, k1);
         bool c = false;

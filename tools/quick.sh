@@ -8,3 +8,6 @@ python3 -c "
 import json; d=json.loads(open('gpurun_out/q_bench.json').read()); st=d['stages']
 print(d['value'],'GB/s', d['ms_per_step'],'ms  mr',st['map_reduce_ms'],'fin',st['finalize_ms'],'records',st['records'])"
 WC_MAP_STAMPS=1 timeout -k 10 120 python bench.py --steps 3 --warmup 1 2>&1 | grep "phase clock"
+timeout -k 10 120 python bench.py --vocab 500 > gpurun_out/q_bench500.json 2>/dev/null || exit 1
+python3 -c "
+import json; d=json.loads(open('gpurun_out/q_bench500.json').read()); print('vocab500', d['value'],'GB/s')"
