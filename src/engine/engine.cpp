@@ -282,7 +282,8 @@ void Engine::Impl::compact_local() {
   unsigned long long arena_used = 0;
   WC_HIP_CHECK(hipMemcpyAsync(&arena_used, d_arena_cursor, 8, hipMemcpyDeviceToHost, s));
   WC_HIP_CHECK(hipStreamSynchronize(s));
-  std::vector<uint64_t> boff(nb);
+  if (h_boff.size() < nb * 8) h_boff.resize(nb * 8);
+  uint64_t* boff = reinterpret_cast<uint64_t*>(h_boff.data());
   uint64_t n = 0;
   for (size_t b = 0; b < nb; ++b) {
     boff[b] = n;
@@ -300,9 +301,8 @@ void Engine::Impl::compact_local() {
   cols.sref_off = fin_mem.take_n<uint64_t>(n + 1);
   cols.sref_len = fin_mem.take_n<uint32_t>(n + 1);
   uint64_t* d_boff = fin_mem.take_n<uint64_t>(nb);
-  WC_HIP_CHECK(hipMemcpyAsync(d_boff, boff.data(), nb * 8, hipMemcpyHostToDevice, s));
+  WC_HIP_CHECK(hipMemcpyAsync(d_boff, boff, nb * 8, hipMemcpyHostToDevice, s));  // pinned: no sync needed
   launch_table_compact(t, d_boff, cols.k0, cols.k1, cols.cnt, cols.first, cols.sref_off, cols.sref_len, s);
-  WC_HIP_CHECK(hipStreamSynchronize(s));  // boff is pageable host memory
   cols.n = n;
   cols_arena = d_arena;
   cols_arena_bytes = std::min<uint64_t>(arena_used, opt.arena_bytes);
@@ -335,12 +335,8 @@ void Engine::Impl::sort_cols_by_first() {
   int bits = 1;
   while (bits < 64 && (max_end >> bits) != 0) ++bits;
   radix_sort_pairs(keys, vals, tkeys, tvals, hist, n, bits, s);
-  launch_gather_u64(cols.k0, vals, o.k0, n, s);
-  launch_gather_u64(cols.k1, vals, o.k1, n, s);
-  launch_gather_u64(cols.cnt, vals, o.cnt, n, s);
-  launch_gather_u64(cols.first, vals, o.first, n, s);
-  launch_gather_u64(cols.sref_off, vals, o.sref_off, n, s);
-  launch_gather_u32(cols.sref_len, vals, o.sref_len, n, s);
+  launch_gather_cols(cols.k0, cols.k1, cols.cnt, cols.first, cols.sref_off, cols.sref_len, vals, o.k0, o.k1, o.cnt,
+                     o.first, o.sref_off, o.sref_len, n, s);
   cols = o;
 }
 

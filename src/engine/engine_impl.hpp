@@ -91,6 +91,7 @@ struct Engine::Impl {
 
   // finalisation workspace
   DeviceArena fin_mem;   // compact output
+  PinnedBuffer h_boff;   // per-bucket compaction offsets (H2D without a sync)
   DeviceArena merge_mem; // merge buffers (merged columns live here)
   DeviceArena merge_small;  // merge metadata (count matrices)
   DeviceArena sort_mem;  // first-occurrence sort + sorted columns

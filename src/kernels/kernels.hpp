@@ -133,7 +133,10 @@ size_t radix_hist_words(uint64_t n);
 void radix_sort_pairs(uint64_t* keys, uint32_t* vals, uint64_t* tmp_keys, uint32_t* tmp_vals, uint32_t* hist,
                       uint64_t n, int bits, hipStream_t s);
 
-// out[i] = in[perm[i]] for the six key-table columns.
+// out[i] = in[perm[i]] for the six key-table columns (one launch).
+void launch_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
+                        const uint64_t* soff, const uint32_t* slen, const uint32_t* perm, uint64_t* ok0, uint64_t* ok1,
+                        uint64_t* ocnt, uint64_t* ofirst, uint64_t* osoff, uint32_t* oslen, uint64_t n, hipStream_t s);
 void launch_gather_u64(const uint64_t* in, const uint32_t* perm, uint64_t* out, uint64_t n, hipStream_t s);
 void launch_gather_u32(const uint32_t* in, const uint32_t* perm, uint32_t* out, uint64_t n, hipStream_t s);
 void launch_iota_u32(uint32_t* v, uint64_t n, hipStream_t s);

@@ -37,37 +37,30 @@ __global__ void __launch_bounds__(RS_THREADS) wc_radix_hist(const uint64_t* keys
   hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
 }
 
-// Single-block exclusive scan of m words (digit-major histogram).
+// Single-block exclusive scan of m words (digit-major histogram): each
+// thread scans a contiguous run of ceil(m / 1024) words, one block scan of the
+// run totals, then each thread rewrites its run — one pass instead of m / 1024
+// barrier-separated steps.
 __global__ void __launch_bounds__(1024) wc_radix_scan(uint32_t* hist, uint64_t m) {
   __shared__ uint32_t wsum[16];
-  __shared__ uint32_t carry;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (uint64_t base = 0; base < m; base += 1024) {
-    const uint64_t i = base + threadIdx.x;
-    const uint32_t v = i < m ? hist[i] : 0;
-    uint32_t x = v;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o);
-      if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[wave] = x;
-    __syncthreads();
-    if (wave == 0) {
-      uint32_t s = lane < 16 ? wsum[lane] : 0;
-      for (int o = 1; o < 16; o <<= 1) {
-        const uint32_t y = __shfl_up(s, o);
-        if (lane >= o) s += y;
-      }
-      if (lane < 16) wsum[lane] = s;
-    }
-    __syncthreads();
-    const uint32_t excl = carry + (wave ? wsum[wave - 1] : 0) + x - v;
-    if (i < m) hist[i] = excl;
-    __syncthreads();
-    if (threadIdx.x == 0) carry += wsum[15];
-    __syncthreads();
+  const uint64_t per = (m + 1023) / 1024;
+  const uint64_t b = threadIdx.x * per, e = b + per < m ? b + per : m;
+  uint32_t tot = 0;
+  for (uint64_t i = b; i < e; ++i) tot += hist[i];
+  uint32_t x = tot;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  uint32_t run = x - tot;
+  for (int w = 0; w < wave; ++w) run += wsum[w];
+  for (uint64_t i = b; i < e; ++i) {
+    const uint32_t v = hist[i];
+    hist[i] = run;
+    run += v;
   }
 }
 
@@ -111,6 +104,22 @@ __global__ void __launch_bounds__(RS_THREADS) wc_radix_scatter(const uint64_t* k
       ovals[dst] = vals[i];
     }
     __syncthreads();
+  }
+}
+
+// out.col[i] = in.col[perm[i]] for all six key-table columns (one launch).
+__global__ void wc_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
+                               const uint64_t* soff, const uint32_t* slen, const uint32_t* perm, uint64_t* ok0,
+                               uint64_t* ok1, uint64_t* ocnt, uint64_t* ofirst, uint64_t* osoff, uint32_t* oslen,
+                               uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t j = perm[i];
+    ok0[i] = k0[j];
+    ok1[i] = k1[j];
+    ocnt[i] = cnt[j];
+    ofirst[i] = first[j];
+    osoff[i] = soff[j];
+    oslen[i] = slen[j];
   }
 }
 
@@ -177,6 +186,14 @@ void radix_sort_pairs(uint64_t* keys, uint32_t* vals, uint64_t* tmp_keys, uint32
     WC_HIP_CHECK(hipMemcpyAsync(keys, ki, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
     WC_HIP_CHECK(hipMemcpyAsync(vals, vi, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   }
+}
+
+void launch_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
+                        const uint64_t* soff, const uint32_t* slen, const uint32_t* perm, uint64_t* ok0, uint64_t* ok1,
+                        uint64_t* ocnt, uint64_t* ofirst, uint64_t* osoff, uint32_t* oslen, uint64_t n, hipStream_t s) {
+  if (n)
+    hipLaunchKernelGGL(dev::wc_gather_cols, dev::grid_for(n), dim3(256), 0, s, k0, k1, cnt, first, soff, slen, perm,
+                       ok0, ok1, ocnt, ofirst, osoff, oslen, n);
 }
 
 void launch_gather_u64(const uint64_t* in, const uint32_t* perm, uint64_t* out, uint64_t n, hipStream_t s) {
