@@ -22,7 +22,7 @@
 namespace wc {
 namespace dev {
 
-constexpr int RED_UNROLL = 4;
+constexpr int RED_UNROLL = 8;
 
 struct RedLds {
   SlotGroup grp[TAB_GROUPS];  // first: 16-B aligned group reads
