@@ -12,7 +12,8 @@ import os
 from ctypes import POINTER, c_char, c_char_p, c_double, c_int, c_uint32, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libwc.so")
+# WC_LIB selects another in-tree build of the engine (tuning variants, tools/variants.sh).
+LIB_PATH = os.environ.get("WC_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libwc.so")
 
 
 class WcError(RuntimeError):

@@ -125,8 +125,9 @@ Engine::Impl::~Impl() {
                                                "combine",     "retry",  "flush", "barrier"};
       fprintf(stderr, "[wc] map phase clock (share of wave lifetime):");
       for (int i = 0; i < MS_TOTAL; ++i) fprintf(stderr, " %s=%.3f", names[i], (double)h[i] / h[MS_TOTAL]);
-      fprintf(stderr, "; slowest-wave token phase / mean = %.3f\n",
-              h[MS_TOKSUM] ? (double)h[MS_TOKMAX] * MAP_THREADS / 64 / (double)h[MS_TOKSUM] : 0.0);
+      fprintf(stderr, "; slowest-wave token phase / mean = %.3f; tile flushes %llu, retry flushes %llu\n",
+              h[MS_TOKSUM] ? (double)h[MS_TOKMAX] * MAP_THREADS / 64 / (double)h[MS_TOKSUM] : 0.0, h[MS_NFLUSH],
+              h[MS_NRETRY]);
     }
     (void)hipFree(d_stamps);
   }

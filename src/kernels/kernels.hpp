@@ -23,7 +23,10 @@ constexpr int MAP_TILE = MAP_THREADS * MAP_BPL;      // 32 KiB LDS text tile
 constexpr int MAP_HALO = 256;                        // bytes past the tile kept in LDS
 constexpr int MAP_SLOTS = 4096;                      // LDS combiner slots (groups of 8)
 constexpr int MAP_GROUPS = MAP_SLOTS / 4;
-constexpr int MAP_FILL_MAX = MAP_SLOTS * 3 / 4;      // adaptive flush: target max fill
+#ifndef WC_MAP_FILL_EIGHTHS
+#define WC_MAP_FILL_EIGHTHS 6
+#endif
+constexpr int MAP_FILL_MAX = MAP_SLOTS * WC_MAP_FILL_EIGHTHS / 8;  // adaptive flush: target max fill (sticky included)
 constexpr int MAP_MAX_GROUP_PROBES = 8;              // then flush and retry the token
 constexpr int MAX_REC_BUCKETS_LOG2 = 9;              // shuffle partitions <= 512
 constexpr int MAX_REC_BUCKETS = 1 << MAX_REC_BUCKETS_LOG2;
@@ -91,7 +94,7 @@ struct MapArgs {
   unsigned long long* stamps;  // profiling: per-phase s_memtime sums (MAP_STAMP_N), nullptr = off
 };
 // In-kernel phase stamps of the map (diagnostic build path, WC_MAP_STAMPS=1).
-enum : int { MS_TOP = 0, MS_COMMIT, MS_MASK, MS_LIST, MS_KEYS, MS_COMBINE, MS_RETRY, MS_FLUSH, MS_BARRIER, MS_TOTAL, MS_TOKSUM, MS_TOKMAX, MS_TOKMAX_TILE, MAP_STAMP_N };
+enum : int { MS_TOP = 0, MS_COMMIT, MS_MASK, MS_LIST, MS_KEYS, MS_COMBINE, MS_RETRY, MS_FLUSH, MS_BARRIER, MS_TOTAL, MS_TOKSUM, MS_TOKMAX, MS_TOKMAX_TILE, MS_NFLUSH, MS_NRETRY, MAP_STAMP_N };
 
 struct ReduceArgs {
   Records rec;

@@ -42,6 +42,15 @@ constexpr int MAP_LIST = 256;                    // token-list entries per wave 
 constexpr int MAP_GS = 8;                        // slots per probe group
 constexpr int MAP_NGROUPS = MAP_SLOTS / MAP_GS;  // 256
 constexpr int MAP_SPT = MAP_SLOTS / MAP_THREADS; // table slots per thread in a flush
+constexpr uint32_t MAP_STICKY = 0x80000000u;     // cnt flag: hot slot, kept across flushes
+#ifndef WC_MAP_PROMOTE
+#define WC_MAP_PROMOTE 5
+#endif
+#ifndef WC_MAP_STICKY_CAP
+#define WC_MAP_STICKY_CAP (MAP_SLOTS / 4)
+#endif
+constexpr uint32_t MAP_PROMOTE = WC_MAP_PROMOTE;     // tokens in one window that make a slot sticky
+constexpr int MAP_STICKY_CAP = WC_MAP_STICKY_CAP;    // sticky budget per block (0 = off)
 constexpr uint32_t MAP_LONG = 31u;               // list length field: >= 31 bytes or past the lane window
 constexpr int MAP_WAVE_BYTES = 64 * MAP_BPL;     // text bytes owned by one wave (list positions are relative)
 static_assert(MAP_WAVE_BYTES <= 2048, "list entries hold 11-bit wave-relative positions");
@@ -63,6 +72,7 @@ struct MapLds {
   uint8_t tile[MAP_TILE + MAP_HALO + 16];  // +16: tile8() reads one word past
   uint32_t wsum[MAP_WAVES];
   uint32_t occupied;
+  uint32_t sticky;  // slots promoted to sticky (budget counter)
   uint32_t occ_before, last_new;  // adaptive flush: keys added by the last tile
   uint32_t prev;
   uint32_t flush_ok;
@@ -118,11 +128,11 @@ __device__ __forceinline__ void clear_slots(MapLds& L) {
 // Four block barriers: bucket histogram | wave sums of the scan | offsets +
 // region | records written (then the histogram is re-zeroed).  trailing_sync
 // adds a fifth when inserts follow immediately (retry path).
-__device__ void flush_table(MapLds& L, const MapArgs& a, bool trailing_sync) {
+__device__ void flush_table(MapLds& L, const MapArgs& a, bool trailing_sync, bool final = false) {
   static_assert(MAX_REC_BUCKETS < MAP_THREADS, "one bucket per thread in the scan");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t nb = 1u << a.log2_rec_buckets;
-  uint32_t sb[MAP_SPT], sr[MAP_SPT];
+  uint32_t sb[MAP_SPT], sr[MAP_SPT], kept = 0;
   if (a.ablate != 5) {  // 5 (profiling): flush = clear only
 #pragma unroll
     for (int j = 0; j < MAP_SPT; ++j) {
@@ -130,8 +140,22 @@ __device__ void flush_table(MapLds& L, const MapArgs& a, bool trailing_sync) {
       sb[j] = 0xFFFFFFFFu;
       const uint32_t tag = L.tag[s];
       if (tag != 0) {
-        sb[j] = (tag >> 2) & (nb - 1u);  // == bucket_of(place_hash): bucket bits live in the tag
-        sr[j] = atomicAdd(&L.boff[sb[j]], 1u);
+        // Sticky slots (hot keys) stay and keep counting until the block's
+        // final flush; a slot that counted MAP_PROMOTE tokens in this window
+        // becomes sticky while the sticky budget lasts.
+        const uint32_t c = L.cnt[s];
+        bool stick = (c & MAP_STICKY) != 0;
+        if (!final && !stick && c >= MAP_PROMOTE && L.sticky < (uint32_t)MAP_STICKY_CAP &&
+            atomicAdd(&L.sticky, 1u) < (uint32_t)MAP_STICKY_CAP) {
+          L.cnt[s] = c | MAP_STICKY;
+          stick = true;
+        }
+        if (stick && !final) {
+          ++kept;
+        } else {
+          sb[j] = (tag >> 2) & (nb - 1u);  // == bucket_of(place_hash): bucket bits live in the tag
+          sr[j] = atomicAdd(&L.boff[sb[j]], 1u);
+        }
       }
     }
     __syncthreads();
@@ -187,14 +211,25 @@ __device__ void flush_table(MapLds& L, const MapArgs& a, bool trailing_sync) {
         Rec r;
         r.k0 = kk.x;
         r.k1 = kk.y;
-        r.co = ((uint64_t)L.cnt[s] << 32) | L.off[s];
+        r.co = ((uint64_t)(L.cnt[s] & ~MAP_STICKY) << 32) | L.off[s];
         a.rec.recs[base + L.boff[sb[k]] + sr[k]] = r;
       }
     }
-  } else if (tid == 0) {
-    L.occupied = 0;
+    if (kept) atomicAdd(&L.occupied, kept);
+#pragma unroll
+    for (int k = 0; k < MAP_SPT; ++k) {  // own emitted slots only: no barrier needed before
+      if (sb[k] == 0xFFFFFFFFu) continue;
+      const int s = tid + k * MAP_THREADS;
+      L.tag[s] = 0;
+      L.key[s].y = K1_EMPTY;
+      L.cnt[s] = 0;
+      L.off[s] = 0xFFFFFFFFu;
+    }
+  } else {
+    if (tid == 0) L.occupied = 0;
+    clear_slots(L);
   }
-  clear_slots(L);   // own slots only: no barrier needed before
+  if (final && tid == 0) L.sticky = 0;
   __syncthreads();  // every thread done reading boff (and the slots cleared)
   if ((uint32_t)tid <= nb) L.boff[tid] = 0;
   if (trailing_sync) __syncthreads();
@@ -363,6 +398,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
   for (uint32_t b = tid; b < MAX_REC_BUCKETS + 4; b += MAP_THREADS) L.boff[b] = 0;
   if (tid == 0) {
     L.occupied = 0;
+    L.sticky = 0;
     L.last_new = 0;
     L.tokens = 0;
     L.nflush = 0;
@@ -396,7 +432,12 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
     // Flush only if the keys the last tile added would not fit again: Zipf
     // text with a small vocabulary keeps its table across many tiles, large
     // vocabularies flush before every tile instead of overflowing mid-tile.
-    if (L.occupied + L.last_new > MAP_FILL_MAX) flush_table(L, a, false);  // the commit barrier follows
+    if (L.occupied + L.last_new > MAP_FILL_MAX) {
+      if constexpr (ST) {
+        if (tid == 0) st_acc[MS_NFLUSH] += 1;
+      }
+      flush_table(L, a, false);  // the commit barrier follows
+    }
     clk.lap(MS_FLUSH);
     if (tid == 0) L.occ_before = L.occupied;
     // ---- commit the prefetched tile to LDS, start loading the next ----
@@ -498,9 +539,13 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
       }
     }
     // ---- probe sequences that were full: flush, then the owners retry ----
-    while (__syncthreads_or(any_fail)) {
+    // (a second retry in one tile also evicts the sticky slots: always progresses)
+    for (uint32_t attempt = 0; __syncthreads_or(any_fail); ++attempt) {
       clk.lap(MS_RETRY);
-      flush_table(L, a, true);
+      if constexpr (ST) {
+        if (tid == 0) st_acc[MS_NRETRY] += 1;
+      }
+      flush_table(L, a, true, attempt > 0);
       clk.lap(MS_FLUSH);
       uint32_t todo = L.fail[tid];
       L.fail[tid] = 0;
@@ -533,7 +578,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
   }
   __syncthreads();
   clk.lap(MS_TOP);
-  if (L.occupied) flush_table(L, a, false);
+  if (L.occupied) flush_table(L, a, false, true);  // final: sticky slots too
   clk.lap(MS_FLUSH);
   if constexpr (ST) {
     if (lane == 0) atomicAdd(&st_acc[MS_TOTAL], (unsigned long long)(clk.t - t_begin));
