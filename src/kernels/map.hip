@@ -124,11 +124,42 @@ __device__ __forceinline__ void clear_slots(MapLds& L) {
   }
 }
 
+// Phase clock for the diagnostic build (ST = true): accumulates s_memtime
+// deltas per wave; the real kernel (ST = false) compiles it away.
+template <bool ST>
+struct PhaseClock {
+  unsigned long long* acc = nullptr;  // block accumulators in LDS (lane 0 of each wave adds)
+  uint64_t t = 0;
+  __device__ __forceinline__ void start(unsigned long long* lds_acc) {
+    if (ST) {
+      acc = lds_acc;
+      t = __builtin_amdgcn_s_memtime();
+    }
+  }
+  __device__ __forceinline__ void lap(int phase) {
+    if (ST) {
+      const uint64_t n = __builtin_amdgcn_s_memtime();
+      if (__lane_id() == 0) atomicAdd(&acc[phase], (unsigned long long)(n - t));
+      t = n;
+    }
+  }
+};
+
+// Block barrier; the diagnostic build books the time before it to `phase`
+// and the wait itself to MS_BARRIER.
+template <bool ST>
+__device__ __forceinline__ void bsync(PhaseClock<ST>& clk, int phase) {
+  clk.lap(phase);
+  __syncthreads();
+  clk.lap(MS_BARRIER);
+}
+
 // Shuffle write of the combiner table: one contiguous bucket-sorted chunk.
 // Four block barriers: bucket histogram | wave sums of the scan | offsets +
 // region | records written (then the histogram is re-zeroed).  trailing_sync
 // adds a fifth when inserts follow immediately (retry path).
-__device__ void flush_table(MapLds& L, const MapArgs& a, bool trailing_sync, bool final = false) {
+template <bool ST>
+__device__ void flush_table(MapLds& L, const MapArgs& a, PhaseClock<ST>& clk, bool trailing_sync, bool final = false) {
   static_assert(MAX_REC_BUCKETS < MAP_THREADS, "one bucket per thread in the scan");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t nb = 1u << a.log2_rec_buckets;
@@ -158,7 +189,7 @@ __device__ void flush_table(MapLds& L, const MapArgs& a, bool trailing_sync, boo
         }
       }
     }
-    __syncthreads();
+    bsync(clk, MS_FL_HIST);
     // exclusive scan of boff[0, nb): one bucket per thread
     const uint32_t v = (uint32_t)tid < nb ? L.boff[tid] : 0u;
     uint32_t x = v;
@@ -167,7 +198,7 @@ __device__ void flush_table(MapLds& L, const MapArgs& a, bool trailing_sync, boo
       if (lane >= o) x += y;
     }
     if (lane == 63) L.wsum[wave] = x;
-    __syncthreads();
+    bsync(clk, MS_FL_SCAN);
     uint32_t before = 0, total = 0;
 #pragma unroll
     for (int w = 0; w < MAP_WAVES; ++w) {
@@ -196,7 +227,7 @@ __device__ void flush_table(MapLds& L, const MapArgs& a, bool trailing_sync, boo
       }
       L.flush_ok = ok;
     }
-    __syncthreads();
+    bsync(clk, MS_FL_SCAN);
     if (L.flush_ok) {
       const uint32_t j = L.nflush - 1;
       const size_t row = (size_t)gridDim.x * a.rec.dir_per_block;
@@ -230,9 +261,9 @@ __device__ void flush_table(MapLds& L, const MapArgs& a, bool trailing_sync, boo
     clear_slots(L);
   }
   if (final && tid == 0) L.sticky = 0;
-  __syncthreads();  // every thread done reading boff (and the slots cleared)
+  bsync(clk, MS_FL_WRITE);  // every thread done reading boff (and the slots cleared)
   if ((uint32_t)tid <= nb) L.boff[tid] = 0;
-  if (trailing_sync) __syncthreads();
+  if (trailing_sync) bsync(clk, MS_FL_WRITE);
 }
 
 // Key of a token that does not end inside the 64-byte lane window.
@@ -366,27 +397,6 @@ __device__ __forceinline__ uint4 load16(const MapArgs& a, uint64_t g) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// Phase clock for the diagnostic build (ST = true): accumulates s_memtime
-// deltas per wave; the real kernel (ST = false) compiles it away.
-template <bool ST>
-struct PhaseClock {
-  unsigned long long* acc = nullptr;  // block accumulators in LDS (lane 0 of each wave adds)
-  uint64_t t = 0;
-  __device__ __forceinline__ void start(unsigned long long* lds_acc) {
-    if (ST) {
-      acc = lds_acc;
-      t = __builtin_amdgcn_s_memtime();
-    }
-  }
-  __device__ __forceinline__ void lap(int phase) {
-    if (ST) {
-      const uint64_t n = __builtin_amdgcn_s_memtime();
-      if (__lane_id() == 0) atomicAdd(&acc[phase], (unsigned long long)(n - t));
-      t = n;
-    }
-  }
-};
-
 template <bool ST>
 __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  // 2nd arg: waves per SIMD
   __shared__ MapLds L;
@@ -436,7 +446,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
       if constexpr (ST) {
         if (tid == 0) st_acc[MS_NFLUSH] += 1;
       }
-      flush_table(L, a, false);  // the commit barrier follows
+      flush_table(L, a, clk, false);  // the commit barrier follows
     }
     clk.lap(MS_FLUSH);
     if (tid == 0) L.occ_before = L.occupied;
@@ -545,7 +555,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
       if constexpr (ST) {
         if (tid == 0) st_acc[MS_NRETRY] += 1;
       }
-      flush_table(L, a, true, attempt > 0);
+      flush_table(L, a, clk, true, attempt > 0);
       clk.lap(MS_FLUSH);
       uint32_t todo = L.fail[tid];
       L.fail[tid] = 0;
@@ -578,7 +588,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
   }
   __syncthreads();
   clk.lap(MS_TOP);
-  if (L.occupied) flush_table(L, a, false, true);  // final: sticky slots too
+  if (L.occupied) flush_table(L, a, clk, false, true);  // final: sticky slots too
   clk.lap(MS_FLUSH);
   if constexpr (ST) {
     if (lane == 0) atomicAdd(&st_acc[MS_TOTAL], (unsigned long long)(clk.t - t_begin));
