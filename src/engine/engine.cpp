@@ -59,6 +59,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   map_blocks = opt.map_blocks ? opt.map_blocks : MAP_BLOCKS_PER_CU * (uint32_t)device_cu_count(dev);
   if (const char* e = std::getenv("WC_ABLATE_MAP")) ablate_map = (uint32_t)std::atoi(e);  // profiling only
   if (const char* e = std::getenv("WC_SYNC_DEBUG")) sync_debug = std::atoi(e) != 0;
+  if (const char* e = std::getenv("WC_MAP_DEC")) map_dec = std::atoi(e) != 0;
   if (const char* e = std::getenv("WC_MAP_STAMPS"); e && std::atoi(e)) {
     WC_HIP_CHECK(hipMalloc(&d_stamps, MAP_STAMP_N * 8));
     WC_HIP_CHECK(hipMemset(d_stamps, 0, MAP_STAMP_N * 8));
@@ -168,7 +169,8 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   pass_rec.cursor = &d_ctr->records;
   pass_rec.dir_per_block = dir_per_block_for(len, blocks);
   MapArgs m{text, len, avail, prev, log2_rb, pass_rec, d_ctr->flags, &d_ctr->tokens, ablate_map, d_stamps};
-  launch_map(m, blocks, s);
+  if (map_dec) launch_map_decoupled(m, blocks, s);
+  else launch_map(m, blocks, s);
   if (sync_debug) {  // WC_SYNC_DEBUG: attribute a device fault to a kernel and a chunk
     const hipError_t e = hipStreamSynchronize(s);
     fprintf(stderr, "[wc] map    base=%llu len=%llu avail=%llu blocks=%u J=%u -> %s\n", (unsigned long long)base,

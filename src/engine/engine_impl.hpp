@@ -46,6 +46,7 @@ struct Engine::Impl {
   uint32_t map_blocks = 0;
   uint32_t ablate_map = 0;  // WC_ABLATE_MAP (profiling ablations, MapArgs::ablate)
   bool sync_debug = false;  // WC_SYNC_DEBUG: sync + log after every kernel
+  bool map_dec = true;      // WC_MAP_DEC=0: block-synchronous tile kernel (map.hip) instead of map_dec.hip
   unsigned long long* d_stamps = nullptr;  // WC_MAP_STAMPS: map phase clock sums
 
   // shuffle records
@@ -53,9 +54,11 @@ struct Engine::Impl {
   Records rec{};       // full-capacity views
   Records pass_rec{};  // views of the current map/reduce pass
   uint32_t dir_per_block_max = 0;
+  // Flush directory columns per map block: at most one flush per 16 KiB of the
+  // block's text, doubled (a full region re-runs the chunk in halves anyway).
   static uint32_t dir_per_block_for(uint64_t len, uint32_t blocks) {
-    const uint64_t tiles = (len + MAP_TILE - 1) / MAP_TILE;
-    return (uint32_t)(2 * ((tiles + blocks - 1) / blocks) + 8);
+    const uint64_t per_block = (len + blocks - 1) / blocks;
+    return (uint32_t)(2 * ((per_block + 16383) / 16384) + 8);
   }
   DeviceArena rec_mem;
 

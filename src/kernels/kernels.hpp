@@ -122,6 +122,7 @@ struct SynthVocab {
 
 // ---- launchers (all stream-ordered, no host sync) ----------------------------
 void launch_map(const MapArgs& a, uint32_t map_blocks, hipStream_t s);
+void launch_map_decoupled(const MapArgs& a, uint32_t map_blocks, hipStream_t s);  // map_dec.hip
 void launch_reduce(const ReduceArgs& a, hipStream_t s);
 void launch_table_split(const TableView& src, const TableView& dst, hipStream_t s);
 void launch_table_clear(const TableView& t, hipStream_t s);

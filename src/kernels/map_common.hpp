@@ -1,0 +1,359 @@
+// map_common.hpp — building blocks shared by the map kernels (map.hip: block-
+// synchronous tiles; map_dec.hip: wave-decoupled units): delimiter masks, keys
+// from an LDS text buffer, the LDS combiner (probe / claim / count) and the
+// shuffle-write flush.  Functions touching the combiner take the kernel's LDS
+// struct as a template parameter; it must provide key, tag, cnt, off, boff,
+// wsum, occupied, sticky, flush_ok, nflush, used and flush_base.
+#pragma once
+#include "kernels.hpp"
+#include "keys.hpp"
+
+namespace wc {
+namespace dev {
+
+constexpr int MAP_WAVES = MAP_THREADS / 64;
+constexpr int MAP_LIST = 256;                    // token-list entries per wave per round (u16)
+constexpr int MAP_GS = 8;                        // slots per probe group
+constexpr int MAP_NGROUPS = MAP_SLOTS / MAP_GS;  // 256
+constexpr int MAP_SPT = MAP_SLOTS / MAP_THREADS; // table slots per thread in a flush
+constexpr uint32_t MAP_STICKY = 0x80000000u;     // cnt flag: hot slot, kept across flushes
+#ifndef WC_MAP_PROMOTE
+#define WC_MAP_PROMOTE 5
+#endif
+#ifndef WC_MAP_STICKY_CAP
+#define WC_MAP_STICKY_CAP (MAP_SLOTS / 4)
+#endif
+constexpr uint32_t MAP_PROMOTE = WC_MAP_PROMOTE;     // tokens in one window that make a slot sticky
+constexpr int MAP_STICKY_CAP = WC_MAP_STICKY_CAP;    // sticky budget per block (0 = off)
+constexpr uint32_t MAP_LONG = 31u;               // list length field: >= 31 bytes or past the lane window
+constexpr int MAP_WAVE_BYTES = 64 * MAP_BPL;     // text bytes owned by one wave (list positions are relative)
+static_assert(MAP_WAVE_BYTES <= 2048, "list entries hold 11-bit wave-relative positions");
+static_assert(MAP_SLOTS % MAP_THREADS == 0, "flush assumes whole slots per thread");
+static_assert(MAP_TILE <= 65536, "list entries hold 16-bit tile positions");
+static_assert((MAP_NGROUPS & (MAP_NGROUPS - 1)) == 0, "group count must be a power of two");
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+
+__device__ __forceinline__ uint32_t map_tag(uint64_t ph) { return ((uint32_t)ph & ~1u) | 2u; }  // never 0
+__device__ __forceinline__ uint32_t map_group(uint64_t ph) { return (uint32_t)(ph >> 32) & (MAP_NGROUPS - 1); }
+
+// Per-byte "is delimiter" for 8 packed bytes -> 8-bit mask (exact SWAR zero test).
+__device__ __forceinline__ uint64_t delim_mask8(uint64_t x) {
+  constexpr uint64_t ONES = 0x0101010101010101ull, LOW7 = 0x7F7F7F7F7F7F7F7Full;
+  auto zero_bytes = [](uint64_t y) { return ~(((y & LOW7) + LOW7) | y) & 0x8080808080808080ull; };
+  const uint64_t m = zero_bytes(x ^ (0x20 * ONES)) | zero_bytes(x ^ (0x0D * ONES)) | zero_bytes(x ^ (0x0A * ONES));
+  return ((m >> 7) * 0x0102040810204080ull) >> 56;
+}
+
+// 8 bytes of the LDS tile starting at byte p: two aligned ds_read_b64 + funnel
+// shift (dynamic indexing of a register window would be lowered to scratch).
+__device__ __forceinline__ uint64_t tile8(const uint8_t* tile, uint32_t p) {
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(tile + (p & ~7u));
+  const uint32_t sh = (p & 7) * 8;
+  const uint64_t lo = q[0], hi = q[1];
+  return sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
+}
+
+__device__ __forceinline__ uint64_t low_bytes(uint64_t v, uint32_t n) {
+  return n >= 8 ? v : (v & ((1ull << (8 * n)) - 1ull));
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <class LDS>
+__device__ __forceinline__ void clear_slots(LDS& L) {
+#pragma unroll
+  for (int k = 0; k < MAP_SPT; ++k) {
+    const int s = threadIdx.x + k * MAP_THREADS;
+    L.tag[s] = 0;
+    L.key[s].y = K1_EMPTY;
+    L.cnt[s] = 0;
+    L.off[s] = 0xFFFFFFFFu;
+  }
+}
+
+// Phase clock for the diagnostic build (ST = true): accumulates s_memtime
+// deltas per wave; the real kernel (ST = false) compiles it away.
+template <bool ST>
+struct PhaseClock {
+  unsigned long long* acc = nullptr;  // block accumulators in LDS (lane 0 of each wave adds)
+  uint64_t t = 0;
+  __device__ __forceinline__ void start(unsigned long long* lds_acc) {
+    if (ST) {
+      acc = lds_acc;
+      t = __builtin_amdgcn_s_memtime();
+    }
+  }
+  __device__ __forceinline__ void lap(int phase) {
+    if (ST) {
+      const uint64_t n = __builtin_amdgcn_s_memtime();
+      if (__lane_id() == 0) atomicAdd(&acc[phase], (unsigned long long)(n - t));
+      t = n;
+    }
+  }
+};
+
+// Block barrier; the diagnostic build books the time before it to `phase`
+// and the wait itself to MS_BARRIER.
+template <bool ST>
+__device__ __forceinline__ void bsync(PhaseClock<ST>& clk, int phase) {
+  clk.lap(phase);
+  __syncthreads();
+  clk.lap(MS_BARRIER);
+}
+
+// Shuffle write of the combiner table: one contiguous bucket-sorted chunk.
+// Four block barriers: bucket histogram | wave sums of the scan | offsets +
+// region | records written (then the histogram is re-zeroed).  trailing_sync
+// adds a fifth when inserts follow immediately (retry path).
+template <bool ST, class LDS>
+__device__ void flush_table(LDS& L, const MapArgs& a, PhaseClock<ST>& clk, bool trailing_sync, bool final = false) {
+  static_assert(MAX_REC_BUCKETS < MAP_THREADS, "one bucket per thread in the scan");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t nb = 1u << a.log2_rec_buckets;
+  uint32_t sb[MAP_SPT], sr[MAP_SPT], kept = 0;
+  if (a.ablate != 5) {  // 5 (profiling): flush = clear only
+#pragma unroll
+    for (int j = 0; j < MAP_SPT; ++j) {
+      const int s = tid + j * MAP_THREADS;
+      sb[j] = 0xFFFFFFFFu;
+      const uint32_t tag = L.tag[s];
+      if (tag != 0) {
+        // Sticky slots (hot keys) stay and keep counting until the block's
+        // final flush; a slot that counted MAP_PROMOTE tokens in this window
+        // becomes sticky while the sticky budget lasts.
+        const uint32_t c = L.cnt[s];
+        bool stick = (c & MAP_STICKY) != 0;
+        if (!final && !stick && c >= MAP_PROMOTE && L.sticky < (uint32_t)MAP_STICKY_CAP &&
+            atomicAdd(&L.sticky, 1u) < (uint32_t)MAP_STICKY_CAP) {
+          L.cnt[s] = c | MAP_STICKY;
+          stick = true;
+        }
+        if (stick && !final) {
+          ++kept;
+        } else {
+          sb[j] = (tag >> 2) & (nb - 1u);  // == bucket_of(place_hash): bucket bits live in the tag
+          sr[j] = atomicAdd(&L.boff[sb[j]], 1u);
+        }
+      }
+    }
+    bsync(clk, MS_FL_HIST);
+    // exclusive scan of boff[0, nb): one bucket per thread
+    const uint32_t v = (uint32_t)tid < nb ? L.boff[tid] : 0u;
+    uint32_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) L.wsum[wave] = x;
+    bsync(clk, MS_FL_SCAN);
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < MAP_WAVES; ++w) {
+      const uint32_t ws = L.wsum[w];
+      before += w < wave ? ws : 0u;
+      total += ws;
+    }
+    if ((uint32_t)tid <= nb) L.boff[tid] = before + x - v;  // boff[nb] = total
+    if (tid == 0) {
+      uint32_t ok = 0;
+      L.occupied = 0;
+      if (total) {
+        // block-private record region: no global cursor contention
+        const uint64_t region = a.rec.cap / gridDim.x;
+        const uint64_t base = (uint64_t)blockIdx.x * region + L.used;
+        const uint32_t j = L.nflush;
+        ok = (L.used + total <= region && j < a.rec.dir_per_block) ? 1u : 0u;
+        L.used += total;
+        if (ok) {
+          L.nflush = j + 1;
+          a.rec.dir_base[(size_t)blockIdx.x * a.rec.dir_per_block + j] = base;
+        } else {
+          atomicOr(&a.flags[FLAG_REGION_OVF], 1u);
+        }
+        L.flush_base = base;
+      }
+      L.flush_ok = ok;
+    }
+    bsync(clk, MS_FL_SCAN);
+    if (L.flush_ok) {
+      const uint32_t j = L.nflush - 1;
+      const size_t row = (size_t)gridDim.x * a.rec.dir_per_block;
+      if (a.ablate != 3 && (uint32_t)tid <= nb)
+        a.rec.dir_off[(size_t)tid * row + (size_t)blockIdx.x * a.rec.dir_per_block + j] = L.boff[tid];
+      const uint64_t base = L.flush_base;
+#pragma unroll
+      for (int k = 0; k < MAP_SPT; ++k) {
+        if (sb[k] == 0xFFFFFFFFu) continue;
+        const int s = tid + k * MAP_THREADS;
+        const u64x2 kk = L.key[s];
+        Rec r;
+        r.k0 = kk.x;
+        r.k1 = kk.y;
+        r.co = ((uint64_t)(L.cnt[s] & ~MAP_STICKY) << 32) | L.off[s];
+        a.rec.recs[base + L.boff[sb[k]] + sr[k]] = r;
+      }
+    }
+    if (kept) atomicAdd(&L.occupied, kept);
+#pragma unroll
+    for (int k = 0; k < MAP_SPT; ++k) {  // own emitted slots only: no barrier needed before
+      if (sb[k] == 0xFFFFFFFFu) continue;
+      const int s = tid + k * MAP_THREADS;
+      L.tag[s] = 0;
+      L.key[s].y = K1_EMPTY;
+      L.cnt[s] = 0;
+      L.off[s] = 0xFFFFFFFFu;
+    }
+  } else {
+    if (tid == 0) L.occupied = 0;
+    clear_slots(L);
+  }
+  if (final && tid == 0) L.sticky = 0;
+  bsync(clk, MS_FL_WRITE);  // every thread done reading boff (and the slots cleared)
+  if ((uint32_t)tid <= nb) L.boff[tid] = 0;
+  if (trailing_sync) bsync(clk, MS_FL_WRITE);
+}
+
+// Key of a token that does not end inside the 64-byte lane window: byte loop
+// over the LDS text buffer `buf` (buf_len bytes readable), then global memory.
+__device__ __forceinline__ void key_slow(const uint8_t* buf, uint32_t buf_len, const MapArgs& a, uint64_t pos,
+                                         uint64_t g, uint64_t& k0, uint64_t& k1) {
+  uint64_t len = 0, h = FNV_OFFSET, chunk = 0;
+  k0 = 0;
+  for (;;) {
+    uint32_t c;
+    if (pos < (uint64_t)buf_len) c = buf[pos];
+    else if (g < a.avail_len) c = a.text[g];
+    else break;
+    if (is_delim(c)) break;
+    if (len < 8) {
+      k0 |= (uint64_t)c << (8 * len);
+    } else {
+      chunk |= (uint64_t)c << (8 * (len & 7));
+      if ((len & 7) == 7) {
+        h = tail_fold(h, chunk);
+        chunk = 0;
+      }
+    }
+    ++len, ++pos, ++g;
+  }
+  if (len > 8 && (len & 7)) h = tail_fold(h, chunk);
+  k1 = make_k1(len, h);
+}
+
+// Key of the token at buffer position p with known length (< 31) or MAP_LONG;
+// buf[0] is global text offset t0.
+__device__ __forceinline__ void token_key(const uint8_t* buf, uint32_t buf_len, const MapArgs& a, uint64_t t0,
+                                          uint32_t p, uint32_t len, uint64_t& k0, uint64_t& k1) {
+  if (len != MAP_LONG) {
+    k0 = low_bytes(tile8(buf, p), len);
+    if (len <= 8) {
+      k1 = len;
+    } else {
+      uint64_t h = FNV_OFFSET;
+      for (uint32_t c = 8; c < len; c += 8) h = tail_fold(h, low_bytes(tile8(buf, p + c), len - c));
+      k1 = make_k1(len, h);
+    }
+  } else {
+    key_slow(buf, buf_len, a, p, t0 + p, k0, k1);
+  }
+}
+
+// Combiner slot of (k0, k1) — claiming one if the key is absent — or -1 when
+// MAP_MAX_GROUP_PROBES groups are full.  Claim = ONE CAS of the tag; the
+// claimer then writes k0 before k1 (LDS executes one wave's writes in order,
+// and the reader loads the 16-byte key in one instruction), so a reader that
+// sees the new k1 also sees the new k0; one that sees the tag before the key
+// does not match and may claim a duplicate slot, which the reducer merges.
+template <class LDS>
+__device__ __forceinline__ int combiner_slot(LDS& L, uint64_t ph, uint64_t k0, uint64_t k1, bool& claimed) {
+  const uint32_t tag = map_tag(ph);
+  uint32_t g = map_group(ph);
+  claimed = false;
+  for (int steps = 0; steps < MAP_MAX_GROUP_PROBES;) {
+    asm volatile("" ::: "memory");
+    const u32x4 ta = *reinterpret_cast<const u32x4*>(&L.tag[g * MAP_GS]);
+    const u32x4 tb = *reinterpret_cast<const u32x4*>(&L.tag[g * MAP_GS + 4]);
+    uint32_t m = (ta.x == tag ? 1u : 0u) | (ta.y == tag ? 2u : 0u) | (ta.z == tag ? 4u : 0u) |
+                 (ta.w == tag ? 8u : 0u) | (tb.x == tag ? 16u : 0u) | (tb.y == tag ? 32u : 0u) |
+                 (tb.z == tag ? 64u : 0u) | (tb.w == tag ? 128u : 0u);
+    while (m) {
+      const uint32_t i = __ffs(m) - 1;
+      m &= m - 1;
+      const u64x2 kk = L.key[g * MAP_GS + i];
+      if (kk.x == k0 && kk.y == k1) return (int)(g * MAP_GS + i);
+    }
+    const uint32_t e = (ta.x == 0 ? 1u : 0u) | (ta.y == 0 ? 2u : 0u) | (ta.z == 0 ? 4u : 0u) |
+                       (ta.w == 0 ? 8u : 0u) | (tb.x == 0 ? 16u : 0u) | (tb.y == 0 ? 32u : 0u) |
+                       (tb.z == 0 ? 64u : 0u) | (tb.w == 0 ? 128u : 0u);
+    if (!e) {
+      ++steps;
+      g = (g + 1) & (MAP_NGROUPS - 1);
+      continue;
+    }
+    const uint32_t s = g * MAP_GS + (__ffs(e) - 1);
+    if (atomicCAS(&L.tag[s], 0u, tag) == 0u) {
+      L.key[s].x = k0;
+      asm volatile("" ::: "memory");
+      L.key[s].y = k1;
+      claimed = true;
+      return (int)s;
+    }
+    // lost the slot to another lane: re-read this group
+  }
+  return -1;
+}
+
+// Count one token; false if its probe sequence is full.
+template <class LDS>
+__device__ __forceinline__ bool combine(LDS& L, uint64_t k0, uint64_t k1, uint32_t off, bool& claimed) {
+  const int s = combiner_slot(L, place_hash(k0, k1), k0, k1, claimed);
+  if (s < 0) return false;
+  atomicAdd(&L.cnt[s], 1u);  // results unused: no-return ds_add / ds_min
+  atomicMin(&L.off[s], off);
+  return true;
+}
+
+// 32 text bytes at global offset g as two 16-B vectors (' ' past avail).
+__device__ __forceinline__ void load32(const MapArgs& a, uint64_t g, uint4& v0, uint4& v1) {
+  if (g + MAP_BPL <= a.avail_len) {
+    const uint4* src = reinterpret_cast<const uint4*>(a.text + g);
+    v0 = src[0];
+    v1 = src[1];
+  } else {
+    uint32_t w[8];
+    for (int k = 0; k < 8; ++k) {
+      uint32_t x = 0;
+      for (int b = 0; b < 4; ++b) {
+        const uint64_t i = g + 4 * k + b;
+        x |= (uint32_t)(i < a.avail_len ? a.text[i] : 0x20) << (8 * b);
+      }
+      w[k] = x;
+    }
+    v0 = make_uint4(w[0], w[1], w[2], w[3]);
+    v1 = make_uint4(w[4], w[5], w[6], w[7]);
+  }
+}
+
+__device__ __forceinline__ uint4 load16(const MapArgs& a, uint64_t g) {
+  if (g + 16 <= a.avail_len) return *reinterpret_cast<const uint4*>(a.text + g);
+  uint32_t w[4];
+  for (int k = 0; k < 4; ++k) {
+    uint32_t x = 0;
+    for (int b = 0; b < 4; ++b) {
+      const uint64_t i = g + 4 * k + b;
+      x |= (uint32_t)(i < a.avail_len ? a.text[i] : 0x20) << (8 * b);
+    }
+    w[k] = x;
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+}  // namespace dev
+}  // namespace wc
