@@ -122,8 +122,8 @@ Engine::Impl::~Impl() {
   if (d_stamps) {
     unsigned long long h[MAP_STAMP_N];
     if (hipMemcpy(h, d_stamps, sizeof h, hipMemcpyDeviceToHost) == hipSuccess && h[MS_TOTAL]) {
-      static const char* names[MS_TOTAL] = {"top-barrier", "commit", "mask", "list", "keys",
-                                               "combine",     "retry",  "flush", "barrier"};
+      static const char* names[MS_TOTAL] = {"top-barrier", "commit", "mask",    "list",    "keys",    "combine",
+                                            "retry",       "flush",  "barrier", "fl-hist", "fl-scan", "fl-write"};
       fprintf(stderr, "[wc] map phase clock (share of wave lifetime):");
       for (int i = 0; i < MS_TOTAL; ++i) fprintf(stderr, " %s=%.3f", names[i], (double)h[i] / h[MS_TOTAL]);
       fprintf(stderr, "; slowest-wave token phase / mean = %.3f; tile flushes %llu, retry flushes %llu\n",
