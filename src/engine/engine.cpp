@@ -74,16 +74,12 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   opt.chunk_bytes = opt.chunk_bytes / MAP_TILE * MAP_TILE;
 
   rec_total = std::max<uint64_t>(opt.min_records, (uint64_t)((double)opt.chunk_bytes * opt.records_per_byte));
-  // flush directory: at most one flush per tile (+ retries, + the final one)
-  dir_per_block_max = dir_per_block_for(opt.chunk_bytes, map_blocks);
-  const size_t dir_cols = (size_t)map_blocks * dir_per_block_max;
-  const size_t nrb1 = (size_t)MAX_REC_BUCKETS + 1;  // partitions follow the table up to the max
-  rec_mem.reserve(rec_total * sizeof(Rec) + dir_cols * (8 + 4 * nrb1) + map_blocks * 4 + 8192);
+  // record store + per-(block, bucket) counts; partitions follow the table up to the max
+  const size_t ncount = (size_t)map_blocks * MAX_REC_BUCKETS;
+  rec_mem.reserve(rec_total * sizeof(Rec) + ncount * 4 + 8192);
   rec.recs = rec_mem.take_n<Rec>(rec_total);
   rec.cap = rec_total;
-  rec.dir_base = rec_mem.take_n<uint64_t>(dir_cols);
-  rec.dir_off = rec_mem.take_n<uint32_t>(dir_cols * nrb1);
-  rec.dir_count = rec_mem.take_n<uint32_t>(map_blocks);
+  rec.count = rec_mem.take_n<uint32_t>(ncount);
 
   WC_HIP_CHECK(hipMalloc(&d_ctr, sizeof(DevCounters)));
   WC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_ctr), sizeof(DevCounters), hipHostMallocDefault));
@@ -167,14 +163,15 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   WC_HIP_CHECK(hipMemsetAsync(d_ctr, 0, sizeof(DevCounters), s));
   pass_rec = rec;
   pass_rec.cursor = &d_ctr->records;
-  pass_rec.dir_per_block = dir_per_block_for(len, blocks);
+  pass_rec.subcap = (uint32_t)std::min<uint64_t>(rec.cap / ((uint64_t)blocks << log2_rb), 0xFFFFFFFFull);
+  WC_CHECK(pass_rec.subcap > 0, "shuffle record capacity below one record per (map block, bucket)");
   MapArgs m{text, len, avail, prev, log2_rb, pass_rec, d_ctr->flags, &d_ctr->tokens, ablate_map, d_stamps};
   if (map_dec) launch_map_decoupled(m, blocks, s);
   else launch_map(m, blocks, s);
   if (sync_debug) {  // WC_SYNC_DEBUG: attribute a device fault to a kernel and a chunk
     const hipError_t e = hipStreamSynchronize(s);
-    fprintf(stderr, "[wc] map    base=%llu len=%llu avail=%llu blocks=%u J=%u -> %s\n", (unsigned long long)base,
-            (unsigned long long)len, (unsigned long long)avail, blocks, pass_rec.dir_per_block, hipGetErrorString(e));
+    fprintf(stderr, "[wc] map    base=%llu len=%llu avail=%llu blocks=%u subcap=%u -> %s\n", (unsigned long long)base,
+            (unsigned long long)len, (unsigned long long)avail, blocks, pass_rec.subcap, hipGetErrorString(e));
     WC_HIP_CHECK(e);
   }
   ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,

@@ -53,13 +53,6 @@ struct Engine::Impl {
   uint64_t rec_total = 0;
   Records rec{};       // full-capacity views
   Records pass_rec{};  // views of the current map/reduce pass
-  uint32_t dir_per_block_max = 0;
-  // Flush directory columns per map block: at most one flush per 16 KiB of the
-  // block's text, doubled (a full region re-runs the chunk in halves anyway).
-  static uint32_t dir_per_block_for(uint64_t len, uint32_t blocks) {
-    const uint64_t per_block = (len + blocks - 1) / blocks;
-    return (uint32_t)(2 * ((per_block + 16383) / 16384) + 8);
-  }
   DeviceArena rec_mem;
 
   // counters + pinned mirror

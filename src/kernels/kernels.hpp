@@ -47,20 +47,19 @@ struct Rec {
   uint64_t k0, k1, co;
 };
 
-// Shuffle output.  Every combiner flush of map block p writes ONE contiguous,
-// bucket-sorted chunk of records (coalesced stores) and a directory entry j:
-//   dir_base[p * dir_per_block + j]                      first record of the chunk
-//   dir_off[(b * map_blocks + p) * dir_per_block + j]    start of bucket b in it (b = 0..B)
-// Bucket-major directory rows let the reducer of bucket b read its run
-// boundaries for consecutive flushes with coalesced loads.
+// Shuffle output.  The record store of a pass is split into one sub-region of
+// `subcap` records per (map block p, shuffle bucket b):
+//   recs[(p * nb + b) * subcap + i],  i < count[p * nb + b]
+// A map flush appends each emitted slot to its bucket's sub-region through a
+// per-bucket LDS cursor (no histogram, no scan, no directory); the reducer of
+// bucket b reads one contiguous run per map block.  A full sub-region sets
+// FLAG_REGION_OVF and the host re-runs the chunk in halves.
 struct Records {
   Rec* recs;
-  unsigned long long* cursor;  // records allocated so far (device counter)
-  uint64_t cap;                // record capacity
-  uint64_t* dir_base;
-  uint32_t* dir_off;
-  uint32_t* dir_count;  // [map_blocks] flushes written per block
-  uint32_t dir_per_block;
+  unsigned long long* cursor;  // records emitted (stats)
+  uint64_t cap;                // record capacity of the store
+  uint32_t* count;             // [map_blocks * nb] records appended per sub-region
+  uint32_t subcap;             // records per sub-region (cap / (map_blocks * nb) of the pass)
 };
 
 // Running key table: n_buckets x TAB_SLOTS open-addressing slices.

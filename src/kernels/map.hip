@@ -42,18 +42,15 @@ struct MapLds {
   uint32_t cnt[MAP_SLOTS];
   uint32_t off[MAP_SLOTS];
   uint16_t list[MAP_WAVES][MAP_LIST];  // token rounds: wave-relative position | min(length, 31) << 11
-  uint32_t boff[MAX_REC_BUCKETS + 4];  // flush: bucket counts -> exclusive offsets (+ total); 0 between flushes
+  uint32_t bcur[MAX_REC_BUCKETS];  // records appended to each bucket's sub-region (persistent)
   uint32_t fail[MAP_THREADS];  // bit i of word t: token at tile byte 32 t + i must be retried
   uint8_t tile[MAP_TILE + MAP_HALO + 16];  // +16: tile8() reads one word past
-  uint32_t wsum[MAP_WAVES];
   uint32_t occupied;
+  uint32_t flush_kept;  // flush: sticky slots kept (-> occupied)
   uint32_t sticky;  // slots promoted to sticky (budget counter)
   uint32_t occ_before, last_new;  // adaptive flush: keys added by the last tile
   uint32_t prev;
-  uint32_t flush_ok;
-  uint32_t nflush;  // directory entries written by this block
-  uint64_t used;    // records written into this block's region
-  uint64_t flush_base;
+  unsigned long long used;  // records emitted by this block (stats)
   unsigned long long tokens;
 };
 static_assert(sizeof(MapLds) <= 160 * 1024 / MAP_BLOCKS_PER_CU, "map blocks per CU must fit its LDS");
@@ -66,13 +63,13 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
   if (ST && tid < MAP_STAMP_N) st_acc[tid] = 0;
   clear_slots(L);
   L.fail[tid] = 0;
-  for (uint32_t b = tid; b < MAX_REC_BUCKETS + 4; b += MAP_THREADS) L.boff[b] = 0;
+  for (uint32_t b = tid; b < MAX_REC_BUCKETS; b += MAP_THREADS) L.bcur[b] = 0;
   if (tid == 0) {
     L.occupied = 0;
     L.sticky = 0;
     L.last_new = 0;
     L.tokens = 0;
-    L.nflush = 0;
+    L.flush_kept = 0;
     L.used = 0;
   }
 
@@ -266,9 +263,9 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  
   }
   if (tid == 0) {
     atomicAdd(a.tokens, L.tokens);
-    atomicAdd(a.rec.cursor, (unsigned long long)L.used);  // stats: records after the combiner
-    a.rec.dir_count[blockIdx.x] = L.nflush;
+    atomicAdd(a.rec.cursor, L.used);  // stats: records after the combiner
   }
+  publish_bucket_counts(L, a);
 }
 
 }  // namespace dev

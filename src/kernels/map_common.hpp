@@ -2,8 +2,8 @@
 // synchronous tiles; map_dec.hip: wave-decoupled units): delimiter masks, keys
 // from an LDS text buffer, the LDS combiner (probe / claim / count) and the
 // shuffle-write flush.  Functions touching the combiner take the kernel's LDS
-// struct as a template parameter; it must provide key, tag, cnt, off, boff,
-// wsum, occupied, sticky, flush_ok, nflush, used and flush_base.
+// struct as a template parameter; it must provide key, tag, cnt, off, bcur,
+// occupied, sticky, flush_kept and used.
 #pragma once
 #include "kernels.hpp"
 #include "keys.hpp"
@@ -108,116 +108,83 @@ __device__ __forceinline__ void bsync(PhaseClock<ST>& clk, int phase) {
   clk.lap(MS_BARRIER);
 }
 
-// Shuffle write of the combiner table: one contiguous bucket-sorted chunk.
-// Four block barriers: bucket histogram | wave sums of the scan | offsets +
-// region | records written (then the histogram is re-zeroed).  trailing_sync
-// adds a fifth when inserts follow immediately (retry path).
+// Shuffle write of the combiner table: every emitted slot is appended to its
+// bucket's sub-region of this block (Records) through a per-bucket LDS cursor
+// (L.bcur, persistent across flushes) — one pass, one LDS atomic per record, no
+// histogram / scan / directory.  Sticky slots (hot keys) stay and keep
+// counting until the block's final flush; a slot that counted MAP_PROMOTE
+// tokens in this window becomes sticky while the sticky budget lasts.  Two
+// block barriers (occupancy / statistics | trailing, only when inserts follow
+// immediately).
 template <bool ST, class LDS>
 __device__ void flush_table(LDS& L, const MapArgs& a, PhaseClock<ST>& clk, bool trailing_sync, bool final = false) {
-  static_assert(MAX_REC_BUCKETS < MAP_THREADS, "one bucket per thread in the scan");
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t nb = 1u << a.log2_rec_buckets;
-  uint32_t sb[MAP_SPT], sr[MAP_SPT], kept = 0;
-  if (a.ablate != 5) {  // 5 (profiling): flush = clear only
+  const uint64_t sub = a.rec.subcap;
+  Rec* const region = a.rec.recs + (uint64_t)blockIdx.x * nb * sub;
+  uint32_t kept = 0, emitted = 0;
 #pragma unroll
-    for (int j = 0; j < MAP_SPT; ++j) {
-      const int s = tid + j * MAP_THREADS;
-      sb[j] = 0xFFFFFFFFu;
-      const uint32_t tag = L.tag[s];
-      if (tag != 0) {
-        // Sticky slots (hot keys) stay and keep counting until the block's
-        // final flush; a slot that counted MAP_PROMOTE tokens in this window
-        // becomes sticky while the sticky budget lasts.
-        const uint32_t c = L.cnt[s];
-        bool stick = (c & MAP_STICKY) != 0;
-        if (!final && !stick && c >= MAP_PROMOTE && L.sticky < (uint32_t)MAP_STICKY_CAP &&
-            atomicAdd(&L.sticky, 1u) < (uint32_t)MAP_STICKY_CAP) {
-          L.cnt[s] = c | MAP_STICKY;
-          stick = true;
-        }
-        if (stick && !final) {
-          ++kept;
-        } else {
-          sb[j] = (tag >> 2) & (nb - 1u);  // == bucket_of(place_hash): bucket bits live in the tag
-          sr[j] = atomicAdd(&L.boff[sb[j]], 1u);
-        }
+  for (int j = 0; j < MAP_SPT; ++j) {
+    const int s = tid + j * MAP_THREADS;
+    const uint32_t tag = L.tag[s];
+    if (tag == 0) continue;
+    bool keep = false;
+    if (a.ablate != 5) {  // 5 (profiling): flush = clear only
+      const uint32_t c = L.cnt[s];
+      keep = (c & MAP_STICKY) != 0;
+      if (!final && !keep && c >= MAP_PROMOTE && L.sticky < (uint32_t)MAP_STICKY_CAP &&
+          atomicAdd(&L.sticky, 1u) < (uint32_t)MAP_STICKY_CAP) {
+        L.cnt[s] = c | MAP_STICKY;
+        keep = true;
       }
-    }
-    bsync(clk, MS_FL_HIST);
-    // exclusive scan of boff[0, nb): one bucket per thread
-    const uint32_t v = (uint32_t)tid < nb ? L.boff[tid] : 0u;
-    uint32_t x = v;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o);
-      if (lane >= o) x += y;
-    }
-    if (lane == 63) L.wsum[wave] = x;
-    bsync(clk, MS_FL_SCAN);
-    uint32_t before = 0, total = 0;
-#pragma unroll
-    for (int w = 0; w < MAP_WAVES; ++w) {
-      const uint32_t ws = L.wsum[w];
-      before += w < wave ? ws : 0u;
-      total += ws;
-    }
-    if ((uint32_t)tid <= nb) L.boff[tid] = before + x - v;  // boff[nb] = total
-    if (tid == 0) {
-      uint32_t ok = 0;
-      L.occupied = 0;
-      if (total) {
-        // block-private record region: no global cursor contention
-        const uint64_t region = a.rec.cap / gridDim.x;
-        const uint64_t base = (uint64_t)blockIdx.x * region + L.used;
-        const uint32_t j = L.nflush;
-        ok = (L.used + total <= region && j < a.rec.dir_per_block) ? 1u : 0u;
-        L.used += total;
-        if (ok) {
-          L.nflush = j + 1;
-          a.rec.dir_base[(size_t)blockIdx.x * a.rec.dir_per_block + j] = base;
+      keep = keep && !final;
+      if (!keep) {
+        const uint32_t b = (tag >> 2) & (nb - 1u);  // == bucket_of(place_hash): bucket bits live in the tag
+        const uint32_t pos = atomicAdd(&L.bcur[b], 1u);
+        if (pos < sub) {
+          const u64x2 kk = L.key[s];
+          Rec r;
+          r.k0 = kk.x;
+          r.k1 = kk.y;
+          r.co = ((uint64_t)(c & ~MAP_STICKY) << 32) | L.off[s];
+          region[(uint64_t)b * sub + pos] = r;
         } else {
           atomicOr(&a.flags[FLAG_REGION_OVF], 1u);
         }
-        L.flush_base = base;
-      }
-      L.flush_ok = ok;
-    }
-    bsync(clk, MS_FL_SCAN);
-    if (L.flush_ok) {
-      const uint32_t j = L.nflush - 1;
-      const size_t row = (size_t)gridDim.x * a.rec.dir_per_block;
-      if (a.ablate != 3 && (uint32_t)tid <= nb)
-        a.rec.dir_off[(size_t)tid * row + (size_t)blockIdx.x * a.rec.dir_per_block + j] = L.boff[tid];
-      const uint64_t base = L.flush_base;
-#pragma unroll
-      for (int k = 0; k < MAP_SPT; ++k) {
-        if (sb[k] == 0xFFFFFFFFu) continue;
-        const int s = tid + k * MAP_THREADS;
-        const u64x2 kk = L.key[s];
-        Rec r;
-        r.k0 = kk.x;
-        r.k1 = kk.y;
-        r.co = ((uint64_t)(L.cnt[s] & ~MAP_STICKY) << 32) | L.off[s];
-        a.rec.recs[base + L.boff[sb[k]] + sr[k]] = r;
+        ++emitted;
       }
     }
-    if (kept) atomicAdd(&L.occupied, kept);
-#pragma unroll
-    for (int k = 0; k < MAP_SPT; ++k) {  // own emitted slots only: no barrier needed before
-      if (sb[k] == 0xFFFFFFFFu) continue;
-      const int s = tid + k * MAP_THREADS;
+    if (keep) {
+      ++kept;
+    } else {  // own slot: no barrier needed before clearing it
       L.tag[s] = 0;
       L.key[s].y = K1_EMPTY;
       L.cnt[s] = 0;
       L.off[s] = 0xFFFFFFFFu;
     }
-  } else {
-    if (tid == 0) L.occupied = 0;
-    clear_slots(L);
   }
-  if (final && tid == 0) L.sticky = 0;
-  bsync(clk, MS_FL_WRITE);  // every thread done reading boff (and the slots cleared)
-  if ((uint32_t)tid <= nb) L.boff[tid] = 0;
+  for (int o = 32; o > 0; o >>= 1) {
+    kept += __shfl_down(kept, o);
+    emitted += __shfl_down(emitted, o);
+  }
+  if (lane == 0 && (kept | emitted)) {
+    atomicAdd(&L.flush_kept, kept);
+    atomicAdd(&L.used, (unsigned long long)emitted);
+  }
+  bsync(clk, MS_FL_WRITE);
+  if (tid == 0) {
+    L.occupied = L.flush_kept;
+    L.flush_kept = 0;
+    if (final) L.sticky = 0;
+  }
   if (trailing_sync) bsync(clk, MS_FL_WRITE);
+}
+
+// Block epilogue: this block's per-bucket record counts for the reducer.
+template <class LDS>
+__device__ __forceinline__ void publish_bucket_counts(LDS& L, const MapArgs& a) {
+  const uint32_t nb = 1u << a.log2_rec_buckets;
+  for (uint32_t b = threadIdx.x; b < nb; b += MAP_THREADS) a.rec.count[(size_t)blockIdx.x * nb + b] = L.bcur[b];
 }
 
 // Key of a token that does not end inside the 64-byte lane window: byte loop

@@ -20,6 +20,11 @@ constexpr int DEC_UNIT = 64 * MAP_BPL;  // text bytes per wave unit (2 KiB)
 constexpr int DEC_HALO = 64;            // bytes past the unit kept in LDS
 constexpr int DEC_BUF = DEC_UNIT + DEC_HALO + 16;  // +16: tile8() reads one word past
 constexpr uint32_t DEC_NONE = 0xFFFFFFFFu;
+#ifndef WC_DEC_TPL
+#define WC_DEC_TPL 2
+#endif
+constexpr uint32_t DEC_TPL = WC_DEC_TPL;  // list entries per lane per step (1 or 2)
+constexpr uint32_t DEC_STEP = 64 * DEC_TPL;
 #ifndef WC_DEC_FLUSH_EIGHTHS
 #define WC_DEC_FLUSH_EIGHTHS 4
 #endif
@@ -32,13 +37,12 @@ struct DecLds {
   uint32_t cnt[MAP_SLOTS];
   uint32_t off[MAP_SLOTS];
   uint16_t list[MAP_WAVES][MAP_LIST];
-  uint32_t boff[MAX_REC_BUCKETS + 4];
+  uint32_t bcur[MAX_REC_BUCKETS];  // records appended to each bucket's sub-region (persistent)
   uint32_t fail[MAP_THREADS];  // bit i of word t: token at unit byte 32 (t % 64) + i of wave t / 64 must be retried
   uint8_t buf[MAP_WAVES][DEC_BUF];
-  uint32_t wsum[MAP_WAVES];
-  uint32_t occupied, sticky, flush_ok, nflush;
+  uint32_t occupied, sticky, flush_kept;
   uint32_t flush_req, done_waves, next_unit;
-  uint64_t used, flush_base;
+  unsigned long long used;
   unsigned long long tokens;
 };
 static_assert(sizeof(DecLds) + 8 * MAP_STAMP_N <= 160 * 1024, "one decoupled map block per CU");
@@ -51,7 +55,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_decoupled(MapArgs a) {
   if (ST && tid < MAP_STAMP_N) st_acc[tid] = 0;
   clear_slots(L);
   L.fail[tid] = 0;
-  for (uint32_t b = tid; b < MAX_REC_BUCKETS + 4; b += MAP_THREADS) L.boff[b] = 0;
+  for (uint32_t b = tid; b < MAX_REC_BUCKETS; b += MAP_THREADS) L.bcur[b] = 0;
   const uint64_t nunits = (a.chunk_len + DEC_UNIT - 1) / DEC_UNIT;
   const uint64_t per = (nunits + gridDim.x - 1) / gridDim.x;
   const uint64_t u_begin = min((uint64_t)blockIdx.x * per, nunits), u_end = min(u_begin + per, nunits);
@@ -59,7 +63,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_decoupled(MapArgs a) {
     L.occupied = 0;
     L.sticky = 0;
     L.tokens = 0;
-    L.nflush = 0;
+    L.flush_kept = 0;
     L.used = 0;
     L.flush_req = 0;
     L.done_waves = 0;
@@ -173,7 +177,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_decoupled(MapArgs a) {
         clk.lap(MS_LIST);
       }
       // ---- one step: two list entries per lane ----
-      const bool h1 = j + lane < round_n, h2 = j + 64 + lane < round_n;
+      const bool h1 = j + lane < round_n, h2 = DEC_TPL > 1 && j + 64 + lane < round_n;
       const uint32_t e1 = h1 ? list[j + lane] : 0u, e2 = h2 ? list[j + 64 + lane] : 0u;
       const uint32_t q1 = e1 & 0x7FFu, q2 = e2 & 0x7FFu;
       uint64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
@@ -183,7 +187,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_decoupled(MapArgs a) {
         asm volatile("" ::"v"(a0), "v"(a1), "v"(b0), "v"(b1));
       }
       clk.lap(MS_KEYS);
-      j += 128;
+      j += DEC_STEP;
       if (j >= round_n) {
         wave_sync();  // entries read before the next round overwrites them
         base += MAP_LIST;
@@ -268,9 +272,9 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_decoupled(MapArgs a) {
   }
   if (tid == 0) {
     atomicAdd(a.tokens, L.tokens);
-    atomicAdd(a.rec.cursor, (unsigned long long)L.used);
-    a.rec.dir_count[blockIdx.x] = L.nflush;
+    atomicAdd(a.rec.cursor, L.used);
   }
+  publish_bucket_counts(L, a);
 }
 
 }  // namespace dev

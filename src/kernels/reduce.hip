@@ -6,10 +6,10 @@
 //
 //  wc_reduce_buckets  one 1024-thread block per table bucket (one per CU).
 //                     The bucket's 4096-slot slice of the running table is
-//                     loaded into LDS (144 KiB with tags), the bucket's run of
-//                     every map flush is gathered (directory -> wave scan of
-//                     run lengths -> 64 consecutive records per wave step)
-//                     and merged with LDS atomics (count +=, first = min), and
+//                     loaded into LDS (144 KiB with tags), the bucket's
+//                     contiguous record run of every map block is streamed
+//                     (RED_UNROLL x 64 records in flight per wave) and merged
+//                     with LDS atomics (count +=, first = min), and
 //                     the slice is written back.  New long words copy their
 //                     bytes into the key arena so keys outlive streamed chunks.
 //                     If a slice overflows it is NOT written back; the host
@@ -150,47 +150,20 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
 
   const uint32_t shift = a.tab.log2_buckets - a.log2_rec_buckets;  // table buckets per record bucket (log2)
   const uint32_t rb = b & ((1u << a.log2_rec_buckets) - 1u);       // buckets nest on the low bits
-  const uint32_t J = a.rec.dir_per_block;
-  const size_t row = (size_t)a.map_blocks * J;
-  const uint32_t* lo_row = a.rec.dir_off + (size_t)rb * row;
-  const uint32_t* hi_row = lo_row + row;
+  const uint32_t nrb = 1u << a.log2_rec_buckets;
+  const uint64_t sub = a.rec.subcap;
+  // one contiguous run per map block: sub-region (p, rb) of the record store
   for (uint32_t p = wave; p < a.map_blocks; p += nwaves) {
-    const uint32_t nf = a.rec.dir_count[p];
-    for (uint32_t j0 = 0; j0 < nf; j0 += 64) {
-      // one flush per lane: its run [lo, hi) of bucket rb
-      const uint32_t j = j0 + lane;
-      const size_t col = (size_t)p * J + j;
-      uint32_t len = 0;
-      uint64_t start = 0;
-      if (j < nf) {
-        const uint32_t lo = lo_row[col];
-        len = hi_row[col] - lo;
-        start = a.rec.dir_base[col] + lo;
-      }
-      // concatenate the 64 runs: inclusive scan of run lengths
-      uint32_t incl = len;
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-      }
-      const uint32_t total = __shfl(incl, 63);
-      const uint32_t excl = incl - len;
-      // RED_UNROLL x 64 records in flight per wave before any is merged
-      for (uint32_t k = 0; k < total; k += RED_UNROLL * 64) {
-        Rec rr[RED_UNROLL];
+    const uint32_t n = min(a.rec.count[(size_t)p * nrb + rb], (uint32_t)sub);
+    const Rec* run = a.rec.recs + ((uint64_t)p * nrb + rb) * sub;
+    // RED_UNROLL x 64 records in flight per wave before any is merged
+    for (uint32_t k = 0; k < n; k += RED_UNROLL * 64) {
+      Rec rr[RED_UNROLL];
 #pragma unroll
-        for (int u = 0; u < RED_UNROLL; ++u) {
-          const uint32_t q = min(k + u * 64 + lane, total - 1);  // clamp: always a valid record
-          int o = 0;  // owner lane: the last lane whose exclusive prefix is <= q
-          for (int step = 32; step > 0; step >>= 1)
-            if (__shfl(excl, o + step) <= q) o += step;
-          const uint64_t ostart = ((uint64_t)__shfl((uint32_t)(start >> 32), o) << 32) | __shfl((uint32_t)start, o);
-          rr[u] = a.rec.recs[ostart + (q - __shfl(excl, o))];
-        }
+      for (int u = 0; u < RED_UNROLL; ++u) rr[u] = run[min(k + u * 64 + lane, n - 1)];  // clamp: always valid
 #pragma unroll
-        for (int u = 0; u < RED_UNROLL; ++u)
-          if (k + u * 64 + lane < total) merge_record(L, a, b, rr[u], shift);
-      }
+      for (int u = 0; u < RED_UNROLL; ++u)
+        if (k + u * 64 + lane < n) merge_record(L, a, b, rr[u], shift);
     }
   }
   __syncthreads();
