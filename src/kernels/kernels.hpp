@@ -16,12 +16,17 @@
 namespace wc {
 
 // ---- geometry (gfx950: wave64, 256 CUs, 160 KiB LDS per CU) -------------------
-constexpr int MAP_THREADS = 1024;                    // 16 waves, one block per CU
-constexpr int MAP_BLOCKS_PER_CU = 1;
+#ifndef WC_MAP_THREADS
+#define WC_MAP_THREADS 1024
+#define WC_MAP_BLOCKS_PER_CU 1
+#define WC_MAP_SLOTS 4096
+#endif
+constexpr int MAP_THREADS = WC_MAP_THREADS;          // 16 waves, one block per CU
+constexpr int MAP_BLOCKS_PER_CU = WC_MAP_BLOCKS_PER_CU;
 constexpr int MAP_BPL = 32;                          // text bytes per lane
 constexpr int MAP_TILE = MAP_THREADS * MAP_BPL;      // 32 KiB LDS text tile
 constexpr int MAP_HALO = 256;                        // bytes past the tile kept in LDS
-constexpr int MAP_SLOTS = 4096;                      // LDS combiner slots (groups of 8)
+constexpr int MAP_SLOTS = WC_MAP_SLOTS;              // LDS combiner slots (groups of 8)
 constexpr int MAP_GROUPS = MAP_SLOTS / 4;
 #ifndef WC_MAP_FILL_EIGHTHS
 #define WC_MAP_FILL_EIGHTHS 6

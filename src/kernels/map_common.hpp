@@ -12,7 +12,10 @@ namespace wc {
 namespace dev {
 
 constexpr int MAP_WAVES = MAP_THREADS / 64;
-constexpr int MAP_LIST = 256;                    // token-list entries per wave per round (u16)
+#ifndef WC_MAP_LIST
+#define WC_MAP_LIST 256
+#endif
+constexpr int MAP_LIST = WC_MAP_LIST;            // token-list entries per wave per round (u16)
 constexpr int MAP_GS = 8;                        // slots per probe group
 constexpr int MAP_NGROUPS = MAP_SLOTS / MAP_GS;  // 256
 constexpr int MAP_SPT = MAP_SLOTS / MAP_THREADS; // table slots per thread in a flush

@@ -14,8 +14,13 @@ while [ $# -ge 2 ]; do
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Isrc $flags -c $f -o $o &
     objs="$objs $o"
   done
+  cpp=""
+  for f in src/common/*.cpp src/engine/*.cpp src/dist/*.cpp src/cpu/*.cpp src/io/*.cpp src/output/*.cpp src/capi.cpp; do
+    o=$d/cpp_$(echo $f | tr '/' '_' | sed 's/\.cpp$//').o
+    g++ -O3 -std=c++17 -fPIC -D__HIP_PLATFORM_AMD__ -Iinclude -Isrc -I/opt/rocm/include $flags -c $f -o $o &
+    cpp="$cpp $o"
+  done
   wait
-  cpp=$(ls build/common/*.o build/engine/*.o build/dist/*.o build/cpu/*.o build/io/*.o build/output/*.o build/capi.o)
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o cuda_mapreduce_amd/lib/variants/libwc_$name.so $objs $cpp \
     -L/opt/rocm/lib -lrccl -lrocprofiler-sdk-roctx -lamdhip64 -lpthread -Wl,-rpath,/opt/rocm/lib
   echo built $name
