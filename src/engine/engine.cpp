@@ -76,8 +76,9 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   rec_total = std::max<uint64_t>(opt.min_records, (uint64_t)((double)opt.chunk_bytes * opt.records_per_byte));
   // record store + per-(block, bucket) counts; partitions follow the table up to the max
   const size_t ncount = (size_t)map_blocks * MAX_REC_BUCKETS;
-  rec_mem.reserve(rec_total * sizeof(Rec) + ncount * 4 + 8192);
+  rec_mem.reserve(rec_total * (sizeof(Rec) + sizeof(Rec16)) + ncount * 4 + 8192);
   rec.recs = rec_mem.take_n<Rec>(rec_total);
+  rec.recs16 = rec_mem.take_n<Rec16>(rec_total);
   rec.cap = rec_total;
   rec.count = rec_mem.take_n<uint32_t>(ncount);
 
@@ -163,7 +164,7 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   WC_HIP_CHECK(hipMemsetAsync(d_ctr, 0, sizeof(DevCounters), s));
   pass_rec = rec;
   pass_rec.cursor = &d_ctr->records;
-  pass_rec.subcap = (uint32_t)std::min<uint64_t>(rec.cap / ((uint64_t)blocks << log2_rb), 0xFFFFFFFFull);
+  pass_rec.subcap = (uint32_t)std::min<uint64_t>(rec.cap / ((uint64_t)blocks << log2_rb), 0xFFFFull);
   WC_CHECK(pass_rec.subcap > 0, "shuffle record capacity below one record per (map block, bucket)");
   MapArgs m{text, len, avail, prev, log2_rb, pass_rec, d_ctr->flags, &d_ctr->tokens, ablate_map, d_stamps};
   if (map_dec) launch_map_decoupled(m, blocks, s);

@@ -51,20 +51,28 @@ enum : int { FLAG_REGION_OVF = 0, FLAG_ARENA_OVF = 1, FLAG_TABLE_OVF = 2, FLAG_M
 struct Rec {
   uint64_t k0, k1, co;
 };
+// Short-key record (k1 = length <= 8): 16 bytes, w = off | len << 32 | count << 36.
+struct Rec16 {
+  uint64_t k0, w;
+};
+constexpr uint32_t REC16_MAX_COUNT = (1u << 28) - 1;  // counts of one map window stay far below
 
-// Shuffle output.  The record store of a pass is split into one sub-region of
-// `subcap` records per (map block p, shuffle bucket b):
-//   recs[(p * nb + b) * subcap + i],  i < count[p * nb + b]
+// Shuffle output.  Two record stores (short keys as 16-B Rec16, long keys as
+// 24-B Rec), each split into one sub-region of `subcap` records per (map block
+// p, shuffle bucket b):
+//   recs16[(p * nb + b) * subcap + i],  i < count[p * nb + b] & 0xFFFF
+//   recs  [(p * nb + b) * subcap + i],  i < count[p * nb + b] >> 16
 // A map flush appends each emitted slot to its bucket's sub-region through a
 // per-bucket LDS cursor (no histogram, no scan, no directory); the reducer of
 // bucket b reads one contiguous run per map block.  A full sub-region sets
 // FLAG_REGION_OVF and the host re-runs the chunk in halves.
 struct Records {
-  Rec* recs;
+  Rec* recs;                   // long-key records
+  Rec16* recs16;               // short-key records
   unsigned long long* cursor;  // records emitted (stats)
-  uint64_t cap;                // record capacity of the store
-  uint32_t* count;             // [map_blocks * nb] records appended per sub-region
-  uint32_t subcap;             // records per sub-region (cap / (map_blocks * nb) of the pass)
+  uint64_t cap;                // record capacity of each store
+  uint32_t* count;             // [map_blocks * nb] short (low 16 bits) | long (high 16) records appended
+  uint32_t subcap;             // records per sub-region, <= 65535 (cap / (map_blocks * nb) of the pass)
 };
 
 // Running key table: n_buckets x TAB_SLOTS open-addressing slices.

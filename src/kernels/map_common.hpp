@@ -125,6 +125,7 @@ __device__ void flush_table(LDS& L, const MapArgs& a, PhaseClock<ST>& clk, bool 
   const uint32_t nb = 1u << a.log2_rec_buckets;
   const uint64_t sub = a.rec.subcap;
   Rec* const region = a.rec.recs + (uint64_t)blockIdx.x * nb * sub;
+  Rec16* const region16 = a.rec.recs16 + (uint64_t)blockIdx.x * nb * sub;
   uint32_t kept = 0, emitted = 0;
 #pragma unroll
   for (int j = 0; j < MAP_SPT; ++j) {
@@ -143,14 +144,24 @@ __device__ void flush_table(LDS& L, const MapArgs& a, PhaseClock<ST>& clk, bool 
       keep = keep && !final;
       if (!keep) {
         const uint32_t b = (tag >> 2) & (nb - 1u);  // == bucket_of(place_hash): bucket bits live in the tag
-        const uint32_t pos = atomicAdd(&L.bcur[b], 1u);
+        const u64x2 kk = L.key[s];
+        const bool shortk = kk.y <= 8 && (c & ~MAP_STICKY) <= REC16_MAX_COUNT;  // k1 = length: a 16-byte record
+        const uint32_t packed = atomicAdd(&L.bcur[b], shortk ? 1u : 0x10000u);
+        const uint32_t pos = shortk ? (packed & 0xFFFFu) : (packed >> 16);
         if (pos < sub) {
-          const u64x2 kk = L.key[s];
-          Rec r;
-          r.k0 = kk.x;
-          r.k1 = kk.y;
-          r.co = ((uint64_t)(c & ~MAP_STICKY) << 32) | L.off[s];
-          region[(uint64_t)b * sub + pos] = r;
+          const uint64_t cnt = c & ~MAP_STICKY;
+          if (shortk) {
+            Rec16 r;
+            r.k0 = kk.x;
+            r.w = (uint64_t)L.off[s] | (kk.y << 32) | (cnt << 36);
+            region16[(uint64_t)b * sub + pos] = r;
+          } else {
+            Rec r;
+            r.k0 = kk.x;
+            r.k1 = kk.y;
+            r.co = (cnt << 32) | L.off[s];
+            region[(uint64_t)b * sub + pos] = r;
+          }
         } else {
           atomicOr(&a.flags[FLAG_REGION_OVF], 1u);
         }

@@ -154,9 +154,28 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   const uint64_t sub = a.rec.subcap;
   // one contiguous run per map block: sub-region (p, rb) of the record store
   for (uint32_t p = wave; p < a.map_blocks; p += nwaves) {
-    const uint32_t n = min(a.rec.count[(size_t)p * nrb + rb], (uint32_t)sub);
-    const Rec* run = a.rec.recs + ((uint64_t)p * nrb + rb) * sub;
-    // RED_UNROLL x 64 records in flight per wave before any is merged
+    const uint32_t packed = a.rec.count[(size_t)p * nrb + rb];
+    const uint64_t sr = ((uint64_t)p * nrb + rb) * sub;
+    // short-key records (16 B): k1 = length, count and offset packed in w
+    const uint32_t n16 = min(packed & 0xFFFFu, (uint32_t)sub);
+    const Rec16* run16 = a.rec.recs16 + sr;
+    for (uint32_t k = 0; k < n16; k += RED_UNROLL * 64) {
+      Rec16 rr[RED_UNROLL];
+#pragma unroll
+      for (int u = 0; u < RED_UNROLL; ++u) rr[u] = run16[min(k + u * 64 + lane, n16 - 1)];  // clamp: always valid
+#pragma unroll
+      for (int u = 0; u < RED_UNROLL; ++u) {
+        if (k + u * 64 + lane >= n16) continue;
+        Rec r;
+        r.k0 = rr[u].k0;
+        r.k1 = (rr[u].w >> 32) & 0xFu;
+        r.co = ((rr[u].w >> 36) << 32) | (rr[u].w & 0xFFFFFFFFull);
+        merge_record(L, a, b, r, shift);
+      }
+    }
+    // long-key records (24 B)
+    const uint32_t n = min(packed >> 16, (uint32_t)sub);
+    const Rec* run = a.rec.recs + sr;
     for (uint32_t k = 0; k < n; k += RED_UNROLL * 64) {
       Rec rr[RED_UNROLL];
 #pragma unroll

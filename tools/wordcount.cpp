@@ -23,6 +23,8 @@ const char* kUsage =
     "usage: wordcount [FILE] [options]\n"
     "  FILE                    input text (default: test.txt, as the reference)\n"
     "  --gpus N                shard across N GPUs, merged with RCCL (default 1)\n"
+    "  --merge shuffle|dense   cross-GPU merge: all-to-all by key owner (default) or\n"
+    "                          dictionary union + reduce-scatter / all-gather\n"
     "  --cpu                   single-thread CPU oracle (hash map)\n"
     "  --compat=reference      CPU emulation of the reference program's quirks\n"
     "  --echo | --no-echo      echo the input after 'Input Data:' (default: echo)\n"
@@ -54,6 +56,7 @@ struct Cli {
   int gpus = 1;
   bool cpu = false, compat = false, echo = true, list = true, host_staged = false;
   uint64_t top = 0, chunk = 1ull << 30;
+  uint32_t merge_mode = 0;
   bool synthetic = false;
   uint64_t synth_bytes = 0;
   wc::SynthSpec spec;
@@ -73,6 +76,12 @@ Cli parse(int argc, char** argv) {
       std::exit(0);
     } else if (a == "--gpus") c.gpus = std::stoi(need("--gpus"));
     else if (a == "--cpu") c.cpu = true;
+    else if (a == "--merge") {
+      const std::string m = need("--merge");
+      if (m == "shuffle") c.merge_mode = 0;
+      else if (m == "dense") c.merge_mode = 1;
+      else wc::fail("--merge expects shuffle or dense, got " + m);
+    }
     else if (a == "--compat=reference") c.compat = true;
     else if (a == "--echo") c.echo = true;
     else if (a == "--no-echo") c.echo = false;
@@ -150,6 +159,7 @@ int run(const Cli& c) {
         wc::Options o;
         o.device = devs[r];
         o.chunk_bytes = c.chunk;
+        o.merge_mode = c.merge_mode;
         wc::Engine eng(o);
         if (c.synthetic) {
           // shard at segment granularity: every segment ends with a delimiter
