@@ -38,16 +38,25 @@ __global__ void __launch_bounds__(RS_THREADS) wc_radix_hist(const uint64_t* keys
 }
 
 // Single-block exclusive scan of m words (digit-major histogram): each
-// thread scans a contiguous run of ceil(m / 1024) words, one block scan of the
-// run totals, then each thread rewrites its run — one pass instead of m / 1024
-// barrier-separated steps.
+// thread scans a contiguous run of ceil(m / 1024) words held in registers (all
+// loads in flight at once when the run is <= 16 words), one block scan of the
+// run totals, then each thread rewrites its run.
 __global__ void __launch_bounds__(1024) wc_radix_scan(uint32_t* hist, uint64_t m) {
+  constexpr int REG = 16;
   __shared__ uint32_t wsum[16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t per = (m + 1023) / 1024;
   const uint64_t b = threadIdx.x * per, e = b + per < m ? b + per : m;
+  uint32_t v[REG];
   uint32_t tot = 0;
-  for (uint64_t i = b; i < e; ++i) tot += hist[i];
+  if (per <= REG) {
+#pragma unroll
+    for (int k = 0; k < REG; ++k) v[k] = b + k < e ? hist[b + k] : 0u;
+#pragma unroll
+    for (int k = 0; k < REG; ++k) tot += v[k];
+  } else {
+    for (uint64_t i = b; i < e; ++i) tot += hist[i];
+  }
   uint32_t x = tot;
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t y = __shfl_up(x, o);
@@ -57,10 +66,18 @@ __global__ void __launch_bounds__(1024) wc_radix_scan(uint32_t* hist, uint64_t m
   __syncthreads();
   uint32_t run = x - tot;
   for (int w = 0; w < wave; ++w) run += wsum[w];
-  for (uint64_t i = b; i < e; ++i) {
-    const uint32_t v = hist[i];
-    hist[i] = run;
-    run += v;
+  if (per <= REG) {
+#pragma unroll
+    for (int k = 0; k < REG; ++k) {
+      if (b + k < e) hist[b + k] = run;
+      run += v[k];
+    }
+  } else {
+    for (uint64_t i = b; i < e; ++i) {
+      const uint32_t t = hist[i];
+      hist[i] = run;
+      run += t;
+    }
   }
 }
 
