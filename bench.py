@@ -131,6 +131,15 @@ def main() -> int:
         ms, tokens_total = float(mx[0]), float(sm[1])
     else:
         tokens_total = float(tokens)
+    # Validation (untimed): the merged table's counts must sum to the words the
+    # map kernels counted — catches lost or duplicated counts in any stage.
+    res = eng.result(comm)
+    valid = True
+    if rank == 0:
+        valid = int(res.total) == int(tokens_total) and int(res.counts.sum()) == int(tokens_total)
+        if not valid:
+            print(f"bench: VALIDATION FAILED: table total {int(res.total)} (rows sum {int(res.counts.sum())}) "
+                  f"!= tokens {int(tokens_total)}", file=sys.stderr, flush=True)
     total_bytes = nbytes * world
     gbps = total_bytes / (ms / 1e3) / 1e9
     words = tokens_total / (ms / 1e3)
@@ -150,6 +159,7 @@ def main() -> int:
             "data": (f"synthetic ({'host pool replayed over PCIe' if host_staged else 'device-generated'} "
                      f"Zipf({zipf}) text, {vocab}-word vocabulary, seed {seed})"),
             "words_per_s": round(words, 1),
+            "validated": valid,
             "distinct_words": keys,
             "config": {
                 "model": f"wordcount-mapreduce/{cfg.name}",
@@ -171,7 +181,7 @@ def main() -> int:
     eng.close()
     if world > 1:
         dist.destroy_process_group()
-    return 0
+    return 0 if valid else 1
 
 
 if __name__ == "__main__":

@@ -19,15 +19,14 @@ constexpr int MAP_LIST = WC_MAP_LIST;            // token-list entries per wave 
 constexpr int MAP_GS = 8;                        // slots per probe group
 constexpr int MAP_NGROUPS = MAP_SLOTS / MAP_GS;  // 256
 constexpr int MAP_SPT = MAP_SLOTS / MAP_THREADS; // table slots per thread in a flush
-constexpr uint32_t MAP_STICKY = 0x80000000u;     // cnt flag: hot slot, kept across flushes
 #ifndef WC_MAP_PROMOTE
 #define WC_MAP_PROMOTE 5
 #endif
 #ifndef WC_MAP_STICKY_CAP
-#define WC_MAP_STICKY_CAP (MAP_SLOTS / 4)
+#define WC_MAP_STICKY_CAP (MAP_SLOTS * 3 / 16)
 #endif
-constexpr uint32_t MAP_PROMOTE = WC_MAP_PROMOTE;     // tokens in one window that make a slot sticky
-constexpr int MAP_STICKY_CAP = WC_MAP_STICKY_CAP;    // sticky budget per block (0 = off)
+constexpr uint32_t MAP_PROMOTE = WC_MAP_PROMOTE;     // tokens in one flush window that keep a key resident
+constexpr int MAP_STICKY_CAP = WC_MAP_STICKY_CAP;    // keys kept per flush and block (0 = off)
 constexpr uint32_t MAP_LONG = 31u;               // list length field: >= 31 bytes or past the lane window
 constexpr int MAP_WAVE_BYTES = 64 * MAP_BPL;     // text bytes owned by one wave (list positions are relative)
 static_assert(MAP_WAVE_BYTES <= 2048, "list entries hold 11-bit wave-relative positions");
@@ -111,21 +110,52 @@ __device__ __forceinline__ void bsync(PhaseClock<ST>& clk, int phase) {
   clk.lap(MS_BARRIER);
 }
 
-// Shuffle write of the combiner table: every emitted slot is appended to its
-// bucket's sub-region of this block (Records) through a per-bucket LDS cursor
-// (L.bcur, persistent across flushes) — one pass, one LDS atomic per record, no
-// histogram / scan / directory.  Sticky slots (hot keys) stay and keep
-// counting until the block's final flush; a slot that counted MAP_PROMOTE
-// tokens in this window becomes sticky while the sticky budget lasts.  Two
-// block barriers (occupancy / statistics | trailing, only when inserts follow
-// immediately).
-template <bool ST, class LDS>
-__device__ void flush_table(LDS& L, const MapArgs& a, PhaseClock<ST>& clk, bool trailing_sync, bool final = false) {
+// Append one record (key, count, first offset) to bucket b's sub-region of this
+// block: a 16-byte record for short keys (k1 = length <= 8), else 24 bytes.
+// L.bcur[b] packs both cursors (short count | long count << 16).
+template <class LDS>
+__device__ __forceinline__ void emit_record(LDS& L, const MapArgs& a, uint32_t b, uint64_t k0, uint64_t k1,
+                                            uint64_t cnt, uint32_t off) {
+  const uint64_t sub = a.rec.subcap;
+  const uint64_t at = ((uint64_t)blockIdx.x << a.log2_rec_buckets | b) * sub;
+  const bool shortk = k1 <= 8 && cnt <= REC16_MAX_COUNT;
+  const uint32_t packed = atomicAdd(&L.bcur[b], shortk ? 1u : 0x10000u);
+  const uint32_t pos = shortk ? (packed & 0xFFFFu) : (packed >> 16);
+  if (pos < sub) {
+    if (shortk) {
+      Rec16 r;
+      r.k0 = k0;
+      r.w = (uint64_t)off | (k1 << 32) | (cnt << 36);
+      a.rec.recs16[at + pos] = r;
+    } else {
+      Rec r;
+      r.k0 = k0;
+      r.k1 = k1;
+      r.co = (cnt << 32) | off;
+      a.rec.recs[at + pos] = r;
+    }
+  } else {
+    atomicOr(&a.flags[FLAG_REGION_OVF], 1u);
+  }
+}
+
+// Shuffle write of the combiner table: every counted slot is appended to its
+// bucket's sub-region of this block (emit_record) — one pass, one LDS atomic
+// per record, no histogram / scan / directory.  A slot that counted
+// MAP_PROMOTE tokens in this window KEEPS its key (count and first offset
+// restart from zero) while the block's keep budget lasts, so hot keys stay
+// resident and adapt to the text: a key that cools down is evicted at the next
+// flush.  `final` evicts every slot.  Two block barriers (occupancy / budget |
+// trailing, only when inserts follow immediately); `between` runs on thread 0
+// between them.
+struct NoHook {
+  __device__ void operator()() const {}
+};
+template <bool ST, class LDS, class Hook = NoHook>
+__device__ void flush_table(LDS& L, const MapArgs& a, PhaseClock<ST>& clk, bool trailing_sync, bool final = false,
+                            Hook between = Hook()) {
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t nb = 1u << a.log2_rec_buckets;
-  const uint64_t sub = a.rec.subcap;
-  Rec* const region = a.rec.recs + (uint64_t)blockIdx.x * nb * sub;
-  Rec16* const region16 = a.rec.recs16 + (uint64_t)blockIdx.x * nb * sub;
   uint32_t kept = 0, emitted = 0;
 #pragma unroll
   for (int j = 0; j < MAP_SPT; ++j) {
@@ -135,46 +165,21 @@ __device__ void flush_table(LDS& L, const MapArgs& a, PhaseClock<ST>& clk, bool 
     bool keep = false;
     if (a.ablate != 5) {  // 5 (profiling): flush = clear only
       const uint32_t c = L.cnt[s];
-      keep = (c & MAP_STICKY) != 0;
-      if (!final && !keep && c >= MAP_PROMOTE && L.sticky < (uint32_t)MAP_STICKY_CAP &&
-          atomicAdd(&L.sticky, 1u) < (uint32_t)MAP_STICKY_CAP) {
-        L.cnt[s] = c | MAP_STICKY;
-        keep = true;
-      }
-      keep = keep && !final;
-      if (!keep) {
-        const uint32_t b = (tag >> 2) & (nb - 1u);  // == bucket_of(place_hash): bucket bits live in the tag
+      keep = !final && c >= MAP_PROMOTE && L.sticky < (uint32_t)MAP_STICKY_CAP &&
+             atomicAdd(&L.sticky, 1u) < (uint32_t)MAP_STICKY_CAP;
+      if (c) {
         const u64x2 kk = L.key[s];
-        const bool shortk = kk.y <= 8 && (c & ~MAP_STICKY) <= REC16_MAX_COUNT;  // k1 = length: a 16-byte record
-        const uint32_t packed = atomicAdd(&L.bcur[b], shortk ? 1u : 0x10000u);
-        const uint32_t pos = shortk ? (packed & 0xFFFFu) : (packed >> 16);
-        if (pos < sub) {
-          const uint64_t cnt = c & ~MAP_STICKY;
-          if (shortk) {
-            Rec16 r;
-            r.k0 = kk.x;
-            r.w = (uint64_t)L.off[s] | (kk.y << 32) | (cnt << 36);
-            region16[(uint64_t)b * sub + pos] = r;
-          } else {
-            Rec r;
-            r.k0 = kk.x;
-            r.k1 = kk.y;
-            r.co = (cnt << 32) | L.off[s];
-            region[(uint64_t)b * sub + pos] = r;
-          }
-        } else {
-          atomicOr(&a.flags[FLAG_REGION_OVF], 1u);
-        }
+        emit_record(L, a, (tag >> 2) & (nb - 1u), kk.x, kk.y, c, L.off[s]);  // bucket bits live in the tag
         ++emitted;
       }
     }
+    L.cnt[s] = 0;  // own slot: no barrier needed before resetting it
+    L.off[s] = 0xFFFFFFFFu;
     if (keep) {
       ++kept;
-    } else {  // own slot: no barrier needed before clearing it
+    } else {
       L.tag[s] = 0;
       L.key[s].y = K1_EMPTY;
-      L.cnt[s] = 0;
-      L.off[s] = 0xFFFFFFFFu;
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
@@ -189,7 +194,8 @@ __device__ void flush_table(LDS& L, const MapArgs& a, PhaseClock<ST>& clk, bool 
   if (tid == 0) {
     L.occupied = L.flush_kept;
     L.flush_kept = 0;
-    if (final) L.sticky = 0;
+    L.sticky = 0;
+    between();
   }
   if (trailing_sync) bsync(clk, MS_FL_WRITE);
 }
@@ -246,14 +252,16 @@ __device__ __forceinline__ void token_key(const uint8_t* buf, uint32_t buf_len, 
   }
 }
 
-// Combiner slot of (k0, k1) — claiming one if the key is absent — or -1 when
-// MAP_MAX_GROUP_PROBES groups are full.  Claim = ONE CAS of the tag; the
+// Combiner slot of (k0, k1) — claiming one if the key is absent and `admit` —
+// or -1 when MAP_MAX_GROUP_PROBES groups are full (or the key is absent and
+// !admit).  Claim = ONE CAS of the tag; the
 // claimer then writes k0 before k1 (LDS executes one wave's writes in order,
 // and the reader loads the 16-byte key in one instruction), so a reader that
 // sees the new k1 also sees the new k0; one that sees the tag before the key
 // does not match and may claim a duplicate slot, which the reducer merges.
 template <class LDS>
-__device__ __forceinline__ int combiner_slot(LDS& L, uint64_t ph, uint64_t k0, uint64_t k1, bool& claimed) {
+__device__ __forceinline__ int combiner_slot(LDS& L, uint64_t ph, uint64_t k0, uint64_t k1, bool& claimed,
+                                             bool admit = true) {
   const uint32_t tag = map_tag(ph);
   uint32_t g = map_group(ph);
   claimed = false;
@@ -278,6 +286,7 @@ __device__ __forceinline__ int combiner_slot(LDS& L, uint64_t ph, uint64_t k0, u
       g = (g + 1) & (MAP_NGROUPS - 1);
       continue;
     }
+    if (!admit) return -1;
     const uint32_t s = g * MAP_GS + (__ffs(e) - 1);
     if (atomicCAS(&L.tag[s], 0u, tag) == 0u) {
       L.key[s].x = k0;

@@ -7,10 +7,17 @@
 // registers while tokenizing the current one.  Waves therefore never wait for
 // each other at a tile boundary (map.hip's phase clock: ~25 % of wave time was
 // spent at per-tile barriers).  The only block-wide synchronisation is the
-// combiner flush: when the shared table passes DEC_FLUSH_AT occupied slots (or a
-// probe sequence is full), the wave that notices sets a flag, every wave stops
+// combiner flush.  The table admits new keys until DEC_ADMIT_AT slots are
+// occupied; after that a token whose key is absent (or whose probe sequence is
+// full) becomes a record of its own, written straight to the shuffle store, so
+// no token ever waits for a flush.  Flushes only REFRESH the table: after
+// DEC_REFRESH direct records the wave that notices sets a flag, every wave stops
 // after its current step (its position in the unit is kept in registers), the
-// block flushes, failed tokens are retried and the waves resume.
+// block emits every counted slot, keys that were hot in the window stay
+// resident (see flush_table; at most MAP_STICKY_CAP, so DEC_ADMIT_AT leaves room
+// for keys that turn hot later) and the waves resume.  On Zipf text this cuts
+// flushes ~8x against flushing whenever the table is half full (tail keys are
+// singletons within a window anyway), and fewer probes per token.
 #include "map_common.hpp"
 
 namespace wc {
@@ -25,10 +32,15 @@ constexpr uint32_t DEC_NONE = 0xFFFFFFFFu;
 #endif
 constexpr uint32_t DEC_TPL = WC_DEC_TPL;  // list entries per lane per step (1 or 2)
 constexpr uint32_t DEC_STEP = 64 * DEC_TPL;
-#ifndef WC_DEC_FLUSH_EIGHTHS
-#define WC_DEC_FLUSH_EIGHTHS 4
+#ifndef WC_DEC_ADMIT_EIGHTHS
+#define WC_DEC_ADMIT_EIGHTHS 2
 #endif
-constexpr uint32_t DEC_FLUSH_AT = MAP_SLOTS * WC_DEC_FLUSH_EIGHTHS / 8;  // occupancy that requests a flush
+#ifndef WC_DEC_REFRESH
+#define WC_DEC_REFRESH 16384
+#endif
+constexpr uint32_t DEC_ADMIT_AT = MAP_SLOTS * WC_DEC_ADMIT_EIGHTHS / 8;  // occupancy that stops new claims
+static_assert(DEC_ADMIT_AT >= MAP_STICKY_CAP + 128, "room for new keys after every refresh");
+constexpr uint32_t DEC_REFRESH = WC_DEC_REFRESH;  // direct records that request a flush (table refresh)
 static_assert(DEC_UNIT <= 2048, "list entries hold 11-bit unit-relative positions");
 
 struct DecLds {
@@ -38,14 +50,29 @@ struct DecLds {
   uint32_t off[MAP_SLOTS];
   uint16_t list[MAP_WAVES][MAP_LIST];
   uint32_t bcur[MAX_REC_BUCKETS];  // records appended to each bucket's sub-region (persistent)
-  uint32_t fail[MAP_THREADS];  // bit i of word t: token at unit byte 32 (t % 64) + i of wave t / 64 must be retried
   uint8_t buf[MAP_WAVES][DEC_BUF];
   uint32_t occupied, sticky, flush_kept;
-  uint32_t flush_req, done_waves, next_unit;
+  uint32_t flush_req, done_waves, next_unit, direct;
   unsigned long long used;
   unsigned long long tokens;
 };
 static_assert(sizeof(DecLds) + 8 * MAP_STAMP_N <= 160 * 1024, "one decoupled map block per CU");
+
+// Count one token in the combiner or, when its key is absent and the table
+// admits no new keys (or its probe sequence is full), append it straight to
+// the shuffle records as (key, 1, offset).  Returns true for a direct record.
+__device__ __forceinline__ bool combine_or_emit(DecLds& L, const MapArgs& a, uint64_t k0, uint64_t k1, uint32_t off,
+                                                bool admit, bool& claimed) {
+  const uint64_t ph = place_hash(k0, k1);
+  const int s = combiner_slot(L, ph, k0, k1, claimed, admit);
+  if (s >= 0) {
+    atomicAdd(&L.cnt[s], 1u);  // results unused: no-return ds_add / ds_min
+    atomicMin(&L.off[s], off);
+    return false;
+  }
+  emit_record(L, a, ((uint32_t)ph >> 2) & ((1u << a.log2_rec_buckets) - 1u), k0, k1, 1, off);
+  return true;
+}
 
 template <bool ST>
 __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_decoupled(MapArgs a) {
@@ -54,7 +81,6 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_decoupled(MapArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (ST && tid < MAP_STAMP_N) st_acc[tid] = 0;
   clear_slots(L);
-  L.fail[tid] = 0;
   for (uint32_t b = tid; b < MAX_REC_BUCKETS; b += MAP_THREADS) L.bcur[b] = 0;
   const uint64_t nunits = (a.chunk_len + DEC_UNIT - 1) / DEC_UNIT;
   const uint64_t per = (nunits + gridDim.x - 1) / gridDim.x;
@@ -68,6 +94,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_decoupled(MapArgs a) {
     L.flush_req = 0;
     L.done_waves = 0;
     L.next_unit = 0;
+    L.direct = 0;
   }
   __syncthreads();
 
@@ -103,6 +130,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_decoupled(MapArgs a) {
   uint32_t starts = 0, bits = 0, k = 0, wave_total = 0, base = 0, round_n = 0, j = 0, prevb = 0x20;
   uint64_t u0 = 0;
   bool counted = false;
+  uint32_t occ_seen = 0;  // wave's latest view of L.occupied (claims stop at DEC_ADMIT_AT)
   const uint32_t pbase = lane * MAP_BPL;
 
   for (;;) {
@@ -196,20 +224,20 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_decoupled(MapArgs a) {
         sink ^= place_hash(a0, a1) + place_hash(b0, b1);
         continue;
       }
-      bool c1 = false, c2 = false, f = false;
-      if (h1 && !combine(L, a0, a1, (uint32_t)(u0 + q1), c1)) {
-        atomicOr(&L.fail[wave * 64 + (q1 >> 5)], 1u << (q1 & 31));
-        f = true;
-      }
-      if (h2 && !combine(L, b0, b1, (uint32_t)(u0 + q2), c2)) {
-        atomicOr(&L.fail[wave * 64 + (q2 >> 5)], 1u << (q2 & 31));
-        f = true;
-      }
+      const bool admit = occ_seen < DEC_ADMIT_AT;
+      bool c1 = false, c2 = false, d1 = false, d2 = false;
+      if (h1) d1 = combine_or_emit(L, a, a0, a1, (uint32_t)(u0 + q1), admit, c1);
+      if (h2) d2 = combine_or_emit(L, a, b0, b1, (uint32_t)(u0 + q2), admit, c2);
       const uint32_t claims = (uint32_t)__popcll(__ballot(c1)) + (uint32_t)__popcll(__ballot(c2));
-      const bool anyf = __ballot(f) != 0;
-      if (lane == 0) {
-        const uint32_t occ = claims ? atomicAdd(&L.occupied, claims) + claims : 0u;
-        if (anyf || occ > DEC_FLUSH_AT) atomicOr(&L.flush_req, 1u);
+      const uint32_t direct = (uint32_t)__popcll(__ballot(d1)) + (uint32_t)__popcll(__ballot(d2));
+      if (claims | direct) {
+        uint32_t occ = 0, dir = 0;
+        if (lane == 0) {
+          if (claims) occ = atomicAdd(&L.occupied, claims) + claims;
+          if (direct) dir = atomicAdd(&L.direct, direct) + direct;
+          if (dir > DEC_REFRESH) atomicOr(&L.flush_req, 1u);
+        }
+        if (claims) occ_seen = __builtin_amdgcn_readfirstlane(occ);
       }
       clk.lap(MS_COMBINE);
     }
@@ -227,35 +255,19 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_decoupled(MapArgs a) {
       if constexpr (ST) {
         if (tid == 0) st_acc[MS_NFLUSH] += 1;
       }
-      flush_table(L, a, clk, true);  // every thread has read flush_req before its first barrier
-      if (tid == 0) L.flush_req = 0;
+      // cleared between the flush's barriers: every thread has read flush_req
+      // (first barrier) and none resumes before the trailing one
+      flush_table(L, a, clk, true, false, [&]() {
+        L.flush_req = 0;
+        L.used += L.direct;
+        L.direct = 0;
+      });
+      occ_seen = L.occupied;
       clk.lap(MS_FLUSH);
-      // owners retry the tokens whose probe sequence was full (the unit is still in buf)
-      uint32_t todo = L.fail[tid];
-      L.fail[tid] = 0;
-      uint32_t claims = 0;
-      bool f = false;
-      while (todo) {
-        const uint32_t i = __ffs(todo) - 1;
-        todo &= todo - 1;
-        const uint64_t rest = dm >> i;
-        const uint32_t len = rest ? min((uint32_t)__ffsll((unsigned long long)rest) - 1, MAP_LONG) : MAP_LONG;
-        uint64_t k0, k1;
-        token_key(buf, DEC_UNIT + DEC_HALO, a, u0, pbase + i, len, k0, k1);
-        bool c = false;
-        if (!combine(L, k0, k1, (uint32_t)(u0 + pbase + i), c)) {
-          atomicOr(&L.fail[tid], 1u << i);
-          f = true;
-        }
-        claims += c;
-      }
-      if (claims) atomicAdd(&L.occupied, claims);
-      if (f) atomicOr(&L.flush_req, 1u);  // retried again after the next flush
-      __syncthreads();
-      clk.lap(MS_RETRY);
     }
   }
   clk.lap(MS_TOP);
+  if (tid == 0) L.used += L.direct;
   if (L.occupied) flush_table(L, a, clk, false, true);  // final: sticky slots too
   clk.lap(MS_FLUSH);
   if constexpr (ST) {
