@@ -388,6 +388,7 @@ void Engine::reset() {
   launch_table_clear(im.table(), im.s);
   WC_HIP_CHECK(hipMemsetAsync(im.d_arena_cursor, 0, sizeof(unsigned long long), im.s));
   WC_HIP_CHECK(hipStreamSynchronize(im.s));
+  if (im.copy_s) WC_HIP_CHECK(hipStreamSynchronize(im.copy_s));  // a failed stream may have left copies
   im.st = Stats{};
   im.max_end = 0;
 }

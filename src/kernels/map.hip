@@ -52,6 +52,15 @@ struct MapLds {
   uint32_t prev;
   unsigned long long used;  // records emitted by this block (stats)
   unsigned long long tokens;
+  // slot state (flush_table): the bucket bits of place_hash live in the tag
+  __device__ int bucket(int s, uint32_t log2_nb) const {
+    const uint32_t t = tag[s];
+    return t ? (int)((t >> 2) & ((1u << log2_nb) - 1u)) : -1;
+  }
+  __device__ void evict(int s) {
+    tag[s] = 0;
+    key[s].y = K1_EMPTY;
+  }
 };
 static_assert(sizeof(MapLds) <= 160 * 1024 / MAP_BLOCKS_PER_CU, "map blocks per CU must fit its LDS");
 

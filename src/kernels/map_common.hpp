@@ -2,8 +2,9 @@
 // synchronous tiles; map_dec.hip: wave-decoupled units): delimiter masks, keys
 // from an LDS text buffer, the LDS combiner (probe / claim / count) and the
 // shuffle-write flush.  Functions touching the combiner take the kernel's LDS
-// struct as a template parameter; it must provide key, tag, cnt, off, bcur,
-// occupied, sticky, flush_kept and used.
+// struct as a template parameter; it must provide key, cnt, off, bcur,
+// occupied, sticky, flush_kept and used, plus the slot-state accessors
+// bucket(s, log2_buckets) (-1 = empty) and evict(s) of its probing scheme.
 #pragma once
 #include "kernels.hpp"
 #include "keys.hpp"
@@ -73,8 +74,7 @@ __device__ __forceinline__ void clear_slots(LDS& L) {
 #pragma unroll
   for (int k = 0; k < MAP_SPT; ++k) {
     const int s = threadIdx.x + k * MAP_THREADS;
-    L.tag[s] = 0;
-    L.key[s].y = K1_EMPTY;
+    L.evict(s);
     L.cnt[s] = 0;
     L.off[s] = 0xFFFFFFFFu;
   }
@@ -155,13 +155,12 @@ template <bool ST, class LDS, class Hook = NoHook>
 __device__ void flush_table(LDS& L, const MapArgs& a, PhaseClock<ST>& clk, bool trailing_sync, bool final = false,
                             Hook between = Hook()) {
   const int tid = threadIdx.x, lane = tid & 63;
-  const uint32_t nb = 1u << a.log2_rec_buckets;
   uint32_t kept = 0, emitted = 0;
 #pragma unroll
   for (int j = 0; j < MAP_SPT; ++j) {
     const int s = tid + j * MAP_THREADS;
-    const uint32_t tag = L.tag[s];
-    if (tag == 0) continue;
+    const int b = L.bucket(s, a.log2_rec_buckets);
+    if (b < 0) continue;
     bool keep = false;
     if (a.ablate != 5) {  // 5 (profiling): flush = clear only
       const uint32_t c = L.cnt[s];
@@ -169,18 +168,14 @@ __device__ void flush_table(LDS& L, const MapArgs& a, PhaseClock<ST>& clk, bool 
              atomicAdd(&L.sticky, 1u) < (uint32_t)MAP_STICKY_CAP;
       if (c) {
         const u64x2 kk = L.key[s];
-        emit_record(L, a, (tag >> 2) & (nb - 1u), kk.x, kk.y, c, L.off[s]);  // bucket bits live in the tag
+        emit_record(L, a, (uint32_t)b, kk.x, kk.y, c, L.off[s]);
         ++emitted;
       }
     }
     L.cnt[s] = 0;  // own slot: no barrier needed before resetting it
     L.off[s] = 0xFFFFFFFFu;
-    if (keep) {
-      ++kept;
-    } else {
-      L.tag[s] = 0;
-      L.key[s].y = K1_EMPTY;
-    }
+    if (keep) ++kept;
+    else L.evict(s);
   }
   for (int o = 32; o > 0; o >>= 1) {
     kept += __shfl_down(kept, o);

@@ -45,7 +45,7 @@ static_assert(DEC_UNIT <= 2048, "list entries hold 11-bit unit-relative position
 
 struct DecLds {
   u64x2 key[MAP_SLOTS];
-  uint32_t tag[MAP_SLOTS];
+  uint32_t tag[MAP_SLOTS];  // group g = tag[8g, 8g+8); 0 = empty
   uint32_t cnt[MAP_SLOTS];
   uint32_t off[MAP_SLOTS];
   uint16_t list[MAP_WAVES][MAP_LIST];
@@ -55,6 +55,15 @@ struct DecLds {
   uint32_t flush_req, done_waves, next_unit, direct;
   unsigned long long used;
   unsigned long long tokens;
+  // slot state (flush_table): the bucket bits of place_hash live in the tag
+  __device__ int bucket(int s, uint32_t log2_nb) const {
+    const uint32_t t = tag[s];
+    return t ? (int)((t >> 2) & ((1u << log2_nb) - 1u)) : -1;
+  }
+  __device__ void evict(int s) {
+    tag[s] = 0;
+    key[s].y = K1_EMPTY;
+  }
 };
 static_assert(sizeof(DecLds) + 8 * MAP_STAMP_N <= 160 * 1024, "one decoupled map block per CU");
 
