@@ -50,9 +50,19 @@ __device__ __forceinline__ uint64_t delim_mask8(uint64_t x) {
   return ((m >> 7) * 0x0102040810204080ull) >> 56;
 }
 
-// 8 bytes of the LDS tile starting at byte p: two aligned ds_read_b64 + funnel
-// shift (dynamic indexing of a register window would be lowered to scratch).
+// 8 bytes of the LDS tile starting at byte p (dynamic indexing of a register
+// window would be lowered to scratch).  Default: ONE unaligned ds_read_b64
+// (gfx950 runs HSA queues in unaligned-access mode, and the compiler emits it
+// for a byte-aligned memcpy); WC_TILE8_ALIGNED=1: two aligned reads + shift.
+#ifndef WC_TILE8_ALIGNED
+#define WC_TILE8_ALIGNED 0
+#endif
 __device__ __forceinline__ uint64_t tile8(const uint8_t* tile, uint32_t p) {
+  if (!WC_TILE8_ALIGNED) {
+    uint64_t v;
+    __builtin_memcpy(&v, tile + p, 8);
+    return v;
+  }
   const uint64_t* q = reinterpret_cast<const uint64_t*>(tile + (p & ~7u));
   const uint32_t sh = (p & 7) * 8;
   const uint64_t lo = q[0], hi = q[1];
