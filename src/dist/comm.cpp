@@ -64,6 +64,8 @@ class RcclComm final : public Comm {
   void broadcast(void* buf, size_t bytes, int root, hipStream_t s) override {
     if (bytes) WC_NCCL_CHECK(ncclBroadcast(buf, buf, bytes, ncclUint8, root, c_, s));
   }
+  void group_begin() override { WC_NCCL_CHECK(ncclGroupStart()); }
+  void group_end() override { WC_NCCL_CHECK(ncclGroupEnd()); }
   void barrier(hipStream_t s) override {
     WC_NCCL_CHECK(ncclAllReduce(scratch_, scratch_, 1, ncclUint64, ncclSum, c_, s));
     WC_HIP_CHECK(hipStreamSynchronize(s));

@@ -35,6 +35,10 @@ class Comm {
   virtual void alltoallv(const void* send, const size_t* send_off, const size_t* send_bytes, void* recv,
                          const size_t* recv_off, const size_t* recv_bytes, hipStream_t s) = 0;
   virtual void broadcast(void* buf, size_t bytes, int root, hipStream_t s) = 0;
+  // Bracket several collectives / point-to-point exchanges into ONE launch
+  // (RCCL group); no-op for backends that run each call on its own.
+  virtual void group_begin() {}
+  virtual void group_end() {}
   virtual void barrier(hipStream_t s) = 0;
 };
 

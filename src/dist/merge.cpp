@@ -208,8 +208,10 @@ void merge_cols_shuffle(Engine::Impl& im, Comm& comm, bool all_ranks) {
   uint8_t* recv_bytes = take_aligned<uint8_t>(A, rbt);
   launch_owner_scatter(im.cols.k0, im.cols.k1, im.cols.cnt, im.cols.first, im.cols.sref_off, im.cols.sref_len,
                        im.cols_arena, n, (uint32_t)W, d_cnt, d_cnt + C, send_rows, send_bytes, s);
+  comm.group_begin();  // rows and long-word bytes in one exchange
   comm.alltoallv(send_rows, so_r.data(), sb_r.data(), recv_rows, ro_r.data(), rb_r.data(), s);
   comm.alltoallv(send_bytes, so_b.data(), sb_b.data(), recv_bytes, ro_b.data(), rb_b.data(), s);
+  comm.group_end();
 
   // 3. owner-side merge
   uint32_t* state = take_aligned<uint32_t>(A, T);
@@ -234,16 +236,18 @@ void merge_cols_shuffle(Engine::Impl& im, Comm& comm, bool all_ranks) {
   launch_mrow_compact(recv_rows, state, tcnt, tfirst, T, d_base, d_base + W + 1, (uint32_t)W, merged, d_m, s);
 
   // 4. gather merged rows + bytes to rank 0 (and broadcast for all_ranks)
-  unsigned long long own[2] = {0, rbt};
-  WC_HIP_CHECK(hipMemcpyAsync(&own[0], d_m, 8, hipMemcpyDeviceToHost, s));
-  WC_HIP_CHECK(hipStreamSynchronize(s));  // base[] / own[] are pageable host memory
+  // (merged rows, bytes) of every owner: the row count stays on the device
+  // until this allgather, so one host sync serves both
+  const unsigned long long own_bytes = rbt;
   unsigned long long* d_own = take_aligned<unsigned long long>(A, 2);
   unsigned long long* d_owns = take_aligned<unsigned long long>(A, 2 * (size_t)W);
-  WC_HIP_CHECK(hipMemcpyAsync(d_own, own, 16, hipMemcpyHostToDevice, s));
+  WC_HIP_CHECK(hipMemcpyAsync(d_own, d_m, 8, hipMemcpyDeviceToDevice, s));
+  WC_HIP_CHECK(hipMemcpyAsync(d_own + 1, &own_bytes, 8, hipMemcpyHostToDevice, s));
   comm.allgather(d_own, d_owns, 16, s);
   std::vector<unsigned long long> owns(2 * (size_t)W);
   WC_HIP_CHECK(hipMemcpyAsync(owns.data(), d_owns, owns.size() * 8, hipMemcpyDeviceToHost, s));
-  WC_HIP_CHECK(hipStreamSynchronize(s));
+  WC_HIP_CHECK(hipStreamSynchronize(s));  // also: base[] / own_bytes are pageable host memory
+  const unsigned long long own[2] = {owns[2 * (size_t)R], own_bytes};
   std::vector<size_t> go_r(W, 0), gb_r(W, 0), go_b(W, 0), gb_b(W, 0), zs(W, 0);
   std::vector<size_t> sr(W, 0), sb(W, 0);
   uint64_t G = 0, GB = 0;
@@ -267,11 +271,15 @@ void merge_cols_shuffle(Engine::Impl& im, Comm& comm, bool all_ranks) {
   const bool have = R == 0 || all_ranks;
   MRow* grows = take_aligned<MRow>(A, G);
   uint8_t* gbytes = take_aligned<uint8_t>(A, GB);
+  comm.group_begin();
   comm.alltoallv(merged, zs.data(), sr.data(), grows, go_r.data(), gb_r.data(), s);
   comm.alltoallv(recv_bytes, zs.data(), sb.data(), gbytes, go_b.data(), gb_b.data(), s);
+  comm.group_end();
   if (all_ranks) {
+    comm.group_begin();
     comm.broadcast(grows, G * sizeof(MRow), 0, s);
     comm.broadcast(gbytes, GB, 0, s);
+    comm.group_end();
   }
   KeyCols o;
   o.n = have ? G : 0;

@@ -123,9 +123,11 @@ Engine::Impl::~Impl() {
                                             "retry",       "flush",  "barrier", "fl-hist", "fl-scan", "fl-write"};
       fprintf(stderr, "[wc] map phase clock (share of wave lifetime):");
       for (int i = 0; i < MS_TOTAL; ++i) fprintf(stderr, " %s=%.3f", names[i], (double)h[i] / h[MS_TOTAL]);
-      fprintf(stderr, "; slowest-wave token phase / mean = %.3f; tile flushes %llu, retry flushes %llu\n",
+      fprintf(stderr, "; slowest-wave token phase / mean = %.3f; tile flushes %llu, retry flushes %llu",
               h[MS_TOKSUM] ? (double)h[MS_TOKMAX] * MAP_THREADS / 64 / (double)h[MS_TOKSUM] : 0.0, h[MS_NFLUSH],
               h[MS_NRETRY]);
+      fprintf(stderr, "; slowest block / mean block = %.3f\n",
+              h[MS_BLKSUM] ? (double)h[MS_BLKMAX] * blocks_stamped / (double)h[MS_BLKSUM] : 0.0);
     }
     (void)hipFree(d_stamps);
   }
@@ -167,6 +169,7 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   pass_rec.subcap = (uint32_t)std::min<uint64_t>(rec.cap / ((uint64_t)blocks << log2_rb), 0xFFFFull);
   WC_CHECK(pass_rec.subcap > 0, "shuffle record capacity below one record per (map block, bucket)");
   MapArgs m{text, len, avail, prev, log2_rb, pass_rec, d_ctr->flags, &d_ctr->tokens, ablate_map, d_stamps};
+  if (d_stamps) blocks_stamped += blocks;
   if (map_dec) launch_map_decoupled(m, blocks, s);
   else launch_map(m, blocks, s);
   if (sync_debug) {  // WC_SYNC_DEBUG: attribute a device fault to a kernel and a chunk
@@ -558,7 +561,10 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
   WC_HIP_CHECK(hipSetDevice(im.dev));
   const double t0 = now_seconds();
   im.compact_local();
-  if (comm && comm->size() > 1) {
+  // WC_MERGE_ALWAYS=1 (tests): run the merge protocol even with one rank, so
+  // the RCCL exchange code is exercised on a one-GPU box
+  static const bool merge_always = getenv("WC_MERGE_ALWAYS") && atoi(getenv("WC_MERGE_ALWAYS")) != 0;
+  if (comm && (comm->size() > 1 || merge_always)) {
     const double tm = now_seconds();
     merge_cols(im, *comm, all_ranks);
     im.st.merge_ms += (now_seconds() - tm) * 1e3;

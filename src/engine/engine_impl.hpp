@@ -48,6 +48,7 @@ struct Engine::Impl {
   bool sync_debug = false;  // WC_SYNC_DEBUG: sync + log after every kernel
   bool map_dec = true;      // WC_MAP_DEC=0: block-synchronous tile kernel (map.hip) instead of map_dec.hip
   unsigned long long* d_stamps = nullptr;  // WC_MAP_STAMPS: map phase clock sums
+  uint64_t blocks_stamped = 0;             // map blocks launched with stamps (block-duration mean)
 
   // shuffle records
   uint64_t rec_total = 0;

@@ -106,7 +106,7 @@ struct MapArgs {
   unsigned long long* stamps;  // profiling: per-phase s_memtime sums (MAP_STAMP_N), nullptr = off
 };
 // In-kernel phase stamps of the map (diagnostic build path, WC_MAP_STAMPS=1).
-enum : int { MS_TOP = 0, MS_COMMIT, MS_MASK, MS_LIST, MS_KEYS, MS_COMBINE, MS_RETRY, MS_FLUSH, MS_BARRIER, MS_FL_HIST, MS_FL_SCAN, MS_FL_WRITE, MS_TOTAL, MS_TOKSUM, MS_TOKMAX, MS_TOKMAX_TILE, MS_NFLUSH, MS_NRETRY, MAP_STAMP_N };
+enum : int { MS_TOP = 0, MS_COMMIT, MS_MASK, MS_LIST, MS_KEYS, MS_COMBINE, MS_RETRY, MS_FLUSH, MS_BARRIER, MS_FL_HIST, MS_FL_SCAN, MS_FL_WRITE, MS_TOTAL, MS_TOKSUM, MS_TOKMAX, MS_TOKMAX_TILE, MS_NFLUSH, MS_NRETRY, MS_BLKSUM, MS_BLKMAX, MAP_STAMP_N };
 
 struct ReduceArgs {
   Records rec;

@@ -281,6 +281,10 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_decoupled(MapArgs a) {
   clk.lap(MS_FLUSH);
   if constexpr (ST) {
     if (lane == 0) atomicAdd(&st_acc[MS_TOTAL], (unsigned long long)(clk.t - t_begin));
+    if (tid == 0) {  // block duration (load balance across the grid; the host divides by the grid)
+      atomicAdd(&a.stamps[MS_BLKSUM], (unsigned long long)(clk.t - t_begin));
+      atomicMax(&a.stamps[MS_BLKMAX], (unsigned long long)(clk.t - t_begin));
+    }
   }
 
   uint64_t t = my_tokens;

@@ -7,6 +7,7 @@ merge are all checked end to end.
 """
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -165,6 +166,31 @@ def test_rccl_world1():
         got = e.result(comm)
     comm.close()
     assert_same(got, ops.cpu_count(text))
+
+
+@pytest.mark.parametrize("merge_mode", [0, 1])
+def test_rccl_merge_protocol_world1(merge_mode):
+    """The full RCCL merge (grouped send/recv, allgather, broadcast / reduce-scatter)
+    on one rank: WC_MERGE_ALWAYS makes finalize run it even at world size 1 (the
+    only RCCL world a one-GPU box can build).  Runs in a child process so the
+    env switch does not leak into other tests."""
+    code = (
+        "import os, sys\n"
+        "from cuda_mapreduce_amd import ops\n"
+        "uid = ops.Comm.unique_id(); comm = ops.Comm(uid, 0, 1, 0)\n"
+        f"e = ops.Engine(device=0, chunk_bytes=1 << 20, merge_mode={merge_mode})\n"
+        "text = ops.synth_host(3 << 18, seed=2, vocab=3000, zipf_s=0.8)\n"
+        "e.count_bytes(text)\n"
+        "for all_ranks in (False, True):\n"
+        "    got = e.result(comm, all_ranks=all_ranks)\n"
+        "    want = ops.cpu_count(text)\n"
+        "    assert got.words == want.words and got.counts.tolist() == want.counts.tolist(), 'mismatch'\n"
+        "assert e.stats()['merge_ms'] > 0\n"
+        "e.close(); comm.close(); print('ok')\n"
+    )
+    env = dict(os.environ, WC_MERGE_ALWAYS="1")
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, timeout=120)
+    assert out.returncode == 0 and b"ok" in out.stdout, out.stderr.decode()[-2000:]
 
 
 def test_cli_golden(tmp_path, golden_text):
