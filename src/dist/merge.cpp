@@ -38,16 +38,16 @@ void merge_cols_dense(Engine::Impl& im, Comm& comm) {
   const int W = comm.size(), R = comm.rank();
   const uint64_t n = im.cols.n;
 
-  // 1. metadata
-  uint64_t* d_meta = nullptr;
-  WC_HIP_CHECK(hipMalloc(&d_meta, (size_t)(W + 1) * 4 * 8));
+  // 1. metadata (small buffers: own arena, reserved once)
+  DeviceArena& S = im.merge_small;
+  S.reserve((size_t)(W + 1) * 4 * 8 + 1024);
+  uint64_t* d_meta = S.take_n<uint64_t>((size_t)(W + 1) * 4);
   uint64_t meta[4] = {n, im.cols_arena_bytes, im.max_end, 0};
   WC_HIP_CHECK(hipMemcpyAsync(d_meta, meta, sizeof meta, hipMemcpyHostToDevice, s));
   comm.allgather(d_meta, d_meta + 4, 4 * 8, s);
   std::vector<uint64_t> all((size_t)W * 4);
   WC_HIP_CHECK(hipMemcpyAsync(all.data(), d_meta + 4, all.size() * 8, hipMemcpyDeviceToHost, s));
   WC_HIP_CHECK(hipStreamSynchronize(s));
-  WC_HIP_CHECK(hipFree(d_meta));
   uint64_t n_max = 1, a_max = 16, gmax_end = 0;
   for (int r = 0; r < W; ++r) {
     n_max = std::max(n_max, all[r * 4 + 0]);
@@ -60,8 +60,12 @@ void merge_cols_dense(Engine::Impl& im, Comm& comm) {
 
   // 2. workspace
   DeviceArena& A = im.merge_mem;
-  const size_t need = n_max * 28 + m * (28 + 16 + 8 + 8 + 4 + 28) + vpad_max * 8 * 4 + radix_hist_words(m) * 4 +
-                      a_max * (W + 1) + 64 * 1024;
+  // every take_n below, in order (+ 256 B alignment slack per allocation)
+  const size_t need = n_max * 28 + a_max + m * 28 + (size_t)W * a_max  // send + gathered columns
+                      + m * (16 + 8) + radix_hist_words(m) * 4              // union sort
+                      + m * (8 + 4) + vpad_max * 28                         // flags, ids, merged key columns
+                      + vpad_max * 8 * 4 + 2 * (vpad_max / W) * 8           // dense vectors + slices
+                      + 32 * 256 + 64 * 1024;
   A.reserve(need);
   A.reset();
   uint64_t* sk0 = A.take_n<uint64_t>(n_max);

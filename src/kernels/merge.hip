@@ -110,6 +110,28 @@ __device__ __forceinline__ uint32_t owner_of(uint64_t ph, uint32_t W) {
   return (uint32_t)(((ph >> 32) * (uint64_t)W) >> 32);  // high hash bits (bucket bits are low)
 }
 
+// Wave-aggregated LDS counter add: lanes with owner `o` (OWN_MAX = none) add 1
+// to ctr[2 o] — one LDS atomic per distinct owner in the wave (<= W), not one
+// per lane (a W = 1 or 2 merge would serialise 64 lanes on one address).
+// Returns this lane's rank among all adds to its counter.
+__device__ __forceinline__ unsigned long long wave_owner_add(unsigned long long* ctr, uint32_t o) {
+  const int lane = (int)__lane_id();
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  uint64_t pending = __ballot(o != (uint32_t)OWN_MAX);
+  unsigned long long mine = 0;
+  while (pending) {
+    const int leader = __ffsll((unsigned long long)pending) - 1;
+    const uint32_t po = (uint32_t)__shfl((int)o, leader);
+    const uint64_t m = __ballot(o == po);
+    unsigned long long b = 0;
+    if (lane == leader) b = atomicAdd(&ctr[2 * po], (unsigned long long)__popcll(m));
+    b = __shfl(b, leader);
+    if (o == po) mine = b + (unsigned long long)__popcll(m & lt);
+    pending &= ~m;
+  }
+  return mine;
+}
+
 // counts[2o] += rows owned by o, counts[2o+1] += their long-word bytes.
 __global__ void __launch_bounds__(256) wc_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* slen,
                                                       uint64_t n, uint32_t W, unsigned long long* counts) {
@@ -118,8 +140,8 @@ __global__ void __launch_bounds__(256) wc_owner_count(const uint64_t* k0, const 
   __syncthreads();
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t o = owner_of(place_hash(k0[i], k1[i]), W);
-    atomicAdd(&h[2 * o], 1ull);
     if (!key_is_short(k1[i])) atomicAdd(&h[2 * o + 1], (unsigned long long)slen[i]);
+    (void)wave_owner_add(h, o);
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < 2 * W; i += blockDim.x)
@@ -145,11 +167,12 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
   for (int j = 0; j < PER; ++j) {
     const uint64_t i = r0 + threadIdx.x + (uint64_t)j * 256;
     own[j] = OWN_MAX;
+    lb[j] = 0;
     if (i < n) {
       own[j] = owner_of(place_hash(k0[i], k1[i]), W);
-      lr[j] = atomicAdd(&h[2 * own[j]], 1ull);
-      lb[j] = key_is_short(k1[i]) ? 0 : atomicAdd(&h[2 * own[j] + 1], (unsigned long long)slen[i]);
+      if (!key_is_short(k1[i])) lb[j] = atomicAdd(&h[2 * own[j] + 1], (unsigned long long)slen[i]);
     }
+    lr[j] = wave_owner_add(h, own[j]);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -211,34 +234,37 @@ __global__ void __launch_bounds__(256) wc_mrow_insert(const MRow* rows, uint64_t
 
 // Occupied slots -> merged rows; aoff becomes absolute in the received byte
 // buffer (rbase/bbase: exclusive prefixes of rows / bytes received per source).
-__global__ void __launch_bounds__(1024) wc_mrow_compact(const MRow* rows, const uint32_t* state,
-                                                        const unsigned long long* cnt,
-                                                        const unsigned long long* first, uint64_t T,
-                                                        const uint64_t* rbase, const uint64_t* bbase, uint32_t W,
-                                                        MRow* out, unsigned long long* out_n) {
+constexpr int MCOMPACT_PER = 4;  // slots per thread (256-thread blocks: 1024 slots per block)
+__global__ void __launch_bounds__(256) wc_mrow_compact(const MRow* rows, const uint32_t* state,
+                                                       const unsigned long long* cnt,
+                                                       const unsigned long long* first, uint64_t T,
+                                                       const uint64_t* rbase, const uint64_t* bbase, uint32_t W,
+                                                       MRow* out, unsigned long long* out_n) {
   __shared__ unsigned long long blk;
   __shared__ uint32_t bcount;
-  constexpr int PER = 16;
-  const uint64_t s0 = (uint64_t)blockIdx.x * 1024 * PER;
+  const int lane = (int)__lane_id();
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  const uint64_t s0 = (uint64_t)blockIdx.x * 256 * MCOMPACT_PER;
   if (threadIdx.x == 0) bcount = 0;
   __syncthreads();
-  uint32_t mine = 0, local[PER];
+  uint32_t local[MCOMPACT_PER];
 #pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const uint64_t sl = s0 + threadIdx.x + (uint64_t)j * 1024;
-    local[j] = 0xFFFFFFFFu;
-    if (sl < T && state[sl]) {
-      local[j] = atomicAdd(&bcount, 1u);
-      ++mine;
-    }
+  for (int j = 0; j < MCOMPACT_PER; ++j) {  // wave-aggregated ranks: one LDS atomic per wave and j
+    const uint64_t sl = s0 + threadIdx.x + (uint64_t)j * 256;
+    const bool occ = sl < T && state[sl] != 0u;
+    const uint64_t m = __ballot(occ);
+    uint32_t b = 0;
+    if (lane == 0 && m) b = atomicAdd(&bcount, (uint32_t)__popcll(m));
+    b = (uint32_t)__shfl((int)b, 0);
+    local[j] = occ ? b + (uint32_t)__popcll(m & lt) : 0xFFFFFFFFu;
   }
   __syncthreads();
   if (threadIdx.x == 0) blk = bcount ? atomicAdd(out_n, (unsigned long long)bcount) : 0;
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < PER; ++j) {
+  for (int j = 0; j < MCOMPACT_PER; ++j) {
     if (local[j] == 0xFFFFFFFFu) continue;
-    const uint64_t sl = s0 + threadIdx.x + (uint64_t)j * 1024;
+    const uint64_t sl = s0 + threadIdx.x + (uint64_t)j * 256;
     const uint64_t r = state[sl] - 1u;
     uint32_t src = 0;
     while (src + 1 < W && rbase[src + 1] <= r) ++src;
@@ -248,7 +274,6 @@ __global__ void __launch_bounds__(1024) wc_mrow_compact(const MRow* rows, const 
     if (m.alen) m.aoff = (uint32_t)(bbase[src] + m.aoff);
     out[blk + local[j]] = m;
   }
-  (void)mine;
 }
 
 // Gathered merged rows (grouped by owner) -> key columns; sref_off is made
@@ -291,8 +316,8 @@ void launch_mrow_insert(const MRow* rows, uint64_t R, uint32_t* state, unsigned 
 void launch_mrow_compact(const MRow* rows, const uint32_t* state, const unsigned long long* cnt,
                          const unsigned long long* first, uint64_t T, const uint64_t* rbase, const uint64_t* bbase,
                          uint32_t W, MRow* out, unsigned long long* out_n, hipStream_t s) {
-  const uint64_t blocks = (T + 1024 * 16 - 1) / (1024 * 16);
-  hipLaunchKernelGGL(dev::wc_mrow_compact, dim3((unsigned)blocks), dim3(1024), 0, s, rows, state, cnt, first, T, rbase,
+  const uint64_t blocks = (T + 256 * dev::MCOMPACT_PER - 1) / (256 * dev::MCOMPACT_PER);
+  hipLaunchKernelGGL(dev::wc_mrow_compact, dim3((unsigned)blocks), dim3(256), 0, s, rows, state, cnt, first, T, rbase,
                      bbase, W, out, out_n);
 }
 void launch_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rbase, const uint64_t* bbase, uint32_t W,
