@@ -122,7 +122,8 @@ struct ReduceArgs {
   const uint8_t* bucket_enable;   // nullptr = all
   uint64_t* newkeys;              // [n_buckets * NEWKEY_CAP] (slot << 32 | offset) of new long words
 };
-constexpr int NEWKEY_CAP = 1024;  // per bucket and pass; beyond it words are copied inline
+constexpr int NEWKEY_CAP = 4096;  // per bucket and pass (= TAB_SLOTS: never exceeded); else copied inline
+constexpr int NEWKEY_PER_THREAD = 4;
 
 struct SynthVocab {
   const uint8_t* bytes;

@@ -37,6 +37,14 @@ constexpr uint64_t K1_PENDING = ~0ull;
 
 WC_HD bool is_delim(uint32_t c) { return c == 0x20u || c == 0x0Du || c == 0x0Au; }
 
+// Per-byte "is delimiter" for 8 packed bytes -> 8-bit mask (exact SWAR zero test).
+WC_HD uint64_t delim_mask8(uint64_t x) {
+  constexpr uint64_t ONES = 0x0101010101010101ull, LOW7 = 0x7F7F7F7F7F7F7F7Full;
+  auto zero_bytes = [](uint64_t y) { return ~(((y & LOW7) + LOW7) | y) & 0x8080808080808080ull; };
+  const uint64_t m = zero_bytes(x ^ (0x20 * ONES)) | zero_bytes(x ^ (0x0D * ONES)) | zero_bytes(x ^ (0x0A * ONES));
+  return ((m >> 7) * 0x0102040810204080ull) >> 56;
+}
+
 WC_HD uint64_t fnv1a_step(uint64_t h, uint32_t byte) { return (h ^ (uint64_t)(byte & 0xFFu)) * FNV_PRIME; }
 
 // murmur3 fmix64 finalizer: FNV's low bits are weak, placement needs all 64.

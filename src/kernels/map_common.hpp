@@ -42,14 +42,6 @@ typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t map_tag(uint64_t ph) { return ((uint32_t)ph & ~1u) | 2u; }  // never 0
 __device__ __forceinline__ uint32_t map_group(uint64_t ph) { return (uint32_t)(ph >> 32) & (MAP_NGROUPS - 1); }
 
-// Per-byte "is delimiter" for 8 packed bytes -> 8-bit mask (exact SWAR zero test).
-__device__ __forceinline__ uint64_t delim_mask8(uint64_t x) {
-  constexpr uint64_t ONES = 0x0101010101010101ull, LOW7 = 0x7F7F7F7F7F7F7F7Full;
-  auto zero_bytes = [](uint64_t y) { return ~(((y & LOW7) + LOW7) | y) & 0x8080808080808080ull; };
-  const uint64_t m = zero_bytes(x ^ (0x20 * ONES)) | zero_bytes(x ^ (0x0D * ONES)) | zero_bytes(x ^ (0x0A * ONES));
-  return ((m >> 7) * 0x0102040810204080ull) >> 56;
-}
-
 // 8 bytes of the LDS tile starting at byte p (dynamic indexing of a register
 // window would be lowered to scratch).  Default: ONE unaligned ds_read_b64
 // (gfx950 runs HSA queues in unaligned-access mode, and the compiler emits it

@@ -59,10 +59,39 @@ __device__ __forceinline__ void store_slice(const RedLds& L, const TableView& t,
   }
 }
 
+// Length of the word at text offset o: 16-byte chunks with a SWAR delimiter
+// test (unaligned global loads; the byte loop only within 16 B of avail_len).
+__device__ __forceinline__ uint64_t word_len(const ReduceArgs& a, uint64_t o) {
+  uint64_t len = 0;
+  while (o + len + 16 <= a.avail_len) {
+    uint64_t w[2];
+    __builtin_memcpy(w, a.text + o + len, 16);
+    const uint32_t m = (uint32_t)(delim_mask8(w[0]) | (delim_mask8(w[1]) << 8));
+    if (m) return len + (uint64_t)(__ffs(m) - 1);
+    len += 16;
+  }
+  while (o + len < a.avail_len && !is_delim(a.text[o + len])) ++len;
+  return len;
+}
+
+// Copy len bytes text[o..) -> arena[p..): 16-byte pieces, then the tail in
+// 8/4/2/1-byte pieces (never past len: neighbouring words are written concurrently).
+__device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uint64_t len) {
+  uint64_t c = 0;
+  for (; c + 16 <= len; c += 16) {
+    uint64_t w[2];
+    __builtin_memcpy(w, src + c, 16);
+    __builtin_memcpy(dst + c, w, 16);
+  }
+  if (len - c >= 8) { uint64_t w; __builtin_memcpy(&w, src + c, 8); __builtin_memcpy(dst + c, &w, 8); c += 8; }
+  if (len - c >= 4) { uint32_t w; __builtin_memcpy(&w, src + c, 4); __builtin_memcpy(dst + c, &w, 4); c += 4; }
+  if (len - c >= 2) { uint16_t w; __builtin_memcpy(&w, src + c, 2); __builtin_memcpy(dst + c, &w, 2); c += 2; }
+  if (len - c >= 1) dst[c] = src[c];
+}
+
 // Copy the bytes of a newly seen long word into the key arena.
 __device__ void arena_copy_word(const ReduceArgs& a, uint64_t off, size_t gslot) {
-  uint64_t len = 0;
-  while (off + len < a.avail_len && !is_delim(a.text[off + len])) ++len;
+  const uint64_t len = word_len(a, off);
   const uint64_t p = atomicAdd(a.arena.cursor, (unsigned long long)len);
   if (p + len > a.arena.cap) {
     atomicOr(&a.flags[FLAG_ARENA_OVF], 1u);
@@ -70,31 +99,33 @@ __device__ void arena_copy_word(const ReduceArgs& a, uint64_t off, size_t gslot)
     a.tab.sref_len[gslot] = 0;
     return;
   }
-  for (uint64_t i = 0; i < len; ++i) a.arena.bytes[p + i] = a.text[off + i];
+  copy_bytes(a.arena.bytes + p, a.text + off, len);
   a.tab.sref_off[gslot] = p;
   a.tab.sref_len[gslot] = (uint32_t)len;
 }
 
-// Copy the bytes of this pass's new long words into the key arena: one word
-// per thread, one global arena reservation per block.
+// Copy the bytes of this pass's new long words into the key arena: up to
+// NEWKEY_PER_THREAD words per thread, one global arena reservation per block.
 __device__ void copy_new_words(RedLds& L, const ReduceArgs& a, uint32_t b) {
+  static_assert(NEWKEY_CAP <= NEWKEY_PER_THREAD * RED_THREADS, "newkeys per thread");
   const uint32_t n = min(L.nnew, (uint32_t)NEWKEY_CAP);
-  uint64_t len[2], mine[2];
-  unsigned long long off[2];
-  for (int k = 0; k < 2; ++k) {  // up to 2 words per thread (NEWKEY_CAP <= 2 * RED_THREADS)
+  uint64_t len[NEWKEY_PER_THREAD], mine[NEWKEY_PER_THREAD];
+  unsigned long long off[NEWKEY_PER_THREAD];
+#pragma unroll
+  for (int k = 0; k < NEWKEY_PER_THREAD; ++k) {
     const uint32_t i = threadIdx.x + k * RED_THREADS;
     len[k] = 0;
     if (i < n) {
       mine[k] = a.newkeys[(size_t)b * NEWKEY_CAP + i];
-      const uint64_t o = mine[k] & 0xFFFFFFFFull;
-      while (o + len[k] < a.avail_len && !is_delim(a.text[o + len[k]])) ++len[k];
+      len[k] = word_len(a, mine[k] & 0xFFFFFFFFull);
       off[k] = atomicAdd(&L.arena_need, (unsigned long long)len[k]);
     }
   }
   __syncthreads();
   if (threadIdx.x == 0) L.arena_base = L.arena_need ? atomicAdd(a.arena.cursor, L.arena_need) : 0;
   __syncthreads();
-  for (int k = 0; k < 2; ++k) {
+#pragma unroll
+  for (int k = 0; k < NEWKEY_PER_THREAD; ++k) {
     const uint32_t i = threadIdx.x + k * RED_THREADS;
     if (i >= n) continue;
     const size_t gslot = (size_t)b * TAB_SLOTS + (mine[k] >> 32);
@@ -105,7 +136,7 @@ __device__ void copy_new_words(RedLds& L, const ReduceArgs& a, uint32_t b) {
       a.tab.sref_len[gslot] = 0;
       continue;
     }
-    for (uint64_t j = 0; j < len[k]; ++j) a.arena.bytes[p + j] = a.text[o + j];
+    copy_bytes(a.arena.bytes + p, a.text + o, len[k]);
     a.tab.sref_off[gslot] = p;
     a.tab.sref_len[gslot] = (uint32_t)len[k];
   }
