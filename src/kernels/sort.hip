@@ -5,8 +5,11 @@
 // free from its serial append, /root/reference/main.cu:97-104) and the
 // deterministic dictionary union of the cross-GPU merge.
 //
-// Per 8-bit digit pass: wc_radix_hist (LDS histogram per 2048-item tile) ->
-// wc_radix_scan (exclusive scan, digit-major) -> wc_radix_scatter (stable
+// Per 8-bit digit pass: wc_radix_hist (LDS histogram per 2048-item tile, plus
+// the pass's per-digit totals) -> wc_radix_scan (one block per digit: base of
+// the digit + exclusive scan of its row of tile counts; the v8 single-block
+// scan of the whole digit-major array took 195 us at 1M keys, this ~5 us) ->
+// wc_radix_scatter (stable
 // in-tile ranking with 64-lane ballots: lanes with equal digits are matched
 // with 8 ballots, ranked with popcount, waves combined through LDS).
 #include <utility>
@@ -24,7 +27,7 @@ constexpr int RS_TILE = RS_THREADS * RS_ROUNDS;  // 2048 items per block
 constexpr int RS_WAVES = RS_THREADS / 64;
 
 __global__ void __launch_bounds__(RS_THREADS) wc_radix_hist(const uint64_t* keys, uint64_t n, int shift,
-                                                            uint32_t* hist, uint32_t nblocks) {
+                                                            uint32_t* hist, uint32_t nblocks, uint32_t* totals) {
   __shared__ uint32_t h[256];
   h[threadIdx.x] = 0;
   __syncthreads();
@@ -35,49 +38,51 @@ __global__ void __launch_bounds__(RS_THREADS) wc_radix_hist(const uint64_t* keys
   }
   __syncthreads();
   hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+  if (h[threadIdx.x]) atomicAdd(&totals[threadIdx.x], h[threadIdx.x]);
 }
 
-// Single-block exclusive scan of m words (digit-major histogram): each
-// thread scans a contiguous run of ceil(m / 1024) words held in registers (all
-// loads in flight at once when the run is <= 16 words), one block scan of the
-// run totals, then each thread rewrites its run.
-__global__ void __launch_bounds__(1024) wc_radix_scan(uint32_t* hist, uint64_t m) {
-  constexpr int REG = 16;
-  __shared__ uint32_t wsum[16];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint64_t per = (m + 1023) / 1024;
-  const uint64_t b = threadIdx.x * per, e = b + per < m ? b + per : m;
-  uint32_t v[REG];
-  uint32_t tot = 0;
-  if (per <= REG) {
-#pragma unroll
-    for (int k = 0; k < REG; ++k) v[k] = b + k < e ? hist[b + k] : 0u;
-#pragma unroll
-    for (int k = 0; k < REG; ++k) tot += v[k];
-  } else {
-    for (uint64_t i = b; i < e; ++i) tot += hist[i];
-  }
-  uint32_t x = tot;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) wsum[wave] = x;
+// Block d: hist row d (tile counts of digit d, nb words) -> exclusive offsets,
+// starting at the total of all smaller digits.
+__global__ void __launch_bounds__(256) wc_radix_scan(uint32_t* hist, uint32_t nb, const uint32_t* totals) {
+  __shared__ uint32_t wsum[4];
+  const uint32_t d = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // base of digit d
+  uint32_t x = (uint32_t)tid < d ? totals[tid] : 0u;
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o);
+  if (lane == 0) wsum[wave] = x;
   __syncthreads();
-  uint32_t run = x - tot;
-  for (int w = 0; w < wave; ++w) run += wsum[w];
-  if (per <= REG) {
+  uint32_t run = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  __syncthreads();
+  uint32_t* row = hist + (size_t)d * nb;
+  for (uint32_t c = 0; c < nb; c += 1024) {  // 4 consecutive words per thread
+    const uint32_t b = c + 4 * tid;
+    uint32_t v[4], t = 0;
 #pragma unroll
-    for (int k = 0; k < REG; ++k) {
-      if (b + k < e) hist[b + k] = run;
-      run += v[k];
+    for (int k = 0; k < 4; ++k) {
+      v[k] = b + k < nb ? row[b + k] : 0u;
+      t += v[k];
     }
-  } else {
-    for (uint64_t i = b; i < e; ++i) {
-      const uint32_t t = hist[i];
-      hist[i] = run;
-      run += t;
+    uint32_t incl = t;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
     }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t pre = run + incl - t, chunk = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      pre += w < wave ? wsum[w] : 0u;
+      chunk += wsum[w];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (b + k < nb) row[b + k] = pre;
+      pre += v[k];
+    }
+    run += chunk;
+    __syncthreads();  // wsum reused by the next chunk
   }
 }
 
@@ -178,9 +183,11 @@ inline dim3 grid_for(uint64_t n) {
 
 }  // namespace dev
 
+constexpr int RS_MAX_PASSES = 8;  // 64-bit keys
+
 size_t radix_hist_words(uint64_t n) {
   const uint64_t nb = (n + dev::RS_TILE - 1) / dev::RS_TILE;
-  return (size_t)256 * (nb ? nb : 1);
+  return (size_t)256 * (nb ? nb : 1) + 256 * RS_MAX_PASSES;  // tile counts + per-pass digit totals
 }
 
 void radix_sort_pairs(uint64_t* keys, uint32_t* vals, uint64_t* tmp_keys, uint32_t* tmp_vals, uint32_t* hist,
@@ -188,12 +195,15 @@ void radix_sort_pairs(uint64_t* keys, uint32_t* vals, uint64_t* tmp_keys, uint32
   if (n <= 1 || bits <= 0) return;
   const uint32_t nb = (uint32_t)((n + dev::RS_TILE - 1) / dev::RS_TILE);
   const int passes = (bits + 7) / 8;
+  uint32_t* totals = hist + (size_t)256 * nb;  // [passes][256]
+  WC_HIP_CHECK(hipMemsetAsync(totals, 0, (size_t)256 * passes * sizeof(uint32_t), s));
   uint64_t *ki = keys, *ko = tmp_keys;
   uint32_t *vi = vals, *vo = tmp_vals;
   for (int p = 0; p < passes; ++p) {
     const int shift = 8 * p;
-    hipLaunchKernelGGL(dev::wc_radix_hist, dim3(nb), dim3(dev::RS_THREADS), 0, s, ki, n, shift, hist, nb);
-    hipLaunchKernelGGL(dev::wc_radix_scan, dim3(1), dim3(1024), 0, s, hist, (uint64_t)256 * nb);
+    hipLaunchKernelGGL(dev::wc_radix_hist, dim3(nb), dim3(dev::RS_THREADS), 0, s, ki, n, shift, hist, nb,
+                       totals + 256 * p);
+    hipLaunchKernelGGL(dev::wc_radix_scan, dim3(256), dim3(256), 0, s, hist, nb, totals + 256 * p);
     hipLaunchKernelGGL(dev::wc_radix_scatter, dim3(nb), dim3(dev::RS_THREADS), 0, s, ki, vi, ko, vo, n, shift, hist,
                        nb);
     std::swap(ki, ko);
