@@ -61,6 +61,7 @@ struct MapLds {
     tag[s] = 0;
     key[s].y = K1_EMPTY;
   }
+  __device__ u64x2 key_at(int s) const { return key[s]; }
 };
 static_assert(sizeof(MapLds) <= 160 * 1024 / MAP_BLOCKS_PER_CU, "map blocks per CU must fit its LDS");
 

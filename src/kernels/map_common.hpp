@@ -4,7 +4,7 @@
 // shuffle-write flush.  Functions touching the combiner take the kernel's LDS
 // struct as a template parameter; it must provide key, cnt, off, bcur,
 // occupied, sticky, flush_kept and used, plus the slot-state accessors
-// bucket(s, log2_buckets) (-1 = empty) and evict(s) of its probing scheme.
+// bucket(s, log2_buckets) (-1 = empty), key_at(s) and evict(s) of its layout.
 #pragma once
 #include "kernels.hpp"
 #include "keys.hpp"
@@ -169,7 +169,7 @@ __device__ void flush_table(LDS& L, const MapArgs& a, PhaseClock<ST>& clk, bool 
       keep = !final && c >= MAP_PROMOTE && L.sticky < (uint32_t)MAP_STICKY_CAP &&
              atomicAdd(&L.sticky, 1u) < (uint32_t)MAP_STICKY_CAP;
       if (c) {
-        const u64x2 kk = L.key[s];
+        const u64x2 kk = L.key_at(s);
         emit_record(L, a, (uint32_t)b, kk.x, kk.y, c, L.off[s]);
         ++emitted;
       }
