@@ -7,8 +7,10 @@ every rank owns a fixed 1 GiB shard of one logical synthetic stream).
 
 One process per GPU.  For N > 1 the driver launches
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
-and ranks merge their key tables with RCCL (reduce-scatter + all-gather over
-xGMI) through the native communicator; torch.distributed (backend "nccl" =
+and ranks merge their key tables with RCCL over xGMI through the native
+communicator (default: the MapReduce shuffle — all-to-all of every key to its
+hash owner, owner-side merge, gather to rank 0; `merge_mode=1`: reduce-scatter
++ all-gather of dense count vectors); torch.distributed (backend "nccl" =
 RCCL) carries the rendezvous, the RCCL unique id and the timing barriers.
 
 A timed step is the full job on the resident shard: map (tokenize + combine),
