@@ -102,6 +102,38 @@ def test_table_split_large_vocab():
     assert_same(got, ops.cpu_count(text))
 
 
+def test_combiner_closed_admission_and_refresh():
+    """A near-flat 1M-word vocabulary over 96 MiB: every map block sees far more
+    distinct keys than its table admits (1024), so most tokens become direct
+    shuffle records and every block refreshes its table many times (> 16 k
+    direct records each); counts and first occurrences must stay exact."""
+    text = ops.synth_host(96 << 20, seed=21, vocab=1000000, zipf_s=0.4)
+    with ops.Engine(device=0) as e:
+        e.count_bytes(text)
+        got = e.result()
+        st = e.stats()
+    assert st["records"] > st["tokens"] // 2  # mostly direct records
+    assert_same(got, ops.cpu_count(text))
+
+
+def test_combiner_vocabulary_drift():
+    """The hot keys change half way through every block's share of the text
+    (alternate pieces are upper-cased): retained hot keys are evicted and the
+    new ones admitted while tokens keep flowing — counts and first occurrences
+    must stay exact."""
+    half = ops.synth_host(48 << 20, seed=5, vocab=20000)
+    upper = bytes.maketrans(b"abcdefghijklmnopqrstuvwxyz", b"ABCDEFGHIJKLMNOPQRSTUVWXYZ")
+    n = len(half) // 2
+    # alternate 32 KiB pieces (whole 1 KiB synthetic segments, which end in a
+    # delimiter) so every map block's ~190 KiB share switches hot sets
+    piece = 32 << 10
+    text = b"".join(half[i:i + piece] + half[i:i + piece].translate(upper) for i in range(0, n, piece))
+    with ops.Engine(device=0) as e:
+        e.count_bytes(text)
+        got = e.result()
+    assert_same(got, ops.cpu_count(text))
+
+
 def test_region_overflow_reruns():
     rng = np.random.default_rng(9)
     text = b" ".join(f"k{i}".encode() for i in rng.integers(0, 200000, 200000))
