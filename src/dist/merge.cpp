@@ -25,6 +25,7 @@
 // Ring reduce-scatter over 7 xGMI links moves ~V x 8 B x (W-1)/W per rank:
 // ~50 us for a million-word vocabulary, negligible next to the text scan.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "../engine/engine_impl.hpp"
@@ -151,6 +152,90 @@ T* take_aligned(DeviceArena& A, size_t n) {
 }
 }  // namespace
 
+// Small-vocabulary variant of the shuffle merge (see merge_cols_shuffle):
+// pack all local rows (one "owner"), send them to rank 0, merge there.
+void merge_to_root(Engine::Impl& im, Comm& comm, const std::vector<uint64_t>& rank_rows,
+                   const std::vector<uint64_t>& rank_bytes, uint64_t gmax_end) {
+  Range rg("wc_merge_root");
+  hipStream_t s = im.s;
+  const int W = comm.size(), R = comm.rank();
+  const uint64_t n = im.cols.n;
+  const uint64_t my_rows = rank_rows[R], my_bytes = rank_bytes[R];
+  uint64_t rr = 0, rbt = 0;  // received by rank 0
+  std::vector<size_t> zs(W, 0), sr(W, 0), sb(W, 0), ro_r(W, 0), rb_r(W, 0), ro_b(W, 0), rb_b(W, 0);
+  std::vector<uint64_t> base(2 * (size_t)W + 2, 0);
+  for (int p = 0; p < W; ++p) {
+    base[p] = rr;
+    base[W + 1 + p] = rbt;
+    ro_r[p] = rr * sizeof(MRow);
+    ro_b[p] = rbt;
+    if (R == 0) {
+      rb_r[p] = rank_rows[p] * sizeof(MRow);
+      rb_b[p] = rank_bytes[p];
+    }
+    rr += rank_rows[p];
+    rbt += rank_bytes[p];
+  }
+  base[W] = rr;
+  base[2 * W + 1] = rbt;
+  sr[0] = my_rows * sizeof(MRow);
+  sb[0] = my_bytes;
+  if (R != 0) rr = rbt = 0;
+  uint64_t T = 1024;
+  while (T < 2 * rr) T <<= 1;
+  DeviceArena& A = im.merge_mem;
+  A.reserve((my_rows + 2 * rr) * sizeof(MRow) + my_bytes + rbt + T * (4 + 16) + rr * (5 * 8 + 4) +
+            (2 * (size_t)W + 8) * 8 + 32 * 1024);
+  MRow* send_rows = take_aligned<MRow>(A, my_rows);
+  uint8_t* send_bytes = take_aligned<uint8_t>(A, my_bytes);
+  MRow* recv_rows = take_aligned<MRow>(A, rr);
+  uint8_t* recv_bytes = take_aligned<uint8_t>(A, rbt);
+  unsigned long long* d_cur = take_aligned<unsigned long long>(A, 4);  // zero counts (2) | cursor (2)
+  WC_HIP_CHECK(hipMemsetAsync(d_cur, 0, 4 * 8, s));
+  launch_owner_scatter(im.cols.k0, im.cols.k1, im.cols.cnt, im.cols.first, im.cols.sref_off, im.cols.sref_len,
+                       im.cols_arena, n, 1u, d_cur, d_cur + 2, send_rows, send_bytes, s);
+  comm.group_begin();
+  comm.alltoallv(send_rows, zs.data(), sr.data(), recv_rows, ro_r.data(), rb_r.data(), s);
+  comm.alltoallv(send_bytes, zs.data(), sb.data(), recv_bytes, ro_b.data(), rb_b.data(), s);
+  comm.group_end();
+  KeyCols o;
+  uint64_t gb[4] = {0, 0, 0, rbt};  // one output group (rows 0..G, byte base 0); outlives its async H2D
+  if (R == 0) {
+    uint32_t* state = take_aligned<uint32_t>(A, T);
+    unsigned long long* tcnt = take_aligned<unsigned long long>(A, T);
+    unsigned long long* tfirst = take_aligned<unsigned long long>(A, T);
+    MRow* merged = take_aligned<MRow>(A, rr);
+    uint64_t* d_base = take_aligned<uint64_t>(A, base.size() + 4);
+    unsigned long long* d_m = take_aligned<unsigned long long>(A, 1);
+    WC_HIP_CHECK(hipMemcpyAsync(d_base, base.data(), base.size() * 8, hipMemcpyHostToDevice, s));
+    WC_HIP_CHECK(hipMemsetAsync(state, 0, T * 4, s));
+    WC_HIP_CHECK(hipMemsetAsync(tcnt, 0, T * 8, s));
+    launch_fill_u64(reinterpret_cast<uint64_t*>(tfirst), ~0ull, T, s);
+    WC_HIP_CHECK(hipMemsetAsync(d_m, 0, 8, s));
+    launch_mrow_insert(recv_rows, rr, state, tcnt, tfirst, T, s);
+    launch_mrow_compact(recv_rows, state, tcnt, tfirst, T, d_base, d_base + W + 1, (uint32_t)W, merged, d_m, s);
+    unsigned long long G = 0;
+    WC_HIP_CHECK(hipMemcpyAsync(&G, d_m, 8, hipMemcpyDeviceToHost, s));
+    WC_HIP_CHECK(hipStreamSynchronize(s));
+    o.n = G;
+    o.k0 = take_aligned<uint64_t>(A, G);
+    o.k1 = take_aligned<uint64_t>(A, G);
+    o.cnt = take_aligned<uint64_t>(A, G);
+    o.first = take_aligned<uint64_t>(A, G);
+    o.sref_off = take_aligned<uint64_t>(A, G);
+    o.sref_len = take_aligned<uint32_t>(A, G);
+    uint64_t* d_gbase = d_base + base.size();  // one group: row base 0 .. G, byte base 0
+    gb[1] = G;
+    WC_HIP_CHECK(hipMemcpyAsync(d_gbase, gb, sizeof gb, hipMemcpyHostToDevice, s));
+    launch_mrow_to_cols(merged, G, d_gbase, d_gbase + 2, 1u, o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len, s);
+  }
+  WC_HIP_CHECK(hipStreamSynchronize(s));  // also: base[] / gb[] are pageable host memory
+  im.cols = o;
+  im.cols_arena = recv_bytes;
+  im.cols_arena_bytes = R == 0 ? rbt : 0;
+  im.max_end = gmax_end;
+}
+
 void merge_cols_shuffle(Engine::Impl& im, Comm& comm, bool all_ranks) {
   Range rg("wc_merge_shuffle");
   hipStream_t s = im.s;
@@ -174,6 +259,24 @@ void merge_cols_shuffle(Engine::Impl& im, Comm& comm, bool all_ranks) {
   WC_HIP_CHECK(hipStreamSynchronize(s));
   uint64_t gmax_end = 0;
   for (int r = 0; r < W; ++r) gmax_end = std::max<uint64_t>(gmax_end, all[(size_t)r * C + 2 * W]);
+  std::vector<uint64_t> rank_rows(W, 0), rank_bytes(W, 0);
+  uint64_t total_rows = 0;
+  for (int r = 0; r < W; ++r) {
+    for (int p = 0; p < W; ++p) {
+      rank_rows[r] += all[(size_t)r * C + 2 * p];
+      rank_bytes[r] += all[(size_t)r * C + 2 * p + 1];
+    }
+    total_rows += rank_rows[r];
+  }
+  // Few keys in total: every rank sends its rows straight to rank 0, which
+  // merges them alone — one exchange instead of two (owner exchange + gather)
+  // and one host sync fewer.  WC_MERGE_ROOT_ROWS overrides the threshold.
+  uint64_t root_max = MERGE_ROOT_MAX_ROWS;
+  if (const char* e = std::getenv("WC_MERGE_ROOT_ROWS")) root_max = std::strtoull(e, nullptr, 10);
+  if (!all_ranks && total_rows <= root_max) {
+    merge_to_root(im, comm, rank_rows, rank_bytes, gmax_end);
+    return;
+  }
 
   // 2. pack by owner and exchange
   std::vector<size_t> so_r(W), sb_r(W), so_b(W), sb_b(W), ro_r(W), rb_r(W), ro_b(W), rb_b(W);

@@ -145,16 +145,22 @@ def test_region_overflow_reruns():
     assert_same(got, ops.cpu_count(text))
 
 
+@pytest.mark.parametrize("root_rows", [None, "0"])
 @pytest.mark.parametrize("merge_mode", [0, 1])
 @pytest.mark.parametrize("ranks", [1, 2, 3, 4, 8])
-def test_loopback_merge(ranks, merge_mode):
+def test_loopback_merge(ranks, merge_mode, root_rows, monkeypatch):
     """Sharding + cross-rank merge at N virtual ranks: shuffle (all-to-all by key
-    owner, gather to rank 0, broadcast with all_ranks) and dense (dictionary
-    union + reduce-scatter + all-gather) protocols."""
+    owner, gather to rank 0, broadcast with all_ranks; below WC_MERGE_ROOT_ROWS
+    total rows — the default for this small input — every rank sends straight
+    to rank 0 instead) and dense (dictionary union + reduce-scatter +
+    all-gather) protocols."""
+    if root_rows is not None:
+        monkeypatch.setenv("WC_MERGE_ROOT_ROWS", root_rows)  # 0: always the owner exchange
     rng = np.random.default_rng(ranks)
     text = random_text(rng, 400_000, alphabet=b"abcdefg  \n", long_words=4) + ops.synth_host(1 << 20, seed=2, vocab=3000)
-    got = ops.loopback_count(text, ranks, chunk_bytes=1 << 20, merge_mode=merge_mode, all_ranks=(ranks % 2 == 0))
-    assert_same(got, ops.cpu_count(text))
+    for all_ranks in (False, True):
+        got = ops.loopback_count(text, ranks, chunk_bytes=1 << 20, merge_mode=merge_mode, all_ranks=all_ranks)
+        assert_same(got, ops.cpu_count(text))
 
 
 @pytest.mark.parametrize("ranks", [2, 5])
@@ -164,8 +170,9 @@ def test_loopback_merge_many_long_words(ranks):
     words = [bytes(rng.integers(97, 123, int(rng.integers(9, 40))).astype(np.uint8)) for _ in range(5000)]
     picks = rng.integers(0, len(words), 200_000)
     text = b" ".join(words[i] for i in picks) + b"\n"
-    got = ops.loopback_count(text, ranks, chunk_bytes=1 << 20, all_ranks=True)
-    assert_same(got, ops.cpu_count(text))
+    want = ops.cpu_count(text)
+    for all_ranks in (False, True):  # rank-0 gather path | owner exchange + broadcast
+        assert_same(ops.loopback_count(text, ranks, chunk_bytes=1 << 20, all_ranks=all_ranks), want)
 
 
 def test_file_stream(tmp_path):
