@@ -390,7 +390,7 @@ void Engine::reset() {
   WC_HIP_CHECK(hipSetDevice(im.dev));
   launch_table_clear(im.table(), im.s);
   WC_HIP_CHECK(hipMemsetAsync(im.d_arena_cursor, 0, sizeof(unsigned long long), im.s));
-  WC_HIP_CHECK(hipStreamSynchronize(im.s));
+  // no sync: the next pass is stream-ordered behind the clear
   if (im.copy_s) WC_HIP_CHECK(hipStreamSynchronize(im.copy_s));  // a failed stream may have left copies
   im.st = Stats{};
   im.max_end = 0;

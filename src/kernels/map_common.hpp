@@ -249,6 +249,35 @@ __device__ __forceinline__ void token_key(const uint8_t* buf, uint32_t buf_len, 
   }
 }
 
+// Key from the token's first 8-byte window w (already read at p).
+__device__ __forceinline__ void finish_key(const uint8_t* buf, uint32_t buf_len, const MapArgs& a, uint64_t t0,
+                                           uint64_t w, uint32_t p, uint32_t len, uint64_t& k0, uint64_t& k1) {
+  if (len != MAP_LONG) {
+    k0 = low_bytes(w, len);
+    if (len <= 8) {
+      k1 = len;
+    } else {
+      uint64_t h = FNV_OFFSET;
+      for (uint32_t c = 8; c < len; c += 8) h = tail_fold(h, low_bytes(tile8(buf, p + c), len - c));
+      k1 = make_k1(len, h);
+    }
+  } else {
+    key_slow(buf, buf_len, a, p, t0 + p, k0, k1);
+  }
+}
+
+// Keys of a lane's two tokens of a step: both first windows are read before
+// either key is finished, so short words cost ONE LDS round trip for both.
+// Lanes without a token read harmless in-buffer bytes (p = 0) and get 0 keys.
+__device__ __forceinline__ void token_keys2(const uint8_t* buf, uint32_t buf_len, const MapArgs& a, uint64_t t0,
+                                            bool h1, uint32_t p1, uint32_t len1, bool h2, uint32_t p2, uint32_t len2,
+                                            uint64_t& a0, uint64_t& a1, uint64_t& b0, uint64_t& b1) {
+  const uint64_t w1 = tile8(buf, p1), w2 = tile8(buf, p2);
+  a0 = a1 = b0 = b1 = 0;
+  if (h1) finish_key(buf, buf_len, a, t0, w1, p1, len1, a0, a1);
+  if (h2) finish_key(buf, buf_len, a, t0, w2, p2, len2, b0, b1);
+}
+
 // Combiner slot of (k0, k1) — claiming one if the key is absent and `admit` —
 // or -1 when MAP_MAX_GROUP_PROBES groups are full (or the key is absent and
 // !admit).  Claim = ONE CAS of the tag; the

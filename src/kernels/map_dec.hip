@@ -32,6 +32,9 @@ constexpr uint32_t DEC_NONE = 0xFFFFFFFFu;
 #endif
 constexpr uint32_t DEC_TPL = WC_DEC_TPL;  // list entries per lane per step (1 or 2)
 constexpr uint32_t DEC_STEP = 64 * DEC_TPL;
+#ifndef WC_DEC_KEYS2
+#define WC_DEC_KEYS2 1  // both tokens' key windows in one LDS round trip
+#endif
 #ifndef WC_DEC_ADMIT_EIGHTHS
 #define WC_DEC_ADMIT_EIGHTHS 2
 #endif
@@ -159,7 +162,8 @@ __device__ __forceinline__ bool combine_or_emit(DecLds& L, const MapArgs& a, uin
     atomicMin(&L.off[s], off);
     return false;
   }
-  emit_record(L, a, ((uint32_t)ph >> 2) & ((1u << a.log2_rec_buckets) - 1u), k0, k1, 1, off);
+  if (a.ablate != 7)  // 7 (profiling): direct records dropped
+    emit_record(L, a, ((uint32_t)ph >> 2) & ((1u << a.log2_rec_buckets) - 1u), k0, k1, 1, off);
   return true;
 }
 
@@ -297,9 +301,14 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_decoupled(MapArgs a) {
       const bool h1 = j + lane < round_n, h2 = DEC_TPL > 1 && j + 64 + lane < round_n;
       const uint32_t e1 = h1 ? list[j + lane] : 0u, e2 = h2 ? list[j + 64 + lane] : 0u;
       const uint32_t q1 = e1 & 0x7FFu, q2 = e2 & 0x7FFu;
-      uint64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+      uint64_t a0, a1, b0, b1;
+#if WC_DEC_KEYS2
+      token_keys2(buf, DEC_UNIT + DEC_HALO, a, u0, h1, q1, e1 >> 11, h2, q2, e2 >> 11, a0, a1, b0, b1);
+#else
+      a0 = a1 = b0 = b1 = 0;
       if (h1) token_key(buf, DEC_UNIT + DEC_HALO, a, u0, q1, e1 >> 11, a0, a1);
       if (h2) token_key(buf, DEC_UNIT + DEC_HALO, a, u0, q2, e2 >> 11, b0, b1);
+#endif
       if (ST) {
         asm volatile("" ::"v"(a0), "v"(a1), "v"(b0), "v"(b1));
       }
