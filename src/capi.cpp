@@ -7,6 +7,7 @@
 #include "common/hip_util.hpp"
 #include "dist/comm.hpp"
 #include "io/source.hpp"
+#include "kernels/kernels.hpp"
 #include "wc/wc.h"
 #include "wc/wc.hpp"
 
@@ -66,6 +67,28 @@ extern "C" {
 
 const char* wc_last_error(void) { return g_err.c_str(); }
 const char* wc_version(void) { return "wc-mi355x 0.1.0"; }
+
+int wc_debug_radix_sort(int device, const uint64_t* keys, uint64_t n, int bits, uint64_t* sorted, uint32_t* perm) {
+  return guard([&] {
+    WC_HIP_CHECK(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    uint8_t* mem = nullptr;
+    const size_t nn = n ? n : 1, hw = wc::radix_hist_words(n);
+    const size_t bytes = nn * (8 + 8 + 4 + 4) + hw * 4 + 1024;
+    WC_HIP_CHECK(hipMalloc(&mem, bytes));
+    uint64_t* k = reinterpret_cast<uint64_t*>(mem);
+    uint64_t* tk = k + nn;
+    uint32_t* v = reinterpret_cast<uint32_t*>(tk + nn);
+    uint32_t* tv = v + nn;
+    uint32_t* hist = tv + nn;
+    WC_HIP_CHECK(hipMemcpy(k, keys, n * 8, hipMemcpyHostToDevice));
+    wc::launch_iota_u32(v, n, s);
+    wc::radix_sort_pairs(k, v, tk, tv, hist, n, bits, s);
+    WC_HIP_CHECK(hipMemcpy(sorted, k, n * 8, hipMemcpyDeviceToHost));
+    WC_HIP_CHECK(hipMemcpy(perm, v, n * 4, hipMemcpyDeviceToHost));
+    WC_HIP_CHECK(hipFree(mem));
+  });
+}
 
 int wc_device_count(void) {
   int n = 0;

@@ -254,3 +254,28 @@ def test_pinned_replay_host_staged():
         want[w] = want.get(w, 0) + int(c)
     assert got.total == 5 * one.total + q.total
     assert dict(zip(got.words, got.counts.tolist())) == want
+
+
+@pytest.mark.parametrize("n", [1, 2, 5, 2047, 2048, 2049, 100_003, 1_000_000])
+@pytest.mark.parametrize("bits", [8, 13, 30, 64])
+def test_radix_sort_kernel(n, bits):
+    """Kernel unit test: wc_radix_hist / wc_radix_scan / wc_radix_scatter against
+    numpy's stable argsort (many equal keys, so stability is checked too)."""
+    import ctypes
+
+    from cuda_mapreduce_amd.ops._lib import check, lib
+
+    rng = np.random.default_rng(n * 131 + bits)
+    hi = (1 << bits) - 1 if bits < 64 else (1 << 64) - 1
+    keys = rng.integers(0, 1 << 62, n, dtype=np.uint64) * np.uint64(4) + rng.integers(0, 4, n, dtype=np.uint64)
+    keys &= np.uint64(hi)
+    if n > 10:
+        keys[: n // 3] = keys[n // 3 : 2 * (n // 3)] % np.uint64(97)  # duplicates
+    out = np.zeros(n, np.uint64)
+    perm = np.zeros(n, np.uint32)
+    P64 = ctypes.POINTER(ctypes.c_uint64)
+    check(lib.wc_debug_radix_sort(0, keys.ctypes.data_as(P64), n, bits, out.ctypes.data_as(P64),
+                                  perm.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))))
+    want = np.argsort(keys, kind="stable")
+    assert np.array_equal(perm, want.astype(np.uint32))
+    assert np.array_equal(out, keys[want])
