@@ -1,2 +1,3 @@
 """Data parallelism across GPUs: torch.distributed rendezvous + native RCCL merge."""
-from .dist import DistEnv, DistributedWordCount, host_merge, init_from_env, rccl_comm  # noqa: F401
+from .dist import (CommFault, DistEnv, DistributedWordCount, comm_timeout_s, host_merge, init_from_env,  # noqa: F401
+                   rccl_comm)

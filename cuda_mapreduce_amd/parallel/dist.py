@@ -14,6 +14,7 @@ range (``shard_range``), so shards need no halo exchange.
 """
 from __future__ import annotations
 
+import datetime
 import os
 from dataclasses import dataclass
 from typing import Optional
@@ -31,8 +32,40 @@ class DistEnv:
     backend: str = "none"
 
 
+class CommFault(RuntimeError):
+    """A simulated communication failure (``WC_COMM_FAULT``) or a failed peer."""
+
+
+def comm_timeout_s() -> float:
+    """Collective timeout (``WC_COMM_TIMEOUT_S``, default 300 s) — shared with the native RCCL watchdog."""
+    try:
+        t = float(os.environ.get("WC_COMM_TIMEOUT_S", "300"))
+    except ValueError:
+        t = 300.0
+    return t if t > 0 else 300.0
+
+
+_calls = 0
+
+
+def _fault_tick(rank: int) -> None:
+    """Fault injection, same contract as src/dist/comm.cpp: ``WC_COMM_FAULT=<rank>[:<n>]``
+    makes rank <rank> fail its n-th collective (default the first)."""
+    global _calls
+    spec = os.environ.get("WC_COMM_FAULT", "")
+    _calls += 1
+    if not spec:
+        return
+    r, _, n = spec.partition(":")
+    if int(r) == rank and _calls == (int(n) if n else 1):
+        raise CommFault(f"injected comm fault (WC_COMM_FAULT) at collective {_calls} of rank {rank}")
+
+
 def init_from_env(backend: Optional[str] = None) -> DistEnv:
-    """Initialise torch.distributed from RANK/WORLD_SIZE/LOCAL_RANK (127.0.0.1 rendezvous)."""
+    """Initialise torch.distributed from RANK/WORLD_SIZE/LOCAL_RANK (127.0.0.1 rendezvous).
+
+    Collectives time out after ``comm_timeout_s()`` instead of hanging when a
+    peer dies (the reference has no failure handling at all)."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -45,11 +78,12 @@ def init_from_env(backend: Optional[str] = None) -> DistEnv:
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if not dist.is_initialized():
+        timeout = datetime.timedelta(seconds=comm_timeout_s())
         if backend == "nccl":
             torch.cuda.set_device(local)
-            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+            dist.init_process_group(backend, device_id=torch.device("cuda", local), timeout=timeout)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=timeout)
     return DistEnv(rank, world, local, backend)
 
 
@@ -90,8 +124,9 @@ def host_merge(local: Result) -> Result:
     import torch
     import torch.distributed as dist
 
-    world = dist.get_world_size()
+    world, rank = dist.get_world_size(), dist.get_rank()
     keys = [None] * world
+    _fault_tick(rank)
     dist.all_gather_object(keys, list(local.words))
     union = sorted(set().union(*map(set, keys)))
     gid = {w: i for i, w in enumerate(union)}
@@ -101,11 +136,15 @@ def host_merge(local: Result) -> Result:
     for w, c, f in zip(local.words, local.counts, local.first_off):
         cnt[gid[w]] = int(c)
         first[gid[w]] = int(f)
+    _fault_tick(rank)
     scnt = _reduce_scatter(cnt, dist.ReduceOp.SUM)
+    _fault_tick(rank)
     sfirst = _reduce_scatter(first, dist.ReduceOp.MIN)
     full_cnt = [torch.empty_like(scnt) for _ in range(world)]
     full_first = [torch.empty_like(sfirst) for _ in range(world)]
+    _fault_tick(rank)
     dist.all_gather(full_cnt, scnt)
+    _fault_tick(rank)
     dist.all_gather(full_first, sfirst)
     c = torch.cat(full_cnt)[: len(union)].numpy()
     f = torch.cat(full_first)[: len(union)].numpy()

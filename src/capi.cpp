@@ -320,6 +320,7 @@ wc_result* wc_loopback_count(const uint8_t* text, uint64_t n, int ranks, const i
         }
       } catch (const std::exception& ex) {
         errs[r] = ex.what();
+        comms[r]->abort(ex.what());  // peers blocked in a collective fail instead of waiting forever
       }
     });
   }

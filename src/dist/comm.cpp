@@ -4,8 +4,10 @@
 #include <rccl/rccl.h>
 
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 
 #include "../common/hip_util.hpp"
 
@@ -20,6 +22,34 @@ void launch_combine_u64(uint64_t* dst, const uint64_t* src, uint64_t n, int op, 
       ::wc::fail(std::string("RCCL error ") + ncclGetErrorString(r_) + " at " + __FILE__ + ":" +     \
                  std::to_string(__LINE__) + " in " #expr);                                           \
   } while (0)
+
+Comm::Comm() {
+  if (const char* e = std::getenv("WC_COMM_TIMEOUT_S")) {
+    const double t = std::atof(e);
+    if (t > 0) timeout_s_ = t;
+  }
+  if (const char* e = std::getenv("WC_COMM_FAULT"); e && *e) {
+    char* end = nullptr;
+    fault_rank_ = (int)std::strtol(e, &end, 10);
+    fault_at_ = (end && *end == ':') ? std::strtoull(end + 1, nullptr, 10) : 1;
+  }
+}
+
+void Comm::tick(int rank) {
+  if (failed()) fail("communicator failed earlier: " + failed_);
+  ++calls_;
+  if (rank == fault_rank_ && calls_ == fault_at_) {
+    const std::string why = "injected comm fault (WC_COMM_FAULT) at collective " + std::to_string(calls_) +
+                            " of rank " + std::to_string(rank);
+    abort(why);
+    fail(why);
+  }
+}
+
+void Comm::sync(hipStream_t s) {
+  if (failed()) fail("communicator failed earlier: " + failed_);
+  WC_HIP_CHECK(hipStreamSynchronize(s));
+}
 
 namespace {
 
@@ -39,19 +69,22 @@ class RcclComm final : public Comm {
   }
   ~RcclComm() override {
     (void)hipFree(scratch_);
-    (void)ncclCommDestroy(c_);
+    if (c_) (void)ncclCommDestroy(c_);
   }
   int rank() const override { return rank_; }
   int size() const override { return size_; }
   const char* backend() const override { return "rccl"; }
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    tick(rank_);
     WC_NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, c_, s));
   }
   void reduce_scatter_u64(const uint64_t* send, uint64_t* recv, size_t count, RedOp op, hipStream_t s) override {
+    tick(rank_);
     WC_NCCL_CHECK(ncclReduceScatter(send, recv, count, ncclUint64, to_nccl(op), c_, s));
   }
   void alltoallv(const void* send, const size_t* send_off, const size_t* send_bytes, void* recv,
                  const size_t* recv_off, const size_t* recv_bytes, hipStream_t s) override {
+    tick(rank_);
     WC_NCCL_CHECK(ncclGroupStart());
     for (int p = 0; p < size_; ++p) {
       if (send_bytes[p])
@@ -62,13 +95,44 @@ class RcclComm final : public Comm {
     WC_NCCL_CHECK(ncclGroupEnd());
   }
   void broadcast(void* buf, size_t bytes, int root, hipStream_t s) override {
+    tick(rank_);
     if (bytes) WC_NCCL_CHECK(ncclBroadcast(buf, buf, bytes, ncclUint8, root, c_, s));
   }
   void group_begin() override { WC_NCCL_CHECK(ncclGroupStart()); }
   void group_end() override { WC_NCCL_CHECK(ncclGroupEnd()); }
   void barrier(hipStream_t s) override {
+    tick(rank_);
     WC_NCCL_CHECK(ncclAllReduce(scratch_, scratch_, 1, ncclUint64, ncclSum, c_, s));
-    WC_HIP_CHECK(hipStreamSynchronize(s));
+    sync(s);
+  }
+  // Watchdog wait: a peer that died or diverged leaves our collective kernel
+  // spinning forever under a plain hipStreamSynchronize.
+  void sync(hipStream_t s) override {
+    if (failed()) fail("communicator failed earlier: " + failed_);
+    const double t0 = now_seconds();
+    for (;;) {
+      const hipError_t q = hipStreamQuery(s);
+      if (q == hipSuccess) return;
+      if (q != hipErrorNotReady) WC_HIP_CHECK(q);
+      ncclResult_t ar = ncclSuccess;
+      WC_NCCL_CHECK(ncclCommGetAsyncError(c_, &ar));
+      std::string why;
+      if (ar != ncclSuccess && ar != ncclInProgress) why = std::string("RCCL async error: ") + ncclGetErrorString(ar);
+      else if (now_seconds() - t0 > timeout_s())
+        why = "RCCL collective made no progress for " + std::to_string((int)timeout_s()) + " s (WC_COMM_TIMEOUT_S)";
+      if (!why.empty()) {
+        abort(why);
+        fail(why + " on rank " + std::to_string(rank_) + "; communicator aborted");
+      }
+      std::this_thread::yield();
+    }
+  }
+  void abort(const std::string& why) override {
+    Comm::abort(why);
+    if (c_) {
+      (void)ncclCommAbort(c_);
+      c_ = nullptr;
+    }
   }
 
  private:
@@ -87,16 +151,28 @@ struct Hub {
   int arrived = 0;
   uint64_t gen = 0;
   std::vector<const void*> ptrs;
+  bool aborted = false;  // a rank failed: every current and later wait throws
+  std::string why;
   void wait_all() {
     std::unique_lock<std::mutex> lk(mu);
+    if (aborted) fail("loopback peer failed: " + why);
     const uint64_t g = gen;
     if (++arrived == n) {
       arrived = 0;
       ++gen;
       cv.notify_all();
     } else {
-      cv.wait(lk, [&] { return gen != g; });
+      cv.wait(lk, [&] { return gen != g || aborted; });
+      if (gen == g) fail("loopback peer failed: " + why);
     }
+  }
+  void abort(const std::string& w) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!aborted) {
+      aborted = true;
+      why = w;
+    }
+    cv.notify_all();
   }
 };
 
@@ -106,7 +182,12 @@ class LoopbackComm final : public Comm {
   int rank() const override { return rank_; }
   int size() const override { return hub_->n; }
   const char* backend() const override { return "loopback"; }
+  void abort(const std::string& why) override {
+    Comm::abort(why);
+    hub_->abort("rank " + std::to_string(rank_) + ": " + failed_);
+  }
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    tick(rank_);
     WC_HIP_CHECK(hipStreamSynchronize(s));
     hub_->ptrs[rank_] = send;
     hub_->wait_all();
@@ -117,6 +198,7 @@ class LoopbackComm final : public Comm {
     hub_->wait_all();  // senders may reuse their buffers after everyone copied
   }
   void reduce_scatter_u64(const uint64_t* send, uint64_t* recv, size_t count, RedOp op, hipStream_t s) override {
+    tick(rank_);
     WC_HIP_CHECK(hipStreamSynchronize(s));
     hub_->ptrs[rank_] = send;
     hub_->wait_all();
@@ -138,6 +220,7 @@ class LoopbackComm final : public Comm {
   }
   void alltoallv(const void* send, const size_t* send_off, const size_t* /*send_bytes*/, void* recv,
                  const size_t* recv_off, const size_t* recv_bytes, hipStream_t s) override {
+    tick(rank_);
     WC_HIP_CHECK(hipStreamSynchronize(s));
     hub_->ptrs[rank_] = send;
     hub_->offs[rank_] = send_off;
@@ -151,6 +234,7 @@ class LoopbackComm final : public Comm {
     hub_->wait_all();
   }
   void broadcast(void* buf, size_t bytes, int root, hipStream_t s) override {
+    tick(rank_);
     WC_HIP_CHECK(hipStreamSynchronize(s));
     if (rank_ == root) hub_->ptrs[root] = buf;
     hub_->wait_all();
@@ -159,6 +243,7 @@ class LoopbackComm final : public Comm {
     hub_->wait_all();
   }
   void barrier(hipStream_t s) override {
+    tick(rank_);
     WC_HIP_CHECK(hipStreamSynchronize(s));
     hub_->wait_all();
   }

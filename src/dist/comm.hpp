@@ -40,6 +40,30 @@ class Comm {
   virtual void group_begin() {}
   virtual void group_end() {}
   virtual void barrier(hipStream_t s) = 0;
+  // Wait for everything queued on s (collectives included) — the merge's only
+  // host sync points.  RCCL polls the stream and ncclCommGetAsyncError; an
+  // async error, or no progress within timeout_s(), aborts the communicator
+  // (ncclCommAbort) and throws instead of hanging the job.
+  virtual void sync(hipStream_t s);
+  // Mark the communicator failed: later calls throw, and peers blocked in a
+  // collective of the loopback backend wake up and throw.
+  virtual void abort(const std::string& why) { failed_ = why.empty() ? "aborted" : why; }
+  bool failed() const { return !failed_.empty(); }
+  double timeout_s() const { return timeout_s_; }
+
+ protected:
+  Comm();
+  // Called at the top of every collective: throws once the communicator has
+  // failed, and implements fault injection — WC_COMM_FAULT=<rank>[:<n>] makes
+  // rank <rank> fail its n-th collective (default 1st) as a simulated comm
+  // failure, for tests of the failure path.
+  void tick(int rank);
+  std::string failed_;
+
+ private:
+  double timeout_s_ = 300.0;  // WC_COMM_TIMEOUT_S
+  int fault_rank_ = -1;
+  uint64_t fault_at_ = 0, calls_ = 0;
 };
 
 // RCCL.  unique_id is the 128-byte ncclUniqueId blob.

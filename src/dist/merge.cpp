@@ -48,7 +48,7 @@ void merge_cols_dense(Engine::Impl& im, Comm& comm) {
   comm.allgather(d_meta, d_meta + 4, 4 * 8, s);
   std::vector<uint64_t> all((size_t)W * 4);
   WC_HIP_CHECK(hipMemcpyAsync(all.data(), d_meta + 4, all.size() * 8, hipMemcpyDeviceToHost, s));
-  WC_HIP_CHECK(hipStreamSynchronize(s));
+  comm.sync(s);
   uint64_t n_max = 1, a_max = 16, gmax_end = 0;
   for (int r = 0; r < W; ++r) {
     n_max = std::max(n_max, all[r * 4 + 0]);
@@ -110,7 +110,7 @@ void merge_cols_dense(Engine::Impl& im, Comm& comm) {
   launch_exclusive_scan_u32(flag, ex, m, d_total, s);
   uint32_t vg = 0;
   WC_HIP_CHECK(hipMemcpyAsync(&vg, d_total, 4, hipMemcpyDeviceToHost, s));
-  WC_HIP_CHECK(hipStreamSynchronize(s));
+  comm.sync(s);
   const uint64_t vpad = std::max<uint64_t>(W, ((uint64_t)vg + W - 1) / W * W);
   uint32_t* id_of_pos = A.take_n<uint32_t>(m);
   KeyCols o;
@@ -135,7 +135,7 @@ void merge_cols_dense(Engine::Impl& im, Comm& comm) {
   comm.reduce_scatter_u64(dfirst, sfirst, vpad / W, RedOp::Min, s);
   comm.allgather(scnt, o.cnt, vpad / W * 8, s);
   comm.allgather(sfirst, o.first, vpad / W * 8, s);
-  WC_HIP_CHECK(hipStreamSynchronize(s));
+  comm.sync(s);
 
   o.n = vg;
   im.cols = o;
@@ -216,7 +216,7 @@ void merge_to_root(Engine::Impl& im, Comm& comm, const std::vector<uint64_t>& ra
     launch_mrow_compact(recv_rows, state, tcnt, tfirst, T, d_base, d_base + W + 1, (uint32_t)W, merged, d_m, s);
     unsigned long long G = 0;
     WC_HIP_CHECK(hipMemcpyAsync(&G, d_m, 8, hipMemcpyDeviceToHost, s));
-    WC_HIP_CHECK(hipStreamSynchronize(s));
+    comm.sync(s);
     o.n = G;
     o.k0 = take_aligned<uint64_t>(A, G);
     o.k1 = take_aligned<uint64_t>(A, G);
@@ -229,7 +229,7 @@ void merge_to_root(Engine::Impl& im, Comm& comm, const std::vector<uint64_t>& ra
     WC_HIP_CHECK(hipMemcpyAsync(d_gbase, gb, sizeof gb, hipMemcpyHostToDevice, s));
     launch_mrow_to_cols(merged, G, d_gbase, d_gbase + 2, 1u, o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len, s);
   }
-  WC_HIP_CHECK(hipStreamSynchronize(s));  // also: base[] / gb[] are pageable host memory
+  comm.sync(s);  // also: base[] / gb[] are pageable host memory
   im.cols = o;
   im.cols_arena = recv_bytes;
   im.cols_arena_bytes = R == 0 ? rbt : 0;
@@ -256,7 +256,7 @@ void merge_cols_shuffle(Engine::Impl& im, Comm& comm, bool all_ranks) {
   comm.allgather(d_cnt, d_all, C * 8, s);
   std::vector<unsigned long long> all((size_t)W * C);
   WC_HIP_CHECK(hipMemcpyAsync(all.data(), d_all, all.size() * 8, hipMemcpyDeviceToHost, s));
-  WC_HIP_CHECK(hipStreamSynchronize(s));
+  comm.sync(s);
   uint64_t gmax_end = 0;
   for (int r = 0; r < W; ++r) gmax_end = std::max<uint64_t>(gmax_end, all[(size_t)r * C + 2 * W]);
   std::vector<uint64_t> rank_rows(W, 0), rank_bytes(W, 0);
@@ -353,7 +353,7 @@ void merge_cols_shuffle(Engine::Impl& im, Comm& comm, bool all_ranks) {
   comm.allgather(d_own, d_owns, 16, s);
   std::vector<unsigned long long> owns(2 * (size_t)W);
   WC_HIP_CHECK(hipMemcpyAsync(owns.data(), d_owns, owns.size() * 8, hipMemcpyDeviceToHost, s));
-  WC_HIP_CHECK(hipStreamSynchronize(s));  // also: base[] / own_bytes are pageable host memory
+  comm.sync(s);  // also: base[] / own_bytes are pageable host memory
   const unsigned long long own[2] = {owns[2 * (size_t)R], own_bytes};
   std::vector<size_t> go_r(W, 0), gb_r(W, 0), go_b(W, 0), gb_b(W, 0), zs(W, 0);
   std::vector<size_t> sr(W, 0), sb(W, 0);
@@ -402,7 +402,7 @@ void merge_cols_shuffle(Engine::Impl& im, Comm& comm, bool all_ranks) {
     launch_mrow_to_cols(grows, G, d_gbase, d_gbase + W + 1, (uint32_t)W, o.k0, o.k1, o.cnt, o.first, o.sref_off,
                         o.sref_len, s);
   }
-  WC_HIP_CHECK(hipStreamSynchronize(s));
+  comm.sync(s);
   im.cols = o;
   im.cols_arena = gbytes;
   im.cols_arena_bytes = have ? GB : 0;

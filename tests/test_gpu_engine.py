@@ -232,6 +232,46 @@ def test_rccl_merge_protocol_world1(merge_mode):
     assert out.returncode == 0 and b"ok" in out.stdout, out.stderr.decode()[-2000:]
 
 
+@pytest.mark.parametrize("fault", ["1:1", "2:3", "0:2"])
+@pytest.mark.parametrize("merge_mode", [0, 1])
+def test_loopback_injected_comm_fault(fault, merge_mode, monkeypatch):
+    """one rank's collective fails (WC_COMM_FAULT=<rank>:<n>); every
+    rank must leave its merge with an error — the failed rank aborts the
+    communicator, which wakes the peers blocked in the collective — instead of
+    hanging or returning a partial table.  A fresh job afterwards is unaffected."""
+    text = ops.synth_host(1 << 20, seed=3, vocab=3000)
+    monkeypatch.setenv("WC_MERGE_ROOT_ROWS", "0")  # the owner exchange: most collectives
+    monkeypatch.setenv("WC_COMM_FAULT", fault)
+    with pytest.raises(RuntimeError, match="injected comm fault"):
+        ops.loopback_count(text, 3, chunk_bytes=1 << 20, merge_mode=merge_mode, all_ranks=True)
+    monkeypatch.delenv("WC_COMM_FAULT")
+    assert_same(ops.loopback_count(text, 3, chunk_bytes=1 << 20, merge_mode=merge_mode), ops.cpu_count(text))
+
+
+def test_rccl_injected_fault_aborts_communicator():
+    """RCCL path of the failure handling: the injected fault aborts the
+    communicator (ncclCommAbort) and raises; a later merge on it raises at once
+    ('failed earlier') instead of issuing collectives on a dead communicator.
+    Child process: the env switches must not leak into other tests."""
+    code = (
+        "from cuda_mapreduce_amd import ops\n"
+        "uid = ops.Comm.unique_id(); comm = ops.Comm(uid, 0, 1, 0)\n"
+        "e = ops.Engine(device=0, chunk_bytes=1 << 20)\n"
+        "e.count_bytes(ops.synth_host(1 << 18, seed=1, vocab=500))\n"
+        "msgs = []\n"
+        "for _ in range(2):\n"
+        "    try:\n"
+        "        e.result(comm)\n"
+        "    except RuntimeError as ex:\n"
+        "        msgs.append(str(ex))\n"
+        "assert len(msgs) == 2 and 'injected comm fault' in msgs[0] and 'failed earlier' in msgs[1], msgs\n"
+        "e.close(); comm.close(); print('ok')\n"
+    )
+    env = dict(os.environ, WC_MERGE_ALWAYS="1", WC_COMM_FAULT="0:1")
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, timeout=120)
+    assert out.returncode == 0 and b"ok" in out.stdout, out.stderr.decode()[-2000:]
+
+
 def test_cli_golden(tmp_path, golden_text):
     exe = os.path.join(ROOT, "wordcount")
     (tmp_path / "test.txt").write_bytes(golden_text)

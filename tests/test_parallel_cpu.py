@@ -58,3 +58,48 @@ def test_gloo_data_parallel_matches_single(tmp_path, world):
         assert words == want.words
         assert counts == [int(c) for c in want.counts]
         assert first == [int(f) for f in want.first_off]
+
+
+def _fault_worker(rank, world, port, path, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), WC_COMM_FAULT="1:2", WC_COMM_TIMEOUT_S="15")
+    from cuda_mapreduce_amd.parallel import CommFault, DistributedWordCount, init_from_env
+
+    env = init_from_env("gloo")
+    job = DistributedWordCount(env, use_gpu=False)
+    try:
+        job.count_file(path)
+        q.put((rank, "ok", ""))
+    except CommFault as ex:
+        q.put((rank, "fault", str(ex)))
+        q.close()
+        q.join_thread()  # flush the queue before the hard exit
+        os._exit(3)  # the failed rank leaves without tearing down the group, like a crash
+    except Exception as ex:  # peers: gloo reports the lost rank or times out
+        q.put((rank, "error", type(ex).__name__))
+        q.close()
+        q.join_thread()
+        os._exit(4)
+
+
+def test_gloo_injected_comm_fault_fails_every_rank(tmp_path):
+    """a rank whose collective fails (WC_COMM_FAULT=1:2 — rank 1, 2nd
+    collective of the merge) ends the job on EVERY rank with an error within the
+    collective timeout; nobody hangs and nobody reports a (wrong) result."""
+    from cuda_mapreduce_amd.ops import synth_host
+
+    p = tmp_path / "in.txt"
+    p.write_bytes(synth_host(50_000, seed=2, vocab=500))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fault_worker, args=(r, 2, port, str(p), q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    outs = dict((r, (kind, msg)) for r, kind, msg in (q.get(timeout=90) for _ in range(2)))
+    for pr in procs:
+        pr.join(timeout=30)
+    assert outs[1][0] == "fault" and "injected comm fault" in outs[1][1]
+    assert outs[0][0] == "error"
+    assert [pr.exitcode for pr in procs] == [4, 3]
