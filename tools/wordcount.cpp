@@ -14,6 +14,7 @@
 
 #include "../src/common/hip_util.hpp"
 #include "../src/dist/comm.hpp"
+#include "../src/io/checkpoint.hpp"
 #include "../src/io/source.hpp"
 #include "wc/wc.hpp"
 
@@ -33,7 +34,11 @@ const char* kUsage =
     "  --synthetic SIZE[:SEED[:VOCAB[:ZIPF]]]  count generated text instead of FILE\n"
     "  --chunk-bytes N         device chunk size (default 1G)\n"
     "  --host-staged           stream FILE through the pinned host ring (no echo)\n"
-    "  --bench-json PATH       write throughput / stage timings as JSON\n";
+    "  --bench-json PATH       write throughput / stage timings as JSON\n"
+    "  --checkpoint PATH       count FILE in intervals; after each, save the running\n"
+    "                          table + byte offset to PATH (PATH.r<rank>of<N> per GPU)\n"
+    "  --checkpoint-every SIZE interval between checkpoints (default 4G)\n"
+    "  --resume                continue from the checkpoint(s) at PATH when present\n";
 
 uint64_t parse_size(const std::string& s) {
   char* end = nullptr;
@@ -61,6 +66,9 @@ struct Cli {
   uint64_t synth_bytes = 0;
   wc::SynthSpec spec;
   std::string bench_json;
+  std::string ckpt;
+  uint64_t ckpt_every = 4ull << 30;
+  bool resume = false;
 };
 
 Cli parse(int argc, char** argv) {
@@ -90,6 +98,9 @@ Cli parse(int argc, char** argv) {
     else if (a == "--chunk-bytes") c.chunk = parse_size(need("--chunk-bytes"));
     else if (a == "--host-staged") c.host_staged = true;
     else if (a == "--bench-json") c.bench_json = need("--bench-json");
+    else if (a == "--checkpoint") c.ckpt = need("--checkpoint");
+    else if (a == "--checkpoint-every") c.ckpt_every = parse_size(need("--checkpoint-every"));
+    else if (a == "--resume") c.resume = true;
     else if (a == "--synthetic") {
       std::string v = need("--synthetic");
       std::vector<std::string> f;
@@ -105,7 +116,31 @@ Cli parse(int argc, char** argv) {
     else c.file = a;
   }
   if (c.synthetic) c.echo = false;
+  if (!c.ckpt.empty() && (c.synthetic || c.compat)) wc::fail("--checkpoint needs a FILE input and the clean semantics");
+  if (c.resume && c.ckpt.empty()) wc::fail("--resume needs --checkpoint PATH");
   return c;
+}
+
+// Rank `r` of `g`: the saved checkpoint when resuming (validated against the
+// input and the sharding), else a fresh one over the rank's owned range.
+wc::Checkpoint open_checkpoint(const Cli& c, uint64_t input_size, const wc::ShardRange& sr, int r, int g) {
+  const std::string path = wc::checkpoint_path(c.ckpt, r, g);
+  if (c.resume && wc::checkpoint_exists(path)) {
+    wc::Checkpoint k = wc::load_checkpoint(path);
+    if (k.input_size != input_size || k.begin != sr.begin || k.end != sr.end || k.rank != (uint32_t)r ||
+        k.world != (uint32_t)g)
+      wc::fail("checkpoint " + path + " was written for another input or GPU count");
+    std::fprintf(stderr, "wordcount: rank %d resumes at byte %llu of [%llu, %llu) (%u interval(s) done)\n", r,
+                 (unsigned long long)k.next, (unsigned long long)k.begin, (unsigned long long)k.end, k.intervals);
+    return k;
+  }
+  wc::Checkpoint k;
+  k.input_size = input_size;
+  k.begin = k.next = sr.begin;
+  k.end = sr.end;
+  k.rank = (uint32_t)r;
+  k.world = (uint32_t)g;
+  return k;
 }
 
 void write_out(const std::string& s) { std::fwrite(s.data(), 1, s.size(), stdout); }
@@ -141,7 +176,14 @@ int run(const Cli& c) {
       host.assign(v.begin(), v.end());
     }
     const auto* p = reinterpret_cast<const uint8_t*>(host.data());
-    t = c.compat ? wc::cpu::count_reference_compat(p, host.size()) : wc::cpu::count(p, host.size());
+    if (!c.ckpt.empty()) {
+      wc::Checkpoint k = open_checkpoint(c, host.size(), wc::ShardRange{0, host.size()}, 0, 1);
+      wc::run_checkpointed(c.file, k, c.ckpt_every, c.ckpt,
+                           [](const uint8_t* q, uint64_t n, uint64_t base) { return wc::cpu::count(q, n, base); });
+      t = std::move(k.table);
+    } else {
+      t = c.compat ? wc::cpu::count_reference_compat(p, host.size()) : wc::cpu::count(p, host.size());
+    }
     bytes = host.size();
   } else {
     int ndev = 0;
@@ -152,6 +194,7 @@ int run(const Cli& c) {
     std::vector<std::unique_ptr<wc::Comm>> comms;
     if (g > 1) comms = wc::make_rccl_comms_all(devs);
     std::vector<std::string> errs(g);
+    std::vector<wc::KeyTable> rank_tables(g);  // checkpointed runs merge on the host
     const uint64_t total = c.synthetic ? c.synth_bytes : (have_text ? text.size() : wc::file_size(c.file));
     bytes = total;
     auto worker = [&](int r) {
@@ -161,7 +204,21 @@ int run(const Cli& c) {
         o.chunk_bytes = c.chunk;
         o.merge_mode = c.merge_mode;
         wc::Engine eng(o);
-        if (c.synthetic) {
+        if (!c.ckpt.empty()) {
+          // Checkpointed: delimiter-aligned intervals, each finalised on the GPU and
+          // folded into the rank's host table; ranks merge on the host below.
+          const wc::ShardRange sr = wc::shard_range(c.file, r, g);
+          wc::Checkpoint k = open_checkpoint(c, total, sr, r, g);
+          wc::run_checkpointed(c.file, k, c.ckpt_every, wc::checkpoint_path(c.ckpt, r, g),
+                               [&](const uint8_t* q, uint64_t n, uint64_t base) {
+                                 eng.count_host(q, n, base);
+                                 wc::KeyTable kt = eng.result(nullptr, false);
+                                 eng.reset();
+                                 return kt;
+                               });
+          rank_tables[r] = std::move(k.table);
+          return;
+        } else if (c.synthetic) {
           // shard at segment granularity: every segment ends with a delimiter
           const uint64_t nseg = (total + 1023) / 1024, per = (nseg + g - 1) / g;
           const uint64_t s0 = std::min<uint64_t>(nseg, per * r), s1 = std::min<uint64_t>(nseg, per * (r + 1));
@@ -194,6 +251,8 @@ int run(const Cli& c) {
     }
     for (int r = 0; r < g; ++r)
       if (!errs[r].empty()) wc::fail("GPU " + std::to_string(r) + ": " + errs[r]);
+    if (!c.ckpt.empty())
+      for (int r = 0; r < g; ++r) wc::merge_tables(t, rank_tables[r]);
   }
   const double secs = wc::now_seconds() - t0;
   write_out(wc::format_output(t, have_text ? reinterpret_cast<const uint8_t*>(text.data()) : nullptr,
