@@ -3,6 +3,9 @@
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
 #include <mutex>
 
 namespace wc {
@@ -59,6 +62,30 @@ void PinnedBuffer::resize(size_t bytes) {
 
 Range::Range(const char* name) { roctxRangePush(name); }
 Range::~Range() { roctxRangePop(); }
+
+int log_level() {
+  static const int lvl = [] {
+    const char* e = std::getenv("WC_LOG");
+    if (!e || !*e) return (int)LOG_WARN;
+    const std::string v(e);
+    if (v == "debug" || v == "2") return (int)LOG_DEBUG;
+    if (v == "info" || v == "1") return (int)LOG_INFO;
+    return (int)LOG_WARN;
+  }();
+  return lvl;
+}
+
+void log_printf(int level, const char* fmt, ...) {
+  static const double t0 = now_seconds();
+  static const char* tag[] = {"warn", "info", "debug"};
+  char line[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(line, sizeof(line), fmt, ap);
+  va_end(ap);
+  // one fprintf per line: lines of concurrent rank threads do not interleave
+  std::fprintf(stderr, "[wc %s %9.3f] %s\n", tag[level < 0 ? 0 : level > 2 ? 2 : level], now_seconds() - t0, line);
+}
 
 double now_seconds() {
   using clk = std::chrono::steady_clock;

@@ -83,6 +83,16 @@ class Range {
 
 double now_seconds();
 
+// Diagnostics on stderr (stdout stays reference-identical).
+// WC_LOG=warn (default) | info | debug  (or 0 / 1 / 2).
+enum LogLevel { LOG_WARN = 0, LOG_INFO = 1, LOG_DEBUG = 2 };
+int log_level();
+void log_printf(int level, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+#define WC_LOG(level, ...)                                            \
+  do {                                                                \
+    if ((level) <= ::wc::log_level()) ::wc::log_printf((level), __VA_ARGS__); \
+  } while (0)
+
 // Number of compute units of the current device (cached per device).
 int device_cu_count(int device);
 

@@ -130,6 +130,7 @@ class RcclComm final : public Comm {
   void abort(const std::string& why) override {
     Comm::abort(why);
     if (c_) {
+      WC_LOG(LOG_WARN, "rank %d: aborting RCCL communicator: %s", rank_, why.c_str());
       (void)ncclCommAbort(c_);
       c_ = nullptr;
     }

@@ -213,6 +213,7 @@ void Engine::Impl::split_table() {
   launch_table_split(table(), dst.v, s);
   cur ^= 1;
   st.table_splits++;
+  WC_LOG(LOG_INFO, "dev %d: key table split %u -> %u buckets", dev, 1u << lg, 2u << lg);
 }
 
 void Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev,
@@ -223,6 +224,8 @@ void Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
     // Shuffle regions too small for this chunk's record skew: the reduce was
     // skipped (table untouched), so re-run exactly this chunk, smaller.
     st.map_reruns++;
+    WC_LOG(LOG_INFO, "dev %d: shuffle region overflow at base=%llu len=%llu -> re-run in halves", dev,
+           (unsigned long long)base, (unsigned long long)len);
     auto run = [&](const uint8_t* t, uint64_t l, uint64_t av, uint64_t b, int pv, uint32_t rb) {
       const uint32_t bl = blocks_for(l);
       launch_pass(t, l, av, b, pv, rb, bl);
@@ -266,6 +269,9 @@ void Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
     fail("key arena exhausted (" + std::to_string(opt.arena_bytes) + " bytes); raise arena_bytes");
   st.tokens += tokens;
   st.chunks++;
+  WC_LOG(LOG_DEBUG, "dev %d: chunk base=%llu len=%llu blocks=%u tokens=%llu records=%llu", dev,
+         (unsigned long long)base, (unsigned long long)len, blocks, (unsigned long long)tokens,
+         (unsigned long long)c.records);
   max_end = std::max(max_end, base + len);
   if (max_occ >= (uint32_t)TAB_SPLIT_AT && table().log2_buckets < opt.max_log2_tab_buckets) split_table();
 }
@@ -572,6 +578,9 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
   im.sort_cols_by_first();
   WC_HIP_CHECK(hipStreamSynchronize(im.s));
   im.st.finalize_ms += (now_seconds() - t0) * 1e3;
+  WC_LOG(LOG_INFO, "dev %d: finalize %.3f ms (merge %.3f ms), %llu keys, %u chunk(s), %llu records, %u re-run(s)",
+         im.dev, (now_seconds() - t0) * 1e3, im.st.merge_ms, (unsigned long long)im.cols.n, im.st.chunks,
+         (unsigned long long)im.st.records, im.st.map_reruns);
   return im.cols.n;
 }
 

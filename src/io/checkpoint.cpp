@@ -234,6 +234,8 @@ void run_checkpointed(const std::string& file, Checkpoint& c, uint64_t interval,
       c.intervals++;
       if (!path.empty()) {
         save_checkpoint(path, c);
+        WC_LOG(LOG_INFO, "checkpoint %s: rank %u interval %u, next byte %llu of %llu, %zu keys", path.c_str(), c.rank,
+               c.intervals, (unsigned long long)c.next, (unsigned long long)c.end, c.table.size());
         if (stop_after && ++written == stop_after && c.next < c.end)
           fail("WC_CKPT_STOP_AFTER: stopped after " + std::to_string(written) + " checkpoint(s)");
       }

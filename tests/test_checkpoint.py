@@ -125,3 +125,16 @@ def test_gpu_resume_from_cpu_checkpoint(tmp_path):
     g = run(["t.txt", "--no-echo", "--resume"] + ck, tmp_path)
     assert g.returncode == 0, g.stderr
     assert g.stdout == run(["t.txt", "--no-echo", "--cpu"], tmp_path).stdout
+
+
+@pytest.mark.gpu
+def test_gpu_bench_json_stages(tmp_path):
+    import json
+
+    data = make_text(tmp_path / "t.txt", n=20000)
+    r = run(["t.txt", "--no-echo", "--no-list", "--bench-json", "b.json"], tmp_path, {"WC_LOG": "debug"})
+    assert r.returncode == 0, r.stderr
+    d = json.loads((tmp_path / "b.json").read_text())
+    assert d["path"] == "gpu" and d["tokens"] == len(data.split()) and d["chunks"] >= 1
+    assert d["stages_ms"]["map_reduce"] > 0 and d["stages_ms"]["finalize"] > 0
+    assert b"[wc debug" in r.stderr and b"finalize" in r.stderr

@@ -144,3 +144,21 @@ def test_cli_top_k(tmp_path):
     out = subprocess.run([exe, str(p), "--cpu", "--no-echo", "--top", "2"], capture_output=True, timeout=60)
     assert out.stdout.split(b"-" * 26 + b"\n")[1] == b"a\t3\nb\t2\n"
     assert out.stdout.endswith(b"Total Count:7\n")
+
+
+def test_cli_bench_json_and_log_levels(tmp_path, golden_text):
+    # stdout stays reference-identical; diagnostics go to stderr / JSON
+    import json
+
+    exe = os.path.join(ROOT, "wordcount")
+    (tmp_path / "test.txt").write_bytes(golden_text)
+    env = dict(os.environ, WC_LOG="info")
+    out = subprocess.run([exe, "--cpu", "--bench", "--bench-json", "b.json", "--checkpoint", "c", "--checkpoint-every",
+                          "20"], cwd=tmp_path, capture_output=True, timeout=60, env=env)
+    assert out.returncode == 0 and out.stdout == GOLDEN_OUTPUT
+    assert b"wordcount bench: {" in out.stderr and b"[wc info" in out.stderr
+    d = json.loads((tmp_path / "b.json").read_text())
+    assert d["tokens"] == 9 and d["keys"] == 6 and d["path"] == "cpu" and "stages_ms" in d
+    quiet = subprocess.run([exe, "--cpu"], cwd=tmp_path, capture_output=True, timeout=60,
+                           env=dict(os.environ, WC_LOG="warn"))
+    assert quiet.stderr == b""

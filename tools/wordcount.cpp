@@ -6,6 +6,7 @@
 // `wordcount <file>` is the north-star form; everything else is opt-in.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -35,6 +36,7 @@ const char* kUsage =
     "  --chunk-bytes N         device chunk size (default 1G)\n"
     "  --host-staged           stream FILE through the pinned host ring (no echo)\n"
     "  --bench-json PATH       write throughput / stage timings as JSON\n"
+    "  --bench                 print throughput / stage timings to stderr\n"
     "  --checkpoint PATH       count FILE in intervals; after each, save the running\n"
     "                          table + byte offset to PATH (PATH.r<rank>of<N> per GPU)\n"
     "  --checkpoint-every SIZE interval between checkpoints (default 4G)\n"
@@ -66,6 +68,7 @@ struct Cli {
   uint64_t synth_bytes = 0;
   wc::SynthSpec spec;
   std::string bench_json;
+  bool bench = false;
   std::string ckpt;
   uint64_t ckpt_every = 4ull << 30;
   bool resume = false;
@@ -98,6 +101,7 @@ Cli parse(int argc, char** argv) {
     else if (a == "--chunk-bytes") c.chunk = parse_size(need("--chunk-bytes"));
     else if (a == "--host-staged") c.host_staged = true;
     else if (a == "--bench-json") c.bench_json = need("--bench-json");
+    else if (a == "--bench") c.bench = true;
     else if (a == "--checkpoint") c.ckpt = need("--checkpoint");
     else if (a == "--checkpoint-every") c.ckpt_every = parse_size(need("--checkpoint-every"));
     else if (a == "--resume") c.resume = true;
@@ -143,6 +147,20 @@ wc::Checkpoint open_checkpoint(const Cli& c, uint64_t input_size, const wc::Shar
   return k;
 }
 
+void add_stats(wc::Stats& a, const wc::Stats& b) {
+  a.bytes += b.bytes;
+  a.tokens += b.tokens;
+  a.keys = std::max(a.keys, b.keys);
+  a.records += b.records;
+  a.chunks += b.chunks;
+  a.map_reruns += b.map_reruns;
+  a.table_splits += b.table_splits;
+  a.h2d_ms += b.h2d_ms;
+  a.map_reduce_ms += b.map_reduce_ms;
+  a.finalize_ms += b.finalize_ms;
+  a.merge_ms += b.merge_ms;
+}
+
 void write_out(const std::string& s) { std::fwrite(s.data(), 1, s.size(), stdout); }
 
 int run(const Cli& c) {
@@ -151,6 +169,7 @@ int run(const Cli& c) {
   bool have_text = false;
   const double t0 = wc::now_seconds();
   uint64_t bytes = 0;
+  wc::Stats stages;  // GPU path: stage timings (max over ranks) and counters (sums)
 
   const bool need_host_text = !c.synthetic && (c.echo || c.cpu || c.compat);
   if (!c.synthetic) {
@@ -195,6 +214,7 @@ int run(const Cli& c) {
     if (g > 1) comms = wc::make_rccl_comms_all(devs);
     std::vector<std::string> errs(g);
     std::vector<wc::KeyTable> rank_tables(g);  // checkpointed runs merge on the host
+    std::vector<wc::Stats> rank_stats(g);
     const uint64_t total = c.synthetic ? c.synth_bytes : (have_text ? text.size() : wc::file_size(c.file));
     bytes = total;
     auto worker = [&](int r) {
@@ -213,6 +233,7 @@ int run(const Cli& c) {
                                [&](const uint8_t* q, uint64_t n, uint64_t base) {
                                  eng.count_host(q, n, base);
                                  wc::KeyTable kt = eng.result(nullptr, false);
+                                 add_stats(rank_stats[r], eng.stats());
                                  eng.reset();
                                  return kt;
                                });
@@ -237,6 +258,7 @@ int run(const Cli& c) {
           eng.count_source(src, sr.begin);
         }
         wc::KeyTable kt = eng.result(g > 1 ? comms[r].get() : nullptr, false);
+        rank_stats[r] = eng.stats();
         if (r == 0) t = std::move(kt);
       } catch (const std::exception& ex) {
         errs[r] = ex.what();
@@ -253,18 +275,38 @@ int run(const Cli& c) {
       if (!errs[r].empty()) wc::fail("GPU " + std::to_string(r) + ": " + errs[r]);
     if (!c.ckpt.empty())
       for (int r = 0; r < g; ++r) wc::merge_tables(t, rank_tables[r]);
+    for (int r = 0; r < g; ++r) {
+      const wc::Stats& x = rank_stats[r];
+      // per-rank stage maxima: ranks run concurrently, the slowest sets the pace
+      stages.map_reduce_ms = std::max(stages.map_reduce_ms, x.map_reduce_ms);
+      stages.finalize_ms = std::max(stages.finalize_ms, x.finalize_ms);
+      stages.merge_ms = std::max(stages.merge_ms, x.merge_ms);
+      stages.h2d_ms = std::max(stages.h2d_ms, x.h2d_ms);
+      stages.records += x.records;
+      stages.chunks += x.chunks;
+      stages.map_reruns += x.map_reruns;
+      stages.table_splits += x.table_splits;
+    }
   }
   const double secs = wc::now_seconds() - t0;
   write_out(wc::format_output(t, have_text ? reinterpret_cast<const uint8_t*>(text.data()) : nullptr,
                               have_text ? text.size() : 0, c.echo && have_text, c.list, c.top));
+  const bool gpu_path = !(c.cpu || c.compat);
+  char js[1024];
+  std::snprintf(js, sizeof(js),
+                "{\"bytes\": %llu, \"tokens\": %llu, \"keys\": %zu, \"seconds\": %.6f, \"gb_per_s\": %.3f, "
+                "\"words_per_s\": %.1f, \"gpus\": %d, \"path\": \"%s\", \"chunk_bytes\": %llu, "
+                "\"stages_ms\": {\"map_reduce\": %.3f, \"finalize\": %.3f, \"merge\": %.3f}, "
+                "\"chunks\": %u, \"records\": %llu, \"map_reruns\": %u, \"table_splits\": %u}",
+                (unsigned long long)bytes, (unsigned long long)t.total, t.size(), secs, bytes / secs / 1e9,
+                t.total / secs, gpu_path ? c.gpus : 0, c.compat ? "compat" : (c.cpu ? "cpu" : "gpu"),
+                (unsigned long long)c.chunk, stages.map_reduce_ms, stages.finalize_ms, stages.merge_ms,
+                stages.chunks, (unsigned long long)stages.records, stages.map_reruns, stages.table_splits);
+  if (c.bench) std::fprintf(stderr, "wordcount bench: %s\n", js);
   if (!c.bench_json.empty()) {
     FILE* f = std::fopen(c.bench_json.c_str(), "w");
     if (!f) wc::fail("cannot write " + c.bench_json);
-    std::fprintf(f,
-                 "{\"bytes\": %llu, \"tokens\": %llu, \"keys\": %zu, \"seconds\": %.6f, \"gb_per_s\": %.3f, "
-                 "\"words_per_s\": %.1f, \"gpus\": %d, \"path\": \"%s\"}\n",
-                 (unsigned long long)bytes, (unsigned long long)t.total, t.size(), secs, bytes / secs / 1e9,
-                 t.total / secs, c.cpu || c.compat ? 0 : c.gpus, c.compat ? "compat" : (c.cpu ? "cpu" : "gpu"));
+    std::fprintf(f, "%s\n", js);
     std::fclose(f);
   }
   return 0;
