@@ -39,11 +39,23 @@ $(BUILD)/tools/wordcount.o: tools/wordcount.cpp $(HEADERS)
 wordcount: $(BUILD)/tools/wordcount.o $(HIP_OBJS) $(CPP_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ $(LIBS)
 
-# Host-side sanitizers only: GPU ASan is not available on this pool.
-ASAN := -O1 -g -std=c++17 -fPIC -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -fno-omit-frame-pointer
-asan: $(HIP_OBJS)
-	@mkdir -p $(BUILD)/asan
-	$(HIPCC) $(ASAN) $(INCS) -o $(BUILD)/wordcount_asan tools/wordcount.cpp $(CPP_SRCS) $(HIP_OBJS) $(LIBS)
+# Host-side sanitizers only: GPU ASan is not available on this pool.  Host
+# sources are built by g++ with ASan/UBSan; the HIP objects (host stubs +
+# gfx950 code objects) link in unsanitised.
+ASAN     := -O1 -g -std=c++17 -fPIC -fsanitize=address,undefined -fno-omit-frame-pointer
+ASAN_OBJS := $(patsubst src/%.cpp,$(BUILD)/asan/%.o,$(CPP_SRCS)) $(BUILD)/asan/tools/wordcount.o
+
+$(BUILD)/asan/%.o: src/%.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(ASAN) -D__HIP_PLATFORM_AMD__ $(INCS) -c $< -o $@
+
+$(BUILD)/asan/tools/wordcount.o: tools/wordcount.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(ASAN) -D__HIP_PLATFORM_AMD__ $(INCS) -c $< -o $@
+
+asan: $(BUILD)/wordcount_asan
+$(BUILD)/wordcount_asan: $(ASAN_OBJS) $(HIP_OBJS)
+	$(CXX) -fsanitize=address,undefined -o $@ $^ $(LIBS)
 
 clean:
 	rm -rf $(BUILD) $(PYLIB) wordcount

@@ -162,3 +162,28 @@ def test_cli_bench_json_and_log_levels(tmp_path, golden_text):
     quiet = subprocess.run([exe, "--cpu"], cwd=tmp_path, capture_output=True, timeout=60,
                            env=dict(os.environ, WC_LOG="warn"))
     assert quiet.stderr == b""
+
+
+@pytest.mark.timeout(600)
+def test_host_code_under_asan_ubsan(tmp_path, golden_text):
+    """host code (CLI, CPU oracle, quirks emulation, checkpoint I/O,
+    formatter) built with -fsanitize=address,undefined (`make asan`) runs the CPU
+    paths clean; GPU code is not sanitised (no GPU ASan on this pool)."""
+    b = subprocess.run(["make", "-C", ROOT, "-j8", "asan"], capture_output=True, timeout=600)
+    assert b.returncode == 0, b.stderr[-2000:]
+    exe = os.path.join(ROOT, "build", "wordcount_asan")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    (tmp_path / "test.txt").write_bytes(golden_text)
+    rng = np.random.default_rng(5)
+    alphabet = np.frombuffer(b"abcXYZ,\t  \r\n", dtype=np.uint8)
+    (tmp_path / "r.txt").write_bytes(alphabet[rng.integers(0, len(alphabet), 200000)].tobytes())
+    for args in (["--cpu"], ["--compat=reference"], ["r.txt", "--cpu", "--no-echo", "--top", "5"],
+                 ["r.txt", "--compat=reference", "--no-echo"],
+                 ["r.txt", "--cpu", "--no-echo", "--checkpoint", "ck", "--checkpoint-every", "30000"],
+                 ["r.txt", "--cpu", "--no-echo", "--checkpoint", "ck", "--resume", "--bench"]):
+        r = subprocess.run([exe] + args, cwd=tmp_path, capture_output=True, timeout=120, env=env)
+        assert r.returncode == 0, (args, r.stderr[-3000:])
+        assert b"ERROR: AddressSanitizer" not in r.stderr and b"runtime error" not in r.stderr, args
+    r = subprocess.run([exe, "--cpu"], cwd=tmp_path, capture_output=True, timeout=120, env=env)
+    assert r.stdout == GOLDEN_OUTPUT
