@@ -57,13 +57,7 @@ struct Reader {
 };
 
 void pread_all(int fd, uint8_t* dst, uint64_t n, uint64_t off, const std::string& file) {
-  while (n) {
-    const ssize_t got = ::pread(fd, dst, n, (off_t)off);
-    if (got <= 0) fail("read failed: " + file);
-    dst += got;
-    off += (uint64_t)got;
-    n -= (uint64_t)got;
-  }
+  if (pread_parallel(fd, dst, n, off) != n) fail("read failed (file shrank?): " + file);
 }
 
 }  // namespace

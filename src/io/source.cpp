@@ -6,8 +6,11 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <stdexcept>
+#include <thread>
 #include <vector>
 
 #include "../common/hip_util.hpp"
@@ -77,19 +80,55 @@ FileSource::~FileSource() {
   if (fd_ >= 0) ::close(fd_);
 }
 
-uint64_t FileSource::read(uint8_t* dst, uint64_t cap) {
-  uint64_t got = 0;
-  while (got < cap && pos_ < end_) {
-    const uint64_t want = std::min<uint64_t>(cap - got, end_ - pos_);
-    const ssize_t k = ::pread(fd_, dst + got, std::min<uint64_t>(want, 1ull << 30), (off_t)pos_);
-    if (k < 0) {
-      if (errno == EINTR) continue;
-      fail(std::string("read error: ") + std::strerror(errno));
+uint64_t pread_parallel(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
+  // One thread copies ~5-8 GB/s out of the page cache, below PCIe Gen5 x16
+  // (57 GB/s measured pinned H2D): large reads are split over WC_IO_THREADS
+  // (default 8) threads, 16 MiB minimum per thread.
+  static const unsigned kThreads = [] {
+    const char* e = std::getenv("WC_IO_THREADS");
+    const long v = e ? std::strtol(e, nullptr, 10) : 8;
+    return (unsigned)std::max(1l, std::min(64l, v));
+  }();
+  constexpr uint64_t kMinSlice = 16ull << 20;
+  const unsigned t = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(kThreads, n / kMinSlice));
+  auto slice = [&](uint64_t b, uint64_t e, uint64_t& got, int& err) {
+    got = 0;
+    err = 0;
+    while (b + got < e) {
+      const ssize_t k = ::pread(fd, dst + b + got, std::min<uint64_t>(e - b - got, 1ull << 30), (off_t)(off + b + got));
+      if (k < 0) {
+        if (errno == EINTR) continue;
+        err = errno;
+        return;
+      }
+      if (k == 0) return;  // end of file
+      got += (uint64_t)k;
     }
-    if (k == 0) break;
-    got += (uint64_t)k;
-    pos_ += (uint64_t)k;
+  };
+  std::vector<uint64_t> got(t), lo(t);
+  std::vector<int> err(t);
+  const uint64_t per = (n + t - 1) / t;
+  std::vector<std::thread> th;
+  for (unsigned i = 0; i < t; ++i) {
+    lo[i] = std::min(n, (uint64_t)i * per);
+    const uint64_t hi = std::min(n, lo[i] + per);
+    if (i + 1 < t) th.emplace_back(slice, lo[i], hi, std::ref(got[i]), std::ref(err[i]));
+    else slice(lo[i], hi, got[i], err[i]);
   }
+  for (auto& x : th) x.join();
+  uint64_t total = 0;  // contiguous prefix: a short slice ends the read
+  for (unsigned i = 0; i < t; ++i) {
+    if (err[i]) fail(std::string("read error: ") + std::strerror(err[i]));
+    total += got[i];
+    if (lo[i] + got[i] < std::min(n, lo[i] + per)) break;
+  }
+  return total;
+}
+
+uint64_t FileSource::read(uint8_t* dst, uint64_t cap) {
+  const uint64_t want = std::min<uint64_t>(cap, end_ - pos_);
+  const uint64_t got = want ? pread_parallel(fd_, dst, want, pos_) : 0;
+  pos_ += got;
   return got;
 }
 

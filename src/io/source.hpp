@@ -51,4 +51,8 @@ class ReplaySource : public ChunkSource {
 
 std::string read_file(const std::string& path);
 
+// pread of [off, off+n) into dst split over worker threads; returns the bytes
+// read (short only at end of file), throws on a read error.
+uint64_t pread_parallel(int fd, uint8_t* dst, uint64_t n, uint64_t off);
+
 }  // namespace wc
