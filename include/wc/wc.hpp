@@ -45,6 +45,11 @@ struct Options {
   uint64_t arena_bytes = 256ull << 20; // key arena for >8-byte words
   uint32_t map_blocks = 0;             // 0 = 2 per CU
   uint32_t staging_buffers = 3;        // pinned host ring depth (host-staged path)
+  // Streaming sources (files, host buffers) move through the pinned ring in
+  // pieces of min(chunk_bytes, stream_chunk_bytes): small pieces start the
+  // pipeline sooner and keep the page-locked ring cheap to allocate (4 GiB
+  // file, whole CLI: 3.5 GB/s at 1 GiB pieces, 11 GB/s at 64 MiB).
+  uint64_t stream_chunk_bytes = 64ull << 20;
   // Cross-GPU merge: 0 = shuffle (all-to-all of each key to its hash owner, owner-side
   // merge, gather to rank 0); 1 = dense (dictionary union on every rank, reduce-scatter of
   // dense count vectors + all-gather).

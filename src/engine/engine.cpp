@@ -450,7 +450,9 @@ void Engine::count_source(ChunkSource& src, uint64_t global_base) {
   WC_HIP_CHECK(hipSetDevice(im.dev));
   Range r("wc_count_stream");
   const double t0 = now_seconds();
-  const uint64_t C = im.opt.chunk_bytes;
+  uint64_t stream = im.opt.stream_chunk_bytes;
+  if (const char* e = std::getenv("WC_STREAM_CHUNK")) stream = std::strtoull(e, nullptr, 10);  // sweeps only
+  const uint64_t C = std::min(im.opt.chunk_bytes, std::max<uint64_t>(1ull << 20, stream / 256 * 256));
   im.ensure_staging(C);
   std::vector<uint8_t> carry;
   bool eof = false;
