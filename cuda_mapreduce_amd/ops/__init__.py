@@ -5,6 +5,7 @@ from .engine import (  # noqa: F401
     Result,
     cpu_count,
     cpu_count_compat,
+    cpu_count_file_checkpointed,
     default_options,
     device_count,
     format_output,

@@ -57,6 +57,9 @@ def _load() -> ctypes.CDLL:
         "wc_engine_reset": (c_int, [c_void_p]),
         "wc_count_host": (c_int, [c_void_p, P8, c_uint64, c_uint64]),
         "wc_count_file": (c_int, [c_void_p, c_char_p, c_uint64, c_uint64, c_uint64]),
+        "wc_count_file_checkpointed": (c_void_p, [c_void_p, c_char_p, c_uint64, c_uint64, c_int, c_int, c_char_p,
+                                                   c_uint64, c_int]),
+        "wc_result_merge": (c_int, [c_void_p, c_void_p]),
         "wc_count_replay": (c_int, [c_void_p, P8, c_uint64, c_uint64, c_uint64]),
         "wc_count_pinned_replay": (c_int, [c_void_p, P8, c_uint64, c_uint64, c_uint64]),
         "wc_synth_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint32, c_double]),

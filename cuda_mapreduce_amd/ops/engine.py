@@ -152,6 +152,14 @@ class Engine:
             end = os.path.getsize(path)
         check(lib.wc_count_file(self._p, path.encode(), begin, end, begin if global_base is None else global_base))
 
+    def count_file_checkpointed(self, path: str, checkpoint: str = "", interval: int = 4 << 30, resume: bool = True,
+                                begin: int = 0, end: Optional[int] = None, rank: int = 0, world: int = 1) -> "Result":
+        """Resumable count of [begin, end) of a file: delimiter-aligned intervals,
+        each finalised on the GPU and folded into a host table that is saved with the next byte
+        offset to `checkpoint` (per-rank suffix when world > 1).  Returns this rank's table; the
+        engine's running table is left empty."""
+        return _count_file_checkpointed(self._p, path, checkpoint, interval, resume, begin, end, rank, world)
+
     def count_replay(self, pool: np.ndarray, total: int, global_base: int = 0) -> None:
         """Replay a host pool of self-contained chunks until `total` bytes (host-staged config)."""
         ptr, keep = _u8ptr(pool)
@@ -186,7 +194,22 @@ class Engine:
         return json.loads(buf.value.decode())
 
 
+def _count_file_checkpointed(eng, path, checkpoint, interval, resume, begin, end, rank, world) -> "Result":
+    import os
+
+    if end is None:
+        end = os.path.getsize(path)
+    return Result._from_native(check_ptr(lib.wc_count_file_checkpointed(
+        eng, path.encode(), begin, end, rank, world, checkpoint.encode(), interval, int(resume))))
+
+
 # ---------------------------------------------------------------- CPU paths --
+def cpu_count_file_checkpointed(path: str, checkpoint: str = "", interval: int = 4 << 30, resume: bool = True,
+                                begin: int = 0, end: Optional[int] = None) -> Result:
+    """CPU-oracle twin of Engine.count_file_checkpointed (same checkpoint file format)."""
+    return _count_file_checkpointed(None, path, checkpoint, interval, resume, begin, end, 0, 1)
+
+
 def cpu_count(data: bytes, global_base: int = 0) -> Result:
     """Single-thread CPU oracle (BASELINE config 1)."""
     ptr, keep = _u8ptr(data)

@@ -41,6 +41,14 @@ void wc_engine_destroy(wc_engine* e);
 int wc_engine_reset(wc_engine* e);
 int wc_count_host(wc_engine* e, const uint8_t* text, uint64_t n, uint64_t global_base);
 int wc_count_file(wc_engine* e, const char* path, uint64_t begin, uint64_t end, uint64_t global_base);
+/* Checkpointed count of [begin, end) of a file (rank `rank` of `world`): intervals of
+   `interval` bytes, each finalised and folded into a host table saved with the next offset to
+   `ckpt` (empty: no file).  `resume` continues from an existing checkpoint.  e == NULL counts
+   on the CPU oracle.  Returns this rank's table (first-occurrence order) or NULL on error. */
+wc_result* wc_count_file_checkpointed(wc_engine* e, const char* path, uint64_t begin, uint64_t end, int rank,
+                                      int world, const char* ckpt, uint64_t interval, int resume);
+/* Fold `src` into `dst` (counts add, first offset = min, first-occurrence order). */
+int wc_result_merge(wc_result* dst, const wc_result* src);
 int wc_count_replay(wc_engine* e, const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t global_base);
 /* Host-staged benchmark path: pool page-locked once, chunks DMA'd directly. */
 int wc_count_pinned_replay(wc_engine* e, const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t global_base);

@@ -6,6 +6,7 @@
 
 #include "common/hip_util.hpp"
 #include "dist/comm.hpp"
+#include "io/checkpoint.hpp"
 #include "io/source.hpp"
 #include "kernels/kernels.hpp"
 #include "wc/wc.h"
@@ -138,6 +139,28 @@ int wc_count_file(wc_engine* e, const char* path, uint64_t begin, uint64_t end, 
     e->e->count_source(src, base);
   });
 }
+
+wc_result* wc_count_file_checkpointed(wc_engine* e, const char* path, uint64_t begin, uint64_t end, int rank,
+                                      int world, const char* ckpt, uint64_t interval, int resume) {
+  wc_result* r = nullptr;
+  const int rc = guard([&] {
+    const std::string file(path), base(ckpt ? ckpt : "");
+    const std::string cpath = base.empty() ? std::string() : wc::checkpoint_path(base, rank, world);
+    wc::Checkpoint k = wc::open_checkpoint(cpath, resume != 0 && !cpath.empty(), wc::file_size(file), begin, end,
+                                           rank, world);
+    wc::run_checkpointed(file, k, interval, cpath, [&](const uint8_t* q, uint64_t n, uint64_t gbase) {
+      if (!e) return wc::cpu::count(q, n, gbase);
+      e->e->count_host(q, n, gbase);
+      wc::KeyTable kt = e->e->result(nullptr, false);
+      e->e->reset();
+      return kt;
+    });
+    r = new wc_result{std::move(k.table)};
+  });
+  return rc == 0 ? r : nullptr;
+}
+
+int wc_result_merge(wc_result* dst, const wc_result* src) { return guard([&] { wc::merge_tables(dst->t, src->t); }); }
 
 int wc_count_replay(wc_engine* e, const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t base) {
   return guard([&] {

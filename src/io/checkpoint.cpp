@@ -194,6 +194,26 @@ Checkpoint load_checkpoint(const std::string& path) {
   return c;
 }
 
+Checkpoint open_checkpoint(const std::string& path, bool resume, uint64_t input_size, uint64_t begin, uint64_t end,
+                           int rank, int world) {
+  if (resume && checkpoint_exists(path)) {
+    Checkpoint k = load_checkpoint(path);
+    if (k.input_size != input_size || k.begin != begin || k.end != end || k.rank != (uint32_t)rank ||
+        k.world != (uint32_t)world)
+      fail("checkpoint " + path + " was written for another input or GPU count");
+    std::fprintf(stderr, "wordcount: rank %d resumes at byte %llu of [%llu, %llu) (%u interval(s) done)\n", rank,
+                 (unsigned long long)k.next, (unsigned long long)k.begin, (unsigned long long)k.end, k.intervals);
+    return k;
+  }
+  Checkpoint k;
+  k.input_size = input_size;
+  k.begin = k.next = begin;
+  k.end = end;
+  k.rank = (uint32_t)rank;
+  k.world = (uint32_t)world;
+  return k;
+}
+
 void run_checkpointed(const std::string& file, Checkpoint& c, uint64_t interval, const std::string& path,
                       const std::function<KeyTable(const uint8_t*, uint64_t, uint64_t)>& count_interval) {
   WC_CHECK(interval > 0, "checkpoint interval must be positive");

@@ -43,6 +43,12 @@ bool checkpoint_exists(const std::string& path);
 // Per-rank file name: "<base>" for world 1, "<base>.r<rank>of<world>" otherwise.
 std::string checkpoint_path(const std::string& base, int rank, int world);
 
+// Rank `rank` of `world` over [begin, end) of an input of `input_size` bytes:
+// the checkpoint at `path` when `resume` and it exists (validated against the
+// input size, range, rank and world; throws otherwise), else a fresh one.
+Checkpoint open_checkpoint(const std::string& path, bool resume, uint64_t input_size, uint64_t begin, uint64_t end,
+                           int rank, int world);
+
 // Counts [c.begin, c.end) of `file` in delimiter-aligned intervals of about
 // `interval` bytes, starting at c.next (resume) and folding into c.table.
 // `count_interval(host_ptr, len, global_base)` counts one interval and returns

@@ -138,3 +138,32 @@ def test_gpu_bench_json_stages(tmp_path):
     assert d["path"] == "gpu" and d["tokens"] == len(data.split()) and d["chunks"] >= 1
     assert d["stages_ms"]["map_reduce"] > 0 and d["stages_ms"]["finalize"] > 0
     assert b"[wc debug" in r.stderr and b"finalize" in r.stderr
+
+
+def test_python_cpu_checkpointed_api(tmp_path):
+    ops = pytest.importorskip("cuda_mapreduce_amd.ops")
+    data = make_text(tmp_path / "t.txt", n=20000)
+    want = ops.cpu_count(data)
+    ck = str(tmp_path / "py.ck")
+    got = ops.cpu_count_file_checkpointed(str(tmp_path / "t.txt"), ck, interval=3000)
+    assert got.words == want.words and list(got.counts) == list(want.counts) and got.total == want.total
+    assert list(got.first_off) == list(want.first_off)
+    # a finished checkpoint resumes to the same table without reading anything
+    again = ops.cpu_count_file_checkpointed(str(tmp_path / "t.txt"), ck, interval=3000, resume=True)
+    assert again.words == want.words and list(again.counts) == list(want.counts)
+    with pytest.raises(ops.WcError):
+        ops.cpu_count_file_checkpointed(str(tmp_path / "t.txt"), ck, interval=3000, begin=5)
+
+
+@pytest.mark.gpu
+def test_python_gpu_checkpointed_api(tmp_path):
+    ops = pytest.importorskip("cuda_mapreduce_amd.ops")
+    data = make_text(tmp_path / "t.txt", n=50000)
+    want = ops.cpu_count(data)
+    with ops.Engine(device=0) as eng:
+        got = eng.count_file_checkpointed(str(tmp_path / "t.txt"), str(tmp_path / "g.ck"), interval=40000)
+        assert got.words == want.words and list(got.counts) == list(want.counts)
+        assert list(got.first_off) == list(want.first_off) and got.total == want.total
+        # the engine is reusable afterwards
+        eng.count_bytes(data)
+        assert eng.result().words == want.words

@@ -125,26 +125,8 @@ Cli parse(int argc, char** argv) {
   return c;
 }
 
-// Rank `r` of `g`: the saved checkpoint when resuming (validated against the
-// input and the sharding), else a fresh one over the rank's owned range.
 wc::Checkpoint open_checkpoint(const Cli& c, uint64_t input_size, const wc::ShardRange& sr, int r, int g) {
-  const std::string path = wc::checkpoint_path(c.ckpt, r, g);
-  if (c.resume && wc::checkpoint_exists(path)) {
-    wc::Checkpoint k = wc::load_checkpoint(path);
-    if (k.input_size != input_size || k.begin != sr.begin || k.end != sr.end || k.rank != (uint32_t)r ||
-        k.world != (uint32_t)g)
-      wc::fail("checkpoint " + path + " was written for another input or GPU count");
-    std::fprintf(stderr, "wordcount: rank %d resumes at byte %llu of [%llu, %llu) (%u interval(s) done)\n", r,
-                 (unsigned long long)k.next, (unsigned long long)k.begin, (unsigned long long)k.end, k.intervals);
-    return k;
-  }
-  wc::Checkpoint k;
-  k.input_size = input_size;
-  k.begin = k.next = sr.begin;
-  k.end = sr.end;
-  k.rank = (uint32_t)r;
-  k.world = (uint32_t)g;
-  return k;
+  return wc::open_checkpoint(wc::checkpoint_path(c.ckpt, r, g), c.resume, input_size, sr.begin, sr.end, r, g);
 }
 
 void add_stats(wc::Stats& a, const wc::Stats& b) {
