@@ -157,6 +157,34 @@ def host_merge(local: Result) -> Result:
     )
 
 
+def gather_merge(local: Result) -> Result:
+    """Every rank receives every rank's (small) host table and folds them in rank order:
+    counts add, first offset = min, rows in first-occurrence order.  Works on any
+    process-group backend (the object all-gather goes through the device for nccl)."""
+    import torch.distributed as dist
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    tabs = [None] * world
+    _fault_tick(rank)
+    dist.all_gather_object(tabs, (list(local.words), [int(c) for c in local.counts],
+                                  [int(f) for f in local.first_off]))
+    acc = {}
+    for words, counts, firsts in tabs:
+        for w, c, f in zip(words, counts, firsts):
+            if w in acc:
+                acc[w][0] += c
+                acc[w][1] = min(acc[w][1], f)
+            else:
+                acc[w] = [c, f]
+    rows = sorted(acc.items(), key=lambda kv: kv[1][1])
+    return Result(
+        words=[w for w, _ in rows],
+        counts=np.array([v[0] for _, v in rows], dtype=np.uint64),
+        first_off=np.array([v[1] for _, v in rows], dtype=np.uint64),
+        total=sum(v[0] for _, v in rows),
+    )
+
+
 class DistributedWordCount:
     """Count one logical input across all ranks; rank 0 (or all) gets the result."""
 
@@ -176,8 +204,21 @@ class DistributedWordCount:
         b, e = shard_range(data, self.env.rank, self.env.world)
         return self._count(lambda eng: eng.count_bytes(data[b:e], global_base=b), lambda: cpu_count(data[b:e], b))
 
-    def count_file(self, path: str) -> Result:
+    def count_file(self, path: str, checkpoint: str = "", interval: int = 4 << 30, resume: bool = True) -> Result:
+        """Count a file sharded over the ranks.  With `checkpoint`, every rank counts its
+        shard resumably (src/io/checkpoint.cpp; file `<checkpoint>.r<rank>of<world>`) and
+        the per-rank host tables are merged with gather_merge."""
         b, e = shard_range_file(path, self.env.rank, self.env.world)
+        if checkpoint:
+            if self.use_gpu:
+                local = self.engine.count_file_checkpointed(path, checkpoint, interval, resume, b, e,
+                                                            self.env.rank, self.env.world)
+            else:
+                from ..ops.engine import _count_file_checkpointed
+
+                local = _count_file_checkpointed(None, path, checkpoint, interval, resume, b, e,
+                                                 self.env.rank, self.env.world)
+            return local if self.env.world == 1 else gather_merge(local)
 
         def host():
             with open(path, "rb") as fh:

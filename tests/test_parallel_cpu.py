@@ -19,7 +19,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, path, q):
+def _worker(rank, world, port, path, q, ckpt=""):
     sys.path.insert(0, ROOT)
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -29,14 +29,14 @@ def _worker(rank, world, port, path, q):
 
     env = init_from_env("gloo")
     job = DistributedWordCount(env, use_gpu=False)
-    res = job.count_file(path)
+    res = job.count_file(path, checkpoint=ckpt, interval=20000) if ckpt else job.count_file(path)
     q.put((rank, res.words, [int(c) for c in res.counts], [int(f) for f in res.first_off], res.total))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_data_parallel_matches_single(tmp_path, world):
+@pytest.mark.parametrize("world,ckpt", [(2, False), (3, False), (2, True)])
+def test_gloo_data_parallel_matches_single(tmp_path, world, ckpt):
     from cuda_mapreduce_amd.ops import cpu_count, synth_host
 
     text = synth_host(300_000, seed=5, vocab=4000) + b"tail-without-newline"
@@ -45,13 +45,16 @@ def test_gloo_data_parallel_matches_single(tmp_path, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, str(p), q)) for r in range(world)]
+    ck = str(tmp_path / "ck") if ckpt else ""
+    procs = [ctx.Process(target=_worker, args=(r, world, port, str(p), q, ck)) for r in range(world)]
     for pr in procs:
         pr.start()
     outs = [q.get(timeout=120) for _ in range(world)]
     for pr in procs:
         pr.join(timeout=60)
         assert pr.exitcode == 0
+    if ckpt:  # one checkpoint file per rank, each finished at the end of its shard
+        assert sorted(os.listdir(tmp_path)) == sorted(["in.txt"] + [f"ck.r{r}of{world}" for r in range(world)])
     want = cpu_count(text)
     for rank, words, counts, first, total in outs:
         assert total == want.total
