@@ -167,3 +167,13 @@ def test_python_gpu_checkpointed_api(tmp_path):
         # the engine is reusable afterwards
         eng.count_bytes(data)
         assert eng.result().words == want.words
+
+
+@pytest.mark.gpu
+def test_gpu_checkpointed_long_words(tmp_path):
+    # words longer than the interval (and than the map's short-key window) on the GPU path
+    make_text(tmp_path / "t.txt", n=6000, long_every=53)
+    a = run(["t.txt", "--no-echo", "--cpu"], tmp_path)
+    b = run(["t.txt", "--no-echo", "--checkpoint", "c", "--checkpoint-every", "4096"], tmp_path)
+    assert b.returncode == 0, b.stderr
+    assert a.stdout == b.stdout
