@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--chunk-gb", type=float, default=None)
     ap.add_argument("--pool-gb", type=float, default=None, help="host-staged: replay pool per GPU")
+    ap.add_argument("--merge", choices=["shuffle", "dense"], default="shuffle",
+                    help="cross-GPU merge: shuffle (all-to-all to hash owners) or dense (reduce-scatter + all-gather)")
     ap.add_argument("--json-out", default="")
     return ap.parse_args()
 
@@ -72,7 +74,10 @@ def main() -> int:
     host_staged = cfg.source == "host-staged"
 
     torch.cuda.set_device(local)
-    if world > 1:
+    # WC_MERGE_ALWAYS=1 runs the RCCL communicator and the merge protocol even at
+    # world size 1 (launcher / unique-id broadcast / native Comm end to end).
+    use_comm = world > 1 or os.environ.get("WC_MERGE_ALWAYS", "0") not in ("", "0")
+    if use_comm:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
@@ -83,9 +88,10 @@ def main() -> int:
     seg = 1024
     nbytes = per_gpu // seg * seg
     chunk = min(chunk, nbytes) // seg * seg
-    eng = Engine(device=local, chunk_bytes=chunk)
+    merge_mode = {"shuffle": 0, "dense": 1}[a.merge]
+    eng = Engine(device=local, chunk_bytes=chunk, merge_mode=merge_mode)
     comm = None
-    if world > 1:
+    if use_comm:
         uid = [Comm.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         comm = Comm(uid[0], rank, world, local)
@@ -170,6 +176,7 @@ def main() -> int:
                 "parallelism": f"dp{world}",
                 "bytes_per_gpu": nbytes,
                 "chunk_bytes": chunk,
+                "merge": a.merge,
             },
             "stages": st,
         }
@@ -181,7 +188,7 @@ def main() -> int:
     if comm is not None:
         comm.close()
     eng.close()
-    if world > 1:
+    if use_comm:
         dist.destroy_process_group()
     return 0 if valid else 1
 
