@@ -33,7 +33,7 @@ class Options(ctypes.Structure):
         ("min_records", c_uint64),
         ("records_per_byte", c_double),
         ("merge_mode", c_uint32),  # 0 shuffle (all-to-all by key owner), 1 dense reduce-scatter
-        ("reserved", c_uint32),
+        ("k1_hash_bits", c_uint32),  # tests: LONG-word hash bits kept (0 = all) to force collisions
     ]
 
 

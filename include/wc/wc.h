@@ -25,7 +25,7 @@ typedef struct wc_options {
   uint64_t min_records;
   double records_per_byte;
   uint32_t merge_mode; /* 0 shuffle (all-to-all by key owner), 1 dense reduce-scatter */
-  uint32_t reserved;
+  uint32_t k1_hash_bits; /* tests: LONG-word hash bits kept (0 = all) to force collisions */
 } wc_options;
 
 const char* wc_last_error(void);

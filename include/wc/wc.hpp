@@ -54,6 +54,9 @@ struct Options {
   // merge, gather to rank 0); 1 = dense (dictionary union on every rank, reduce-scatter of
   // dense count vectors + all-gather).
   uint32_t merge_mode = 0;
+  // Tests only: keep this many bits of the LONG-word (>= 16 bytes) tail hash
+  // (0 = all 62) to force key collisions; equality stays exact (bytes compared).
+  uint32_t k1_hash_bits = 0;
 };
 
 // Synthetic text spec (see src/kernels/synth.hpp).

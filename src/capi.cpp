@@ -52,6 +52,7 @@ wc::Options to_opts(const wc_options* o) {
   x.min_records = o->min_records;
   x.records_per_byte = o->records_per_byte;
   x.merge_mode = o->merge_mode;
+  x.k1_hash_bits = o->k1_hash_bits;
   return x;
 }
 
@@ -110,7 +111,7 @@ void wc_default_options(wc_options* o) {
   o->min_records = d.min_records;
   o->records_per_byte = d.records_per_byte;
   o->merge_mode = d.merge_mode;
-  o->reserved = 0;
+  o->k1_hash_bits = d.k1_hash_bits;
 }
 
 wc_engine* wc_engine_create(const wc_options* o) {

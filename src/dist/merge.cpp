@@ -64,7 +64,7 @@ void merge_cols_dense(Engine::Impl& im, Comm& comm) {
   // every take_n below, in order (+ 256 B alignment slack per allocation)
   const size_t need = n_max * 28 + a_max + m * 28 + (size_t)W * a_max  // send + gathered columns
                       + m * (16 + 8) + radix_hist_words(m) * 4              // union sort
-                      + m * (8 + 4) + vpad_max * 28                         // flags, ids, merged key columns
+                      + m * (8 + 8) + vpad_max * 28                         // flags, ids, merged key columns
                       + vpad_max * 8 * 4 + 2 * (vpad_max / W) * 8           // dense vectors + slices
                       + 32 * 256 + 64 * 1024;
   A.reserve(need);
@@ -104,9 +104,10 @@ void merge_cols_dense(Engine::Impl& im, Comm& comm) {
   launch_gather_u64(K0, pos, keys, m, s);
   radix_sort_pairs(keys, pos, tkeys, tpos, hist, m, 64, s);
   uint32_t* flag = A.take_n<uint32_t>(m);
+  uint32_t* rep = A.take_n<uint32_t>(m);
   uint32_t* ex = A.take_n<uint32_t>(m);
   uint32_t* d_total = A.take_n<uint32_t>(1);
-  launch_union_flags(pos, K0, K1, flag, m, s);
+  launch_union_flags(pos, K0, K1, SO, SL, AR, n_max, a_max, flag, rep, m, s);
   launch_exclusive_scan_u32(flag, ex, m, d_total, s);
   uint32_t vg = 0;
   WC_HIP_CHECK(hipMemcpyAsync(&vg, d_total, 4, hipMemcpyDeviceToHost, s));
@@ -118,8 +119,8 @@ void merge_cols_dense(Engine::Impl& im, Comm& comm) {
   o.k1 = A.take_n<uint64_t>(vpad);
   o.sref_off = A.take_n<uint64_t>(vpad);
   o.sref_len = A.take_n<uint32_t>(vpad);
-  launch_union_assign(pos, flag, ex, K0, K1, SO, SL, m, n_max, a_max, id_of_pos, o.k0, o.k1, o.sref_off, o.sref_len,
-                      s);
+  launch_union_assign(pos, flag, rep, ex, K0, K1, SO, SL, m, n_max, a_max, id_of_pos, o.k0, o.k1, o.sref_off,
+                      o.sref_len, s);
 
   // 4-6. dense counts: scatter, reduce-scatter, all-gather
   uint64_t* dcnt = A.take_n<uint64_t>(vpad);
@@ -212,7 +213,7 @@ void merge_to_root(Engine::Impl& im, Comm& comm, const std::vector<uint64_t>& ra
     WC_HIP_CHECK(hipMemsetAsync(tcnt, 0, T * 8, s));
     launch_fill_u64(reinterpret_cast<uint64_t*>(tfirst), ~0ull, T, s);
     WC_HIP_CHECK(hipMemsetAsync(d_m, 0, 8, s));
-    launch_mrow_insert(recv_rows, rr, state, tcnt, tfirst, T, s);
+    launch_mrow_insert(recv_rows, rr, recv_bytes, d_base, d_base + W + 1, (uint32_t)W, state, tcnt, tfirst, T, s);
     launch_mrow_compact(recv_rows, state, tcnt, tfirst, T, d_base, d_base + W + 1, (uint32_t)W, merged, d_m, s);
     unsigned long long G = 0;
     WC_HIP_CHECK(hipMemcpyAsync(&G, d_m, 8, hipMemcpyDeviceToHost, s));
@@ -339,7 +340,7 @@ void merge_cols_shuffle(Engine::Impl& im, Comm& comm, bool all_ranks) {
   WC_HIP_CHECK(hipMemsetAsync(tcnt, 0, T * 8, s));
   launch_fill_u64(reinterpret_cast<uint64_t*>(tfirst), ~0ull, T, s);
   WC_HIP_CHECK(hipMemsetAsync(d_m, 0, 8, s));
-  launch_mrow_insert(recv_rows, rr, state, tcnt, tfirst, T, s);
+  launch_mrow_insert(recv_rows, rr, recv_bytes, d_base, d_base + W + 1, (uint32_t)W, state, tcnt, tfirst, T, s);
   launch_mrow_compact(recv_rows, state, tcnt, tfirst, T, d_base, d_base + W + 1, (uint32_t)W, merged, d_m, s);
 
   // 4. gather merged rows + bytes to rank 0 (and broadcast for all_ranks)

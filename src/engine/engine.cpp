@@ -59,9 +59,8 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   WC_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   WC_HIP_CHECK(hipStreamCreateWithFlags(&copy_s, hipStreamNonBlocking));
   map_blocks = opt.map_blocks ? opt.map_blocks : MAP_BLOCKS_PER_CU * (uint32_t)device_cu_count(dev);
-  if (const char* e = std::getenv("WC_ABLATE_MAP")) ablate_map = (uint32_t)std::atoi(e);  // profiling only
   if (const char* e = std::getenv("WC_SYNC_DEBUG")) sync_debug = std::atoi(e) != 0;
-  if (const char* e = std::getenv("WC_MAP_DEC")) map_dec = std::atoi(e) != 0;
+  k1_mask = k1_hash_mask(opt.k1_hash_bits);
   if (const char* e = std::getenv("WC_MAP_STAMPS"); e && std::atoi(e)) {
     WC_HIP_CHECK(hipMalloc(&d_stamps, MAP_STAMP_N * 8));
     WC_HIP_CHECK(hipMemset(d_stamps, 0, MAP_STAMP_N * 8));
@@ -84,6 +83,18 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   rec.cap = rec_total;
   rec.count = rec_mem.take_n<uint32_t>(ncount);
 
+  hot_mem.reserve(HOT_TABLE_CAP * (8 + 4) + HOT_TABLE_CAP * 16 + 2 * MAP_SLOTS * 8 + (HOT_SEL_BINS + 3) * 4 +
+                  MAP_SLOTS + 8192);
+  hot.cap = HOT_TABLE_CAP;
+  hot.fp = hot_mem.take_n<unsigned long long>(HOT_TABLE_CAP);
+  hot.cnt = hot_mem.take_n<uint32_t>(HOT_TABLE_CAP);
+  hot.img_sig = hot_mem.take_n<uint64_t>(MAP_SLOTS);  // cleared region: fp .. gocc (one memset)
+  hot.img_side = hot_mem.take_n<uint64_t>(MAP_SLOTS);
+  hot.sel = hot_mem.take_n<uint32_t>(HOT_SEL_BINS + 3);
+  hot.gocc = hot_mem.take_n<uint32_t>(MAP_SLOTS / 4);
+  hot_clear_bytes = (size_t)(reinterpret_cast<uint8_t*>(hot.gocc + MAP_SLOTS / 4) - reinterpret_cast<uint8_t*>(hot.fp));
+  hot.sig = hot_mem.take_n<uint64_t>(HOT_TABLE_CAP);
+  hot.side = hot_mem.take_n<uint64_t>(HOT_TABLE_CAP);
   WC_HIP_CHECK(hipMalloc(&d_ctr, sizeof(DevCounters)));
   WC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_ctr), sizeof(DevCounters), hipHostMallocDefault));
   const size_t maxb = (size_t)1 << opt.max_log2_tab_buckets;
@@ -117,17 +128,15 @@ Engine::Impl::~Impl() {
   if (d_bucket_en) (void)hipFree(d_bucket_en);
   if (d_arena) (void)hipFree(d_arena);
   if (d_arena_cursor) (void)hipFree(d_arena_cursor);
-  if (d_newkeys) (void)hipFree(d_newkeys);
   if (d_stamps) {
     unsigned long long h[MAP_STAMP_N];
     if (hipMemcpy(h, d_stamps, sizeof h, hipMemcpyDeviceToHost) == hipSuccess && h[MS_TOTAL]) {
-      static const char* names[MS_TOTAL] = {"top-barrier", "commit", "mask",    "list",    "keys",    "combine",
-                                            "retry",       "flush",  "barrier", "fl-hist", "fl-scan", "fl-write"};
+      static const char* names[MS_TOTAL] = {"commit", "mask", "list", "keys", "probe",
+                                            "slow",   "emit", "wait", "flush"};
       fprintf(stderr, "[wc] map phase clock (share of wave lifetime):");
       for (int i = 0; i < MS_TOTAL; ++i) fprintf(stderr, " %s=%.3f", names[i], (double)h[i] / h[MS_TOTAL]);
-      fprintf(stderr, "; slowest-wave token phase / mean = %.3f; tile flushes %llu, retry flushes %llu",
-              h[MS_TOKSUM] ? (double)h[MS_TOKMAX] * MAP_THREADS / 64 / (double)h[MS_TOKSUM] : 0.0, h[MS_NFLUSH],
-              h[MS_NRETRY]);
+      fprintf(stderr, "; refreshes %llu; tokens: first-group hits %llu, deferred %llu, claims %llu, direct records %llu",
+              h[MS_NFLUSH], h[MS_N_HIT], h[MS_N_DEFER], h[MS_N_CLAIM], h[MS_N_DIRECT]);
       fprintf(stderr, "; slowest block / mean block = %.3f\n",
               h[MS_BLKSUM] ? (double)h[MS_BLKMAX] * blocks_stamped / (double)h[MS_BLKSUM] : 0.0);
     }
@@ -147,11 +156,16 @@ void Engine::Impl::ensure_text(uint64_t n) {
   }
 }
 
+// Own allocation: the resident text (synth_device, count_resident) stays valid
+// while streaming sources use the staging pair, in either order.
 void Engine::Impl::ensure_staging(uint64_t chunk) {
-  if (d_stage[0] && pinned.size() >= 2 && pinned[0].size() >= chunk) return;
-  ensure_text(2 * chunk + 256);
-  d_stage[0] = d_text;
-  d_stage[1] = d_text + (chunk + 255) / 256 * 256;
+  if (d_stage[0] && stage_cap >= chunk && pinned.size() >= 2 && pinned[0].size() >= chunk) return;
+  const uint64_t per = (chunk + 4096 + 255) / 256 * 256;  // + read-ahead slack past the chunk
+  stage_mem.reserve(2 * per);
+  stage_mem.reset();
+  d_stage[0] = static_cast<uint8_t*>(stage_mem.take(per));
+  d_stage[1] = static_cast<uint8_t*>(stage_mem.take(per));
+  stage_cap = chunk;
   pinned.clear();
   const uint32_t nring = std::max<uint32_t>(2, opt.staging_buffers);
   for (uint32_t i = 0; i < nring; ++i) pinned.emplace_back(chunk);
@@ -170,10 +184,10 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   pass_rec.cursor = &d_ctr->records;
   pass_rec.subcap = (uint32_t)std::min<uint64_t>(rec.cap / ((uint64_t)blocks << log2_rb), 0xFFFFull);
   WC_CHECK(pass_rec.subcap > 0, "shuffle record capacity below one record per (map block, bucket)");
-  MapArgs m{text, len, avail, prev, log2_rb, pass_rec, d_ctr->flags, &d_ctr->tokens, ablate_map, d_stamps};
+  MapArgs m{text, len, avail, prev, log2_rb, pass_rec, d_ctr->flags, &d_ctr->tokens, k1_mask, d_stamps};
   if (d_stamps) blocks_stamped += blocks;
-  if (map_dec) launch_map_decoupled(m, blocks, s);
-  else launch_map(m, blocks, s);
+  WC_HIP_CHECK(hipMemsetAsync(hot.fp, 0, hot_clear_bytes, s));
+  launch_map(m, hot, blocks, s);
   if (sync_debug) {  // WC_SYNC_DEBUG: attribute a device fault to a kernel and a chunk
     const hipError_t e = hipStreamSynchronize(s);
     fprintf(stderr, "[wc] map    base=%llu len=%llu avail=%llu blocks=%u subcap=%u -> %s\n", (unsigned long long)base,
@@ -182,8 +196,8 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   }
   ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                 avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
-                d_ctr->flags, d_bucket_ovf, nullptr, newkeys()};
-  if (ablate_map == 0 || ablate_map >= 7) launch_reduce(ra, s);  // modes 1-6 leave no valid shuffle
+                d_ctr->flags, d_bucket_ovf, nullptr};
+  launch_reduce(ra, s);
   if (sync_debug) {
     const hipError_t e = hipStreamSynchronize(s);
     fprintf(stderr, "[wc] reduce base=%llu buckets=%u -> %s\n", (unsigned long long)base, 1u << table().log2_buckets,
@@ -191,17 +205,6 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
     WC_HIP_CHECK(e);
   }
   WC_HIP_CHECK(hipMemcpyAsync(h_ctr, d_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));
-}
-
-uint64_t* Engine::Impl::newkeys() {
-  const size_t nb = (size_t)1 << table().log2_buckets;
-  if (nb > newkeys_buckets) {
-    if (d_newkeys) WC_HIP_CHECK(hipFree(d_newkeys));
-    d_newkeys = nullptr;
-    WC_HIP_CHECK(hipMalloc(&d_newkeys, nb * NEWKEY_CAP * sizeof(uint64_t)));
-    newkeys_buckets = nb;
-  }
-  return d_newkeys;
 }
 
 void Engine::Impl::split_table() {
@@ -260,7 +263,7 @@ void Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
     WC_HIP_CHECK(hipMemsetAsync(d_ctr, 0, sizeof(DevCounters), s));
     ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                   avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
-                  d_ctr->flags, d_bucket_ovf, d_bucket_en, newkeys()};
+                  d_ctr->flags, d_bucket_ovf, d_bucket_en};
     launch_reduce(ra, s);
     WC_HIP_CHECK(hipMemcpyAsync(h_ctr, d_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));
     WC_HIP_CHECK(hipStreamSynchronize(s));
@@ -374,10 +377,10 @@ KeyTable Engine::Impl::download_cols() {
   t.counts = std::move(cnt);
   t.first_off = std::move(first);
   for (uint64_t i = 0; i < n; ++i) {
-    if (key_is_short(k1[i])) {
-      const uint64_t len = k1[i];
-      t.words[i].resize(len);
-      for (uint64_t b = 0; b < len; ++b) t.words[i][b] = (char)((k0[i] >> (8 * b)) & 0xFF);
+    if (!key_is_hashed(k1[i])) {
+      uint8_t w[KEY_INLINE_MAX];
+      const uint32_t len = inline_bytes(k0[i], k1[i], w);
+      t.words[i].assign(reinterpret_cast<const char*>(w), len);
     } else {
       WC_CHECK(soff[i] + slen[i] <= arena.size(), "arena reference out of range");
       t.words[i].assign(reinterpret_cast<const char*>(arena.data()) + soff[i], slen[i]);

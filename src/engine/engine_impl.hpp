@@ -44,9 +44,8 @@ struct Engine::Impl {
   int dev = 0;
   hipStream_t s = nullptr, copy_s = nullptr;
   uint32_t map_blocks = 0;
-  uint32_t ablate_map = 0;  // WC_ABLATE_MAP (profiling ablations, MapArgs::ablate)
   bool sync_debug = false;  // WC_SYNC_DEBUG: sync + log after every kernel
-  bool map_dec = true;      // WC_MAP_DEC=0: block-synchronous tile kernel (map.hip) instead of map_dec.hip
+  uint64_t k1_mask = K1_HASH_MASK;  // Options::k1_hash_bits (collision tests)
   unsigned long long* d_stamps = nullptr;  // WC_MAP_STAMPS: map phase clock sums
   uint64_t blocks_stamped = 0;             // map blocks launched with stamps (block-duration mean)
 
@@ -64,18 +63,21 @@ struct Engine::Impl {
   int cur = 0;
   uint32_t* d_bucket_ovf = nullptr;
   uint8_t* d_bucket_en = nullptr;
-  uint64_t* d_newkeys = nullptr;  // [buckets * NEWKEY_CAP], grows with the table
-  size_t newkeys_buckets = 0;
-  uint64_t* newkeys();            // sized for the current table
+  // hot-key sampling workspace of the map (HotArgs)
+  DeviceArena hot_mem;
+  HotArgs hot{};
+  size_t hot_clear_bytes = 0;  // fp, cnt, image, selection state: zeroed before every map pass
 
-  // key arena (bytes of >8-byte words)
+  // key arena (bytes of LONG words, >= 16 bytes)
   uint8_t* d_arena = nullptr;
   unsigned long long* d_arena_cursor = nullptr;
 
-  // resident / staging text
+  // resident text (synth_device) and, separately, the streaming staging pair
   DeviceArena text_mem;
   uint8_t* d_text = nullptr;
   uint64_t text_cap = 0;
+  DeviceArena stage_mem;
+  uint64_t stage_cap = 0;
   uint8_t* d_stage[2] = {nullptr, nullptr};
   std::vector<PinnedBuffer> pinned;
   const uint8_t* registered = nullptr;  // caller pool page-locked by count_pinned_replay

@@ -1,7 +1,7 @@
 // kernels.hpp — host-side launch interface of every hand-written CDNA4 kernel.
 //
 // Pipeline per chunk (SURVEY §2.2 replacement column):
-//   wc_map_tokenize   text -> token keys -> LDS pre-aggregation -> bucketed records
+//   wc_map            text -> token keys -> LDS pre-aggregation -> bucketed records
 //   wc_reduce_buckets records -> per-bucket LDS hash table -> running key table
 //   wc_table_split    running table B -> 2B buckets (grows with the vocabulary)
 //   wc_table_compact  running table -> dense key list
@@ -24,15 +24,8 @@ namespace wc {
 constexpr int MAP_THREADS = WC_MAP_THREADS;          // 16 waves, one block per CU
 constexpr int MAP_BLOCKS_PER_CU = WC_MAP_BLOCKS_PER_CU;
 constexpr int MAP_BPL = 32;                          // text bytes per lane
-constexpr int MAP_TILE = MAP_THREADS * MAP_BPL;      // 32 KiB LDS text tile
-constexpr int MAP_HALO = 256;                        // bytes past the tile kept in LDS
-constexpr int MAP_SLOTS = WC_MAP_SLOTS;              // LDS combiner slots (groups of 8)
-constexpr int MAP_GROUPS = MAP_SLOTS / 4;
-#ifndef WC_MAP_FILL_EIGHTHS
-#define WC_MAP_FILL_EIGHTHS 6
-#endif
-constexpr int MAP_FILL_MAX = MAP_SLOTS * WC_MAP_FILL_EIGHTHS / 8;  // adaptive flush: target max fill (sticky included)
-constexpr int MAP_MAX_GROUP_PROBES = 8;              // then flush and retry the token
+constexpr int MAP_TILE = MAP_THREADS * MAP_BPL;      // 32 KiB: chunk-length granule of the engine
+constexpr int MAP_SLOTS = WC_MAP_SLOTS;              // LDS combiner slots (groups of 4)
 constexpr int MAX_REC_BUCKETS_LOG2 = 9;              // shuffle partitions <= 512
 constexpr int MAX_REC_BUCKETS = 1 << MAX_REC_BUCKETS_LOG2;
 
@@ -102,11 +95,32 @@ struct MapArgs {
   Records rec;
   uint32_t* flags;
   unsigned long long* tokens;   // += tokens owned by this chunk
-  uint32_t ablate;             // profiling: 0 full map; 1 keys only (no combiner); 2 scan only
-  unsigned long long* stamps;  // profiling: per-phase s_memtime sums (MAP_STAMP_N), nullptr = off
+  uint64_t k1_mask;            // LONG-key hash bits kept (K1_HASH_MASK; collision tests truncate)
+  unsigned long long* stamps;  // diagnostic build: per-phase s_memtime sums (MAP_STAMP_N), nullptr = off
 };
-// In-kernel phase stamps of the map (diagnostic build path, WC_MAP_STAMPS=1).
-enum : int { MS_TOP = 0, MS_COMMIT, MS_MASK, MS_LIST, MS_KEYS, MS_COMBINE, MS_RETRY, MS_FLUSH, MS_BARRIER, MS_FL_HIST, MS_FL_SCAN, MS_FL_WRITE, MS_TOTAL, MS_TOKSUM, MS_TOKMAX, MS_TOKMAX_TILE, MS_NFLUSH, MS_NRETRY, MS_BLKSUM, MS_BLKMAX, MAP_STAMP_N };
+// Hot-key sampling workspace (map.hip): a global fingerprint table filled by
+// wc_hot_sample (fp/cnt zeroed before each chunk) and the LDS table image
+// written by wc_hot_select.
+struct HotArgs {
+  unsigned long long* fp;  // [cap] 0 = empty
+  uint32_t* cnt;           // [cap]
+  uint64_t* sig;           // [cap] signature of the first block's sample of the word
+  uint64_t* side;          // [cap]
+  uint64_t cap;            // power of two
+  uint64_t* img_sig;       // [MAP_SLOTS] zeroed before each chunk
+  uint64_t* img_side;      // [MAP_SLOTS]
+  uint32_t* sel;           // [HOT_SEL_BINS + 3] zeroed: count histogram, threshold, tie quota / counter
+  uint32_t* gocc;          // [MAP_SLOTS / 4] zeroed: fill of each image group
+};
+constexpr uint64_t HOT_TABLE_CAP = 1ull << 18;
+constexpr int HOT_SEL_BINS = 4096;
+constexpr int HOT_SEL_BLOCKS = 32;
+
+// In-kernel phase stamps of the map (diagnostic build, WC_MAP_STAMPS=1): shares
+// of wave lifetime per phase, then counters.
+enum : int { MS_COMMIT = 0, MS_MASK, MS_LIST, MS_KEYS, MS_PROBE, MS_SLOW, MS_EMIT, MS_WAIT, MS_FLUSH, MS_TOTAL,
+             MS_NFLUSH, MS_N_HIT, MS_N_DEFER, MS_N_CLAIM, MS_N_DIRECT,
+             MS_BLKSUM, MS_BLKMAX, MAP_STAMP_N };
 
 struct ReduceArgs {
   Records rec;
@@ -120,10 +134,7 @@ struct ReduceArgs {
   uint32_t* flags;
   uint32_t* bucket_overflow;      // [n_buckets] set when a slice overflowed
   const uint8_t* bucket_enable;   // nullptr = all
-  uint64_t* newkeys;              // [n_buckets * NEWKEY_CAP] (slot << 32 | offset) of new long words
 };
-constexpr int NEWKEY_CAP = 4096;  // per bucket and pass (= TAB_SLOTS: never exceeded); else copied inline
-constexpr int NEWKEY_PER_THREAD = 4;
 
 struct SynthVocab {
   const uint8_t* bytes;
@@ -134,8 +145,8 @@ struct SynthVocab {
 };
 
 // ---- launchers (all stream-ordered, no host sync) ----------------------------
-void launch_map(const MapArgs& a, uint32_t map_blocks, hipStream_t s);
-void launch_map_decoupled(const MapArgs& a, uint32_t map_blocks, hipStream_t s);  // map_dec.hip
+// wc_hot_sample + wc_hot_hist/_threshold/_place + wc_map (HotArgs zeroed first: hot_clear).
+void launch_map(const MapArgs& a, const HotArgs& h, uint32_t map_blocks, hipStream_t s);
 void launch_reduce(const ReduceArgs& a, hipStream_t s);
 void launch_table_split(const TableView& src, const TableView& dst, hipStream_t s);
 void launch_table_clear(const TableView& t, hipStream_t s);
@@ -162,18 +173,18 @@ void launch_synth(uint8_t* out, uint64_t n, uint64_t first_segment, uint64_t see
                   hipStream_t s);
 
 // Merge-protocol helpers (dist/merge.cpp).
-void launch_place_hash(const uint64_t* k0, const uint64_t* k1, uint64_t* ph, uint64_t n, hipStream_t s);
 // Dense scatter: dst_cnt[id[i]] += cnt[i] (ids unique per rank, so plain stores), dst_first min.
 void launch_scatter_dense(const uint32_t* ids, const uint64_t* cnt, const uint64_t* first, uint64_t* dense_cnt,
                           uint64_t* dense_first, uint64_t n, hipStream_t s);
 void launch_fill_u64(uint64_t* p, uint64_t v, uint64_t n, hipStream_t s);
 // merge.hip
-void launch_union_flags(const uint32_t* pos, const uint64_t* K0, const uint64_t* K1, uint32_t* flag, uint64_t m,
-                        hipStream_t s);
-void launch_union_assign(const uint32_t* pos, const uint32_t* flag, const uint32_t* ex, const uint64_t* K0,
-                         const uint64_t* K1, const uint64_t* SO, const uint32_t* SL, uint64_t m, uint64_t n_max,
-                         uint64_t arena_stride, uint32_t* id_of_pos, uint64_t* ok0, uint64_t* ok1, uint64_t* osoff,
-                         uint32_t* oslen, hipStream_t s);
+void launch_union_flags(const uint32_t* pos, const uint64_t* K0, const uint64_t* K1, const uint64_t* SO,
+                        const uint32_t* SL, const uint8_t* AR, uint64_t n_max, uint64_t arena_stride, uint32_t* flag,
+                        uint32_t* rep, uint64_t m, hipStream_t s);
+void launch_union_assign(const uint32_t* pos, const uint32_t* flag, const uint32_t* rep, const uint32_t* ex,
+                         const uint64_t* K0, const uint64_t* K1, const uint64_t* SO, const uint32_t* SL, uint64_t m,
+                         uint64_t n_max, uint64_t arena_stride, uint32_t* id_of_pos, uint64_t* ok0, uint64_t* ok1,
+                         uint64_t* osoff, uint32_t* oslen, hipStream_t s);
 // ---- shuffle merge (src/kernels/merge.hip) ----
 struct MRow {  // one key row on the wire (40 B)
   uint64_t k0, k1, cnt, first;
@@ -188,7 +199,8 @@ void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t
                           const uint64_t* soff, const uint32_t* slen, const uint8_t* arena, uint64_t n, uint32_t W,
                           const unsigned long long* counts, unsigned long long* cursor, MRow* rows, uint8_t* bytes,
                           hipStream_t s);
-void launch_mrow_insert(const MRow* rows, uint64_t R, uint32_t* state, unsigned long long* cnt,
+void launch_mrow_insert(const MRow* rows, uint64_t R, const uint8_t* bytes, const uint64_t* rbase,
+                        const uint64_t* bbase, uint32_t W, uint32_t* state, unsigned long long* cnt,
                         unsigned long long* first, uint64_t T, hipStream_t s);
 void launch_mrow_compact(const MRow* rows, const uint32_t* state, const unsigned long long* cnt,
                          const unsigned long long* first, uint64_t T, const uint64_t* rbase, const uint64_t* bbase,

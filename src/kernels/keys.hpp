@@ -3,17 +3,21 @@
 //
 // Reference parity: the reference identifies a word by a byte-at-a-time *prefix*
 // test (`compare`, /root/reference/main.cu:57-67) over NUL-terminated 30-byte
-// buffers (main.cu:16-22).  Here a word is identified EXACTLY by a packed
-// 128-bit key so every equality test is two 64-bit integer compares:
+// buffers (main.cu:16-22).  Here a word is identified by a packed 128-bit key,
+// so every equality test is two 64-bit integer compares:
 //
 //   k0 = the first min(len, 8) bytes, little-endian packed, zero-padded
-//   k1 = len                                   when len <= 8  (exact, no hash)
-//        TAG | fnv1a64(word) & HASH_MASK       when len >  8
+//   k1 = len                                   len <= 8   SHORT  (exact)
+//        bytes [8, len) packed | len << 56     9..15      MEDIUM (exact)
+//        TAG | hash62(bytes [8, len), len)     len >= 16  LONG   (hashed)
 //
-// Words of <= 8 bytes (the vast majority of natural text) are therefore keyed
-// with no hashing at all; longer words collide only if they share their first
-// 8 bytes AND a 62-bit FNV-1a tail hash.  k1 is never 0 (0 marks an empty
-// slot) and never ~0 (PENDING marks a slot being claimed).
+// Words of <= 15 bytes — all but a vanishing fraction of natural text — are
+// keyed exactly with no hashing at all.  LONG keys can collide (same first 8
+// bytes, same 62-bit tail hash), so they never meet by key alone: every LONG
+// token reaches the key table as its own record and is merged only after a
+// byte comparison with the table's stored copy of the word (reduce.hip
+// wc_long_merge, merge.hip wc_mrow_insert); two colliding words keep two slots.
+// k1 is never 0 (empty slot) and never ~0 (PENDING: bit 62 of a LONG k1 is 0).
 //
 // Delimiters are exactly the reference's set {' ', '\r', '\n'} (main.cu:188);
 // TAB and every other byte, NUL included, are word bytes.
@@ -57,53 +61,69 @@ WC_HD uint64_t fmix64(uint64_t k) {
   return k;
 }
 
-// Long-word tail hash: word-wise FNV-1a-64 over the 8-byte little-endian
+// LONG-word tail hash: word-wise FNV-1a-64 over the 8-byte little-endian
 // chunks that follow k0 (last chunk zero-padded), folded with the length and
 // finalised with fmix64.  Chunk-at-a-time so the map kernel hashes straight
-// from registers (one fold per 8 bytes instead of one per byte).
+// from registers (one fold per 8 bytes instead of one per byte).  `mask` keeps
+// all 62 bits in production; the collision tests truncate it (Options::k1_hash_bits).
+constexpr uint32_t KEY_INLINE_MAX = 15;  // longest word keyed exactly (SHORT / MEDIUM)
 WC_HD uint64_t tail_fold(uint64_t h, uint64_t chunk) { return (h ^ chunk) * FNV_PRIME; }
-WC_HD uint64_t make_k1(uint64_t len, uint64_t h) {
-  return len <= 8 ? len : (K1_TAG | (fmix64(h ^ len) & K1_HASH_MASK));
+WC_HD uint64_t long_k1(uint64_t len, uint64_t h, uint64_t mask = K1_HASH_MASK) {
+  return K1_TAG | (fmix64(h ^ len) & mask);
 }
+WC_HD uint64_t medium_k1(uint64_t tail, uint64_t len) { return tail | (len << 56); }  // tail = bytes [8, len)
+WC_HD uint64_t k1_hash_mask(uint32_t bits) { return bits >= 62 || bits == 0 ? K1_HASH_MASK : ((1ull << bits) - 1); }
 
-// Placement hash of the packed key: (k0 ^ rotl(k1, 56)) through a two-multiply
-// xor-shift mixer (splitmix64-style finaliser).  Two full 64-bit multiplies —
-// the map computes it once per token, so it is kept cheaper than a byte-wise
-// FNV.  Bits [2, 2+log2 B) select the shuffle / table bucket (they live inside
-// the 32-bit LDS tag, so a flush recovers the bucket without rehashing), bits
-// [32, ..) the slot group inside a table, the top bits the merge owner rank.
-WC_HD uint64_t place_hash(uint64_t k0, uint64_t k1) {
-  uint64_t h = (k0 ^ ((k1 << 56) | (k1 >> 8))) * 0x9E3779B97F4A7C15ull;
-  h ^= h >> 29;
-  h *= 0xBF58476D1CE4E5B9ull;
-  return h ^ (h >> 32);
+// Placement hash of the packed key (32 bits, four 32-bit multiplies — the map
+// computes it once per token): the middle words are pre-mixed by odd-constant
+// multiplies, then lowbias32.  Bits [0, log2 B) select the shuffle / table
+// bucket, bits [20, 29) the map combiner group, the high bits the merge owner;
+// the reduce slice group is taken from a multiplied copy so it stays spread
+// when the bucket bits are many.
+WC_HD uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  return x ^ (x >> 16);
+}
+WC_HD uint32_t place_hash(uint64_t k0, uint64_t k1) {
+  const uint32_t a = (uint32_t)k0, b = (uint32_t)(k0 >> 32), c = (uint32_t)k1 ^ (uint32_t)(k1 >> 32);
+  return mix32(a ^ (b * 0x9E3779B1u) ^ (c * 0x85EBCA77u));
 }
 
 // Nested: the bucket under 2B buckets is b or b + B for bucket b under B.
-WC_HD uint32_t bucket_of(uint64_t ph, uint32_t log2_buckets) {
-  return (uint32_t)(ph >> 2) & ((1u << log2_buckets) - 1u);
-}
+WC_HD uint32_t bucket_of(uint32_t ph, uint32_t log2_buckets) { return ph & ((1u << log2_buckets) - 1u); }
 
 // Host helper: key of an explicit byte string.
-WC_HD void key_of(const uint8_t* w, uint64_t len, uint64_t* k0, uint64_t* k1) {
-  uint64_t a = 0, h = FNV_OFFSET, chunk = 0;
+WC_HD void key_of(const uint8_t* w, uint64_t len, uint64_t* k0, uint64_t* k1, uint64_t mask = K1_HASH_MASK) {
+  uint64_t a = 0, h = FNV_OFFSET, chunk = 0, first_tail = 0;
   for (uint64_t i = 0; i < len; ++i) {
     if (i < 8) {
       a |= (uint64_t)w[i] << (8 * i);
     } else {
       chunk |= (uint64_t)w[i] << (8 * (i & 7));
       if ((i & 7) == 7) {
+        if (i == 15) first_tail = chunk;
         h = tail_fold(h, chunk);
         chunk = 0;
       }
     }
   }
+  if (len > 8 && len <= KEY_INLINE_MAX) first_tail = chunk;
   if (len > 8 && (len & 7)) h = tail_fold(h, chunk);
   *k0 = a;
-  *k1 = make_k1(len, h);
+  *k1 = len <= 8 ? len : (len <= KEY_INLINE_MAX ? medium_k1(first_tail, len) : long_k1(len, h, mask));
 }
 
-// Short words (len <= 8) are recoverable from the key alone.
 WC_HD bool key_is_short(uint64_t k1) { return k1 <= 8; }
+WC_HD bool key_is_hashed(uint64_t k1) { return (k1 >> 63) != 0; }  // LONG: bytes live in the key arena
+WC_HD uint32_t inline_len(uint64_t k1) { return k1 <= 8 ? (uint32_t)k1 : (uint32_t)(k1 >> 56); }
+// Bytes of an inline (SHORT / MEDIUM) key: out must hold 15 bytes; returns the length.
+WC_HD uint32_t inline_bytes(uint64_t k0, uint64_t k1, uint8_t* out) {
+  const uint32_t len = inline_len(k1);
+  for (uint32_t i = 0; i < len; ++i) out[i] = (uint8_t)((i < 8 ? k0 >> (8 * i) : k1 >> (8 * (i - 8))) & 0xFF);
+  return len;
+}
 
 }  // namespace wc

@@ -1,6 +1,6 @@
 // lds_table.hpp — group-probed hash table in LDS keyed by the packed 128-bit
-// word key (keys.hpp).  Used by the map kernel (per-block combiner) and the
-// reduce kernel (per-bucket slice of the running table).
+// word key (keys.hpp): the per-bucket slice of the running key table held by
+// the reduce and table-split kernels (reduce.hip).
 //
 // Layout: slots come in groups of 4 stored together (SlotGroup, 80 B): four
 // 32-bit tags derived from the placement hash, then the four k1 and four k0.
@@ -12,10 +12,10 @@
 //
 // Claim protocol (no spin inside a branch, so lanes of one wave can never
 // dead-lock on each other): tag 0 -> PENDING by LDS CAS, the claimer writes
-// k0/k1, waits for them, then publishes the real tag (never 0 or PENDING).
-// The tag is the publish flag: a reader only trusts k0/k1 of a slot whose tag
-// it saw published, and it reads the tags before the keys (LDS executes one
-// wave's reads in order).  A prober that sees PENDING in a group re-reads the
+// k0/k1, then publishes the real tag (never 0 or PENDING).  The tag is the
+// publish flag: a reader only trusts k0/k1 of a slot whose tag it saw
+// published, and it reads the tags before the keys (LDS executes one wave's
+// accesses in order).  A prober that sees PENDING in a group re-reads the
 // group on its next loop iteration; the claimer always finishes its publish
 // inside the iteration that won the CAS.
 #pragma once
@@ -36,16 +36,21 @@ struct alignas(16) SlotGroup {
 };
 static_assert(sizeof(SlotGroup) == 80, "SlotGroup layout");
 
-__device__ __forceinline__ uint32_t make_tag(uint64_t ph) { return ((uint32_t)ph & ~1u) | 2u; }
-__device__ __forceinline__ uint32_t group_of(uint64_t ph, uint32_t ngroups) {
-  return (uint32_t)(ph >> 32) & (ngroups - 1);
+// The bucket bits of the placement hash are the low bits (constant inside a
+// slice), so tags and groups are taken from a multiplied copy: its high bits
+// depend on every bit of the hash.
+__device__ __forceinline__ uint32_t slice_hash(uint32_t ph) { return ph * 0x9E3779B1u; }
+__device__ __forceinline__ uint32_t make_tag(uint32_t ph) { return (slice_hash(ph) & ~1u) | 2u; }
+__device__ __forceinline__ uint32_t group_of(uint32_t ph, uint32_t ngroups) {
+  return (uint32_t)(((uint64_t)slice_hash(ph) * ngroups) >> 32);
 }
 
 // Returns the slot (4 * group + lane-in-group) holding (k0,k1) — claiming the
 // first empty slot of the first non-full group if the key is new
-// (claimed = true) — or -1 after `max_groups` full groups.
-__device__ __forceinline__ int lds_find_or_claim(SlotGroup* groups, uint32_t ngroups, uint64_t ph, uint64_t k0,
-                                                 uint64_t k1, int max_groups, bool& claimed) {
+// (claimed = true) — or -1 after `max_groups` full groups.  find = false skips
+// the lookup (the caller knows the key is not in the slice: table split).
+__device__ __forceinline__ int lds_find_or_claim(SlotGroup* groups, uint32_t ngroups, uint32_t ph, uint64_t k0,
+                                                 uint64_t k1, int max_groups, bool& claimed, bool find = true) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
   const uint32_t tag = make_tag(ph);
@@ -61,10 +66,10 @@ __device__ __forceinline__ int lds_find_or_claim(SlotGroup* groups, uint32_t ngr
     const u64x2 b1 = *reinterpret_cast<const u64x2*>(&G.k1[2]);
     const u64x2 a0 = *reinterpret_cast<const u64x2*>(&G.k0[0]);
     const u64x2 b0 = *reinterpret_cast<const u64x2*>(&G.k0[2]);
-    const bool h0 = t.x == tag && a1.x == k1 && a0.x == k0;
-    const bool h1 = t.y == tag && a1.y == k1 && a0.y == k0;
-    const bool h2 = t.z == tag && b1.x == k1 && b0.x == k0;
-    const bool h3 = t.w == tag && b1.y == k1 && b0.y == k0;
+    const bool h0 = find && t.x == tag && a1.x == k1 && a0.x == k0;
+    const bool h1 = find && t.y == tag && a1.y == k1 && a0.y == k0;
+    const bool h2 = find && t.z == tag && b1.x == k1 && b0.x == k0;
+    const bool h3 = find && t.w == tag && b1.y == k1 && b0.y == k0;
     if (h0 | h1 | h2 | h3) return 4 * (int)g + (h0 ? 0 : (h1 ? 1 : (h2 ? 2 : 3)));
     if (t.x == TAG_PENDING || t.y == TAG_PENDING || t.z == TAG_PENDING || t.w == TAG_PENDING)
       continue;  // someone is publishing in this group: look again
@@ -85,19 +90,32 @@ __device__ __forceinline__ int lds_find_or_claim(SlotGroup* groups, uint32_t ngr
   }
 }
 
+// Next slot after `from` (-1: start of the probe sequence) whose key is
+// (k0, k1), or -1 at the first group with an empty slot.  LONG keys may sit in
+// several slots (colliding words, keys.hpp): the caller verifies bytes.
+// Read-only: the slice must not change concurrently.
+__device__ __forceinline__ int lds_find_next(const SlotGroup* groups, uint32_t ngroups, uint32_t ph, uint64_t k0,
+                                             uint64_t k1, int from) {
+  const uint32_t tag = make_tag(ph);
+  uint32_t g = from < 0 ? group_of(ph, ngroups) : (uint32_t)from / 4;
+  int i = from < 0 ? 0 : (from & 3) + 1;
+  for (uint32_t n = 0; n < ngroups; ++n) {
+    const SlotGroup& G = groups[g];
+    bool empty = false;
+    for (; i < 4; ++i) {
+      if (G.tag[i] == TAG_EMPTY) empty = true;
+      else if (G.tag[i] == tag && G.k1[i] == k1 && G.k0[i] == k0) return 4 * (int)g + i;
+    }
+    if (empty) return -1;
+    i = 0;
+    g = (g + 1) & (ngroups - 1);
+  }
+  return -1;
+}
+
 __device__ __forceinline__ uint32_t slot_tag(const SlotGroup* groups, int s) { return groups[s >> 2].tag[s & 3]; }
 __device__ __forceinline__ uint64_t slot_k0(const SlotGroup* groups, int s) { return groups[s >> 2].k0[s & 3]; }
 __device__ __forceinline__ uint64_t slot_k1(const SlotGroup* groups, int s) { return groups[s >> 2].k1[s & 3]; }
-
-__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
-
-// Exclusive prefix count of set predicate among lower lanes + wave total.
-__device__ __forceinline__ uint32_t wave_rank(bool pred, uint32_t& total) {
-  const uint64_t b = __ballot(pred);
-  total = (uint32_t)__popcll(b);
-  const uint64_t lt = (lane_id() == 0) ? 0ull : (~0ull >> (64 - lane_id()));
-  return (uint32_t)__popcll(b & lt);
-}
 
 }  // namespace dev
 }  // namespace wc

@@ -1,288 +1,600 @@
-// map.hip — wc_map_tokenize: the MAP stage (+ combiner + shuffle write).
+// map.hip — the MAP stage: hot-key sampling, hot-table build, and wc_map
+// (tokenize -> key -> LDS hot table | shuffle record).
 //
-// Reference: mapKernel (/root/reference/main.cu:109-117) runs one thread per
-// pre-split input record and only copies words the HOST tokenizer
-// (main.cu:181-206) already found.  Here the GPU does the whole map:
+// Reference: mapKernel / mapper (/root/reference/main.cu:37-54, 109-117) copy
+// one pre-split line's words per thread with <= 9 threads active; the host
+// tokenizes (main.cu:181-206).  Here the GPU tokenizes and pre-aggregates in
+// three launches per chunk:
 //
-//  1. A persistent grid of 2 blocks/CU walks 16 KiB text tiles.  The next
-//     tile (+256 B halo) is prefetched into registers while the current one is
-//     tokenized, then committed to LDS.
-//  2. Each lane owns 32 bytes and builds a 64-bit delimiter mask over its
-//     bytes and its neighbour's (SWAR zero-byte test against {0x20,0x0D,0x0A}).
-//     Token starts are  ~d & (d << 1 | carry-in)  restricted to the owned 32
-//     bytes, so a token straddling lanes / tiles / chunks / GPU shards is owned
-//     by the unit holding its FIRST byte.
-//  3. Load balance: a wave scan of the per-lane token counts compacts the
-//     wave's tokens into an LDS list of (position, length) entries, and the 64
-//     lanes then take list entries two at a time — every lane keys and combines
-//     the same number of tokens, instead of each lane walking its own (uneven)
-//     tokens while the rest of the wave idles.
-//  4. Keys (keys.hpp) come from two aligned ds_read_b64 per 8 bytes; words
-//     longer than the lane window fall back to a byte loop (LDS halo, then
-//     global memory).
-//  5. Combiner: 2048-slot LDS hash table, 8-slot groups.  A probe reads the
-//     group's eight 32-bit tags (two ds_read_b128) and then only the matching
-//     slot's 16-byte key.  Claims are ONE CAS on the tag (duplicates are
-//     allowed: the reducer merges them), count / first-offset updates are
-//     no-return LDS atomics, occupancy is counted once per wave.
-//  6. A token whose probe sequence is full is marked in a per-tile failure
-//     bitmap; the block flushes and the owning lanes retry those tokens.
-//  7. Flush = shuffle write: occupied slots are counting-sorted by shuffle
-//     bucket (LDS histogram + block scan) and written as ONE contiguous chunk
-//     (coalesced) plus a bucket-offset directory entry; the reducer of bucket
-//     b reads its run of every chunk.
+//  wc_hot_sample  every map block tokenizes HOT_SAMPLE units spread over its
+//                 range, counts their words in an LDS table and adds the counts
+//                 to a global fingerprint table (one global atomic per distinct
+//                 word per block);
+//  wc_hot_hist / _threshold / _place  keep the HOT_K most frequent sampled
+//                 words and place them in a 2-choice, 4-slot-group table image
+//                 (4096 slots of 64-bit signatures + side words);
+//  wc_map         persistent, ONE 1024-thread block (16 waves) per CU over a
+//                 contiguous range of 2 KiB text units.  The block loads the
+//                 image into LDS; each wave grabs its next unit from an LDS
+//                 cursor and prefetches it into registers (32 B per lane) while
+//                 tokenizing the current one from its private LDS copy:
+//                 SWAR delimiter masks -> token starts `~d & (d << 1 | c)` ->
+//                 ballot-bit prefix sum -> a list of (position, length)
+//                 entries -> per step two tokens per lane: exact inline key
+//                 from two 8-byte windows (keys.hpp), 32-bit placement hash,
+//                 both candidate groups read in ONE LDS round trip; a hit is
+//                 two no-return LDS atomics (count, min first offset), a miss
+//                 is a shuffle record (key, 1, offset) appended to the
+//                 (block, bucket) sub-region of its reduce bucket.  The table
+//                 is READ-ONLY while tokens stream: no claims, no refresh
+//                 barriers, no divergent slow path.  A token belongs to the
+//                 unit holding its first byte (lanes, units, chunks and GPU
+//                 shards all use this rule).  The block ends by emitting every
+//                 counted hot slot as one record.
+//
+// Signatures: a word of <= 7 bytes is its own 64-bit signature (bytes | len
+// << 56, one compare); 8..15-byte words use len << 56 | low 7 bytes of
+// (k0 ^ tail) plus k0 in `side`.  LONG words (>= 16 bytes, hashed keys) never
+// enter the table: each token is a record, so the reducer compares its bytes.
 #include "map_common.hpp"
 
 namespace wc {
 namespace dev {
 
-struct MapLds {
-  u64x2 key[MAP_SLOTS];    // {k0, k1}; k1 = K1_EMPTY after a flush, so a stale key never matches
-  uint32_t tag[MAP_SLOTS];  // group g = tag[8g, 8g+8); 0 = empty
+constexpr int UNIT = 64 * MAP_BPL;     // text bytes per wave unit (2 KiB)
+constexpr int HALO = 64;               // bytes past the unit kept in LDS
+constexpr int BUF = UNIT + HALO + 16;  // + one 16-byte key read past the halo
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr int GS = 4;                  // slots per group
+constexpr int NG = MAP_SLOTS / GS;     // groups
+constexpr int SPT = MAP_SLOTS / MAP_THREADS;
+#ifndef WC_HOT_K
+#define WC_HOT_K (MAP_SLOTS * 3 / 4)
+#endif
+#ifndef WC_HOT_SAMPLE
+#define WC_HOT_SAMPLE 8
+#endif
+constexpr uint32_t HOT_K = WC_HOT_K;            // words placed in the hot table
+constexpr uint32_t HOT_SAMPLE = WC_HOT_SAMPLE;  // units sampled per map block
+constexpr int SAMPLE_PROBES = 8;
+static_assert(MAP_SLOTS % MAP_THREADS == 0 && (NG & (NG - 1)) == 0, "table geometry");
+static_assert(UNIT <= 2048, "list entries hold 11-bit unit-relative positions");
+
+// Profiling builds only (tools/variants.sh -DWC_MAP_ABLATE=N; results are NOT
+// valid): 1 tokenize + list only, 2 + keys and hashes, 3 + table probes and
+// hit counts (misses dropped).
+#ifndef WC_MAP_ABLATE
+#define WC_MAP_ABLATE 0
+#endif
+
+constexpr uint64_t LOW7 = 0x00FFFFFFFFFFFFFFull;
+__device__ __forceinline__ bool two_word(uint64_t sig) { return (sig >> 56) >= 8; }
+
+__device__ __forceinline__ void sig_key(uint64_t sig, uint64_t side, uint64_t& k0, uint64_t& k1) {
+  const uint64_t top = sig >> 56;
+  if (top < 8) {
+    k0 = sig & LOW7;
+    k1 = top;
+  } else {
+    k0 = side;
+    k1 = top == 8 ? 8ull : (((sig ^ side) & LOW7) | (top << 56));
+  }
+}
+
+// Inline key of a token of known length 1..15 from its windows w0 = bytes
+// [p, p+8) and w1 = [p+8, p+16), and its table signature.
+__device__ __forceinline__ void inline_key(uint64_t w0, uint64_t w1, uint32_t len, uint64_t& k0, uint64_t& k1,
+                                           uint64_t& sig) {
+  k0 = len >= 8 ? w0 : (w0 & ((1ull << (8 * len)) - 1ull));
+  const uint32_t tl = len > 8 ? len - 8 : 0u;
+  const uint64_t t = w1 & ((1ull << (8 * tl)) - 1ull);
+  const uint64_t lt = (uint64_t)len << 56;
+  k1 = len <= 8 ? (uint64_t)len : (t | lt);
+  sig = (len <= 7 ? k0 : ((t ^ k0) & LOW7)) | lt;
+}
+
+// The two candidate groups of a key (2-choice placement; g2 != g1).
+__device__ __forceinline__ void hot_groups(uint32_t ph, uint32_t& g1, uint32_t& g2) {
+  g1 = (ph >> 20) & (NG - 1);
+  g2 = (g1 + 1u + ((ph >> 8) % (NG - 1))) & (NG - 1);
+}
+
+// 64-bit fingerprint of a sampled word (never 0): keys the global sample table.
+__device__ __forceinline__ uint64_t sample_fp(uint64_t sig, uint64_t side) {
+  return fmix64(sig ^ (side * 0x9E3779B97F4A7C15ull)) | 1ull;
+}
+
+// Delimiter bits of the lane's 32 bytes (registers) and of the following 32
+// (neighbour lane; lane 63: the halo in `buf`), token starts of the lane.
+__device__ __forceinline__ void unit_masks(const uint4& p0, const uint4& p1, const uint8_t* buf, uint32_t pv,
+                                           uint64_t u0, uint32_t pbase, uint64_t chunk_len, uint64_t& dm,
+                                           uint32_t& starts) {
+  const int lane = (int)__lane_id();
+  const uint32_t w8[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+  uint32_t mine = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) mine |= delim_bits4(w8[q]) << (4 * q);
+  const uint32_t next = __shfl_down(mine, 1);
+  uint32_t hb = 0;
+  if (lane == 63) {
+    const uint4 hv = *reinterpret_cast<const uint4*>(&buf[UNIT]);
+    const uint4 hw = *reinterpret_cast<const uint4*>(&buf[UNIT + 16]);
+    const uint32_t h8[8] = {hv.x, hv.y, hv.z, hv.w, hw.x, hw.y, hw.z, hw.w};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) hb |= delim_bits4(h8[q]) << (4 * q);
+  }
+  dm = (uint64_t)mine | ((uint64_t)(lane == 63 ? hb : next) << 32);
+  const uint32_t prevd = __shfl_up(mine, 1) >> 31;  // last byte of the lane below
+  const uint32_t carry = lane == 0 ? (is_delim(pv) ? 1u : 0u) : prevd;
+  starts = ~mine & ((mine << 1) | carry);
+  const uint64_t lane_base = u0 + pbase;
+  if (lane_base >= chunk_len) starts = 0;
+  else if (lane_base + MAP_BPL > chunk_len) starts &= (1u << (uint32_t)(chunk_len - lane_base)) - 1u;
+}
+
+// Unit range of map block `blk` (units of UNIT bytes).
+__device__ __forceinline__ void unit_range(uint64_t chunk_len, uint32_t grid, uint32_t blk, uint64_t& ub,
+                                           uint64_t& ue) {
+  const uint64_t nunits = (chunk_len + UNIT - 1) / UNIT;
+  const uint64_t per = (nunits + grid - 1) / grid;
+  ub = min((uint64_t)blk * per, nunits);
+  ue = min(ub + per, nunits);
+}
+
+// ------------------------------------------------------------------ sampling
+struct SampleLds {
+  uint64_t fp[MAP_SLOTS];  // 0 empty, else the word's fingerprint
+  uint64_t sig[MAP_SLOTS];
+  uint64_t side[MAP_SLOTS];
   uint32_t cnt[MAP_SLOTS];
-  uint32_t off[MAP_SLOTS];
-  uint16_t list[MAP_WAVES][MAP_LIST];  // token rounds: wave-relative position | min(length, 31) << 11
-  uint32_t bcur[MAX_REC_BUCKETS];  // records appended to each bucket's sub-region (persistent)
-  uint32_t fail[MAP_THREADS];  // bit i of word t: token at tile byte 32 t + i must be retried
-  uint8_t tile[MAP_TILE + MAP_HALO + 16];  // +16: tile8() reads one word past
-  uint32_t occupied;
-  uint32_t flush_kept;  // flush: sticky slots kept (-> occupied)
-  uint32_t sticky;  // slots promoted to sticky (budget counter)
-  uint32_t occ_before, last_new;  // adaptive flush: keys added by the last tile
-  uint32_t prev;
-  unsigned long long used;  // records emitted by this block (stats)
-  unsigned long long tokens;
-  // slot state (flush_table): the bucket bits of place_hash live in the tag
-  __device__ int bucket(int s, uint32_t log2_nb) const {
-    const uint32_t t = tag[s];
-    return t ? (int)((t >> 2) & ((1u << log2_nb) - 1u)) : -1;
-  }
-  __device__ void evict(int s) {
-    tag[s] = 0;
-    key[s].y = K1_EMPTY;
-  }
-  __device__ u64x2 key_at(int s) const { return key[s]; }
+  uint8_t buf[MAP_WAVES][BUF];
 };
-static_assert(sizeof(MapLds) <= 160 * 1024 / MAP_BLOCKS_PER_CU, "map blocks per CU must fit its LDS");
+static_assert(sizeof(SampleLds) <= 160 * 1024, "one sample block per CU");
+
+// Each wave takes sampled units (stride over the block's range) and counts
+// their inline words per lane; the block then adds its table into the global
+// fingerprint table (HotArgs::cap slots, linear probing, device atomics).
+__global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs h) {
+  __shared__ SampleLds L;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int s = tid; s < MAP_SLOTS; s += MAP_THREADS) {
+    L.fp[s] = 0;
+    L.cnt[s] = 0;
+  }
+  __syncthreads();
+  uint64_t ub, ue;
+  unit_range(a.chunk_len, gridDim.x, blockIdx.x, ub, ue);
+  const uint64_t nu = ue - ub;
+  const uint64_t ns = min<uint64_t>(nu, HOT_SAMPLE);
+  uint8_t* buf = L.buf[wave];
+  const uint32_t pbase = lane * MAP_BPL;
+  for (uint64_t i = wave; i < ns; i += MAP_WAVES) {
+    const uint64_t u = ub + i * nu / ns;
+    const uint64_t u0 = u * UNIT;
+    uint4 p0, p1;
+    load32(a, u0 + pbase, p0, p1);
+    reinterpret_cast<uint4*>(&buf[pbase])[0] = p0;
+    reinterpret_cast<uint4*>(&buf[pbase])[1] = p1;
+    if (lane < HALO / 16) *reinterpret_cast<uint4*>(&buf[UNIT + lane * 16]) = load16(a, u0 + UNIT + lane * 16);
+    const uint32_t pv = (u0 == 0 && a.prev_byte >= 0) ? (uint32_t)a.prev_byte : a.text[(int64_t)u0 - 1];
+    wave_sync();
+    uint64_t dm;
+    uint32_t bits;
+    unit_masks(p0, p1, buf, pv, u0, pbase, a.chunk_len, dm, bits);
+    while (bits) {
+      const uint32_t b = __ffs(bits) - 1;
+      bits &= bits - 1;
+      const uint64_t rest = dm >> b;
+      const uint32_t len = rest ? (uint32_t)__ffsll((unsigned long long)rest) - 1 : 64u;
+      if (len > KEY_INLINE_MAX) continue;
+      const uint32_t p = pbase + b;
+      uint64_t k0, k1, sg;
+      inline_key(tile8(buf, p), tile8(buf, p + 8), len, k0, k1, sg);
+      const uint64_t sd = two_word(sg) ? k0 : 0ull;
+      const uint64_t f = sample_fp(sg, sd);
+      uint32_t g = (place_hash(k0, k1) >> 20) & (NG - 1);
+      for (int st = 0; st < SAMPLE_PROBES * GS; ++st) {
+        const uint32_t s = GS * g + (st & (GS - 1));
+        uint64_t cur = L.fp[s];
+        if (cur == 0) {
+          cur = atomicCAS(reinterpret_cast<unsigned long long*>(&L.fp[s]), 0ull, (unsigned long long)f);
+          if (cur == 0) {  // claimed: the claimer stores the key (read after the block barrier)
+            L.sig[s] = sg;
+            L.side[s] = sd;
+            cur = f;
+          }
+        }
+        if (cur == f) {
+          atomicAdd(&L.cnt[s], 1u);
+          break;
+        }
+        if ((st & (GS - 1)) == GS - 1) g = (g + 1) & (NG - 1);
+      }
+    }
+    wave_sync();
+  }
+  __syncthreads();
+  const uint64_t gmask = h.cap - 1;
+  for (int s = tid; s < MAP_SLOTS; s += MAP_THREADS) {
+    const uint32_t c = L.cnt[s];
+    if (!c) continue;
+    const uint64_t f = L.fp[s];
+    uint64_t gs = (f >> 20) & gmask;
+    for (int n = 0; n < 64; ++n) {  // bounded: a word that finds no room is simply not a candidate
+      const unsigned long long old = atomicCAS(&h.fp[gs], 0ull, (unsigned long long)f);
+      if (old == 0ull || old == f) {
+        atomicAdd(&h.cnt[gs], c);
+        if (old == 0ull) {  // first block to see the word stores it (read by the next launch)
+          h.sig[gs] = L.sig[s];
+          h.side[gs] = L.side[s];
+        }
+        break;
+      }
+      gs = (gs + 1) & gmask;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ selection
+// Three short launches over the fingerprint table (HOT_SEL_BLOCKS blocks for
+// the two scans): count histogram -> threshold keeping <= HOT_K words (ties
+// at the threshold taken while room remains) -> 2-choice placement into the
+// image (the emptier of the word's two groups, else the other; both full: the
+// word stays out).  HotArgs::sel holds [0, SEL_BINS) histogram, then the
+// threshold, the tie quota and the tie counter; HotArgs::gocc the group fill.
+constexpr int SEL_BINS = HOT_SEL_BINS;
+
+__global__ void __launch_bounds__(1024) wc_hot_hist(HotArgs h) {
+  __shared__ uint32_t hist[SEL_BINS];
+  for (int i = threadIdx.x; i < SEL_BINS; i += 1024) hist[i] = 0;
+  __syncthreads();
+  for (uint64_t s = blockIdx.x * 1024ull + threadIdx.x; s < h.cap; s += (uint64_t)gridDim.x * 1024) {
+    const uint32_t c = h.cnt[s];
+    if (c) atomicAdd(&hist[min(c, (uint32_t)SEL_BINS - 1)], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < SEL_BINS; i += 1024)
+    if (hist[i]) atomicAdd(&h.sel[i], hist[i]);
+}
+
+// Threshold t: the smallest count whose words (counted >= t) fit in HOT_K.
+// One block: thread i owns bins [4i, 4i + 4); a reverse block scan gives the
+// number of words counted >= each bin.
+__global__ void __launch_bounds__(1024) wc_hot_threshold(HotArgs h) {
+  static_assert(SEL_BINS == 4 * 1024, "threshold: 4 bins per thread");
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t best;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t b[4], own = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) own += b[i] = h.sel[4 * tid + i];
+  // inclusive scan from the top: suffix = words in bins >= 4 tid
+  uint32_t x = own;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_down(x, o);
+    if (lane + o < 64) x += y;
+  }
+  if (lane == 0) wsum[wave] = x;
+  if (tid == 0) best = SEL_BINS;
+  __syncthreads();
+  uint32_t above = 0;  // words in the waves above this one
+  for (int w = wave + 1; w < 16; ++w) above += wsum[w];
+  const uint32_t suf0 = x + above;  // words counted >= 4 tid
+  uint32_t suf = suf0, t = SEL_BINS;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // words counted >= bin 4 tid + i
+    if (t == SEL_BINS && suf <= HOT_K && 4 * tid + i >= 1) t = 4 * tid + i;
+    suf -= b[i];
+  }
+  if (t < SEL_BINS) atomicMin(&best, t);
+  __syncthreads();
+  const uint32_t tt = best == SEL_BINS ? 1u : best;
+  if ((uint32_t)tid == tt / 4) {  // the owner of bin tt: words counted >= tt, then the tie quota
+    uint32_t cum = suf0;
+    for (uint32_t i = 0; i < tt % 4; ++i) cum -= b[i];
+    h.sel[SEL_BINS] = tt;
+    h.sel[SEL_BINS + 1] = tt > 1 ? HOT_K - min(cum, HOT_K) : 0;
+    h.sel[SEL_BINS + 2] = 0;
+  }
+}
+
+// pass 0 places the words counted >= HOT_FIRST_MUL * t (the most frequent:
+// their tokens must never flood one shuffle bucket), pass 1 the rest.
+constexpr uint32_t HOT_FIRST_MUL = 8;
+__global__ void __launch_bounds__(1024) wc_hot_place(HotArgs h, int pass) {
+  const uint32_t t = h.sel[SEL_BINS], ties = h.sel[SEL_BINS + 1];
+  const uint32_t big = min(HOT_FIRST_MUL * t, (uint32_t)SEL_BINS - 1);
+  for (uint64_t s = blockIdx.x * 1024ull + threadIdx.x; s < h.cap; s += (uint64_t)gridDim.x * 1024) {
+    const uint32_t c = min(h.cnt[s], (uint32_t)SEL_BINS - 1);
+    if (c == 0 || c + 1 < t || (pass == 0) != (c >= big)) continue;
+    if (c < t && atomicAdd(&h.sel[SEL_BINS + 2], 1u) >= ties) continue;
+    const uint64_t sg = h.sig[s], sd = h.side[s];
+    uint64_t k0, k1;
+    sig_key(sg, sd, k0, k1);
+    uint32_t g1, g2;
+    hot_groups(place_hash(k0, k1), g1, g2);
+    if (__hip_atomic_load(&h.gocc[g2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+        __hip_atomic_load(&h.gocc[g1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      const uint32_t x = g1;
+      g1 = g2;
+      g2 = x;
+    }
+    uint32_t g = g1, o = atomicAdd(&h.gocc[g1], 1u);
+    if (o >= GS) {
+      g = g2;
+      o = atomicAdd(&h.gocc[g2], 1u);
+    }
+    if (o >= GS) continue;
+    h.img_sig[GS * g + o] = sg;
+    h.img_side[GS * g + o] = sd;
+  }
+}
+
+// ------------------------------------------------------------------ map
+struct alignas(16) MapLds {
+  alignas(16) uint64_t sig[MAP_SLOTS];  // hot table image (read-only while tokens stream); 0 = empty
+  uint64_t side[MAP_SLOTS];             // k0 of two-word signatures
+  uint32_t cnt[MAP_SLOTS];
+  uint32_t off[MAP_SLOTS];              // chunk-relative first offset in the block
+  uint16_t list[MAP_WAVES][MAP_LIST];
+  uint32_t bcur[MAX_REC_BUCKETS];       // records appended to each bucket's sub-region (short | long << 16)
+  uint8_t buf[MAP_WAVES][BUF];
+  uint32_t next_unit;
+  unsigned long long used, tokens;
+};
+static_assert(sizeof(MapLds) + 8 * MAP_STAMP_N <= 160 * 1024, "one map block per CU");
+
+// Index (0..7) of the first of a key's eight candidate signatures equal to sig, else -1.
+__device__ __forceinline__ int sig_match8(const u64x2& a, const u64x2& b, const u64x2& c, const u64x2& d,
+                                          uint64_t sig) {
+  const uint32_t m = (a.x == sig ? 1u : 0u) | (a.y == sig ? 2u : 0u) | (b.x == sig ? 4u : 0u) |
+                     (b.y == sig ? 8u : 0u) | (c.x == sig ? 16u : 0u) | (c.y == sig ? 32u : 0u) |
+                     (d.x == sig ? 64u : 0u) | (d.y == sig ? 128u : 0u);
+  return (int)__ffs(m) - 1;
+}
 
 template <bool ST>
-__global__ void __launch_bounds__(MAP_THREADS, 4) wc_map_tokenize(MapArgs a) {  // 2nd arg: waves per SIMD
+__global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   __shared__ MapLds L;
   __shared__ unsigned long long st_acc[ST ? MAP_STAMP_N : 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (ST && tid < MAP_STAMP_N) st_acc[tid] = 0;
-  clear_slots(L);
-  L.fail[tid] = 0;
-  for (uint32_t b = tid; b < MAX_REC_BUCKETS; b += MAP_THREADS) L.bcur[b] = 0;
-  if (tid == 0) {
-    L.occupied = 0;
-    L.sticky = 0;
-    L.last_new = 0;
-    L.tokens = 0;
-    L.flush_kept = 0;
-    L.used = 0;
+#pragma unroll
+  for (int j = 0; j < SPT; ++j) {
+    const int s = tid + j * MAP_THREADS;
+    L.sig[s] = h.img_sig[s];
+    L.side[s] = h.img_side[s];
+    L.cnt[s] = 0;
+    L.off[s] = 0xFFFFFFFFu;
   }
+  for (uint32_t b = tid; b < MAX_REC_BUCKETS; b += MAP_THREADS) L.bcur[b] = 0;
+  uint64_t u_begin, u_end;
+  unit_range(a.chunk_len, gridDim.x, blockIdx.x, u_begin, u_end);
+  if (tid == 0) {
+    L.next_unit = 0;
+    L.used = L.tokens = 0;
+  }
+  __syncthreads();
 
-  const uint64_t ntiles = (a.chunk_len + MAP_TILE - 1) / MAP_TILE;
-  uint32_t my_tokens = 0;
-  uint64_t sink = 0;  // keeps ablated work alive
-
-  // Software pipeline: the next tile's 32 B per lane (+ halo) are loaded into
-  // registers while the current tile is being tokenized.
+  const uint32_t bmask = (1u << a.log2_rec_buckets) - 1u;
+  uint8_t* buf = L.buf[wave];
+  uint16_t* list = L.list[wave];
+  uint32_t my_tokens = 0, my_direct = 0;
+  uint64_t sink = 0;  // profiling builds: keeps ablated work alive
+  auto grab = [&]() -> uint32_t {
+    uint32_t v = 0;
+    if (lane == 0) v = atomicAdd(&L.next_unit, 1u);
+    v = __builtin_amdgcn_readfirstlane(v);
+    return u_begin + v < u_end ? (uint32_t)(u_begin + v) : NONE;
+  };
+  // next unit's 32 B per lane (+ halo, + the byte before it) in registers
   uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0, ph16 = p0;
   uint32_t pprev = 0x20;
-  auto prefetch = [&](uint64_t tile) {
-    if (tile >= ntiles) return;
-    const uint64_t t0 = tile * MAP_TILE;
-    load32(a, t0 + (uint64_t)tid * MAP_BPL, p0, p1);
-    if (tid < MAP_HALO / 16) ph16 = load16(a, t0 + MAP_TILE + (uint64_t)tid * 16);
-    if (tid == 0) pprev = (t0 == 0 && a.prev_byte >= 0) ? (uint32_t)a.prev_byte : a.text[(int64_t)t0 - 1];
+  auto prefetch = [&](uint32_t u) {
+    if (u == NONE) return;
+    const uint64_t g0 = (uint64_t)u * UNIT;
+    load32(a, g0 + (uint64_t)lane * MAP_BPL, p0, p1);
+    if (lane < HALO / 16) ph16 = load16(a, g0 + UNIT + (uint64_t)lane * 16);
+    if (lane == 0) pprev = (g0 == 0 && a.prev_byte >= 0) ? (uint32_t)a.prev_byte : a.text[(int64_t)g0 - 1];
   };
-  prefetch(blockIdx.x);
   PhaseClock<ST> clk;
   clk.start(st_acc);
   const uint64_t t_begin = clk.t;
+  const uint32_t pbase = lane * MAP_BPL;
+  uint32_t ndef = 0;  // deferred LONG entries of the current round (list[0, ndef))
 
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const uint64_t t0 = tile * MAP_TILE;
-    __syncthreads();  // previous tile fully consumed
-    clk.lap(MS_TOP);
-    // Flush only if the keys the last tile added would not fit again: Zipf
-    // text with a small vocabulary keeps its table across many tiles, large
-    // vocabularies flush before every tile instead of overflowing mid-tile.
-    if (L.occupied + L.last_new > MAP_FILL_MAX) {
-      if constexpr (ST) {
-        if (tid == 0) st_acc[MS_NFLUSH] += 1;
+  // LONG words of the round (>= 16 bytes or longer than the lane window):
+  // byte-loop keys, one record each; 64 per pass, the unit still in `buf`.
+  auto run_deferred = [&](uint64_t u0) {
+    wave_sync();
+    for (uint32_t c = 0; c < ndef; c += 64) {
+      const bool hv = c + lane < ndef;
+      const uint32_t q = (hv ? list[c + lane] : 0u) & 0x7FFu;
+      if (hv) {
+        uint64_t k0, k1;
+        key_slow(buf, UNIT + HALO, a, q, u0 + q, k0, k1);
+        emit_record(L.bcur, a, place_hash(k0, k1) & bmask, k0, k1, 1, (uint32_t)(u0 + q));
       }
-      flush_table(L, a, clk, false);  // the commit barrier follows
     }
-    clk.lap(MS_FLUSH);
-    if (tid == 0) L.occ_before = L.occupied;
-    // ---- commit the prefetched tile to LDS, start loading the next ----
-    reinterpret_cast<uint4*>(&L.tile[tid * MAP_BPL])[0] = p0;
-    reinterpret_cast<uint4*>(&L.tile[tid * MAP_BPL])[1] = p1;
-    if (tid < MAP_HALO / 16) *reinterpret_cast<uint4*>(&L.tile[MAP_TILE + tid * 16]) = ph16;
-    if (tid == 0) L.prev = pprev;
-    __syncthreads();
-    prefetch(tile + gridDim.x);
+    my_direct += ndef;
+    ndef = 0;
+    wave_sync();
+  };
+
+  uint32_t u = grab();
+  prefetch(u);
+  uint32_t nu = u == NONE ? NONE : grab();
+  while (u != NONE) {
+    // ---- commit the prefetched unit, build its masks and token count ----
+    const uint64_t u0 = (uint64_t)u * UNIT;
+    wave_sync();  // the previous unit's reads are done
+    reinterpret_cast<uint4*>(&buf[pbase])[0] = p0;
+    reinterpret_cast<uint4*>(&buf[pbase])[1] = p1;
+    if (lane < HALO / 16) *reinterpret_cast<uint4*>(&buf[UNIT + lane * 16]) = ph16;
+    const uint32_t pv = __shfl(pprev, 0);
+    const uint4 c0 = p0, c1 = p1;
+    wave_sync();
+    prefetch(nu);
     clk.lap(MS_COMMIT);
-
-    // ---- 64-byte window (own 32 B + next lane's), delimiter / start masks ----
-    uint64_t dm = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint4 v = reinterpret_cast<const uint4*>(&L.tile[tid * MAP_BPL])[j];
-      dm |= delim_mask8((uint64_t)v.x | ((uint64_t)v.y << 32)) << (16 * j);
-      dm |= delim_mask8((uint64_t)v.z | ((uint64_t)v.w << 32)) << (16 * j + 8);
-    }
-    const uint32_t prevb = (tid == 0) ? L.prev : L.tile[tid * MAP_BPL - 1];
-    uint32_t starts = (uint32_t)(~dm & ((dm << 1) | (is_delim(prevb) ? 1ull : 0ull)));
-    const uint64_t lane_base = t0 + (uint64_t)tid * MAP_BPL;
-    if (lane_base >= a.chunk_len) {
-      starts = 0;
-    } else if (lane_base + MAP_BPL > a.chunk_len) {
-      starts &= (1u << (uint32_t)(a.chunk_len - lane_base)) - 1u;
-    }
-    const uint32_t ntok = __popc(starts);
+    uint64_t dm;
+    uint32_t bits;
+    unit_masks(c0, c1, buf, pv, u0, pbase, a.chunk_len, dm, bits);
+    const uint32_t ntok = __popc(bits);
     my_tokens += ntok;
-    uint64_t t_tok = 0;
-    if constexpr (ST) t_tok = __builtin_amdgcn_s_memtime();
+    uint32_t wave_total;
+    uint32_t k = wave_excl_small(ntok, wave_total);
+    wave_total = __builtin_amdgcn_readfirstlane(wave_total);
     clk.lap(MS_MASK);
-    if (a.ablate == 2) {
-      sink ^= dm;
-      continue;
-    }
-
-    // ---- compact the wave's tokens into list rounds of MAP_LIST entries ----
-    uint32_t incl = ntok;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(incl, o);
-      if (lane >= o) incl += y;
-    }
-    const uint32_t wave_total = __shfl(incl, 63), excl = incl - ntok;
-    const uint32_t pbase = tid * MAP_BPL;
-    uint16_t* list = L.list[wave];
-    const uint32_t wbase = wave * MAP_WAVE_BYTES;
-    bool any_fail = false;
-    uint32_t bits = starts, k = excl;  // this lane's next token and its wave index
     for (uint32_t base = 0; base < wave_total; base += MAP_LIST) {
+      // ---- list round: entries [base, base + MAP_LIST) of the unit ----
       const uint32_t lim = base + MAP_LIST;
       while (bits && k < lim) {
         const uint32_t i = __ffs(bits) - 1;
         bits &= bits - 1;
         const uint64_t rest = dm >> i;
         const uint32_t len = rest ? min((uint32_t)__ffsll((unsigned long long)rest) - 1, MAP_LONG) : MAP_LONG;
-        list[k - base] = (uint16_t)((pbase + i - wbase) | (len << 11));
+        list[k - base] = (uint16_t)((pbase + i) | (len << 11));
         ++k;
       }
       wave_sync();
+      const uint32_t round_n = min(wave_total - base, (uint32_t)MAP_LIST);
       clk.lap(MS_LIST);
-      const uint32_t n = min(wave_total - base, (uint32_t)MAP_LIST);
-      for (uint32_t j = 0; j < n; j += 128) {
-      const bool h1 = j + lane < n, h2 = j + 64 + lane < n;
-      const uint32_t e1 = h1 ? list[j + lane] : 0u, e2 = h2 ? list[j + 64 + lane] : 0u;
-      const uint32_t q1 = wbase + (e1 & 0x7FFu), q2 = wbase + (e2 & 0x7FFu);
-      uint64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
-      if (h1) token_key(L.tile, MAP_TILE + MAP_HALO, a, t0, q1, e1 >> 11, a0, a1);
-      if (h2) token_key(L.tile, MAP_TILE + MAP_HALO, a, t0, q2, e2 >> 11, b0, b1);
-      if (ST) {  // force the keys before the keys/combine boundary stamp
-        asm volatile("" ::"v"(a0), "v"(a1), "v"(b0), "v"(b1));
+      for (uint32_t j = 0; j < round_n; j += 128) {
+        // ---- one step: two list entries per lane, both probed in one round trip ----
+        const bool h1 = j + lane < round_n, h2 = j + 64 + lane < round_n;
+        const uint32_t e1 = h1 ? list[j + lane] : 0u, e2 = h2 ? list[j + 64 + lane] : 0u;
+        const uint32_t q1 = e1 & 0x7FFu, q2 = e2 & 0x7FFu, n1 = e1 >> 11, n2 = e2 >> 11;
+        const uint64_t w10 = tile8(buf, q1), w11 = tile8(buf, q1 + 8);
+        const uint64_t w20 = tile8(buf, q2), w21 = tile8(buf, q2 + 8);
+        if (WC_MAP_ABLATE == 1) {
+          sink ^= w10 ^ w21;
+          continue;
+        }
+        const bool in1 = h1 && n1 <= KEY_INLINE_MAX, in2 = h2 && n2 <= KEY_INLINE_MAX;
+        uint64_t a0, a1, as, b0, b1, bs;
+        inline_key(w10, w11, n1, a0, a1, as);
+        inline_key(w20, w21, n2, b0, b1, bs);
+        const uint32_t ha = place_hash(a0, a1), hb = place_hash(b0, b1);
+        uint32_t ga1, ga2, gb1, gb2;
+        hot_groups(ha, ga1, ga2);
+        hot_groups(hb, gb1, gb2);
+        clk.lap(MS_KEYS);
+        if (WC_MAP_ABLATE == 2) {
+          sink ^= as ^ bs ^ ga2 ^ gb2;
+          continue;
+        }
+        const u64x2* S = reinterpret_cast<const u64x2*>(L.sig);
+        const u64x2 xa0 = S[2 * ga1], xa1 = S[2 * ga1 + 1], xa2 = S[2 * ga2], xa3 = S[2 * ga2 + 1];
+        const u64x2 xb0 = S[2 * gb1], xb1 = S[2 * gb1 + 1], xb2 = S[2 * gb2], xb3 = S[2 * gb2 + 1];
+        const int ma = in1 ? sig_match8(xa0, xa1, xa2, xa3, as) : -1;
+        const int mb = in2 ? sig_match8(xb0, xb1, xb2, xb3, bs) : -1;
+        int s1 = ma < 0 ? -1 : (int)(GS * (ma < GS ? ga1 : ga2)) + (ma & (GS - 1));
+        int s2 = mb < 0 ? -1 : (int)(GS * (mb < GS ? gb1 : gb2)) + (mb & (GS - 1));
+        // two-word keys: the matching slot's side word decides
+        const bool ta = two_word(as), tb = two_word(bs);
+        const uint64_t ca = s1 >= 0 && ta ? L.side[s1] : a0, cb = s2 >= 0 && tb ? L.side[s2] : b0;
+        if (ca != a0) s1 = -1;
+        if (cb != b0) s2 = -1;
+        clk.lap(MS_PROBE);
+        const uint32_t o1 = (uint32_t)(u0 + q1), o2 = (uint32_t)(u0 + q2);
+        if (s1 >= 0) {
+          atomicAdd(&L.cnt[s1], 1u);  // results unused: no-return ds_add / ds_min
+          atomicMin(&L.off[s1], o1);
+        }
+        if (s2 >= 0) {
+          atomicAdd(&L.cnt[s2], 1u);
+          atomicMin(&L.off[s2], o2);
+        }
+        if (WC_MAP_ABLATE == 3) continue;
+        // misses of inline words become records now; LONG words wait for the round end
+        const bool d1 = in1 && s1 < 0, d2 = in2 && s2 < 0;
+        emit_two(L.bcur, a, d1, ha & bmask, a0, a1, o1, d2, hb & bmask, b0, b1, o2);
+        const bool f1 = h1 && !in1, f2 = h2 && !in2;
+        const uint64_t mf1 = __ballot(f1), mf2 = __ballot(f2);
+        if (mf1 | mf2) {  // entries before j are consumed: ndef <= j
+          const uint32_t r1 =
+              __builtin_amdgcn_mbcnt_hi((uint32_t)(mf1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mf1, 0u));
+          const uint32_t r2 =
+              __builtin_amdgcn_mbcnt_hi((uint32_t)(mf2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mf2, 0u));
+          const uint32_t n1c = (uint32_t)__popcll(mf1);
+          if (f1) list[ndef + r1] = (uint16_t)e1;
+          if (f2) list[ndef + n1c + r2] = (uint16_t)e2;
+          ndef += n1c + (uint32_t)__popcll(mf2);
+        }
+        my_direct += (uint32_t)(__popcll(__ballot(d1)) + __popcll(__ballot(d2)));
+        if constexpr (ST) {
+          const uint32_t nh = (uint32_t)(__popcll(__ballot(s1 >= 0)) + __popcll(__ballot(s2 >= 0)));
+          if (lane == 0) {
+            atomicAdd(&st_acc[MS_N_HIT], (unsigned long long)nh);
+            atomicAdd(&st_acc[MS_N_DEFER], (unsigned long long)__popcll(mf1 | mf2));
+          }
+        }
+        clk.lap(MS_EMIT);
       }
-      clk.lap(MS_KEYS);
-      if (a.ablate == 1) {
-        sink ^= place_hash(a0, a1) + place_hash(b0, b1);
-        continue;
-      }
-      bool c1 = false, c2 = false;
-      if (h1 && !combine(L, a0, a1, (uint32_t)(t0 + q1), c1)) {
-        atomicOr(&L.fail[q1 >> 5], 1u << (q1 & 31));
-        any_fail = true;
-      }
-      if (h2 && !combine(L, b0, b1, (uint32_t)(t0 + q2), c2)) {
-        atomicOr(&L.fail[q2 >> 5], 1u << (q2 & 31));
-        any_fail = true;
-      }
-      const uint32_t claims = (uint32_t)__popcll(__ballot(c1)) + (uint32_t)__popcll(__ballot(c2));
-      if (lane == 0 && claims) atomicAdd(&L.occupied, claims);
-      clk.lap(MS_COMBINE);
+      if (ndef) {
+        run_deferred(u0);
+        clk.lap(MS_SLOW);
       }
       wave_sync();  // entries read before the next round overwrites them
     }
-
-    if constexpr (ST) {  // spread of the waves' token-phase times (diagnostic)
-      const uint64_t dt = __builtin_amdgcn_s_memtime() - t_tok;
-      if (lane == 0) {
-        atomicAdd(&st_acc[MS_TOKSUM], (unsigned long long)dt);
-        atomicMax(&st_acc[MS_TOKMAX_TILE], (unsigned long long)dt);
-      }
-    }
-    // ---- probe sequences that were full: flush, then the owners retry ----
-    // (a second retry in one tile also evicts the sticky slots: always progresses)
-    for (uint32_t attempt = 0; __syncthreads_or(any_fail); ++attempt) {
-      clk.lap(MS_RETRY);
-      if constexpr (ST) {
-        if (tid == 0) st_acc[MS_NRETRY] += 1;
-      }
-      flush_table(L, a, clk, true, attempt > 0);
-      clk.lap(MS_FLUSH);
-      uint32_t todo = L.fail[tid];
-      L.fail[tid] = 0;
-      any_fail = false;
-      uint32_t claims = 0;
-      while (todo) {
-        const uint32_t i = __ffs(todo) - 1;
-        todo &= todo - 1;
-        const uint64_t rest = dm >> i;
-        const uint32_t len = rest ? min((uint32_t)__ffsll((unsigned long long)rest) - 1, MAP_LONG) : MAP_LONG;
-        uint64_t k0, k1;
-        token_key(L.tile, MAP_TILE + MAP_HALO, a, t0, pbase + i, len, k0, k1);
-        bool c = false;
-        if (!combine(L, k0, k1, (uint32_t)(t0 + pbase + i), c)) {
-          atomicOr(&L.fail[tid], 1u << i);
-          any_fail = true;
-        }
-        claims += c;
-      }
-      if (claims) atomicAdd(&L.occupied, claims);
-    }
-    clk.lap(MS_RETRY);
-    if (tid == 0) L.last_new = L.occupied > L.occ_before ? L.occupied - L.occ_before : L.occupied;
-    if constexpr (ST) {
-      if (tid == 0) {  // all waves passed __syncthreads_or: the tile's max is final
-        st_acc[MS_TOKMAX] += st_acc[MS_TOKMAX_TILE];
-        st_acc[MS_TOKMAX_TILE] = 0;
-      }
-    }
+    u = nu;
+    nu = u == NONE ? NONE : grab();
   }
   __syncthreads();
-  clk.lap(MS_TOP);
-  if (L.occupied) flush_table(L, a, clk, false, true);  // final: sticky slots too
+  clk.lap(MS_WAIT);
+  // block end: every counted hot slot becomes one record of its bucket
+  uint32_t emitted = 0;
+#pragma unroll
+  for (int j = 0; j < SPT; ++j) {
+    const int s = tid + j * MAP_THREADS;
+    const uint32_t c = L.cnt[s];
+    if (!c) continue;
+    uint64_t k0, k1;
+    sig_key(L.sig[s], L.side[s], k0, k1);
+    emit_record(L.bcur, a, place_hash(k0, k1) & bmask, k0, k1, c, L.off[s]);
+    ++emitted;
+  }
   clk.lap(MS_FLUSH);
   if constexpr (ST) {
     if (lane == 0) atomicAdd(&st_acc[MS_TOTAL], (unsigned long long)(clk.t - t_begin));
+    if (lane == 0) atomicAdd(&st_acc[MS_N_DIRECT], (unsigned long long)my_direct);
+    if (tid == 0) {  // block duration (load balance across the grid)
+      atomicAdd(&a.stamps[MS_BLKSUM], (unsigned long long)(clk.t - t_begin));
+      atomicMax(&a.stamps[MS_BLKMAX], (unsigned long long)(clk.t - t_begin));
+    }
   }
-
-  // block totals -> one global atomic
-  uint64_t t = my_tokens;
-  for (int o = 32; o > 0; o >>= 1) t += __shfl_down(t, o);
-  if (lane == 0) atomicAdd(&L.tokens, (unsigned long long)t);
-  if (sink == 0x9E3779B97F4A7C15ull) atomicOr(&a.flags[FLAG_COUNT - 1], 0u);  // never true
+  if (WC_MAP_ABLATE && sink == 0x9E3779B97F4A7C15ull) atomicOr(&a.flags[FLAG_COUNT - 1], 0u);  // never true
+  uint64_t t = my_tokens, e = emitted;
+  for (int o = 32; o > 0; o >>= 1) {
+    t += __shfl_down(t, o);
+    e += __shfl_down(e, o);
+  }
+  if (lane == 0) {
+    atomicAdd(&L.tokens, (unsigned long long)t);
+    atomicAdd(&L.used, (unsigned long long)(e + my_direct));
+  }
   __syncthreads();
   if constexpr (ST) {
-    if (tid < MAP_STAMP_N) atomicAdd(&a.stamps[tid], st_acc[tid]);
+    if (tid < MS_BLKSUM) atomicAdd(&a.stamps[tid], st_acc[tid]);
   }
   if (tid == 0) {
     atomicAdd(a.tokens, L.tokens);
-    atomicAdd(a.rec.cursor, L.used);  // stats: records after the combiner
+    atomicAdd(a.rec.cursor, L.used);
   }
-  publish_bucket_counts(L, a);
+  const uint32_t nb = 1u << a.log2_rec_buckets;
+  for (uint32_t b = tid; b < nb; b += MAP_THREADS) a.rec.count[(size_t)blockIdx.x * nb + b] = L.bcur[b];
 }
 
 }  // namespace dev
 
-void launch_map(const MapArgs& a, uint32_t map_blocks, hipStream_t s) {
-  if (a.stamps) hipLaunchKernelGGL(dev::wc_map_tokenize<true>, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a);
-  else hipLaunchKernelGGL(dev::wc_map_tokenize<false>, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a);
+void launch_map(const MapArgs& a, const HotArgs& h, uint32_t map_blocks, hipStream_t s) {
+  hipLaunchKernelGGL(dev::wc_hot_sample, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
+  hipLaunchKernelGGL(dev::wc_hot_hist, dim3(HOT_SEL_BLOCKS), dim3(1024), 0, s, h);
+  hipLaunchKernelGGL(dev::wc_hot_threshold, dim3(1), dim3(1024), 0, s, h);
+  hipLaunchKernelGGL(dev::wc_hot_place, dim3(HOT_SEL_BLOCKS), dim3(1024), 0, s, h, 0);
+  hipLaunchKernelGGL(dev::wc_hot_place, dim3(HOT_SEL_BLOCKS), dim3(1024), 0, s, h, 1);
+  if (a.stamps) hipLaunchKernelGGL(dev::wc_map<true>, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
+  else hipLaunchKernelGGL(dev::wc_map<false>, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
 }
 
 }  // namespace wc

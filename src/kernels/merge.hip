@@ -22,30 +22,65 @@ inline dim3 mgrid(uint64_t n) {
   return dim3((unsigned)(g < 1 ? 1 : (g > 4096 ? 4096 : g)));
 }
 
-// flag[i] = 1 iff sorted entry i is a valid key differing from entry i-1.
-__global__ void wc_union_flags(const uint32_t* pos, const uint64_t* K0, const uint64_t* K1, uint32_t* flag,
-                               uint64_t m) {
+__device__ __forceinline__ bool mem_equal(const uint8_t* x, const uint8_t* y, uint64_t len) {
+  for (uint64_t c = 0; c < len; ++c)
+    if (x[c] != y[c]) return false;
+  return true;
+}
+
+// Bytes of the LONG key at union position p (all-gathered arenas, one per rank).
+struct UnionBytes {
+  const uint64_t* SO;
+  const uint32_t* SL;
+  const uint8_t* AR;
+  uint64_t n_max, arena_stride;
+  __device__ const uint8_t* at(uint32_t p) const { return AR + (p / n_max) * arena_stride + SO[p]; }
+};
+
+// flag[i] = 1 iff sorted entry i is a valid key differing from entry i-1 —
+// for LONG keys (hashed, keys.hpp): differing in bytes from every earlier
+// entry of its (k0, k1) run; rep[i] = sorted index of the run's first entry
+// with the same bytes (only read for LONG non-heads).
+__global__ void wc_union_flags(const uint32_t* pos, const uint64_t* K0, const uint64_t* K1, UnionBytes ub,
+                               uint32_t* flag, uint32_t* rep, uint64_t m) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t p = pos[i];
     const bool valid = K1[p] != K1_EMPTY;
     bool head = valid;
+    uint32_t r = (uint32_t)i;
     if (valid && i > 0) {
       const uint32_t q = pos[i - 1];
       head = !(K0[q] == K0[p] && K1[q] == K1[p]);
+      if (!head && key_is_hashed(K1[p])) {
+        // walk back to the run start; the earliest entry with equal bytes is the representative
+        uint64_t j = i;
+        while (j > 0 && K0[pos[j - 1]] == K0[p] && K1[pos[j - 1]] == K1[p]) --j;
+        head = true;
+        for (uint64_t t = j; t < i; ++t) {
+          const uint32_t pt = pos[t];
+          if (ub.SL[pt] == ub.SL[p] && mem_equal(ub.at(pt), ub.at(p), ub.SL[p])) {
+            head = false;
+            r = (uint32_t)t;
+            break;
+          }
+        }
+      }
     }
     flag[i] = head ? 1u : 0u;
+    rep[i] = r;
   }
 }
 
-// After an EXCLUSIVE scan of flags in `ex`: id = ex[i] (+ head) - 1.
-__global__ void wc_union_assign(const uint32_t* pos, const uint32_t* flag, const uint32_t* ex, const uint64_t* K0,
-                                const uint64_t* K1, const uint64_t* SO, const uint32_t* SL, uint64_t m,
-                                uint64_t n_max, uint64_t arena_stride, uint32_t* id_of_pos, uint64_t* ok0,
+// After an EXCLUSIVE scan of flags in `ex`: id = ex[i] (+ head) - 1; a LONG
+// non-head takes its representative's id.
+__global__ void wc_union_assign(const uint32_t* pos, const uint32_t* flag, const uint32_t* rep, const uint32_t* ex,
+                                const uint64_t* K0, const uint64_t* K1, const uint64_t* SO, const uint32_t* SL,
+                                uint64_t m, uint64_t n_max, uint64_t arena_stride, uint32_t* id_of_pos, uint64_t* ok0,
                                 uint64_t* ok1, uint64_t* osoff, uint32_t* oslen) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t p = pos[i];
     if (K1[p] == K1_EMPTY) continue;
-    const uint32_t id = ex[i] + flag[i] - 1;
+    const uint32_t id = (!flag[i] && key_is_hashed(K1[p])) ? ex[rep[i]] : ex[i] + flag[i] - 1;
     id_of_pos[p] = id;
     if (flag[i]) {
       ok0[id] = K0[p];
@@ -106,8 +141,8 @@ __global__ void __launch_bounds__(1024) wc_exclusive_scan_u32(const uint32_t* in
 constexpr int OWN_MAX = 64;       // ranks supported by the shuffle merge
 constexpr int OWN_ROWS_PER_BLOCK = 1024;
 
-__device__ __forceinline__ uint32_t owner_of(uint64_t ph, uint32_t W) {
-  return (uint32_t)(((ph >> 32) * (uint64_t)W) >> 32);  // high hash bits (bucket bits are low)
+__device__ __forceinline__ uint32_t owner_of(uint32_t ph, uint32_t W) {
+  return (uint32_t)(((uint64_t)ph * W) >> 32);  // high hash bits (bucket bits are low)
 }
 
 // Wave-aggregated LDS counter add: lanes with owner `o` (OWN_MAX = none) add 1
@@ -140,7 +175,7 @@ __global__ void __launch_bounds__(256) wc_owner_count(const uint64_t* k0, const 
   __syncthreads();
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t o = owner_of(place_hash(k0[i], k1[i]), W);
-    if (!key_is_short(k1[i])) atomicAdd(&h[2 * o + 1], (unsigned long long)slen[i]);
+    if (key_is_hashed(k1[i])) atomicAdd(&h[2 * o + 1], (unsigned long long)slen[i]);
     (void)wave_owner_add(h, o);
   }
   __syncthreads();
@@ -170,7 +205,7 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
     lb[j] = 0;
     if (i < n) {
       own[j] = owner_of(place_hash(k0[i], k1[i]), W);
-      if (!key_is_short(k1[i])) lb[j] = atomicAdd(&h[2 * own[j] + 1], (unsigned long long)slen[i]);
+      if (key_is_hashed(k1[i])) lb[j] = atomicAdd(&h[2 * own[j] + 1], (unsigned long long)slen[i]);
     }
     lr[j] = wave_owner_add(h, own[j]);
   }
@@ -197,7 +232,7 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
     r.first = first[i];
     r.aoff = 0;
     r.alen = 0;
-    if (!key_is_short(r.k1)) {
+    if (key_is_hashed(r.k1)) {
       const unsigned long long bpos = base[2 * o + 1] + lb[j];
       for (uint32_t b = 0; b < slen[i]; ++b) bytes[bpos + b] = arena[soff[i] + b];
       unsigned long long bb = 0;  // offset inside owner o's byte payload
@@ -209,13 +244,26 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
   }
 }
 
+// Source rank of received row r (rbase: exclusive prefix of rows per source).
+__device__ __forceinline__ uint32_t source_of(const uint64_t* rbase, uint32_t W, uint64_t r) {
+  uint32_t src = 0;
+  while (src + 1 < W && rbase[src + 1] <= r) ++src;
+  return src;
+}
+
 // Owner-side merge: a slot belongs to the first row that CAS-es its id in;
 // later rows of the same key compare against that row (immutable input) and add
-// their counts with device-scope atomics.  T is a power of two >= 2 R.
-__global__ void __launch_bounds__(256) wc_mrow_insert(const MRow* rows, uint64_t R, uint32_t* state,
-                                                      unsigned long long* cnt, unsigned long long* first, uint64_t T) {
+// their counts with device-scope atomics.  LONG keys (hashed) also compare the
+// word bytes of the two rows, so colliding words take different slots.  T is a
+// power of two >= 2 R.
+__global__ void __launch_bounds__(256) wc_mrow_insert(const MRow* rows, uint64_t R, const uint8_t* bytes,
+                                                      const uint64_t* rbase, const uint64_t* bbase, uint32_t W,
+                                                      uint32_t* state, unsigned long long* cnt,
+                                                      unsigned long long* first, uint64_t T) {
   for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < R; r += (uint64_t)gridDim.x * blockDim.x) {
     const MRow me = rows[r];
+    const bool hashed = key_is_hashed(me.k1);
+    const uint8_t* mb = hashed ? bytes + bbase[source_of(rbase, W, r)] + me.aoff : nullptr;
     uint64_t slot = place_hash(me.k0, me.k1) & (T - 1);
     for (;;) {
       uint32_t s = __hip_atomic_load(&state[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -224,7 +272,9 @@ __global__ void __launch_bounds__(256) wc_mrow_insert(const MRow* rows, uint64_t
         if (s == 0) break;  // claimed
       }
       const MRow& o = rows[s - 1];
-      if (o.k0 == me.k0 && o.k1 == me.k1) break;  // same key
+      if (o.k0 == me.k0 && o.k1 == me.k1 &&
+          (!hashed || (o.alen == me.alen && mem_equal(bytes + bbase[source_of(rbase, W, s - 1)] + o.aoff, mb, me.alen))))
+        break;  // same word
       slot = (slot + 1) & (T - 1);
     }
     atomicAdd(&cnt[slot], (unsigned long long)me.cnt);
@@ -266,8 +316,7 @@ __global__ void __launch_bounds__(256) wc_mrow_compact(const MRow* rows, const u
     if (local[j] == 0xFFFFFFFFu) continue;
     const uint64_t sl = s0 + threadIdx.x + (uint64_t)j * 256;
     const uint64_t r = state[sl] - 1u;
-    uint32_t src = 0;
-    while (src + 1 < W && rbase[src + 1] <= r) ++src;
+    const uint32_t src = source_of(rbase, W, r);
     MRow m = rows[r];
     m.cnt = cnt[sl];
     m.first = first[sl];
@@ -309,9 +358,12 @@ void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t
     hipLaunchKernelGGL(dev::wc_owner_scatter, dim3((unsigned)blocks), dim3(256), 0, s, k0, k1, cnt, first, soff, slen,
                        arena, n, W, counts, cursor, rows, bytes);
 }
-void launch_mrow_insert(const MRow* rows, uint64_t R, uint32_t* state, unsigned long long* cnt,
+void launch_mrow_insert(const MRow* rows, uint64_t R, const uint8_t* bytes, const uint64_t* rbase,
+                        const uint64_t* bbase, uint32_t W, uint32_t* state, unsigned long long* cnt,
                         unsigned long long* first, uint64_t T, hipStream_t s) {
-  if (R) hipLaunchKernelGGL(dev::wc_mrow_insert, dev::mgrid(R), dim3(256), 0, s, rows, R, state, cnt, first, T);
+  if (R)
+    hipLaunchKernelGGL(dev::wc_mrow_insert, dev::mgrid(R), dim3(256), 0, s, rows, R, bytes, rbase, bbase, W, state, cnt,
+                       first, T);
 }
 void launch_mrow_compact(const MRow* rows, const uint32_t* state, const unsigned long long* cnt,
                          const unsigned long long* first, uint64_t T, const uint64_t* rbase, const uint64_t* bbase,
@@ -328,17 +380,20 @@ void launch_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rbase, co
                        first, soff, slen);
 }
 
-void launch_union_flags(const uint32_t* pos, const uint64_t* K0, const uint64_t* K1, uint32_t* flag, uint64_t m,
-                        hipStream_t s) {
-  if (m) hipLaunchKernelGGL(dev::wc_union_flags, dev::mgrid(m), dim3(256), 0, s, pos, K0, K1, flag, m);
-}
-void launch_union_assign(const uint32_t* pos, const uint32_t* flag, const uint32_t* ex, const uint64_t* K0,
-                         const uint64_t* K1, const uint64_t* SO, const uint32_t* SL, uint64_t m, uint64_t n_max,
-                         uint64_t arena_stride, uint32_t* id_of_pos, uint64_t* ok0, uint64_t* ok1, uint64_t* osoff,
-                         uint32_t* oslen, hipStream_t s) {
+void launch_union_flags(const uint32_t* pos, const uint64_t* K0, const uint64_t* K1, const uint64_t* SO,
+                        const uint32_t* SL, const uint8_t* AR, uint64_t n_max, uint64_t arena_stride, uint32_t* flag,
+                        uint32_t* rep, uint64_t m, hipStream_t s) {
   if (m)
-    hipLaunchKernelGGL(dev::wc_union_assign, dev::mgrid(m), dim3(256), 0, s, pos, flag, ex, K0, K1, SO, SL, m, n_max,
-                       arena_stride, id_of_pos, ok0, ok1, osoff, oslen);
+    hipLaunchKernelGGL(dev::wc_union_flags, dev::mgrid(m), dim3(256), 0, s, pos, K0, K1,
+                       dev::UnionBytes{SO, SL, AR, n_max, arena_stride}, flag, rep, m);
+}
+void launch_union_assign(const uint32_t* pos, const uint32_t* flag, const uint32_t* rep, const uint32_t* ex,
+                         const uint64_t* K0, const uint64_t* K1, const uint64_t* SO, const uint32_t* SL, uint64_t m,
+                         uint64_t n_max, uint64_t arena_stride, uint32_t* id_of_pos, uint64_t* ok0, uint64_t* ok1,
+                         uint64_t* osoff, uint32_t* oslen, hipStream_t s) {
+  if (m)
+    hipLaunchKernelGGL(dev::wc_union_assign, dev::mgrid(m), dim3(256), 0, s, pos, flag, rep, ex, K0, K1, SO, SL, m,
+                       n_max, arena_stride, id_of_pos, ok0, ok1, osoff, oslen);
 }
 void launch_combine_u64(uint64_t* dst, const uint64_t* src, uint64_t n, int op, hipStream_t s) {
   if (n) hipLaunchKernelGGL(dev::wc_combine_u64, dev::mgrid(n), dim3(256), 0, s, dst, src, n, op);

@@ -9,11 +9,15 @@
 //                     loaded into LDS (144 KiB with tags), the bucket's
 //                     contiguous record run of every map block is streamed
 //                     (RED_UNROLL x 64 records in flight per wave) and merged
-//                     with LDS atomics (count +=, first = min), and
-//                     the slice is written back.  New long words copy their
-//                     bytes into the key arena so keys outlive streamed chunks.
-//                     If a slice overflows it is NOT written back; the host
-//                     splits the table and re-runs only the overflowed buckets.
+//                     with LDS atomics (count +=, first = min), and the slice
+//                     is written back.  LONG words (>= 16 bytes, hashed keys)
+//                     are merged only after a byte comparison with the stored
+//                     copy of the word (exact equality, keys.hpp): found in
+//                     parallel, new ones claimed by one wave in order, their
+//                     bytes copied to the key arena so keys outlive streamed
+//                     chunks.  If a slice overflows it is NOT written back;
+//                     the host splits the table and re-runs only the
+//                     overflowed buckets.
 //  wc_table_split     B -> 2B buckets (rehash into new slices).
 //  wc_table_compact   occupied slots -> dense columns (per-bucket block scan).
 #include "kernels.hpp"
@@ -23,17 +27,19 @@ namespace wc {
 namespace dev {
 
 constexpr int RED_UNROLL = 8;
+constexpr int LONGQ = 2048;  // LONG records queued per bucket pass (more: re-scan in batches)
 
 struct RedLds {
   SlotGroup grp[TAB_GROUPS];  // first: 16-B aligned group reads
   uint64_t cnt[TAB_SLOTS];
   uint64_t first[TAB_SLOTS];
+  uint32_t longq[LONGQ];      // record indices of LONG records, then the unmatched ones
   uint32_t occupied;
   uint32_t overflow;
-  uint32_t nnew;                 // new long words queued in a.newkeys
-  unsigned long long arena_base;  // this block's arena reservation
-  unsigned long long arena_need;
+  uint32_t nlong, nmiss;
+  uint32_t long_ovf;          // more LONG records than LONGQ: re-scan the 24-byte runs
 };
+static_assert(sizeof(RedLds) <= 160 * 1024, "one reduce block per CU");
 
 __device__ __forceinline__ void load_slice(RedLds& L, const TableView& t, uint32_t b) {
   const size_t base = (size_t)b * TAB_SLOTS;
@@ -89,79 +95,109 @@ __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uin
   if (len - c >= 1) dst[c] = src[c];
 }
 
-// Copy the bytes of a newly seen long word into the key arena.
-__device__ void arena_copy_word(const ReduceArgs& a, uint64_t off, size_t gslot) {
-  const uint64_t len = word_len(a, off);
-  const uint64_t p = atomicAdd(a.arena.cursor, (unsigned long long)len);
-  if (p + len > a.arena.cap) {
-    atomicOr(&a.flags[FLAG_ARENA_OVF], 1u);
-    a.tab.sref_off[gslot] = 0;
-    a.tab.sref_len[gslot] = 0;
+__device__ __forceinline__ bool bytes_equal(const uint8_t* x, const uint8_t* y, uint64_t len) {
+  uint64_t c = 0;
+  for (; c + 8 <= len; c += 8) {
+    uint64_t u, v;
+    __builtin_memcpy(&u, x + c, 8);
+    __builtin_memcpy(&v, y + c, 8);
+    if (u != v) return false;
+  }
+  for (; c < len; ++c)
+    if (x[c] != y[c]) return false;
+  return true;
+}
+
+__device__ __forceinline__ void merge_record(RedLds& L, const ReduceArgs& a, uint32_t b, uint64_t k0, uint64_t k1,
+                                             uint64_t cnt, uint32_t off, uint32_t shift, uint32_t idx) {
+  const uint32_t ph = place_hash(k0, k1);
+  if (shift && bucket_of(ph, a.tab.log2_buckets) != b) return;
+  if (key_is_hashed(k1)) {  // LONG: merged after the byte comparison (long_phase)
+    const uint32_t q = atomicAdd(&L.nlong, 1u);
+    if (q < (uint32_t)LONGQ) L.longq[q] = idx;
+    else L.long_ovf = 1;
     return;
   }
-  copy_bytes(a.arena.bytes + p, a.text + off, len);
-  a.tab.sref_off[gslot] = p;
-  a.tab.sref_len[gslot] = (uint32_t)len;
-}
-
-// Copy the bytes of this pass's new long words into the key arena: up to
-// NEWKEY_PER_THREAD words per thread, one global arena reservation per block.
-__device__ void copy_new_words(RedLds& L, const ReduceArgs& a, uint32_t b) {
-  static_assert(NEWKEY_CAP <= NEWKEY_PER_THREAD * RED_THREADS, "newkeys per thread");
-  const uint32_t n = min(L.nnew, (uint32_t)NEWKEY_CAP);
-  uint64_t len[NEWKEY_PER_THREAD], mine[NEWKEY_PER_THREAD];
-  unsigned long long off[NEWKEY_PER_THREAD];
-#pragma unroll
-  for (int k = 0; k < NEWKEY_PER_THREAD; ++k) {
-    const uint32_t i = threadIdx.x + k * RED_THREADS;
-    len[k] = 0;
-    if (i < n) {
-      mine[k] = a.newkeys[(size_t)b * NEWKEY_CAP + i];
-      len[k] = word_len(a, mine[k] & 0xFFFFFFFFull);
-      off[k] = atomicAdd(&L.arena_need, (unsigned long long)len[k]);
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) L.arena_base = L.arena_need ? atomicAdd(a.arena.cursor, L.arena_need) : 0;
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < NEWKEY_PER_THREAD; ++k) {
-    const uint32_t i = threadIdx.x + k * RED_THREADS;
-    if (i >= n) continue;
-    const size_t gslot = (size_t)b * TAB_SLOTS + (mine[k] >> 32);
-    const uint64_t p = L.arena_base + off[k], o = mine[k] & 0xFFFFFFFFull;
-    if (p + len[k] > a.arena.cap) {
-      atomicOr(&a.flags[FLAG_ARENA_OVF], 1u);
-      a.tab.sref_off[gslot] = 0;
-      a.tab.sref_len[gslot] = 0;
-      continue;
-    }
-    copy_bytes(a.arena.bytes + p, a.text + o, len[k]);
-    a.tab.sref_off[gslot] = p;
-    a.tab.sref_len[gslot] = (uint32_t)len[k];
-  }
-}
-
-__device__ __forceinline__ void merge_record(RedLds& L, const ReduceArgs& a, uint32_t b, const Rec& r, uint32_t shift) {
-  const uint64_t ph = place_hash(r.k0, r.k1);
-  if (shift && bucket_of(ph, a.tab.log2_buckets) != b) return;
   bool claimed;
-  const int s = lds_find_or_claim(L.grp, TAB_GROUPS, ph, r.k0, r.k1, TAB_MAX_GROUP_PROBES, claimed);
+  const int s = lds_find_or_claim(L.grp, TAB_GROUPS, ph, k0, k1, TAB_MAX_GROUP_PROBES, claimed);
   if (s < 0) {
     L.overflow = 1;
     return;
   }
-  atomicAdd(reinterpret_cast<unsigned long long*>(&L.cnt[s]), (unsigned long long)(r.co >> 32));
-  atomicMin(reinterpret_cast<unsigned long long*>(&L.first[s]),
-            (unsigned long long)(a.chunk_base + (r.co & 0xFFFFFFFFull)));
-  if (claimed) {
-    if (atomicAdd(&L.occupied, 1u) + 1 > (uint32_t)TAB_MAX_OCC) L.overflow = 1;
-    if (!key_is_short(r.k1)) {  // copy its bytes after the merge loop, all threads in parallel
-      const uint32_t q = atomicAdd(&L.nnew, 1u);
-      if (q < (uint32_t)NEWKEY_CAP) a.newkeys[(size_t)b * NEWKEY_CAP + q] = ((uint64_t)s << 32) | (r.co & 0xFFFFFFFFull);
-      else arena_copy_word(a, r.co & 0xFFFFFFFFull, (size_t)b * TAB_SLOTS + s);
+  atomicAdd(reinterpret_cast<unsigned long long*>(&L.cnt[s]), (unsigned long long)cnt);
+  atomicMin(reinterpret_cast<unsigned long long*>(&L.first[s]), (unsigned long long)(a.chunk_base + off));
+  if (claimed && atomicAdd(&L.occupied, 1u) + 1 > (uint32_t)TAB_MAX_OCC) L.overflow = 1;
+}
+
+// LONG records longq[0, n) of bucket b (all threads of the block):
+//  A. every thread looks its record up among the slots holding its key and
+//     compares the word bytes with each slot's arena copy -> count it;
+//  B. the unmatched records are taken IN ORDER by wave 0 (claims are rare:
+//     one per new long word per chunk): look up again (a word claimed
+//     earlier in this phase may match), else claim a slot and copy the bytes
+//     to the arena.  Sequential claims need no publication protocol.
+__device__ void long_batch(RedLds& L, const ReduceArgs& a, uint32_t b, uint32_t n) {
+  const size_t sbase = (size_t)b * TAB_SLOTS;
+  if (threadIdx.x == 0) L.nmiss = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t idx = L.longq[i];
+    const Rec r = a.rec.recs[idx];
+    const uint32_t off = (uint32_t)r.co;
+    const uint64_t len = word_len(a, off);
+    const uint32_t ph = place_hash(r.k0, r.k1);
+    int s = -1;
+    while ((s = lds_find_next(L.grp, TAB_GROUPS, ph, r.k0, r.k1, s)) >= 0) {
+      if (a.tab.sref_len[sbase + s] == len && bytes_equal(a.arena.bytes + a.tab.sref_off[sbase + s], a.text + off, len))
+        break;
+    }
+    if (s >= 0) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(&L.cnt[s]), (unsigned long long)(r.co >> 32));
+      atomicMin(reinterpret_cast<unsigned long long*>(&L.first[s]), (unsigned long long)(a.chunk_base + off));
+    } else {
+      L.longq[atomicAdd(&L.nmiss, 1u)] = idx;  // i-th entry already read: compaction in place is safe
     }
   }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const uint32_t m = L.nmiss;
+    for (uint32_t i = 0; i < m; ++i) {
+      if (L.overflow) break;
+      if (threadIdx.x != 0) continue;
+      const Rec r = a.rec.recs[L.longq[i]];
+      const uint32_t off = (uint32_t)r.co;
+      const uint64_t len = word_len(a, off);
+      const uint32_t ph = place_hash(r.k0, r.k1);
+      int s = -1;
+      while ((s = lds_find_next(L.grp, TAB_GROUPS, ph, r.k0, r.k1, s)) >= 0) {
+        if (a.tab.sref_len[sbase + s] == len &&
+            bytes_equal(a.arena.bytes + a.tab.sref_off[sbase + s], a.text + off, len))
+          break;
+      }
+      if (s < 0) {
+        bool claimed;
+        s = lds_find_or_claim(L.grp, TAB_GROUPS, ph, r.k0, r.k1, TAB_MAX_GROUP_PROBES, claimed, false);
+        if (s < 0 || ++L.occupied > (uint32_t)TAB_MAX_OCC) {
+          L.overflow = 1;
+          continue;
+        }
+        const uint64_t p = atomicAdd(a.arena.cursor, (unsigned long long)len);
+        if (p + len > a.arena.cap) {
+          atomicOr(&a.flags[FLAG_ARENA_OVF], 1u);
+          a.tab.sref_off[sbase + s] = 0;
+          a.tab.sref_len[sbase + s] = 0;
+        } else {
+          copy_bytes(a.arena.bytes + p, a.text + off, len);
+          a.tab.sref_off[sbase + s] = p;
+          a.tab.sref_len[sbase + s] = (uint32_t)len;
+        }
+        __threadfence_block();  // this lane re-reads the copy for later words of the batch
+      }
+      L.cnt[s] += r.co >> 32;
+      L.first[s] = min(L.first[s], a.chunk_base + off);
+    }
+  }
+  __syncthreads();
 }
 
 __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
@@ -174,8 +210,8 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   if (tid == 0) {
     L.occupied = a.tab.occupancy[b];
     L.overflow = 0;
-    L.nnew = 0;
-    L.arena_need = 0;
+    L.nlong = 0;
+    L.long_ovf = 0;
   }
   __syncthreads();
 
@@ -197,14 +233,10 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
 #pragma unroll
       for (int u = 0; u < RED_UNROLL; ++u) {
         if (k + u * 64 + lane >= n16) continue;
-        Rec r;
-        r.k0 = rr[u].k0;
-        r.k1 = (rr[u].w >> 32) & 0xFu;
-        r.co = ((rr[u].w >> 36) << 32) | (rr[u].w & 0xFFFFFFFFull);
-        merge_record(L, a, b, r, shift);
+        merge_record(L, a, b, rr[u].k0, (rr[u].w >> 32) & 0xFu, rr[u].w >> 36, (uint32_t)rr[u].w, shift, 0);
       }
     }
-    // long-key records (24 B)
+    // MEDIUM / LONG records (24 B)
     const uint32_t n = min(packed >> 16, (uint32_t)sub);
     const Rec* run = a.rec.recs + sr;
     for (uint32_t k = 0; k < n; k += RED_UNROLL * 64) {
@@ -213,7 +245,31 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
       for (int u = 0; u < RED_UNROLL; ++u) rr[u] = run[min(k + u * 64 + lane, n - 1)];  // clamp: always valid
 #pragma unroll
       for (int u = 0; u < RED_UNROLL; ++u)
-        if (k + u * 64 + lane < n) merge_record(L, a, b, rr[u], shift);
+        if (k + u * 64 + lane < n)
+          merge_record(L, a, b, rr[u].k0, rr[u].k1, rr[u].co >> 32, (uint32_t)rr[u].co, shift,
+                       (uint32_t)(sr + k + u * 64 + lane));
+    }
+  }
+  __syncthreads();
+  // LONG words: from the queue, or (queue overflow) by re-scanning the 24-byte runs in batches
+  if (!L.long_ovf) {
+    if (L.nlong) long_batch(L, a, b, L.nlong);
+  } else {
+    for (uint32_t p = 0; p < a.map_blocks; ++p) {
+      const uint32_t n = min(a.rec.count[(size_t)p * nrb + rb] >> 16, (uint32_t)sub);
+      const uint64_t sr = ((uint64_t)p * nrb + rb) * sub;
+      for (uint32_t k0 = 0; k0 < n; k0 += RED_THREADS) {
+        if (tid == 0) L.nlong = 0;
+        __syncthreads();
+        const uint32_t k = k0 + tid;
+        if (k < n) {
+          const Rec r = a.rec.recs[sr + k];
+          if (key_is_hashed(r.k1) && (!shift || bucket_of(place_hash(r.k0, r.k1), a.tab.log2_buckets) == b))
+            L.longq[atomicAdd(&L.nlong, 1u)] = (uint32_t)(sr + k);
+        }
+        __syncthreads();
+        if (L.nlong) long_batch(L, a, b, L.nlong);
+      }
     }
   }
   __syncthreads();
@@ -224,7 +280,6 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
     }
     return;
   }
-  copy_new_words(L, a, b);
   store_slice(L, a.tab, b);
   if (tid == 0) {
     a.tab.occupancy[b] = L.occupied;
@@ -232,7 +287,9 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   }
 }
 
-// Rehash parent slice (new_b mod B) of `src` into slice new_b of `dst` (2B buckets).
+// Rehash parent slice (new_b mod B) of `src` into slice new_b of `dst` (2B
+// buckets).  Source slots hold distinct words, so every one claims a fresh
+// slot (colliding LONG keys stay apart).
 __global__ void __launch_bounds__(RED_THREADS) wc_table_split(TableView src, TableView dst) {
   __shared__ RedLds L;
   const uint32_t nb = blockIdx.x, ob = nb & ((1u << src.log2_buckets) - 1u);
@@ -248,10 +305,10 @@ __global__ void __launch_bounds__(RED_THREADS) wc_table_split(TableView src, Tab
     const uint64_t k1 = src.k1[obase + s];
     if (k1 == K1_EMPTY) continue;
     const uint64_t k0 = src.k0[obase + s];
-    const uint64_t ph = place_hash(k0, k1);
+    const uint32_t ph = place_hash(k0, k1);
     if (bucket_of(ph, dst.log2_buckets) != nb) continue;
     bool claimed;
-    const int d = lds_find_or_claim(L.grp, TAB_GROUPS, ph, k0, k1, TAB_GROUPS, claimed);
+    const int d = lds_find_or_claim(L.grp, TAB_GROUPS, ph, k0, k1, TAB_GROUPS, claimed, false);
     // d >= 0 always: a child receives at most the parent's occupancy.
     L.cnt[d] = src.cnt[obase + s];
     L.first[d] = src.first[obase + s];
@@ -305,12 +362,13 @@ __global__ void __launch_bounds__(1024) wc_table_compact(TableView t, const uint
   for (int j = 0; j < 4; ++j) {
     if (kk1[j] == K1_EMPTY) continue;
     const size_t i = base + j;
+    const bool h = key_is_hashed(kk1[j]);
     k0[o] = t.k0[i];
     k1[o] = kk1[j];
     cnt[o] = t.cnt[i];
     first[o] = t.first[i];
-    sref_off[o] = t.sref_off[i];
-    sref_len[o] = t.sref_len[i];
+    sref_off[o] = h ? t.sref_off[i] : 0;
+    sref_len[o] = h ? t.sref_len[i] : 0;
     ++o;
   }
 }

@@ -161,10 +161,6 @@ __global__ void wc_fill_u64(uint64_t* p, uint64_t v, uint64_t n) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     p[i] = v;
 }
-__global__ void wc_place_hash(const uint64_t* k0, const uint64_t* k1, uint64_t* ph, uint64_t n) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    ph[i] = place_hash(k0[i], k1[i]);
-}
 __global__ void wc_scatter_dense(const uint32_t* ids, const uint64_t* cnt, const uint64_t* first, uint64_t* dcnt,
                                  uint64_t* dfirst, uint64_t n) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -234,9 +230,6 @@ void launch_iota_u32(uint32_t* v, uint64_t n, hipStream_t s) {
 }
 void launch_fill_u64(uint64_t* p, uint64_t v, uint64_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(dev::wc_fill_u64, dev::grid_for(n), dim3(256), 0, s, p, v, n);
-}
-void launch_place_hash(const uint64_t* k0, const uint64_t* k1, uint64_t* ph, uint64_t n, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(dev::wc_place_hash, dev::grid_for(n), dim3(256), 0, s, k0, k1, ph, n);
 }
 void launch_scatter_dense(const uint32_t* ids, const uint64_t* cnt, const uint64_t* first, uint64_t* dense_cnt,
                           uint64_t* dense_first, uint64_t n, hipStream_t s) {
