@@ -114,7 +114,7 @@ struct HotArgs {
 };
 constexpr uint64_t HOT_TABLE_CAP = 1ull << 18;
 constexpr int HOT_SEL_BINS = 4096;
-constexpr int HOT_SEL_BLOCKS = 32;
+constexpr int HOT_SEL_BLOCKS = 256;
 
 // In-kernel phase stamps of the map (diagnostic build, WC_MAP_STAMPS=1): shares
 // of wave lifetime per phase, then counters.

@@ -43,7 +43,7 @@ namespace dev {
 
 constexpr int UNIT = 64 * MAP_BPL;     // text bytes per wave unit (2 KiB)
 constexpr int HALO = 64;               // bytes past the unit kept in LDS
-constexpr int BUF = UNIT + HALO + 16;  // + one 16-byte key read past the halo
+constexpr int BUF = UNIT + HALO + 24;  // + one 24-byte window read past the halo
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr int GS = 4;                  // slots per group
 constexpr int NG = MAP_SLOTS / GS;     // groups
@@ -93,10 +93,15 @@ __device__ __forceinline__ void inline_key(uint64_t w0, uint64_t w1, uint32_t le
   sig = (len <= 7 ? k0 : ((t ^ k0) & LOW7)) | lt;
 }
 
+// Slot i of group g: slots 0-1 of every group form the first half of the
+// table, slots 2-3 the second, so each 16-byte probe read of a group half
+// lands on bank quad (g mod 16) — all 16 quads — instead of only even / odd.
+__device__ __forceinline__ uint32_t slot_of(uint32_t g, uint32_t i) { return (i < 2 ? 0u : MAP_SLOTS / 2) + 2 * g + (i & 1); }
+
 // The two candidate groups of a key (2-choice placement; g2 != g1).
 __device__ __forceinline__ void hot_groups(uint32_t ph, uint32_t& g1, uint32_t& g2) {
   g1 = (ph >> 20) & (NG - 1);
-  g2 = (g1 + 1u + ((ph >> 8) % (NG - 1))) & (NG - 1);
+  g2 = g1 ^ max((ph >> 8) & (NG - 1), 1u);
 }
 
 // 64-bit fingerprint of a sampled word (never 0): keys the global sample table.
@@ -104,28 +109,30 @@ __device__ __forceinline__ uint64_t sample_fp(uint64_t sig, uint64_t side) {
   return fmix64(sig ^ (side * 0x9E3779B97F4A7C15ull)) | 1ull;
 }
 
+// Delimiter bits of 16 bytes.
+__device__ __forceinline__ uint32_t delim_bits16(const uint4& v) {
+  return delim_bits4(v.x) | (delim_bits4(v.y) << 4) | (delim_bits4(v.z) << 8) | (delim_bits4(v.w) << 12);
+}
+
+// Delimiter bits of the first 32 halo bytes (lanes 0 and 1 hold them in h16),
+// wave-uniform.
+__device__ __forceinline__ uint32_t halo_bits(const uint4& h16) {
+  const uint32_t hb = __lane_id() < 2 ? delim_bits16(h16) : 0u;
+  return (uint32_t)__builtin_amdgcn_readlane((int)hb, 0) | ((uint32_t)__builtin_amdgcn_readlane((int)hb, 1) << 16);
+}
+
 // Delimiter bits of the lane's 32 bytes (registers) and of the following 32
-// (neighbour lane; lane 63: the halo in `buf`), token starts of the lane.
-__device__ __forceinline__ void unit_masks(const uint4& p0, const uint4& p1, const uint8_t* buf, uint32_t pv,
+// (neighbour lane by a DPP wave shift; lane 63: the halo bits), and the lane's
+// token starts.  Registers only: no LDS round trip.
+__device__ __forceinline__ void unit_masks(const uint4& p0, const uint4& p1, uint32_t hbits, uint32_t pv,
                                            uint64_t u0, uint32_t pbase, uint64_t chunk_len, uint64_t& dm,
                                            uint32_t& starts) {
   const int lane = (int)__lane_id();
-  const uint32_t w8[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
-  uint32_t mine = 0;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) mine |= delim_bits4(w8[q]) << (4 * q);
-  const uint32_t next = __shfl_down(mine, 1);
-  uint32_t hb = 0;
-  if (lane == 63) {
-    const uint4 hv = *reinterpret_cast<const uint4*>(&buf[UNIT]);
-    const uint4 hw = *reinterpret_cast<const uint4*>(&buf[UNIT + 16]);
-    const uint32_t h8[8] = {hv.x, hv.y, hv.z, hv.w, hw.x, hw.y, hw.z, hw.w};
-#pragma unroll
-    for (int q = 0; q < 8; ++q) hb |= delim_bits4(h8[q]) << (4 * q);
-  }
-  dm = (uint64_t)mine | ((uint64_t)(lane == 63 ? hb : next) << 32);
-  const uint32_t prevd = __shfl_up(mine, 1) >> 31;  // last byte of the lane below
-  const uint32_t carry = lane == 0 ? (is_delim(pv) ? 1u : 0u) : prevd;
+  const uint32_t mine = delim_bits16(p0) | (delim_bits16(p1) << 16);
+  const uint32_t next = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mine, 0x130, 0xF, 0xF, false);  // wave_shl:1
+  const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mine, 0x138, 0xF, 0xF, false);  // wave_shr:1
+  dm = (uint64_t)mine | ((uint64_t)(lane == 63 ? hbits : next) << 32);
+  const uint32_t carry = lane == 0 ? (is_delim(pv) ? 1u : 0u) : (prev >> 31);  // last byte of the lane below
   starts = ~mine & ((mine << 1) | carry);
   const uint64_t lane_base = u0 + pbase;
   if (lane_base >= chunk_len) starts = 0;
@@ -147,7 +154,7 @@ struct SampleLds {
   uint64_t sig[MAP_SLOTS];
   uint64_t side[MAP_SLOTS];
   uint32_t cnt[MAP_SLOTS];
-  uint8_t buf[MAP_WAVES][BUF];
+  alignas(16) uint8_t buf[MAP_WAVES][BUF];
 };
 static_assert(sizeof(SampleLds) <= 160 * 1024, "one sample block per CU");
 
@@ -175,12 +182,16 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs 
     load32(a, u0 + pbase, p0, p1);
     reinterpret_cast<uint4*>(&buf[pbase])[0] = p0;
     reinterpret_cast<uint4*>(&buf[pbase])[1] = p1;
-    if (lane < HALO / 16) *reinterpret_cast<uint4*>(&buf[UNIT + lane * 16]) = load16(a, u0 + UNIT + lane * 16);
+    uint4 h16 = make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
+    if (lane < HALO / 16) {
+      h16 = load16(a, u0 + UNIT + lane * 16);
+      *reinterpret_cast<uint4*>(&buf[UNIT + lane * 16]) = h16;
+    }
     const uint32_t pv = (u0 == 0 && a.prev_byte >= 0) ? (uint32_t)a.prev_byte : a.text[(int64_t)u0 - 1];
     wave_sync();
     uint64_t dm;
     uint32_t bits;
-    unit_masks(p0, p1, buf, pv, u0, pbase, a.chunk_len, dm, bits);
+    unit_masks(p0, p1, halo_bits(h16), pv, u0, pbase, a.chunk_len, dm, bits);
     while (bits) {
       const uint32_t b = __ffs(bits) - 1;
       bits &= bits - 1;
@@ -188,8 +199,9 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs 
       const uint32_t len = rest ? (uint32_t)__ffsll((unsigned long long)rest) - 1 : 64u;
       if (len > KEY_INLINE_MAX) continue;
       const uint32_t p = pbase + b;
-      uint64_t k0, k1, sg;
-      inline_key(tile8(buf, p), tile8(buf, p + 8), len, k0, k1, sg);
+      uint64_t k0, k1, sg, w0, w1;
+      window16(buf, p, w0, w1);
+      inline_key(w0, w1, len, k0, k1, sg);
       const uint64_t sd = two_word(sg) ? k0 : 0ull;
       const uint64_t f = sample_fp(sg, sd);
       uint32_t g = (place_hash(k0, k1) >> 20) & (NG - 1);
@@ -325,8 +337,8 @@ __global__ void __launch_bounds__(1024) wc_hot_place(HotArgs h, int pass) {
       o = atomicAdd(&h.gocc[g2], 1u);
     }
     if (o >= GS) continue;
-    h.img_sig[GS * g + o] = sg;
-    h.img_side[GS * g + o] = sd;
+    h.img_sig[slot_of(g, o)] = sg;
+    h.img_side[slot_of(g, o)] = sd;
   }
 }
 
@@ -338,7 +350,7 @@ struct alignas(16) MapLds {
   uint32_t off[MAP_SLOTS];              // chunk-relative first offset in the block
   uint16_t list[MAP_WAVES][MAP_LIST];
   uint32_t bcur[MAX_REC_BUCKETS];       // records appended to each bucket's sub-region (short | long << 16)
-  uint8_t buf[MAP_WAVES][BUF];
+  alignas(16) uint8_t buf[MAP_WAVES][BUF];
   uint32_t next_unit;
   unsigned long long used, tokens;
 };
@@ -431,14 +443,14 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     reinterpret_cast<uint4*>(&buf[pbase])[0] = p0;
     reinterpret_cast<uint4*>(&buf[pbase])[1] = p1;
     if (lane < HALO / 16) *reinterpret_cast<uint4*>(&buf[UNIT + lane * 16]) = ph16;
-    const uint32_t pv = __shfl(pprev, 0);
+    const uint32_t pv = (uint32_t)__builtin_amdgcn_readlane((int)pprev, 0);
     const uint4 c0 = p0, c1 = p1;
-    wave_sync();
-    prefetch(nu);
+    const uint32_t hb = halo_bits(ph16);
+    prefetch(nu);  // the LDS copy is first read by the steps, behind the list round's wave_sync
     clk.lap(MS_COMMIT);
     uint64_t dm;
     uint32_t bits;
-    unit_masks(c0, c1, buf, pv, u0, pbase, a.chunk_len, dm, bits);
+    unit_masks(c0, c1, hb, pv, u0, pbase, a.chunk_len, dm, bits);
     const uint32_t ntok = __popc(bits);
     my_tokens += ntok;
     uint32_t wave_total;
@@ -464,8 +476,9 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
         const bool h1 = j + lane < round_n, h2 = j + 64 + lane < round_n;
         const uint32_t e1 = h1 ? list[j + lane] : 0u, e2 = h2 ? list[j + 64 + lane] : 0u;
         const uint32_t q1 = e1 & 0x7FFu, q2 = e2 & 0x7FFu, n1 = e1 >> 11, n2 = e2 >> 11;
-        const uint64_t w10 = tile8(buf, q1), w11 = tile8(buf, q1 + 8);
-        const uint64_t w20 = tile8(buf, q2), w21 = tile8(buf, q2 + 8);
+        uint64_t w10, w11, w20, w21;
+        window16(buf, q1, w10, w11);
+        window16(buf, q2, w20, w21);
         if (WC_MAP_ABLATE == 1) {
           sink ^= w10 ^ w21;
           continue;
@@ -483,13 +496,13 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
           sink ^= as ^ bs ^ ga2 ^ gb2;
           continue;
         }
-        const u64x2* S = reinterpret_cast<const u64x2*>(L.sig);
-        const u64x2 xa0 = S[2 * ga1], xa1 = S[2 * ga1 + 1], xa2 = S[2 * ga2], xa3 = S[2 * ga2 + 1];
-        const u64x2 xb0 = S[2 * gb1], xb1 = S[2 * gb1 + 1], xb2 = S[2 * gb2], xb3 = S[2 * gb2 + 1];
+        const u64x2* S = reinterpret_cast<const u64x2*>(L.sig);  // S[g]: slots 0-1, S[NG + g]: slots 2-3
+        const u64x2 xa0 = S[ga1], xa1 = S[NG + ga1], xa2 = S[ga2], xa3 = S[NG + ga2];
+        const u64x2 xb0 = S[gb1], xb1 = S[NG + gb1], xb2 = S[gb2], xb3 = S[NG + gb2];
         const int ma = in1 ? sig_match8(xa0, xa1, xa2, xa3, as) : -1;
         const int mb = in2 ? sig_match8(xb0, xb1, xb2, xb3, bs) : -1;
-        int s1 = ma < 0 ? -1 : (int)(GS * (ma < GS ? ga1 : ga2)) + (ma & (GS - 1));
-        int s2 = mb < 0 ? -1 : (int)(GS * (mb < GS ? gb1 : gb2)) + (mb & (GS - 1));
+        int s1 = ma < 0 ? -1 : (int)slot_of(ma < GS ? ga1 : ga2, ma & (GS - 1));
+        int s2 = mb < 0 ? -1 : (int)slot_of(mb < GS ? gb1 : gb2, mb & (GS - 1));
         // two-word keys: the matching slot's side word decides
         const bool ta = two_word(as), tb = two_word(bs);
         const uint64_t ca = s1 >= 0 && ta ? L.side[s1] : a0, cb = s2 >= 0 && tb ? L.side[s2] : b0;

@@ -37,6 +37,20 @@ __device__ __forceinline__ uint64_t tile8(const uint8_t* tile, uint32_t p) {
   return sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
 }
 
+// Bytes [p, p+8) and [p+8, p+16) of an 8-byte-aligned LDS text buffer from
+// three ALIGNED ds_read_b64 and two funnel shifts (an unaligned 16-byte read
+// stalls the LDS pipe: SQ_LDS_UNALIGNED_STALL was a third of its busy cycles).
+// The buffer must be readable 24 bytes past p & ~7.
+__device__ __forceinline__ void window16(const uint8_t* buf, uint32_t p, uint64_t& w0, uint64_t& w1) {
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(buf + (p & ~7u));
+  const uint64_t d0 = q[0], d1 = q[1], d2 = q[2];
+  const uint32_t sh = (p & 7u) * 8u;
+  // (x << 1) << (63 - sh) == x << (64 - sh) without the undefined shift by 64 at sh = 0
+  // (64-bit shifts measured faster here than a 32-bit v_alignbyte_b32 funnel)
+  w0 = (d0 >> sh) | ((d1 << 1) << (63 - sh));
+  w1 = (d1 >> sh) | ((d2 << 1) << (63 - sh));
+}
+
 // Low n bytes of v (n <= 8).
 __device__ __forceinline__ uint64_t low_bytes(uint64_t v, uint32_t n) {
   return n >= 8 ? v : (v & ((1ull << (8 * n)) - 1ull));
