@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--pool-gb", type=float, default=None, help="host-staged: replay pool per GPU")
     ap.add_argument("--merge", choices=["shuffle", "dense"], default="shuffle",
                     help="cross-GPU merge: shuffle (all-to-all to hash owners) or dense (reduce-scatter + all-gather)")
+    ap.add_argument("--no-oracle", action="store_true",
+                    help="skip the key-for-key check against the generator-walk oracle (sum check only)")
     ap.add_argument("--json-out", default="")
     return ap.parse_args()
 
@@ -60,9 +62,11 @@ def main() -> int:
     import torch
     import torch.distributed as dist
 
+    import resource
+
     from cuda_mapreduce_amd.models import CONFIGS
-    from cuda_mapreduce_amd.ops import Comm, Engine, synth_host
-    import numpy as np
+    from cuda_mapreduce_amd.ops import Comm, Engine, HostPool
+    from cuda_mapreduce_amd.utils import compare_results, synthetic_oracle
 
     cfg = CONFIGS[a.config]
     gib = 1 << 30
@@ -99,19 +103,23 @@ def main() -> int:
     # rank r owns segments [r*nseg, (r+1)*nseg) of the logical stream
     first_seg = rank * (nbytes // seg)
     base = rank * nbytes
+    pool_bytes = 0
+    pool_info = None
     if host_staged:
-        # pinned host pool of whole chunks replayed over PCIe (1 TB config: 128 GiB per GPU)
+        # page-locked host pool of whole chunks replayed over PCIe (1 TB config: 128 GiB per GPU),
+        # generated natively in place on 16 threads (no pageable copy)
         pool_bytes = int((a.pool_gb if a.pool_gb is not None else cfg.pool_bytes / gib) * gib)
         pool_bytes = max(chunk, pool_bytes // chunk * chunk)
-        pool = np.frombuffer(synth_host(pool_bytes, first_segment=first_seg, seed=seed, vocab=vocab, zipf_s=zipf),
-                             np.uint8)
+        pool = HostPool(pool_bytes, first_segment=first_seg, seed=seed, vocab=vocab, zipf_s=zipf, threads=16)
+        pool_info = {"pool_bytes": pool_bytes, "build_s": round(pool.build_seconds, 3),
+                     "peak_rss_bytes": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024}
     else:
         eng.synth_device(nbytes, first_segment=first_seg, seed=seed, vocab=vocab, zipf_s=zipf)
 
     def step():
         eng.reset()
         if host_staged:
-            eng.count_replay_pinned(pool, nbytes, global_base=base)
+            eng.count_pool(pool, nbytes, global_base=base)
         else:
             eng.count_resident(nbytes, global_base=base)
         return eng.finalize_device(comm)
@@ -139,15 +147,28 @@ def main() -> int:
         ms, tokens_total = float(mx[0]), float(sm[1])
     else:
         tokens_total = float(tokens)
-    # Validation (untimed): the merged table's counts must sum to the words the
-    # map kernels counted — catches lost or duplicated counts in any stage.
+    # Validation (untimed): the merged table must equal, key for key (words,
+    # first-occurrence order, counts, first offsets, total), the exact table of
+    # the whole logical stream computed on the CPU from the synthetic
+    # generator's own word walk — independent of every GPU stage and of any
+    # tokenizer; and its counts must sum to the words the map kernels counted.
     res = eng.result(comm)
     valid = True
+    check = {}
     if rank == 0:
         valid = int(res.total) == int(tokens_total) and int(res.counts.sum()) == int(tokens_total)
         if not valid:
             print(f"bench: VALIDATION FAILED: table total {int(res.total)} (rows sum {int(res.counts.sum())}) "
                   f"!= tokens {int(tokens_total)}", file=sys.stderr, flush=True)
+        if not a.no_oracle:
+            t1 = time.perf_counter()
+            want = synthetic_oracle(world, nbytes, seed, vocab, zipf, pool_bytes=pool_bytes, chunk=chunk)
+            diff = compare_results(res, want)
+            check = {"oracle": "generator word walk (cpu_count_synth)", "identical": not diff,
+                     "seconds": round(time.perf_counter() - t1, 2)}
+            if diff:
+                valid = False
+                print(f"bench: VALIDATION FAILED vs oracle: {diff}", file=sys.stderr, flush=True)
     total_bytes = nbytes * world
     gbps = total_bytes / (ms / 1e3) / 1e9
     words = tokens_total / (ms / 1e3)
@@ -168,6 +189,7 @@ def main() -> int:
                      f"Zipf({zipf}) text, {vocab}-word vocabulary, seed {seed})"),
             "words_per_s": round(words, 1),
             "validated": valid,
+            "validation": check or {"oracle": "skipped (--no-oracle): token-sum check only"},
             "distinct_words": keys,
             "config": {
                 "model": f"wordcount-mapreduce/{cfg.name}",
@@ -180,6 +202,8 @@ def main() -> int:
             },
             "stages": st,
         }
+        if pool_info:
+            out["host_pool"] = pool_info
         line = json.dumps(out)
         print(line, flush=True)
         if a.json_out:

@@ -10,7 +10,6 @@ Layout:
   models/    job definitions: the BASELINE word-count configurations
   parallel/  one-process-per-GPU driver: torch.distributed rendezvous, RCCL
              communicator, shard ownership, host (gloo) merge for CPU runs
-  utils/     sizes, synthetic corpora, timing helpers
 """
 from .ops import Engine, Result, cpu_count, cpu_count_compat, format_output, synth_host  # noqa: F401
 

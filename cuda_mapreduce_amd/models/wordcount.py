@@ -12,8 +12,6 @@ import time
 from dataclasses import dataclass, field
 from typing import Optional
 
-import numpy as np
-
 GiB = 1 << 30
 SEG = 1024  # synthetic segment size (src/kernels/synth.hpp)
 
@@ -68,7 +66,7 @@ class JobResult:
 def run_job(cfg: JobConfig, rank: int = 0, world: int = 1, local_rank: int = 0, comm=None, engine=None) -> JobResult:
     """Run one configuration on this rank.  Synthetic shards are segment-aligned
     slices of ONE logical stream, so results are independent of `world`."""
-    from ..ops import Engine, cpu_count, synth_host
+    from ..ops import Engine, HostPool, cpu_count
 
     if cfg.source == "cpu":
         data = open(cfg.path, "rb").read()
@@ -88,11 +86,10 @@ def run_job(cfg: JobConfig, rank: int = 0, world: int = 1, local_rank: int = 0, 
             t0 = time.perf_counter()
             eng.count_resident(nbytes, global_base=base)
         elif cfg.source == "host-staged":
-            pool_bytes = min(cfg.pool_bytes, nbytes) // SEG * SEG
-            pool = np.frombuffer(synth_host(pool_bytes, first_segment=first_seg, seed=cfg.seed, vocab=cfg.vocab,
-                                            zipf_s=cfg.zipf_s), np.uint8)
+            pool_bytes = max(cfg.chunk_bytes, min(cfg.pool_bytes, nbytes) // cfg.chunk_bytes * cfg.chunk_bytes)
+            pool = HostPool(pool_bytes, first_segment=first_seg, seed=cfg.seed, vocab=cfg.vocab, zipf_s=cfg.zipf_s)
             t0 = time.perf_counter()
-            eng.count_replay(pool, nbytes, global_base=base)
+            eng.count_pool(pool, nbytes, global_base=base)
         else:
             raise ValueError(f"unknown source {cfg.source}")
         distinct = eng.finalize_device(comm)

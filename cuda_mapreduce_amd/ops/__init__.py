@@ -2,8 +2,10 @@
 from .engine import (  # noqa: F401
     Comm,
     Engine,
+    HostPool,
     Result,
     cpu_count,
+    cpu_count_synth,
     cpu_count_compat,
     cpu_count_file_checkpointed,
     default_options,
@@ -13,5 +15,6 @@ from .engine import (  # noqa: F401
     shard_range,
     shard_range_file,
     synth_host,
+    synth_host_array,
 )
 from ._lib import LIB_PATH, WcError  # noqa: F401

@@ -78,6 +78,12 @@ def _load() -> ctypes.CDLL:
         "wc_cpu_count": (c_void_p, [P8, c_uint64, c_uint64]),
         "wc_cpu_count_compat": (c_void_p, [P8, c_uint64]),
         "wc_synth_host": (c_int, [P8, c_uint64, c_uint64, c_uint64, c_uint32, c_double]),
+        "wc_synth_host_mt": (c_int, [P8, c_uint64, c_uint64, c_uint64, c_uint32, c_double, c_int]),
+        "wc_cpu_count_synth": (c_void_p, [c_uint64, c_uint64, c_uint64, c_uint32, c_double, c_uint64, c_int]),
+        "wc_pool_create": (c_void_p, [c_uint64, c_uint64, c_uint64, c_uint32, c_double, c_int]),
+        "wc_pool_destroy": (None, [c_void_p]),
+        "wc_pool_build_seconds": (c_double, [c_void_p]),
+        "wc_count_pool": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64]),
         "wc_shard_range_mem": (c_int, [P8, c_uint64, c_int, c_int, P64, P64]),
         "wc_shard_range_file": (c_int, [c_char_p, c_int, c_int, P64, P64]),
         "wc_rccl_unique_id": (c_int, [POINTER(c_char)]),

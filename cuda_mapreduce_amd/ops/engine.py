@@ -172,6 +172,10 @@ class Engine:
         self._pool = keep  # must stay alive (and registered) while the engine uses it
         check(lib.wc_count_pinned_replay(self._p, ptr, len(keep), total, global_base))
 
+    def count_pool(self, pool: "HostPool", total: int, global_base: int = 0) -> None:
+        """Host-staged path from a native page-locked pool (HostPool): no registration, no copies."""
+        check(lib.wc_count_pool(self._p, pool._p, total, global_base))
+
     def synth_device(self, nbytes: int, first_segment: int = 0, seed: int = 1, vocab: int = 100000, zipf_s: float = 1.0) -> None:
         """Generate synthetic text directly in HBM (no host/PCIe involvement)."""
         check(lib.wc_synth_device(self._p, nbytes, first_segment, seed, vocab, zipf_s))
@@ -222,11 +226,44 @@ def cpu_count_compat(data: bytes) -> Result:
     return Result._from_native(check_ptr(lib.wc_cpu_count_compat(ptr, len(keep))))
 
 
-def synth_host(nbytes: int, first_segment: int = 0, seed: int = 1, vocab: int = 100000, zipf_s: float = 1.0) -> bytes:
+def synth_host(nbytes: int, first_segment: int = 0, seed: int = 1, vocab: int = 100000, zipf_s: float = 1.0,
+               threads: int = 1) -> bytes:
     """Host copy of the synthetic stream (bit-identical to the device generator)."""
-    out = np.zeros(nbytes, np.uint8)
-    check(lib.wc_synth_host(out.ctypes.data_as(_P8), nbytes, first_segment, seed, vocab, zipf_s))
-    return out.tobytes()
+    return synth_host_array(nbytes, first_segment, seed, vocab, zipf_s, threads).tobytes()
+
+
+def synth_host_array(nbytes: int, first_segment: int = 0, seed: int = 1, vocab: int = 100000, zipf_s: float = 1.0,
+                     threads: int = 8) -> np.ndarray:
+    """The synthetic stream generated in place into a numpy array on `threads` threads."""
+    out = np.empty(nbytes, np.uint8)
+    check(lib.wc_synth_host_mt(out.ctypes.data_as(_P8), nbytes, first_segment, seed, vocab, zipf_s, threads))
+    return out
+
+
+def cpu_count_synth(nbytes: int, first_segment: int = 0, seed: int = 1, vocab: int = 100000, zipf_s: float = 1.0,
+                    global_base: int = 0, threads: int = 0) -> Result:
+    """Exact counts of the synthetic stream from the generator's own word walk (full-scale
+    benchmark oracle): independent of every tokenizer."""
+    return Result._from_native(check_ptr(lib.wc_cpu_count_synth(nbytes, first_segment, seed, vocab, zipf_s,
+                                                                 global_base, threads)))
+
+
+class HostPool:
+    """Page-locked synthetic replay pool (host-staged configs), generated in place natively."""
+
+    def __init__(self, nbytes: int, first_segment: int = 0, seed: int = 1, vocab: int = 100000,
+                 zipf_s: float = 1.0, threads: int = 16):
+        self._p = check_ptr(lib.wc_pool_create(nbytes, first_segment, seed, vocab, zipf_s, threads))
+        self.nbytes = nbytes
+        self.build_seconds = float(lib.wc_pool_build_seconds(self._p))
+
+    def close(self) -> None:
+        if getattr(self, "_p", None):
+            lib.wc_pool_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        self.close()
 
 
 def shard_range(data: bytes, rank: int, world: int):

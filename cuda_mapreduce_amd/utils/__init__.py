@@ -1,2 +1,2 @@
-"""Small helpers: size parsing and formatting."""
-from .sizes import fmt_bytes, parse_size  # noqa: F401
+"""Helpers shared by the Python entry points (bench.py, tests)."""
+from .validate import compare_results, merge_results, synthetic_oracle  # noqa: F401

@@ -52,6 +52,12 @@ int wc_result_merge(wc_result* dst, const wc_result* src);
 int wc_count_replay(wc_engine* e, const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t global_base);
 /* Host-staged benchmark path: pool page-locked once, chunks DMA'd directly. */
 int wc_count_pinned_replay(wc_engine* e, const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t global_base);
+/* Page-locked synthetic replay pool generated in place on `threads` threads (host-staged config). */
+typedef struct wc_pool wc_pool;
+wc_pool* wc_pool_create(uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double zipf_s, int threads);
+void wc_pool_destroy(wc_pool* p);
+double wc_pool_build_seconds(const wc_pool* p);
+int wc_count_pool(wc_engine* e, const wc_pool* p, uint64_t total, uint64_t global_base);
 /* Generate synthetic text into the engine's device text buffer ... */
 int wc_synth_device(wc_engine* e, uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double zipf_s);
 /* ... and count [0, n) of it. */
@@ -76,7 +82,14 @@ void wc_free(void* p);
 /* CPU paths */
 wc_result* wc_cpu_count(const uint8_t* text, uint64_t n, uint64_t global_base);
 wc_result* wc_cpu_count_compat(const uint8_t* text, uint64_t n);
+/* Exact counts of n bytes of the synthetic stream from segment first_segment (offsets from
+   global_base), computed from the generator's word walk on `threads` CPU threads (0 = all). */
+wc_result* wc_cpu_count_synth(uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double zipf_s,
+                              uint64_t global_base, int threads);
 int wc_synth_host(uint8_t* out, uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double zipf_s);
+/* The same on `threads` threads, written in place. */
+int wc_synth_host_mt(uint8_t* out, uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double zipf_s,
+                     int threads);
 int wc_shard_range_mem(const uint8_t* text, uint64_t n, int rank, int world, uint64_t* begin, uint64_t* end);
 int wc_shard_range_file(const char* path, int rank, int world, uint64_t* begin, uint64_t* end);
 

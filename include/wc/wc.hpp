@@ -98,7 +98,9 @@ class Engine {
   // Host-staged benchmark path: `total` bytes replayed from a host pool of
   // whole chunks (each ending with a delimiter), page-locked once and DMA'd
   // straight into HBM with H2D of chunk k+1 overlapping compute of chunk k.
-  void count_pinned_replay(const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t global_base);
+  // `pinned`: the pool is already page-locked (hipHostMalloc, e.g. a HostPool).
+  void count_pinned_replay(const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t global_base,
+                           bool pinned = false);
 
   // Device-resident synthetic text: allocates (or reuses) a buffer of n bytes
   // holding segments [first_segment, ...) of the spec's stream.
@@ -122,10 +124,34 @@ class Engine {
 namespace cpu {
 // Single-thread oracle (BASELINE config 1): hash map keyed by the word bytes.
 KeyTable count(const uint8_t* text, uint64_t n, uint64_t global_base = 0);
+// Exact counts of n bytes of the synthetic stream starting at segment
+// `first_segment`, offsets from global_base; `threads` workers (0 = all):
+// the full-scale benchmark oracle (words come from the generator's own walk).
+KeyTable count_synth(uint64_t n, uint64_t first_segment, const SynthSpec& spec, uint64_t global_base, int threads);
 // The reference program's exact quirks (prefix compare, 99-byte fgets records,
 // blank line stops input, ...) for differential tests.
-KeyTable count_reference_compat(const uint8_t* text, uint64_t n);
+// `echo` (optional) receives what the reference echoes: every record it reads,
+// up to and including the short record that ends its input.
+KeyTable count_reference_compat(const uint8_t* text, uint64_t n, std::string* echo = nullptr);
 }  // namespace cpu
+
+// Page-locked host buffer holding a synthetic replay pool (host-staged
+// benchmark config): generated in place by `threads` threads, no pageable copy.
+class HostPool {
+ public:
+  HostPool(uint64_t n, uint64_t first_segment, const SynthSpec& spec, int threads);
+  ~HostPool();
+  HostPool(const HostPool&) = delete;
+  HostPool& operator=(const HostPool&) = delete;
+  const uint8_t* data() const { return p_; }
+  uint64_t size() const { return n_; }
+  double build_seconds() const { return secs_; }
+
+ private:
+  uint8_t* p_ = nullptr;
+  uint64_t n_ = 0;
+  double secs_ = 0;
+};
 
 // Host copy of the synthetic stream (bit-identical to the device generator).
 std::vector<uint8_t> synth_host(uint64_t n, uint64_t first_segment, const SynthSpec& spec);

@@ -2,12 +2,14 @@
 #include <cstdlib>
 #include <cstring>
 #include <exception>
+#include <memory>
 #include <thread>
 
 #include "common/hip_util.hpp"
 #include "dist/comm.hpp"
 #include "io/checkpoint.hpp"
 #include "io/source.hpp"
+#include "io/synth_host.hpp"
 #include "kernels/kernels.hpp"
 #include "wc/wc.h"
 #include "wc/wc.hpp"
@@ -147,7 +149,7 @@ wc_result* wc_count_file_checkpointed(wc_engine* e, const char* path, uint64_t b
   const int rc = guard([&] {
     const std::string file(path), base(ckpt ? ckpt : "");
     const std::string cpath = base.empty() ? std::string() : wc::checkpoint_path(base, rank, world);
-    wc::Checkpoint k = wc::open_checkpoint(cpath, resume != 0 && !cpath.empty(), wc::file_size(file), begin, end,
+    wc::Checkpoint k = wc::open_checkpoint(cpath, resume != 0 && !cpath.empty(), file, wc::file_size(file), begin, end,
                                            rank, world);
     wc::run_checkpointed(file, k, interval, cpath, [&](const uint8_t* q, uint64_t n, uint64_t gbase) {
       if (!e) return wc::cpu::count(q, n, gbase);
@@ -276,11 +278,44 @@ wc_result* wc_cpu_count_compat(const uint8_t* text, uint64_t n) {
   return r;
 }
 
+wc_result* wc_cpu_count_synth(uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double zs,
+                              uint64_t base, int threads) {
+  wc_result* r = new wc_result;
+  if (guard([&] { r->t = wc::cpu::count_synth(n, first_segment, spec_of(seed, vocab, zs), base, threads); }) != 0) {
+    delete r;
+    return nullptr;
+  }
+  return r;
+}
+
 int wc_synth_host(uint8_t* out, uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double s) {
+  return wc_synth_host_mt(out, n, first_segment, seed, vocab, s, 1);
+}
+
+int wc_synth_host_mt(uint8_t* out, uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double s,
+                     int threads) {
   return guard([&] {
-    const std::vector<uint8_t> v = wc::synth_host(n, first_segment, spec_of(seed, vocab, s));
-    std::memcpy(out, v.data(), n);
+    const wc::SynthSpec sp = spec_of(seed, vocab, s);
+    wc::synth_host_into(out, n, first_segment, sp, wc::build_vocab(sp), threads);
   });
+}
+
+struct wc_pool {
+  std::unique_ptr<wc::HostPool> p;
+};
+
+wc_pool* wc_pool_create(uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double s, int threads) {
+  wc_pool* r = new wc_pool;
+  if (guard([&] { r->p.reset(new wc::HostPool(n, first_segment, spec_of(seed, vocab, s), threads)); }) != 0) {
+    delete r;
+    return nullptr;
+  }
+  return r;
+}
+void wc_pool_destroy(wc_pool* p) { delete p; }
+double wc_pool_build_seconds(const wc_pool* p) { return p ? p->p->build_seconds() : 0.0; }
+int wc_count_pool(wc_engine* e, const wc_pool* p, uint64_t total, uint64_t base) {
+  return guard([&] { e->e->count_pinned_replay(p->p->data(), p->p->size(), total, base, true); });
 }
 
 int wc_shard_range_mem(const uint8_t* text, uint64_t n, int rank, int world, uint64_t* begin, uint64_t* end) {

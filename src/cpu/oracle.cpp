@@ -58,7 +58,7 @@ KeyTable count(const uint8_t* text, uint64_t n, uint64_t global_base) {
   return t;
 }
 
-KeyTable count_reference_compat(const uint8_t* text, uint64_t n) {
+KeyTable count_reference_compat(const uint8_t* text, uint64_t n, std::string* echo) {
   // Split into fgets-style records of at most 99 bytes (a record ends after '\n').
   std::vector<std::string> tokens;
   uint64_t i = 0;
@@ -70,6 +70,7 @@ KeyTable count_reference_compat(const uint8_t* text, uint64_t n) {
     i = e;
     const size_t nul = rec.find('\0');  // strlen semantics
     if (nul != std::string::npos) rec.resize(nul);
+    if (echo) echo->append(rec);  // printf("%s") of the record precedes the strlen < 2 check (main.cu:180-186)
     if (rec.size() < 2) break;
     std::string cur;
     for (char c : rec) {

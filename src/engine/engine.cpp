@@ -507,7 +507,8 @@ void Engine::count_source(ChunkSource& src, uint64_t global_base) {
   im.st.map_reduce_ms += (now_seconds() - t0) * 1e3;
 }
 
-void Engine::count_pinned_replay(const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t global_base) {
+void Engine::count_pinned_replay(const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t global_base,
+                                 bool pinned) {
   Impl& im = *p_;
   WC_HIP_CHECK(hipSetDevice(im.dev));
   Range r("wc_count_pinned_replay");
@@ -517,7 +518,7 @@ void Engine::count_pinned_replay(const uint8_t* pool, uint64_t pool_bytes, uint6
   for (uint64_t c = C; c <= pool_bytes; c += C)
     WC_CHECK(is_delim(pool[c - 1]), "every replay chunk must end with a delimiter");
   // Page-lock the caller's pool once: chunks are DMA'd straight from it.
-  if (im.registered != pool) {
+  if (!pinned && im.registered != pool) {
     if (im.registered) (void)hipHostUnregister(const_cast<uint8_t*>(im.registered));
     im.registered = nullptr;
     WC_HIP_CHECK(hipHostRegister(const_cast<uint8_t*>(pool), pool_bytes, hipHostRegisterDefault));
@@ -609,4 +610,16 @@ KeyTable Engine::result(Comm* comm, bool all_ranks) {
   return im.download_cols();
 }
 
+}  // namespace wc
+
+namespace wc {
+HostPool::HostPool(uint64_t n, uint64_t first_segment, const SynthSpec& spec, int threads) : n_(n) {
+  const double t0 = now_seconds();
+  WC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_), std::max<uint64_t>(n, 1), hipHostMallocDefault));
+  synth_host_into(p_, n, first_segment, spec, build_vocab(spec), threads);
+  secs_ = now_seconds() - t0;
+}
+HostPool::~HostPool() {
+  if (p_) (void)hipHostFree(p_);
+}
 }  // namespace wc

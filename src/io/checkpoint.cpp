@@ -115,7 +115,7 @@ bool checkpoint_exists(const std::string& path) {
 void save_checkpoint(const std::string& path, const Checkpoint& c) {
   Writer w;
   w.buf.append(kMagic, sizeof(kMagic));
-  w.put<uint32_t>(1);  // format version
+  w.put<uint32_t>(2);  // format version (2: + prefix fingerprint)
   w.put(c.rank);
   w.put(c.world);
   w.put(c.intervals);
@@ -123,6 +123,7 @@ void save_checkpoint(const std::string& path, const Checkpoint& c) {
   w.put(c.begin);
   w.put(c.end);
   w.put(c.next);
+  w.put(c.prefix_fp);
   w.put(c.table.total);
   w.put<uint64_t>(c.table.size());
   for (size_t i = 0; i < c.table.size(); ++i) {
@@ -169,7 +170,8 @@ Checkpoint load_checkpoint(const std::string& path) {
   if (f.h != want) fail("checkpoint checksum mismatch (corrupt file): " + path);
   const std::string body = buf.substr(0, buf.size() - 8);
   Reader r{body, sizeof(kMagic)};
-  if (r.get<uint32_t>() != 1) fail("unsupported checkpoint version: " + path);
+  const uint32_t version = r.get<uint32_t>();
+  if (version != 1 && version != 2) fail("unsupported checkpoint version: " + path);
   Checkpoint c;
   c.rank = r.get<uint32_t>();
   c.world = r.get<uint32_t>();
@@ -178,6 +180,7 @@ Checkpoint load_checkpoint(const std::string& path) {
   c.begin = r.get<uint64_t>();
   c.end = r.get<uint64_t>();
   c.next = r.get<uint64_t>();
+  c.prefix_fp = version >= 2 ? r.get<uint64_t>() : 0;  // 0: not recorded (version 1)
   c.table.total = r.get<uint64_t>();
   const uint64_t rows = r.get<uint64_t>();
   if (c.next < c.begin || c.next > c.end) fail("checkpoint offsets inconsistent: " + path);
@@ -194,13 +197,43 @@ Checkpoint load_checkpoint(const std::string& path) {
   return c;
 }
 
-Checkpoint open_checkpoint(const std::string& path, bool resume, uint64_t input_size, uint64_t begin, uint64_t end,
-                           int rank, int world) {
+uint64_t prefix_fingerprint(int fd, uint64_t begin, uint64_t next, const std::string& file) {
+  Fnv f;
+  const uint64_t n = next - begin;
+  uint8_t b[4096];
+  for (uint64_t i = 0; i < 256 && n >= 32; ++i) {
+    const uint64_t off = begin + (n - 32) * i / 255;
+    pread_all(fd, b, 32, off, file);
+    f.add(reinterpret_cast<const char*>(b), 32);
+  }
+  const uint64_t tail = std::min<uint64_t>(n, sizeof(b));
+  if (tail) {
+    pread_all(fd, b, tail, next - tail, file);
+    f.add(reinterpret_cast<const char*>(b), tail);
+  }
+  return f.h;
+}
+
+Checkpoint open_checkpoint(const std::string& path, bool resume, const std::string& file, uint64_t input_size,
+                           uint64_t begin, uint64_t end, int rank, int world) {
   if (resume && checkpoint_exists(path)) {
     Checkpoint k = load_checkpoint(path);
     if (k.input_size != input_size || k.begin != begin || k.end != end || k.rank != (uint32_t)rank ||
         k.world != (uint32_t)world)
       fail("checkpoint " + path + " was written for another input or GPU count");
+    if (k.prefix_fp) {
+      const int fd = ::open(file.c_str(), O_RDONLY);
+      if (fd < 0) fail("cannot open " + file);
+      uint64_t fp = 0;
+      try {
+        fp = prefix_fingerprint(fd, k.begin, k.next, file);
+      } catch (...) {
+        ::close(fd);
+        throw;
+      }
+      ::close(fd);
+      if (fp != k.prefix_fp) fail("checkpoint " + path + ": the counted part of " + file + " changed since it was written");
+    }
     std::fprintf(stderr, "wordcount: rank %d resumes at byte %llu of [%llu, %llu) (%u interval(s) done)\n", rank,
                  (unsigned long long)k.next, (unsigned long long)k.begin, (unsigned long long)k.end, k.intervals);
     return k;
@@ -246,6 +279,7 @@ void run_checkpointed(const std::string& file, Checkpoint& c, uint64_t interval,
       merge_tables(c.table, count_interval(buf.data(), len, c.next));
       c.next += len;
       c.intervals++;
+      if (!path.empty()) c.prefix_fp = prefix_fingerprint(fd, c.begin, c.next, file);
       if (!path.empty()) {
         save_checkpoint(path, c);
         WC_LOG(LOG_INFO, "checkpoint %s: rank %u interval %u, next byte %llu of %llu, %zu keys", path.c_str(), c.rank,

@@ -26,8 +26,14 @@ struct Checkpoint {
   uint64_t next = 0;            // first byte not yet counted (begin <= next <= end)
   uint32_t rank = 0, world = 1;
   uint32_t intervals = 0;       // intervals counted so far
+  uint64_t prefix_fp = 0;       // fingerprint of the counted bytes [begin, next) (prefix_fingerprint)
   KeyTable table;               // running table, first-occurrence order
 };
+
+// Fingerprint of the bytes [begin, next) of an open input: FNV-1a-64 over 256
+// evenly spaced 32-byte samples and the last 4 KiB before `next`.  A resume
+// re-reads them, so an input modified in place (same size) is refused.
+uint64_t prefix_fingerprint(int fd, uint64_t begin, uint64_t next, const std::string& file);
 
 // Fold `add` into `acc`: counts add, first_off takes the min, rows stay in
 // first-occurrence order (the output contract, main.cu:208-218).
@@ -43,11 +49,12 @@ bool checkpoint_exists(const std::string& path);
 // Per-rank file name: "<base>" for world 1, "<base>.r<rank>of<world>" otherwise.
 std::string checkpoint_path(const std::string& base, int rank, int world);
 
-// Rank `rank` of `world` over [begin, end) of an input of `input_size` bytes:
-// the checkpoint at `path` when `resume` and it exists (validated against the
-// input size, range, rank and world; throws otherwise), else a fresh one.
-Checkpoint open_checkpoint(const std::string& path, bool resume, uint64_t input_size, uint64_t begin, uint64_t end,
-                           int rank, int world);
+// Rank `rank` of `world` over [begin, end) of `file` (input_size bytes): the
+// checkpoint at `path` when `resume` and it exists (validated against the input
+// size, range, rank, world and the fingerprint of the counted prefix; throws
+// otherwise), else a fresh one.
+Checkpoint open_checkpoint(const std::string& path, bool resume, const std::string& file, uint64_t input_size,
+                           uint64_t begin, uint64_t end, int rank, int world);
 
 // Counts [c.begin, c.end) of `file` in delimiter-aligned intervals of about
 // `interval` bytes, starting at c.next (resume) and folding into c.table.

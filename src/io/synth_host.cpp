@@ -2,7 +2,9 @@
 // the host copy of the generator (bit-identical to wc_synth_text).
 #include "synth_host.hpp"
 
+#include <algorithm>
 #include <cmath>
+#include <thread>
 #include <unordered_set>
 
 #include "../kernels/synth.hpp"
@@ -65,24 +67,33 @@ SynthVocab HostVocab::view() const {
   return s;
 }
 
-void synth_host_into(uint8_t* out, uint64_t n, uint64_t first_segment, const SynthSpec& spec, const HostVocab& v) {
+void synth_host_into(uint8_t* out, uint64_t n, uint64_t first_segment, const SynthSpec& spec, const HostVocab& v,
+                     int threads) {
   const SynthVocab sv = v.view();
-  uint8_t seg[SYNTH_SEG];
   const uint64_t nseg = (n + SYNTH_SEG - 1) / SYNTH_SEG;
-  for (uint64_t s = 0; s < nseg; ++s) {
-    const uint64_t base = s * SYNTH_SEG;
-    if (base + SYNTH_SEG <= n) {
-      synth_segment(first_segment + s, spec.seed, sv, out + base);
-    } else {
-      synth_segment(first_segment + s, spec.seed, sv, seg);
-      for (uint64_t i = 0; base + i < n; ++i) out[base + i] = seg[i];
+  // segments are independent: T threads write disjoint ranges of `out`
+  const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>(threads > 0 ? (uint64_t)threads : 1, nseg / 64 + 1));
+  auto work = [&](uint64_t s0, uint64_t s1) {
+    uint8_t seg[SYNTH_SEG];
+    for (uint64_t s = s0; s < s1; ++s) {
+      const uint64_t base = s * SYNTH_SEG;
+      if (base + SYNTH_SEG <= n) {
+        synth_segment(first_segment + s, spec.seed, sv, out + base);
+      } else {
+        synth_segment(first_segment + s, spec.seed, sv, seg);
+        for (uint64_t i = 0; base + i < n; ++i) out[base + i] = seg[i];
+      }
     }
-  }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; ++t) th.emplace_back(work, nseg * t / T, nseg * (t + 1) / T);
+  work(0, nseg / T);
+  for (auto& x : th) x.join();
 }
 
 std::vector<uint8_t> synth_host(uint64_t n, uint64_t first_segment, const SynthSpec& spec) {
   std::vector<uint8_t> out(n);
-  synth_host_into(out.data(), n, first_segment, spec, build_vocab(spec));
+  synth_host_into(out.data(), n, first_segment, spec, build_vocab(spec), 1);
   return out;
 }
 

@@ -18,6 +18,8 @@ struct HostVocab {
 };
 
 HostVocab build_vocab(const SynthSpec& spec);
-void synth_host_into(uint8_t* out, uint64_t n, uint64_t first_segment, const SynthSpec& spec, const HostVocab& v);
+// n bytes of the stream from segment first_segment into out, on `threads` threads.
+void synth_host_into(uint8_t* out, uint64_t n, uint64_t first_segment, const SynthSpec& spec, const HostVocab& v,
+                     int threads = 1);
 
 }  // namespace wc

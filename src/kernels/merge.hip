@@ -45,29 +45,29 @@ __global__ void wc_union_flags(const uint32_t* pos, const uint64_t* K0, const ui
                                uint32_t* flag, uint32_t* rep, uint64_t m) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t p = pos[i];
-    const bool valid = K1[p] != K1_EMPTY;
+    const uint64_t k0 = K0[p], k1 = K1[p];
+    const bool valid = k1 != K1_EMPTY;
     bool head = valid;
-    uint32_t r = (uint32_t)i;
-    if (valid && i > 0) {
-      const uint32_t q = pos[i - 1];
-      head = !(K0[q] == K0[p] && K1[q] == K1[p]);
-      if (!head && key_is_hashed(K1[p])) {
-        // walk back to the run start; the earliest entry with equal bytes is the representative
-        uint64_t j = i;
-        while (j > 0 && K0[pos[j - 1]] == K0[p] && K1[pos[j - 1]] == K1[p]) --j;
-        head = true;
-        for (uint64_t t = j; t < i; ++t) {
+    uint64_t r = i;
+    if (valid && i > 0 && K0[pos[i - 1]] == k0 && K1[pos[i - 1]] == k1) {
+      if (!key_is_hashed(k1)) {
+        head = false;
+      } else {  // walk back over the (k0, k1) run; the earliest entry with equal bytes represents it
+        const uint32_t len = ub.SL[p];
+        const uint8_t* mine = ub.at(p);
+        uint64_t found = i;
+        for (uint64_t t = i; t > 0;) {
+          --t;
           const uint32_t pt = pos[t];
-          if (ub.SL[pt] == ub.SL[p] && mem_equal(ub.at(pt), ub.at(p), ub.SL[p])) {
-            head = false;
-            r = (uint32_t)t;
-            break;
-          }
+          if (K0[pt] != k0 || K1[pt] != k1) break;
+          if (ub.SL[pt] == len && mem_equal(ub.at(pt), mine, len)) found = t;
         }
+        head = found == i;
+        r = found;
       }
     }
     flag[i] = head ? 1u : 0u;
-    rep[i] = r;
+    rep[i] = (uint32_t)r;
   }
 }
 

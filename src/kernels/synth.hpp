@@ -24,8 +24,11 @@ WC_HD uint64_t splitmix64(uint64_t& s) {
   return z ^ (z >> 31);
 }
 
-// Writes exactly SYNTH_SEG bytes to out.
-WC_HD void synth_segment(uint64_t seg, uint64_t seed, const SynthVocab& v, uint8_t* out) {
+// Walks segment `seg`: calls word(rank, pos) for every word placed at byte
+// `pos` of the segment (delimiters between words are one byte: ' ' or '\n'),
+// and returns the number of bytes used (the rest is '\n' padding).
+template <class Word>
+WC_HD uint32_t synth_walk(uint64_t seg, uint64_t seed, const SynthVocab& v, Word&& word) {
   uint64_t st = seed ^ fmix64(seg + 0x632BE59BD9B4E019ull);
   uint32_t pos = 0, in_line = 0;
   uint32_t line_words = 8 + (uint32_t)(splitmix64(st) % 12);
@@ -40,17 +43,25 @@ WC_HD void synth_segment(uint64_t seg, uint64_t seed, const SynthVocab& v, uint8
     }
     const uint32_t len = v.len[lo];
     if (pos + len + 1 > SYNTH_SEG) break;
-    const uint8_t* w = v.bytes + v.off[lo];
-    for (uint32_t i = 0; i < len; ++i) out[pos + i] = w[i];
-    pos += len;
-    if (++in_line >= line_words) {
-      out[pos++] = '\n';
+    const bool nl = ++in_line >= line_words;
+    word(lo, pos, nl);
+    pos += len + 1;
+    if (nl) {
       in_line = 0;
       line_words = 8 + (uint32_t)((r >> 40) % 12);
-    } else {
-      out[pos++] = ' ';
     }
   }
+  return pos;
+}
+
+// Writes exactly SYNTH_SEG bytes to out.
+WC_HD void synth_segment(uint64_t seg, uint64_t seed, const SynthVocab& v, uint8_t* out) {
+  uint32_t pos = synth_walk(seg, seed, v, [&](uint32_t w, uint32_t p, bool nl) {
+    const uint8_t* src = v.bytes + v.off[w];
+    const uint32_t len = v.len[w];
+    for (uint32_t i = 0; i < len; ++i) out[p + i] = src[i];
+    out[p + len] = nl ? '\n' : ' ';
+  });
   while (pos < SYNTH_SEG) out[pos++] = '\n';
 }
 

@@ -95,9 +95,10 @@ def test_checkpoint_layout(tmp_path):
     assert r.returncode == 0
     raw = (tmp_path / "ck.bin").read_bytes()
     ver, rank, world, intervals = struct.unpack_from("<4I", raw, 8)
-    size, begin, end, nxt, total, rows = struct.unpack_from("<6Q", raw, 24)
-    assert (ver, rank, world, intervals) == (1, 0, 1, 1)
+    size, begin, end, nxt, fp, total, rows = struct.unpack_from("<7Q", raw, 24)
+    assert (ver, rank, world, intervals) == (2, 0, 1, 1)
     assert (size, begin, end, nxt) == (len(data), 0, len(data), len(data))
+    assert fp != 0  # prefix fingerprint of the counted bytes
     assert total == len(data.split()) and rows == len(set(data.split()))
     assert not os.path.exists(tmp_path / "ck.bin.tmp")
 
@@ -177,3 +178,23 @@ def test_gpu_checkpointed_long_words(tmp_path):
     b = run(["t.txt", "--no-echo", "--checkpoint", "c", "--checkpoint-every", "4096"], tmp_path)
     assert b.returncode == 0, b.stderr
     assert a.stdout == b.stdout
+
+
+def test_resume_refuses_input_modified_in_place(tmp_path):
+    """Same size, different bytes in the already-counted prefix: the checkpoint's
+    prefix fingerprint no longer matches, so --resume refuses instead of mixing
+    stale and new counts."""
+    data = make_text(tmp_path / "t.txt", n=6000)
+    ck = ["--cpu", "--no-echo", "--checkpoint", "ck.bin", "--checkpoint-every", "4000"]
+    assert run(["t.txt"] + ck, tmp_path, {"WC_CKPT_STOP_AFTER": "2"}).returncode == 1
+    # flip one word near the start (same length, delimiters untouched)
+    i = data.index(b"w")
+    mod = bytearray(data)
+    mod[i] = ord(b"x")
+    (tmp_path / "t.txt").write_bytes(bytes(mod))
+    r = run(["t.txt"] + ck + ["--resume"], tmp_path)
+    assert r.returncode != 0 and b"changed since it was written" in r.stderr
+    # the untouched file resumes fine
+    (tmp_path / "t.txt").write_bytes(data)
+    r = run(["t.txt"] + ck + ["--resume"], tmp_path)
+    assert r.returncode == 0 and b"resumes at byte" in r.stderr

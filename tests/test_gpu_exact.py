@@ -1,0 +1,106 @@
+"""Exact word equality for LONG words (>= 16 bytes, hashed keys: keys.hpp) and
+engine buffer independence — GPU tests against the CPU oracle.
+
+`k1_hash_bits` (Options) truncates the LONG-word tail hash to a few bits, so
+words that share their first 8 bytes and length collide in (k0, k1) by
+construction; the map never combines LONG words, the reducer and both merge
+protocols compare the word bytes, so the counts must still equal the
+byte-keyed CPU oracle exactly."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ops = pytest.importorskip("cuda_mapreduce_amd.ops")
+
+
+def assert_same(got, want):
+    assert got.total == want.total
+    assert got.words == want.words
+    assert np.array_equal(got.counts, want.counts)
+    assert np.array_equal(got.first_off, want.first_off)
+
+
+def colliding_text(seed, n_words=60000, distinct=300):
+    """LONG words sharing one 8-byte prefix and one length (so only the tail
+    hash separates them), mixed with short and medium words."""
+    rng = np.random.default_rng(seed)
+    longs = [b"prefix__" + bytes(rng.integers(97, 123, 12, dtype=np.uint8)) for _ in range(distinct)]
+    other = [b"a", b"bb", b"ccccccccc", b"medium_word_15b", b"prefix__xyz"]
+    out = []
+    for i in range(n_words):
+        if rng.random() < 0.6:
+            out.append(longs[int(rng.zipf(1.3)) % distinct])
+        else:
+            out.append(other[int(rng.integers(0, len(other)))])
+        out.append(b" " if rng.random() < 0.9 else b"\n")
+    return b"".join(out)
+
+
+@pytest.mark.parametrize("bits", [1, 3])
+def test_forced_long_key_collisions_single_gpu(bits):
+    text = colliding_text(bits)
+    want = ops.cpu_count(text)
+    with ops.Engine(device=0, chunk_bytes=1 << 20, k1_hash_bits=bits) as e:
+        e.count_bytes(text)
+        assert_same(e.result(), want)
+
+
+@pytest.mark.parametrize("merge_mode", [0, 1])
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_forced_long_key_collisions_merge(ranks, merge_mode, monkeypatch):
+    monkeypatch.setenv("WC_MERGE_ROOT_ROWS", "0")  # the owner exchange, not the root gather
+    text = colliding_text(10 + ranks)
+    want = ops.cpu_count(text)
+    got = ops.loopback_count(text, ranks, merge_mode=merge_mode, k1_hash_bits=2, chunk_bytes=1 << 20)
+    assert_same(got, want)
+
+
+def test_resident_text_survives_streaming():
+    """Streamed counts use their own staging buffers: a resident synthetic
+    text stays valid around them, in either order (advisor finding)."""
+    host = ops.synth_host(3 << 20, first_segment=5, seed=9, vocab=2000)
+    with ops.Engine(device=0, chunk_bytes=1 << 22) as e:
+        e.count_bytes(host)
+        a = e.result()
+        e.synth_device(8 << 20, first_segment=0, seed=4, vocab=3000)
+        e.reset()
+        e.count_bytes(host)
+        b = e.result()
+        e.reset()
+        e.count_resident(8 << 20)
+        c = e.result()
+    assert_same(a, ops.cpu_count(host))
+    assert_same(b, ops.cpu_count(host))
+    assert_same(c, ops.cpu_count(ops.synth_host(8 << 20, first_segment=0, seed=4, vocab=3000)))
+
+
+def test_headline_stream_key_for_key():
+    """The exact benchmark input (1 GiB, seed 1, Zipf(1.0), 100k words, one
+    device chunk) against the generator-walk oracle; and 256 MiB of it against
+    the tokenizing CPU oracle, which also checks the walk oracle itself."""
+    n = 1 << 30
+    with ops.Engine(device=0, chunk_bytes=n) as e:
+        e.synth_device(n, first_segment=0, seed=1, vocab=100000, zipf_s=1.0)
+        e.count_resident(n)
+        got = e.result()
+    assert_same(got, ops.cpu_count_synth(n, 0, 1, 100000, 1.0, 0, 16))
+    m = 256 << 20
+    with ops.Engine(device=0, chunk_bytes=m) as e:
+        e.synth_device(m, first_segment=0, seed=1, vocab=100000, zipf_s=1.0)
+        e.count_resident(m)
+        got = e.result()
+    assert_same(got, ops.cpu_count(ops.synth_host_array(m, 0, 1, 100000, 1.0, 16)))
+
+
+def test_host_pool_replay_matches_oracle():
+    """Native page-locked pool (HostPool) replayed chunk by chunk == oracle of the replay."""
+    from cuda_mapreduce_amd.utils import compare_results, synthetic_oracle
+
+    pool_b, chunk, total = 64 << 20, 16 << 20, 160 << 20
+    pool = ops.HostPool(pool_b, first_segment=0, seed=3, vocab=20000, zipf_s=1.0, threads=8)
+    with ops.Engine(device=0, chunk_bytes=chunk) as e:
+        e.count_pool(pool, total)
+        got = e.result()
+    pool.close()
+    assert compare_results(got, synthetic_oracle(1, total, 3, 20000, 1.0, pool_bytes=pool_b, chunk=chunk)) == ""

@@ -114,3 +114,17 @@ def test_clean_mode_matches_reference_inside_envelope(ref_exe, tmp_path):
         t = envelope_text(rng, vocab)
         want = run_in(tmp_path, [ref_exe], t)
         assert run_in(tmp_path, [EXE, "--cpu"], t) == want, t
+
+
+def test_compat_mode_echo_stops_at_blank_line(ref_exe, tmp_path):
+    """A blank line ends the reference's input (main.cu:185-186): the echo stops there too."""
+    rng = np.random.default_rng(23)
+    vocab = [b"one", b"two", b"three", b"four", b"Go", b"Good"]
+    for _ in range(20):
+        head = envelope_text(rng, vocab, max_lines=4)
+        tail = envelope_text(rng, vocab, max_lines=4)
+        t = head + b"\n" + tail  # the blank line hides `tail` from the reference
+        want = run_in(tmp_path, [ref_exe], t)
+        got = run_in(tmp_path, [EXE, "--compat=reference"], t)
+        assert got == want, t
+        assert tail not in got.split(b"-" * 26)[0][len(b"Input Data:\n") + len(head):]

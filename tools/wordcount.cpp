@@ -126,7 +126,7 @@ Cli parse(int argc, char** argv) {
 }
 
 wc::Checkpoint open_checkpoint(const Cli& c, uint64_t input_size, const wc::ShardRange& sr, int r, int g) {
-  return wc::open_checkpoint(wc::checkpoint_path(c.ckpt, r, g), c.resume, input_size, sr.begin, sr.end, r, g);
+  return wc::open_checkpoint(wc::checkpoint_path(c.ckpt, r, g), c.resume, c.file, input_size, sr.begin, sr.end, r, g);
 }
 
 void add_stats(wc::Stats& a, const wc::Stats& b) {
@@ -183,7 +183,13 @@ int run(const Cli& c) {
                            [](const uint8_t* q, uint64_t n, uint64_t base) { return wc::cpu::count(q, n, base); });
       t = std::move(k.table);
     } else {
-      t = c.compat ? wc::cpu::count_reference_compat(p, host.size()) : wc::cpu::count(p, host.size());
+      if (c.compat) {
+        std::string echoed;
+        t = wc::cpu::count_reference_compat(p, host.size(), &echoed);
+        if (have_text) text = std::move(echoed);  // the reference echoes only the records it read
+      } else {
+        t = wc::cpu::count(p, host.size());
+      }
     }
     bytes = host.size();
   } else {
@@ -244,6 +250,10 @@ int run(const Cli& c) {
         if (r == 0) t = std::move(kt);
       } catch (const std::exception& ex) {
         errs[r] = ex.what();
+        // peers may be blocked in (or heading into) the merge collectives:
+        // abort this rank's communicator so they fail fast instead of waiting
+        // for the watchdog timeout
+        if (g > 1 && comms[r]) comms[r]->abort(ex.what());
       }
     };
     if (g == 1) {
