@@ -43,8 +43,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--chunk-gb", type=float, default=None)
     ap.add_argument("--pool-gb", type=float, default=None, help="host-staged: replay pool per GPU")
-    ap.add_argument("--merge", choices=["shuffle", "dense"], default="shuffle",
-                    help="cross-GPU merge: shuffle (all-to-all to hash owners) or dense (reduce-scatter + all-gather)")
+    ap.add_argument("--merge", choices=["shuffle", "dense"], default=None,
+                    help="cross-GPU merge: shuffle (all-to-all to hash owners) or dense (reduce-scatter + all-gather);"
+                         " default: the config's (dense for 256gb-8gpu)")
     ap.add_argument("--no-oracle", action="store_true",
                     help="skip the key-for-key check against the generator-walk oracle (sum check only)")
     ap.add_argument("--json-out", default="")
@@ -92,7 +93,8 @@ def main() -> int:
     seg = 1024
     nbytes = per_gpu // seg * seg
     chunk = min(chunk, nbytes) // seg * seg
-    merge_mode = {"shuffle": 0, "dense": 1}[a.merge]
+    merge = a.merge or cfg.merge
+    merge_mode = {"shuffle": 0, "dense": 1}[merge]
     eng = Engine(device=local, chunk_bytes=chunk, merge_mode=merge_mode)
     comm = None
     if use_comm:
@@ -198,7 +200,7 @@ def main() -> int:
                 "parallelism": f"dp{world}",
                 "bytes_per_gpu": nbytes,
                 "chunk_bytes": chunk,
-                "merge": a.merge,
+                "merge": merge,
             },
             "stages": st,
         }

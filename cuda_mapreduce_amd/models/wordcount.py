@@ -29,6 +29,11 @@ class JobConfig:
     zipf_s: float = 1.0
     seed: int = 1
     path: Optional[str] = None
+    merge: str = "shuffle"  # cross-GPU merge: shuffle (all-to-all to hash owners) | dense (reduce-scatter + all-gather)
+
+    @property
+    def merge_mode(self) -> int:
+        return {"shuffle": 0, "dense": 1}[self.merge]
 
 
 CONFIGS = {
@@ -40,7 +45,7 @@ CONFIGS = {
         JobConfig("64gb", "64 GB synthetic text, single MI355X (HBM-resident, chunked)", bytes_per_gpu=64 * GiB,
                   chunk_bytes=2 * GiB),
         JobConfig("256gb-8gpu", "256 GB synthetic text sharded across 8x MI355X, RCCL reduce-scatter merge",
-                  bytes_per_gpu=32 * GiB, gpus=8, chunk_bytes=2 * GiB),
+                  bytes_per_gpu=32 * GiB, gpus=8, chunk_bytes=2 * GiB, merge="dense"),
         JobConfig("1tb-8gpu-host-staged", "1 TB synthetic text, 8x MI355X, host-staged pinned hipMemcpyAsync",
                   bytes_per_gpu=128 * GiB, gpus=8, source="host-staged", chunk_bytes=GiB),
     ]
@@ -78,7 +83,7 @@ def run_job(cfg: JobConfig, rank: int = 0, world: int = 1, local_rank: int = 0, 
     first_seg = rank * (nbytes // SEG)
     base = rank * nbytes
     own = engine is None
-    eng = engine or Engine(device=local_rank, chunk_bytes=cfg.chunk_bytes)
+    eng = engine or Engine(device=local_rank, chunk_bytes=cfg.chunk_bytes, merge_mode=cfg.merge_mode)
     try:
         eng.reset()
         if cfg.source == "device":

@@ -13,7 +13,7 @@
 
 namespace wc {
 
-void launch_combine_u64(uint64_t* dst, const uint64_t* src, uint64_t n, int op, hipStream_t s);  // sort.hip
+void launch_combine_u64(uint64_t* dst, const uint64_t* src, uint64_t n, int op, hipStream_t s);  // merge.hip
 
 #define WC_NCCL_CHECK(expr)                                                                          \
   do {                                                                                                \

@@ -174,18 +174,9 @@ void launch_synth(uint8_t* out, uint64_t n, uint64_t first_segment, uint64_t see
 
 // Merge-protocol helpers (dist/merge.cpp).
 // Dense scatter: dst_cnt[id[i]] += cnt[i] (ids unique per rank, so plain stores), dst_first min.
-void launch_scatter_dense(const uint32_t* ids, const uint64_t* cnt, const uint64_t* first, uint64_t* dense_cnt,
-                          uint64_t* dense_first, uint64_t n, hipStream_t s);
 void launch_fill_u64(uint64_t* p, uint64_t v, uint64_t n, hipStream_t s);
 // merge.hip
-void launch_union_flags(const uint32_t* pos, const uint64_t* K0, const uint64_t* K1, const uint64_t* SO,
-                        const uint32_t* SL, const uint8_t* AR, uint64_t n_max, uint64_t arena_stride, uint32_t* flag,
-                        uint32_t* rep, uint64_t m, hipStream_t s);
-void launch_union_assign(const uint32_t* pos, const uint32_t* flag, const uint32_t* rep, const uint32_t* ex,
-                         const uint64_t* K0, const uint64_t* K1, const uint64_t* SO, const uint32_t* SL, uint64_t m,
-                         uint64_t n_max, uint64_t arena_stride, uint32_t* id_of_pos, uint64_t* ok0, uint64_t* ok1,
-                         uint64_t* osoff, uint32_t* oslen, hipStream_t s);
-// ---- shuffle merge (src/kernels/merge.hip) ----
+// ---- shuffle / dense merge (src/kernels/merge.hip) ----
 struct MRow {  // one key row on the wire (40 B)
   uint64_t k0, k1, cnt, first;
   uint32_t aoff, alen;  // long word: bytes [aoff, aoff + alen) of the accompanying byte payload
@@ -198,18 +189,20 @@ void launch_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* 
 void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
                           const uint64_t* soff, const uint32_t* slen, const uint8_t* arena, uint64_t n, uint32_t W,
                           const unsigned long long* counts, unsigned long long* cursor, MRow* rows, uint8_t* bytes,
-                          hipStream_t s);
+                          uint32_t* send_pos, hipStream_t s);  // send_pos (nullable): row index of each local key
 void launch_mrow_insert(const MRow* rows, uint64_t R, const uint8_t* bytes, const uint64_t* rbase,
                         const uint64_t* bbase, uint32_t W, uint32_t* state, unsigned long long* cnt,
-                        unsigned long long* first, uint64_t T, hipStream_t s);
+                        unsigned long long* first, uint64_t T, uint32_t* row_slot, hipStream_t s);  // row_slot nullable
 void launch_mrow_compact(const MRow* rows, const uint32_t* state, const unsigned long long* cnt,
                          const unsigned long long* first, uint64_t T, const uint64_t* rbase, const uint64_t* bbase,
-                         uint32_t W, MRow* out, unsigned long long* out_n, hipStream_t s);
+                         uint32_t W, MRow* out, unsigned long long* out_n, uint32_t* slot_id, hipStream_t s);  // nullable
 void launch_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rbase, const uint64_t* bbase, uint32_t W,
                          uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first, uint64_t* soff, uint32_t* slen,
                          hipStream_t s);
 void launch_combine_u64(uint64_t* dst, const uint64_t* src, uint64_t n, int op, hipStream_t s);  // 0 sum 1 min 2 max
-void launch_pad_u64(const uint64_t* in, uint64_t n, uint64_t* out, uint64_t m, uint64_t fill, hipStream_t s);
-void launch_exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint64_t m, uint32_t* total, hipStream_t s);
+void launch_row_ids(const uint32_t* row_slot, const uint32_t* slot_id, uint64_t R, uint64_t id_base, uint32_t* ids,
+                    hipStream_t s);
+void launch_scatter_ids(const uint32_t* send_pos, const uint32_t* ids_back, const uint64_t* cnt, const uint64_t* first,
+                        uint64_t n, uint64_t* dcnt, uint64_t* dfirst, hipStream_t s);
 
 }  // namespace wc

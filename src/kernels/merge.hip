@@ -8,8 +8,11 @@
 // compaction (wc_mrow_compact), and rank-0 conversion to key columns
 // (wc_mrow_to_cols).
 //
-// Dense merge (merge_mode 1): dictionary-union head flags, global-id
-// assignment, dense combine, and a single-block exclusive scan.
+// Dense merge (merge_mode 1) runs the same owner partition / exchange / merge
+// to build the dictionary, then numbers each owner's keys (wc_row_ids), returns
+// the ids to the senders, and scatters local counts into dense vectors by id
+// (wc_scatter_ids) for the reduce-scatter.  wc_combine_u64 is the loopback
+// communicator's reduction.
 #include "kernels.hpp"
 #include "keys.hpp"
 #include "lds_table.hpp"
@@ -28,114 +31,11 @@ __device__ __forceinline__ bool mem_equal(const uint8_t* x, const uint8_t* y, ui
   return true;
 }
 
-// Bytes of the LONG key at union position p (all-gathered arenas, one per rank).
-struct UnionBytes {
-  const uint64_t* SO;
-  const uint32_t* SL;
-  const uint8_t* AR;
-  uint64_t n_max, arena_stride;
-  __device__ const uint8_t* at(uint32_t p) const { return AR + (p / n_max) * arena_stride + SO[p]; }
-};
-
-// flag[i] = 1 iff sorted entry i is a valid key differing from entry i-1 —
-// for LONG keys (hashed, keys.hpp): differing in bytes from every earlier
-// entry of its (k0, k1) run; rep[i] = sorted index of the run's first entry
-// with the same bytes (only read for LONG non-heads).
-__global__ void wc_union_flags(const uint32_t* pos, const uint64_t* K0, const uint64_t* K1, UnionBytes ub,
-                               uint32_t* flag, uint32_t* rep, uint64_t m) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t p = pos[i];
-    const uint64_t k0 = K0[p], k1 = K1[p];
-    const bool valid = k1 != K1_EMPTY;
-    bool head = valid;
-    uint64_t r = i;
-    if (valid && i > 0 && K0[pos[i - 1]] == k0 && K1[pos[i - 1]] == k1) {
-      if (!key_is_hashed(k1)) {
-        head = false;
-      } else {  // walk back over the (k0, k1) run; the earliest entry with equal bytes represents it
-        const uint32_t len = ub.SL[p];
-        const uint8_t* mine = ub.at(p);
-        uint64_t found = i;
-        for (uint64_t t = i; t > 0;) {
-          --t;
-          const uint32_t pt = pos[t];
-          if (K0[pt] != k0 || K1[pt] != k1) break;
-          if (ub.SL[pt] == len && mem_equal(ub.at(pt), mine, len)) found = t;
-        }
-        head = found == i;
-        r = found;
-      }
-    }
-    flag[i] = head ? 1u : 0u;
-    rep[i] = (uint32_t)r;
-  }
-}
-
-// After an EXCLUSIVE scan of flags in `ex`: id = ex[i] (+ head) - 1; a LONG
-// non-head takes its representative's id.
-__global__ void wc_union_assign(const uint32_t* pos, const uint32_t* flag, const uint32_t* rep, const uint32_t* ex,
-                                const uint64_t* K0, const uint64_t* K1, const uint64_t* SO, const uint32_t* SL,
-                                uint64_t m, uint64_t n_max, uint64_t arena_stride, uint32_t* id_of_pos, uint64_t* ok0,
-                                uint64_t* ok1, uint64_t* osoff, uint32_t* oslen) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t p = pos[i];
-    if (K1[p] == K1_EMPTY) continue;
-    const uint32_t id = (!flag[i] && key_is_hashed(K1[p])) ? ex[rep[i]] : ex[i] + flag[i] - 1;
-    id_of_pos[p] = id;
-    if (flag[i]) {
-      ok0[id] = K0[p];
-      ok1[id] = K1[p];
-      osoff[id] = SO[p] + (p / n_max) * arena_stride;  // owner = lowest rank holding the key
-      oslen[id] = SL[p];
-    }
-  }
-}
-
 __global__ void wc_combine_u64(uint64_t* dst, const uint64_t* src, uint64_t n, int op) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t a = dst[i], b = src[i];
     dst[i] = op == 0 ? a + b : (op == 1 ? (a < b ? a : b) : (a > b ? a : b));
   }
-}
-
-// Pad: out[i] = i < n ? in[i] : fill.
-__global__ void wc_pad_u64(const uint64_t* in, uint64_t n, uint64_t* out, uint64_t m, uint64_t fill) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x)
-    out[i] = i < n ? in[i] : fill;
-}
-
-__global__ void __launch_bounds__(1024) wc_exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint64_t m,
-                                                              uint32_t* total) {
-  __shared__ uint32_t wsum[16];
-  __shared__ uint32_t carry;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (uint64_t base = 0; base < m; base += 1024) {
-    const uint64_t i = base + threadIdx.x;
-    const uint32_t v = i < m ? in[i] : 0;
-    uint32_t x = v;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o);
-      if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[wave] = x;
-    __syncthreads();
-    if (wave == 0) {
-      uint32_t s = lane < 16 ? wsum[lane] : 0;
-      for (int o = 1; o < 16; o <<= 1) {
-        const uint32_t y = __shfl_up(s, o);
-        if (lane >= o) s += y;
-      }
-      if (lane < 16) wsum[lane] = s;
-    }
-    __syncthreads();
-    if (i < m) out[i] = carry + (wave ? wsum[wave - 1] : 0) + x - v;
-    __syncthreads();
-    if (threadIdx.x == 0) carry += wsum[15];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) *total = carry;
 }
 
 constexpr int OWN_MAX = 64;       // ranks supported by the shuffle merge
@@ -190,7 +90,8 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
                                                         const uint64_t* first, const uint64_t* soff,
                                                         const uint32_t* slen, const uint8_t* arena, uint64_t n,
                                                         uint32_t W, const unsigned long long* counts,
-                                                        unsigned long long* cursor, MRow* rows, uint8_t* bytes) {
+                                                        unsigned long long* cursor, MRow* rows, uint8_t* bytes,
+                                                        uint32_t* send_pos) {
   __shared__ unsigned long long base[2 * OWN_MAX], h[2 * OWN_MAX];
   constexpr int PER = OWN_ROWS_PER_BLOCK / 256;
   const uint64_t r0 = (uint64_t)blockIdx.x * OWN_ROWS_PER_BLOCK;
@@ -241,6 +142,7 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
       r.alen = slen[i];
     }
     rows[base[2 * o] + lr[j]] = r;
+    if (send_pos) send_pos[i] = (uint32_t)(base[2 * o] + lr[j]);
   }
 }
 
@@ -259,7 +161,7 @@ __device__ __forceinline__ uint32_t source_of(const uint64_t* rbase, uint32_t W,
 __global__ void __launch_bounds__(256) wc_mrow_insert(const MRow* rows, uint64_t R, const uint8_t* bytes,
                                                       const uint64_t* rbase, const uint64_t* bbase, uint32_t W,
                                                       uint32_t* state, unsigned long long* cnt,
-                                                      unsigned long long* first, uint64_t T) {
+                                                      unsigned long long* first, uint64_t T, uint32_t* row_slot) {
   for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < R; r += (uint64_t)gridDim.x * blockDim.x) {
     const MRow me = rows[r];
     const bool hashed = key_is_hashed(me.k1);
@@ -279,6 +181,7 @@ __global__ void __launch_bounds__(256) wc_mrow_insert(const MRow* rows, uint64_t
     }
     atomicAdd(&cnt[slot], (unsigned long long)me.cnt);
     atomicMin(&first[slot], (unsigned long long)me.first);
+    if (row_slot) row_slot[r] = (uint32_t)slot;
   }
 }
 
@@ -289,7 +192,7 @@ __global__ void __launch_bounds__(256) wc_mrow_compact(const MRow* rows, const u
                                                        const unsigned long long* cnt,
                                                        const unsigned long long* first, uint64_t T,
                                                        const uint64_t* rbase, const uint64_t* bbase, uint32_t W,
-                                                       MRow* out, unsigned long long* out_n) {
+                                                       MRow* out, unsigned long long* out_n, uint32_t* slot_id) {
   __shared__ unsigned long long blk;
   __shared__ uint32_t bcount;
   const int lane = (int)__lane_id();
@@ -322,11 +225,33 @@ __global__ void __launch_bounds__(256) wc_mrow_compact(const MRow* rows, const u
     m.first = first[sl];
     if (m.alen) m.aoff = (uint32_t)(bbase[src] + m.aoff);
     out[blk + local[j]] = m;
+    if (slot_id) slot_id[sl] = (uint32_t)(blk + local[j]);
+  }
+}
+
+// Dense merge: global id of received row r = this owner's id base + the compact
+// index of the slot the row merged into.
+__global__ void wc_row_ids(const uint32_t* row_slot, const uint32_t* slot_id, uint64_t R, uint64_t id_base,
+                           uint32_t* ids) {
+  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < R; r += (uint64_t)gridDim.x * blockDim.x)
+    ids[r] = (uint32_t)(id_base + slot_id[row_slot[r]]);
+}
+
+// Dense merge: local key i (sent as row send_pos[i], whose id came back in
+// ids_back) stores its count and first offset at its global id — ids of one
+// rank's keys are distinct, so plain stores.
+__global__ void wc_scatter_ids(const uint32_t* send_pos, const uint32_t* ids_back, const uint64_t* cnt,
+                               const uint64_t* first, uint64_t n, uint64_t* dcnt, uint64_t* dfirst) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t g = ids_back[send_pos[i]];
+    dcnt[g] = cnt[i];
+    dfirst[g] = first[i];
   }
 }
 
 // Gathered merged rows (grouped by owner) -> key columns; sref_off is made
-// absolute in the gathered byte buffer.
+// absolute in the gathered byte buffer.  cnt / first may be null (the dense
+// merge takes them from its reduced vectors).
 __global__ void wc_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rbase, const uint64_t* bbase,
                                 uint32_t W, uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first,
                                 uint64_t* soff, uint32_t* slen) {
@@ -336,8 +261,8 @@ __global__ void wc_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rb
     const MRow m = rows[i];
     k0[i] = m.k0;
     k1[i] = m.k1;
-    cnt[i] = m.cnt;
-    first[i] = m.first;
+    if (cnt) cnt[i] = m.cnt;
+    if (first) first[i] = m.first;
     soff[i] = m.alen ? bbase[o] + m.aoff : 0;
     slen[i] = m.alen;
   }
@@ -352,25 +277,25 @@ void launch_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* 
 void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
                           const uint64_t* soff, const uint32_t* slen, const uint8_t* arena, uint64_t n, uint32_t W,
                           const unsigned long long* counts, unsigned long long* cursor, MRow* rows, uint8_t* bytes,
-                          hipStream_t s) {
+                          uint32_t* send_pos, hipStream_t s) {
   const uint64_t blocks = (n + dev::OWN_ROWS_PER_BLOCK - 1) / dev::OWN_ROWS_PER_BLOCK;
   if (n)
     hipLaunchKernelGGL(dev::wc_owner_scatter, dim3((unsigned)blocks), dim3(256), 0, s, k0, k1, cnt, first, soff, slen,
-                       arena, n, W, counts, cursor, rows, bytes);
+                       arena, n, W, counts, cursor, rows, bytes, send_pos);
 }
 void launch_mrow_insert(const MRow* rows, uint64_t R, const uint8_t* bytes, const uint64_t* rbase,
                         const uint64_t* bbase, uint32_t W, uint32_t* state, unsigned long long* cnt,
-                        unsigned long long* first, uint64_t T, hipStream_t s) {
+                        unsigned long long* first, uint64_t T, uint32_t* row_slot, hipStream_t s) {
   if (R)
     hipLaunchKernelGGL(dev::wc_mrow_insert, dev::mgrid(R), dim3(256), 0, s, rows, R, bytes, rbase, bbase, W, state, cnt,
-                       first, T);
+                       first, T, row_slot);
 }
 void launch_mrow_compact(const MRow* rows, const uint32_t* state, const unsigned long long* cnt,
                          const unsigned long long* first, uint64_t T, const uint64_t* rbase, const uint64_t* bbase,
-                         uint32_t W, MRow* out, unsigned long long* out_n, hipStream_t s) {
+                         uint32_t W, MRow* out, unsigned long long* out_n, uint32_t* slot_id, hipStream_t s) {
   const uint64_t blocks = (T + 256 * dev::MCOMPACT_PER - 1) / (256 * dev::MCOMPACT_PER);
   hipLaunchKernelGGL(dev::wc_mrow_compact, dim3((unsigned)blocks), dim3(256), 0, s, rows, state, cnt, first, T, rbase,
-                     bbase, W, out, out_n);
+                     bbase, W, out, out_n, slot_id);
 }
 void launch_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rbase, const uint64_t* bbase, uint32_t W,
                          uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first, uint64_t* soff, uint32_t* slen,
@@ -380,29 +305,17 @@ void launch_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rbase, co
                        first, soff, slen);
 }
 
-void launch_union_flags(const uint32_t* pos, const uint64_t* K0, const uint64_t* K1, const uint64_t* SO,
-                        const uint32_t* SL, const uint8_t* AR, uint64_t n_max, uint64_t arena_stride, uint32_t* flag,
-                        uint32_t* rep, uint64_t m, hipStream_t s) {
-  if (m)
-    hipLaunchKernelGGL(dev::wc_union_flags, dev::mgrid(m), dim3(256), 0, s, pos, K0, K1,
-                       dev::UnionBytes{SO, SL, AR, n_max, arena_stride}, flag, rep, m);
+void launch_row_ids(const uint32_t* row_slot, const uint32_t* slot_id, uint64_t R, uint64_t id_base, uint32_t* ids,
+                    hipStream_t s) {
+  if (R) hipLaunchKernelGGL(dev::wc_row_ids, dev::mgrid(R), dim3(256), 0, s, row_slot, slot_id, R, id_base, ids);
 }
-void launch_union_assign(const uint32_t* pos, const uint32_t* flag, const uint32_t* rep, const uint32_t* ex,
-                         const uint64_t* K0, const uint64_t* K1, const uint64_t* SO, const uint32_t* SL, uint64_t m,
-                         uint64_t n_max, uint64_t arena_stride, uint32_t* id_of_pos, uint64_t* ok0, uint64_t* ok1,
-                         uint64_t* osoff, uint32_t* oslen, hipStream_t s) {
-  if (m)
-    hipLaunchKernelGGL(dev::wc_union_assign, dev::mgrid(m), dim3(256), 0, s, pos, flag, rep, ex, K0, K1, SO, SL, m,
-                       n_max, arena_stride, id_of_pos, ok0, ok1, osoff, oslen);
+void launch_scatter_ids(const uint32_t* send_pos, const uint32_t* ids_back, const uint64_t* cnt, const uint64_t* first,
+                        uint64_t n, uint64_t* dcnt, uint64_t* dfirst, hipStream_t s) {
+  if (n)
+    hipLaunchKernelGGL(dev::wc_scatter_ids, dev::mgrid(n), dim3(256), 0, s, send_pos, ids_back, cnt, first, n, dcnt,
+                       dfirst);
 }
 void launch_combine_u64(uint64_t* dst, const uint64_t* src, uint64_t n, int op, hipStream_t s) {
   if (n) hipLaunchKernelGGL(dev::wc_combine_u64, dev::mgrid(n), dim3(256), 0, s, dst, src, n, op);
 }
-void launch_pad_u64(const uint64_t* in, uint64_t n, uint64_t* out, uint64_t m, uint64_t fill, hipStream_t s) {
-  if (m) hipLaunchKernelGGL(dev::wc_pad_u64, dev::mgrid(m), dim3(256), 0, s, in, n, out, m, fill);
-}
-void launch_exclusive_scan_u32(const uint32_t* in, uint32_t* out, uint64_t m, uint32_t* total, hipStream_t s) {
-  hipLaunchKernelGGL(dev::wc_exclusive_scan_u32, dim3(1), dim3(1024), 0, s, in, out, m, total);
-}
-
 }  // namespace wc

@@ -161,15 +161,6 @@ __global__ void wc_fill_u64(uint64_t* p, uint64_t v, uint64_t n) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     p[i] = v;
 }
-__global__ void wc_scatter_dense(const uint32_t* ids, const uint64_t* cnt, const uint64_t* first, uint64_t* dcnt,
-                                 uint64_t* dfirst, uint64_t n) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t id = ids[i];
-    dcnt[id] += cnt[i];
-    dfirst[id] = first[i] < dfirst[id] ? first[i] : dfirst[id];
-  }
-}
-
 inline dim3 grid_for(uint64_t n) {
   uint64_t g = (n + 255) / 256;
   if (g < 1) g = 1;
@@ -231,10 +222,4 @@ void launch_iota_u32(uint32_t* v, uint64_t n, hipStream_t s) {
 void launch_fill_u64(uint64_t* p, uint64_t v, uint64_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(dev::wc_fill_u64, dev::grid_for(n), dim3(256), 0, s, p, v, n);
 }
-void launch_scatter_dense(const uint32_t* ids, const uint64_t* cnt, const uint64_t* first, uint64_t* dense_cnt,
-                          uint64_t* dense_first, uint64_t n, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(dev::wc_scatter_dense, dev::grid_for(n), dim3(256), 0, s, ids, cnt, first, dense_cnt,
-                            dense_first, n);
-}
-
 }  // namespace wc

@@ -163,16 +163,19 @@ def test_loopback_merge(ranks, merge_mode, root_rows, monkeypatch):
         assert_same(got, ops.cpu_count(text))
 
 
-@pytest.mark.parametrize("ranks", [2, 5])
-def test_loopback_merge_many_long_words(ranks):
-    """Shuffle merge with many >8-byte words (owner byte payloads, arena offsets)."""
+@pytest.mark.parametrize("merge_mode", [0, 1])
+@pytest.mark.parametrize("ranks", [2, 5, 8])
+def test_loopback_merge_many_long_words(ranks, merge_mode):
+    """Both merges with many >8-byte words (owner byte payloads, arena offsets,
+    dense ids returned to the senders)."""
     rng = np.random.default_rng(40 + ranks)
     words = [bytes(rng.integers(97, 123, int(rng.integers(9, 40))).astype(np.uint8)) for _ in range(5000)]
     picks = rng.integers(0, len(words), 200_000)
     text = b" ".join(words[i] for i in picks) + b"\n"
     want = ops.cpu_count(text)
     for all_ranks in (False, True):  # rank-0 gather path | owner exchange + broadcast
-        assert_same(ops.loopback_count(text, ranks, chunk_bytes=1 << 20, all_ranks=all_ranks), want)
+        assert_same(ops.loopback_count(text, ranks, chunk_bytes=1 << 20, merge_mode=merge_mode, all_ranks=all_ranks),
+                    want)
 
 
 def test_file_stream(tmp_path):
