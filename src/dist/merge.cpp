@@ -37,6 +37,15 @@ template <class T>
 T* take_aligned(DeviceArena& A, size_t n) {
   return A.take_n<T>(n ? n : 1);
 }
+
+// Pinned host words of one merge (W <= 64): async H2D copies from them need no
+// host sync before the merge returns.  Fixed slots: max offset, source bases,
+// own bytes, gather bases.
+enum : size_t { HW_MX = 0, HW_BASE = 8, HW_OWNB = 160, HW_GBASE = 192, HW_WORDS = 512 };
+uint64_t* host_words(Engine::Impl& im) {
+  if (im.h_merge.size() < HW_WORDS * 8) im.h_merge.resize(HW_WORDS * 8);
+  return reinterpret_cast<uint64_t*>(im.h_merge.data());
+}
 }  // namespace
 
 // Small-vocabulary variant of the shuffle merge (see merge_cols_owner):
@@ -50,7 +59,7 @@ void merge_to_root(Engine::Impl& im, Comm& comm, const std::vector<uint64_t>& ra
   const uint64_t my_rows = rank_rows[R], my_bytes = rank_bytes[R];
   uint64_t rr = 0, rbt = 0;  // received by rank 0
   std::vector<size_t> zs(W, 0), sr(W, 0), sb(W, 0), ro_r(W, 0), rb_r(W, 0), ro_b(W, 0), rb_b(W, 0);
-  std::vector<uint64_t> base(2 * (size_t)W + 2, 0);
+  uint64_t* base = host_words(im) + HW_BASE;  // row bases | byte bases per source
   for (int p = 0; p < W; ++p) {
     base[p] = rr;
     base[W + 1 + p] = rbt;
@@ -86,15 +95,18 @@ void merge_to_root(Engine::Impl& im, Comm& comm, const std::vector<uint64_t>& ra
   comm.alltoallv(send_bytes, zs.data(), sb.data(), recv_bytes, ro_b.data(), rb_b.data(), s);
   comm.group_end();
   KeyCols o;
-  uint64_t gb[4] = {0, 0, 0, rbt};  // one output group (rows 0..G, byte base 0); outlives its async H2D
+  uint64_t* gb = host_words(im) + HW_GBASE;  // one output group (rows 0..G, byte base 0)
+  gb[0] = gb[2] = 0;
+  gb[3] = rbt;
   if (R == 0) {
     uint32_t* state = take_aligned<uint32_t>(A, T);
     unsigned long long* tcnt = take_aligned<unsigned long long>(A, T);
     unsigned long long* tfirst = take_aligned<unsigned long long>(A, T);
     MRow* merged = take_aligned<MRow>(A, rr);
-    uint64_t* d_base = take_aligned<uint64_t>(A, base.size() + 4);
+    const size_t nbase = 2 * (size_t)W + 2;
+    uint64_t* d_base = take_aligned<uint64_t>(A, nbase + 4);
     unsigned long long* d_m = take_aligned<unsigned long long>(A, 1);
-    WC_HIP_CHECK(hipMemcpyAsync(d_base, base.data(), base.size() * 8, hipMemcpyHostToDevice, s));
+    WC_HIP_CHECK(hipMemcpyAsync(d_base, base, nbase * 8, hipMemcpyHostToDevice, s));
     WC_HIP_CHECK(hipMemsetAsync(state, 0, T * 4, s));
     WC_HIP_CHECK(hipMemsetAsync(tcnt, 0, T * 8, s));
     launch_fill_u64(reinterpret_cast<uint64_t*>(tfirst), ~0ull, T, s);
@@ -113,13 +125,12 @@ void merge_to_root(Engine::Impl& im, Comm& comm, const std::vector<uint64_t>& ra
     o.first = take_aligned<uint64_t>(A, G);
     o.sref_off = take_aligned<uint64_t>(A, G);
     o.sref_len = take_aligned<uint32_t>(A, G);
-    uint64_t* d_gbase = d_base + base.size();  // one group: row base 0 .. G, byte base 0
+    uint64_t* d_gbase = d_base + nbase;  // one group: row base 0 .. G, byte base 0
     gb[1] = G;
-    WC_HIP_CHECK(hipMemcpyAsync(d_gbase, gb, sizeof gb, hipMemcpyHostToDevice, s));
+    WC_HIP_CHECK(hipMemcpyAsync(d_gbase, gb, 4 * 8, hipMemcpyHostToDevice, s));
     launch_mrow_to_cols(merged, G, d_gbase, d_gbase + 2, 1u, o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len, s);
   }
-  comm.sync(s);  // also: base[] / gb[] are pageable host memory
-  im.cols = o;
+  im.cols = o;  // still in flight: finalize waits under the comm watchdog
   im.cols_arena = recv_bytes;
   im.cols_arena_bytes = R == 0 ? rbt : 0;
   im.max_end = gmax_end;
@@ -155,13 +166,14 @@ OwnerPlan plan_owners(Engine::Impl& im, Comm& comm) {
   P.d_cnt = take_aligned<unsigned long long>(S, 2 * C);
   unsigned long long* d_all = take_aligned<unsigned long long>(S, (size_t)W * C);
   WC_HIP_CHECK(hipMemsetAsync(P.d_cnt, 0, 2 * C * 8, s));
-  const unsigned long long mx = im.max_end;
-  WC_HIP_CHECK(hipMemcpyAsync(P.d_cnt + 2 * W, &mx, 8, hipMemcpyHostToDevice, s));
+  uint64_t* mx = host_words(im) + HW_MX;
+  *mx = im.max_end;
+  WC_HIP_CHECK(hipMemcpyAsync(P.d_cnt + 2 * W, mx, 8, hipMemcpyHostToDevice, s));
   launch_owner_count(im.cols.k0, im.cols.k1, im.cols.sref_len, im.cols.n, (uint32_t)W, P.d_cnt, s);
   comm.allgather(P.d_cnt, d_all, C * 8, s);
   P.all.resize((size_t)W * C);
   WC_HIP_CHECK(hipMemcpyAsync(P.all.data(), d_all, P.all.size() * 8, hipMemcpyDeviceToHost, s));
-  comm.sync(s);  // also: mx is pageable host memory
+  comm.sync(s);
   P.rank_rows.assign(W, 0);
   P.rank_bytes.assign(W, 0);
   for (int r = 0; r < W; ++r) {
@@ -253,14 +265,14 @@ void merge_cols_owner(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense) 
   uint32_t* slot_id = dense ? take_aligned<uint32_t>(A, T) : nullptr;
   uint64_t* d_base = take_aligned<uint64_t>(A, 2 * (size_t)W + 2);  // row / byte bases per source (then per owner)
   unsigned long long* d_m = take_aligned<unsigned long long>(A, 1);
-  std::vector<uint64_t> base(2 * (size_t)W + 2);
+  uint64_t* base = host_words(im) + HW_BASE;  // row | byte bases per source
   for (int p = 0; p < W; ++p) {
     base[p] = P.ro_r[p] / sizeof(MRow);
     base[W + 1 + p] = P.ro_b[p];
   }
   base[W] = rr;
   base[2 * W + 1] = rbt;
-  WC_HIP_CHECK(hipMemcpyAsync(d_base, base.data(), base.size() * 8, hipMemcpyHostToDevice, s));
+  WC_HIP_CHECK(hipMemcpyAsync(d_base, base, (2 * (size_t)W + 2) * 8, hipMemcpyHostToDevice, s));
   WC_HIP_CHECK(hipMemsetAsync(state, 0, T * 4, s));
   WC_HIP_CHECK(hipMemsetAsync(tcnt, 0, T * 8, s));
   launch_fill_u64(reinterpret_cast<uint64_t*>(tfirst), ~0ull, T, s);
@@ -271,20 +283,21 @@ void merge_cols_owner(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense) 
 
   // 4. (merged rows, bytes) of every owner: the row count stays on the device
   // until this allgather, so one host sync serves both
-  const unsigned long long own_bytes = rbt;
+  uint64_t* own_bytes = host_words(im) + HW_OWNB;
+  *own_bytes = rbt;
   unsigned long long* d_own = take_aligned<unsigned long long>(A, 2);
   unsigned long long* d_owns = take_aligned<unsigned long long>(A, 2 * (size_t)W);
   WC_HIP_CHECK(hipMemcpyAsync(d_own, d_m, 8, hipMemcpyDeviceToDevice, s));
-  WC_HIP_CHECK(hipMemcpyAsync(d_own + 1, &own_bytes, 8, hipMemcpyHostToDevice, s));
+  WC_HIP_CHECK(hipMemcpyAsync(d_own + 1, own_bytes, 8, hipMemcpyHostToDevice, s));
   comm.allgather(d_own, d_owns, 16, s);
   std::vector<unsigned long long> owns(2 * (size_t)W);
   WC_HIP_CHECK(hipMemcpyAsync(owns.data(), d_owns, owns.size() * 8, hipMemcpyDeviceToHost, s));
-  comm.sync(s);  // also: base[] / own_bytes are pageable host memory
-  const unsigned long long own[2] = {owns[2 * (size_t)R], own_bytes};
+  comm.sync(s);
+  const unsigned long long own[2] = {owns[2 * (size_t)R], rbt};
   std::vector<size_t> go_r(W, 0), gb_r(W, 0), go_b(W, 0), gb_b(W, 0), zs(W, 0);
   std::vector<size_t> sr(W, 0), sb(W, 0);
   uint64_t G = 0, GB = 0;
-  std::vector<uint64_t> gbase(2 * (size_t)W + 2);
+  uint64_t* gbase = host_words(im) + HW_GBASE;  // row | byte bases per owner in the gathered dictionary
   for (int p = 0; p < W; ++p) {
     gbase[p] = G;
     gbase[W + 1 + p] = GB;
@@ -356,13 +369,12 @@ void merge_cols_owner(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense) 
     o.first = dense ? dfirst : take_aligned<uint64_t>(A, G);
     o.sref_off = take_aligned<uint64_t>(A, G);
     o.sref_len = take_aligned<uint32_t>(A, G);
-    uint64_t* d_gbase = take_aligned<uint64_t>(A, gbase.size());
-    WC_HIP_CHECK(hipMemcpyAsync(d_gbase, gbase.data(), gbase.size() * 8, hipMemcpyHostToDevice, s));
+    uint64_t* d_gbase = take_aligned<uint64_t>(A, 2 * (size_t)W + 2);
+    WC_HIP_CHECK(hipMemcpyAsync(d_gbase, gbase, (2 * (size_t)W + 2) * 8, hipMemcpyHostToDevice, s));
     launch_mrow_to_cols(grows, G, d_gbase, d_gbase + W + 1, (uint32_t)W, o.k0, o.k1, dense ? nullptr : o.cnt,
                         dense ? nullptr : o.first, o.sref_off, o.sref_len, s);
   }
-  comm.sync(s);  // also: gbase[] is pageable host memory
-  im.cols = o;
+  im.cols = o;  // still in flight: finalize waits under the comm watchdog
   im.cols_arena = gbytes;
   im.cols_arena_bytes = have ? GB : 0;
   im.max_end = P.gmax_end;

@@ -586,13 +586,16 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
   // WC_MERGE_ALWAYS=1 (tests): run the merge protocol even with one rank, so
   // the RCCL exchange code is exercised on a one-GPU box
   static const bool merge_always = getenv("WC_MERGE_ALWAYS") && atoi(getenv("WC_MERGE_ALWAYS")) != 0;
-  if (comm && (comm->size() > 1 || merge_always)) {
+  const bool merged = comm && (comm->size() > 1 || merge_always);
+  if (merged) {
     const double tm = now_seconds();
     merge_cols(im, *comm, all_ranks);
     im.st.merge_ms += (now_seconds() - tm) * 1e3;
   }
   im.sort_cols_by_first();
-  WC_HIP_CHECK(hipStreamSynchronize(im.s));
+  // the merge's last collectives are still in flight: wait under the comm watchdog
+  if (merged) comm->sync(im.s);
+  else WC_HIP_CHECK(hipStreamSynchronize(im.s));
   im.st.finalize_ms += (now_seconds() - t0) * 1e3;
   WC_LOG(LOG_INFO, "dev %d: finalize %.3f ms (merge %.3f ms), %llu keys, %u chunk(s), %llu records, %u re-run(s)",
          im.dev, (now_seconds() - t0) * 1e3, im.st.merge_ms, (unsigned long long)im.cols.n, im.st.chunks,

@@ -93,6 +93,7 @@ struct Engine::Impl {
   PinnedBuffer h_boff;   // per-bucket compaction offsets (H2D without a sync)
   DeviceArena merge_mem; // merge buffers (merged columns live here)
   DeviceArena merge_small;  // merge metadata (count matrices)
+  PinnedBuffer h_merge;     // merge host words for async H2D copies (no sync before they go out of scope)
   DeviceArena sort_mem;  // first-occurrence sort + sorted columns
   KeyCols cols;        // local (compact) or merged, sorted by first after finalize
   uint8_t* cols_arena = nullptr;   // arena the sref_* of cols point into

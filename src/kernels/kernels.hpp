@@ -183,7 +183,11 @@ struct MRow {  // one key row on the wire (40 B)
 };
 static_assert(sizeof(MRow) == 40, "MRow layout");
 constexpr uint32_t MERGE_MAX_RANKS = 64;
-constexpr uint64_t MERGE_ROOT_MAX_ROWS = 1ull << 21;  // shuffle merge: gather straight to rank 0 below this
+// Shuffle merge: below this many rows in total every rank sends straight to
+// rank 0, which merges alone.  Rank 0 then inserts all W x V rows instead of
+// V / W x W; the owner path costs one more exchange + host sync (~50 us at one
+// rank, tools/merge_cost.py) — the insert + compact of ~2.5e5 rows.
+constexpr uint64_t MERGE_ROOT_MAX_ROWS = 1ull << 18;
 void launch_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* slen, uint64_t n, uint32_t W,
                         unsigned long long* counts, hipStream_t s);
 void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,

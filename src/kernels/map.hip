@@ -36,6 +36,8 @@
 // << 56, one compare); 8..15-byte words use len << 56 | low 7 bytes of
 // (k0 ^ tail) plus k0 in `side`.  LONG words (>= 16 bytes, hashed keys) never
 // enter the table: each token is a record, so the reducer compares its bytes.
+#include <type_traits>
+
 #include "map_common.hpp"
 
 namespace wc {
@@ -460,51 +462,59 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     for (uint32_t base = 0; base < wave_total; base += MAP_LIST) {
       // ---- list round: entries [base, base + MAP_LIST) of the unit ----
       const uint32_t lim = base + MAP_LIST;
+      const uint32_t dlo = (uint32_t)dm, dhi = (uint32_t)(dm >> 32);
       while (bits && k < lim) {
         const uint32_t i = __ffs(bits) - 1;
         bits &= bits - 1;
-        const uint64_t rest = dm >> i;
-        const uint32_t len = rest ? min((uint32_t)__ffsll((unsigned long long)rest) - 1, MAP_LONG) : MAP_LONG;
+        // delimiter bits from the token start on (i < 32: one funnel shift); none
+        // within 31 bytes -> MAP_LONG (ffbl of 0 is all ones)
+        const uint32_t rest = __builtin_amdgcn_alignbit(dhi, dlo, i);
+        const uint32_t len = min(ffbl_raw(rest), MAP_LONG);
         list[k - base] = (uint16_t)((pbase + i) | (len << 11));
         ++k;
       }
       wave_sync();
       const uint32_t round_n = min(wave_total - base, (uint32_t)MAP_LIST);
       clk.lap(MS_LIST);
-      for (uint32_t j = 0; j < round_n; j += 128) {
-        // ---- one step: two list entries per lane, both probed in one round trip ----
-        const bool h1 = j + lane < round_n, h2 = j + 64 + lane < round_n;
+      // one step: two list entries per lane, both probed in one LDS round trip;
+      // a tail of <= 64 entries takes the one-entry step (no dead second half)
+      auto step = [&](uint32_t j, auto two_c) {
+        constexpr bool TWO = decltype(two_c)::value;
+        const bool h1 = j + lane < round_n, h2 = TWO && j + 64 + lane < round_n;
         const uint32_t e1 = h1 ? list[j + lane] : 0u, e2 = h2 ? list[j + 64 + lane] : 0u;
         const uint32_t q1 = e1 & 0x7FFu, q2 = e2 & 0x7FFu, n1 = e1 >> 11, n2 = e2 >> 11;
-        uint64_t w10, w11, w20, w21;
+        uint64_t w10, w11, w20 = 0, w21 = 0;
         window16(buf, q1, w10, w11);
-        window16(buf, q2, w20, w21);
+        if (TWO) window16(buf, q2, w20, w21);
         if (WC_MAP_ABLATE == 1) {
           sink ^= w10 ^ w21;
-          continue;
+          return;
         }
         const bool in1 = h1 && n1 <= KEY_INLINE_MAX, in2 = h2 && n2 <= KEY_INLINE_MAX;
-        uint64_t a0, a1, as, b0, b1, bs;
+        uint64_t a0, a1, as, b0 = 0, b1 = 0, bs = 0;
         inline_key(w10, w11, n1, a0, a1, as);
-        inline_key(w20, w21, n2, b0, b1, bs);
-        const uint32_t ha = place_hash(a0, a1), hb = place_hash(b0, b1);
-        uint32_t ga1, ga2, gb1, gb2;
+        if (TWO) inline_key(w20, w21, n2, b0, b1, bs);
+        const uint32_t ha = place_hash(a0, a1), hb = TWO ? place_hash(b0, b1) : 0u;
+        uint32_t ga1, ga2, gb1 = 0, gb2 = 0;
         hot_groups(ha, ga1, ga2);
-        hot_groups(hb, gb1, gb2);
+        if (TWO) hot_groups(hb, gb1, gb2);
         clk.lap(MS_KEYS);
         if (WC_MAP_ABLATE == 2) {
           sink ^= as ^ bs ^ ga2 ^ gb2;
-          continue;
+          return;
         }
         const u64x2* S = reinterpret_cast<const u64x2*>(L.sig);  // S[g]: slots 0-1, S[NG + g]: slots 2-3
         const u64x2 xa0 = S[ga1], xa1 = S[NG + ga1], xa2 = S[ga2], xa3 = S[NG + ga2];
-        const u64x2 xb0 = S[gb1], xb1 = S[NG + gb1], xb2 = S[gb2], xb3 = S[NG + gb2];
+        int s1 = -1, s2 = -1;
+        if (TWO) {
+          const u64x2 xb0 = S[gb1], xb1 = S[NG + gb1], xb2 = S[gb2], xb3 = S[NG + gb2];
+          const int mb = in2 ? sig_match8(xb0, xb1, xb2, xb3, bs) : -1;
+          s2 = mb < 0 ? -1 : (int)slot_of(mb < GS ? gb1 : gb2, mb & (GS - 1));
+        }
         const int ma = in1 ? sig_match8(xa0, xa1, xa2, xa3, as) : -1;
-        const int mb = in2 ? sig_match8(xb0, xb1, xb2, xb3, bs) : -1;
-        int s1 = ma < 0 ? -1 : (int)slot_of(ma < GS ? ga1 : ga2, ma & (GS - 1));
-        int s2 = mb < 0 ? -1 : (int)slot_of(mb < GS ? gb1 : gb2, mb & (GS - 1));
+        s1 = ma < 0 ? -1 : (int)slot_of(ma < GS ? ga1 : ga2, ma & (GS - 1));
         // two-word keys: the matching slot's side word decides
-        const bool ta = two_word(as), tb = two_word(bs);
+        const bool ta = two_word(as), tb = TWO && two_word(bs);
         const uint64_t ca = s1 >= 0 && ta ? L.side[s1] : a0, cb = s2 >= 0 && tb ? L.side[s2] : b0;
         if (ca != a0) s1 = -1;
         if (cb != b0) s2 = -1;
@@ -514,16 +524,16 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
           atomicAdd(&L.cnt[s1], 1u);  // results unused: no-return ds_add / ds_min
           atomicMin(&L.off[s1], o1);
         }
-        if (s2 >= 0) {
+        if (TWO && s2 >= 0) {
           atomicAdd(&L.cnt[s2], 1u);
           atomicMin(&L.off[s2], o2);
         }
-        if (WC_MAP_ABLATE == 3) continue;
+        if (WC_MAP_ABLATE == 3) return;
         // misses of inline words become records now; LONG words wait for the round end
-        const bool d1 = in1 && s1 < 0, d2 = in2 && s2 < 0;
+        const bool d1 = in1 && s1 < 0, d2 = TWO && in2 && s2 < 0;
         emit_two(L.bcur, a, d1, ha & bmask, a0, a1, o1, d2, hb & bmask, b0, b1, o2);
-        const bool f1 = h1 && !in1, f2 = h2 && !in2;
-        const uint64_t mf1 = __ballot(f1), mf2 = __ballot(f2);
+        const bool f1 = h1 && !in1, f2 = TWO && h2 && !in2;
+        const uint64_t mf1 = __ballot(f1), mf2 = TWO ? __ballot(f2) : 0ull;
         if (mf1 | mf2) {  // entries before j are consumed: ndef <= j
           const uint32_t r1 =
               __builtin_amdgcn_mbcnt_hi((uint32_t)(mf1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mf1, 0u));
@@ -534,7 +544,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
           if (f2) list[ndef + n1c + r2] = (uint16_t)e2;
           ndef += n1c + (uint32_t)__popcll(mf2);
         }
-        my_direct += (uint32_t)(__popcll(__ballot(d1)) + __popcll(__ballot(d2)));
+        my_direct += (uint32_t)(__popcll(__ballot(d1)) + (TWO ? __popcll(__ballot(d2)) : 0));
         if constexpr (ST) {
           const uint32_t nh = (uint32_t)(__popcll(__ballot(s1 >= 0)) + __popcll(__ballot(s2 >= 0)));
           if (lane == 0) {
@@ -543,7 +553,10 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
           }
         }
         clk.lap(MS_EMIT);
-      }
+      };
+      uint32_t j = 0;
+      for (; j + 64 < round_n; j += 128) step(j, std::true_type{});
+      if (j < round_n) step(j, std::false_type{});
       if (ndef) {
         run_deferred(u0);
         clk.lap(MS_SLOW);

@@ -10,7 +10,7 @@ namespace dev {
 
 constexpr int MAP_WAVES = MAP_THREADS / 64;
 #ifndef WC_MAP_LIST
-#define WC_MAP_LIST 256
+#define WC_MAP_LIST 512
 #endif
 constexpr int MAP_LIST = WC_MAP_LIST;            // token-list entries per wave per round (u16)
 constexpr uint32_t MAP_LONG = 31u;               // list length field: >= 31 bytes or past the lane window
@@ -68,6 +68,14 @@ __device__ __forceinline__ uint32_t delim_bits4(uint32_t x) {
   auto zb = [](uint32_t y) { return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u; };
   const uint32_t m = zb(x ^ 0x20202020u) | zb(x ^ 0x0D0D0D0Du) | zb(x ^ 0x0A0A0A0Au);
   return (((m >> 7) * 0x00204081u) >> 21) & 0xFu;
+}
+
+// v_ffbl_b32 as the hardware defines it: index of the lowest set bit, all ones
+// for 0 (the builtins add a select for 0).
+__device__ __forceinline__ uint32_t ffbl_raw(uint32_t x) {
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
 }
 
 // Wave-wide exclusive prefix sum of a small per-lane value v < 32 (bit

@@ -45,23 +45,45 @@ __device__ __forceinline__ uint32_t owner_of(uint32_t ph, uint32_t W) {
   return (uint32_t)(((uint64_t)ph * W) >> 32);  // high hash bits (bucket bits are low)
 }
 
-// Wave-aggregated LDS counter add: lanes with owner `o` (OWN_MAX = none) add 1
-// to ctr[2 o] — one LDS atomic per distinct owner in the wave (<= W), not one
-// per lane (a W = 1 or 2 merge would serialise 64 lanes on one address).
-// Returns this lane's rank among all adds to its counter.
-__device__ __forceinline__ unsigned long long wave_owner_add(unsigned long long* ctr, uint32_t o) {
+// Wave-aggregated LDS counter adds: lanes with owner `o` (OWN_MAX = none) add 1
+// to ctr[2 o] and `bytes` to ctr[2 o + 1] — two LDS atomics per distinct owner
+// in the wave (<= W), not two per lane (a W = 1 or 2 merge would serialise 64
+// lanes on one address).  Returns this lane's rank among the row adds to its
+// counter; `boff` = its offset among the byte adds.
+__device__ __forceinline__ unsigned long long wave_owner_add(unsigned long long* ctr, uint32_t o, uint32_t bytes,
+                                                             unsigned long long& boff) {
   const int lane = (int)__lane_id();
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   uint64_t pending = __ballot(o != (uint32_t)OWN_MAX);
+  const bool any_bytes = __ballot(bytes != 0) != 0;
   unsigned long long mine = 0;
+  boff = 0;
   while (pending) {
     const int leader = __ffsll((unsigned long long)pending) - 1;
     const uint32_t po = (uint32_t)__shfl((int)o, leader);
-    const uint64_t m = __ballot(o == po);
-    unsigned long long b = 0;
-    if (lane == leader) b = atomicAdd(&ctr[2 * po], (unsigned long long)__popcll(m));
+    const bool in = o == po;
+    const uint64_t m = __ballot(in);
+    uint32_t incl = 0, total = 0;  // inclusive wave scan of this owner's byte counts
+    if (any_bytes) {
+      incl = in ? bytes : 0u;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
+        if (lane >= d) incl += y;
+      }
+      total = (uint32_t)__shfl((int)incl, 63);
+    }
+    unsigned long long b = 0, bb = 0;
+    if (lane == leader) {
+      b = atomicAdd(&ctr[2 * po], (unsigned long long)__popcll(m));
+      if (total) bb = atomicAdd(&ctr[2 * po + 1], (unsigned long long)total);
+    }
     b = __shfl(b, leader);
-    if (o == po) mine = b + (unsigned long long)__popcll(m & lt);
+    bb = __shfl(bb, leader);
+    if (in) {
+      mine = b + (unsigned long long)__popcll(m & lt);
+      boff = bb + incl - bytes;
+    }
     pending &= ~m;
   }
   return mine;
@@ -73,10 +95,16 @@ __global__ void __launch_bounds__(256) wc_owner_count(const uint64_t* k0, const 
   __shared__ unsigned long long h[2 * OWN_MAX];
   for (uint32_t i = threadIdx.x; i < 2 * W; i += blockDim.x) h[i] = 0;
   __syncthreads();
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t o = owner_of(place_hash(k0[i], k1[i]), W);
-    if (key_is_hashed(k1[i])) atomicAdd(&h[2 * o + 1], (unsigned long long)slen[i]);
-    (void)wave_owner_add(h, o);
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 < n; i0 += stride) {  // whole waves call the wave op
+    const uint64_t i = i0 + threadIdx.x;
+    uint32_t o = OWN_MAX, nb = 0;
+    if (i < n) {
+      o = owner_of(place_hash(k0[i], k1[i]), W);
+      if (key_is_hashed(k1[i])) nb = slen[i];
+    }
+    unsigned long long bo;
+    (void)wave_owner_add(h, o, nb, bo);
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < 2 * W; i += blockDim.x)
@@ -103,12 +131,12 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
   for (int j = 0; j < PER; ++j) {
     const uint64_t i = r0 + threadIdx.x + (uint64_t)j * 256;
     own[j] = OWN_MAX;
-    lb[j] = 0;
+    uint32_t nb = 0;
     if (i < n) {
       own[j] = owner_of(place_hash(k0[i], k1[i]), W);
-      if (key_is_hashed(k1[i])) lb[j] = atomicAdd(&h[2 * own[j] + 1], (unsigned long long)slen[i]);
+      if (key_is_hashed(k1[i])) nb = slen[i];
     }
-    lr[j] = wave_owner_add(h, own[j]);
+    lr[j] = wave_owner_add(h, own[j], nb, lb[j]);
   }
   __syncthreads();
   if (threadIdx.x == 0) {

@@ -78,7 +78,7 @@ def main():
             m = r[name]
             V = m["keys"]
             merge = m["merge"] - m["local"]
-            root = name == "shuffle" and W_MODEL * V <= (1 << 21)  # MERGE_ROOT_MAX_ROWS
+            root = name == "shuffle" and W_MODEL * V <= (1 << 18)  # MERGE_ROOT_MAX_ROWS
             w = wire_us(V, W_MODEL, mode == 1, root)
             print(f"| {vocab} | {V} | {name} | {m['local']:.3f} | {m['merge']:.3f} | {merge:.3f} | {w:.1f} |"
                   f" {merge + w / 1e3:.3f} |", flush=True)
