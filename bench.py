@@ -112,9 +112,16 @@ def main() -> int:
         # generated natively in place on 16 threads (no pageable copy)
         pool_bytes = int((a.pool_gb if a.pool_gb is not None else cfg.pool_bytes / gib) * gib)
         pool_bytes = max(chunk, pool_bytes // chunk * chunk)
+        def rss_now():
+            with open("/proc/self/statm") as f:
+                return int(f.read().split()[1]) * os.sysconf("SC_PAGE_SIZE")
+
+        rss_before = rss_now()  # interpreter + torch + HIP runtime, before the pool exists
         pool = HostPool(pool_bytes, first_segment=first_seg, seed=seed, vocab=vocab, zipf_s=zipf, threads=16)
+        peak = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024
         pool_info = {"pool_bytes": pool_bytes, "build_s": round(pool.build_seconds, 3),
-                     "peak_rss_bytes": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024}
+                     "rss_before_pool_bytes": rss_before, "peak_rss_bytes": peak,
+                     "pool_rss_ratio": round((peak - rss_before) / pool_bytes, 4)}
     else:
         eng.synth_device(nbytes, first_segment=first_seg, seed=seed, vocab=vocab, zipf_s=zipf)
 

@@ -59,11 +59,14 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   WC_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   WC_HIP_CHECK(hipStreamCreateWithFlags(&copy_s, hipStreamNonBlocking));
   map_blocks = opt.map_blocks ? opt.map_blocks : MAP_BLOCKS_PER_CU * (uint32_t)device_cu_count(dev);
+  map_blocks = std::min<uint32_t>(map_blocks, RED_MAX_RUNS);
   if (const char* e = std::getenv("WC_SYNC_DEBUG")) sync_debug = std::atoi(e) != 0;
   k1_mask = k1_hash_mask(opt.k1_hash_bits);
   if (const char* e = std::getenv("WC_MAP_STAMPS"); e && std::atoi(e)) {
     WC_HIP_CHECK(hipMalloc(&d_stamps, MAP_STAMP_N * 8));
     WC_HIP_CHECK(hipMemset(d_stamps, 0, MAP_STAMP_N * 8));
+    WC_HIP_CHECK(hipMalloc(&d_red_stamps, RED_STAMP_N * 8));
+    WC_HIP_CHECK(hipMemset(d_red_stamps, 0, RED_STAMP_N * 8));
   }
 
   opt.log2_rec_buckets = std::min<uint32_t>(opt.log2_rec_buckets, MAX_REC_BUCKETS_LOG2);
@@ -77,9 +80,9 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   rec_total = std::max<uint64_t>(opt.min_records, (uint64_t)((double)opt.chunk_bytes * opt.records_per_byte));
   // record store + per-(block, bucket) counts; partitions follow the table up to the max
   const size_t ncount = (size_t)map_blocks * MAX_REC_BUCKETS;
-  rec_mem.reserve(rec_total * (sizeof(Rec) + sizeof(Rec16)) + ncount * 4 + 8192);
+  rec_mem.reserve(rec_total * (sizeof(Rec) + sizeof(Rec12)) + ncount * 4 + 8192);
   rec.recs = rec_mem.take_n<Rec>(rec_total);
-  rec.recs16 = rec_mem.take_n<Rec16>(rec_total);
+  rec.recs12 = rec_mem.take_n<Rec12>(rec_total);
   rec.cap = rec_total;
   rec.count = rec_mem.take_n<uint32_t>(ncount);
 
@@ -142,6 +145,19 @@ Engine::Impl::~Impl() {
     }
     (void)hipFree(d_stamps);
   }
+  if (d_red_stamps) {
+    unsigned long long h[RED_STAMP_N];
+    if (hipMemcpy(h, d_red_stamps, sizeof h, hipMemcpyDeviceToHost) == hipSuccess && h[RS_RECORDS]) {
+      fprintf(stderr,
+              "[wc] reduce counters: records %llu, slow lanes %llu, slow wave-steps %llu, claim-loop iterations %llu, "
+              "CAS failures %llu, PENDING re-reads %llu, claims %llu; run phase / wave lifetime = %.3f; blocks %llu, "
+              "mean wave lifetime %.0f clk, slowest block %llu clk\n",
+              h[RS_RECORDS], h[RS_SLOW_LANES], h[RS_SLOW_WAVES], h[RS_PROBE_ITERS], h[RS_CAS_FAIL], h[RS_PENDING],
+              h[RS_CLAIMS], h[RS_T_WAVE] ? (double)h[RS_T_RUNS] / h[RS_T_WAVE] : 0.0, h[RS_BLOCKS],
+              h[RS_BLOCKS] ? (double)h[RS_T_WAVE] / (h[RS_BLOCKS] * (RED_THREADS / 64)) : 0.0, h[RS_T_BLKMAX]);
+    }
+    (void)hipFree(d_red_stamps);
+  }
   if (registered) (void)hipHostUnregister(const_cast<uint8_t*>(registered));
   if (s) (void)hipStreamDestroy(s);
   if (copy_s) (void)hipStreamDestroy(copy_s);
@@ -196,7 +212,7 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   }
   ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                 avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
-                d_ctr->flags, d_bucket_ovf, nullptr};
+                d_ctr->flags, d_bucket_ovf, nullptr, d_red_stamps};
   launch_reduce(ra, s);
   if (sync_debug) {
     const hipError_t e = hipStreamSynchronize(s);
@@ -263,7 +279,7 @@ void Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
     WC_HIP_CHECK(hipMemsetAsync(d_ctr, 0, sizeof(DevCounters), s));
     ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                   avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
-                  d_ctr->flags, d_bucket_ovf, d_bucket_en};
+                  d_ctr->flags, d_bucket_ovf, d_bucket_en, d_red_stamps};
     launch_reduce(ra, s);
     WC_HIP_CHECK(hipMemcpyAsync(h_ctr, d_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));
     WC_HIP_CHECK(hipStreamSynchronize(s));

@@ -30,6 +30,7 @@ constexpr int MAX_REC_BUCKETS_LOG2 = 9;              // shuffle partitions <= 51
 constexpr int MAX_REC_BUCKETS = 1 << MAX_REC_BUCKETS_LOG2;
 
 constexpr int RED_THREADS = 1024;                    // 16 waves, one block per CU
+constexpr int RED_MAX_RUNS = 1024;                   // map blocks per pass (the reducer stages their run counts in LDS)
 constexpr int TAB_SLOTS_LOG2 = 12;
 constexpr int TAB_SLOTS = 1 << TAB_SLOTS_LOG2;       // 4096 slots x 32 B = 128 KiB LDS
 constexpr int TAB_MAX_OCC = TAB_SLOTS * 7 / 8;       // overflow -> split the table
@@ -44,27 +45,28 @@ enum : int { FLAG_REGION_OVF = 0, FLAG_ARENA_OVF = 1, FLAG_TABLE_OVF = 2, FLAG_M
 struct Rec {
   uint64_t k0, k1, co;
 };
-// Short-key record (k1 = length <= 8): 16 bytes, w = off | len << 32 | count << 36.
-struct Rec16 {
-  uint64_t k0, w;
+// One occurrence of a short word (k1 = length <= 8) whose last byte is nonzero,
+// so k0 implies the length (keys.hpp implied_len): 12 bytes, count 1.  Every
+// other record — counted hot-slot flushes included — is a 24-byte Rec.
+struct Rec12 {
+  uint32_t lo, hi, off;  // k0 = lo | hi << 32; chunk-relative offset
 };
-constexpr uint32_t REC16_MAX_COUNT = (1u << 28) - 1;  // counts of one map window stay far below
 
-// Shuffle output.  Two record stores (short keys as 16-B Rec16, long keys as
-// 24-B Rec), each split into one sub-region of `subcap` records per (map block
-// p, shuffle bucket b):
-//   recs16[(p * nb + b) * subcap + i],  i < count[p * nb + b] & 0xFFFF
+// Shuffle output.  Two record stores (single short-word occurrences as 12-B
+// Rec12, everything else as 24-B Rec), each split into one sub-region of
+// `subcap` records per (map block p, shuffle bucket b):
+//   recs12[(p * nb + b) * subcap + i],  i < count[p * nb + b] & 0xFFFF
 //   recs  [(p * nb + b) * subcap + i],  i < count[p * nb + b] >> 16
 // A map flush appends each emitted slot to its bucket's sub-region through a
 // per-bucket LDS cursor (no histogram, no scan, no directory); the reducer of
 // bucket b reads one contiguous run per map block.  A full sub-region sets
 // FLAG_REGION_OVF and the host re-runs the chunk in halves.
 struct Records {
-  Rec* recs;                   // long-key records
-  Rec16* recs16;               // short-key records
+  Rec* recs;                   // 24-byte records
+  Rec12* recs12;               // single short-word occurrences
   unsigned long long* cursor;  // records emitted (stats)
   uint64_t cap;                // record capacity of each store
-  uint32_t* count;             // [map_blocks * nb] short (low 16 bits) | long (high 16) records appended
+  uint32_t* count;             // [map_blocks * nb] Rec12 (low 16 bits) | Rec (high 16) records appended
   uint32_t subcap;             // records per sub-region, <= 65535 (cap / (map_blocks * nb) of the pass)
 };
 
@@ -134,7 +136,11 @@ struct ReduceArgs {
   uint32_t* flags;
   uint32_t* bucket_overflow;      // [n_buckets] set when a slice overflowed
   const uint8_t* bucket_enable;   // nullptr = all
+  unsigned long long* stamps;     // [RED_STAMP_N] diagnostic counters (WC_RED_STAMPS builds), nullable
 };
+// Reduce diagnostic counters (src/kernels/reduce.hip built with -DWC_RED_STAMPS=1).
+enum : int { RS_RECORDS = 0, RS_SLOW_LANES, RS_SLOW_WAVES, RS_PROBE_ITERS, RS_CAS_FAIL, RS_PENDING, RS_CLAIMS,
+             RS_T_WAVE, RS_T_SLOW, RS_T_RUNS, RS_BLOCKS, RS_T_BLKMAX, RED_STAMP_N };
 
 struct SynthVocab {
   const uint8_t* bytes;

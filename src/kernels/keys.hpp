@@ -92,6 +92,10 @@ WC_HD uint32_t place_hash(uint64_t k0, uint64_t k1) {
   return mix32(a ^ (b * 0x9E3779B1u) ^ (c * 0x85EBCA77u));
 }
 
+// Length of a short word implied by its k0: bytes up to the highest nonzero one
+// (0 for k0 = 0).  Equals the length iff the word's last byte is not 0x00.
+WC_HD uint32_t implied_len(uint64_t k0) { return k0 ? (71u - (uint32_t)__builtin_clzll(k0)) >> 3 : 0u; }
+
 // Nested: the bucket under 2B buckets is b or b + B for bucket b under B.
 WC_HD uint32_t bucket_of(uint32_t ph, uint32_t log2_buckets) { return ph & ((1u << log2_buckets) - 1u); }
 

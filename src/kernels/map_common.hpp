@@ -114,64 +114,54 @@ struct PhaseClock {
   }
 };
 
-// Append one record (key, count, first offset) to bucket b's sub-region of this
-// block: a 16-byte record for SHORT keys (k1 = length <= 8), else 24 bytes.
-// bcur[b] packs both cursors (short count | long count << 16).
-__device__ __forceinline__ void emit_record(uint32_t* bcur, const MapArgs& a, uint32_t b, uint64_t k0, uint64_t k1,
-                                            uint64_t cnt, uint32_t off) {
+// Record format of a key with count cnt: 12-byte Rec12 (single occurrence of a
+// short word with an implied length) or 24-byte Rec.
+__device__ __forceinline__ bool rec12_fits(uint64_t k0, uint64_t k1, uint64_t cnt) {
+  return cnt == 1 && k1 <= 8 && implied_len(k0) == (uint32_t)k1;
+}
+
+// Store one record at position `packed`'s cursor of bucket b's sub-region of this block.
+__device__ __forceinline__ void put_record(const MapArgs& a, uint32_t b, uint32_t packed, bool r12, uint64_t k0,
+                                          uint64_t k1, uint64_t cnt, uint32_t off) {
   const uint64_t sub = a.rec.subcap;
   const uint64_t at = ((uint64_t)blockIdx.x << a.log2_rec_buckets | b) * sub;
-  const bool shortk = k1 <= 8 && cnt <= REC16_MAX_COUNT;
-  const uint32_t packed = atomicAdd(&bcur[b], shortk ? 1u : 0x10000u);
-  const uint32_t pos = shortk ? (packed & 0xFFFFu) : (packed >> 16);
-  if (pos < sub) {
-    if (shortk) {
-      Rec16 r;
-      r.k0 = k0;
-      r.w = (uint64_t)off | (k1 << 32) | (cnt << 36);
-      a.rec.recs16[at + pos] = r;
-    } else {
-      Rec r;
-      r.k0 = k0;
-      r.k1 = k1;
-      r.co = (cnt << 32) | off;
-      a.rec.recs[at + pos] = r;
-    }
-  } else {
+  const uint32_t pos = r12 ? (packed & 0xFFFFu) : (packed >> 16);
+  if (pos >= sub) {
     atomicOr(&a.flags[FLAG_REGION_OVF], 1u);
+  } else if (r12) {
+    Rec12 r;
+    r.lo = (uint32_t)k0;
+    r.hi = (uint32_t)(k0 >> 32);
+    r.off = off;
+    a.rec.recs12[at + pos] = r;
+  } else {
+    Rec r;
+    r.k0 = k0;
+    r.k1 = k1;
+    r.co = (cnt << 32) | off;
+    a.rec.recs[at + pos] = r;
   }
 }
 
-// Two records of one lane (either may be absent): both cursor atomics are
-// issued before either store waits for its position.
+// Append one record (key, count, first offset) to bucket b's sub-region of
+// this block; bcur[b] packs both cursors (Rec12 count | Rec count << 16).
+__device__ __forceinline__ void emit_record(uint32_t* bcur, const MapArgs& a, uint32_t b, uint64_t k0, uint64_t k1,
+                                            uint64_t cnt, uint32_t off) {
+  const bool r12 = rec12_fits(k0, k1, cnt);
+  put_record(a, b, atomicAdd(&bcur[b], r12 ? 1u : 0x10000u), r12, k0, k1, cnt, off);
+}
+
+// Two single-occurrence records of one lane (either may be absent): both
+// cursor atomics are issued before either store waits for its position.
 __device__ __forceinline__ void emit_two(uint32_t* bcur, const MapArgs& a, bool d1, uint32_t b1, uint64_t x0,
                                          uint64_t x1, uint32_t o1, bool d2, uint32_t b2, uint64_t y0, uint64_t y1,
                                          uint32_t o2) {
-  const uint64_t sub = a.rec.subcap;
-  const bool s1 = x1 <= 8, s2 = y1 <= 8;
+  const bool s1 = rec12_fits(x0, x1, 1), s2 = rec12_fits(y0, y1, 1);
   uint32_t p1 = 0, p2 = 0;
   if (d1) p1 = atomicAdd(&bcur[b1], s1 ? 1u : 0x10000u);
   if (d2) p2 = atomicAdd(&bcur[b2], s2 ? 1u : 0x10000u);
-  auto put = [&](uint32_t b, uint32_t packed, bool sk, uint64_t k0, uint64_t k1, uint32_t off) {
-    const uint64_t at = ((uint64_t)blockIdx.x << a.log2_rec_buckets | b) * sub;
-    const uint32_t pos = sk ? (packed & 0xFFFFu) : (packed >> 16);
-    if (pos >= sub) {
-      atomicOr(&a.flags[FLAG_REGION_OVF], 1u);
-    } else if (sk) {
-      Rec16 r;
-      r.k0 = k0;
-      r.w = (uint64_t)off | (k1 << 32) | (1ull << 36);
-      a.rec.recs16[at + pos] = r;
-    } else {
-      Rec r;
-      r.k0 = k0;
-      r.k1 = k1;
-      r.co = (1ull << 32) | off;
-      a.rec.recs[at + pos] = r;
-    }
-  };
-  if (d1) put(b1, p1, s1, x0, x1, o1);
-  if (d2) put(b2, p2, s2, y0, y1, o2);
+  if (d1) put_record(a, b1, p1, s1, x0, x1, 1, o1);
+  if (d2) put_record(a, b2, p2, s2, y0, y1, 1, o2);
 }
 
 // Key of a token whose length is unknown inside the lane window (MAP_LONG) or

@@ -21,12 +21,34 @@
 //  wc_table_split     B -> 2B buckets (rehash into new slices).
 //  wc_table_compact   occupied slots -> dense columns (per-bucket block scan).
 #include "kernels.hpp"
+
 #include "lds_table.hpp"
+
+// Diagnostic build (-DWC_RED_STAMPS=1, tools/variants.sh; run with WC_MAP_STAMPS=1):
+// per-block LDS counters of records, slow-path lanes / waves, claim-loop
+// iterations, CAS failures, PENDING re-reads, claims and s_memtime wave time.
+#ifndef WC_RED_STAMPS
+#define WC_RED_STAMPS 0
+#endif
 
 namespace wc {
 namespace dev {
 
-constexpr int RED_UNROLL = 8;
+// Profiling builds only (tools/variants.sh -DWC_RED_ABLATE=N; results NOT
+// valid): 1 record loads only, 2 + hashes and both probe reads, 3 everything
+// but the hit atomics.
+#ifndef WC_RED_ABLATE
+#define WC_RED_ABLATE 0
+#endif
+
+#ifndef WC_RED_UNROLL
+#define WC_RED_UNROLL 4
+#endif
+constexpr int RED_UNROLL = WC_RED_UNROLL;  // 12-byte records in flight per lane
+#ifndef WC_RED_UNROLL_24
+#define WC_RED_UNROLL_24 2
+#endif
+constexpr int RED_UNROLL_24 = WC_RED_UNROLL_24;  // 24-byte records in flight per lane (VGPR budget)
 constexpr int LONGQ = 2048;  // LONG records queued per bucket pass (more: re-scan in batches)
 
 struct RedLds {
@@ -38,6 +60,8 @@ struct RedLds {
   uint32_t overflow;
   uint32_t nlong, nmiss;
   uint32_t long_ovf;          // more LONG records than LONGQ: re-scan the 24-byte runs
+  uint32_t runcnt[RED_MAX_RUNS];  // packed record counts of this bucket's run in every map block
+  unsigned long long st[RED_STAMP_N];  // diagnostic counters (WC_RED_STAMPS builds only)
 };
 static_assert(sizeof(RedLds) <= 160 * 1024, "one reduce block per CU");
 
@@ -108,25 +132,138 @@ __device__ __forceinline__ bool bytes_equal(const uint8_t* x, const uint8_t* y, 
   return true;
 }
 
-__device__ __forceinline__ void merge_record(RedLds& L, const ReduceArgs& a, uint32_t b, uint64_t k0, uint64_t k1,
-                                             uint64_t cnt, uint32_t off, uint32_t shift, uint32_t idx) {
-  const uint32_t ph = place_hash(k0, k1);
-  if (shift && bucket_of(ph, a.tab.log2_buckets) != b) return;
-  if (key_is_hashed(k1)) {  // LONG: merged after the byte comparison (long_phase)
-    const uint32_t q = atomicAdd(&L.nlong, 1u);
-    if (q < (uint32_t)LONGQ) L.longq[q] = idx;
-    else L.long_ovf = 1;
-    return;
-  }
+// Count + first offset into slot s.
+__device__ __forceinline__ void add_to_slot(RedLds& L, int s, uint64_t cnt, uint64_t first) {
+  atomicAdd(reinterpret_cast<unsigned long long*>(&L.cnt[s]), (unsigned long long)cnt);
+  atomicMin(reinterpret_cast<unsigned long long*>(&L.first[s]), (unsigned long long)first);
+}
+
+// A key not found in its home group: full probe, claiming a slot if new.
+#ifndef WC_RED_SLOW_INLINE
+#define WC_RED_SLOW_INLINE 0
+#endif
+#if WC_RED_SLOW_INLINE
+#define WC_RED_SLOW_ATTR __forceinline__
+#else
+#define WC_RED_SLOW_ATTR __noinline__  // one copy: keeps the unrolled batch loop small in the instruction cache
+#endif
+// Returns 1 if it claimed a new slot (the caller counts occupancy per wave:
+// a per-lane atomic on one LDS word serialised every claim of the block).
+__device__ WC_RED_SLOW_ATTR uint32_t merge_slow(RedLds& L, uint32_t ph, uint64_t k0, uint64_t k1, uint64_t cnt,
+                                            uint64_t first) {
   bool claimed;
-  const int s = lds_find_or_claim(L.grp, TAB_GROUPS, ph, k0, k1, TAB_MAX_GROUP_PROBES, claimed);
+  const int s = lds_find_or_claim(L.grp, TAB_GROUPS, ph, k0, k1, TAB_MAX_GROUP_PROBES, claimed, true,
+                                  WC_RED_STAMPS ? L.st : nullptr);
+  if (WC_RED_STAMPS) atomicAdd(&L.st[RS_SLOW_LANES], 1ull);
   if (s < 0) {
     L.overflow = 1;
+    return 0;
+  }
+  add_to_slot(L, s, cnt, first);
+  return claimed ? 1u : 0u;
+}
+
+// Records [k, k + U * 64) of one run, three phases so a lane keeps all its
+// records' LDS traffic in flight together: (1) load the records, hash them,
+// read the tags of the first two groups of every record's probe sequence (one
+// LDS round trip for all); (2) read k1 / k0 of the first slot whose tag
+// matches (a second round trip); (3) a key match counts with two LDS atomics.
+// A record with no matching slot in those groups — a new key, a key placed
+// further along its sequence, a tag collision — takes merge_slow.  LONG keys (hashed, 24-byte runs
+// only) are queued for the byte comparison.
+template <class RecT, int U>
+__device__ __forceinline__ void load_batch(RecT (&rr)[U], const RecT* run, uint32_t n, uint32_t k) {
+  const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+  for (int u = 0; u < U; ++u) rr[u] = run[min(k + u * 64 + lane, n - 1)];  // clamp (n > 0): always valid
+}
+
+template <bool R12, int U, class RecT>
+__device__ __forceinline__ void merge_batch(RedLds& L, const ReduceArgs& a, uint32_t b, const RecT (&rr)[U],
+                                            uint32_t n, uint32_t k, uint64_t sr, uint32_t shift, uint32_t& claims) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  uint64_t k0[U], k1[R12 ? 1 : U];  // Rec12: the length is recomputed from k0 (VGPR budget)
+  uint32_t ph[U], slot[U];
+  auto key1 = [&](int u) -> uint64_t {
+    if constexpr (R12) return implied_len(k0[u]);
+    else return k1[u];
+  };
+  bool mine[U];
+  u32x4 tg[U], tg2[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if constexpr (R12) {
+      k0[u] = rr[u].lo | ((uint64_t)rr[u].hi << 32);
+    } else {
+      k0[u] = rr[u].k0;
+      k1[u] = rr[u].k1;
+    }
+    if (WC_RED_ABLATE == 1) {
+      if (k0[u] == 0x9E3779B97F4A7C15ull) L.overflow = 2;  // never true: keeps the load
+      continue;
+    }
+    ph[u] = place_hash(k0[u], key1(u));
+    const uint32_t i = k + u * 64 + lane;
+    mine[u] = i < n && (!shift || bucket_of(ph[u], a.tab.log2_buckets) == b);
+    if (!R12 && mine[u] && key_is_hashed(key1(u))) {
+      const uint32_t q = atomicAdd(&L.nlong, 1u);
+      if (q < (uint32_t)LONGQ) L.longq[q] = (uint32_t)(sr + i);
+      else L.long_ovf = 1;
+      mine[u] = false;
+    }
+    tg[u] = *reinterpret_cast<const u32x4*>(L.grp[group_of(ph[u], TAB_GROUPS)].tag);
+    tg2[u] = *reinterpret_cast<const u32x4*>(L.grp[group2_of(ph[u], TAB_GROUPS)].tag);
+  }
+  if (WC_RED_ABLATE == 1) return;
+  uint64_t c1[U], c0[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t tag = make_tag(ph[u]);
+    const uint32_t m = (tg[u].x == tag ? 1u : 0u) | (tg[u].y == tag ? 2u : 0u) | (tg[u].z == tag ? 4u : 0u) |
+                       (tg[u].w == tag ? 8u : 0u) | (tg2[u].x == tag ? 16u : 0u) | (tg2[u].y == tag ? 32u : 0u) |
+                       (tg2[u].z == tag ? 64u : 0u) | (tg2[u].w == tag ? 128u : 0u);
+    const uint32_t f = (uint32_t)__ffs(m) - 1u;  // first candidate (g1 before g2)
+    slot[u] = m ? 4 * (f < 4 ? group_of(ph[u], TAB_GROUPS) : group2_of(ph[u], TAB_GROUPS)) + (f & 3) : 0xFFFFFFFFu;
+    const uint32_t s = m ? slot[u] : 0u;
+    c1[u] = slot_k1(L.grp, (int)s);
+    c0[u] = slot_k0(L.grp, (int)s);
+  }
+  if (WC_RED_ABLATE == 2) {
+    uint64_t x = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) x ^= c0[u] ^ c1[u];
+    if (x == 0x9E3779B97F4A7C15ull) L.overflow = 2;  // never true
     return;
   }
-  atomicAdd(reinterpret_cast<unsigned long long*>(&L.cnt[s]), (unsigned long long)cnt);
-  atomicMin(reinterpret_cast<unsigned long long*>(&L.first[s]), (unsigned long long)(a.chunk_base + off));
-  if (claimed && atomicAdd(&L.occupied, 1u) + 1 > (uint32_t)TAB_MAX_OCC) L.overflow = 1;
+  if (WC_RED_STAMPS && lane == 0) {
+    uint32_t nrec = 0;
+    for (uint32_t u = 0; u < (uint32_t)U; ++u) nrec += min(64u, n > k + u * 64 ? n - (k + u * 64) : 0u);
+    atomicAdd(&L.st[RS_RECORDS], (unsigned long long)nrec);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (WC_RED_STAMPS) {
+      const bool slow = mine[u] && !(slot[u] != 0xFFFFFFFFu && c1[u] == key1(u) && c0[u] == k0[u]);
+      if (__ballot(slow) && lane == 0) atomicAdd(&L.st[RS_SLOW_WAVES], 1ull);
+    }
+    if (!mine[u]) continue;
+    uint64_t cnt;
+    uint32_t off;
+    if constexpr (R12) {
+      cnt = 1;
+      off = rr[u].off;
+    } else {
+      cnt = rr[u].co >> 32;
+      off = (uint32_t)rr[u].co;
+    }
+    const uint64_t first = a.chunk_base + off;
+    if (slot[u] != 0xFFFFFFFFu && c1[u] == key1(u) && c0[u] == k0[u]) {
+      if (WC_RED_ABLATE != 3) add_to_slot(L, (int)slot[u], cnt, first);
+    } else {
+      claims += merge_slow(L, ph[u], k0[u], key1(u), cnt, first);
+    }
+  }
 }
 
 // LONG records longq[0, n) of bucket b (all threads of the block):
@@ -146,8 +283,8 @@ __device__ void long_batch(RedLds& L, const ReduceArgs& a, uint32_t b, uint32_t 
     const uint32_t off = (uint32_t)r.co;
     const uint64_t len = word_len(a, off);
     const uint32_t ph = place_hash(r.k0, r.k1);
-    int s = -1;
-    while ((s = lds_find_next(L.grp, TAB_GROUPS, ph, r.k0, r.k1, s)) >= 0) {
+    int s = -1, cur = -1;
+    while ((s = lds_find_next(L.grp, TAB_GROUPS, ph, r.k0, r.k1, cur)) >= 0) {
       if (a.tab.sref_len[sbase + s] == len && bytes_equal(a.arena.bytes + a.tab.sref_off[sbase + s], a.text + off, len))
         break;
     }
@@ -168,8 +305,8 @@ __device__ void long_batch(RedLds& L, const ReduceArgs& a, uint32_t b, uint32_t 
       const uint32_t off = (uint32_t)r.co;
       const uint64_t len = word_len(a, off);
       const uint32_t ph = place_hash(r.k0, r.k1);
-      int s = -1;
-      while ((s = lds_find_next(L.grp, TAB_GROUPS, ph, r.k0, r.k1, s)) >= 0) {
+      int s = -1, cur = -1;
+      while ((s = lds_find_next(L.grp, TAB_GROUPS, ph, r.k0, r.k1, cur)) >= 0) {
         if (a.tab.sref_len[sbase + s] == len &&
             bytes_equal(a.arena.bytes + a.tab.sref_off[sbase + s], a.text + off, len))
           break;
@@ -200,57 +337,88 @@ __device__ void long_batch(RedLds& L, const ReduceArgs& a, uint32_t b, uint32_t 
   __syncthreads();
 }
 
+// One record kind's stream over this wave's runs (map blocks p = wave,
+// wave + nwaves, ...; run p = sub-region (p, rb), its length in L.runcnt):
+// batches of U x 64 records, each loaded one batch AHEAD of its merge, so a
+// wave always has a batch in flight from HBM while it merges the previous one
+// (unpipelined, every batch waited for its loads: the reduce was latency-bound
+// at ~2 us per batch whatever the record count).
+template <bool R12, int U, class RecT>
+__device__ __forceinline__ void merge_stream(RedLds& L, const ReduceArgs& a, uint32_t b, const RecT* recs, uint32_t wave,
+                                             uint32_t nwaves, uint32_t nrb, uint32_t rb, uint64_t sub, uint32_t shift,
+                                             uint32_t& claims) {
+  auto count = [&](uint32_t p) -> uint32_t {
+    const uint32_t packed = L.runcnt[p];
+    return min(R12 ? (packed & 0xFFFFu) : (packed >> 16), (uint32_t)sub);
+  };
+  // position of a batch: run p, offset k (p >= map_blocks: none)
+  auto first_from = [&](uint32_t p) -> uint32_t {
+    while (p < a.map_blocks && count(p) == 0) p += nwaves;
+    return p;
+  };
+  auto advance = [&](uint32_t& p, uint32_t& k) {
+    k += U * 64;
+    if (k >= count(p)) {
+      p = first_from(p + nwaves);
+      k = 0;
+    }
+  };
+  uint32_t pa = first_from(wave), ka = 0;
+  if (pa >= a.map_blocks) return;
+  RecT ra[U], rb2[U];
+  auto base = [&](uint32_t p) -> uint64_t { return ((uint64_t)p * nrb + rb) * sub; };
+  load_batch(ra, recs + base(pa), count(pa), ka);
+  for (;;) {  // unrolled by two: the register sets swap roles without copies
+    uint32_t pb = pa, kb = ka;
+    advance(pb, kb);
+    if (pb < a.map_blocks) load_batch(rb2, recs + base(pb), count(pb), kb);
+    merge_batch<R12, U>(L, a, b, ra, count(pa), ka, base(pa), shift, claims);
+    if (pb >= a.map_blocks) return;
+    pa = pb;
+    ka = kb;
+    advance(pa, ka);
+    if (pa < a.map_blocks) load_batch(ra, recs + base(pa), count(pa), ka);
+    merge_batch<R12, U>(L, a, b, rb2, count(pb), kb, base(pb), shift, claims);
+    if (pa >= a.map_blocks) return;
+  }
+}
+
 __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   __shared__ RedLds L;
   const uint32_t b = blockIdx.x;
   if (a.bucket_enable && !a.bucket_enable[b]) return;
   if (a.flags[FLAG_REGION_OVF]) return;  // shuffle output incomplete: host re-runs the chunk
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = RED_THREADS / 64;
+  const int tid = threadIdx.x, wave = tid >> 6, nwaves = RED_THREADS / 64;
   load_slice(L, a.tab, b);
+  {
+    const uint32_t rb0 = b & ((1u << a.log2_rec_buckets) - 1u), nrb0 = 1u << a.log2_rec_buckets;
+    for (uint32_t p = tid; p < a.map_blocks; p += RED_THREADS) L.runcnt[p] = a.rec.count[(size_t)p * nrb0 + rb0];
+  }
   if (tid == 0) {
     L.occupied = a.tab.occupancy[b];
     L.overflow = 0;
     L.nlong = 0;
     L.long_ovf = 0;
   }
+  if (WC_RED_STAMPS && tid < RED_STAMP_N) L.st[tid] = 0;
   __syncthreads();
+  const uint64_t t_start = WC_RED_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
 
   const uint32_t shift = a.tab.log2_buckets - a.log2_rec_buckets;  // table buckets per record bucket (log2)
   const uint32_t rb = b & ((1u << a.log2_rec_buckets) - 1u);       // buckets nest on the low bits
   const uint32_t nrb = 1u << a.log2_rec_buckets;
   const uint64_t sub = a.rec.subcap;
-  // one contiguous run per map block: sub-region (p, rb) of the record store
-  for (uint32_t p = wave; p < a.map_blocks; p += nwaves) {
-    const uint32_t packed = a.rec.count[(size_t)p * nrb + rb];
-    const uint64_t sr = ((uint64_t)p * nrb + rb) * sub;
-    // short-key records (16 B): k1 = length, count and offset packed in w
-    const uint32_t n16 = min(packed & 0xFFFFu, (uint32_t)sub);
-    const Rec16* run16 = a.rec.recs16 + sr;
-    for (uint32_t k = 0; k < n16; k += RED_UNROLL * 64) {
-      Rec16 rr[RED_UNROLL];
-#pragma unroll
-      for (int u = 0; u < RED_UNROLL; ++u) rr[u] = run16[min(k + u * 64 + lane, n16 - 1)];  // clamp: always valid
-#pragma unroll
-      for (int u = 0; u < RED_UNROLL; ++u) {
-        if (k + u * 64 + lane >= n16) continue;
-        merge_record(L, a, b, rr[u].k0, (rr[u].w >> 32) & 0xFu, rr[u].w >> 36, (uint32_t)rr[u].w, shift, 0);
-      }
-    }
-    // MEDIUM / LONG records (24 B)
-    const uint32_t n = min(packed >> 16, (uint32_t)sub);
-    const Rec* run = a.rec.recs + sr;
-    for (uint32_t k = 0; k < n; k += RED_UNROLL * 64) {
-      Rec rr[RED_UNROLL];
-#pragma unroll
-      for (int u = 0; u < RED_UNROLL; ++u) rr[u] = run[min(k + u * 64 + lane, n - 1)];  // clamp: always valid
-#pragma unroll
-      for (int u = 0; u < RED_UNROLL; ++u)
-        if (k + u * 64 + lane < n)
-          merge_record(L, a, b, rr[u].k0, rr[u].k1, rr[u].co >> 32, (uint32_t)rr[u].co, shift,
-                       (uint32_t)(sr + k + u * 64 + lane));
-    }
-  }
+  // one contiguous run per map block: sub-region (p, rb) of the record store;
+  // the wave streams the 12-byte records of its runs, then the 24-byte ones
+  uint32_t claims = 0;
+  merge_stream<true, RED_UNROLL>(L, a, b, a.rec.recs12, wave, nwaves, nrb, rb, sub, shift, claims);
+  merge_stream<false, RED_UNROLL_24>(L, a, b, a.rec.recs, wave, nwaves, nrb, rb, sub, shift, claims);
+  for (int o = 32; o > 0; o >>= 1) claims += __shfl_down(claims, o);
+  if ((tid & 63) == 0 && claims) atomicAdd(&L.occupied, claims);
+  if (WC_RED_STAMPS && (tid & 63) == 0)
+    atomicAdd(&L.st[RS_T_RUNS], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
   __syncthreads();
+  if (tid == 0 && L.occupied > (uint32_t)TAB_MAX_OCC) L.overflow = 1;  // too full: split and re-run
   // LONG words: from the queue, or (queue overflow) by re-scanning the 24-byte runs in batches
   if (!L.long_ovf) {
     if (L.nlong) long_batch(L, a, b, L.nlong);
@@ -284,6 +452,17 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   if (tid == 0) {
     a.tab.occupancy[b] = L.occupied;
     atomicMax(&a.flags[FLAG_MAX_OCC], L.occupied);
+  }
+  if (WC_RED_STAMPS && a.stamps) {
+    if ((tid & 63) == 0) atomicAdd(&L.st[RS_T_WAVE], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
+    __syncthreads();
+    if (tid == 0) {
+      L.st[RS_BLOCKS] = 1;
+      L.st[RS_T_BLKMAX] = 0;
+      atomicMax(&a.stamps[RS_T_BLKMAX], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
+    }
+    __syncthreads();
+    if (tid < RED_STAMP_N) atomicAdd(&a.stamps[tid], L.st[tid]);
   }
 }
 
