@@ -75,7 +75,8 @@ WC_HD uint64_t medium_k1(uint64_t tail, uint64_t len) { return tail | (len << 56
 WC_HD uint64_t k1_hash_mask(uint32_t bits) { return bits >= 62 || bits == 0 ? K1_HASH_MASK : ((1ull << bits) - 1); }
 
 // Placement hash of the packed key (32 bits, four 32-bit multiplies — the map
-// computes it once per token): the middle words are pre-mixed by odd-constant
+// computes it once per token; a 24-bit-multiply variant measured no faster in
+// the map and spread keys worse: reduce +25 % at 1M words): the middle words are pre-mixed by odd-constant
 // multiplies, then lowbias32.  Bits [0, log2 B) select the shuffle / table
 // bucket, bits [20, 29) the map combiner group, the high bits the merge owner;
 // the reduce slice group is taken from a multiplied copy so it stays spread

@@ -391,6 +391,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   __syncthreads();
 
   const uint32_t bmask = (1u << a.log2_rec_buckets) - 1u;
+  const RecOut rout = rec_out(a);
   uint8_t* buf = L.buf[wave];
   uint16_t* list = L.list[wave];
   uint32_t my_tokens = 0, my_direct = 0;
@@ -427,7 +428,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
       if (hv) {
         uint64_t k0, k1;
         key_slow(buf, UNIT + HALO, a, q, u0 + q, k0, k1);
-        emit_record(L.bcur, a, place_hash(k0, k1) & bmask, k0, k1, 1, (uint32_t)(u0 + q));
+        emit_record(L.bcur, a, rout, place_hash(k0, k1) & bmask, k0, k1, 1, (uint32_t)(u0 + q));
       }
     }
     my_direct += ndef;
@@ -531,7 +532,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
         if (WC_MAP_ABLATE == 3) return;
         // misses of inline words become records now; LONG words wait for the round end
         const bool d1 = in1 && s1 < 0, d2 = TWO && in2 && s2 < 0;
-        emit_two(L.bcur, a, d1, ha & bmask, a0, a1, o1, d2, hb & bmask, b0, b1, o2);
+        emit_two(L.bcur, a, rout, d1, ha & bmask, a0, a1, o1, d2, hb & bmask, b0, b1, o2);
         const bool f1 = h1 && !in1, f2 = TWO && h2 && !in2;
         const uint64_t mf1 = __ballot(f1), mf2 = TWO ? __ballot(f2) : 0ull;
         if (mf1 | mf2) {  // entries before j are consumed: ndef <= j
@@ -577,7 +578,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     if (!c) continue;
     uint64_t k0, k1;
     sig_key(L.sig[s], L.side[s], k0, k1);
-    emit_record(L.bcur, a, place_hash(k0, k1) & bmask, k0, k1, c, L.off[s]);
+    emit_record(L.bcur, a, rout, place_hash(k0, k1) & bmask, k0, k1, c, L.off[s]);
     ++emitted;
   }
   clk.lap(MS_FLUSH);

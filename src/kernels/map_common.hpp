@@ -114,54 +114,90 @@ struct PhaseClock {
   }
 };
 
+// Profiling builds only (-DWC_EMIT_ABLATE=N, results NOT valid): 1 no record
+// stores, 2 no cursor atomics (lane-derived positions), 3 neither.
+#ifndef WC_EMIT_ABLATE
+#define WC_EMIT_ABLATE 0
+#endif
+#ifndef WC_REC_NT
+#define WC_REC_NT 0  // non-temporal record stores (A/B)
+#endif
+
 // Record format of a key with count cnt: 12-byte Rec12 (single occurrence of a
-// short word with an implied length) or 24-byte Rec.
+// short word whose last byte is nonzero, so keys.hpp implied_len(k0) == k1 —
+// inline keys have zero bytes past the length) or 24-byte Rec.
 __device__ __forceinline__ bool rec12_fits(uint64_t k0, uint64_t k1, uint64_t cnt) {
-  return cnt == 1 && k1 <= 8 && implied_len(k0) == (uint32_t)k1;
+  return cnt == 1 && k1 - 1 < 8 && ((k0 >> (8 * (k1 - 1))) & 0xFFu) != 0;
 }
 
-// Store one record at position `packed`'s cursor of bucket b's sub-region of this block.
-__device__ __forceinline__ void put_record(const MapArgs& a, uint32_t b, uint32_t packed, bool r12, uint64_t k0,
-                                          uint64_t k1, uint64_t cnt, uint32_t off) {
-  const uint64_t sub = a.rec.subcap;
-  const uint64_t at = ((uint64_t)blockIdx.x << a.log2_rec_buckets | b) * sub;
+// This block's record sub-regions: bucket b's run starts at (b * sub) records
+// from the block base (b * sub < 2^25: 32-bit index math, full-rate multiply).
+struct RecOut {
+  Rec12* b12;
+  Rec* b24;
+  uint32_t sub;
+};
+__device__ __forceinline__ RecOut rec_out(const MapArgs& a) {
+  const uint64_t first = ((uint64_t)blockIdx.x << a.log2_rec_buckets) * a.rec.subcap;
+  return RecOut{a.rec.recs12 + first, a.rec.recs + first, a.rec.subcap};
+}
+
+// Store one record at cursor value `packed` of bucket b's sub-region.
+__device__ __forceinline__ void put_record(const MapArgs& a, const RecOut& o, uint32_t b, uint32_t packed, bool r12,
+                                          uint64_t k0, uint64_t k1, uint64_t cnt, uint32_t off) {
   const uint32_t pos = r12 ? (packed & 0xFFFFu) : (packed >> 16);
-  if (pos >= sub) {
+  const uint32_t idx = __umul24(b, o.sub) + pos;
+  if (pos >= o.sub) {
     atomicOr(&a.flags[FLAG_REGION_OVF], 1u);
   } else if (r12) {
     Rec12 r;
     r.lo = (uint32_t)k0;
     r.hi = (uint32_t)(k0 >> 32);
     r.off = off;
-    a.rec.recs12[at + pos] = r;
+    o.b12[idx] = r;
   } else {
     Rec r;
     r.k0 = k0;
     r.k1 = k1;
     r.co = (cnt << 32) | off;
-    a.rec.recs[at + pos] = r;
+    o.b24[idx] = r;
   }
 }
 
 // Append one record (key, count, first offset) to bucket b's sub-region of
 // this block; bcur[b] packs both cursors (Rec12 count | Rec count << 16).
-__device__ __forceinline__ void emit_record(uint32_t* bcur, const MapArgs& a, uint32_t b, uint64_t k0, uint64_t k1,
-                                            uint64_t cnt, uint32_t off) {
+__device__ __forceinline__ void emit_record(uint32_t* bcur, const MapArgs& a, const RecOut& o, uint32_t b, uint64_t k0,
+                                            uint64_t k1, uint64_t cnt, uint32_t off) {
   const bool r12 = rec12_fits(k0, k1, cnt);
-  put_record(a, b, atomicAdd(&bcur[b], r12 ? 1u : 0x10000u), r12, k0, k1, cnt, off);
+  put_record(a, o, b, atomicAdd(&bcur[b], r12 ? 1u : 0x10000u), r12, k0, k1, cnt, off);
 }
+
+// Profiling builds only (-DWC_EMIT_ABLATE=N, results NOT valid): 1 no record
+// stores, 2 no cursor atomics (lane-derived positions), 3 neither.
+#ifndef WC_EMIT_ABLATE
+#define WC_EMIT_ABLATE 0
+#endif
 
 // Two single-occurrence records of one lane (either may be absent): both
 // cursor atomics are issued before either store waits for its position.
-__device__ __forceinline__ void emit_two(uint32_t* bcur, const MapArgs& a, bool d1, uint32_t b1, uint64_t x0,
-                                         uint64_t x1, uint32_t o1, bool d2, uint32_t b2, uint64_t y0, uint64_t y1,
-                                         uint32_t o2) {
+__device__ __forceinline__ void emit_two(uint32_t* bcur, const MapArgs& a, const RecOut& o, bool d1, uint32_t b1,
+                                         uint64_t x0, uint64_t x1, uint32_t o1, bool d2, uint32_t b2, uint64_t y0,
+                                         uint64_t y1, uint32_t o2) {
   const bool s1 = rec12_fits(x0, x1, 1), s2 = rec12_fits(y0, y1, 1);
   uint32_t p1 = 0, p2 = 0;
-  if (d1) p1 = atomicAdd(&bcur[b1], s1 ? 1u : 0x10000u);
-  if (d2) p2 = atomicAdd(&bcur[b2], s2 ? 1u : 0x10000u);
-  if (d1) put_record(a, b1, p1, s1, x0, x1, 1, o1);
-  if (d2) put_record(a, b2, p2, s2, y0, y1, 1, o2);
+  if (WC_EMIT_ABLATE & 2) {
+    p1 = (__lane_id() & 7) * 0x10001u;
+    p2 = p1 + 0x80008u;
+  } else {
+    if (d1) p1 = atomicAdd(&bcur[b1], s1 ? 1u : 0x10000u);
+    if (d2) p2 = atomicAdd(&bcur[b2], s2 ? 1u : 0x10000u);
+  }
+  if (WC_EMIT_ABLATE & 1) {
+    if ((p1 ^ p2) == 0xFFFFFFFFu) atomicOr(&a.flags[FLAG_COUNT - 1], 0u);  // never true: keeps the atomics
+    return;
+  }
+  if (d1) put_record(a, o, b1, p1, s1, x0, x1, 1, o1);
+  if (d2) put_record(a, o, b2, p2, s2, y0, y1, 1, o2);
 }
 
 // Key of a token whose length is unknown inside the lane window (MAP_LONG) or
