@@ -341,6 +341,54 @@ void Engine::Impl::compact_local() {
   st.log2_buckets = t.log2_buckets;
 }
 
+void Engine::Impl::finalize_local_sorted() {
+  Range r("wc_finalize_local");
+  const TableView& t = table();
+  const size_t nb = (size_t)1 << t.log2_buckets;
+  std::vector<uint32_t> occ(nb);
+  WC_HIP_CHECK(hipMemcpyAsync(occ.data(), t.occupancy, nb * 4, hipMemcpyDeviceToHost, s));
+  unsigned long long arena_used = 0;
+  WC_HIP_CHECK(hipMemcpyAsync(&arena_used, d_arena_cursor, 8, hipMemcpyDeviceToHost, s));
+  WC_HIP_CHECK(hipStreamSynchronize(s));
+  if (h_boff.size() < nb * 8) h_boff.resize(nb * 8);
+  uint64_t* boff = reinterpret_cast<uint64_t*>(h_boff.data());
+  uint64_t n = 0;
+  for (size_t b = 0; b < nb; ++b) {
+    boff[b] = n;
+    n += occ[b];
+  }
+  DeviceArena& A = sort_mem;
+  A.reserve((n + 1) * (2 * 8 + 2 * 4 + 5 * 8 + 4) + nb * 8 + radix_hist_words(n) * 4 + 64 * 1024);
+  A.reset();
+  uint64_t* d_boff = A.take_n<uint64_t>(nb);
+  uint64_t* keys = A.take_n<uint64_t>(n + 1);
+  uint64_t* tkeys = A.take_n<uint64_t>(n + 1);
+  uint32_t* slots = A.take_n<uint32_t>(n + 1);
+  uint32_t* tslots = A.take_n<uint32_t>(n + 1);
+  uint32_t* hist = A.take_n<uint32_t>(radix_hist_words(n));
+  KeyCols o;
+  o.k0 = A.take_n<uint64_t>(n + 1);
+  o.k1 = A.take_n<uint64_t>(n + 1);
+  o.cnt = A.take_n<uint64_t>(n + 1);
+  o.first = A.take_n<uint64_t>(n + 1);
+  o.sref_off = A.take_n<uint64_t>(n + 1);
+  o.sref_len = A.take_n<uint32_t>(n + 1);
+  o.n = n;
+  WC_HIP_CHECK(hipMemcpyAsync(d_boff, boff, nb * 8, hipMemcpyHostToDevice, s));  // pinned: no sync needed
+  launch_table_keys(t, d_boff, keys, slots, s);
+  int bits = 1;
+  while (bits < 64 && (max_end >> bits) != 0) ++bits;
+  bool in_tmp = false;
+  radix_sort_pairs(keys, slots, tkeys, tslots, hist, n, bits, s, &in_tmp);
+  launch_gather_table(t, in_tmp ? tkeys : keys, in_tmp ? tslots : slots, n, o.k0, o.k1, o.cnt, o.first, o.sref_off,
+                      o.sref_len, s);
+  cols = o;
+  cols_arena = d_arena;
+  cols_arena_bytes = std::min<uint64_t>(arena_used, opt.arena_bytes);
+  st.keys = n;
+  st.log2_buckets = t.log2_buckets;
+}
+
 void Engine::Impl::sort_cols_by_first() {
   Range r("wc_finalize_sort");
   const uint64_t n = cols.n;
@@ -365,9 +413,10 @@ void Engine::Impl::sort_cols_by_first() {
   launch_iota_u32(vals, n, s);
   int bits = 1;
   while (bits < 64 && (max_end >> bits) != 0) ++bits;
-  radix_sort_pairs(keys, vals, tkeys, tvals, hist, n, bits, s);
-  launch_gather_cols(cols.k0, cols.k1, cols.cnt, cols.first, cols.sref_off, cols.sref_len, vals, o.k0, o.k1, o.cnt,
-                     o.first, o.sref_off, o.sref_len, n, s);
+  bool in_tmp = false;
+  radix_sort_pairs(keys, vals, tkeys, tvals, hist, n, bits, s, &in_tmp);
+  launch_gather_cols(cols.k0, cols.k1, cols.cnt, cols.first, cols.sref_off, cols.sref_len, in_tmp ? tvals : vals, o.k0,
+                     o.k1, o.cnt, o.first, o.sref_off, o.sref_len, n, s);
   cols = o;
 }
 
@@ -598,17 +647,19 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
   Impl& im = *this;
   WC_HIP_CHECK(hipSetDevice(im.dev));
   const double t0 = now_seconds();
-  im.compact_local();
   // WC_MERGE_ALWAYS=1 (tests): run the merge protocol even with one rank, so
   // the RCCL exchange code is exercised on a one-GPU box
   static const bool merge_always = getenv("WC_MERGE_ALWAYS") && atoi(getenv("WC_MERGE_ALWAYS")) != 0;
   const bool merged = comm && (comm->size() > 1 || merge_always);
   if (merged) {
+    im.compact_local();
     const double tm = now_seconds();
     merge_cols(im, *comm, all_ranks);
     im.st.merge_ms += (now_seconds() - tm) * 1e3;
+    im.sort_cols_by_first();
+  } else {
+    im.finalize_local_sorted();  // sort (first, slot) pairs, gather the columns from the table once
   }
-  im.sort_cols_by_first();
   // the merge's last collectives are still in flight: wait under the comm watchdog
   if (merged) comm->sync(im.s);
   else WC_HIP_CHECK(hipStreamSynchronize(im.s));

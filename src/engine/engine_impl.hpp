@@ -125,6 +125,7 @@ struct Engine::Impl {
 
   uint64_t finalize(Comm* comm, bool all_ranks);  // compact [+ merge] + order by first
   void compact_local();                     // table -> cols (unsorted)
+  void finalize_local_sorted();             // table -> cols ordered by first (no merge: no column copy)
   void sort_cols_by_first();                // cols ordered by first occurrence
   KeyTable download_cols();
 };

@@ -552,7 +552,68 @@ __global__ void __launch_bounds__(1024) wc_table_compact(TableView t, const uint
   }
 }
 
+// As wc_table_compact, but only (first offset, global slot index) per key.
+__global__ void __launch_bounds__(1024) wc_table_keys(TableView t, const uint64_t* bucket_off, uint64_t* keys,
+                                                      uint32_t* slots) {
+  __shared__ uint32_t wsum[16];
+  const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const size_t base = (size_t)b * TAB_SLOTS + 4 * tid;
+  bool occ[4];
+  uint32_t n = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    occ[j] = t.k1[base + j] != K1_EMPTY;
+    n += occ[j];
+  }
+  uint32_t incl = n;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  uint32_t before = 0;
+  for (uint32_t w = 0; w < wave; ++w) before += wsum[w];
+  uint64_t o = bucket_off[b] + before + incl - n;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (!occ[j]) continue;
+    keys[o] = t.first[base + j];
+    slots[o] = (uint32_t)(base + j);
+    ++o;
+  }
+}
+
+// Sorted (first, slot) pairs -> the six key columns, read from the table.
+__global__ void wc_gather_table(TableView t, const uint64_t* keys, const uint32_t* slots, uint64_t n, uint64_t* ok0,
+                                uint64_t* ok1, uint64_t* ocnt, uint64_t* ofirst, uint64_t* osoff, uint32_t* oslen) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t j = slots[i];
+    const uint64_t k1 = t.k1[j];
+    const bool h = key_is_hashed(k1);
+    ok0[i] = t.k0[j];
+    ok1[i] = k1;
+    ocnt[i] = t.cnt[j];
+    ofirst[i] = keys[i];
+    osoff[i] = h ? t.sref_off[j] : 0;
+    oslen[i] = h ? t.sref_len[j] : 0;
+  }
+}
+
 }  // namespace dev
+
+void launch_table_keys(const TableView& t, const uint64_t* bucket_off, uint64_t* keys, uint32_t* slots, hipStream_t s) {
+  hipLaunchKernelGGL(dev::wc_table_keys, dim3(1u << t.log2_buckets), dim3(1024), 0, s, t, bucket_off, keys, slots);
+}
+void launch_gather_table(const TableView& t, const uint64_t* keys, const uint32_t* slots, uint64_t n, uint64_t* ok0,
+                         uint64_t* ok1, uint64_t* ocnt, uint64_t* ofirst, uint64_t* osoff, uint32_t* oslen,
+                         hipStream_t s) {
+  if (!n) return;
+  uint64_t g = (n + 255) / 256;
+  g = g > 4096 ? 4096 : g;
+  hipLaunchKernelGGL(dev::wc_gather_table, dim3((unsigned)g), dim3(256), 0, s, t, keys, slots, n, ok0, ok1, ocnt,
+                     ofirst, osoff, oslen);
+}
 
 void launch_reduce(const ReduceArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(dev::wc_reduce_buckets, dim3(1u << a.tab.log2_buckets), dim3(RED_THREADS), 0, s, a);

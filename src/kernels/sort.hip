@@ -5,7 +5,7 @@
 // free from its serial append, /root/reference/main.cu:97-104) and the
 // deterministic dictionary union of the cross-GPU merge.
 //
-// Per 8-bit digit pass: wc_radix_hist (LDS histogram per 2048-item tile, plus
+// Per digit pass (<= 11 bits): wc_radix_hist (LDS histogram per 2048-item tile, plus
 // the pass's per-digit totals) -> wc_radix_scan (one block per digit: base of
 // the digit + exclusive scan of its row of tile counts; the v8 single-block
 // scan of the whole digit-major array took 195 us at 1M keys, this ~5 us) ->
@@ -25,20 +25,26 @@ constexpr int RS_THREADS = 256;
 constexpr int RS_ROUNDS = 8;
 constexpr int RS_TILE = RS_THREADS * RS_ROUNDS;  // 2048 items per block
 constexpr int RS_WAVES = RS_THREADS / 64;
+constexpr int RS_MAX_DB = 8;                     // digit bits per pass (11-bit digits measured slower: the
+                                                  // per-round LDS work on 2048 bins outweighs one pass fewer)
+constexpr int RS_BINS = 1 << RS_MAX_DB;
 
-__global__ void __launch_bounds__(RS_THREADS) wc_radix_hist(const uint64_t* keys, uint64_t n, int shift,
+__global__ void __launch_bounds__(RS_THREADS) wc_radix_hist(const uint64_t* keys, uint64_t n, int shift, int db,
                                                             uint32_t* hist, uint32_t nblocks, uint32_t* totals) {
-  __shared__ uint32_t h[256];
-  h[threadIdx.x] = 0;
+  __shared__ uint32_t h[RS_BINS];
+  const uint32_t nd = 1u << db, dmask = nd - 1;
+  for (uint32_t d = threadIdx.x; d < nd; d += RS_THREADS) h[d] = 0;
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
   for (int r = 0; r < RS_ROUNDS; ++r) {
     const uint64_t i = base + (uint64_t)r * RS_THREADS + threadIdx.x;
-    if (i < n) atomicAdd(&h[(keys[i] >> shift) & 0xFF], 1u);
+    if (i < n) atomicAdd(&h[(keys[i] >> shift) & dmask], 1u);
   }
   __syncthreads();
-  hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
-  if (h[threadIdx.x]) atomicAdd(&totals[threadIdx.x], h[threadIdx.x]);
+  for (uint32_t d = threadIdx.x; d < nd; d += RS_THREADS) {
+    hist[(size_t)d * nblocks + blockIdx.x] = h[d];
+    if (h[d]) atomicAdd(&totals[d], h[d]);
+  }
 }
 
 // Block d: hist row d (tile counts of digit d, nb words) -> exclusive offsets,
@@ -47,8 +53,9 @@ __global__ void __launch_bounds__(256) wc_radix_scan(uint32_t* hist, uint32_t nb
   __shared__ uint32_t wsum[4];
   const uint32_t d = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // base of digit d
-  uint32_t x = (uint32_t)tid < d ? totals[tid] : 0u;
+  // base of digit d: sum of totals[0, d)
+  uint32_t x = 0;
+  for (uint32_t t = tid; t < d; t += 256) x += totals[t];
   for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o);
   if (lane == 0) wsum[wave] = x;
   __syncthreads();
@@ -88,36 +95,39 @@ __global__ void __launch_bounds__(256) wc_radix_scan(uint32_t* hist, uint32_t nb
 
 __global__ void __launch_bounds__(RS_THREADS) wc_radix_scatter(const uint64_t* keys, const uint32_t* vals,
                                                                uint64_t* okeys, uint32_t* ovals, uint64_t n,
-                                                               int shift, const uint32_t* hist, uint32_t nblocks) {
-  __shared__ uint32_t run[256];             // next output slot per digit
-  __shared__ uint32_t wcnt[RS_WAVES][256];  // per-wave digit counts, then offsets
+                                                               int shift, int db, const uint32_t* hist,
+                                                               uint32_t nblocks) {
+  __shared__ uint32_t run[RS_BINS];             // next output slot per digit
+  __shared__ uint32_t wcnt[RS_WAVES][RS_BINS];  // per-wave digit counts, then offsets
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  run[tid] = hist[(size_t)tid * nblocks + blockIdx.x];
+  const uint32_t nd = 1u << db, dmask = nd - 1;
+  for (uint32_t d = tid; d < nd; d += RS_THREADS) run[d] = hist[(size_t)d * nblocks + blockIdx.x];
   const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   for (int r = 0; r < RS_ROUNDS; ++r) {
-    for (int w = 0; w < RS_WAVES; ++w) wcnt[w][tid] = 0;
+    for (int w = 0; w < RS_WAVES; ++w)
+      for (uint32_t d = tid; d < nd; d += RS_THREADS) wcnt[w][d] = 0;
     __syncthreads();
     const uint64_t i = base + (uint64_t)r * RS_THREADS + tid;
     const bool valid = i < n;
     const uint64_t k = valid ? keys[i] : 0;
-    const uint32_t d = (uint32_t)(k >> shift) & 0xFF;
+    const uint32_t d = (uint32_t)(k >> shift) & dmask;
     uint64_t peers = __ballot(valid);
-    for (int bit = 0; bit < 8; ++bit) {
+    for (int bit = 0; bit < db; ++bit) {  // lanes with equal digits
       const uint64_t bb = __ballot((d >> bit) & 1);
       peers &= ((d >> bit) & 1) ? bb : ~bb;
     }
     const uint32_t rank = (uint32_t)__popcll(peers & lt);
     if (valid && rank == 0) wcnt[wave][d] = (uint32_t)__popcll(peers);
     __syncthreads();
-    {
-      uint32_t acc = run[tid];
+    for (uint32_t e = tid; e < nd; e += RS_THREADS) {
+      uint32_t acc = run[e];
       for (int w = 0; w < RS_WAVES; ++w) {
-        const uint32_t c = wcnt[w][tid];
-        wcnt[w][tid] = acc;
+        const uint32_t c = wcnt[w][e];
+        wcnt[w][e] = acc;
         acc += c;
       }
-      run[tid] = acc;
+      run[e] = acc;
     }
     __syncthreads();
     if (valid) {
@@ -174,29 +184,35 @@ constexpr int RS_MAX_PASSES = 8;  // 64-bit keys
 
 size_t radix_hist_words(uint64_t n) {
   const uint64_t nb = (n + dev::RS_TILE - 1) / dev::RS_TILE;
-  return (size_t)256 * (nb ? nb : 1) + 256 * RS_MAX_PASSES;  // tile counts + per-pass digit totals
+  return (size_t)dev::RS_BINS * (nb ? nb : 1) + (size_t)dev::RS_BINS * RS_MAX_PASSES;  // tile counts + digit totals
 }
 
+// Passes of at most 11 bits, split evenly (30 bits: 3 x 10): fewer passes than
+// 8-bit digits (4) while every digit's tile row still scans in one block.
 void radix_sort_pairs(uint64_t* keys, uint32_t* vals, uint64_t* tmp_keys, uint32_t* tmp_vals, uint32_t* hist,
-                      uint64_t n, int bits, hipStream_t s) {
+                      uint64_t n, int bits, hipStream_t s, bool* in_tmp) {
+  if (in_tmp) *in_tmp = false;
   if (n <= 1 || bits <= 0) return;
   const uint32_t nb = (uint32_t)((n + dev::RS_TILE - 1) / dev::RS_TILE);
-  const int passes = (bits + 7) / 8;
-  uint32_t* totals = hist + (size_t)256 * nb;  // [passes][256]
-  WC_HIP_CHECK(hipMemsetAsync(totals, 0, (size_t)256 * passes * sizeof(uint32_t), s));
+  const int passes = (bits + dev::RS_MAX_DB - 1) / dev::RS_MAX_DB;
+  const int db = (bits + passes - 1) / passes;
+  uint32_t* totals = hist + (size_t)dev::RS_BINS * nb;  // [passes][2^db]
+  WC_HIP_CHECK(hipMemsetAsync(totals, 0, (size_t)dev::RS_BINS * passes * sizeof(uint32_t), s));
   uint64_t *ki = keys, *ko = tmp_keys;
   uint32_t *vi = vals, *vo = tmp_vals;
   for (int p = 0; p < passes; ++p) {
-    const int shift = 8 * p;
-    hipLaunchKernelGGL(dev::wc_radix_hist, dim3(nb), dim3(dev::RS_THREADS), 0, s, ki, n, shift, hist, nb,
-                       totals + 256 * p);
-    hipLaunchKernelGGL(dev::wc_radix_scan, dim3(256), dim3(256), 0, s, hist, nb, totals + 256 * p);
-    hipLaunchKernelGGL(dev::wc_radix_scatter, dim3(nb), dim3(dev::RS_THREADS), 0, s, ki, vi, ko, vo, n, shift, hist,
-                       nb);
+    const int shift = db * p;
+    uint32_t* tot = totals + (size_t)dev::RS_BINS * p;
+    hipLaunchKernelGGL(dev::wc_radix_hist, dim3(nb), dim3(dev::RS_THREADS), 0, s, ki, n, shift, db, hist, nb, tot);
+    hipLaunchKernelGGL(dev::wc_radix_scan, dim3(1u << db), dim3(256), 0, s, hist, nb, tot);
+    hipLaunchKernelGGL(dev::wc_radix_scatter, dim3(nb), dim3(dev::RS_THREADS), 0, s, ki, vi, ko, vo, n, shift, db,
+                       hist, nb);
     std::swap(ki, ko);
     std::swap(vi, vo);
   }
-  if (ki != keys) {  // odd pass count: result lives in tmp
+  if (ki != keys && in_tmp) {  // odd pass count: the caller takes the result from tmp
+    *in_tmp = true;
+  } else if (ki != keys) {
     WC_HIP_CHECK(hipMemcpyAsync(keys, ki, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
     WC_HIP_CHECK(hipMemcpyAsync(vals, vi, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   }
