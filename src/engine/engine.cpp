@@ -78,6 +78,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   opt.chunk_bytes = opt.chunk_bytes / MAP_TILE * MAP_TILE;
 
   rec_total = std::max<uint64_t>(opt.min_records, (uint64_t)((double)opt.chunk_bytes * opt.records_per_byte));
+  rec_total = std::min<uint64_t>(rec_total, 0xFFFFFFFFull);  // record indices are 32-bit in the reducer
   // record store + per-(block, bucket) counts; partitions follow the table up to the max
   const size_t ncount = (size_t)map_blocks * MAX_REC_BUCKETS;
   rec_mem.reserve(rec_total * (sizeof(Rec) + sizeof(Rec12)) + ncount * 4 + 8192);

@@ -171,16 +171,10 @@ __device__ WC_RED_SLOW_ATTR uint32_t merge_slow(RedLds& L, uint32_t ph, uint64_t
 // A record with no matching slot in those groups — a new key, a key placed
 // further along its sequence, a tag collision — takes merge_slow.  LONG keys (hashed, 24-byte runs
 // only) are queued for the byte comparison.
-template <class RecT, int U>
-__device__ __forceinline__ void load_batch(RecT (&rr)[U], const RecT* run, uint32_t n, uint32_t k) {
-  const uint32_t lane = threadIdx.x & 63;
-#pragma unroll
-  for (int u = 0; u < U; ++u) rr[u] = run[min(k + u * 64 + lane, n - 1)];  // clamp (n > 0): always valid
-}
-
 template <bool R12, int U, class RecT>
 __device__ __forceinline__ void merge_batch(RedLds& L, const ReduceArgs& a, uint32_t b, const RecT (&rr)[U],
-                                            uint32_t n, uint32_t k, uint64_t sr, uint32_t shift, uint32_t& claims) {
+                                            const bool (&valid)[U], const uint32_t (&idx)[U], uint32_t shift,
+                                            uint32_t& claims) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const int lane = threadIdx.x & 63;
   uint64_t k0[U], k1[R12 ? 1 : U];  // Rec12: the length is recomputed from k0 (VGPR budget)
@@ -204,11 +198,10 @@ __device__ __forceinline__ void merge_batch(RedLds& L, const ReduceArgs& a, uint
       continue;
     }
     ph[u] = place_hash(k0[u], key1(u));
-    const uint32_t i = k + u * 64 + lane;
-    mine[u] = i < n && (!shift || bucket_of(ph[u], a.tab.log2_buckets) == b);
+    mine[u] = valid[u] && (!shift || bucket_of(ph[u], a.tab.log2_buckets) == b);
     if (!R12 && mine[u] && key_is_hashed(key1(u))) {
       const uint32_t q = atomicAdd(&L.nlong, 1u);
-      if (q < (uint32_t)LONGQ) L.longq[q] = (uint32_t)(sr + i);
+      if (q < (uint32_t)LONGQ) L.longq[q] = idx[u];
       else L.long_ovf = 1;
       mine[u] = false;
     }
@@ -236,10 +229,10 @@ __device__ __forceinline__ void merge_batch(RedLds& L, const ReduceArgs& a, uint
     if (x == 0x9E3779B97F4A7C15ull) L.overflow = 2;  // never true
     return;
   }
-  if (WC_RED_STAMPS && lane == 0) {
+  if (WC_RED_STAMPS) {
     uint32_t nrec = 0;
-    for (uint32_t u = 0; u < (uint32_t)U; ++u) nrec += min(64u, n > k + u * 64 ? n - (k + u * 64) : 0u);
-    atomicAdd(&L.st[RS_RECORDS], (unsigned long long)nrec);
+    for (int u = 0; u < U; ++u) nrec += (uint32_t)__popcll(__ballot(valid[u]));
+    if (lane == 0) atomicAdd(&L.st[RS_RECORDS], (unsigned long long)nrec);
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -338,48 +331,79 @@ __device__ void long_batch(RedLds& L, const ReduceArgs& a, uint32_t b, uint32_t 
 }
 
 // One record kind's stream over this wave's runs (map blocks p = wave,
-// wave + nwaves, ...; run p = sub-region (p, rb), its length in L.runcnt):
-// batches of U x 64 records, each loaded one batch AHEAD of its merge, so a
-// wave always has a batch in flight from HBM while it merges the previous one
-// (unpipelined, every batch waited for its loads: the reduce was latency-bound
-// at ~2 us per batch whatever the record count).
+// wave + nwaves, ...; run p = sub-region (p, rb), its length in L.runcnt),
+// flattened: batches of U x 64 CONSECUTIVE records of the concatenated runs,
+// so batches are full however short the runs are (at 1M words a run holds
+// ~270 12-byte records: per-run batches were half empty, and a wave's time is
+// its batch count x the per-batch LDS round trips).  Each batch is loaded one
+// batch AHEAD of its merge.  Lane j holds run j's exclusive prefix P and
+// index adjustment ADJ = first record index of run j - P; a record at stream
+// position t of run j sits at t + ADJ_j.
 template <bool R12, int U, class RecT>
 __device__ __forceinline__ void merge_stream(RedLds& L, const ReduceArgs& a, uint32_t b, const RecT* recs, uint32_t wave,
-                                             uint32_t nwaves, uint32_t nrb, uint32_t rb, uint64_t sub, uint32_t shift,
+                                             uint32_t nwaves, uint32_t nrb, uint32_t rb, uint32_t sub, uint32_t shift,
                                              uint32_t& claims) {
-  auto count = [&](uint32_t p) -> uint32_t {
-    const uint32_t packed = L.runcnt[p];
-    return min(R12 ? (packed & 0xFFFFu) : (packed >> 16), (uint32_t)sub);
-  };
-  // position of a batch: run p, offset k (p >= map_blocks: none)
-  auto first_from = [&](uint32_t p) -> uint32_t {
-    while (p < a.map_blocks && count(p) == 0) p += nwaves;
-    return p;
-  };
-  auto advance = [&](uint32_t& p, uint32_t& k) {
-    k += U * 64;
-    if (k >= count(p)) {
-      p = first_from(p + nwaves);
-      k = 0;
+  constexpr uint32_t B = U * 64;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t nj = wave < a.map_blocks ? (a.map_blocks - wave + nwaves - 1) / nwaves : 0u;  // <= 64 (RED_MAX_RUNS)
+  uint32_t c = 0;
+  if (lane < nj) {
+    const uint32_t packed = L.runcnt[wave + lane * nwaves];
+    c = min(R12 ? (packed & 0xFFFFu) : (packed >> 16), sub);
+  }
+  uint32_t incl = c;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+    if ((int)lane >= o) incl += y;
+  }
+  const uint32_t N = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  if (N == 0) return;
+  const uint32_t P = incl - c;
+  const uint32_t C0 = (wave * nrb + rb) * sub, D = nwaves * nrb * sub;  // < record capacity < 2^32
+  const uint32_t ADJ = C0 + lane * D - P;                               // modular: t + ADJ is exact
+  uint32_t jlo = 0;  // run holding the current batch start (wave-uniform)
+  auto locate = [&](uint32_t T0, uint32_t (&idx)[U], bool (&valid)[U]) {
+    while (jlo + 1 < nj && (uint32_t)__builtin_amdgcn_readlane((int)P, (int)(jlo + 1)) <= T0) ++jlo;
+    const uint32_t adj = (uint32_t)__builtin_amdgcn_readlane((int)ADJ, (int)jlo);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t t = T0 + u * 64 + lane;
+      idx[u] = t + adj;
+      valid[u] = t < N;
+    }
+    for (uint32_t jj = jlo + 1; jj < nj; ++jj) {  // runs starting inside this batch (usually 0-2)
+      const uint32_t pj = (uint32_t)__builtin_amdgcn_readlane((int)P, (int)jj);
+      if (pj >= T0 + B) break;
+      const uint32_t aj = (uint32_t)__builtin_amdgcn_readlane((int)ADJ, (int)jj);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (T0 + u * 64 + lane >= pj) idx[u] = T0 + u * 64 + lane + aj;
     }
   };
-  uint32_t pa = first_from(wave), ka = 0;
-  if (pa >= a.map_blocks) return;
+  auto load = [&](RecT (&rr)[U], const uint32_t (&idx)[U], const bool (&valid)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) rr[u] = recs[valid[u] ? idx[u] : C0];  // C0: inside the store
+  };
   RecT ra[U], rb2[U];
-  auto base = [&](uint32_t p) -> uint64_t { return ((uint64_t)p * nrb + rb) * sub; };
-  load_batch(ra, recs + base(pa), count(pa), ka);
-  for (;;) {  // unrolled by two: the register sets swap roles without copies
-    uint32_t pb = pa, kb = ka;
-    advance(pb, kb);
-    if (pb < a.map_blocks) load_batch(rb2, recs + base(pb), count(pb), kb);
-    merge_batch<R12, U>(L, a, b, ra, count(pa), ka, base(pa), shift, claims);
-    if (pb >= a.map_blocks) return;
-    pa = pb;
-    ka = kb;
-    advance(pa, ka);
-    if (pa < a.map_blocks) load_batch(ra, recs + base(pa), count(pa), ka);
-    merge_batch<R12, U>(L, a, b, rb2, count(pb), kb, base(pb), shift, claims);
-    if (pa >= a.map_blocks) return;
+  uint32_t ia[U], ib[U];
+  bool va[U], vb[U];
+  locate(0, ia, va);
+  load(ra, ia, va);
+  for (uint32_t T0 = 0;; T0 += 2 * B) {  // unrolled by two: the register sets swap roles without copies
+    const bool more = T0 + B < N;
+    if (more) {
+      locate(T0 + B, ib, vb);
+      load(rb2, ib, vb);
+    }
+    merge_batch<R12, U>(L, a, b, ra, va, ia, shift, claims);
+    if (!more) return;
+    const bool more2 = T0 + 2 * B < N;
+    if (more2) {
+      locate(T0 + 2 * B, ia, va);
+      load(ra, ia, va);
+    }
+    merge_batch<R12, U>(L, a, b, rb2, vb, ib, shift, claims);
+    if (!more2) return;
   }
 }
 
@@ -411,8 +435,8 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   // one contiguous run per map block: sub-region (p, rb) of the record store;
   // the wave streams the 12-byte records of its runs, then the 24-byte ones
   uint32_t claims = 0;
-  merge_stream<true, RED_UNROLL>(L, a, b, a.rec.recs12, wave, nwaves, nrb, rb, sub, shift, claims);
-  merge_stream<false, RED_UNROLL_24>(L, a, b, a.rec.recs, wave, nwaves, nrb, rb, sub, shift, claims);
+  merge_stream<true, RED_UNROLL>(L, a, b, a.rec.recs12, wave, nwaves, nrb, rb, (uint32_t)sub, shift, claims);
+  merge_stream<false, RED_UNROLL_24>(L, a, b, a.rec.recs, wave, nwaves, nrb, rb, (uint32_t)sub, shift, claims);
   for (int o = 32; o > 0; o >>= 1) claims += __shfl_down(claims, o);
   if ((tid & 63) == 0 && claims) atomicAdd(&L.occupied, claims);
   if (WC_RED_STAMPS && (tid & 63) == 0)
