@@ -113,6 +113,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   tab[0].alloc(opt.log2_tab_buckets);
   cur = 0;
   launch_table_clear(table(), s);
+  occ_valid = false;
   WC_HIP_CHECK(hipMemsetAsync(d_bucket_ovf, 0, maxb * sizeof(uint32_t), s));
   WC_HIP_CHECK(hipMemsetAsync(d_arena_cursor, 0, sizeof(unsigned long long), s));
   WC_HIP_CHECK(hipStreamSynchronize(s));
@@ -222,6 +223,36 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
     WC_HIP_CHECK(e);
   }
   WC_HIP_CHECK(hipMemcpyAsync(h_ctr, d_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));
+  enqueue_occupancy();  // read at finalize without a sync of its own
+}
+
+void Engine::Impl::enqueue_occupancy() {
+  const size_t nb = (size_t)1 << table().log2_buckets;
+  if (h_occ.size() < nb * 4 + 8) h_occ.resize(std::max<size_t>(nb * 4 + 8, 4096));
+  WC_HIP_CHECK(hipMemcpyAsync(h_occ.data() + 8, table().occupancy, nb * 4, hipMemcpyDeviceToHost, s));
+  WC_HIP_CHECK(hipMemcpyAsync(h_occ.data(), d_arena_cursor, 8, hipMemcpyDeviceToHost, s));
+}
+
+// Bucket offsets and key count from the occupancy copied with the last pass's
+// counters (that pass synced); a stale copy (table split or cleared since) is
+// refreshed with one sync.
+uint64_t Engine::Impl::host_occupancy(uint64_t*& boff, uint64_t& arena_used) {
+  const size_t nb = (size_t)1 << table().log2_buckets;
+  if (!occ_valid) {
+    enqueue_occupancy();
+    WC_HIP_CHECK(hipStreamSynchronize(s));
+    occ_valid = true;
+  }
+  const uint32_t* occ = reinterpret_cast<const uint32_t*>(h_occ.data() + 8);
+  std::memcpy(&arena_used, h_occ.data(), 8);
+  if (h_boff.size() < nb * 8) h_boff.resize(nb * 8);
+  boff = reinterpret_cast<uint64_t*>(h_boff.data());
+  uint64_t n = 0;
+  for (size_t b = 0; b < nb; ++b) {
+    boff[b] = n;
+    n += occ[b];
+  }
+  return n;
 }
 
 void Engine::Impl::split_table() {
@@ -231,6 +262,7 @@ void Engine::Impl::split_table() {
          " keys); raise max_log2_tab_buckets");
   TableStore& dst = tab[cur ^ 1];
   dst.alloc(lg + 1);
+  occ_valid = false;
   launch_table_clear(dst.v, s);
   launch_table_split(table(), dst.v, s);
   cur ^= 1;
@@ -283,6 +315,7 @@ void Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
                   d_ctr->flags, d_bucket_ovf, d_bucket_en, d_red_stamps};
     launch_reduce(ra, s);
     WC_HIP_CHECK(hipMemcpyAsync(h_ctr, d_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));
+    enqueue_occupancy();
     WC_HIP_CHECK(hipStreamSynchronize(s));
     c = *h_ctr;
     max_occ = std::max(max_occ, c.flags[FLAG_MAX_OCC]);
@@ -295,6 +328,7 @@ void Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
          (unsigned long long)base, (unsigned long long)len, blocks, (unsigned long long)tokens,
          (unsigned long long)c.records);
   max_end = std::max(max_end, base + len);
+  occ_valid = true;  // the copies enqueued with this pass's counters completed at its sync
   if (max_occ >= (uint32_t)TAB_SPLIT_AT && table().log2_buckets < opt.max_log2_tab_buckets) split_table();
 }
 
@@ -309,18 +343,9 @@ void Engine::Impl::compact_local() {
   Range r("wc_finalize_compact");
   const TableView& t = table();
   const size_t nb = (size_t)1 << t.log2_buckets;
-  std::vector<uint32_t> occ(nb);
-  WC_HIP_CHECK(hipMemcpyAsync(occ.data(), t.occupancy, nb * 4, hipMemcpyDeviceToHost, s));
-  unsigned long long arena_used = 0;
-  WC_HIP_CHECK(hipMemcpyAsync(&arena_used, d_arena_cursor, 8, hipMemcpyDeviceToHost, s));
-  WC_HIP_CHECK(hipStreamSynchronize(s));
-  if (h_boff.size() < nb * 8) h_boff.resize(nb * 8);
-  uint64_t* boff = reinterpret_cast<uint64_t*>(h_boff.data());
-  uint64_t n = 0;
-  for (size_t b = 0; b < nb; ++b) {
-    boff[b] = n;
-    n += occ[b];
-  }
+  uint64_t* boff = nullptr;
+  uint64_t arena_used = 0;
+  const uint64_t n = host_occupancy(boff, arena_used);
   // columns x2 (sorted copy) + sort scratch + hist
   const size_t per = 5 * 8 + 4;
   fin_mem.reserve(std::max<size_t>(1 << 20, (n + 1) * per + nb * 8 + radix_hist_words(n) * 4 + 64 * 1024));
@@ -346,18 +371,9 @@ void Engine::Impl::finalize_local_sorted() {
   Range r("wc_finalize_local");
   const TableView& t = table();
   const size_t nb = (size_t)1 << t.log2_buckets;
-  std::vector<uint32_t> occ(nb);
-  WC_HIP_CHECK(hipMemcpyAsync(occ.data(), t.occupancy, nb * 4, hipMemcpyDeviceToHost, s));
-  unsigned long long arena_used = 0;
-  WC_HIP_CHECK(hipMemcpyAsync(&arena_used, d_arena_cursor, 8, hipMemcpyDeviceToHost, s));
-  WC_HIP_CHECK(hipStreamSynchronize(s));
-  if (h_boff.size() < nb * 8) h_boff.resize(nb * 8);
-  uint64_t* boff = reinterpret_cast<uint64_t*>(h_boff.data());
-  uint64_t n = 0;
-  for (size_t b = 0; b < nb; ++b) {
-    boff[b] = n;
-    n += occ[b];
-  }
+  uint64_t* boff = nullptr;
+  uint64_t arena_used = 0;
+  const uint64_t n = host_occupancy(boff, arena_used);
   DeviceArena& A = sort_mem;
   A.reserve((n + 1) * (2 * 8 + 2 * 4 + 5 * 8 + 4) + nb * 8 + radix_hist_words(n) * 4 + 64 * 1024);
   A.reset();
@@ -466,6 +482,7 @@ void Engine::reset() {
   Impl& im = *p_;
   WC_HIP_CHECK(hipSetDevice(im.dev));
   launch_table_clear(im.table(), im.s);
+  im.occ_valid = false;
   WC_HIP_CHECK(hipMemsetAsync(im.d_arena_cursor, 0, sizeof(unsigned long long), im.s));
   // no sync: the next pass is stream-ordered behind the clear
   if (im.copy_s) WC_HIP_CHECK(hipStreamSynchronize(im.copy_s));  // a failed stream may have left copies

@@ -92,6 +92,8 @@ struct Engine::Impl {
   // finalisation workspace
   DeviceArena fin_mem;   // compact output
   PinnedBuffer h_boff;   // per-bucket compaction offsets (H2D without a sync)
+  PinnedBuffer h_occ;    // bucket occupancy + key-arena cursor, copied with every pass's counters
+  bool occ_valid = false;  // h_occ matches the table (no split / clear since the last pass)
   DeviceArena merge_mem; // merge buffers (merged columns live here)
   DeviceArena merge_small;  // merge metadata (count matrices)
   PinnedBuffer h_merge;     // merge host words for async H2D copies (no sync before they go out of scope)
@@ -124,6 +126,8 @@ struct Engine::Impl {
   void split_table();
 
   uint64_t finalize(Comm* comm, bool all_ranks);  // compact [+ merge] + order by first
+  void enqueue_occupancy();                 // async D2H of occupancy + arena cursor into h_occ
+  uint64_t host_occupancy(uint64_t*& boff, uint64_t& arena_used);  // h_occ (sync only if stale) -> offsets, n
   void compact_local();                     // table -> cols (unsorted)
   void finalize_local_sorted();             // table -> cols ordered by first (no merge: no column copy)
   void sort_cols_by_first();                // cols ordered by first occurrence

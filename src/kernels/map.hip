@@ -54,7 +54,7 @@ constexpr int SPT = MAP_SLOTS / MAP_THREADS;
 #define WC_HOT_K (MAP_SLOTS * 3 / 4)
 #endif
 #ifndef WC_HOT_SAMPLE
-#define WC_HOT_SAMPLE 8
+#define WC_HOT_SAMPLE 4
 #endif
 constexpr uint32_t HOT_K = WC_HOT_K;            // words placed in the hot table
 constexpr uint32_t HOT_SAMPLE = WC_HOT_SAMPLE;  // units sampled per map block
