@@ -140,8 +140,8 @@ Engine::Impl::~Impl() {
                                             "slow",   "emit", "wait", "flush"};
       fprintf(stderr, "[wc] map phase clock (share of wave lifetime):");
       for (int i = 0; i < MS_TOTAL; ++i) fprintf(stderr, " %s=%.3f", names[i], (double)h[i] / h[MS_TOTAL]);
-      fprintf(stderr, "; refreshes %llu; tokens: first-group hits %llu, deferred %llu, claims %llu, direct records %llu",
-              h[MS_NFLUSH], h[MS_N_HIT], h[MS_N_DEFER], h[MS_N_CLAIM], h[MS_N_DIRECT]);
+      fprintf(stderr, "; tokens: hot-table hits %llu, deferred LONG %llu, miss records %llu", h[MS_N_HIT],
+              h[MS_N_DEFER], h[MS_N_DIRECT]);
       fprintf(stderr, "; slowest block / mean block = %.3f\n",
               h[MS_BLKSUM] ? (double)h[MS_BLKMAX] * blocks_stamped / (double)h[MS_BLKSUM] : 0.0);
     }

@@ -121,7 +121,7 @@ constexpr int HOT_SEL_BLOCKS = 256;
 // In-kernel phase stamps of the map (diagnostic build, WC_MAP_STAMPS=1): shares
 // of wave lifetime per phase, then counters.
 enum : int { MS_COMMIT = 0, MS_MASK, MS_LIST, MS_KEYS, MS_PROBE, MS_SLOW, MS_EMIT, MS_WAIT, MS_FLUSH, MS_TOTAL,
-             MS_NFLUSH, MS_N_HIT, MS_N_DEFER, MS_N_CLAIM, MS_N_DIRECT,
+             MS_N_HIT, MS_N_DEFER, MS_N_DIRECT,
              MS_BLKSUM, MS_BLKMAX, MAP_STAMP_N };
 
 struct ReduceArgs {
@@ -180,8 +180,6 @@ void launch_gather_table(const TableView& t, const uint64_t* keys, const uint32_
 void launch_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
                         const uint64_t* soff, const uint32_t* slen, const uint32_t* perm, uint64_t* ok0, uint64_t* ok1,
                         uint64_t* ocnt, uint64_t* ofirst, uint64_t* osoff, uint32_t* oslen, uint64_t n, hipStream_t s);
-void launch_gather_u64(const uint64_t* in, const uint32_t* perm, uint64_t* out, uint64_t n, hipStream_t s);
-void launch_gather_u32(const uint32_t* in, const uint32_t* perm, uint32_t* out, uint64_t n, hipStream_t s);
 void launch_iota_u32(uint32_t* v, uint64_t n, hipStream_t s);
 
 void launch_synth(uint8_t* out, uint64_t n, uint64_t first_segment, uint64_t seed, const SynthVocab& v,

@@ -114,26 +114,6 @@ __device__ __forceinline__ int lds_find_or_claim(SlotGroup* groups, uint32_t ngr
   }
 }
 
-// Slot of (k0, k1) if it is published in group g, else -1: one read of the
-// group, no claims, no waits — the reducer's common case (the key already has
-// a slot in its home group) without the probe loop's divergent control flow.
-__device__ __forceinline__ int lds_find_in_group(const SlotGroup* groups, uint32_t g, uint32_t tag, uint64_t k0,
-                                                 uint64_t k1) {
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-  const SlotGroup& G = groups[g];
-  const u32x4 t = *reinterpret_cast<const u32x4*>(G.tag);
-  const u64x2 a1 = *reinterpret_cast<const u64x2*>(&G.k1[0]);
-  const u64x2 b1 = *reinterpret_cast<const u64x2*>(&G.k1[2]);
-  const u64x2 a0 = *reinterpret_cast<const u64x2*>(&G.k0[0]);
-  const u64x2 b0 = *reinterpret_cast<const u64x2*>(&G.k0[2]);
-  const uint32_t m = (t.x == tag && a1.x == k1 && a0.x == k0 ? 1u : 0u) |
-                     (t.y == tag && a1.y == k1 && a0.y == k0 ? 2u : 0u) |
-                     (t.z == tag && b1.x == k1 && b0.x == k0 ? 4u : 0u) |
-                     (t.w == tag && b1.y == k1 && b0.y == k0 ? 8u : 0u);
-  return m ? 4 * (int)g + (int)__ffs(m) - 1 : -1;
-}
-
 // Next slot of the probe sequence (cursor: -1 at the start, then kept by the
 // caller) whose key is (k0, k1), or -1 at the first group with an empty slot.
 // LONG keys may sit in several slots (colliding words, keys.hpp): the caller

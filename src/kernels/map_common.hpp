@@ -19,24 +19,6 @@ static_assert(64 * MAP_BPL <= 2048, "list entries hold 11-bit unit-relative posi
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
-// 8 bytes of an LDS text buffer starting at byte p: ONE unaligned ds_read_b64
-// (gfx950 runs HSA queues in unaligned-access mode; the compiler emits it for a
-// byte-aligned memcpy).  WC_TILE8_ALIGNED=1: two aligned reads + a funnel shift.
-#ifndef WC_TILE8_ALIGNED
-#define WC_TILE8_ALIGNED 0
-#endif
-__device__ __forceinline__ uint64_t tile8(const uint8_t* tile, uint32_t p) {
-  if (!WC_TILE8_ALIGNED) {
-    uint64_t v;
-    __builtin_memcpy(&v, tile + p, 8);
-    return v;
-  }
-  const uint64_t* q = reinterpret_cast<const uint64_t*>(tile + (p & ~7u));
-  const uint32_t sh = (p & 7) * 8;
-  const uint64_t lo = q[0], hi = q[1];
-  return sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
-}
-
 // Bytes [p, p+8) and [p+8, p+16) of an 8-byte-aligned LDS text buffer from
 // three ALIGNED ds_read_b64 and two funnel shifts (an unaligned 16-byte read
 // stalls the LDS pipe: SQ_LDS_UNALIGNED_STALL was a third of its busy cycles).
@@ -49,11 +31,6 @@ __device__ __forceinline__ void window16(const uint8_t* buf, uint32_t p, uint64_
   // (64-bit shifts measured faster here than a 32-bit v_alignbyte_b32 funnel)
   w0 = (d0 >> sh) | ((d1 << 1) << (63 - sh));
   w1 = (d1 >> sh) | ((d2 << 1) << (63 - sh));
-}
-
-// Low n bytes of v (n <= 8).
-__device__ __forceinline__ uint64_t low_bytes(uint64_t v, uint32_t n) {
-  return n >= 8 ? v : (v & ((1ull << (8 * n)) - 1ull));
 }
 
 __device__ __forceinline__ void wave_sync() {

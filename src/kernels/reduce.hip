@@ -139,17 +139,8 @@ __device__ __forceinline__ void add_to_slot(RedLds& L, int s, uint64_t cnt, uint
 }
 
 // A key not found in its home group: full probe, claiming a slot if new.
-#ifndef WC_RED_SLOW_INLINE
-#define WC_RED_SLOW_INLINE 0
-#endif
-#if WC_RED_SLOW_INLINE
-#define WC_RED_SLOW_ATTR __forceinline__
-#else
-#define WC_RED_SLOW_ATTR __noinline__  // one copy: keeps the unrolled batch loop small in the instruction cache
-#endif
-// Returns 1 if it claimed a new slot (the caller counts occupancy per wave:
-// a per-lane atomic on one LDS word serialised every claim of the block).
-__device__ WC_RED_SLOW_ATTR uint32_t merge_slow(RedLds& L, uint32_t ph, uint64_t k0, uint64_t k1, uint64_t cnt,
+// Out of line: one copy keeps the unrolled batch loop small (inlining measured no faster).
+__device__ __noinline__ uint32_t merge_slow(RedLds& L, uint32_t ph, uint64_t k0, uint64_t k1, uint64_t cnt,
                                             uint64_t first) {
   bool claimed;
   const int s = lds_find_or_claim(L.grp, TAB_GROUPS, ph, k0, k1, TAB_MAX_GROUP_PROBES, claimed, true,

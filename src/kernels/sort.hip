@@ -155,14 +155,6 @@ __global__ void wc_gather_cols(const uint64_t* k0, const uint64_t* k1, const uin
   }
 }
 
-__global__ void wc_gather_u64(const uint64_t* in, const uint32_t* perm, uint64_t* out, uint64_t n) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    out[i] = in[perm[i]];
-}
-__global__ void wc_gather_u32(const uint32_t* in, const uint32_t* perm, uint32_t* out, uint64_t n) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    out[i] = in[perm[i]];
-}
 __global__ void wc_iota_u32(uint32_t* v, uint64_t n) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     v[i] = (uint32_t)i;
@@ -226,12 +218,6 @@ void launch_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* 
                        ok0, ok1, ocnt, ofirst, osoff, oslen, n);
 }
 
-void launch_gather_u64(const uint64_t* in, const uint32_t* perm, uint64_t* out, uint64_t n, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(dev::wc_gather_u64, dev::grid_for(n), dim3(256), 0, s, in, perm, out, n);
-}
-void launch_gather_u32(const uint32_t* in, const uint32_t* perm, uint32_t* out, uint64_t n, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(dev::wc_gather_u32, dev::grid_for(n), dim3(256), 0, s, in, perm, out, n);
-}
 void launch_iota_u32(uint32_t* v, uint64_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(dev::wc_iota_u32, dev::grid_for(n), dim3(256), 0, s, v, n);
 }
