@@ -34,6 +34,7 @@ int wc_device_count(void);
 /* Kernel test hook: stable LSD radix sort of n u64 keys (low `bits` bits) on
  * `device`; returns the sorted keys and the permutation (host arrays). */
 int wc_debug_radix_sort(int device, const uint64_t* keys, uint64_t n, int bits, uint64_t* sorted, uint32_t* perm);
+int wc_bench_radix_sort(int device, const uint64_t* keys, uint64_t n, int bits, int reps, double* ms);
 void wc_default_options(wc_options* o);
 
 wc_engine* wc_engine_create(const wc_options* o);

@@ -94,6 +94,46 @@ int wc_debug_radix_sort(int device, const uint64_t* keys, uint64_t n, int bits, 
   });
 }
 
+// Device time of radix_sort_pairs on n given keys (+ iota values), averaged
+// over `reps` sorts of the same input: the sort-based-reduce A/B
+// (tools/sort_vs_hash.py) prices one full sort of a pass's records.
+int wc_bench_radix_sort(int device, const uint64_t* keys, uint64_t n, int bits, int reps, double* ms) {
+  return guard([&] {
+    WC_HIP_CHECK(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    uint8_t* mem = nullptr;
+    const size_t nn = n ? n : 1, hw = wc::radix_hist_words(n);
+    WC_HIP_CHECK(hipMalloc(&mem, nn * (8 + 8 + 8 + 4 + 4) + hw * 4 + 1024));
+    uint64_t* src = reinterpret_cast<uint64_t*>(mem);
+    uint64_t* k = src + nn;
+    uint64_t* tk = k + nn;
+    uint32_t* v = reinterpret_cast<uint32_t*>(tk + nn);
+    uint32_t* tv = v + nn;
+    uint32_t* hist = tv + nn;
+    WC_HIP_CHECK(hipMemcpy(src, keys, n * 8, hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    WC_HIP_CHECK(hipEventCreate(&e0));
+    WC_HIP_CHECK(hipEventCreate(&e1));
+    float total = 0;
+    for (int r = 0; r < reps; ++r) {
+      WC_HIP_CHECK(hipMemcpyAsync(k, src, n * 8, hipMemcpyDeviceToDevice, s));
+      wc::launch_iota_u32(v, n, s);
+      WC_HIP_CHECK(hipEventRecord(e0, s));
+      bool in_tmp = false;
+      wc::radix_sort_pairs(k, v, tk, tv, hist, n, bits, s, &in_tmp);
+      WC_HIP_CHECK(hipEventRecord(e1, s));
+      WC_HIP_CHECK(hipEventSynchronize(e1));
+      float t = 0;
+      WC_HIP_CHECK(hipEventElapsedTime(&t, e0, e1));
+      if (r > 0 || reps == 1) total += t;  // first rep warms up
+    }
+    *ms = total / (reps > 1 ? reps - 1 : 1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    WC_HIP_CHECK(hipFree(mem));
+  });
+}
+
 int wc_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
