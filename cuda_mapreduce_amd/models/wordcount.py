@@ -41,7 +41,8 @@ CONFIGS = {
     for c in [
         JobConfig("cpu-test", "test.txt word count on CPU reference path (single-thread hash map, no GPU)",
                   source="cpu", path=os.path.join(os.path.dirname(__file__), "..", "..", "tests", "data", "test.txt")),
-        JobConfig("1gb", "1 GB synthetic ASCII text, single MI355X (map/shuffle/reduce HIP kernels end-to-end)"),
+        JobConfig("1gb", "1 GB synthetic ASCII text per MI355X (map/shuffle/reduce HIP kernels end-to-end; "
+                  "N > 1: RCCL reduce-scatter dense merge)", merge="dense"),
         JobConfig("64gb", "64 GB synthetic text, single MI355X (HBM-resident, chunked)", bytes_per_gpu=64 * GiB,
                   chunk_bytes=2 * GiB),
         JobConfig("256gb-8gpu", "256 GB synthetic text sharded across 8x MI355X, RCCL reduce-scatter merge",

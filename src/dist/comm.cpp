@@ -180,6 +180,9 @@ struct Hub {
 class LoopbackComm final : public Comm {
  public:
   LoopbackComm(std::shared_ptr<Hub> hub, int rank) : hub_(std::move(hub)), rank_(rank) {}
+  ~LoopbackComm() override {
+    if (scratch_) (void)hipFree(scratch_);
+  }
   int rank() const override { return rank_; }
   int size() const override { return hub_->n; }
   const char* backend() const override { return "loopback"; }
@@ -203,8 +206,12 @@ class LoopbackComm final : public Comm {
     WC_HIP_CHECK(hipStreamSynchronize(s));
     hub_->ptrs[rank_] = send;
     hub_->wait_all();
-    uint64_t* tmp = nullptr;
-    if (count) WC_HIP_CHECK(hipMalloc(&tmp, count * 8));
+    if (count > scratch_n_) {  // grown once, reused: no allocation per collective
+      if (scratch_) WC_HIP_CHECK(hipFree(scratch_));
+      WC_HIP_CHECK(hipMalloc(&scratch_, count * 8));
+      scratch_n_ = count;
+    }
+    uint64_t* tmp = scratch_;
     for (int r = 0; r < hub_->n; ++r) {
       const uint64_t* src = static_cast<const uint64_t*>(hub_->ptrs[r]) + (size_t)rank_ * count;
       if (!count) break;
@@ -216,7 +223,6 @@ class LoopbackComm final : public Comm {
       }
     }
     WC_HIP_CHECK(hipStreamSynchronize(s));
-    if (tmp) WC_HIP_CHECK(hipFree(tmp));
     hub_->wait_all();
   }
   void alltoallv(const void* send, const size_t* send_off, const size_t* /*send_bytes*/, void* recv,
@@ -252,6 +258,8 @@ class LoopbackComm final : public Comm {
  private:
   std::shared_ptr<Hub> hub_;
   int rank_;
+  uint64_t* scratch_ = nullptr;  // reduce-scatter staging (device of this rank)
+  size_t scratch_n_ = 0;
 };
 
 }  // namespace

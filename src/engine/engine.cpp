@@ -481,7 +481,9 @@ Stats& Engine::stats() { return p_->st; }
 void Engine::reset() {
   Impl& im = *p_;
   WC_HIP_CHECK(hipSetDevice(im.dev));
-  launch_table_clear(im.table(), im.s);
+  // zero only the occupancy: a bucket with occupancy 0 is empty whatever its
+  // slice holds (reduce / compact / split never read such a slice)
+  WC_HIP_CHECK(hipMemsetAsync(im.table().occupancy, 0, ((size_t)1 << im.table().log2_buckets) * 4, im.s));
   im.occ_valid = false;
   WC_HIP_CHECK(hipMemsetAsync(im.d_arena_cursor, 0, sizeof(unsigned long long), im.s));
   // no sync: the next pass is stream-ordered behind the clear

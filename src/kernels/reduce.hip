@@ -65,8 +65,21 @@ struct RedLds {
 };
 static_assert(sizeof(RedLds) <= 160 * 1024, "one reduce block per CU");
 
+// A bucket with occupancy 0 has UNDEFINED slice contents (Engine::reset zeroes
+// only the occupancy): it starts empty without reading the slice.
 __device__ __forceinline__ void load_slice(RedLds& L, const TableView& t, uint32_t b) {
   const size_t base = (size_t)b * TAB_SLOTS;
+  if (t.occupancy[b] == 0) {
+    for (int s = threadIdx.x; s < TAB_SLOTS; s += blockDim.x) {
+      SlotGroup& G = L.grp[s >> 2];
+      G.k0[s & 3] = 0;
+      G.k1[s & 3] = K1_EMPTY;
+      G.tag[s & 3] = TAG_EMPTY;
+      L.cnt[s] = 0;
+      L.first[s] = ~0ull;
+    }
+    return;
+  }
   for (int s = threadIdx.x; s < TAB_SLOTS; s += blockDim.x) {
     const uint64_t k0 = t.k0[base + s], k1 = t.k1[base + s];
     SlotGroup& G = L.grp[s >> 2];
@@ -495,7 +508,8 @@ __global__ void __launch_bounds__(RED_THREADS) wc_table_split(TableView src, Tab
   if (threadIdx.x == 0) L.occupied = 0;
   __syncthreads();
   const size_t obase = (size_t)ob * TAB_SLOTS, nbase = (size_t)nb * TAB_SLOTS;
-  for (int s = threadIdx.x; s < TAB_SLOTS; s += blockDim.x) {
+  const bool parent_empty = src.occupancy[ob] == 0;  // contents undefined (see load_slice)
+  for (int s = threadIdx.x; s < TAB_SLOTS && !parent_empty; s += blockDim.x) {
     const uint64_t k1 = src.k1[obase + s];
     if (k1 == K1_EMPTY) continue;
     const uint64_t k0 = src.k0[obase + s];
@@ -535,6 +549,7 @@ __global__ void __launch_bounds__(1024) wc_table_compact(TableView t, const uint
   __shared__ uint32_t wsum[16];
   const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const size_t base = (size_t)b * TAB_SLOTS + 4 * tid;
+  if (t.occupancy[b] == 0) return;  // contents undefined (see load_slice); no keys
   uint64_t kk1[4];
   uint32_t n = 0;
 #pragma unroll
@@ -573,6 +588,7 @@ __global__ void __launch_bounds__(1024) wc_table_keys(TableView t, const uint64_
   __shared__ uint32_t wsum[16];
   const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const size_t base = (size_t)b * TAB_SLOTS + 4 * tid;
+  if (t.occupancy[b] == 0) return;  // contents undefined (see load_slice); no keys
   bool occ[4];
   uint32_t n = 0;
 #pragma unroll

@@ -75,6 +75,29 @@ def test_resident_text_survives_streaming():
     assert_same(c, ops.cpu_count(ops.synth_host(8 << 20, first_segment=0, seed=4, vocab=3000)))
 
 
+def test_reset_ignores_stale_slices():
+    """reset() zeroes only the bucket occupancy: slices of a previous job stay
+    in memory and must never leak into the next one (reduce, compaction,
+    split and an empty finalize all treat occupancy-0 buckets as empty)."""
+    big = ops.synth_host(64 << 20, seed=11, vocab=200_000)
+    small = b"alpha beta alpha gamma\nbeta alpha\n"
+    with ops.Engine(device=0, chunk_bytes=16 << 20) as e:
+        e.count_bytes(big)
+        first = e.result()
+        e.reset()
+        empty = e.result()  # no pass since the reset
+        e.reset()
+        e.count_bytes(small)
+        tiny = e.result()
+        e.reset()
+        e.count_bytes(big)  # grows / splits again over stale slices
+        again = e.result()
+    assert_same(first, ops.cpu_count(big))
+    assert empty.total == 0 and len(empty.words) == 0
+    assert_same(tiny, ops.cpu_count(small))
+    assert_same(again, first)
+
+
 def test_headline_stream_key_for_key():
     """The exact benchmark input (1 GiB, seed 1, Zipf(1.0), 100k words, one
     device chunk) against the generator-walk oracle; and 256 MiB of it against
