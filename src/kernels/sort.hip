@@ -22,20 +22,25 @@ namespace wc {
 namespace dev {
 
 constexpr int RS_THREADS = 256;
-constexpr int RS_ROUNDS = 8;
-constexpr int RS_TILE = RS_THREADS * RS_ROUNDS;  // 2048 items per block
+// Tiles of ROUNDS x 256 items per block: 2048 for large sorts, 512 below
+// 2^19 items so a 1e5-key sort still spreads over ~200 blocks (A/B: +1.3 % at
+// 100k words; 2048 wins at 1M).
+constexpr int RS_ROUNDS_BIG = 8, RS_ROUNDS_SMALL = 2;
+constexpr uint64_t RS_SMALL_N = 1ull << 19;
+__host__ __device__ constexpr int rs_rounds(uint64_t n) { return n < RS_SMALL_N ? RS_ROUNDS_SMALL : RS_ROUNDS_BIG; }
 constexpr int RS_WAVES = RS_THREADS / 64;
 constexpr int RS_MAX_DB = 8;                     // digit bits per pass (11-bit digits measured slower: the
                                                   // per-round LDS work on 2048 bins outweighs one pass fewer)
 constexpr int RS_BINS = 1 << RS_MAX_DB;
 
+template <int RS_ROUNDS>
 __global__ void __launch_bounds__(RS_THREADS) wc_radix_hist(const uint64_t* keys, uint64_t n, int shift, int db,
                                                             uint32_t* hist, uint32_t nblocks, uint32_t* totals) {
   __shared__ uint32_t h[RS_BINS];
   const uint32_t nd = 1u << db, dmask = nd - 1;
   for (uint32_t d = threadIdx.x; d < nd; d += RS_THREADS) h[d] = 0;
   __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+  const uint64_t base = (uint64_t)blockIdx.x * (RS_THREADS * RS_ROUNDS);
   for (int r = 0; r < RS_ROUNDS; ++r) {
     const uint64_t i = base + (uint64_t)r * RS_THREADS + threadIdx.x;
     if (i < n) atomicAdd(&h[(keys[i] >> shift) & dmask], 1u);
@@ -93,6 +98,7 @@ __global__ void __launch_bounds__(256) wc_radix_scan(uint32_t* hist, uint32_t nb
   }
 }
 
+template <int RS_ROUNDS>
 __global__ void __launch_bounds__(RS_THREADS) wc_radix_scatter(const uint64_t* keys, const uint32_t* vals,
                                                                uint64_t* okeys, uint32_t* ovals, uint64_t n,
                                                                int shift, int db, const uint32_t* hist,
@@ -102,7 +108,7 @@ __global__ void __launch_bounds__(RS_THREADS) wc_radix_scatter(const uint64_t* k
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t nd = 1u << db, dmask = nd - 1;
   for (uint32_t d = tid; d < nd; d += RS_THREADS) run[d] = hist[(size_t)d * nblocks + blockIdx.x];
-  const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+  const uint64_t base = (uint64_t)blockIdx.x * (RS_THREADS * RS_ROUNDS);
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   for (int r = 0; r < RS_ROUNDS; ++r) {
     for (int w = 0; w < RS_WAVES; ++w)
@@ -175,7 +181,8 @@ inline dim3 grid_for(uint64_t n) {
 constexpr int RS_MAX_PASSES = 8;  // 64-bit keys
 
 size_t radix_hist_words(uint64_t n) {
-  const uint64_t nb = (n + dev::RS_TILE - 1) / dev::RS_TILE;
+  const uint64_t tile = (uint64_t)dev::RS_THREADS * dev::rs_rounds(n);
+  const uint64_t nb = (n + tile - 1) / tile;
   return (size_t)dev::RS_BINS * (nb ? nb : 1) + (size_t)dev::RS_BINS * RS_MAX_PASSES;  // tile counts + digit totals
 }
 
@@ -185,7 +192,9 @@ void radix_sort_pairs(uint64_t* keys, uint32_t* vals, uint64_t* tmp_keys, uint32
                       uint64_t n, int bits, hipStream_t s, bool* in_tmp) {
   if (in_tmp) *in_tmp = false;
   if (n <= 1 || bits <= 0) return;
-  const uint32_t nb = (uint32_t)((n + dev::RS_TILE - 1) / dev::RS_TILE);
+  const bool small = dev::rs_rounds(n) == dev::RS_ROUNDS_SMALL;
+  const uint64_t tile = (uint64_t)dev::RS_THREADS * dev::rs_rounds(n);
+  const uint32_t nb = (uint32_t)((n + tile - 1) / tile);
   const int passes = (bits + dev::RS_MAX_DB - 1) / dev::RS_MAX_DB;
   const int db = (bits + passes - 1) / passes;
   uint32_t* totals = hist + (size_t)dev::RS_BINS * nb;  // [passes][2^db]
@@ -195,10 +204,19 @@ void radix_sort_pairs(uint64_t* keys, uint32_t* vals, uint64_t* tmp_keys, uint32
   for (int p = 0; p < passes; ++p) {
     const int shift = db * p;
     uint32_t* tot = totals + (size_t)dev::RS_BINS * p;
-    hipLaunchKernelGGL(dev::wc_radix_hist, dim3(nb), dim3(dev::RS_THREADS), 0, s, ki, n, shift, db, hist, nb, tot);
+    if (small)
+      hipLaunchKernelGGL(dev::wc_radix_hist<dev::RS_ROUNDS_SMALL>, dim3(nb), dim3(dev::RS_THREADS), 0, s, ki, n, shift,
+                         db, hist, nb, tot);
+    else
+      hipLaunchKernelGGL(dev::wc_radix_hist<dev::RS_ROUNDS_BIG>, dim3(nb), dim3(dev::RS_THREADS), 0, s, ki, n, shift, db,
+                         hist, nb, tot);
     hipLaunchKernelGGL(dev::wc_radix_scan, dim3(1u << db), dim3(256), 0, s, hist, nb, tot);
-    hipLaunchKernelGGL(dev::wc_radix_scatter, dim3(nb), dim3(dev::RS_THREADS), 0, s, ki, vi, ko, vo, n, shift, db,
-                       hist, nb);
+    if (small)
+      hipLaunchKernelGGL(dev::wc_radix_scatter<dev::RS_ROUNDS_SMALL>, dim3(nb), dim3(dev::RS_THREADS), 0, s, ki, vi, ko,
+                         vo, n, shift, db, hist, nb);
+    else
+      hipLaunchKernelGGL(dev::wc_radix_scatter<dev::RS_ROUNDS_BIG>, dim3(nb), dim3(dev::RS_THREADS), 0, s, ki, vi, ko,
+                         vo, n, shift, db, hist, nb);
     std::swap(ki, ko);
     std::swap(vi, vo);
   }
