@@ -61,6 +61,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   map_blocks = opt.map_blocks ? opt.map_blocks : MAP_BLOCKS_PER_CU * (uint32_t)device_cu_count(dev);
   map_blocks = std::min<uint32_t>(map_blocks, RED_MAX_RUNS);
   if (const char* e = std::getenv("WC_SYNC_DEBUG")) sync_debug = std::atoi(e) != 0;
+  if (const char* e = std::getenv("WC_NO_SPECULATE")) speculate = std::atoi(e) == 0;
   k1_mask = k1_hash_mask(opt.k1_hash_bits);
   if (const char* e = std::getenv("WC_MAP_STAMPS"); e && std::atoi(e)) {
     WC_HIP_CHECK(hipMalloc(&d_stamps, MAP_STAMP_N * 8));
@@ -195,7 +196,7 @@ uint32_t Engine::Impl::blocks_for(uint64_t len) const {
 }
 
 void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev,
-                               uint32_t log2_rb, uint32_t blocks) {
+                               uint32_t log2_rb, uint32_t blocks, bool copy_occupancy) {
   WC_CHECK((reinterpret_cast<uintptr_t>(text) & 15) == 0, "chunk text must be 16-byte aligned");
   WC_HIP_CHECK(hipMemsetAsync(d_ctr, 0, sizeof(DevCounters), s));
   pass_rec = rec;
@@ -223,10 +224,19 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
     WC_HIP_CHECK(e);
   }
   WC_HIP_CHECK(hipMemcpyAsync(h_ctr, d_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));
-  enqueue_occupancy();  // read at finalize without a sync of its own
+  occ_copied = false;
+  if (copy_occupancy) enqueue_occupancy();  // read at finalize without a sync of its own
+}
+
+void Engine::Impl::settle() {
+  if (!pend.active) return;
+  const PendingPass p = pend;
+  pend.active = false;
+  complete_pass(p.text, p.len, p.avail, p.base, p.prev, p.rb, p.blocks);
 }
 
 void Engine::Impl::enqueue_occupancy() {
+  occ_copied = true;
   const size_t nb = (size_t)1 << table().log2_buckets;
   if (h_occ.size() < nb * 4 + 8) h_occ.resize(std::max<size_t>(nb * 4 + 8, 4096));
   WC_HIP_CHECK(hipMemcpyAsync(h_occ.data() + 8, table().occupancy, nb * 4, hipMemcpyDeviceToHost, s));
@@ -270,7 +280,7 @@ void Engine::Impl::split_table() {
   WC_LOG(LOG_INFO, "dev %d: key table split %u -> %u buckets", dev, 1u << lg, 2u << lg);
 }
 
-void Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev,
+bool Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev,
                                  uint32_t log2_rb, uint32_t blocks) {
   WC_HIP_CHECK(hipStreamSynchronize(s));
   DevCounters c = *h_ctr;
@@ -294,11 +304,12 @@ void Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
     } else {
       fail("shuffle record capacity too small for a single tile");
     }
-    return;
+    return false;
   }
   const uint64_t tokens = c.tokens;
   st.records += c.records;
   uint32_t max_occ = c.flags[FLAG_MAX_OCC];
+  const bool clean = !c.flags[FLAG_TABLE_OVF];
   while (c.flags[FLAG_TABLE_OVF]) {
     if (c.flags[FLAG_ARENA_OVF]) break;
     const uint32_t lg = table().log2_buckets;
@@ -328,13 +339,23 @@ void Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
          (unsigned long long)base, (unsigned long long)len, blocks, (unsigned long long)tokens,
          (unsigned long long)c.records);
   max_end = std::max(max_end, base + len);
-  occ_valid = true;  // the copies enqueued with this pass's counters completed at its sync
+  occ_valid = occ_copied;  // occupancy copies enqueued with this pass's counters completed at its sync
   if (max_occ >= (uint32_t)TAB_SPLIT_AT && table().log2_buckets < opt.max_log2_tab_buckets) split_table();
+  return clean;
 }
 
-void Engine::Impl::process_chunk(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev) {
+void Engine::Impl::process_chunk(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev,
+                                 bool last) {
+  settle();
   const uint32_t blocks = blocks_for(len);
   const uint32_t rb = rec_buckets_log2();
+  if (last && speculate && !sync_debug) {
+    launch_pass(text, len, avail, base, prev, rb, blocks, false);
+    pend = PendingPass{true, text, len, avail, base, prev, rb, blocks};
+    occ_valid = false;
+    max_end = std::max(max_end, base + len);  // the sort key width of the speculative finalize
+    return;
+  }
   launch_pass(text, len, avail, base, prev, rb, blocks);
   complete_pass(text, len, avail, base, prev, rb, blocks);
 }
@@ -365,6 +386,63 @@ void Engine::Impl::compact_local() {
   cols_arena_bytes = std::min<uint64_t>(arena_used, opt.arena_bytes);
   st.keys = n;
   st.log2_buckets = t.log2_buckets;
+}
+
+// The local finalize launched right behind a pending pass, with no host round
+// trip: bucket offsets and the key count are computed on the device, the sort
+// and gather are sized for the table's capacity and run on the device count.
+// One sync at the end covers the pass counters too; if the pass needed
+// recovery (re-runs / splits) the result is discarded (returns false).
+bool Engine::Impl::finalize_local_speculative() {
+  Range r("wc_finalize_speculative");
+  const PendingPass p = pend;
+  pend.active = false;
+  const TableView& t = table();
+  const size_t nb = (size_t)1 << t.log2_buckets;
+  const uint64_t cap = (uint64_t)nb * TAB_SLOTS;
+  const uint64_t hint = std::min<uint64_t>(cap, last_keys ? last_keys + last_keys / 8 + 1024 : cap / 4);
+  DeviceArena& A = sort_mem;
+  A.reserve((cap + 1) * (2 * 8 + 2 * 4 + 5 * 8 + 4) + nb * 8 + radix_hist_words(cap, hint) * 4 + 64 * 1024);
+  A.reset();
+  uint64_t* d_boff = A.take_n<uint64_t>(nb);
+  uint64_t* d_n = A.take_n<uint64_t>(2);
+  uint64_t* keys = A.take_n<uint64_t>(cap + 1);
+  uint64_t* tkeys = A.take_n<uint64_t>(cap + 1);
+  uint32_t* slots = A.take_n<uint32_t>(cap + 1);
+  uint32_t* tslots = A.take_n<uint32_t>(cap + 1);
+  uint32_t* hist = A.take_n<uint32_t>(radix_hist_words(cap, hint));
+  KeyCols o;
+  o.k0 = A.take_n<uint64_t>(cap + 1);
+  o.k1 = A.take_n<uint64_t>(cap + 1);
+  o.cnt = A.take_n<uint64_t>(cap + 1);
+  o.first = A.take_n<uint64_t>(cap + 1);
+  o.sref_off = A.take_n<uint64_t>(cap + 1);
+  o.sref_len = A.take_n<uint32_t>(cap + 1);
+  launch_bucket_offsets(t.occupancy, (uint32_t)nb, d_boff, d_n, s);
+  launch_table_keys(t, d_boff, keys, slots, s);
+  int bits = 1;
+  while (bits < 64 && (max_end >> bits) != 0) ++bits;
+  bool in_tmp = false;
+  radix_sort_pairs(keys, slots, tkeys, tslots, hist, cap, bits, s, &in_tmp, d_n, hint);
+  launch_gather_table(t, in_tmp ? tkeys : keys, in_tmp ? tslots : slots, cap, o.k0, o.k1, o.cnt, o.first, o.sref_off,
+                      o.sref_len, s, d_n);
+  if (h_spec.size() < 16) h_spec.resize(4096);
+  WC_HIP_CHECK(hipMemcpyAsync(h_spec.data(), d_n, 8, hipMemcpyDeviceToHost, s));
+  WC_HIP_CHECK(hipMemcpyAsync(h_spec.data() + 8, d_arena_cursor, 8, hipMemcpyDeviceToHost, s));
+  WC_HIP_CHECK(hipStreamSynchronize(s));
+  // the pass's counters arrived with this sync: check it (stats, recovery)
+  if (!complete_pass(p.text, p.len, p.avail, p.base, p.prev, p.rb, p.blocks)) return false;
+  uint64_t n = 0, arena_used = 0;
+  std::memcpy(&n, h_spec.data(), 8);
+  std::memcpy(&arena_used, h_spec.data() + 8, 8);
+  o.n = n;
+  cols = o;
+  cols_arena = d_arena;
+  cols_arena_bytes = std::min<uint64_t>(arena_used, opt.arena_bytes);
+  st.keys = n;
+  st.log2_buckets = t.log2_buckets;
+  last_keys = n;
+  return true;
 }
 
 void Engine::Impl::finalize_local_sorted() {
@@ -404,6 +482,7 @@ void Engine::Impl::finalize_local_sorted() {
   cols_arena_bytes = std::min<uint64_t>(arena_used, opt.arena_bytes);
   st.keys = n;
   st.log2_buckets = t.log2_buckets;
+  last_keys = n;
 }
 
 void Engine::Impl::sort_cols_by_first() {
@@ -483,6 +562,7 @@ void Engine::reset() {
   WC_HIP_CHECK(hipSetDevice(im.dev));
   // zero only the occupancy: a bucket with occupancy 0 is empty whatever its
   // slice holds (reduce / compact / split never read such a slice)
+  im.pend.active = false;  // an unchecked pass of the previous job is discarded with it
   WC_HIP_CHECK(hipMemsetAsync(im.table().occupancy, 0, ((size_t)1 << im.table().log2_buckets) * 4, im.s));
   im.occ_valid = false;
   WC_HIP_CHECK(hipMemsetAsync(im.d_arena_cursor, 0, sizeof(unsigned long long), im.s));
@@ -500,7 +580,7 @@ void Engine::count_device(const uint8_t* d_text, uint64_t n, uint64_t avail, uin
   const uint64_t C = im.opt.chunk_bytes;
   for (uint64_t off = 0; off < n; off += C) {
     const uint64_t len = std::min<uint64_t>(C, n - off);
-    im.process_chunk(d_text + off, len, avail - off, global_base + off, off == 0 ? prev_byte : -1);
+    im.process_chunk(d_text + off, len, avail - off, global_base + off, off == 0 ? prev_byte : -1, off + len >= n);
   }
   im.st.bytes += n;
   im.st.map_reduce_ms += (now_seconds() - t0) * 1e3;
@@ -537,6 +617,7 @@ void Engine::count_source(ChunkSource& src, uint64_t global_base) {
   Impl& im = *p_;
   WC_HIP_CHECK(hipSetDevice(im.dev));
   Range r("wc_count_stream");
+  im.settle();
   const double t0 = now_seconds();
   uint64_t stream = im.opt.stream_chunk_bytes;
   if (const char* e = std::getenv("WC_STREAM_CHUNK")) stream = std::strtoull(e, nullptr, 10);  // sweeps only
@@ -597,6 +678,7 @@ void Engine::count_pinned_replay(const uint8_t* pool, uint64_t pool_bytes, uint6
   Impl& im = *p_;
   WC_HIP_CHECK(hipSetDevice(im.dev));
   Range r("wc_count_pinned_replay");
+  im.settle();
   const double t0 = now_seconds();
   const uint64_t C = std::min<uint64_t>(im.opt.chunk_bytes, pool_bytes);
   WC_CHECK(pool_bytes % C == 0, "replay pool must be a whole number of chunks");
@@ -672,12 +754,14 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
   static const bool merge_always = getenv("WC_MERGE_ALWAYS") && atoi(getenv("WC_MERGE_ALWAYS")) != 0;
   const bool merged = comm && (comm->size() > 1 || merge_always);
   if (merged) {
+    im.settle();
     im.compact_local();
     const double tm = now_seconds();
     merge_cols(im, *comm, all_ranks);
     im.st.merge_ms += (now_seconds() - tm) * 1e3;
     im.sort_cols_by_first();
-  } else {
+  } else if (!(im.pend.active && im.finalize_local_speculative())) {
+    im.settle();
     im.finalize_local_sorted();  // sort (first, slot) pairs, gather the columns from the table once
   }
   // the merge's last collectives are still in flight: wait under the comm watchdog

@@ -94,6 +94,7 @@ struct Engine::Impl {
   PinnedBuffer h_boff;   // per-bucket compaction offsets (H2D without a sync)
   PinnedBuffer h_occ;    // bucket occupancy + key-arena cursor, copied with every pass's counters
   bool occ_valid = false;  // h_occ matches the table (no split / clear since the last pass)
+  bool occ_copied = false;  // the current pass enqueued its occupancy copy
   DeviceArena merge_mem; // merge buffers (merged columns live here)
   DeviceArena merge_small;  // merge metadata (count matrices)
   PinnedBuffer h_merge;     // merge host words for async H2D copies (no sync before they go out of scope)
@@ -110,13 +111,28 @@ struct Engine::Impl {
   void ensure_text(uint64_t n);
   void ensure_staging(uint64_t chunk);
 
-  // One chunk: map + reduce with overflow recovery (synchronous).
-  void process_chunk(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev);
-  // Asynchronous part (map + reduce + counters D2H) and the completion check.
+  // One chunk: map + reduce with overflow recovery (synchronous).  With
+  // `last`, the pass is only launched and left PENDING: a local finalize runs
+  // behind it speculatively and checks its counters at its own single sync;
+  // anything else first settles it (complete_pass).
+  void process_chunk(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev, bool last = false);
+  // Asynchronous part (map + reduce + counters D2H) and the completion check;
+  // complete_pass returns false when the pass needed recovery (re-runs / splits).
   void launch_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev, uint32_t log2_rb,
-                   uint32_t blocks);
-  void complete_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev, uint32_t log2_rb,
+                   uint32_t blocks, bool copy_occupancy = true);
+  bool complete_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev, uint32_t log2_rb,
                      uint32_t blocks);
+  struct PendingPass {
+    bool active = false;
+    const uint8_t* text = nullptr;
+    uint64_t len = 0, avail = 0, base = 0;
+    int prev = -1;
+    uint32_t rb = 0, blocks = 0;
+  } pend;
+  bool speculate = true;  // WC_NO_SPECULATE=1: every pass synchronous
+  uint64_t last_keys = 0;  // keys of the previous finalize (sort size hint)
+  PinnedBuffer h_spec;     // speculative finalize: key count + arena cursor
+  void settle();           // complete a pending pass
   uint32_t blocks_for(uint64_t len) const;
   // Shuffle partitions track the running table (one reduce block reads only
   // its own partition) up to MAX_REC_BUCKETS.
@@ -130,6 +146,7 @@ struct Engine::Impl {
   uint64_t host_occupancy(uint64_t*& boff, uint64_t& arena_used);  // h_occ (sync only if stale) -> offsets, n
   void compact_local();                     // table -> cols (unsorted)
   void finalize_local_sorted();             // table -> cols ordered by first (no merge: no column copy)
+  bool finalize_local_speculative();        // same behind a pending pass; false: redo after its recovery
   void sort_cols_by_first();                // cols ordered by first occurrence
   KeyTable download_cols();
 };

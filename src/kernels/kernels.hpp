@@ -165,16 +165,22 @@ void launch_table_compact(const TableView& t, const uint64_t* bucket_off, uint64
 // tmp_* must hold n items; hist must hold radix_hist_words(n) words.  With
 // in_tmp, an odd pass count leaves the result in tmp_* (*in_tmp = true)
 // instead of copying it back.
-size_t radix_hist_words(uint64_t n);
+// dn: the item count on the device; n is then an upper bound (buffers, hist
+// stride) and n_hint the expected count (tile size, grid).
+size_t radix_hist_words(uint64_t n, uint64_t n_hint = 0);
 void radix_sort_pairs(uint64_t* keys, uint32_t* vals, uint64_t* tmp_keys, uint32_t* tmp_vals, uint32_t* hist,
-                      uint64_t n, int bits, hipStream_t s, bool* in_tmp = nullptr);
+                      uint64_t n, int bits, hipStream_t s, bool* in_tmp = nullptr, const uint64_t* dn = nullptr,
+                      uint64_t n_hint = 0);
 // Local finalize without the column copy: occupied slots -> (first offset,
 // global slot index) pairs at host-computed bucket offsets; after the sort,
 // the six output columns are gathered straight from the table.
 void launch_table_keys(const TableView& t, const uint64_t* bucket_off, uint64_t* keys, uint32_t* slots, hipStream_t s);
 void launch_gather_table(const TableView& t, const uint64_t* keys, const uint32_t* slots, uint64_t n, uint64_t* ok0,
                          uint64_t* ok1, uint64_t* ocnt, uint64_t* ofirst, uint64_t* osoff, uint32_t* oslen,
-                         hipStream_t s);
+                         hipStream_t s, const uint64_t* dn = nullptr);
+// Exclusive scan of the bucket occupancy on the device: bucket_off[b] and the
+// key count *n (the speculative finalize: no host round trip after the pass).
+void launch_bucket_offsets(const uint32_t* occupancy, uint32_t nb, uint64_t* bucket_off, uint64_t* n, hipStream_t s);
 
 // out[i] = in[perm[i]] for the six key-table columns (one launch).
 void launch_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,

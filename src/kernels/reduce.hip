@@ -615,9 +615,43 @@ __global__ void __launch_bounds__(1024) wc_table_keys(TableView t, const uint64_
   }
 }
 
+// One block: bucket_off = exclusive scan of occupancy, *n = the total.
+__global__ void __launch_bounds__(1024) wc_bucket_offsets(const uint32_t* occ, uint32_t nb, uint64_t* off,
+                                                          uint64_t* n) {
+  __shared__ uint64_t wsum[16];
+  __shared__ uint64_t carry;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t c = 0; c < nb; c += 1024) {
+    const uint32_t b = c + tid;
+    const uint64_t v = b < nb ? occ[b] : 0;
+    uint64_t incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(incl, o);
+      if ((int)lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint64_t before = carry;
+    for (uint32_t w = 0; w < wave; ++w) before += wsum[w];
+    if (b < nb) off[b] = before + incl - v;
+    __syncthreads();
+    if (tid == 0) {
+      uint64_t t = 0;
+      for (int w = 0; w < 16; ++w) t += wsum[w];
+      carry += t;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) *n = carry;
+}
+
 // Sorted (first, slot) pairs -> the six key columns, read from the table.
-__global__ void wc_gather_table(TableView t, const uint64_t* keys, const uint32_t* slots, uint64_t n, uint64_t* ok0,
-                                uint64_t* ok1, uint64_t* ocnt, uint64_t* ofirst, uint64_t* osoff, uint32_t* oslen) {
+__global__ void wc_gather_table(TableView t, const uint64_t* keys, const uint32_t* slots, uint64_t n,
+                                const uint64_t* dn, uint64_t* ok0, uint64_t* ok1, uint64_t* ocnt, uint64_t* ofirst,
+                                uint64_t* osoff, uint32_t* oslen) {
+  if (dn) n = *dn;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t j = slots[i];
     const uint64_t k1 = t.k1[j];
@@ -638,12 +672,15 @@ void launch_table_keys(const TableView& t, const uint64_t* bucket_off, uint64_t*
 }
 void launch_gather_table(const TableView& t, const uint64_t* keys, const uint32_t* slots, uint64_t n, uint64_t* ok0,
                          uint64_t* ok1, uint64_t* ocnt, uint64_t* ofirst, uint64_t* osoff, uint32_t* oslen,
-                         hipStream_t s) {
+                         hipStream_t s, const uint64_t* dn) {
   if (!n) return;
   uint64_t g = (n + 255) / 256;
   g = g > 4096 ? 4096 : g;
-  hipLaunchKernelGGL(dev::wc_gather_table, dim3((unsigned)g), dim3(256), 0, s, t, keys, slots, n, ok0, ok1, ocnt,
+  hipLaunchKernelGGL(dev::wc_gather_table, dim3((unsigned)g), dim3(256), 0, s, t, keys, slots, n, dn, ok0, ok1, ocnt,
                      ofirst, osoff, oslen);
+}
+void launch_bucket_offsets(const uint32_t* occupancy, uint32_t nb, uint64_t* bucket_off, uint64_t* n, hipStream_t s) {
+  hipLaunchKernelGGL(dev::wc_bucket_offsets, dim3(1), dim3(1024), 0, s, occupancy, nb, bucket_off, n);
 }
 
 void launch_reduce(const ReduceArgs& a, hipStream_t s) {

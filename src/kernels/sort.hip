@@ -12,6 +12,7 @@
 // wc_radix_scatter (stable
 // in-tile ranking with 64-lane ballots: lanes with equal digits are matched
 // with 8 ballots, ranked with popcount, waves combined through LDS).
+#include <algorithm>
 #include <utility>
 
 #include "../common/hip_util.hpp"
@@ -33,30 +34,46 @@ constexpr int RS_MAX_DB = 8;                     // digit bits per pass (11-bit 
                                                   // per-round LDS work on 2048 bins outweighs one pass fewer)
 constexpr int RS_BINS = 1 << RS_MAX_DB;
 
+// dn (nullable): the item count lives on the device and n is only an upper
+// bound: the tiles in use, ceil(*dn / tile), are spread grid-stride over a
+// grid sized from the host's estimate (hist rows keep the stride nb of n).
+__device__ __forceinline__ uint32_t rs_tiles(uint64_t n, const uint64_t* dn, uint64_t tile) {
+  return (uint32_t)(((dn ? *dn : n) + tile - 1) / tile);
+}
+
 template <int RS_ROUNDS>
-__global__ void __launch_bounds__(RS_THREADS) wc_radix_hist(const uint64_t* keys, uint64_t n, int shift, int db,
-                                                            uint32_t* hist, uint32_t nblocks, uint32_t* totals) {
+__global__ void __launch_bounds__(RS_THREADS) wc_radix_hist(const uint64_t* keys, uint64_t n, const uint64_t* dn,
+                                                            int shift, int db, uint32_t* hist, uint32_t nblocks,
+                                                            uint32_t* totals) {
   __shared__ uint32_t h[RS_BINS];
+  constexpr uint64_t TILE = RS_THREADS * RS_ROUNDS;
   const uint32_t nd = 1u << db, dmask = nd - 1;
-  for (uint32_t d = threadIdx.x; d < nd; d += RS_THREADS) h[d] = 0;
-  __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x * (RS_THREADS * RS_ROUNDS);
-  for (int r = 0; r < RS_ROUNDS; ++r) {
-    const uint64_t i = base + (uint64_t)r * RS_THREADS + threadIdx.x;
-    if (i < n) atomicAdd(&h[(keys[i] >> shift) & dmask], 1u);
-  }
-  __syncthreads();
-  for (uint32_t d = threadIdx.x; d < nd; d += RS_THREADS) {
-    hist[(size_t)d * nblocks + blockIdx.x] = h[d];
-    if (h[d]) atomicAdd(&totals[d], h[d]);
+  const uint32_t ntiles = rs_tiles(n, dn, TILE);
+  if (dn) n = *dn;
+  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    for (uint32_t d = threadIdx.x; d < nd; d += RS_THREADS) h[d] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)tile * TILE;
+    for (int r = 0; r < RS_ROUNDS; ++r) {
+      const uint64_t i = base + (uint64_t)r * RS_THREADS + threadIdx.x;
+      if (i < n) atomicAdd(&h[(keys[i] >> shift) & dmask], 1u);
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < nd; d += RS_THREADS) {
+      hist[(size_t)d * nblocks + tile] = h[d];
+      if (h[d]) atomicAdd(&totals[d], h[d]);
+    }
+    __syncthreads();  // h is cleared for the next tile
   }
 }
 
 // Block d: hist row d (tile counts of digit d, nb words) -> exclusive offsets,
 // starting at the total of all smaller digits.
-__global__ void __launch_bounds__(256) wc_radix_scan(uint32_t* hist, uint32_t nb, const uint32_t* totals) {
+__global__ void __launch_bounds__(256) wc_radix_scan(uint32_t* hist, uint32_t stride, const uint32_t* totals,
+                                                     uint64_t n, const uint64_t* dn, uint64_t tile_items) {
   __shared__ uint32_t wsum[4];
   const uint32_t d = blockIdx.x;
+  const uint32_t nb = rs_tiles(n, dn, tile_items);  // tiles in use
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // base of digit d: sum of totals[0, d)
   uint32_t x = 0;
@@ -66,7 +83,7 @@ __global__ void __launch_bounds__(256) wc_radix_scan(uint32_t* hist, uint32_t nb
   __syncthreads();
   uint32_t run = wsum[0] + wsum[1] + wsum[2] + wsum[3];
   __syncthreads();
-  uint32_t* row = hist + (size_t)d * nb;
+  uint32_t* row = hist + (size_t)d * stride;
   for (uint32_t c = 0; c < nb; c += 1024) {  // 4 consecutive words per thread
     const uint32_t b = c + 4 * tid;
     uint32_t v[4], t = 0;
@@ -101,47 +118,52 @@ __global__ void __launch_bounds__(256) wc_radix_scan(uint32_t* hist, uint32_t nb
 template <int RS_ROUNDS>
 __global__ void __launch_bounds__(RS_THREADS) wc_radix_scatter(const uint64_t* keys, const uint32_t* vals,
                                                                uint64_t* okeys, uint32_t* ovals, uint64_t n,
-                                                               int shift, int db, const uint32_t* hist,
-                                                               uint32_t nblocks) {
+                                                               const uint64_t* dn, int shift, int db,
+                                                               const uint32_t* hist, uint32_t nblocks) {
   __shared__ uint32_t run[RS_BINS];             // next output slot per digit
   __shared__ uint32_t wcnt[RS_WAVES][RS_BINS];  // per-wave digit counts, then offsets
+  constexpr uint64_t TILE = RS_THREADS * RS_ROUNDS;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t nd = 1u << db, dmask = nd - 1;
-  for (uint32_t d = tid; d < nd; d += RS_THREADS) run[d] = hist[(size_t)d * nblocks + blockIdx.x];
-  const uint64_t base = (uint64_t)blockIdx.x * (RS_THREADS * RS_ROUNDS);
+  const uint32_t ntiles = rs_tiles(n, dn, TILE);
+  if (dn) n = *dn;
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-  for (int r = 0; r < RS_ROUNDS; ++r) {
-    for (int w = 0; w < RS_WAVES; ++w)
-      for (uint32_t d = tid; d < nd; d += RS_THREADS) wcnt[w][d] = 0;
-    __syncthreads();
-    const uint64_t i = base + (uint64_t)r * RS_THREADS + tid;
-    const bool valid = i < n;
-    const uint64_t k = valid ? keys[i] : 0;
-    const uint32_t d = (uint32_t)(k >> shift) & dmask;
-    uint64_t peers = __ballot(valid);
-    for (int bit = 0; bit < db; ++bit) {  // lanes with equal digits
-      const uint64_t bb = __ballot((d >> bit) & 1);
-      peers &= ((d >> bit) & 1) ? bb : ~bb;
-    }
-    const uint32_t rank = (uint32_t)__popcll(peers & lt);
-    if (valid && rank == 0) wcnt[wave][d] = (uint32_t)__popcll(peers);
-    __syncthreads();
-    for (uint32_t e = tid; e < nd; e += RS_THREADS) {
-      uint32_t acc = run[e];
-      for (int w = 0; w < RS_WAVES; ++w) {
-        const uint32_t c = wcnt[w][e];
-        wcnt[w][e] = acc;
-        acc += c;
+  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    for (uint32_t d = tid; d < nd; d += RS_THREADS) run[d] = hist[(size_t)d * nblocks + tile];
+    const uint64_t base = (uint64_t)tile * TILE;
+    for (int r = 0; r < RS_ROUNDS; ++r) {
+      for (int w = 0; w < RS_WAVES; ++w)
+        for (uint32_t d = tid; d < nd; d += RS_THREADS) wcnt[w][d] = 0;
+      __syncthreads();
+      const uint64_t i = base + (uint64_t)r * RS_THREADS + tid;
+      const bool valid = i < n;
+      const uint64_t k = valid ? keys[i] : 0;
+      const uint32_t d = (uint32_t)(k >> shift) & dmask;
+      uint64_t peers = __ballot(valid);
+      for (int bit = 0; bit < db; ++bit) {  // lanes with equal digits
+        const uint64_t bb = __ballot((d >> bit) & 1);
+        peers &= ((d >> bit) & 1) ? bb : ~bb;
       }
-      run[e] = acc;
+      const uint32_t rank = (uint32_t)__popcll(peers & lt);
+      if (valid && rank == 0) wcnt[wave][d] = (uint32_t)__popcll(peers);
+      __syncthreads();
+      for (uint32_t e = tid; e < nd; e += RS_THREADS) {
+        uint32_t acc = run[e];
+        for (int w = 0; w < RS_WAVES; ++w) {
+          const uint32_t c = wcnt[w][e];
+          wcnt[w][e] = acc;
+          acc += c;
+        }
+        run[e] = acc;
+      }
+      __syncthreads();
+      if (valid) {
+        const uint32_t dst = wcnt[wave][d] + rank;
+        okeys[dst] = k;
+        ovals[dst] = vals[i];
+      }
+      __syncthreads();
     }
-    __syncthreads();
-    if (valid) {
-      const uint32_t dst = wcnt[wave][d] + rank;
-      okeys[dst] = k;
-      ovals[dst] = vals[i];
-    }
-    __syncthreads();
   }
 }
 
@@ -180,21 +202,23 @@ inline dim3 grid_for(uint64_t n) {
 
 constexpr int RS_MAX_PASSES = 8;  // 64-bit keys
 
-size_t radix_hist_words(uint64_t n) {
-  const uint64_t tile = (uint64_t)dev::RS_THREADS * dev::rs_rounds(n);
+size_t radix_hist_words(uint64_t n, uint64_t n_hint) {
+  const uint64_t tile = (uint64_t)dev::RS_THREADS * dev::rs_rounds(n_hint ? n_hint : n);
   const uint64_t nb = (n + tile - 1) / tile;
   return (size_t)dev::RS_BINS * (nb ? nb : 1) + (size_t)dev::RS_BINS * RS_MAX_PASSES;  // tile counts + digit totals
 }
 
-// Passes of at most 11 bits, split evenly (30 bits: 3 x 10): fewer passes than
-// 8-bit digits (4) while every digit's tile row still scans in one block.
+// 8-bit digits (11-bit ones measured slower: the per-round LDS work on 2048
+// bins outweighs one pass fewer).
 void radix_sort_pairs(uint64_t* keys, uint32_t* vals, uint64_t* tmp_keys, uint32_t* tmp_vals, uint32_t* hist,
-                      uint64_t n, int bits, hipStream_t s, bool* in_tmp) {
+                      uint64_t n, int bits, hipStream_t s, bool* in_tmp, const uint64_t* dn, uint64_t n_hint) {
   if (in_tmp) *in_tmp = false;
   if (n <= 1 || bits <= 0) return;
-  const bool small = dev::rs_rounds(n) == dev::RS_ROUNDS_SMALL;
-  const uint64_t tile = (uint64_t)dev::RS_THREADS * dev::rs_rounds(n);
-  const uint32_t nb = (uint32_t)((n + tile - 1) / tile);
+  const uint64_t est = dn && n_hint ? std::min(n, n_hint) : n;  // expected items (tile size, grid)
+  const bool small = dev::rs_rounds(n_hint ? n_hint : n) == dev::RS_ROUNDS_SMALL;
+  const uint64_t tile = (uint64_t)dev::RS_THREADS * (small ? dev::RS_ROUNDS_SMALL : dev::RS_ROUNDS_BIG);
+  const uint32_t nb = (uint32_t)((n + tile - 1) / tile);  // hist row stride (upper bound)
+  const uint32_t grid = dn ? (uint32_t)std::min<uint64_t>(nb, (est + est / 4 + tile - 1) / tile + 1) : nb;
   const int passes = (bits + dev::RS_MAX_DB - 1) / dev::RS_MAX_DB;
   const int db = (bits + passes - 1) / passes;
   uint32_t* totals = hist + (size_t)dev::RS_BINS * nb;  // [passes][2^db]
@@ -205,24 +229,25 @@ void radix_sort_pairs(uint64_t* keys, uint32_t* vals, uint64_t* tmp_keys, uint32
     const int shift = db * p;
     uint32_t* tot = totals + (size_t)dev::RS_BINS * p;
     if (small)
-      hipLaunchKernelGGL(dev::wc_radix_hist<dev::RS_ROUNDS_SMALL>, dim3(nb), dim3(dev::RS_THREADS), 0, s, ki, n, shift,
-                         db, hist, nb, tot);
+      hipLaunchKernelGGL(dev::wc_radix_hist<dev::RS_ROUNDS_SMALL>, dim3(grid), dim3(dev::RS_THREADS), 0, s, ki, n, dn,
+                         shift, db, hist, nb, tot);
     else
-      hipLaunchKernelGGL(dev::wc_radix_hist<dev::RS_ROUNDS_BIG>, dim3(nb), dim3(dev::RS_THREADS), 0, s, ki, n, shift, db,
-                         hist, nb, tot);
-    hipLaunchKernelGGL(dev::wc_radix_scan, dim3(1u << db), dim3(256), 0, s, hist, nb, tot);
+      hipLaunchKernelGGL(dev::wc_radix_hist<dev::RS_ROUNDS_BIG>, dim3(grid), dim3(dev::RS_THREADS), 0, s, ki, n, dn,
+                         shift, db, hist, nb, tot);
+    hipLaunchKernelGGL(dev::wc_radix_scan, dim3(1u << db), dim3(256), 0, s, hist, nb, tot, n, dn, tile);
     if (small)
-      hipLaunchKernelGGL(dev::wc_radix_scatter<dev::RS_ROUNDS_SMALL>, dim3(nb), dim3(dev::RS_THREADS), 0, s, ki, vi, ko,
-                         vo, n, shift, db, hist, nb);
+      hipLaunchKernelGGL(dev::wc_radix_scatter<dev::RS_ROUNDS_SMALL>, dim3(grid), dim3(dev::RS_THREADS), 0, s, ki, vi,
+                         ko, vo, n, dn, shift, db, hist, nb);
     else
-      hipLaunchKernelGGL(dev::wc_radix_scatter<dev::RS_ROUNDS_BIG>, dim3(nb), dim3(dev::RS_THREADS), 0, s, ki, vi, ko,
-                         vo, n, shift, db, hist, nb);
+      hipLaunchKernelGGL(dev::wc_radix_scatter<dev::RS_ROUNDS_BIG>, dim3(grid), dim3(dev::RS_THREADS), 0, s, ki, vi,
+                         ko, vo, n, dn, shift, db, hist, nb);
     std::swap(ki, ko);
     std::swap(vi, vo);
   }
   if (ki != keys && in_tmp) {  // odd pass count: the caller takes the result from tmp
     *in_tmp = true;
   } else if (ki != keys) {
+    WC_CHECK(dn == nullptr, "radix_sort_pairs: a device-side count needs in_tmp");
     WC_HIP_CHECK(hipMemcpyAsync(keys, ki, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
     WC_HIP_CHECK(hipMemcpyAsync(vals, vi, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   }
