@@ -98,6 +98,32 @@ def test_reset_ignores_stale_slices():
     assert_same(again, first)
 
 
+@pytest.mark.parametrize("opts", [dict(log2_tab_buckets=1, chunk_bytes=8 << 20),
+                                  dict(min_records=16384, records_per_byte=0.001, chunk_bytes=1 << 20)])
+def test_speculative_finalize_recovers(opts):
+    """count_resident leaves its last pass pending and finalizes behind it; a
+    pass that overflows (table split / shuffle-region re-run) must discard that
+    speculative result and redo it.  Same table as the fully synchronous path
+    (WC_NO_SPECULATE=1 is read at engine creation) and as the oracle."""
+    import os
+    want = ops.cpu_count(ops.synth_host(24 << 20, seed=5, vocab=50_000))
+    with ops.Engine(device=0, **opts) as e:
+        e.synth_device(24 << 20, seed=5, vocab=50_000)
+        for _ in range(2):  # the second run starts from the grown table / same capacity
+            e.reset()
+            e.count_resident(24 << 20)
+            got = e.result()
+            assert_same(got, want)
+    os.environ["WC_NO_SPECULATE"] = "1"
+    try:
+        with ops.Engine(device=0, **opts) as e:
+            e.synth_device(24 << 20, seed=5, vocab=50_000)
+            e.count_resident(24 << 20)
+            assert_same(e.result(), want)
+    finally:
+        del os.environ["WC_NO_SPECULATE"]
+
+
 def test_headline_stream_key_for_key():
     """The exact benchmark input (1 GiB, seed 1, Zipf(1.0), 100k words, one
     device chunk) against the generator-walk oracle; and 256 MiB of it against
