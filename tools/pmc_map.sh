@@ -8,7 +8,7 @@ P3="SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_LDS_ADDR_CONFLICT SQ_LDS_
 for p in 1 2 3; do
   eval C=\$P$p
   timeout -s KILL 120 rocprofv3 --pmc $C --kernel-include-regex 'wc_map|wc_reduce' -d gpurun_out/pmc_${TAG}_$p -o run --output-format csv \
-    -- python3 bench.py --steps 2 --warmup 0 "$@" > gpurun_out/pmc_${TAG}_$p.log 2>&1 || { echo "pass $p failed"; tail -3 gpurun_out/pmc_${TAG}_$p.log; }
+    -- python3 bench.py --steps 2 --warmup 0 "$@" > gpurun_out/pmc_${TAG}_$p.log 2>&1 || { echo "pass $p failed"; tail -3 gpurun_out/pmc_${TAG}_$p.log; exit 1; }
 done
 python3 - "$TAG" <<'PY'
 import csv, collections, glob, sys
