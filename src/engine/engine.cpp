@@ -62,6 +62,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   map_blocks = std::min<uint32_t>(map_blocks, RED_MAX_RUNS);
   if (const char* e = std::getenv("WC_SYNC_DEBUG")) sync_debug = std::atoi(e) != 0;
   if (const char* e = std::getenv("WC_NO_SPECULATE")) speculate = std::atoi(e) == 0;
+  if (const char* e = std::getenv("WC_SPIN_WAIT")) spin_wait = std::atoi(e) != 0;
   k1_mask = k1_hash_mask(opt.k1_hash_bits);
   if (const char* e = std::getenv("WC_MAP_STAMPS"); e && std::atoi(e)) {
     WC_HIP_CHECK(hipMalloc(&d_stamps, MAP_STAMP_N * 8));
@@ -198,14 +199,23 @@ uint32_t Engine::Impl::blocks_for(uint64_t len) const {
 void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev,
                                uint32_t log2_rb, uint32_t blocks, bool copy_occupancy) {
   WC_CHECK((reinterpret_cast<uintptr_t>(text) & 15) == 0, "chunk text must be 16-byte aligned");
-  WC_HIP_CHECK(hipMemsetAsync(d_ctr, 0, sizeof(DevCounters), s));
+  // one zeroing launch: pass counters, sampling state and, after a reset, the
+  // table occupancy and the key-arena cursor
+  ZeroList z{};
+  z.add(d_ctr, sizeof(DevCounters));
+  z.add(hot.fp, hot_clear_bytes);
+  if (reset_pending) {
+    z.add(table().occupancy, ((size_t)1 << table().log2_buckets) * 4);
+    z.add(d_arena_cursor, sizeof(unsigned long long));
+    reset_pending = false;
+  }
+  launch_zero_regions(z, s);
   pass_rec = rec;
   pass_rec.cursor = &d_ctr->records;
   pass_rec.subcap = (uint32_t)std::min<uint64_t>(rec.cap / ((uint64_t)blocks << log2_rb), 0xFFFFull);
   WC_CHECK(pass_rec.subcap > 0, "shuffle record capacity below one record per (map block, bucket)");
   MapArgs m{text, len, avail, prev, log2_rb, pass_rec, d_ctr->flags, &d_ctr->tokens, k1_mask, d_stamps};
   if (d_stamps) blocks_stamped += blocks;
-  WC_HIP_CHECK(hipMemsetAsync(hot.fp, 0, hot_clear_bytes, s));
   launch_map(m, hot, blocks, s);
   if (sync_debug) {  // WC_SYNC_DEBUG: attribute a device fault to a kernel and a chunk
     const hipError_t e = hipStreamSynchronize(s);
@@ -223,9 +233,13 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
             hipGetErrorString(e));
     WC_HIP_CHECK(e);
   }
-  WC_HIP_CHECK(hipMemcpyAsync(h_ctr, d_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));
+  // counters (+ occupancy and arena cursor, read at finalize without a sync of
+  // their own) into pinned memory: one launch
+  PubList c{};
+  c.add(h_ctr, d_ctr, sizeof(DevCounters));
   occ_copied = false;
-  if (copy_occupancy) enqueue_occupancy();  // read at finalize without a sync of its own
+  if (copy_occupancy) add_occupancy(c);
+  launch_publish(c, s);
 }
 
 void Engine::Impl::settle() {
@@ -235,12 +249,48 @@ void Engine::Impl::settle() {
   complete_pass(p.text, p.len, p.avail, p.base, p.prev, p.rb, p.blocks);
 }
 
-void Engine::Impl::enqueue_occupancy() {
+void Engine::Impl::add_occupancy(PubList& c) {
   occ_copied = true;
   const size_t nb = (size_t)1 << table().log2_buckets;
   if (h_occ.size() < nb * 4 + 8) h_occ.resize(std::max<size_t>(nb * 4 + 8, 4096));
-  WC_HIP_CHECK(hipMemcpyAsync(h_occ.data() + 8, table().occupancy, nb * 4, hipMemcpyDeviceToHost, s));
-  WC_HIP_CHECK(hipMemcpyAsync(h_occ.data(), d_arena_cursor, 8, hipMemcpyDeviceToHost, s));
+  c.add(h_occ.data() + 8, table().occupancy, nb * 4);
+  c.add(h_occ.data(), d_arena_cursor, 8);
+}
+
+void Engine::Impl::enqueue_occupancy() {
+  PubList c{};
+  add_occupancy(c);
+  launch_publish(c, s);
+}
+
+// Wait for a publish launch's sequence word: a host spin on page-locked memory
+// wakes within a microsecond of the kernel's store, where a stream sync waits
+// for the completion signal and the runtime's wake-up (~20-30 us of GPU idle
+// per job, profiles/r2_plumbing.md).  The stream is polled now and then so a
+// device fault still surfaces as an error; the stream sync at the end returns
+// at once (everything before the publish launch has completed).
+void Engine::Impl::wait_published(const uint32_t* seq, uint32_t want) {
+  for (uint64_t it = 1;; ++it) {
+    if (__atomic_load_n(seq, __ATOMIC_ACQUIRE) == want) break;
+    if ((it & 0xFFFF) == 0) {
+      const hipError_t e = hipStreamQuery(s);
+      if (e != hipErrorNotReady) {
+        WC_HIP_CHECK(e);
+        if (__atomic_load_n(seq, __ATOMIC_ACQUIRE) != want) fail("publish launch completed without its sequence word");
+        break;
+      }
+    }
+    __builtin_ia32_pause();
+  }
+}
+
+void Engine::Impl::apply_reset() {
+  if (!reset_pending) return;
+  ZeroList z{};
+  z.add(table().occupancy, ((size_t)1 << table().log2_buckets) * 4);
+  z.add(d_arena_cursor, sizeof(unsigned long long));
+  launch_zero_regions(z, s);
+  reset_pending = false;
 }
 
 // Bucket offsets and key count from the occupancy copied with the last pass's
@@ -281,8 +331,8 @@ void Engine::Impl::split_table() {
 }
 
 bool Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev,
-                                 uint32_t log2_rb, uint32_t blocks) {
-  WC_HIP_CHECK(hipStreamSynchronize(s));
+                                 uint32_t log2_rb, uint32_t blocks, bool synced) {
+  if (!synced) WC_HIP_CHECK(hipStreamSynchronize(s));
   DevCounters c = *h_ctr;
   if (c.flags[FLAG_REGION_OVF]) {
     // Shuffle regions too small for this chunk's record skew: the reduce was
@@ -325,8 +375,10 @@ bool Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
                   avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
                   d_ctr->flags, d_bucket_ovf, d_bucket_en, d_red_stamps};
     launch_reduce(ra, s);
-    WC_HIP_CHECK(hipMemcpyAsync(h_ctr, d_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, s));
-    enqueue_occupancy();
+    PubList pc{};
+    pc.add(h_ctr, d_ctr, sizeof(DevCounters));
+    add_occupancy(pc);
+    launch_publish(pc, s);
     WC_HIP_CHECK(hipStreamSynchronize(s));
     c = *h_ctr;
     max_occ = std::max(max_occ, c.flags[FLAG_MAX_OCC]);
@@ -426,12 +478,23 @@ bool Engine::Impl::finalize_local_speculative() {
   radix_sort_pairs(keys, slots, tkeys, tslots, hist, cap, bits, s, &in_tmp, d_n, hint);
   launch_gather_table(t, in_tmp ? tkeys : keys, in_tmp ? tslots : slots, cap, o.k0, o.k1, o.cnt, o.first, o.sref_off,
                       o.sref_len, s, d_n);
-  if (h_spec.size() < 16) h_spec.resize(4096);
-  WC_HIP_CHECK(hipMemcpyAsync(h_spec.data(), d_n, 8, hipMemcpyDeviceToHost, s));
-  WC_HIP_CHECK(hipMemcpyAsync(h_spec.data() + 8, d_arena_cursor, 8, hipMemcpyDeviceToHost, s));
-  WC_HIP_CHECK(hipStreamSynchronize(s));
+  if (h_spec.size() < 32) {
+    h_spec.resize(4096);
+    std::memset(h_spec.data(), 0, h_spec.size());  // the sequence word starts below every spec_seq
+  }
+  PubList pc{};
+  pc.add(h_spec.data(), d_n, 8);
+  pc.add(h_spec.data() + 8, d_arena_cursor, 8);
+  uint32_t* seq = reinterpret_cast<uint32_t*>(h_spec.data() + 16);
+  if (spin_wait) {
+    pc.seq_dst = seq;
+    pc.seq = ++spec_seq;
+  }
+  launch_publish(pc, s);
+  if (spin_wait) wait_published(seq, spec_seq);
+  else WC_HIP_CHECK(hipStreamSynchronize(s));
   // the pass's counters arrived with this sync: check it (stats, recovery)
-  if (!complete_pass(p.text, p.len, p.avail, p.base, p.prev, p.rb, p.blocks)) return false;
+  if (!complete_pass(p.text, p.len, p.avail, p.base, p.prev, p.rb, p.blocks, true)) return false;
   uint64_t n = 0, arena_used = 0;
   std::memcpy(&n, h_spec.data(), 8);
   std::memcpy(&arena_used, h_spec.data() + 8, 8);
@@ -563,11 +626,12 @@ void Engine::reset() {
   // zero only the occupancy: a bucket with occupancy 0 is empty whatever its
   // slice holds (reduce / compact / split never read such a slice)
   im.pend.active = false;  // an unchecked pass of the previous job is discarded with it
-  WC_HIP_CHECK(hipMemsetAsync(im.table().occupancy, 0, ((size_t)1 << im.table().log2_buckets) * 4, im.s));
+  // no API call: the next pass's zeroing launch clears occupancy + arena cursor
+  // (apply_reset does it first for anything else that reads the table)
+  im.reset_pending = true;
   im.occ_valid = false;
-  WC_HIP_CHECK(hipMemsetAsync(im.d_arena_cursor, 0, sizeof(unsigned long long), im.s));
-  // no sync: the next pass is stream-ordered behind the clear
-  if (im.copy_s) WC_HIP_CHECK(hipStreamSynchronize(im.copy_s));  // a failed stream may have left copies
+  if (im.copy_used) WC_HIP_CHECK(hipStreamSynchronize(im.copy_s));  // a failed stream may have left copies
+  im.copy_used = false;
   im.st = Stats{};
   im.max_end = 0;
 }
@@ -623,6 +687,7 @@ void Engine::count_source(ChunkSource& src, uint64_t global_base) {
   if (const char* e = std::getenv("WC_STREAM_CHUNK")) stream = std::strtoull(e, nullptr, 10);  // sweeps only
   const uint64_t C = std::min(im.opt.chunk_bytes, std::max<uint64_t>(1ull << 20, stream / 256 * 256));
   im.ensure_staging(C);
+  im.copy_used = true;
   std::vector<uint8_t> carry;
   bool eof = false;
   uint64_t offset = global_base;
@@ -692,6 +757,7 @@ void Engine::count_pinned_replay(const uint8_t* pool, uint64_t pool_bytes, uint6
     im.registered = pool;
   }
   im.ensure_staging(C);
+  im.copy_used = true;
   WC_HIP_CHECK(hipEventRecord(im.ev_done[0], im.s));
   WC_HIP_CHECK(hipEventRecord(im.ev_done[1], im.s));
   const uint64_t nchunks = (total + C - 1) / C;
@@ -753,6 +819,8 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
   // the RCCL exchange code is exercised on a one-GPU box
   static const bool merge_always = getenv("WC_MERGE_ALWAYS") && atoi(getenv("WC_MERGE_ALWAYS")) != 0;
   const bool merged = comm && (comm->size() > 1 || merge_always);
+  im.apply_reset();  // a reset with no pass since: the table reads empty
+  bool drained = false;
   if (merged) {
     im.settle();
     im.compact_local();
@@ -760,13 +828,15 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
     merge_cols(im, *comm, all_ranks);
     im.st.merge_ms += (now_seconds() - tm) * 1e3;
     im.sort_cols_by_first();
-  } else if (!(im.pend.active && im.finalize_local_speculative())) {
+  } else if (im.pend.active && im.finalize_local_speculative()) {
+    drained = im.spin_wait;  // its publish wait saw the whole stream complete
+  } else {
     im.settle();
     im.finalize_local_sorted();  // sort (first, slot) pairs, gather the columns from the table once
   }
   // the merge's last collectives are still in flight: wait under the comm watchdog
   if (merged) comm->sync(im.s);
-  else WC_HIP_CHECK(hipStreamSynchronize(im.s));
+  else if (!drained) WC_HIP_CHECK(hipStreamSynchronize(im.s));
   im.st.finalize_ms += (now_seconds() - t0) * 1e3;
   WC_LOG(LOG_INFO, "dev %d: finalize %.3f ms (merge %.3f ms), %llu keys, %u chunk(s), %llu records, %u re-run(s)",
          im.dev, (now_seconds() - t0) * 1e3, im.st.merge_ms, (unsigned long long)im.cols.n, im.st.chunks,

@@ -121,7 +121,7 @@ struct Engine::Impl {
   void launch_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev, uint32_t log2_rb,
                    uint32_t blocks, bool copy_occupancy = true);
   bool complete_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev, uint32_t log2_rb,
-                     uint32_t blocks);
+                     uint32_t blocks, bool synced = false);  // synced: the stream has drained (publish waited)
   struct PendingPass {
     bool active = false;
     const uint8_t* text = nullptr;
@@ -129,9 +129,17 @@ struct Engine::Impl {
     int prev = -1;
     uint32_t rb = 0, blocks = 0;
   } pend;
+  // Engine::reset() only marks the table empty; the next pass's zeroing kernel
+  // (or apply_reset, before anything else reads the table) clears it.
+  bool reset_pending = false;
+  bool copy_used = false;  // copy_s carried H2D copies since the last reset
+  void apply_reset();
   bool speculate = true;  // WC_NO_SPECULATE=1: every pass synchronous
   uint64_t last_keys = 0;  // keys of the previous finalize (sort size hint)
-  PinnedBuffer h_spec;     // speculative finalize: key count + arena cursor
+  PinnedBuffer h_spec;     // speculative finalize: key count + arena cursor + publish sequence word
+  bool spin_wait = true;   // WC_SPIN_WAIT=0: wait for the finalize with a stream sync instead
+  uint32_t spec_seq = 0;
+  void wait_published(const uint32_t* seq, uint32_t want);
   void settle();           // complete a pending pass
   uint32_t blocks_for(uint64_t len) const;
   // Shuffle partitions track the running table (one reduce block reads only
@@ -143,6 +151,7 @@ struct Engine::Impl {
 
   uint64_t finalize(Comm* comm, bool all_ranks);  // compact [+ merge] + order by first
   void enqueue_occupancy();                 // async D2H of occupancy + arena cursor into h_occ
+  void add_occupancy(PubList& c);           // the same as regions of a publish launch
   uint64_t host_occupancy(uint64_t*& boff, uint64_t& arena_used);  // h_occ (sync only if stale) -> offsets, n
   void compact_local();                     // table -> cols (unsorted)
   void finalize_local_sorted();             // table -> cols ordered by first (no merge: no column copy)

@@ -188,6 +188,34 @@ void launch_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* 
                         uint64_t* ocnt, uint64_t* ofirst, uint64_t* osoff, uint32_t* oslen, uint64_t n, hipStream_t s);
 void launch_iota_u32(uint32_t* v, uint64_t n, hipStream_t s);
 
+// util.hip: zero several device regions / copy several small device regions
+// into page-locked host memory, one launch each (sizes in 32-bit words).
+constexpr int ZERO_MAX_REGIONS = 6, PUB_MAX_REGIONS = 4;
+struct ZeroList {
+  uint32_t* ptr[ZERO_MAX_REGIONS];
+  uint64_t words[ZERO_MAX_REGIONS];
+  int n;
+  void add(void* p, uint64_t bytes) {
+    ptr[n] = static_cast<uint32_t*>(p);
+    words[n++] = bytes / 4;
+  }
+};
+struct PubList {
+  const uint32_t* src[PUB_MAX_REGIONS];
+  uint32_t* dst[PUB_MAX_REGIONS];
+  uint32_t words[PUB_MAX_REGIONS];
+  int n;
+  uint32_t* seq_dst;  // nullable: written last (system-scope release) with seq, for a host spin-wait
+  uint32_t seq;
+  void add(void* host_dst, const void* dev_src, uint64_t bytes) {
+    dst[n] = static_cast<uint32_t*>(host_dst);
+    src[n] = static_cast<const uint32_t*>(dev_src);
+    words[n++] = (uint32_t)(bytes / 4);
+  }
+};
+void launch_zero_regions(const ZeroList& z, hipStream_t s);
+void launch_publish(const PubList& c, hipStream_t s);
+
 void launch_synth(uint8_t* out, uint64_t n, uint64_t first_segment, uint64_t seed, const SynthVocab& v,
                   hipStream_t s);
 

@@ -1,0 +1,67 @@
+// util.hip — two small launch-count kernels of the pass / finalize plumbing.
+//
+//  wc_zero_regions  zeroes up to ZERO_MAX_REGIONS device regions in ONE launch:
+//                   the per-pass counters + hot-key sampling state, and (after
+//                   Engine::reset) the table occupancy and key-arena cursor.  It
+//                   replaces four hipMemsetAsync calls whose host-side enqueue
+//                   cost (~5-12 us each, profiles/r2_plumbing.md) left the GPU
+//                   idle between the previous job's sync and the next map.
+//  wc_publish       copies up to PUB_MAX_REGIONS small device regions (pass
+//                   counters, bucket occupancy, key count, arena cursor) into
+//                   page-locked host memory in ONE launch, instead of one
+//                   copy-engine blit per region.
+//
+// Reference: the reference has neither (main.cu:143-161 copies its two result
+// arrays with blocking cudaMemcpy); these exist because the MI355X step is
+// ~1.4 ms and a dozen tiny host-enqueued operations per step are a few %.
+#include <algorithm>
+
+#include "../common/hip_util.hpp"
+#include "kernels.hpp"
+
+namespace wc {
+namespace dev {
+
+__global__ void __launch_bounds__(256) wc_zero_regions(ZeroList z) {
+  const uint64_t tid = blockIdx.x * 256ull + threadIdx.x, stride = (uint64_t)gridDim.x * 256;
+  for (int r = 0; r < z.n; ++r) {
+    uint32_t* p = z.ptr[r];
+    const uint64_t words = z.words[r];
+    const uint64_t quads = (reinterpret_cast<uintptr_t>(p) & 15) == 0 ? words / 4 : 0;
+    uint4* q = reinterpret_cast<uint4*>(p);
+    for (uint64_t i = tid; i < quads; i += stride) q[i] = make_uint4(0, 0, 0, 0);
+    for (uint64_t i = quads * 4 + tid; i < words; i += stride) p[i] = 0;
+  }
+}
+
+__global__ void __launch_bounds__(256) wc_publish(PubList c) {
+  for (int r = 0; r < c.n; ++r) {
+    const uint32_t* src = c.src[r];
+    uint32_t* dst = c.dst[r];
+    for (uint32_t i = threadIdx.x; i < c.words[r]; i += 256) dst[i] = src[i];
+  }
+  __threadfence_system();
+  if (c.seq_dst) {
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(c.seq_dst, c.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+}  // namespace dev
+
+void launch_zero_regions(const ZeroList& z, hipStream_t s) {
+  if (z.n == 0) return;
+  WC_CHECK(z.n <= ZERO_MAX_REGIONS, "launch_zero_regions: too many regions");
+  uint64_t most = 0;
+  for (int r = 0; r < z.n; ++r) most = z.words[r] > most ? z.words[r] : most;
+  const uint64_t blocks = std::min<uint64_t>(256, std::max<uint64_t>(1, (most / 4 + 255) / 256));
+  hipLaunchKernelGGL(dev::wc_zero_regions, dim3((unsigned)blocks), dim3(256), 0, s, z);
+}
+
+void launch_publish(const PubList& c, hipStream_t s) {
+  if (c.n == 0) return;
+  WC_CHECK(c.n <= PUB_MAX_REGIONS, "launch_publish: too many regions");
+  hipLaunchKernelGGL(dev::wc_publish, dim3(1), dim3(256), 0, s, c);
+}
+
+}  // namespace wc
