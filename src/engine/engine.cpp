@@ -90,15 +90,15 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   rec.count = rec_mem.take_n<uint32_t>(ncount);
 
   hot_mem.reserve(HOT_TABLE_CAP * (8 + 4) + HOT_TABLE_CAP * 16 + 2 * MAP_SLOTS * 8 + (HOT_SEL_BINS + 3) * 4 +
-                  MAP_SLOTS + 8192);
+                  HOT_GROUPS * 4 + 8192);
   hot.cap = HOT_TABLE_CAP;
   hot.fp = hot_mem.take_n<unsigned long long>(HOT_TABLE_CAP);
   hot.cnt = hot_mem.take_n<uint32_t>(HOT_TABLE_CAP);
   hot.img_sig = hot_mem.take_n<uint64_t>(MAP_SLOTS);  // cleared region: fp .. gocc (one memset)
   hot.img_side = hot_mem.take_n<uint64_t>(MAP_SLOTS);
   hot.sel = hot_mem.take_n<uint32_t>(HOT_SEL_BINS + 3);
-  hot.gocc = hot_mem.take_n<uint32_t>(MAP_SLOTS / 4);
-  hot_clear_bytes = (size_t)(reinterpret_cast<uint8_t*>(hot.gocc + MAP_SLOTS / 4) - reinterpret_cast<uint8_t*>(hot.fp));
+  hot.gocc = hot_mem.take_n<uint32_t>(HOT_GROUPS);
+  hot_clear_bytes = (size_t)(reinterpret_cast<uint8_t*>(hot.gocc + HOT_GROUPS) - reinterpret_cast<uint8_t*>(hot.fp));
   hot.sig = hot_mem.take_n<uint64_t>(HOT_TABLE_CAP);
   hot.side = hot_mem.take_n<uint64_t>(HOT_TABLE_CAP);
   WC_HIP_CHECK(hipMalloc(&d_ctr, sizeof(DevCounters)));

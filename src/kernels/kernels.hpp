@@ -112,9 +112,20 @@ struct HotArgs {
   uint64_t* img_sig;       // [MAP_SLOTS] zeroed before each chunk
   uint64_t* img_side;      // [MAP_SLOTS]
   uint32_t* sel;           // [HOT_SEL_BINS + 3] zeroed: count histogram, threshold, tie quota / counter
-  uint32_t* gocc;          // [MAP_SLOTS / 4] zeroed: fill of each image group
+  uint32_t* gocc;          // [HOT_GROUPS] zeroed: fill of each image group
 };
 constexpr uint64_t HOT_TABLE_CAP = 1ull << 18;
+// Map hot-table geometry: 2-choice groups of HOT_GROUP_SLOTS signatures.  Two
+// slots per group (4 candidate compares and two 16-byte probe reads per token)
+// holds 7/8 of the slots at the hit rate that 4-slot groups (8 compares, four
+// reads) reach at 3/4 (profiles/r2_plumbing.md: greedy 2-choice placement
+// simulated on Zipf(1.0)).
+#ifndef WC_HOT_GS
+#define WC_HOT_GS 2
+#endif
+constexpr int HOT_GROUP_SLOTS = WC_HOT_GS;
+constexpr int HOT_GROUPS = MAP_SLOTS / HOT_GROUP_SLOTS;
+static_assert(HOT_GROUP_SLOTS == 2 || HOT_GROUP_SLOTS == 4, "hot-table groups of 2 or 4 slots");
 constexpr int HOT_SEL_BINS = 4096;
 constexpr int HOT_SEL_BLOCKS = 256;
 

@@ -11,7 +11,7 @@
 //                 to a global fingerprint table (one global atomic per distinct
 //                 word per block);
 //  wc_hot_hist / _threshold / _place  keep the HOT_K most frequent sampled
-//                 words and place them in a 2-choice, 4-slot-group table image
+//                 words and place them in a 2-choice table image of 2-slot groups
 //                 (4096 slots of 64-bit signatures + side words);
 //  wc_map         persistent, ONE 1024-thread block (16 waves) per CU over a
 //                 contiguous range of 2 KiB text units.  The block loads the
@@ -47,11 +47,11 @@ constexpr int UNIT = 64 * MAP_BPL;     // text bytes per wave unit (2 KiB)
 constexpr int HALO = 64;               // bytes past the unit kept in LDS
 constexpr int BUF = UNIT + HALO + 24;  // + one 24-byte window read past the halo
 constexpr uint32_t NONE = 0xFFFFFFFFu;
-constexpr int GS = 4;                  // slots per group
-constexpr int NG = MAP_SLOTS / GS;     // groups
+constexpr int GS = HOT_GROUP_SLOTS;    // slots per group
+constexpr int NG = HOT_GROUPS;         // groups
 constexpr int SPT = MAP_SLOTS / MAP_THREADS;
 #ifndef WC_HOT_K
-#define WC_HOT_K (MAP_SLOTS * 3 / 4)
+#define WC_HOT_K (HOT_GROUP_SLOTS == 2 ? MAP_SLOTS * 7 / 8 : MAP_SLOTS * 3 / 4)
 #endif
 #ifndef WC_HOT_SAMPLE
 #define WC_HOT_SAMPLE 4
@@ -87,7 +87,10 @@ __device__ __forceinline__ void sig_key(uint64_t sig, uint64_t side, uint64_t& k
 // [p, p+8) and w1 = [p+8, p+16), and its table signature.
 __device__ __forceinline__ void inline_key(uint64_t w0, uint64_t w1, uint32_t len, uint64_t& k0, uint64_t& k1,
                                            uint64_t& sig) {
-  k0 = len >= 8 ? w0 : (w0 & ((1ull << (8 * len)) - 1ull));
+  // k0: the first min(len, 8) bytes — a shift pair by 64 - 8 min(len, 8) in
+  // [0, 56] (len 0 of an empty lane clamps to 1: no shift by 64)
+  const uint32_t s0 = 64u - 8u * min(max(len, 1u), 8u);
+  k0 = (w0 << s0) >> s0;
   const uint32_t tl = len > 8 ? len - 8 : 0u;
   const uint64_t t = w1 & ((1ull << (8 * tl)) - 1ull);
   const uint64_t lt = (uint64_t)len << 56;
@@ -95,10 +98,14 @@ __device__ __forceinline__ void inline_key(uint64_t w0, uint64_t w1, uint32_t le
   sig = (len <= 7 ? k0 : ((t ^ k0) & LOW7)) | lt;
 }
 
-// Slot i of group g: slots 0-1 of every group form the first half of the
-// table, slots 2-3 the second, so each 16-byte probe read of a group half
-// lands on bank quad (g mod 16) — all 16 quads — instead of only even / odd.
-__device__ __forceinline__ uint32_t slot_of(uint32_t g, uint32_t i) { return (i < 2 ? 0u : MAP_SLOTS / 2) + 2 * g + (i & 1); }
+// Slot i of group g.  4-slot groups: slots 0-1 of every group form the first
+// half of the table, slots 2-3 the second, so each 16-byte probe read of a
+// group half lands on bank quad (g mod 16) — all 16 quads — instead of only
+// even / odd.  2-slot groups: one 16-byte read per group, slots 2g, 2g + 1.
+__device__ __forceinline__ uint32_t slot_of(uint32_t g, uint32_t i) {
+  if (GS == 2) return 2 * g + i;
+  return (i < 2 ? 0u : MAP_SLOTS / 2) + 2 * g + (i & 1);
+}
 
 // The two candidate groups of a key (2-choice placement; g2 != g1).
 __device__ __forceinline__ void hot_groups(uint32_t ph, uint32_t& g1, uint32_t& g2) {
@@ -358,6 +365,12 @@ struct alignas(16) MapLds {
 };
 static_assert(sizeof(MapLds) + 8 * MAP_STAMP_N <= 160 * 1024, "one map block per CU");
 
+// Index (0..3) of the first of a key's four candidate signatures equal to sig, else -1.
+__device__ __forceinline__ int sig_match4(const u64x2& a, const u64x2& b, uint64_t sig) {
+  const uint32_t m = (a.x == sig ? 1u : 0u) | (a.y == sig ? 2u : 0u) | (b.x == sig ? 4u : 0u) | (b.y == sig ? 8u : 0u);
+  return (int)__ffs(m) - 1;
+}
+
 // Index (0..7) of the first of a key's eight candidate signatures equal to sig, else -1.
 __device__ __forceinline__ int sig_match8(const u64x2& a, const u64x2& b, const u64x2& c, const u64x2& d,
                                           uint64_t sig) {
@@ -464,14 +477,15 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
       // ---- list round: entries [base, base + MAP_LIST) of the unit ----
       const uint32_t lim = base + MAP_LIST;
       const uint32_t dlo = (uint32_t)dm, dhi = (uint32_t)(dm >> 32);
+      // delimiter bits from the token start on (i < 32: one funnel shift); none
+      // within 31 bytes -> MAP_LONG: ffbl of 0 is all ones, and the u16 entry
+      // keeps 5 length bits, so (ffbl << 11) needs no clamp
+      static_assert(MAP_LONG == 31, "list entries: 11 position bits + 5 length bits");
       while (bits && k < lim) {
         const uint32_t i = __ffs(bits) - 1;
         bits &= bits - 1;
-        // delimiter bits from the token start on (i < 32: one funnel shift); none
-        // within 31 bytes -> MAP_LONG (ffbl of 0 is all ones)
         const uint32_t rest = __builtin_amdgcn_alignbit(dhi, dlo, i);
-        const uint32_t len = min(ffbl_raw(rest), MAP_LONG);
-        list[k - base] = (uint16_t)((pbase + i) | (len << 11));
+        list[k - base] = (uint16_t)((pbase + i) | (ffbl_raw(rest) << 11));
         ++k;
       }
       wave_sync();
@@ -504,16 +518,27 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
           sink ^= as ^ bs ^ ga2 ^ gb2;
           return;
         }
-        const u64x2* S = reinterpret_cast<const u64x2*>(L.sig);  // S[g]: slots 0-1, S[NG + g]: slots 2-3
-        const u64x2 xa0 = S[ga1], xa1 = S[NG + ga1], xa2 = S[ga2], xa3 = S[NG + ga2];
+        const u64x2* S = reinterpret_cast<const u64x2*>(L.sig);
         int s1 = -1, s2 = -1;
-        if (TWO) {
-          const u64x2 xb0 = S[gb1], xb1 = S[NG + gb1], xb2 = S[gb2], xb3 = S[NG + gb2];
-          const int mb = in2 ? sig_match8(xb0, xb1, xb2, xb3, bs) : -1;
-          s2 = mb < 0 ? -1 : (int)slot_of(mb < GS ? gb1 : gb2, mb & (GS - 1));
+        if constexpr (GS == 2) {  // S[g]: both slots of group g
+          const u64x2 xa0 = S[ga1], xa1 = S[ga2];
+          if (TWO) {
+            const u64x2 xb0 = S[gb1], xb1 = S[gb2];
+            const int mb = in2 ? sig_match4(xb0, xb1, bs) : -1;
+            s2 = mb < 0 ? -1 : (int)slot_of(mb < GS ? gb1 : gb2, mb & (GS - 1));
+          }
+          const int ma = in1 ? sig_match4(xa0, xa1, as) : -1;
+          s1 = ma < 0 ? -1 : (int)slot_of(ma < GS ? ga1 : ga2, ma & (GS - 1));
+        } else {  // S[g]: slots 0-1, S[NG + g]: slots 2-3
+          const u64x2 xa0 = S[ga1], xa1 = S[NG + ga1], xa2 = S[ga2], xa3 = S[NG + ga2];
+          if (TWO) {
+            const u64x2 xb0 = S[gb1], xb1 = S[NG + gb1], xb2 = S[gb2], xb3 = S[NG + gb2];
+            const int mb = in2 ? sig_match8(xb0, xb1, xb2, xb3, bs) : -1;
+            s2 = mb < 0 ? -1 : (int)slot_of(mb < GS ? gb1 : gb2, mb & (GS - 1));
+          }
+          const int ma = in1 ? sig_match8(xa0, xa1, xa2, xa3, as) : -1;
+          s1 = ma < 0 ? -1 : (int)slot_of(ma < GS ? ga1 : ga2, ma & (GS - 1));
         }
-        const int ma = in1 ? sig_match8(xa0, xa1, xa2, xa3, as) : -1;
-        s1 = ma < 0 ? -1 : (int)slot_of(ma < GS ? ga1 : ga2, ma & (GS - 1));
         // two-word keys: the matching slot's side word decides
         const bool ta = two_word(as), tb = TWO && two_word(bs);
         const uint64_t ca = s1 >= 0 && ta ? L.side[s1] : a0, cb = s2 >= 0 && tb ? L.side[s2] : b0;

@@ -20,17 +20,33 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
 // Bytes [p, p+8) and [p+8, p+16) of an 8-byte-aligned LDS text buffer from
-// three ALIGNED ds_read_b64 and two funnel shifts (an unaligned 16-byte read
-// stalls the LDS pipe: SQ_LDS_UNALIGNED_STALL was a third of its busy cycles).
-// The buffer must be readable 24 bytes past p & ~7.
+// ALIGNED reads and funnel shifts (an unaligned 16-byte read stalls the LDS
+// pipe: SQ_LDS_UNALIGNED_STALL was a third of its busy cycles).  The buffer
+// must be readable 24 bytes past p & ~7.
+#ifndef WC_WIN_ALIGNBYTE
+#define WC_WIN_ALIGNBYTE 1
+#endif
 __device__ __forceinline__ void window16(const uint8_t* buf, uint32_t p, uint64_t& w0, uint64_t& w1) {
+#if WC_WIN_ALIGNBYTE
+  // five dwords from the 4-byte-aligned address below p (two ds_read2_b32 +
+  // one ds_read_b32: no unaligned LDS access) and four v_alignbyte_b32 funnels
+  // by p & 3 — 5 VALU per window instead of 11 for the 8-byte-aligned
+  // 64-bit-shift form (which needs a dword select for shifts >= 4)
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(buf + (p & ~3u));
+  const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
+  const uint32_t sh = p & 3u;
+  const uint32_t a = __builtin_amdgcn_alignbyte(d1, d0, sh), b = __builtin_amdgcn_alignbyte(d2, d1, sh);
+  const uint32_t c = __builtin_amdgcn_alignbyte(d3, d2, sh), d = __builtin_amdgcn_alignbyte(d4, d3, sh);
+  w0 = (uint64_t)a | ((uint64_t)b << 32);
+  w1 = (uint64_t)c | ((uint64_t)d << 32);
+#else
   const uint64_t* q = reinterpret_cast<const uint64_t*>(buf + (p & ~7u));
   const uint64_t d0 = q[0], d1 = q[1], d2 = q[2];
   const uint32_t sh = (p & 7u) * 8u;
   // (x << 1) << (63 - sh) == x << (64 - sh) without the undefined shift by 64 at sh = 0
-  // (64-bit shifts measured faster here than a 32-bit v_alignbyte_b32 funnel)
   w0 = (d0 >> sh) | ((d1 << 1) << (63 - sh));
   w1 = (d1 >> sh) | ((d2 << 1) << (63 - sh));
+#endif
 }
 
 __device__ __forceinline__ void wave_sync() {
@@ -48,12 +64,12 @@ __device__ __forceinline__ uint32_t delim_bits4(uint32_t x) {
 }
 
 // v_ffbl_b32 as the hardware defines it: index of the lowest set bit, all ones
-// for 0 (the builtins add a select for 0).
-__device__ __forceinline__ uint32_t ffbl_raw(uint32_t x) {
-  uint32_t r;
-  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
-  return r;
-}
+// for 0.  __builtin_ctz is zero-undefined, so it lowers to the bare v_ffbl_b32
+// (no select for 0); callers keep only the low 5 bits of the result or shift
+// it out of a 16-bit entry, which is the same for 31 and all ones.  (An inline
+// asm v_ffbl made the waitcnt pass drain LDS before every use: an lgkmcnt(0)
+// per token-list iteration.)
+__device__ __forceinline__ uint32_t ffbl_raw(uint32_t x) { return (uint32_t)__builtin_ctz(x); }
 
 // Wave-wide exclusive prefix sum of a small per-lane value v < 32 (bit
 // decomposition over ballots: no cross-lane shuffles); total = wave sum.
