@@ -352,11 +352,14 @@ __global__ void __launch_bounds__(1024) wc_hot_place(HotArgs h, int pass) {
 }
 
 // ------------------------------------------------------------------ map
+// cnt / off first: every per-token LDS address (the two hit atomics at 4 s
+// and 16 KiB + 4 s, the probe reads at 32 KiB + 16 g) is one VGPR plus an
+// immediate ds offset (< 64 KiB) — no VALU add per token
 struct alignas(16) MapLds {
-  alignas(16) uint64_t sig[MAP_SLOTS];  // hot table image (read-only while tokens stream); 0 = empty
-  uint64_t side[MAP_SLOTS];             // k0 of two-word signatures
   uint32_t cnt[MAP_SLOTS];
   uint32_t off[MAP_SLOTS];              // chunk-relative first offset in the block
+  alignas(16) uint64_t sig[MAP_SLOTS];  // hot table image (read-only while tokens stream); 0 = empty
+  uint64_t side[MAP_SLOTS];             // k0 of two-word signatures
   uint16_t list[MAP_WAVES][MAP_LIST];
   uint32_t bcur[MAX_REC_BUCKETS];       // records appended to each bucket's sub-region (short | long << 16)
   alignas(16) uint8_t buf[MAP_WAVES][BUF];
@@ -557,7 +560,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
         if (WC_MAP_ABLATE == 3) return;
         // misses of inline words become records now; LONG words wait for the round end
         const bool d1 = in1 && s1 < 0, d2 = TWO && in2 && s2 < 0;
-        emit_two(L.bcur, a, rout, d1, ha & bmask, a0, a1, o1, d2, hb & bmask, b0, b1, o2);
+        emit_two(L.bcur, a, rout, d1, ha & bmask, a0, a1, o1, n1, d2, hb & bmask, b0, b1, o2, n2);
         const bool f1 = h1 && !in1, f2 = TWO && h2 && !in2;
         const uint64_t mf1 = __ballot(f1), mf2 = TWO ? __ballot(f2) : 0ull;
         if (mf1 | mf2) {  // entries before j are consumed: ndef <= j

@@ -171,12 +171,21 @@ __device__ __forceinline__ void emit_record(uint32_t* bcur, const MapArgs& a, co
 #define WC_EMIT_ABLATE 0
 #endif
 
+// rec12_fits for one occurrence of an inline word of known length n: a word
+// of <= 8 bytes whose last byte is nonzero, i.e. k0 >> 8 (n - 1) != 0 (k0
+// holds exactly n bytes).  The shift is masked, so n = 0 of an empty lane is
+// harmless.
+__device__ __forceinline__ bool rec12_inline(uint64_t k0, uint32_t n) {
+  return n - 1u < 8u && (k0 >> ((8u * n - 8u) & 63u)) != 0;
+}
+
 // Two single-occurrence records of one lane (either may be absent): both
 // cursor atomics are issued before either store waits for its position.
+// n1 / n2: the words' lengths (inline keys).
 __device__ __forceinline__ void emit_two(uint32_t* bcur, const MapArgs& a, const RecOut& o, bool d1, uint32_t b1,
-                                         uint64_t x0, uint64_t x1, uint32_t o1, bool d2, uint32_t b2, uint64_t y0,
-                                         uint64_t y1, uint32_t o2) {
-  const bool s1 = rec12_fits(x0, x1, 1), s2 = rec12_fits(y0, y1, 1);
+                                         uint64_t x0, uint64_t x1, uint32_t o1, uint32_t n1, bool d2, uint32_t b2,
+                                         uint64_t y0, uint64_t y1, uint32_t o2, uint32_t n2) {
+  const bool s1 = rec12_inline(x0, n1), s2 = rec12_inline(y0, n2);
   uint32_t p1 = 0, p2 = 0;
   if (WC_EMIT_ABLATE & 2) {
     p1 = (__lane_id() & 7) * 0x10001u;
