@@ -34,8 +34,9 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 def parse():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=1000,
+                    help="timed steps (default ~1.4 s of GPU work at 1 GiB: long enough for an external utilisation sampler)")
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="1gb", help="BASELINE config (cuda_mapreduce_amd.models.CONFIGS)")
     ap.add_argument("--gb-per-gpu", type=float, default=None, help="override: GiB of synthetic text per GPU")
     ap.add_argument("--vocab", type=int, default=None)

@@ -30,7 +30,10 @@ constexpr int RS_ROUNDS_BIG = 8, RS_ROUNDS_SMALL = 2;
 constexpr uint64_t RS_SMALL_N = 1ull << 19;
 __host__ __device__ constexpr int rs_rounds(uint64_t n) { return n < RS_SMALL_N ? RS_ROUNDS_SMALL : RS_ROUNDS_BIG; }
 constexpr int RS_WAVES = RS_THREADS / 64;
-constexpr int RS_MAX_DB = 8;                     // digit bits per pass (11-bit digits measured slower: the
+#ifndef WC_RS_DB
+#define WC_RS_DB 8
+#endif
+constexpr int RS_MAX_DB = WC_RS_DB;              // digit bits per pass (11-bit digits measured slower: the
                                                   // per-round LDS work on 2048 bins outweighs one pass fewer)
 constexpr int RS_BINS = 1 << RS_MAX_DB;
 
