@@ -45,7 +45,10 @@ namespace dev {
 
 constexpr int UNIT = 64 * MAP_BPL;     // text bytes per wave unit (2 KiB)
 constexpr int HALO = 64;               // bytes past the unit kept in LDS
-constexpr int BUF = UNIT + HALO + 24;  // + one 24-byte window read past the halo
+// + one 24-byte window read past the halo, rounded to 16 bytes: every wave's
+// buffer starts 16-byte aligned, so the unit commit's ds_write_b128 are aligned
+// (2136-byte buffers put odd waves at 8 mod 16: SQ_LDS_UNALIGNED_STALL 3.0e7 / GiB)
+constexpr int BUF = (UNIT + HALO + 24 + 15) / 16 * 16;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr int GS = HOT_GROUP_SLOTS;    // slots per group
 constexpr int NG = HOT_GROUPS;         // groups
