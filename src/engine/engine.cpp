@@ -692,23 +692,66 @@ void Engine::count_source(ChunkSource& src, uint64_t global_base) {
   bool eof = false;
   uint64_t offset = global_base;
 
+  // A word longer than a whole piece (no delimiter in C bytes): its bytes are
+  // gathered on the host up to the next delimiter and counted as a pass of its
+  // own from a device buffer sized to it (SURVEY §5.7 long-word fallback; the
+  // map keys it with the byte loop, the reducer copies it to the key arena).
+  std::vector<uint8_t> giant;
+  auto count_giant = [&](uint64_t base) {
+    const uint64_t n = giant.size();
+    WC_LOG(LOG_INFO, "dev %d: %llu-byte word at %llu exceeds the %llu-byte stream piece: own pass", im.dev,
+           (unsigned long long)n, (unsigned long long)base, (unsigned long long)C);
+    im.giant_mem.reserve(n + 4096);
+    im.giant_mem.reset();
+    uint8_t* d = static_cast<uint8_t*>(im.giant_mem.take(n + 4096));
+    WC_HIP_CHECK(hipMemcpy(d, giant.data(), n, hipMemcpyHostToDevice));
+    const uint32_t blocks = im.blocks_for(n), rb = im.rec_buckets_log2();
+    im.launch_pass(d, n, n, base, ' ', rb, blocks);
+    im.complete_pass(d, n, n, base, ' ', rb, blocks);
+    im.st.bytes += n;
+    giant.clear();
+  };
+
   // Fill pinned[k % ring] with carry + fresh bytes, cut at the last delimiter.
+  // A piece with no delimiter at all is the start of a giant word: it moves to
+  // `giant` (counted by the caller, before the returned piece) and the piece is
+  // refilled from the bytes after it.
   auto fill = [&](uint64_t k) -> uint64_t {
     uint8_t* pin = im.pinned[k % im.pinned.size()].data();
-    uint64_t total = carry.size();
-    if (total) std::memcpy(pin, carry.data(), total);
-    carry.clear();
-    while (!eof && total < C) {
-      const uint64_t got = src.read(pin + total, C - total);
-      if (got == 0) eof = true;
-      total += got;
+    for (;;) {
+      uint64_t total = carry.size();
+      if (total) std::memcpy(pin, carry.data(), total);
+      carry.clear();
+      while (!eof && total < C) {
+        const uint64_t got = src.read(pin + total, C - total);
+        if (got == 0) eof = true;
+        total += got;
+      }
+      if (total == 0 || eof) return total;
+      uint64_t cut = total;
+      while (cut > 0 && !is_delim(pin[cut - 1])) --cut;
+      if (cut > 0) {
+        carry.assign(pin + cut, pin + total);
+        return cut;
+      }
+      WC_CHECK(giant.empty(), "one giant word per piece");  // a piece after a giant starts with its delimiter
+      giant.assign(pin, pin + total);
+      std::vector<uint8_t> tmp(std::min<uint64_t>(C, 16ull << 20));
+      while (!eof) {
+        const uint64_t got = src.read(tmp.data(), tmp.size());
+        if (got == 0) {
+          eof = true;
+          break;
+        }
+        uint64_t d = 0;
+        while (d < got && !is_delim(tmp[d])) ++d;
+        giant.insert(giant.end(), tmp.data(), tmp.data() + d);
+        if (d < got) {
+          carry.assign(tmp.data() + d, tmp.data() + got);
+          break;
+        }
+      }
     }
-    if (total == 0 || eof) return total;
-    uint64_t cut = total;
-    while (cut > 0 && !is_delim(pin[cut - 1])) --cut;
-    if (cut == 0) fail("a single word is longer than the chunk size (" + std::to_string(C) + " bytes)");
-    carry.assign(pin + cut, pin + total);
-    return cut;
   };
   auto issue = [&](uint64_t k, uint64_t len) {
     WC_HIP_CHECK(hipStreamWaitEvent(im.copy_s, im.ev_done[k & 1], 0));
@@ -719,6 +762,11 @@ void Engine::count_source(ChunkSource& src, uint64_t global_base) {
   WC_HIP_CHECK(hipEventRecord(im.ev_done[0], im.s));
   WC_HIP_CHECK(hipEventRecord(im.ev_done[1], im.s));
   uint64_t len = fill(0);
+  if (!giant.empty()) {  // the stream starts with a giant word
+    const uint64_t n = giant.size();
+    count_giant(offset);
+    offset += n;
+  }
   if (len) issue(0, len);
   for (uint64_t k = 0; len; ++k) {
     const uint8_t* d = im.d_stage[k & 1];
@@ -732,6 +780,11 @@ void Engine::count_source(ChunkSource& src, uint64_t global_base) {
     WC_HIP_CHECK(hipEventRecord(im.ev_done[k & 1], im.s));
     offset += len;
     im.st.bytes += len;
+    if (!giant.empty()) {  // between piece k and piece k + 1 (stream order)
+      const uint64_t n = giant.size();
+      count_giant(offset);
+      offset += n;
+    }
     len = next;
   }
   WC_HIP_CHECK(hipStreamSynchronize(im.copy_s));

@@ -78,6 +78,7 @@ struct Engine::Impl {
   uint8_t* d_text = nullptr;
   uint64_t text_cap = 0;
   DeviceArena stage_mem;
+  DeviceArena giant_mem;  // a word longer than a stream piece, counted as its own pass
   uint64_t stage_cap = 0;
   uint8_t* d_stage[2] = {nullptr, nullptr};
   std::vector<PinnedBuffer> pinned;
