@@ -69,6 +69,8 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
     WC_HIP_CHECK(hipMemset(d_stamps, 0, MAP_STAMP_N * 8));
     WC_HIP_CHECK(hipMalloc(&d_red_stamps, RED_STAMP_N * 8));
     WC_HIP_CHECK(hipMemset(d_red_stamps, 0, RED_STAMP_N * 8));
+    WC_HIP_CHECK(hipMalloc(&d_blk, (size_t)map_blocks * 4 * 8));
+    WC_HIP_CHECK(hipMemset(d_blk, 0, (size_t)map_blocks * 4 * 8));
   }
 
   opt.log2_rec_buckets = std::min<uint32_t>(opt.log2_rec_buckets, MAX_REC_BUCKETS_LOG2);
@@ -149,6 +151,34 @@ Engine::Impl::~Impl() {
     }
     (void)hipFree(d_stamps);
   }
+  if (d_blk) {  // last map pass: block start skew / duration per XCC (100 MHz realtime ticks -> us)
+    std::vector<unsigned long long> h((size_t)map_blocks * 4);
+    if (hipMemcpy(h.data(), d_blk, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess && h[1]) {
+      unsigned long long t0 = ~0ull, t1 = 0;
+      for (uint32_t b = 0; b < map_blocks; ++b) {
+        if (!h[4 * b + 1]) continue;
+        t0 = std::min(t0, h[4 * b]);
+        t1 = std::max(t1, h[4 * b + 1]);
+      }
+      fprintf(stderr, "[wc] map blocks (last pass): span %.1f us\n", (t1 - t0) / 100.0);
+      for (int x = 0; x < 16; ++x) {
+        double n = 0, st = 0, stmax = 0, du = 0, dumax = 0, dumin = 1e30, un = 0;
+        for (uint32_t b = 0; b < map_blocks; ++b) {
+          const unsigned long long* r = &h[4 * (size_t)b];
+          if (!r[1] || (int)r[2] != x) continue;
+          const double s0 = (r[0] - t0) / 100.0, d = (r[1] - r[0]) / 100.0;
+          n += 1, st += s0, stmax = std::max(stmax, s0), du += d, dumax = std::max(dumax, d);
+          dumin = std::min(dumin, d), un += (double)r[3];
+        }
+        if (n)
+          fprintf(stderr,
+                  "[wc]   xcc %d: %3.0f blocks, start mean %.1f max %.1f us, duration mean %.1f min %.1f max %.1f us, "
+                  "unit grabs/block %.0f\n",
+                  x, n, st / n, stmax, du / n, dumin, dumax, un / n);
+      }
+    }
+    (void)hipFree(d_blk);
+  }
   if (d_red_stamps) {
     unsigned long long h[RED_STAMP_N];
     if (hipMemcpy(h, d_red_stamps, sizeof h, hipMemcpyDeviceToHost) == hipSuccess && h[RS_RECORDS]) {
@@ -214,7 +244,7 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   pass_rec.cursor = &d_ctr->records;
   pass_rec.subcap = (uint32_t)std::min<uint64_t>(rec.cap / ((uint64_t)blocks << log2_rb), 0xFFFFull);
   WC_CHECK(pass_rec.subcap > 0, "shuffle record capacity below one record per (map block, bucket)");
-  MapArgs m{text, len, avail, prev, log2_rb, pass_rec, d_ctr->flags, &d_ctr->tokens, k1_mask, d_stamps};
+  MapArgs m{text, len, avail, prev, log2_rb, pass_rec, d_ctr->flags, &d_ctr->tokens, k1_mask, d_stamps, d_blk};
   if (d_stamps) blocks_stamped += blocks;
   launch_map(m, hot, blocks, s);
   if (sync_debug) {  // WC_SYNC_DEBUG: attribute a device fault to a kernel and a chunk

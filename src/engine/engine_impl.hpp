@@ -47,6 +47,7 @@ struct Engine::Impl {
   bool sync_debug = false;  // WC_SYNC_DEBUG: sync + log after every kernel
   uint64_t k1_mask = K1_HASH_MASK;  // Options::k1_hash_bits (collision tests)
   unsigned long long* d_stamps = nullptr;  // WC_MAP_STAMPS: map phase clock sums
+  unsigned long long* d_blk = nullptr;     // WC_MAP_STAMPS: per-block timing of the last map pass
   unsigned long long* d_red_stamps = nullptr;  // WC_MAP_STAMPS: reduce counters (WC_RED_STAMPS builds)
   uint64_t blocks_stamped = 0;             // map blocks launched with stamps (block-duration mean)
 

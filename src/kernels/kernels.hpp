@@ -99,6 +99,7 @@ struct MapArgs {
   unsigned long long* tokens;   // += tokens owned by this chunk
   uint64_t k1_mask;            // LONG-key hash bits kept (K1_HASH_MASK; collision tests truncate)
   unsigned long long* stamps;  // diagnostic build: per-phase s_memtime sums (MAP_STAMP_N), nullptr = off
+  unsigned long long* blk;     // diagnostic: per map block {start, end (s_memrealtime), XCC id, units}, nullable
 };
 // Hot-key sampling workspace (map.hip): a global fingerprint table filled by
 // wc_hot_sample (fp/cnt zeroed before each chunk) and the LDS table image

@@ -434,6 +434,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   PhaseClock<ST> clk;
   clk.start(st_acc);
   const uint64_t t_begin = clk.t;
+  const uint64_t rt_begin = ST ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz, one clock for every XCD
   const uint32_t pbase = lane * MAP_BPL;
   uint32_t ndef = 0;  // deferred LONG entries of the current round (list[0, ndef))
 
@@ -619,6 +620,13 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     if (tid == 0) {  // block duration (load balance across the grid)
       atomicAdd(&a.stamps[MS_BLKSUM], (unsigned long long)(clk.t - t_begin));
       atomicMax(&a.stamps[MS_BLKMAX], (unsigned long long)(clk.t - t_begin));
+      if (a.blk) {  // where the imbalance comes from: start skew, XCC, units taken
+        unsigned long long* r = a.blk + 4 * (size_t)blockIdx.x;
+        r[0] = rt_begin;
+        r[1] = __builtin_amdgcn_s_memrealtime();
+        r[2] = (unsigned long long)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15);  // HW_REG_XCC_ID [3:0]
+        r[3] = L.next_unit;
+      }
     }
   }
   if (WC_MAP_ABLATE && sink == 0x9E3779B97F4A7C15ull) atomicOr(&a.flags[FLAG_COUNT - 1], 0u);  // never true
