@@ -335,8 +335,10 @@ void merge_cols_owner(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense) 
       WC_HIP_CHECK(hipMemsetAsync(vc, 0, vpad * 8, s));
       launch_fill_u64(vf, ~0ull, vpad, s);
       launch_scatter_ids(send_pos, ids_back, im.cols.cnt, im.cols.first, n, vc, vf, s);
+      comm.group_begin();  // both reductions in one RCCL launch (independent buffers)
       comm.reduce_scatter_u64(vc, scnt, vpad / W, RedOp::Sum, s);
       comm.reduce_scatter_u64(vf, sfirst, vpad / W, RedOp::Min, s);
+      comm.group_end();
       comm.group_begin();
       comm.allgather(scnt, dcnt, vpad / W * 8, s);
       comm.allgather(sfirst, dfirst, vpad / W * 8, s);
