@@ -81,6 +81,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   opt.chunk_bytes = std::min<uint64_t>(std::max<uint64_t>(opt.chunk_bytes, MAP_TILE), max_chunk);
   opt.chunk_bytes = opt.chunk_bytes / MAP_TILE * MAP_TILE;
 
+  if (const char* e = std::getenv("WC_RECORDS_PER_BYTE")) opt.records_per_byte = std::atof(e);  // sweeps only
   rec_total = std::max<uint64_t>(opt.min_records, (uint64_t)((double)opt.chunk_bytes * opt.records_per_byte));
   rec_total = std::min<uint64_t>(rec_total, 0xFFFFFFFFull);  // record indices are 32-bit in the reducer
   // record store + per-(block, bucket) counts; partitions follow the table up to the max
