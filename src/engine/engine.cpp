@@ -106,6 +106,8 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   hot.side = hot_mem.take_n<uint64_t>(HOT_TABLE_CAP);
   WC_HIP_CHECK(hipMalloc(&d_ctr, sizeof(DevCounters)));
   WC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_ctr), sizeof(DevCounters), hipHostMallocDefault));
+  h_pass_seq.resize(256);
+  std::memset(h_pass_seq.data(), 0, h_pass_seq.size());
   const size_t maxb = (size_t)1 << opt.max_log2_tab_buckets;
   WC_HIP_CHECK(hipMalloc(&d_bucket_ovf, maxb * sizeof(uint32_t)));
   WC_HIP_CHECK(hipMalloc(&d_bucket_en, maxb));
@@ -270,6 +272,10 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   c.add(h_ctr, d_ctr, sizeof(DevCounters));
   occ_copied = false;
   if (copy_occupancy) add_occupancy(c);
+  if (spin_wait) {  // complete_pass spins on it instead of a stream sync
+    c.seq_dst = reinterpret_cast<uint32_t*>(h_pass_seq.data());
+    c.seq = ++pass_seq;
+  }
   launch_publish(c, s);
 }
 
@@ -363,7 +369,12 @@ void Engine::Impl::split_table() {
 
 bool Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev,
                                  uint32_t log2_rb, uint32_t blocks, bool synced) {
-  if (!synced) WC_HIP_CHECK(hipStreamSynchronize(s));
+  // the pass's publish launch (counters, occupancy) is what this needs: spin on
+  // its sequence word; later work already on the stream keeps running
+  if (!synced) {
+    if (spin_wait) wait_published(reinterpret_cast<const uint32_t*>(h_pass_seq.data()), pass_seq);
+    else WC_HIP_CHECK(hipStreamSynchronize(s));
+  }
   DevCounters c = *h_ctr;
   if (c.flags[FLAG_REGION_OVF]) {
     // Shuffle regions too small for this chunk's record skew: the reduce was

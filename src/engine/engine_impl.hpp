@@ -141,6 +141,8 @@ struct Engine::Impl {
   PinnedBuffer h_spec;     // speculative finalize: key count + arena cursor + publish sequence word
   bool spin_wait = true;   // WC_SPIN_WAIT=0: wait for the finalize with a stream sync instead
   uint32_t spec_seq = 0;
+  PinnedBuffer h_pass_seq;  // sequence word of the last pass's publish launch
+  uint32_t pass_seq = 0;
   void wait_published(const uint32_t* seq, uint32_t want);
   void settle();           // complete a pending pass
   uint32_t blocks_for(uint64_t len) const;
