@@ -322,15 +322,31 @@ __global__ void __launch_bounds__(1024) wc_hot_threshold(HotArgs h) {
   }
 }
 
-// pass 0 places the words counted >= HOT_FIRST_MUL * t (the most frequent:
-// their tokens must never flood one shuffle bucket), pass 1 the rest.
-constexpr uint32_t HOT_FIRST_MUL = 8;
+// Placement in count tiers, most frequent first: pass 0 places the words
+// counted >= HOT_FIRST_MUL * t (their tokens must never flood one shuffle
+// bucket: placed into a nearly empty image), pass 1 those >= HOT_MID_MUL * t,
+// pass 2 the rest — greedy 2-choice placement into 2-slot groups loses words
+// late in its order, so the order follows the counts (HOT_PLACE_PASSES).
+#ifndef WC_HOT_FIRST_MUL
+#define WC_HOT_FIRST_MUL 8
+#endif
+#ifndef WC_HOT_MID_MUL
+#define WC_HOT_MID_MUL 2
+#endif
+#ifndef WC_HOT_PLACE_PASSES
+#define WC_HOT_PLACE_PASSES 3
+#endif
+constexpr uint32_t HOT_FIRST_MUL = WC_HOT_FIRST_MUL, HOT_MID_MUL = WC_HOT_MID_MUL;
+constexpr int HOT_PLACE_PASSES = WC_HOT_PLACE_PASSES;
+static_assert(HOT_PLACE_PASSES == 2 || HOT_PLACE_PASSES == 3, "2 or 3 placement tiers");
 __global__ void __launch_bounds__(1024) wc_hot_place(HotArgs h, int pass) {
   const uint32_t t = h.sel[SEL_BINS], ties = h.sel[SEL_BINS + 1];
   const uint32_t big = min(HOT_FIRST_MUL * t, (uint32_t)SEL_BINS - 1);
+  const uint32_t mid = HOT_PLACE_PASSES == 3 ? min(HOT_MID_MUL * t, big) : big;
   for (uint64_t s = blockIdx.x * 1024ull + threadIdx.x; s < h.cap; s += (uint64_t)gridDim.x * 1024) {
     const uint32_t c = min(h.cnt[s], (uint32_t)SEL_BINS - 1);
-    if (c == 0 || c + 1 < t || (pass == 0) != (c >= big)) continue;
+    const int tier = c >= big ? 0 : (c >= mid ? 1 : 2);
+    if (c == 0 || c + 1 < t || tier != (pass == HOT_PLACE_PASSES - 1 ? 2 : pass)) continue;
     if (c < t && atomicAdd(&h.sel[SEL_BINS + 2], 1u) >= ties) continue;
     const uint64_t sg = h.sig[s], sd = h.side[s];
     uint64_t k0, k1;
@@ -657,8 +673,8 @@ void launch_map(const MapArgs& a, const HotArgs& h, uint32_t map_blocks, hipStre
   hipLaunchKernelGGL(dev::wc_hot_sample, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
   hipLaunchKernelGGL(dev::wc_hot_hist, dim3(HOT_SEL_BLOCKS), dim3(1024), 0, s, h);
   hipLaunchKernelGGL(dev::wc_hot_threshold, dim3(1), dim3(1024), 0, s, h);
-  hipLaunchKernelGGL(dev::wc_hot_place, dim3(HOT_SEL_BLOCKS), dim3(1024), 0, s, h, 0);
-  hipLaunchKernelGGL(dev::wc_hot_place, dim3(HOT_SEL_BLOCKS), dim3(1024), 0, s, h, 1);
+  for (int p = 0; p < dev::HOT_PLACE_PASSES; ++p)
+    hipLaunchKernelGGL(dev::wc_hot_place, dim3(HOT_SEL_BLOCKS), dim3(1024), 0, s, h, p);
   if (a.stamps) hipLaunchKernelGGL(dev::wc_map<true>, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
   else hipLaunchKernelGGL(dev::wc_map<false>, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
 }
