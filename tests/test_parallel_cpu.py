@@ -1,4 +1,4 @@
-"""Multi-process data-parallel word count on CPU (gloo, world_size 2 and 3):
+"""Multi-process data-parallel word count on CPU (gloo, world_size 2, 3 and 8):
 shard ownership + the merge protocol (reduce-scatter / all-gather) must give
 exactly the single-process result."""
 import os
@@ -35,7 +35,7 @@ def _worker(rank, world, port, path, q, ckpt=""):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,ckpt", [(2, False), (3, False), (2, True)])
+@pytest.mark.parametrize("world,ckpt", [(2, False), (3, False), (8, False), (2, True)])
 def test_gloo_data_parallel_matches_single(tmp_path, world, ckpt):
     from cuda_mapreduce_amd.ops import cpu_count, synth_host
 
