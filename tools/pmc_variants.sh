@@ -2,7 +2,7 @@
 # One PMC pass (instruction mix) per engine build: the default libwc.so and every
 # cuda_mapreduce_amd/lib/variants/*.so (tools/variants.sh), wc_map kernels only.
 export TMPDIR=/tmp
-C="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
+C=${PMC:-"SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"}
 for so in cuda_mapreduce_amd/lib/libwc.so cuda_mapreduce_amd/lib/variants/*.so; do
   [ -f "$so" ] || continue
   n=$(basename $so .so)
