@@ -5,20 +5,32 @@ BASELINE.json metric "GB/s text ingested (whole node) + words/sec at 1/2/4/8
 MI355X"; default config "1 GB synthetic ASCII text" per GPU (weak scaling:
 every rank owns a fixed 1 GiB shard of one logical synthetic stream).
 
-One process per GPU.  For N > 1 the driver launches
-  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
-and ranks merge their key tables with RCCL over xGMI through the native
-communicator (default: the MapReduce shuffle — all-to-all of every key to its
-hash owner, owner-side merge, gather to rank 0; `merge_mode=1`: reduce-scatter
-+ all-gather of dense count vectors); torch.distributed (backend "nccl" =
-RCCL) carries the rendezvous, the RCCL unique id and the timing barriers.
+One process per GPU, each loading only the native engine (/opt/rocm's HIP and
+RCCL; torch is never imported, so no second runtime shares the process):
+  * `python bench.py --gpus N` with no WORLD_SIZE in the environment: this
+    process is a launcher that touches no GPU — it checks that N GPUs are
+    visible (KFD topology + *_VISIBLE_DEVICES), starts N fresh rank processes
+    with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*, relays rank 0's JSON line
+    and fails fast (first failing rank -> siblings stopped, its code returned);
+  * under `python -m torch.distributed.run --nproc-per-node N ... bench.py`
+    (WORLD_SIZE set) each rank runs directly.
+Ranks share rank 0's RCCL unique id through a job-private file
+(cuda_mapreduce_amd/parallel/launch.py); from then on the job's own RCCL
+communicator carries everything: the key-table merge over xGMI, the timing
+barriers (RCCL all-reduce + hipDeviceSynchronize on both sides of the timed
+loop) and the max-over-ranks step time.
+
+Cross-GPU merge (`--merge`, default: the config's): `shuffle` = the MapReduce
+shuffle (all-to-all of every key to its hash owner, owner-side merge, gather to
+rank 0); `dense` = owner-numbered dictionary, reduce-scatter of dense count
+vectors + all-gather.
 
 A timed step is the full job on the resident shard: map (tokenize + combine),
 shuffle, reduce into the running table, compaction, cross-GPU merge and the
 first-occurrence ordering of the final table on device.  Text is generated on
-the device once before timing (synthetic data, random-free: a Zipf(1.0)
-vocabulary of 100k words); nothing inside the timed region is cached between
-steps (the table is cleared at the start of every step).
+the device once before timing (synthetic data: a Zipf(1.0) vocabulary of 100k
+words); nothing inside the timed region is cached between steps (the table is
+cleared at the start of every step).
 """
 from __future__ import annotations
 
@@ -28,10 +40,11 @@ import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000,
@@ -42,33 +55,82 @@ def parse():
     ap.add_argument("--vocab", type=int, default=None)
     ap.add_argument("--zipf", type=float, default=None)
     ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--long-frac", type=float, default=None,
+                    help="share of the vocabulary that is 16-64-byte words (LONG-key path under load)")
     ap.add_argument("--chunk-gb", type=float, default=None)
     ap.add_argument("--pool-gb", type=float, default=None, help="host-staged: replay pool per GPU")
     ap.add_argument("--merge", choices=["shuffle", "dense"], default=None,
                     help="cross-GPU merge: shuffle (all-to-all to hash owners) or dense (reduce-scatter + all-gather);"
-                         " default: the config's (dense: SURVEY §5.8 reduce-scatter; shuffle is ~0.06 ms faster at W = 8)")
+                         " default: the config's")
     ap.add_argument("--no-oracle", action="store_true",
                     help="skip the key-for-key check against the generator-walk oracle (sum check only)")
     ap.add_argument("--json-out", default="")
-    return ap.parse_args()
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="launcher test: ranks report their environment and exit without touching a GPU")
+    return ap.parse_args(argv)
 
 
-def main() -> int:
-    a = parse()
+def launch(a) -> int:
+    """Parent of N rank processes; never loads the engine (no GPU initialised here)."""
+    from cuda_mapreduce_amd.parallel import launch as L
+
+    visible = L.visible_gpus()
+    if visible < a.gpus:
+        print(f"bench: {a.gpus} GPUs requested, {visible} visible", file=sys.stderr, flush=True)
+        return 2
+    return L.spawn([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], a.gpus)
+
+
+def dry_rank(rank: int) -> int:
+    keys = ["RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "WC_RDZV_DIR",
+            "WC_COMM_TIMEOUT_S", "HSA_ENABLE_IPC_MODE_LEGACY"]
+    print(json.dumps({"dry_rank": rank, "env": {k: os.environ.get(k) for k in keys},
+                      "torch_loaded": "torch" in sys.modules}), flush=True)
+    fail = os.environ.get("WC_DRY_FAIL_RANK")
+    if fail is not None and int(fail) == rank:
+        return 3
+    if os.environ.get("WC_DRY_HANG_RANK") not in (None, "") and int(os.environ["WC_DRY_HANG_RANK"]) == rank:
+        time.sleep(600)
+    return 0
+
+
+def loaded_runtime() -> dict:
+    """HIP runtime / RCCL / engine objects mapped into this process (one of each expected)."""
+    libs = {"hip": set(), "rccl": set(), "engine": set(), "torch": "torch" in sys.modules}
+    with open("/proc/self/maps") as f:
+        for line in f:
+            path = line.split()[-1] if "/" in line else ""
+            base = os.path.basename(path)
+            if base.startswith("libamdhip64.so"):
+                libs["hip"].add(path)
+            elif base.startswith("librccl.so"):
+                libs["rccl"].add(path)
+            elif base == "libwc.so":
+                libs["engine"].add(path)
+    return {k: sorted(v) if isinstance(v, set) else v for k, v in libs.items()}
+
+
+def run_rank(a) -> int:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.dry_launch:
+        return dry_rank(rank)
     if world != a.gpus and rank == 0:
         print(f"bench: WORLD_SIZE={world} but --gpus {a.gpus}; using WORLD_SIZE", file=sys.stderr)
-
-    import torch
-    import torch.distributed as dist
+    os.environ.setdefault("WC_COMM_TIMEOUT_S", "120")  # read by the native communicator's watchdog
 
     import resource
 
     from cuda_mapreduce_amd.models import CONFIGS
-    from cuda_mapreduce_amd.ops import Comm, Engine, HostPool
+    from cuda_mapreduce_amd.ops import Comm, Engine, HostPool, device_count
+    from cuda_mapreduce_amd.parallel import launch as L
     from cuda_mapreduce_amd.utils import compare_results, synthetic_oracle
+
+    ndev = device_count()
+    if local >= ndev:
+        print(f"bench: rank {rank}: LOCAL_RANK {local} but {ndev} GPU(s) visible", file=sys.stderr, flush=True)
+        return 2
 
     cfg = CONFIGS[a.config]
     gib = 1 << 30
@@ -76,20 +138,12 @@ def main() -> int:
     vocab = a.vocab if a.vocab is not None else cfg.vocab
     zipf = a.zipf if a.zipf is not None else cfg.zipf_s
     seed = a.seed if a.seed is not None else cfg.seed
+    long_frac = a.long_frac if a.long_frac is not None else cfg.long_frac
     chunk = int(a.chunk_gb * gib) if a.chunk_gb is not None else cfg.chunk_bytes
     host_staged = cfg.source == "host-staged"
-
-    torch.cuda.set_device(local)
     # WC_MERGE_ALWAYS=1 runs the RCCL communicator and the merge protocol even at
-    # world size 1 (launcher / unique-id broadcast / native Comm end to end).
+    # world size 1 (rendezvous / native Comm / merge end to end on one GPU).
     use_comm = world > 1 or os.environ.get("WC_MERGE_ALWAYS", "0") not in ("", "0")
-    if use_comm:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
 
     seg = 1024
     nbytes = per_gpu // seg * seg
@@ -99,32 +153,42 @@ def main() -> int:
     eng = Engine(device=local, chunk_bytes=chunk, merge_mode=merge_mode)
     comm = None
     if use_comm:
-        uid = [Comm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = Comm(uid[0], rank, world, local)
+        timeout = float(os.environ["WC_COMM_TIMEOUT_S"])
+        uid = L.rendezvous_uid(rank, Comm.unique_id, timeout_s=timeout)
+        comm = Comm(uid, rank, world, local)
+        comm.barrier()  # every rank holds its communicator: the id file may go
+        if rank == 0:
+            L.rendezvous_cleanup()
+
+    def barrier():
+        eng.sync()
+        if comm is not None:
+            comm.barrier()
 
     # rank r owns segments [r*nseg, (r+1)*nseg) of the logical stream
     first_seg = rank * (nbytes // seg)
     base = rank * nbytes
     pool_bytes = 0
     pool_info = None
+    synth = dict(seed=seed, vocab=vocab, zipf_s=zipf, long_frac=long_frac)
     if host_staged:
         # page-locked host pool of whole chunks replayed over PCIe (1 TB config: 128 GiB per GPU),
         # generated natively in place on 16 threads (no pageable copy)
         pool_bytes = int((a.pool_gb if a.pool_gb is not None else cfg.pool_bytes / gib) * gib)
-        pool_bytes = max(chunk, pool_bytes // chunk * chunk)
+        pool_bytes = max(chunk, min(pool_bytes, nbytes) // chunk * chunk)
+
         def rss_now():
             with open("/proc/self/statm") as f:
                 return int(f.read().split()[1]) * os.sysconf("SC_PAGE_SIZE")
 
-        rss_before = rss_now()  # interpreter + torch + HIP runtime, before the pool exists
-        pool = HostPool(pool_bytes, first_segment=first_seg, seed=seed, vocab=vocab, zipf_s=zipf, threads=16)
+        rss_before = rss_now()  # interpreter + HIP runtime, before the pool exists
+        pool = HostPool(pool_bytes, first_segment=first_seg, threads=16, **synth)
         peak = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024
         pool_info = {"pool_bytes": pool_bytes, "build_s": round(pool.build_seconds, 3),
                      "rss_before_pool_bytes": rss_before, "peak_rss_bytes": peak,
                      "pool_rss_ratio": round((peak - rss_before) / pool_bytes, 4)}
     else:
-        eng.synth_device(nbytes, first_segment=first_seg, seed=seed, vocab=vocab, zipf_s=zipf)
+        eng.synth_device(nbytes, first_segment=first_seg, **synth)
 
     def step():
         eng.reset()
@@ -137,24 +201,18 @@ def main() -> int:
     for _ in range(a.warmup):
         step()
     barrier()
-    torch.cuda.synchronize()
     t0 = time.perf_counter()
     keys = 0
     for _ in range(a.steps):
         keys = step()
     barrier()
-    torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     st = eng.stats()
     ms = dt / max(a.steps, 1) * 1e3
     tokens = st["tokens"]
-    if world > 1:
-        t = torch.tensor([ms, float(tokens)], dtype=torch.float64, device="cuda")
-        mx = t.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = t.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        ms, tokens_total = float(mx[0]), float(sm[1])
+    if comm is not None:
+        ms = comm.allreduce_f64([ms], "max")[0]
+        tokens_total = comm.allreduce_f64([float(tokens)], "sum")[0]
     else:
         tokens_total = float(tokens)
     # Validation (untimed): the merged table must equal, key for key (words,
@@ -172,17 +230,23 @@ def main() -> int:
                   f"!= tokens {int(tokens_total)}", file=sys.stderr, flush=True)
         if not a.no_oracle:
             t1 = time.perf_counter()
-            want = synthetic_oracle(world, nbytes, seed, vocab, zipf, pool_bytes=pool_bytes, chunk=chunk)
+            want = synthetic_oracle(world, nbytes, seed, vocab, zipf, pool_bytes=pool_bytes, chunk=chunk,
+                                    long_frac=long_frac)
             diff = compare_results(res, want)
             check = {"oracle": "generator word walk (cpu_count_synth)", "identical": not diff,
                      "seconds": round(time.perf_counter() - t1, 2)}
             if diff:
                 valid = False
                 print(f"bench: VALIDATION FAILED vs oracle: {diff}", file=sys.stderr, flush=True)
+    if comm is not None:  # every rank exits with rank 0's verdict
+        valid = comm.allreduce_f64([0.0 if valid else 1.0], "max")[0] == 0.0
     total_bytes = nbytes * world
     gbps = total_bytes / (ms / 1e3) / 1e9
     words = tokens_total / (ms / 1e3)
     if rank == 0:
+        data = (f"synthetic ({'host pool replayed over PCIe' if host_staged else 'device-generated'} "
+                f"Zipf({zipf}) text, {vocab}-word vocabulary, seed {seed}"
+                + (f", {long_frac:g} of the vocabulary 16-64-byte words" if long_frac else "") + ")")
         out = {
             "metric": "GB/s text ingested (whole node)",
             "value": round(gbps, 3),
@@ -195,8 +259,7 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8 text / u64 counts",
-            "data": (f"synthetic ({'host pool replayed over PCIe' if host_staged else 'device-generated'} "
-                     f"Zipf({zipf}) text, {vocab}-word vocabulary, seed {seed})"),
+            "data": data,
             "words_per_s": round(words, 1),
             "validated": valid,
             "validation": check or {"oracle": "skipped (--no-oracle): token-sum check only"},
@@ -210,6 +273,8 @@ def main() -> int:
                 "chunk_bytes": chunk,
                 "merge": merge,
             },
+            "control_plane": "native RCCL communicator (file rendezvous), no torch" if comm else "single process",
+            "runtime": loaded_runtime(),
             "stages": st,
         }
         if pool_info:
@@ -222,9 +287,14 @@ def main() -> int:
     if comm is not None:
         comm.close()
     eng.close()
-    if use_comm:
-        dist.destroy_process_group()
     return 0 if valid else 1
+
+
+def main() -> int:
+    a = parse()
+    if "WORLD_SIZE" not in os.environ and (a.gpus > 1 or a.dry_launch):
+        return launch(a)
+    return run_rank(a)
 
 
 if __name__ == "__main__":

@@ -28,6 +28,7 @@ class JobConfig:
     vocab: int = 100000
     zipf_s: float = 1.0
     seed: int = 1
+    long_frac: float = 0.0  # share of the vocabulary drawn as 16..64-byte words (LONG-key path)
     path: Optional[str] = None
     merge: str = "shuffle"  # cross-GPU merge: shuffle (all-to-all to hash owners) | dense (reduce-scatter + all-gather)
 
@@ -88,12 +89,14 @@ def run_job(cfg: JobConfig, rank: int = 0, world: int = 1, local_rank: int = 0, 
     try:
         eng.reset()
         if cfg.source == "device":
-            eng.synth_device(nbytes, first_segment=first_seg, seed=cfg.seed, vocab=cfg.vocab, zipf_s=cfg.zipf_s)
+            eng.synth_device(nbytes, first_segment=first_seg, seed=cfg.seed, vocab=cfg.vocab, zipf_s=cfg.zipf_s,
+                             long_frac=cfg.long_frac)
             t0 = time.perf_counter()
             eng.count_resident(nbytes, global_base=base)
         elif cfg.source == "host-staged":
             pool_bytes = max(cfg.chunk_bytes, min(cfg.pool_bytes, nbytes) // cfg.chunk_bytes * cfg.chunk_bytes)
-            pool = HostPool(pool_bytes, first_segment=first_seg, seed=cfg.seed, vocab=cfg.vocab, zipf_s=cfg.zipf_s)
+            pool = HostPool(pool_bytes, first_segment=first_seg, seed=cfg.seed, vocab=cfg.vocab, zipf_s=cfg.zipf_s,
+                            long_frac=cfg.long_frac)
             t0 = time.perf_counter()
             eng.count_pool(pool, nbytes, global_base=base)
         else:

@@ -63,7 +63,7 @@ def _load() -> ctypes.CDLL:
         "wc_result_merge": (c_int, [c_void_p, c_void_p]),
         "wc_count_replay": (c_int, [c_void_p, P8, c_uint64, c_uint64, c_uint64]),
         "wc_count_pinned_replay": (c_int, [c_void_p, P8, c_uint64, c_uint64, c_uint64]),
-        "wc_synth_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint32, c_double]),
+        "wc_synth_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint32, c_double, c_double]),
         "wc_count_resident": (c_int, [c_void_p, c_uint64, c_uint64]),
         "wc_finalize_device": (c_int, [c_void_p, c_void_p, P64]),
         "wc_engine_result": (c_void_p, [c_void_p, c_void_p, c_int]),
@@ -79,9 +79,9 @@ def _load() -> ctypes.CDLL:
         "wc_cpu_count": (c_void_p, [P8, c_uint64, c_uint64]),
         "wc_cpu_count_compat": (c_void_p, [P8, c_uint64]),
         "wc_synth_host": (c_int, [P8, c_uint64, c_uint64, c_uint64, c_uint32, c_double]),
-        "wc_synth_host_mt": (c_int, [P8, c_uint64, c_uint64, c_uint64, c_uint32, c_double, c_int]),
-        "wc_cpu_count_synth": (c_void_p, [c_uint64, c_uint64, c_uint64, c_uint32, c_double, c_uint64, c_int]),
-        "wc_pool_create": (c_void_p, [c_uint64, c_uint64, c_uint64, c_uint32, c_double, c_int]),
+        "wc_synth_host_mt": (c_int, [P8, c_uint64, c_uint64, c_uint64, c_uint32, c_double, c_double, c_int]),
+        "wc_cpu_count_synth": (c_void_p, [c_uint64, c_uint64, c_uint64, c_uint32, c_double, c_double, c_uint64, c_int]),
+        "wc_pool_create": (c_void_p, [c_uint64, c_uint64, c_uint64, c_uint32, c_double, c_double, c_int]),
         "wc_pool_destroy": (None, [c_void_p]),
         "wc_pool_build_seconds": (c_double, [c_void_p]),
         "wc_count_pool": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64]),
@@ -90,6 +90,8 @@ def _load() -> ctypes.CDLL:
         "wc_rccl_unique_id": (c_int, [POINTER(c_char)]),
         "wc_comm_rccl_create": (c_void_p, [POINTER(c_char), c_int, c_int, c_int]),
         "wc_comm_destroy": (None, [c_void_p]),
+        "wc_comm_barrier": (c_int, [c_void_p]),
+        "wc_comm_allgather_host": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
         "wc_loopback_count": (c_void_p, [P8, c_uint64, c_int, POINTER(c_int), POINTER(Options), c_int]),
     }
     for name, (res, args) in sig.items():

@@ -106,6 +106,26 @@ class Comm:
         check(lib.wc_rccl_unique_id(buf))
         return buf.raw
 
+    def barrier(self) -> None:
+        """Every rank reaches this point (an RCCL all-reduce waited for under the watchdog)."""
+        check(lib.wc_comm_barrier(self._p))
+
+    def allgather_host(self, data: bytes) -> List[bytes]:
+        """Rank r's ``data`` (same length on every rank) for every r, over the communicator."""
+        n = len(data)
+        send = ctypes.create_string_buffer(data, max(n, 1))
+        recv = ctypes.create_string_buffer(max(n * self.size, 1))
+        check(lib.wc_comm_allgather_host(self._p, send, n, recv))
+        raw = recv.raw
+        return [raw[r * n:(r + 1) * n] for r in range(self.size)]
+
+    def allreduce_f64(self, values: Sequence[float], op: str = "max") -> List[float]:
+        """Element-wise max / sum over ranks of a few host doubles (all-gather + fold)."""
+        a = np.asarray(values, dtype=np.float64)
+        parts = [np.frombuffer(b, dtype=np.float64) for b in self.allgather_host(a.tobytes())]
+        m = np.stack(parts)
+        return list((m.max(axis=0) if op == "max" else m.sum(axis=0)).tolist())
+
     def close(self) -> None:
         if getattr(self, "_p", None):
             lib.wc_comm_destroy(self._p)
@@ -176,9 +196,10 @@ class Engine:
         """Host-staged path from a native page-locked pool (HostPool): no registration, no copies."""
         check(lib.wc_count_pool(self._p, pool._p, total, global_base))
 
-    def synth_device(self, nbytes: int, first_segment: int = 0, seed: int = 1, vocab: int = 100000, zipf_s: float = 1.0) -> None:
+    def synth_device(self, nbytes: int, first_segment: int = 0, seed: int = 1, vocab: int = 100000, zipf_s: float = 1.0,
+                     long_frac: float = 0.0) -> None:
         """Generate synthetic text directly in HBM (no host/PCIe involvement)."""
-        check(lib.wc_synth_device(self._p, nbytes, first_segment, seed, vocab, zipf_s))
+        check(lib.wc_synth_device(self._p, nbytes, first_segment, seed, vocab, zipf_s, long_frac))
         self._resident = nbytes
 
     def count_resident(self, nbytes: Optional[int] = None, global_base: int = 0) -> None:
@@ -191,6 +212,10 @@ class Engine:
 
     def result(self, comm: Optional[Comm] = None, all_ranks: bool = False) -> Result:
         return Result._from_native(check_ptr(lib.wc_engine_result(self._p, comm._p if comm else None, int(all_ranks))))
+
+    def sync(self) -> None:
+        """hipDeviceSynchronize on the engine's device (the bench's timing brackets)."""
+        check(lib.wc_engine_sync(self._p))
 
     def stats(self) -> dict:
         buf = ctypes.create_string_buffer(2048)
@@ -227,33 +252,34 @@ def cpu_count_compat(data: bytes) -> Result:
 
 
 def synth_host(nbytes: int, first_segment: int = 0, seed: int = 1, vocab: int = 100000, zipf_s: float = 1.0,
-               threads: int = 1) -> bytes:
+               threads: int = 1, long_frac: float = 0.0) -> bytes:
     """Host copy of the synthetic stream (bit-identical to the device generator)."""
-    return synth_host_array(nbytes, first_segment, seed, vocab, zipf_s, threads).tobytes()
+    return synth_host_array(nbytes, first_segment, seed, vocab, zipf_s, threads, long_frac).tobytes()
 
 
 def synth_host_array(nbytes: int, first_segment: int = 0, seed: int = 1, vocab: int = 100000, zipf_s: float = 1.0,
-                     threads: int = 8) -> np.ndarray:
+                     threads: int = 8, long_frac: float = 0.0) -> np.ndarray:
     """The synthetic stream generated in place into a numpy array on `threads` threads."""
     out = np.empty(nbytes, np.uint8)
-    check(lib.wc_synth_host_mt(out.ctypes.data_as(_P8), nbytes, first_segment, seed, vocab, zipf_s, threads))
+    check(lib.wc_synth_host_mt(out.ctypes.data_as(_P8), nbytes, first_segment, seed, vocab, zipf_s, long_frac,
+                               threads))
     return out
 
 
 def cpu_count_synth(nbytes: int, first_segment: int = 0, seed: int = 1, vocab: int = 100000, zipf_s: float = 1.0,
-                    global_base: int = 0, threads: int = 0) -> Result:
+                    global_base: int = 0, threads: int = 0, long_frac: float = 0.0) -> Result:
     """Exact counts of the synthetic stream from the generator's own word walk (full-scale
     benchmark oracle): independent of every tokenizer."""
     return Result._from_native(check_ptr(lib.wc_cpu_count_synth(nbytes, first_segment, seed, vocab, zipf_s,
-                                                                 global_base, threads)))
+                                                                 long_frac, global_base, threads)))
 
 
 class HostPool:
     """Page-locked synthetic replay pool (host-staged configs), generated in place natively."""
 
     def __init__(self, nbytes: int, first_segment: int = 0, seed: int = 1, vocab: int = 100000,
-                 zipf_s: float = 1.0, threads: int = 16):
-        self._p = check_ptr(lib.wc_pool_create(nbytes, first_segment, seed, vocab, zipf_s, threads))
+                 zipf_s: float = 1.0, threads: int = 16, long_frac: float = 0.0):
+        self._p = check_ptr(lib.wc_pool_create(nbytes, first_segment, seed, vocab, zipf_s, long_frac, threads))
         self.nbytes = nbytes
         self.build_seconds = float(lib.wc_pool_build_seconds(self._p))
 

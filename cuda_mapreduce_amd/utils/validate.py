@@ -51,24 +51,25 @@ def merge_results(parts) -> Result:
 
 
 def synthetic_oracle(world: int, nbytes: int, seed: int, vocab: int, zipf: float, pool_bytes: int = 0,
-                     chunk: int = 0, threads: int = 16) -> Result:
+                     chunk: int = 0, threads: int = 16, long_frac: float = 0.0) -> Result:
     """Expected table of a benchmark run: rank r owns segments [r*nseg, (r+1)*nseg) of one
     logical stream (global offset r*nbytes).  Device-resident configs count that stream;
     host-staged configs (pool_bytes > 0) replay rank r's first pool_bytes in chunks of
     `chunk` up to nbytes (chunk k from pool offset k*chunk mod pool_bytes)."""
     nseg = nbytes // SEG
     if not pool_bytes:
-        return cpu_count_synth(world * nbytes, 0, seed, vocab, zipf, 0, threads)
+        return cpu_count_synth(world * nbytes, 0, seed, vocab, zipf, 0, threads, long_frac)
     parts = []
     reps, rem = divmod(nbytes, pool_bytes)
     assert chunk and pool_bytes % chunk == 0 and rem % SEG == 0
     for r in range(world):
         base = r * nbytes
-        full = cpu_count_synth(pool_bytes, r * nseg, seed, vocab, zipf, base, threads)
+        full = cpu_count_synth(pool_bytes, r * nseg, seed, vocab, zipf, base, threads, long_frac)
         if reps:
             full.counts = full.counts * np.uint64(reps)
             full.total *= reps
             parts.append(full)
         if rem:  # a last partial pass over the pool's head
-            parts.append(cpu_count_synth(rem, r * nseg, seed, vocab, zipf, base + reps * pool_bytes, threads))
+            parts.append(cpu_count_synth(rem, r * nseg, seed, vocab, zipf, base + reps * pool_bytes, threads,
+                                         long_frac))
     return merge_results(parts) if len(parts) > 1 else parts[0]

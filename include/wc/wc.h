@@ -55,12 +55,15 @@ int wc_count_replay(wc_engine* e, const uint8_t* pool, uint64_t pool_bytes, uint
 int wc_count_pinned_replay(wc_engine* e, const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t global_base);
 /* Page-locked synthetic replay pool generated in place on `threads` threads (host-staged config). */
 typedef struct wc_pool wc_pool;
-wc_pool* wc_pool_create(uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double zipf_s, int threads);
+wc_pool* wc_pool_create(uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double zipf_s,
+                        double long_frac, int threads);
 void wc_pool_destroy(wc_pool* p);
 double wc_pool_build_seconds(const wc_pool* p);
 int wc_count_pool(wc_engine* e, const wc_pool* p, uint64_t total, uint64_t global_base);
-/* Generate synthetic text into the engine's device text buffer ... */
-int wc_synth_device(wc_engine* e, uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double zipf_s);
+/* Generate synthetic text into the engine's device text buffer (long_frac: share of the
+ * vocabulary drawn as 16..64-byte words) ... */
+int wc_synth_device(wc_engine* e, uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double zipf_s,
+                    double long_frac);
 /* ... and count [0, n) of it. */
 int wc_count_resident(wc_engine* e, uint64_t n, uint64_t global_base);
 int wc_finalize_device(wc_engine* e, wc_comm* comm, uint64_t* n_keys);
@@ -86,11 +89,11 @@ wc_result* wc_cpu_count_compat(const uint8_t* text, uint64_t n);
 /* Exact counts of n bytes of the synthetic stream from segment first_segment (offsets from
    global_base), computed from the generator's word walk on `threads` CPU threads (0 = all). */
 wc_result* wc_cpu_count_synth(uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double zipf_s,
-                              uint64_t global_base, int threads);
+                              double long_frac, uint64_t global_base, int threads);
 int wc_synth_host(uint8_t* out, uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double zipf_s);
 /* The same on `threads` threads, written in place. */
 int wc_synth_host_mt(uint8_t* out, uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double zipf_s,
-                     int threads);
+                     double long_frac, int threads);
 int wc_shard_range_mem(const uint8_t* text, uint64_t n, int rank, int world, uint64_t* begin, uint64_t* end);
 int wc_shard_range_file(const char* path, int rank, int world, uint64_t* begin, uint64_t* end);
 
@@ -98,6 +101,10 @@ int wc_shard_range_file(const char* path, int rank, int world, uint64_t* begin, 
 int wc_rccl_unique_id(char out[128]);
 wc_comm* wc_comm_rccl_create(const char* unique_id, int rank, int size, int device);
 void wc_comm_destroy(wc_comm* c);
+/* Control plane over the communicator itself (no second runtime in the process):
+ * a barrier, and recv[r * bytes ...] = rank r's `bytes` host bytes. */
+int wc_comm_barrier(wc_comm* c);
+int wc_comm_allgather_host(wc_comm* c, const void* send, uint64_t bytes, void* recv);
 /* N virtual ranks on `devices` (one thread each) count shards of `text` and
  * merge through the loopback communicator; returns rank 0's result.  With
  * all_ranks every rank receives the merged table and must match rank 0's. */

@@ -31,7 +31,16 @@ struct Stats {
   uint32_t map_reruns = 0;     // shuffle-region overflow -> chunk halved
   uint32_t table_splits = 0;   // running table grew B -> 2B
   uint32_t log2_buckets = 0;   // final table buckets
-  double h2d_ms = 0, map_reduce_ms = 0, finalize_ms = 0, merge_ms = 0;
+  // Host wall clock of the last job's API calls (count_*, finalize / result).
+  double host_count_ms = 0, host_finalize_ms = 0;
+  // Device time of the last job's stages, from events on the engine stream
+  // (WC_STAGE_EVENTS=0 turns them off): map = zeroing + hot-word sampling +
+  // wc_map of every pass; reduce = wc_reduce_buckets + counter publish;
+  // finalize = compaction, first-occurrence sort, gather; merge = the
+  // cross-GPU protocol (kernels + RCCL); idle = stream gaps between them (host
+  // turn-arounds, H2D waits).  device_ms = their sum: first pass start to
+  // finalize end.
+  double map_ms = 0, reduce_ms = 0, finalize_ms = 0, merge_ms = 0, idle_ms = 0, device_ms = 0;
 };
 
 struct Options {
@@ -64,6 +73,9 @@ struct SynthSpec {
   uint64_t seed = 1;
   uint32_t vocab = 100000;
   double zipf_s = 1.0;
+  // Share of the vocabulary drawn as LONG words of 16..64 bytes (hashed keys,
+  // byte-compared downstream); 0 = the English-like length profile only.
+  double long_frac = 0.0;
 };
 
 // Supplies host text chunks for the streaming (host-staged) path.

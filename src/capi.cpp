@@ -24,6 +24,22 @@ struct wc_result {
 };
 struct wc_comm {
   std::unique_ptr<wc::Comm> c;
+  int device = 0;
+  hipStream_t s = nullptr;   // control-plane collectives (barrier, host all-gather)
+  void* scratch = nullptr;   // device staging of wc_comm_allgather_host
+  size_t scratch_bytes = 0;
+  ~wc_comm() {
+    (void)hipSetDevice(device);
+    if (scratch) (void)hipFree(scratch);
+    if (s) (void)hipStreamDestroy(s);
+  }
+  hipStream_t stream() {
+    if (!s) {
+      WC_HIP_CHECK(hipSetDevice(device));
+      WC_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    }
+    return s;
+  }
 };
 
 namespace {
@@ -58,11 +74,12 @@ wc::Options to_opts(const wc_options* o) {
   return x;
 }
 
-wc::SynthSpec spec_of(uint64_t seed, uint32_t vocab, double s) {
+wc::SynthSpec spec_of(uint64_t seed, uint32_t vocab, double s, double long_frac) {
   wc::SynthSpec sp;
   sp.seed = seed;
   sp.vocab = vocab;
   sp.zipf_s = s;
+  sp.long_frac = long_frac;
   return sp;
 }
 }  // namespace
@@ -216,9 +233,10 @@ int wc_count_pinned_replay(wc_engine* e, const uint8_t* pool, uint64_t pool_byte
   return guard([&] { e->e->count_pinned_replay(pool, pool_bytes, total, base); });
 }
 
-int wc_synth_device(wc_engine* e, uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double s) {
+int wc_synth_device(wc_engine* e, uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double s,
+                    double long_frac) {
   return guard([&] {
-    e->d_text = e->e->synth_device(n, first_segment, spec_of(seed, vocab, s));
+    e->d_text = e->e->synth_device(n, first_segment, spec_of(seed, vocab, s, long_frac));
     e->resident = n;
   });
 }
@@ -248,12 +266,14 @@ int wc_engine_stats_json(wc_engine* e, char* buf, int cap) {
   char tmp[1024];
   const int k = snprintf(tmp, sizeof tmp,
                          "{\"bytes\": %llu, \"tokens\": %llu, \"keys\": %llu, \"records\": %llu, \"chunks\": %u, "
-                         "\"map_reruns\": %u, "
-                         "\"table_splits\": %u, \"log2_buckets\": %u, \"map_reduce_ms\": %.3f, \"finalize_ms\": %.3f, "
-                         "\"merge_ms\": %.3f}",
+                         "\"map_reruns\": %u, \"table_splits\": %u, \"log2_buckets\": %u, "
+                         "\"device_ms\": {\"map\": %.4f, \"reduce\": %.4f, \"finalize\": %.4f, \"merge\": %.4f, "
+                         "\"idle\": %.4f, \"total\": %.4f}, "
+                         "\"host_ms\": {\"count\": %.4f, \"finalize\": %.4f}}",
                          (unsigned long long)s.bytes, (unsigned long long)s.tokens, (unsigned long long)s.keys,
-                         (unsigned long long)s.records, s.chunks, s.map_reruns, s.table_splits, s.log2_buckets, s.map_reduce_ms, s.finalize_ms,
-                         s.merge_ms);
+                         (unsigned long long)s.records, s.chunks, s.map_reruns, s.table_splits, s.log2_buckets, s.map_ms,
+                         s.reduce_ms, s.finalize_ms, s.merge_ms, s.idle_ms, s.device_ms, s.host_count_ms,
+                         s.host_finalize_ms);
   if (buf && cap > 0) {
     std::strncpy(buf, tmp, (size_t)cap - 1);
     buf[cap - 1] = 0;
@@ -261,7 +281,12 @@ int wc_engine_stats_json(wc_engine* e, char* buf, int cap) {
   return k;
 }
 
-int wc_engine_sync(wc_engine* e) { return guard([&] { WC_HIP_CHECK(hipDeviceSynchronize()); (void)e; }); }
+int wc_engine_sync(wc_engine* e) {
+  return guard([&] {
+    WC_HIP_CHECK(hipSetDevice(e->e->options().device));
+    WC_HIP_CHECK(hipDeviceSynchronize());
+  });
+}
 
 uint64_t wc_result_size(const wc_result* r) { return r->t.size(); }
 uint64_t wc_result_total(const wc_result* r) { return r->t.total; }
@@ -319,9 +344,10 @@ wc_result* wc_cpu_count_compat(const uint8_t* text, uint64_t n) {
 }
 
 wc_result* wc_cpu_count_synth(uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double zs,
-                              uint64_t base, int threads) {
+                              double long_frac, uint64_t base, int threads) {
   wc_result* r = new wc_result;
-  if (guard([&] { r->t = wc::cpu::count_synth(n, first_segment, spec_of(seed, vocab, zs), base, threads); }) != 0) {
+  if (guard([&] { r->t = wc::cpu::count_synth(n, first_segment, spec_of(seed, vocab, zs, long_frac), base, threads); }) !=
+      0) {
     delete r;
     return nullptr;
   }
@@ -329,13 +355,13 @@ wc_result* wc_cpu_count_synth(uint64_t n, uint64_t first_segment, uint64_t seed,
 }
 
 int wc_synth_host(uint8_t* out, uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double s) {
-  return wc_synth_host_mt(out, n, first_segment, seed, vocab, s, 1);
+  return wc_synth_host_mt(out, n, first_segment, seed, vocab, s, 0.0, 1);
 }
 
 int wc_synth_host_mt(uint8_t* out, uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double s,
-                     int threads) {
+                     double long_frac, int threads) {
   return guard([&] {
-    const wc::SynthSpec sp = spec_of(seed, vocab, s);
+    const wc::SynthSpec sp = spec_of(seed, vocab, s, long_frac);
     wc::synth_host_into(out, n, first_segment, sp, wc::build_vocab(sp), threads);
   });
 }
@@ -344,9 +370,10 @@ struct wc_pool {
   std::unique_ptr<wc::HostPool> p;
 };
 
-wc_pool* wc_pool_create(uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double s, int threads) {
+wc_pool* wc_pool_create(uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double s, double long_frac,
+                        int threads) {
   wc_pool* r = new wc_pool;
-  if (guard([&] { r->p.reset(new wc::HostPool(n, first_segment, spec_of(seed, vocab, s), threads)); }) != 0) {
+  if (guard([&] { r->p.reset(new wc::HostPool(n, first_segment, spec_of(seed, vocab, s, long_frac), threads)); }) != 0) {
     delete r;
     return nullptr;
   }
@@ -383,11 +410,42 @@ int wc_rccl_unique_id(char out[128]) {
 
 wc_comm* wc_comm_rccl_create(const char* unique_id, int rank, int size, int device) {
   wc_comm* c = new wc_comm;
+  c->device = device;
   if (guard([&] { c->c = wc::make_rccl_comm(std::string(unique_id, wc::RCCL_ID_BYTES), rank, size, device); }) != 0) {
     delete c;
     return nullptr;
   }
   return c;
+}
+
+// Control plane of one-process-per-GPU jobs without a second runtime (bench.py):
+// a barrier and a small all-gather of host bytes over the job's own RCCL
+// communicator, both waited for under its watchdog (WC_COMM_TIMEOUT_S).
+int wc_comm_barrier(wc_comm* c) {
+  return guard([&] {
+    WC_HIP_CHECK(hipSetDevice(c->device));
+    c->c->barrier(c->stream());
+  });
+}
+
+int wc_comm_allgather_host(wc_comm* c, const void* send, uint64_t bytes, void* recv) {
+  return guard([&] {
+    WC_HIP_CHECK(hipSetDevice(c->device));
+    hipStream_t s = c->stream();
+    const size_t W = (size_t)c->c->size(), need = bytes * (W + 1);
+    if (need > c->scratch_bytes) {
+      if (c->scratch) WC_HIP_CHECK(hipFree(c->scratch));
+      c->scratch = nullptr;
+      WC_HIP_CHECK(hipMalloc(&c->scratch, need));
+      c->scratch_bytes = need;
+    }
+    uint8_t* d_send = static_cast<uint8_t*>(c->scratch);
+    uint8_t* d_recv = d_send + bytes;
+    WC_HIP_CHECK(hipMemcpyAsync(d_send, send, bytes, hipMemcpyHostToDevice, s));
+    c->c->allgather(d_send, d_recv, bytes, s);
+    WC_HIP_CHECK(hipMemcpyAsync(recv, d_recv, bytes * W, hipMemcpyDeviceToHost, s));
+    c->c->sync(s);
+  });
 }
 
 void wc_comm_destroy(wc_comm* c) { delete c; }

@@ -63,6 +63,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   if (const char* e = std::getenv("WC_SYNC_DEBUG")) sync_debug = std::atoi(e) != 0;
   if (const char* e = std::getenv("WC_NO_SPECULATE")) speculate = std::atoi(e) == 0;
   if (const char* e = std::getenv("WC_SPIN_WAIT")) spin_wait = std::atoi(e) != 0;
+  if (const char* e = std::getenv("WC_STAGE_EVENTS")) stage_events = std::atoi(e) != 0;
   k1_mask = k1_hash_mask(opt.k1_hash_bits);
   if (const char* e = std::getenv("WC_MAP_STAMPS"); e && std::atoi(e)) {
     WC_HIP_CHECK(hipMalloc(&d_stamps, MAP_STAMP_N * 8));
@@ -134,6 +135,7 @@ Engine::Impl::~Impl() {
     if (ev_h2d[i]) (void)hipEventDestroy(ev_h2d[i]);
     if (ev_done[i]) (void)hipEventDestroy(ev_done[i]);
   }
+  for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
   if (d_ctr) (void)hipFree(d_ctr);
   if (h_ctr) (void)hipHostFree(h_ctr);
   if (d_bucket_ovf) (void)hipFree(d_bucket_ovf);
@@ -232,6 +234,7 @@ uint32_t Engine::Impl::blocks_for(uint64_t len) const {
 void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev,
                                uint32_t log2_rb, uint32_t blocks, bool copy_occupancy) {
   WC_CHECK((reinterpret_cast<uintptr_t>(text) & 15) == 0, "chunk text must be 16-byte aligned");
+  mark(EV_PASS);
   // one zeroing launch: pass counters, sampling state and, after a reset, the
   // table occupancy and the key-arena cursor
   ZeroList z{};
@@ -250,6 +253,7 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   MapArgs m{text, len, avail, prev, log2_rb, pass_rec, d_ctr->flags, &d_ctr->tokens, k1_mask, d_stamps, d_blk};
   if (d_stamps) blocks_stamped += blocks;
   launch_map(m, hot, blocks, s);
+  mark(EV_MAP);
   if (sync_debug) {  // WC_SYNC_DEBUG: attribute a device fault to a kernel and a chunk
     const hipError_t e = hipStreamSynchronize(s);
     fprintf(stderr, "[wc] map    base=%llu len=%llu avail=%llu blocks=%u subcap=%u -> %s\n", (unsigned long long)base,
@@ -277,6 +281,40 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
     c.seq = ++pass_seq;
   }
   launch_publish(c, s);
+  mark(EV_REDUCE);
+}
+
+void Engine::Impl::mark(int tag) {
+  if (!stage_events || ev_n >= 8192) return;  // a 1 TB job: ~400 marks
+  if (ev_n == ev_pool.size()) {
+    hipEvent_t e;
+    WC_HIP_CHECK(hipEventCreate(&e));
+    ev_pool.push_back(e);
+    ev_tag.push_back(0);
+  }
+  WC_HIP_CHECK(hipEventRecord(ev_pool[ev_n], s));
+  ev_tag[ev_n++] = tag;
+}
+
+// Called once the job's work has completed (stats()): elapsed time between
+// consecutive marks, charged to the stage the later mark closes.
+void Engine::Impl::collect_stage_times() {
+  if (ev_n < 2) return;
+  double t[EV_FIN_END + 1] = {};
+  for (size_t i = 1; i < ev_n; ++i) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, ev_pool[i - 1], ev_pool[i]) != hipSuccess) {
+      (void)hipGetLastError();
+      return;  // not complete (a pass still pending): keep the previous values
+    }
+    t[ev_tag[i]] += ms;
+  }
+  st.map_ms = t[EV_MAP];
+  st.reduce_ms = t[EV_REDUCE];
+  st.merge_ms = t[EV_MERGE1];
+  st.finalize_ms = t[EV_MERGE0] + t[EV_FIN_END];
+  st.idle_ms = t[EV_PASS] + t[EV_FIN];
+  st.device_ms = st.map_ms + st.reduce_ms + st.merge_ms + st.finalize_ms + st.idle_ms;
 }
 
 void Engine::Impl::settle() {
@@ -524,6 +562,8 @@ bool Engine::Impl::finalize_local_speculative() {
     h_spec.resize(4096);
     std::memset(h_spec.data(), 0, h_spec.size());  // the sequence word starts below every spec_seq
   }
+  mark(EV_FIN_END);
+  fin_end_marked = true;
   PubList pc{};
   pc.add(h_spec.data(), d_n, 8);
   pc.add(h_spec.data() + 8, d_arena_cursor, 8);
@@ -660,7 +700,10 @@ KeyTable Engine::Impl::download_cols() {
 Engine::Engine(const Options& opt) : p_(new Impl(opt)) {}
 Engine::~Engine() = default;
 const Options& Engine::options() const { return p_->opt; }
-Stats& Engine::stats() { return p_->st; }
+Stats& Engine::stats() {
+  p_->collect_stage_times();
+  return p_->st;
+}
 
 void Engine::reset() {
   Impl& im = *p_;
@@ -676,6 +719,7 @@ void Engine::reset() {
   im.copy_used = false;
   im.st = Stats{};
   im.max_end = 0;
+  im.ev_n = 0;
 }
 
 void Engine::count_device(const uint8_t* d_text, uint64_t n, uint64_t avail, uint64_t global_base, int prev_byte) {
@@ -689,7 +733,7 @@ void Engine::count_device(const uint8_t* d_text, uint64_t n, uint64_t avail, uin
     im.process_chunk(d_text + off, len, avail - off, global_base + off, off == 0 ? prev_byte : -1, off + len >= n);
   }
   im.st.bytes += n;
-  im.st.map_reduce_ms += (now_seconds() - t0) * 1e3;
+  im.st.host_count_ms += (now_seconds() - t0) * 1e3;
 }
 
 namespace {
@@ -830,7 +874,7 @@ void Engine::count_source(ChunkSource& src, uint64_t global_base) {
     len = next;
   }
   WC_HIP_CHECK(hipStreamSynchronize(im.copy_s));
-  im.st.map_reduce_ms += (now_seconds() - t0) * 1e3;
+  im.st.host_count_ms += (now_seconds() - t0) * 1e3;
 }
 
 void Engine::count_pinned_replay(const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t global_base,
@@ -877,13 +921,17 @@ void Engine::count_pinned_replay(const uint8_t* pool, uint64_t pool_bytes, uint6
     im.st.bytes += len;
   }
   WC_HIP_CHECK(hipStreamSynchronize(im.copy_s));
-  im.st.map_reduce_ms += (now_seconds() - t0) * 1e3;
+  im.st.host_count_ms += (now_seconds() - t0) * 1e3;
 }
 
 const uint8_t* Engine::synth_device(uint64_t n, uint64_t first_segment, const SynthSpec& spec) {
   Impl& im = *p_;
   WC_HIP_CHECK(hipSetDevice(im.dev));
-  const uint64_t key = spec.seed * 1000003ull ^ ((uint64_t)spec.vocab << 20) ^ (uint64_t)(spec.zipf_s * 1e6);
+  // the generated text is rewritten: a pass still pending on the old text
+  // (speculative last pass) must complete first — its recovery would re-read it
+  im.settle();
+  const uint64_t key = spec.seed * 1000003ull ^ ((uint64_t)spec.vocab << 20) ^ (uint64_t)(spec.zipf_s * 1e6) ^
+                       ((uint64_t)(spec.long_frac * 1e6) << 40);
   if (key != im.vocab_key) {
     const HostVocab hv = build_vocab(spec);
     im.vocab_mem.reserve(hv.bytes.size() + hv.off.size() * 9 + hv.cdf.size() * 4 + 4096);
@@ -915,27 +963,31 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
   static const bool merge_always = getenv("WC_MERGE_ALWAYS") && atoi(getenv("WC_MERGE_ALWAYS")) != 0;
   const bool merged = comm && (comm->size() > 1 || merge_always);
   im.apply_reset();  // a reset with no pass since: the table reads empty
+  im.mark(EV_FIN);
+  im.fin_end_marked = false;
   bool drained = false;
   if (merged) {
     im.settle();
     im.compact_local();
-    const double tm = now_seconds();
+    im.mark(EV_MERGE0);
     merge_cols(im, *comm, all_ranks);
-    im.st.merge_ms += (now_seconds() - tm) * 1e3;
+    im.mark(EV_MERGE1);
     im.sort_cols_by_first();
   } else if (im.pend.active && im.finalize_local_speculative()) {
     drained = im.spin_wait;  // its publish wait saw the whole stream complete
   } else {
+    im.fin_end_marked = false;  // a speculative finalize that needed recovery is redone here
     im.settle();
     im.finalize_local_sorted();  // sort (first, slot) pairs, gather the columns from the table once
   }
+  if (!im.fin_end_marked) im.mark(EV_FIN_END);
   // the merge's last collectives are still in flight: wait under the comm watchdog
   if (merged) comm->sync(im.s);
   else if (!drained) WC_HIP_CHECK(hipStreamSynchronize(im.s));
-  im.st.finalize_ms += (now_seconds() - t0) * 1e3;
-  WC_LOG(LOG_INFO, "dev %d: finalize %.3f ms (merge %.3f ms), %llu keys, %u chunk(s), %llu records, %u re-run(s)",
-         im.dev, (now_seconds() - t0) * 1e3, im.st.merge_ms, (unsigned long long)im.cols.n, im.st.chunks,
-         (unsigned long long)im.st.records, im.st.map_reruns);
+  im.st.host_finalize_ms += (now_seconds() - t0) * 1e3;
+  WC_LOG(LOG_INFO, "dev %d: finalize %.3f ms (host), %llu keys, %u chunk(s), %llu records, %u re-run(s)", im.dev,
+         (now_seconds() - t0) * 1e3, (unsigned long long)im.cols.n, im.st.chunks, (unsigned long long)im.st.records,
+         im.st.map_reruns);
   return im.cols.n;
 }
 

@@ -145,6 +145,17 @@ struct Engine::Impl {
   uint32_t pass_seq = 0;
   void wait_published(const uint32_t* seq, uint32_t want);
   void settle();           // complete a pending pass
+  // Stage events (device time per stage of the last job, Stats::map_ms ...):
+  // mark(tag) records an event on s; the interval from the previous mark to
+  // this one is charged to the stage `tag` closes.
+  enum : int { EV_PASS = 0, EV_MAP, EV_REDUCE, EV_FIN, EV_MERGE0, EV_MERGE1, EV_FIN_END };
+  bool stage_events = true;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<int> ev_tag;
+  size_t ev_n = 0;
+  bool fin_end_marked = false;
+  void mark(int tag);
+  void collect_stage_times();
   uint32_t blocks_for(uint64_t len) const;
   // Shuffle partitions track the running table (one reduce block reads only
   // its own partition) up to MAX_REC_BUCKETS.

@@ -19,15 +19,22 @@ HostVocab build_vocab(const SynthSpec& spec) {
   uint64_t st = spec.seed * 0xA24BAED4963EE407ull + 0x9FB21C651E98DF25ull;
   v.off.reserve(n);
   v.len.reserve(n);
+  // long_frac: each rank independently becomes a 16..64-byte word (its own
+  // stream, so long_frac = 0 leaves the vocabulary bit-identical)
+  uint64_t lst = spec.seed * 0xD1B54A32D192ED03ull + 0x8CB92BA72F3D8DD7ull;
+  const uint64_t long_cut = (uint64_t)(std::min(std::max(spec.long_frac, 0.0), 1.0) * 18446744073709551615.0);
   for (uint32_t i = 0; i < n; ++i) {
     // Frequent ranks are short words, rare ranks long (English-like); ~10% of
     // the vocabulary is longer than 8 bytes.
     const double lg = std::log2((double)i + 2.0);
+    const uint64_t lr = spec.long_frac > 0 ? splitmix64(lst) : ~0ull;
+    const bool is_long = spec.long_frac > 0 && (spec.long_frac >= 1.0 || lr < long_cut);
     std::string w;
     for (int attempt = 0;; ++attempt) {
       const uint64_t r = splitmix64(st);
       uint32_t len = 1 + (uint32_t)(lg * 0.45) + (uint32_t)(r % 4) + (uint32_t)attempt / 4;
       if (len > 24) len = 24;
+      if (is_long) len = 16 + (uint32_t)((r >> 8) % 49) + (uint32_t)attempt / 4;  // 16..64 (+ retries)
       w.assign(len, 'a');
       uint64_t bits = splitmix64(st);
       for (uint32_t c = 0; c < len; ++c) {

@@ -158,7 +158,7 @@ def test_cli_bench_json_and_log_levels(tmp_path, golden_text):
     assert out.returncode == 0 and out.stdout == GOLDEN_OUTPUT
     assert b"wordcount bench: {" in out.stderr and b"[wc info" in out.stderr
     d = json.loads((tmp_path / "b.json").read_text())
-    assert d["tokens"] == 9 and d["keys"] == 6 and d["path"] == "cpu" and "stages_ms" in d
+    assert d["tokens"] == 9 and d["keys"] == 6 and d["path"] == "cpu" and "device_ms" in d
     quiet = subprocess.run([exe, "--cpu"], cwd=tmp_path, capture_output=True, timeout=60,
                            env=dict(os.environ, WC_LOG="warn"))
     assert quiet.stderr == b""

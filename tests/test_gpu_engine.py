@@ -227,7 +227,7 @@ def test_rccl_merge_protocol_world1(merge_mode):
         "    got = e.result(comm, all_ranks=all_ranks)\n"
         "    want = ops.cpu_count(text)\n"
         "    assert got.words == want.words and got.counts.tolist() == want.counts.tolist(), 'mismatch'\n"
-        "assert e.stats()['merge_ms'] > 0\n"
+        "assert e.stats()['device_ms']['merge'] > 0\n"
         "e.close(); comm.close(); print('ok')\n"
     )
     env = dict(os.environ, WC_MERGE_ALWAYS="1")

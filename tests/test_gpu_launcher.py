@@ -28,3 +28,32 @@ def test_torchrun_world1_rccl_merge(merge):
     assert d["validated"] is True
     assert d["config"]["merge"] == merge
     assert d["n_gpus"] == 1 and d["distinct_words"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_self_launch_refuses_missing_gpus():
+    # `bench.py --gpus N` launches N ranks itself; with fewer GPUs visible it must
+    # fail at once, before any rank starts
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    from cuda_mapreduce_amd.parallel.launch import visible_gpus
+
+    n = visible_gpus()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n + 1), "--steps", "1"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=60)
+    assert p.returncode == 2
+    assert f"{n + 1} GPUs requested, {n} visible" in p.stderr
+
+
+@pytest.mark.gpu
+def test_bench_one_runtime_per_rank():
+    # the rank loads only /opt/rocm's HIP runtime and RCCL (no torch, no second copy)
+    env = dict(os.environ, WC_MERGE_ALWAYS="1")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "2", "--warmup", "1",
+                        "--gb-per-gpu", "0.125"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    rt = d["runtime"]
+    assert rt["torch"] is False
+    assert len(rt["hip"]) == 1 and rt["hip"][0].startswith("/opt/rocm"), rt
+    assert len(rt["rccl"]) == 1 and rt["rccl"][0].startswith("/opt/rocm"), rt
+    assert d["validated"] is True and d["control_plane"].startswith("native RCCL")

@@ -32,7 +32,7 @@ const char* kUsage =
     "  --echo | --no-echo      echo the input after 'Input Data:' (default: echo)\n"
     "  --no-list               do not print per-word rows\n"
     "  --top K                 print only the K most frequent words\n"
-    "  --synthetic SIZE[:SEED[:VOCAB[:ZIPF]]]  count generated text instead of FILE\n"
+    "  --synthetic SIZE[:SEED[:VOCAB[:ZIPF[:LONGFRAC]]]]  count generated text instead of FILE\n"
     "  --chunk-bytes N         device chunk size (default 1G)\n"
     "  --host-staged           stream FILE through the pinned host ring (no echo)\n"
     "  --bench-json PATH       write throughput / stage timings as JSON\n"
@@ -116,6 +116,7 @@ Cli parse(int argc, char** argv) {
       if (f.size() > 1) c.spec.seed = std::stoull(f[1]);
       if (f.size() > 2) c.spec.vocab = (uint32_t)std::stoul(f[2]);
       if (f.size() > 3) c.spec.zipf_s = std::stod(f[3]);
+      if (f.size() > 4) c.spec.long_frac = std::stod(f[4]);
     } else if (!a.empty() && a[0] == '-') wc::fail("unknown option " + a + "\n" + kUsage);
     else c.file = a;
   }
@@ -137,10 +138,12 @@ void add_stats(wc::Stats& a, const wc::Stats& b) {
   a.chunks += b.chunks;
   a.map_reruns += b.map_reruns;
   a.table_splits += b.table_splits;
-  a.h2d_ms += b.h2d_ms;
-  a.map_reduce_ms += b.map_reduce_ms;
+  a.map_ms += b.map_ms;
+  a.reduce_ms += b.reduce_ms;
   a.finalize_ms += b.finalize_ms;
   a.merge_ms += b.merge_ms;
+  a.idle_ms += b.idle_ms;
+  a.device_ms += b.device_ms;
 }
 
 void write_out(const std::string& s) { std::fwrite(s.data(), 1, s.size(), stdout); }
@@ -270,10 +273,11 @@ int run(const Cli& c) {
     for (int r = 0; r < g; ++r) {
       const wc::Stats& x = rank_stats[r];
       // per-rank stage maxima: ranks run concurrently, the slowest sets the pace
-      stages.map_reduce_ms = std::max(stages.map_reduce_ms, x.map_reduce_ms);
+      stages.map_ms = std::max(stages.map_ms, x.map_ms);
+      stages.reduce_ms = std::max(stages.reduce_ms, x.reduce_ms);
       stages.finalize_ms = std::max(stages.finalize_ms, x.finalize_ms);
       stages.merge_ms = std::max(stages.merge_ms, x.merge_ms);
-      stages.h2d_ms = std::max(stages.h2d_ms, x.h2d_ms);
+      stages.device_ms = std::max(stages.device_ms, x.device_ms);
       stages.records += x.records;
       stages.chunks += x.chunks;
       stages.map_reruns += x.map_reruns;
@@ -288,11 +292,13 @@ int run(const Cli& c) {
   std::snprintf(js, sizeof(js),
                 "{\"bytes\": %llu, \"tokens\": %llu, \"keys\": %zu, \"seconds\": %.6f, \"gb_per_s\": %.3f, "
                 "\"words_per_s\": %.1f, \"gpus\": %d, \"path\": \"%s\", \"chunk_bytes\": %llu, "
-                "\"stages_ms\": {\"map_reduce\": %.3f, \"finalize\": %.3f, \"merge\": %.3f}, "
+                "\"device_ms\": {\"map\": %.3f, \"reduce\": %.3f, \"finalize\": %.3f, \"merge\": %.3f, "
+                "\"total\": %.3f}, "
                 "\"chunks\": %u, \"records\": %llu, \"map_reruns\": %u, \"table_splits\": %u}",
                 (unsigned long long)bytes, (unsigned long long)t.total, t.size(), secs, bytes / secs / 1e9,
                 t.total / secs, gpu_path ? c.gpus : 0, c.compat ? "compat" : (c.cpu ? "cpu" : "gpu"),
-                (unsigned long long)c.chunk, stages.map_reduce_ms, stages.finalize_ms, stages.merge_ms,
+                (unsigned long long)c.chunk, stages.map_ms, stages.reduce_ms, stages.finalize_ms, stages.merge_ms,
+                stages.device_ms,
                 stages.chunks, (unsigned long long)stages.records, stages.map_reruns, stages.table_splits);
   if (c.bench) std::fprintf(stderr, "wordcount bench: %s\n", js);
   if (!c.bench_json.empty()) {
