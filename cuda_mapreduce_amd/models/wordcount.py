@@ -43,9 +43,11 @@ CONFIGS = {
         JobConfig("cpu-test", "test.txt word count on CPU reference path (single-thread hash map, no GPU)",
                   source="cpu", path=os.path.join(os.path.dirname(__file__), "..", "..", "tests", "data", "test.txt")),
         JobConfig("1gb", "1 GB synthetic ASCII text per MI355X (map/shuffle/reduce HIP kernels end-to-end; "
-                  "N > 1: RCCL reduce-scatter dense merge)", merge="dense"),
+                  "N > 1: shuffle merge — all-to-all to hash owners over xGMI)"),
         JobConfig("64gb", "64 GB synthetic text, single MI355X (HBM-resident, chunked)", bytes_per_gpu=64 * GiB,
                   chunk_bytes=2 * GiB),
+        # the config names the reduce-scatter merge: dense protocol (modelled at W = 8, 100k keys/rank:
+        # ~0.06 ms per job more than the shuffle's all-to-all, profiles/merge_cost.md; unmeasured at W = 8)
         JobConfig("256gb-8gpu", "256 GB synthetic text sharded across 8x MI355X, RCCL reduce-scatter merge",
                   bytes_per_gpu=32 * GiB, gpus=8, chunk_bytes=2 * GiB, merge="dense"),
         JobConfig("1tb-8gpu-host-staged", "1 TB synthetic text, 8x MI355X, host-staged pinned hipMemcpyAsync",

@@ -307,13 +307,15 @@ def shard_range_file(path: str, rank: int, world: int):
 
 
 def loopback_count(data: bytes, ranks: int, devices: Optional[Sequence[int]] = None, all_ranks: bool = False,
-                   **opts) -> Result:
+                   resident: bool = False, **opts) -> Result:
     """`ranks` virtual ranks (threads) on `devices` count shards and merge in-process.
 
     Returns rank 0's table; with ``all_ranks`` every rank receives the merged
-    table and the native side checks that they all equal rank 0's."""
+    table and the native side checks that they all equal rank 0's.  With
+    ``resident`` each shard is counted from HBM and the merge runs behind the
+    pending last pass (the bench's speculative merged finalize)."""
     ptr, keep = _u8ptr(data)
     devs = (ctypes.c_int * ranks)(*(devices if devices is not None else [0] * ranks))
     o = default_options(**opts)
     return Result._from_native(
-        check_ptr(lib.wc_loopback_count(ptr, len(keep), ranks, devs, ctypes.byref(o), int(all_ranks))))
+        check_ptr(lib.wc_loopback_count(ptr, len(keep), ranks, devs, ctypes.byref(o), int(all_ranks), int(resident))))

@@ -1,7 +1,7 @@
 """Data parallelism across GPUs: torch-free launcher / rendezvous (launch.py),
 torch.distributed helpers (dist.py), native RCCL merge."""
 _DIST = ("CommFault", "DistEnv", "DistributedWordCount", "comm_timeout_s", "host_merge", "init_from_env", "rccl_comm",
-         "owner_merge")
+         "gather_merge")
 
 
 def __getattr__(name):

@@ -6,8 +6,10 @@
   created from a unique id that rank 0 broadcasts through torch.distributed;
   the merge (src/dist/merge.cpp) then runs reduce-scatter + all-gather over
   xGMI on device buffers.
-* CPU ranks (tests, hosts without GPUs): the same merge protocol on host data
-  (``host_merge``) over gloo.
+* CPU ranks (tests, hosts without GPUs): the same owner-partitioned merge
+  protocols (shuffle / dense) on host data (``host_merge``) over gloo.
+* bench.py does not use this module: its ranks never import torch
+  (parallel/launch.py: file rendezvous, then the native communicator).
 
 Input sharding: rank r owns every token whose first byte lies in its byte
 range (``shard_range``), so shards need no halo exchange.
@@ -16,6 +18,8 @@ from __future__ import annotations
 
 import datetime
 import os
+import struct
+import zlib
 from dataclasses import dataclass
 from typing import Optional
 
@@ -113,46 +117,127 @@ def _reduce_scatter(t, op):
     return out
 
 
-def host_merge(local: Result) -> Result:
-    """Merge per-rank results on the host (same protocol as src/dist/merge.cpp).
+def _owner(word: bytes, world: int) -> int:
+    return zlib.crc32(word) % world
 
-    1. all-gather every rank's distinct keys
-    2. deterministic union (sorted) -> identical global ids on every rank
-    3. scatter local counts / first offsets into dense vectors
-    4. reduce-scatter (sum / min), 5. all-gather the slices
-    """
+
+def _pack(rows) -> bytes:
+    """(word, count, first) rows -> one byte string: per row u32 length, word, u64 count, u64 first."""
+    out = bytearray()
+    for w, c, f in rows:
+        out += struct.pack("<I", len(w)) + w + struct.pack("<QQ", int(c), int(f))
+    return bytes(out)
+
+
+def _unpack(buf: bytes):
+    rows, i = [], 0
+    while i < len(buf):
+        (n,) = struct.unpack_from("<I", buf, i)
+        w = bytes(buf[i + 4 : i + 4 + n])
+        c, f = struct.unpack_from("<QQ", buf, i + 4 + n)
+        rows.append((w, c, f))
+        i += 4 + n + 16
+    return rows
+
+
+def _alltoallv_bytes(parts) -> list:
+    """Personalised exchange of byte strings: parts[p] goes to rank p; returns what each rank sent here."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size()
+    send_sizes = torch.tensor([len(b) for b in parts], dtype=torch.int64)
+    recv_sizes = torch.empty(world, dtype=torch.int64)
+    dist.all_to_all_single(recv_sizes, send_sizes)
+    send = torch.frombuffer(bytearray(b"".join(parts)) or bytearray(1), dtype=torch.uint8)[: int(send_sizes.sum())]
+    recv = torch.empty(int(recv_sizes.sum()), dtype=torch.uint8)
+    dist.all_to_all_single(recv, send, output_split_sizes=recv_sizes.tolist(), input_split_sizes=send_sizes.tolist())
+    raw, out, o = recv.numpy().tobytes(), [], 0
+    for n in recv_sizes.tolist():
+        out.append(raw[o : o + n])
+        o += n
+    return out
+
+
+def host_merge(local: Result, dense: bool = False) -> Result:
+    """Merge per-rank results on the host over torch.distributed (CPU ranks over
+    gloo) with the owner-partitioned protocol of src/dist/merge.cpp:
+
+    1. owner(word) = crc32(word) mod W; rows are packed by owner
+    2. all-to-all (personalised exchange) of the packed rows
+    3. each owner merges what it received (counts add, first offset = min)
+    shuffle: 4. the owners' merged rows are gathered to every rank
+    dense:   4. owners' sizes all-gathered -> global id = owner base + index;
+             5. ids go back to the senders (reverse all-to-all); every rank
+                scatters its counts / first offsets into dense vectors by id;
+             6. reduce-scatter (sum / min) + all-gather of the vectors; the
+                dictionary rows are gathered to every rank
+    Every rank returns the merged table in first-occurrence order."""
     import torch
     import torch.distributed as dist
 
     world, rank = dist.get_world_size(), dist.get_rank()
-    keys = [None] * world
+    rows = list(zip(local.words, (int(c) for c in local.counts), (int(f) for f in local.first_off)))
+    by_owner = [[] for _ in range(world)]
+    for r in rows:
+        by_owner[_owner(r[0], world)].append(r)
     _fault_tick(rank)
-    dist.all_gather_object(keys, list(local.words))
-    union = sorted(set().union(*map(set, keys)))
-    gid = {w: i for i, w in enumerate(union)}
-    vpad = max(world, -(-len(union) // world) * world)
-    cnt = torch.zeros(vpad, dtype=torch.int64)
-    first = torch.full((vpad,), 1 << 62, dtype=torch.int64)
-    for w, c, f in zip(local.words, local.counts, local.first_off):
-        cnt[gid[w]] = int(c)
-        first[gid[w]] = int(f)
+    received = _alltoallv_bytes([_pack(b) for b in by_owner])
+    merged = {}
+    for buf in received:
+        for w, c, f in _unpack(buf):
+            e = merged.get(w)
+            if e is None:
+                merged[w] = [c, f]
+            else:
+                e[0] += c
+                e[1] = min(e[1], f)
+    own = sorted(merged.items())  # owner slice in a deterministic order (dense: its id order)
     _fault_tick(rank)
-    scnt = _reduce_scatter(cnt, dist.ReduceOp.SUM)
-    _fault_tick(rank)
-    sfirst = _reduce_scatter(first, dist.ReduceOp.MIN)
-    full_cnt = [torch.empty_like(scnt) for _ in range(world)]
-    full_first = [torch.empty_like(sfirst) for _ in range(world)]
-    _fault_tick(rank)
-    dist.all_gather(full_cnt, scnt)
-    _fault_tick(rank)
-    dist.all_gather(full_first, sfirst)
-    c = torch.cat(full_cnt)[: len(union)].numpy()
-    f = torch.cat(full_first)[: len(union)].numpy()
-    order = np.argsort(f, kind="stable")
+    slices = [None] * world
+    dist.all_gather_object(slices, [w for w, _ in own])  # the dictionary (sizes give the id bases)
+    if not dense:
+        vals = [None] * world
+        _fault_tick(rank)
+        dist.all_gather_object(vals, [v for _, v in own])
+        words = [w for sl in slices for w in sl]
+        cnt = [v[0] for vl in vals for v in vl]
+        first = [v[1] for vl in vals for v in vl]
+    else:
+        base = np.cumsum([0] + [len(sl) for sl in slices])
+        ids = {w: int(base[rank]) + i for i, (w, _) in enumerate(own)}
+        # ids back to the senders: for each sender, the ids of the rows it sent here, in its order
+        back = [_pack([(w, ids[w], 0) for w, _, _ in _unpack(buf)]) for buf in received]
+        _fault_tick(rank)
+        mine = _alltoallv_bytes(back)
+        G = int(base[-1])
+        vpad = max(world, -(-G // world) * world)
+        vc = torch.zeros(vpad, dtype=torch.int64)
+        vf = torch.full((vpad,), 1 << 62, dtype=torch.int64)
+        for p in range(world):
+            for (w, c, f), (w2, gid, _) in zip(by_owner[p], _unpack(mine[p])):
+                assert w == w2
+                vc[gid] = c
+                vf[gid] = f
+        _fault_tick(rank)
+        scnt = _reduce_scatter(vc, dist.ReduceOp.SUM)
+        _fault_tick(rank)
+        sfirst = _reduce_scatter(vf, dist.ReduceOp.MIN)
+        full_cnt = [torch.empty_like(scnt) for _ in range(world)]
+        full_first = [torch.empty_like(sfirst) for _ in range(world)]
+        _fault_tick(rank)
+        dist.all_gather(full_cnt, scnt)
+        _fault_tick(rank)
+        dist.all_gather(full_first, sfirst)
+        words = [w for sl in slices for w in sl]
+        cnt = torch.cat(full_cnt)[:G].tolist()
+        first = torch.cat(full_first)[:G].tolist()
+    order = np.argsort(np.asarray(first, dtype=np.uint64), kind="stable")
+    c = np.asarray(cnt, dtype=np.uint64)
     return Result(
-        words=[union[i] for i in order],
-        counts=c[order].astype(np.uint64),
-        first_off=f[order].astype(np.uint64),
+        words=[words[i] for i in order],
+        counts=c[order],
+        first_off=np.asarray(first, dtype=np.uint64)[order],
         total=int(c.sum()),
     )
 
@@ -191,6 +276,7 @@ class DistributedWordCount:
     def __init__(self, env: DistEnv, use_gpu: bool = True, **engine_opts):
         self.env = env
         self.use_gpu = use_gpu
+        self.dense = engine_opts.get("merge_mode", 0) == 1  # CPU ranks: the same protocol choice
         self.engine = Engine(device=env.local_rank, **engine_opts) if use_gpu else None
         self.comm = rccl_comm(env, env.local_rank) if use_gpu else None
 
@@ -235,4 +321,4 @@ class DistributedWordCount:
         local = cpu_fn()
         if self.env.world == 1:
             return local
-        return host_merge(local)
+        return host_merge(local, dense=self.dense)

@@ -107,9 +107,11 @@ int wc_comm_barrier(wc_comm* c);
 int wc_comm_allgather_host(wc_comm* c, const void* send, uint64_t bytes, void* recv);
 /* N virtual ranks on `devices` (one thread each) count shards of `text` and
  * merge through the loopback communicator; returns rank 0's result.  With
- * all_ranks every rank receives the merged table and must match rank 0's. */
+ * all_ranks every rank receives the merged table and must match rank 0's.
+ * resident: shards are copied to HBM first and counted in place (the last
+ * pass stays pending: the speculative merged finalize). */
 wc_result* wc_loopback_count(const uint8_t* text, uint64_t n, int ranks, const int* devices, const wc_options* o,
-                             int all_ranks);
+                             int all_ranks, int resident);
 
 #ifdef __cplusplus
 }

@@ -451,7 +451,7 @@ int wc_comm_allgather_host(wc_comm* c, const void* send, uint64_t bytes, void* r
 void wc_comm_destroy(wc_comm* c) { delete c; }
 
 wc_result* wc_loopback_count(const uint8_t* text, uint64_t n, int ranks, const int* devices, const wc_options* o,
-                             int all_ranks) {
+                             int all_ranks, int resident) {
   wc_result* out = new wc_result;
   std::vector<std::string> errs(ranks);
   std::vector<wc::KeyTable> tables(ranks);
@@ -468,8 +468,20 @@ wc_result* wc_loopback_count(const uint8_t* text, uint64_t n, int ranks, const i
         opt.device = devices ? devices[r] : 0;
         wc::Engine eng(opt);
         const wc::ShardRange sr = wc::shard_range_mem(text, n, r, ranks);
-        if (sr.end > sr.begin) eng.count_host(text + sr.begin, sr.end - sr.begin, sr.begin);
+        uint8_t* d = nullptr;
+        if (sr.end > sr.begin && resident) {
+          // HBM-resident shard: the last pass stays pending and the merge runs
+          // speculatively behind it (merge_cols_speculative)
+          const uint64_t len = sr.end - sr.begin;
+          WC_HIP_CHECK(hipSetDevice(opt.device));
+          WC_HIP_CHECK(hipMalloc(&d, len + 64));
+          WC_HIP_CHECK(hipMemcpy(d, text + sr.begin, len, hipMemcpyHostToDevice));
+          eng.count_device(d, len, len, sr.begin, sr.begin ? text[sr.begin - 1] : ' ');
+        } else if (sr.end > sr.begin) {
+          eng.count_host(text + sr.begin, sr.end - sr.begin, sr.begin);
+        }
         wc::KeyTable t = eng.result(comms[r].get(), all_ranks != 0);
+        if (d) (void)hipFree(d);
         if (r == 0) {
           out->t = std::move(t);
         } else if (all_ranks) {

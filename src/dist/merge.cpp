@@ -136,48 +136,59 @@ void merge_to_root(Engine::Impl& im, Comm& comm, const std::vector<uint64_t>& ra
   im.max_end = gmax_end;
 }
 
-namespace {
-
 // Step 1 of both protocols: rows / long-word bytes per (rank, owner), and the
-// send / receive layouts of the owner exchange derived from them.
+// send / receive layouts of the owner exchange derived from them.  Count
+// vector of one rank (C = 2W + 2 words): (rows, bytes) per owner, its max
+// byte offset, and the flags of its last pass (nonzero: that pass needs
+// recovery, so a speculative compaction behind it is void on EVERY rank).
 struct OwnerPlan {
   int W = 1, R = 0;
-  size_t C = 0;                          // per rank: (rows, bytes) per owner + max offset
+  size_t C = 0;
   std::vector<unsigned long long> all;  // W x C
   uint64_t gmax_end = 0;
+  bool any_flags = false;
   std::vector<uint64_t> rank_rows, rank_bytes;
   uint64_t total_rows = 0, Gmax = 0, GBmax = 0;  // rows / bytes of all ranks (bounds of the merged table)
   std::vector<size_t> so_r, sb_r, so_b, sb_b, ro_r, rb_r, ro_b, rb_b;  // byte offsets / sizes
   uint64_t tr = 0, tb = 0, rr = 0, rbt = 0;                              // rows / bytes sent, received
   unsigned long long* d_cnt = nullptr;  // device: owner counts | scatter cursor
+  unsigned long long* d_all = nullptr;  // device: the all-gathered W x C matrix
 };
 
-OwnerPlan plan_owners(Engine::Impl& im, Comm& comm) {
-  OwnerPlan P;
+// Device half: owner counts of the compact columns (n rows, or *dn rows with
+// n the bound), the max offset and (pass_flags) the last pass's flags, then the
+// all-gather.  Nothing waits here.
+void plan_enqueue(Engine::Impl& im, Comm& comm, uint64_t n, const uint64_t* dn, const uint32_t* pass_flags,
+                  OwnerPlan& P) {
   hipStream_t s = im.s;
   P.W = comm.size();
   P.R = comm.rank();
-  const int W = P.W, R = P.R;
+  const int W = P.W;
   WC_CHECK(W <= (int)MERGE_MAX_RANKS, "merge supports at most 64 ranks");
-  P.C = 2 * (size_t)W + 1;
+  P.C = 2 * (size_t)W + 2;
   const size_t C = P.C;
   DeviceArena& S = im.merge_small;  // small buffers: own arena
   S.reserve(((size_t)W * C + 2 * C + 16) * 8 + 8 * 1024);
+  S.reset();
   P.d_cnt = take_aligned<unsigned long long>(S, 2 * C);
-  unsigned long long* d_all = take_aligned<unsigned long long>(S, (size_t)W * C);
+  P.d_all = take_aligned<unsigned long long>(S, (size_t)W * C);
   WC_HIP_CHECK(hipMemsetAsync(P.d_cnt, 0, 2 * C * 8, s));
   uint64_t* mx = host_words(im) + HW_MX;
   *mx = im.max_end;
   WC_HIP_CHECK(hipMemcpyAsync(P.d_cnt + 2 * W, mx, 8, hipMemcpyHostToDevice, s));
-  launch_owner_count(im.cols.k0, im.cols.k1, im.cols.sref_len, im.cols.n, (uint32_t)W, P.d_cnt, s);
-  comm.allgather(P.d_cnt, d_all, C * 8, s);
-  P.all.resize((size_t)W * C);
-  WC_HIP_CHECK(hipMemcpyAsync(P.all.data(), d_all, P.all.size() * 8, hipMemcpyDeviceToHost, s));
-  comm.sync(s);
+  launch_owner_count(im.cols.k0, im.cols.k1, im.cols.sref_len, n, dn, pass_flags, (uint32_t)W, P.d_cnt, s);
+  comm.allgather(P.d_cnt, P.d_all, C * 8, s);
+}
+
+// Host half, from the all-gathered matrix (P.all).
+void plan_finish(OwnerPlan& P) {
+  const int W = P.W, R = P.R;
+  const size_t C = P.C;
   P.rank_rows.assign(W, 0);
   P.rank_bytes.assign(W, 0);
   for (int r = 0; r < W; ++r) {
     P.gmax_end = std::max<uint64_t>(P.gmax_end, P.all[(size_t)r * C + 2 * W]);
+    if (P.all[(size_t)r * C + 2 * W + 1]) P.any_flags = true;
     for (int p = 0; p < W; ++p) {
       P.rank_rows[r] += P.all[(size_t)r * C + 2 * p];
       P.rank_bytes[r] += P.all[(size_t)r * C + 2 * p + 1];
@@ -203,6 +214,18 @@ OwnerPlan plan_owners(Engine::Impl& im, Comm& comm) {
     P.rr += theirs[2 * R];
     P.rbt += theirs[2 * R + 1];
   }
+}
+
+namespace {
+
+// Synchronous step 1 (compact columns already counted on the host).
+OwnerPlan plan_owners(Engine::Impl& im, Comm& comm) {
+  OwnerPlan P;
+  plan_enqueue(im, comm, im.cols.n, nullptr, nullptr, P);
+  P.all.resize((size_t)P.W * P.C);
+  WC_HIP_CHECK(hipMemcpyAsync(P.all.data(), P.d_all, P.all.size() * 8, hipMemcpyDeviceToHost, im.s));
+  comm.sync(im.s);
+  plan_finish(P);
   return P;
 }
 
@@ -219,10 +242,9 @@ std::vector<size_t> rescale(const std::vector<size_t>& v, size_t es) {
 // Steps 2-4 of both protocols; the dense protocol (dense = true) then numbers
 // the dictionary and reduces dense count vectors instead of using the owners'
 // merged counts.
-void merge_cols_owner(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense) {
+void merge_cols_owner(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense, OwnerPlan& P) {
   Range rg(dense ? "wc_merge_dense" : "wc_merge_shuffle");
   hipStream_t s = im.s;
-  OwnerPlan P = plan_owners(im, comm);
   const int W = P.W, R = P.R;
   const uint64_t n = im.cols.n;
   // Few keys in total: every rank sends its rows straight to rank 0, which
@@ -383,7 +405,79 @@ void merge_cols_owner(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense) 
 }
 
 void merge_cols(Engine::Impl& im, Comm& comm, bool all_ranks) {
-  merge_cols_owner(im, comm, all_ranks, im.opt.merge_mode == 1);
+  OwnerPlan P = plan_owners(im, comm);
+  merge_cols_owner(im, comm, all_ranks, im.opt.merge_mode == 1, P);
+}
+
+// The merged finalize launched right behind the pending last pass (SURVEY
+// §5.8 without the settle): device bucket offsets -> compaction sized to the
+// table's capacity -> owner counts of the device-counted rows + this pass's
+// flags -> all-gather -> one publish into page-locked memory, and ONE host
+// wait for all of it (the pass's counters included).  A rank whose pass needs
+// recovery flags it in its count vector, so every rank sees the same matrix
+// and all of them fall back together (returns false; the caller recovers and
+// runs the synchronous protocol).
+bool merge_cols_speculative(Engine::Impl& im, Comm& comm, bool all_ranks) {
+  Range rg("wc_merge_speculative");
+  const Engine::Impl::PendingPass p = im.pend;
+  im.pend.active = false;
+  hipStream_t s = im.s;
+  const TableView& t = im.table();
+  const size_t nb = (size_t)1 << t.log2_buckets;
+  const uint64_t cap = (uint64_t)nb * TAB_SLOTS;
+  DeviceArena& A = im.fin_mem;
+  A.reserve((cap + 1) * (5 * 8 + 4) + nb * 8 + 64 * 1024);
+  A.reset();
+  KeyCols c;
+  c.k0 = A.take_n<uint64_t>(cap + 1);
+  c.k1 = A.take_n<uint64_t>(cap + 1);
+  c.cnt = A.take_n<uint64_t>(cap + 1);
+  c.first = A.take_n<uint64_t>(cap + 1);
+  c.sref_off = A.take_n<uint64_t>(cap + 1);
+  c.sref_len = A.take_n<uint32_t>(cap + 1);
+  uint64_t* d_boff = A.take_n<uint64_t>(nb);
+  uint64_t* d_n = A.take_n<uint64_t>(2);
+  launch_bucket_offsets(t.occupancy, (uint32_t)nb, d_boff, d_n, s);
+  launch_table_compact(t, d_boff, c.k0, c.k1, c.cnt, c.first, c.sref_off, c.sref_len, s);
+  im.cols = c;
+  im.cols_arena = im.d_arena;
+  im.mark(Engine::Impl::EV_MERGE0);
+  OwnerPlan P;
+  plan_enqueue(im, comm, cap, d_n, im.d_ctr->flags, P);
+  // one publish: the gathered matrix + the local key count, then a sequence word
+  const size_t words = (size_t)P.W * P.C;
+  if (im.h_plan.size() < (words + 4) * 8) {
+    im.h_plan = PinnedBuffer(std::max<size_t>((words + 4) * 8, 4096));
+    std::memset(im.h_plan.data(), 0, im.h_plan.size());
+  }
+  uint64_t* hp = reinterpret_cast<uint64_t*>(im.h_plan.data());
+  PubList pl{};
+  pl.add(hp, P.d_all, words * 8);
+  pl.add(hp + words, d_n, 8);
+  uint32_t* seq = reinterpret_cast<uint32_t*>(hp + words + 2);
+  pl.seq_dst = seq;
+  pl.seq = ++im.plan_seq;
+  launch_publish(pl, s);
+  // the peers' all-gather normally lands within microseconds: spin briefly,
+  // then wait under the communicator's watchdog (a dead peer aborts, no hang)
+  const double t0 = now_seconds();
+  while (__atomic_load_n(seq, __ATOMIC_ACQUIRE) != im.plan_seq) {
+    if (now_seconds() - t0 > 2e-3) {
+      comm.sync(s);
+      break;
+    }
+    __builtin_ia32_pause();
+  }
+  const bool clean = im.complete_pass(p.text, p.len, p.avail, p.base, p.prev, p.rb, p.blocks, true);
+  P.all.assign(hp, hp + words);
+  plan_finish(P);
+  if (!clean || P.any_flags) return false;  // every rank sees the same flags: all redo
+  im.cols.n = hp[words];
+  WC_CHECK(im.cols.n == P.rank_rows[P.R], "speculative compaction: key count != owner row counts");
+  im.st.keys = im.cols.n;
+  im.st.log2_buckets = t.log2_buckets;
+  merge_cols_owner(im, comm, all_ranks, im.opt.merge_mode == 1, P);
+  return true;
 }
 
 }  // namespace wc

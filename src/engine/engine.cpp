@@ -785,6 +785,12 @@ void Engine::count_source(ChunkSource& src, uint64_t global_base) {
   std::vector<uint8_t> giant;
   auto count_giant = [&](uint64_t base) {
     const uint64_t n = giant.size();
+    // records and hot slots carry 32-bit chunk offsets and word lengths; the
+    // word's bytes must also fit the key arena — fail clearly, before launching
+    WC_CHECK(n <= (1ull << 32) - 2 * (uint64_t)MAP_TILE,
+             "a " + std::to_string(n) + "-byte word exceeds the longest supported word (4 GiB - 64 KiB)");
+    WC_CHECK(n + 8 <= im.opt.arena_bytes, "a " + std::to_string(n) + "-byte word does not fit the " +
+                                              std::to_string(im.opt.arena_bytes) + "-byte key arena (raise arena_bytes)");
     WC_LOG(LOG_INFO, "dev %d: %llu-byte word at %llu exceeds the %llu-byte stream piece: own pass", im.dev,
            (unsigned long long)n, (unsigned long long)base, (unsigned long long)C);
     im.giant_mem.reserve(n + 4096);
@@ -967,10 +973,13 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
   im.fin_end_marked = false;
   bool drained = false;
   if (merged) {
-    im.settle();
-    im.compact_local();
-    im.mark(EV_MERGE0);
-    merge_cols(im, *comm, all_ranks);
+    const bool spec = im.pend.active && im.speculate && !im.sync_debug && merge_cols_speculative(im, *comm, all_ranks);
+    if (!spec) {
+      im.settle();
+      im.compact_local();
+      im.mark(EV_MERGE0);
+      merge_cols(im, *comm, all_ranks);
+    }
     im.mark(EV_MERGE1);
     im.sort_cols_by_first();
   } else if (im.pend.active && im.finalize_local_speculative()) {

@@ -100,6 +100,8 @@ struct Engine::Impl {
   DeviceArena merge_mem; // merge buffers (merged columns live here)
   DeviceArena merge_small;  // merge metadata (count matrices)
   PinnedBuffer h_merge;     // merge host words for async H2D copies (no sync before they go out of scope)
+  PinnedBuffer h_plan;      // speculative merge: gathered owner-count matrix + key count + sequence word
+  uint32_t plan_seq = 0;
   DeviceArena sort_mem;  // first-occurrence sort + sorted columns
   KeyCols cols;        // local (compact) or merged, sorted by first after finalize
   uint8_t* cols_arena = nullptr;   // arena the sref_* of cols point into
@@ -179,5 +181,9 @@ struct Engine::Impl {
 // merged global table — on rank 0, or on every rank if all_ranks (the dense
 // protocol always leaves it on every rank).
 void merge_cols(Engine::Impl& im, Comm& comm, bool all_ranks);
+// The same behind a pending last pass (compaction + owner plan without a
+// settle, one host wait); false: some rank's pass needs recovery — the caller
+// settles, compacts and runs merge_cols (every rank takes the same branch).
+bool merge_cols_speculative(Engine::Impl& im, Comm& comm, bool all_ranks);
 
 }  // namespace wc

@@ -247,8 +247,9 @@ constexpr uint32_t MERGE_MAX_RANKS = 64;
 // V / W x W; the owner path costs one more exchange + host sync (~50 us at one
 // rank, tools/merge_cost.py) — the insert + compact of ~2.5e5 rows.
 constexpr uint64_t MERGE_ROOT_MAX_ROWS = 1ull << 18;
-void launch_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* slen, uint64_t n, uint32_t W,
-                        unsigned long long* counts, hipStream_t s);
+// counts of rows [0, n) — or [0, *dn) with n a bound — and (pass_flags) the pass's recovery flags at 2W + 1
+void launch_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* slen, uint64_t n, const uint64_t* dn,
+                        const uint32_t* pass_flags, uint32_t W, unsigned long long* counts, hipStream_t s);
 void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
                           const uint64_t* soff, const uint32_t* slen, const uint8_t* arena, uint64_t n, uint32_t W,
                           const unsigned long long* counts, unsigned long long* cursor, MRow* rows, uint8_t* bytes,

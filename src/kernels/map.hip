@@ -454,16 +454,19 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   const uint32_t pbase = lane * MAP_BPL;
   uint32_t ndef = 0;  // deferred LONG entries of the current round (list[0, ndef))
 
-  // LONG words of the round (>= 16 bytes or longer than the lane window):
-  // byte-loop keys, one record each; 64 per pass, the unit still in `buf`.
+  // LONG words of the round (>= 16 bytes): keys from LDS windows (16..30
+  // bytes) or an 8-byte SWAR scan (>= 31), one record each; 64 per pass, the
+  // unit still in `buf`.
   auto run_deferred = [&](uint64_t u0) {
     wave_sync();
     for (uint32_t c = 0; c < ndef; c += 64) {
       const bool hv = c + lane < ndef;
-      const uint32_t q = (hv ? list[c + lane] : 0u) & 0x7FFu;
+      const uint32_t e = hv ? list[c + lane] : 0u;
+      const uint32_t q = e & 0x7FFu, n = e >> 11;
       if (hv) {
         uint64_t k0, k1;
-        key_slow(buf, UNIT + HALO, a, q, u0 + q, k0, k1);
+        if (n < MAP_LONG) key_long_known(buf, q, n, a.k1_mask, k0, k1);  // 16..30 bytes: length known
+        else key_long_scan(buf, UNIT + HALO, a, q, u0 + q, k0, k1);
         emit_record(L.bcur, a, rout, place_hash(k0, k1) & bmask, k0, k1, 1, (uint32_t)(u0 + q));
       }
     }

@@ -202,32 +202,50 @@ __device__ __forceinline__ void emit_two(uint32_t* bcur, const MapArgs& a, const
   if (d2) put_record(a, o, b2, p2, s2, y0, y1, 1, o2);
 }
 
-// Key of a token whose length is unknown inside the lane window (MAP_LONG) or
-// >= 16 bytes: byte loop over the LDS text buffer `buf` (buf_len bytes
-// readable), then global memory.  Returns the length.
-__device__ __forceinline__ uint64_t key_slow(const uint8_t* buf, uint32_t buf_len, const MapArgs& a, uint64_t pos,
-                                             uint64_t g, uint64_t& k0, uint64_t& k1) {
-  uint64_t len = 0, h = FNV_OFFSET, chunk = 0, tail = 0;
+// Key of a LONG token (>= 16 bytes) of known length 16..30 from its LDS
+// windows: k0 = the first 8 bytes, then the tail's 8-byte chunks folded
+// (keys.hpp key_of: full chunks, then the zero-padded partial one).  Two
+// window16 reads instead of a byte loop.
+__device__ __forceinline__ void key_long_known(const uint8_t* buf, uint32_t p, uint32_t len, uint64_t k1_mask,
+                                               uint64_t& k0, uint64_t& k1) {
+  uint64_t w0, w1, w2, w3;
+  window16(buf, p, w0, w1);
+  window16(buf, p + 16, w2, w3);
+  k0 = w0;
+  uint64_t h = tail_fold(FNV_OFFSET, w1);
+  auto lo = [](uint64_t x, uint32_t n) { return n >= 8 ? x : (x & ((1ull << (8 * n)) - 1ull)); };
+  if (len > 16) h = tail_fold(h, lo(w2, len - 16));
+  if (len > 24) h = tail_fold(h, lo(w3, len - 24));
+  k1 = long_k1(len, h, k1_mask);
+}
+
+// Key of a token of unknown length (>= 31 bytes): 8 bytes per step with a
+// SWAR delimiter test, from the LDS buffer (buf_len bytes) and then global
+// memory (past avail_len reads as a delimiter).  Returns the length.
+__device__ __forceinline__ uint64_t key_long_scan(const uint8_t* buf, uint32_t buf_len, const MapArgs& a, uint32_t pos,
+                                                  uint64_t g, uint64_t& k0, uint64_t& k1) {
+  uint64_t len = 0, h = FNV_OFFSET, tail = 0;
   k0 = 0;
-  for (;;) {
-    uint32_t c;
-    if (pos < (uint64_t)buf_len) c = buf[pos];
-    else if (g < a.avail_len) c = a.text[g];
-    else break;
-    if (is_delim(c)) break;
-    if (len < 8) {
-      k0 |= (uint64_t)c << (8 * len);
+  for (uint32_t j = 0;; ++j) {
+    uint64_t x;
+    if (pos + len + 16 <= buf_len) {
+      uint64_t y;
+      window16(buf, (uint32_t)(pos + len), x, y);
+    } else if (g + len + 8 <= a.avail_len) {
+      __builtin_memcpy(&x, a.text + g + len, 8);
     } else {
-      chunk |= (uint64_t)c << (8 * (len & 7));
-      if ((len & 7) == 7) {
-        h = tail_fold(h, chunk);
-        chunk = 0;
-      }
+      x = 0;
+      for (int i = 0; i < 8; ++i) x |= (uint64_t)(g + len + i < a.avail_len ? a.text[g + len + i] : 0x20) << (8 * i);
     }
-    ++len, ++pos, ++g;
+    const uint64_t m = delim_mask8(x);
+    const uint32_t r = m ? (uint32_t)__ffsll((unsigned long long)m) - 1u : 8u;  // word bytes in this block
+    const uint64_t part = r == 8 ? x : (x & ((1ull << (8 * r)) - 1ull));
+    if (j == 0) k0 = part;
+    else if (r) h = tail_fold(h, part);
+    if (j == 1) tail = part;
+    len += r;
+    if (r < 8) break;
   }
-  if (len > 8 && len <= KEY_INLINE_MAX) tail = chunk;
-  if (len > 8 && (len & 7)) h = tail_fold(h, chunk);
   k1 = len <= 8 ? len : (len <= KEY_INLINE_MAX ? medium_k1(tail, len) : long_k1(len, h, a.k1_mask));
   return len;
 }

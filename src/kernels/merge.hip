@@ -25,10 +25,23 @@ inline dim3 mgrid(uint64_t n) {
   return dim3((unsigned)(g < 1 ? 1 : (g > 4096 ? 4096 : g)));
 }
 
+// Byte equality of two LONG-word payloads, 8 bytes per compare (unaligned
+// loads), the tail in one masked compare of the bytes that remain.
 __device__ __forceinline__ bool mem_equal(const uint8_t* x, const uint8_t* y, uint64_t len) {
-  for (uint64_t c = 0; c < len; ++c)
-    if (x[c] != y[c]) return false;
-  return true;
+  uint64_t c = 0;
+  for (; c + 8 <= len; c += 8) {
+    uint64_t u, v;
+    __builtin_memcpy(&u, x + c, 8);
+    __builtin_memcpy(&v, y + c, 8);
+    if (u != v) return false;
+  }
+  if (c == len) return true;
+  uint64_t u = 0, v = 0;
+  for (uint64_t i = c; i < len; ++i) {
+    u |= (uint64_t)x[i] << (8 * (i - c));
+    v |= (uint64_t)y[i] << (8 * (i - c));
+  }
+  return u == v;
 }
 
 __global__ void wc_combine_u64(uint64_t* dst, const uint64_t* src, uint64_t n, int op) {
@@ -89,11 +102,19 @@ __device__ __forceinline__ unsigned long long wave_owner_add(unsigned long long*
   return mine;
 }
 
-// counts[2o] += rows owned by o, counts[2o+1] += their long-word bytes.
+// counts[2o] += rows owned by o, counts[2o+1] += their long-word bytes; rows
+// [0, n) or [0, *dn) (device-side count, n the bound); pass_flags (nullable):
+// counts[2W + 1] |= the pass's re-run / table-overflow flags.
 __global__ void __launch_bounds__(256) wc_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* slen,
-                                                      uint64_t n, uint32_t W, unsigned long long* counts) {
+                                                      uint64_t n, const uint64_t* dn, const uint32_t* pass_flags,
+                                                      uint32_t W, unsigned long long* counts) {
   __shared__ unsigned long long h[2 * OWN_MAX];
   for (uint32_t i = threadIdx.x; i < 2 * W; i += blockDim.x) h[i] = 0;
+  if (dn) n = *dn;
+  if (pass_flags && blockIdx.x == 0 && threadIdx.x == 0) {
+    const uint32_t f = pass_flags[FLAG_REGION_OVF] | pass_flags[FLAG_TABLE_OVF] | pass_flags[FLAG_ARENA_OVF];
+    if (f) atomicOr(&counts[2 * W + 1], 1ull);
+  }
   __syncthreads();
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 < n; i0 += stride) {  // whole waves call the wave op
@@ -298,9 +319,11 @@ __global__ void wc_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rb
 
 }  // namespace dev
 
-void launch_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* slen, uint64_t n, uint32_t W,
-                        unsigned long long* counts, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(dev::wc_owner_count, dev::mgrid(n), dim3(256), 0, s, k0, k1, slen, n, W, counts);
+void launch_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* slen, uint64_t n, const uint64_t* dn,
+                        const uint32_t* pass_flags, uint32_t W, unsigned long long* counts, hipStream_t s) {
+  // with a device-side count the grid is sized for the bound (grid-stride inside)
+  hipLaunchKernelGGL(dev::wc_owner_count, dev::mgrid(n ? n : 1), dim3(256), 0, s, k0, k1, slen, n, dn, pass_flags, W,
+                     counts);
 }
 void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
                           const uint64_t* soff, const uint32_t* slen, const uint8_t* arena, uint64_t n, uint32_t W,

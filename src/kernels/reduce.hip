@@ -12,10 +12,12 @@
 //                     with LDS atomics (count +=, first = min), and the slice
 //                     is written back.  LONG words (>= 16 bytes, hashed keys)
 //                     are merged only after a byte comparison with the stored
-//                     copy of the word (exact equality, keys.hpp): found in
-//                     parallel, new ones claimed by one wave in order, their
-//                     bytes copied to the key arena so keys outlive streamed
-//                     chunks.  If a slice overflows it is NOT written back;
+//                     copy of the word (exact equality, keys.hpp), in line with
+//                     every other record: a new LONG word is claimed by the
+//                     first lane that meets it (slot PENDING while its bytes
+//                     are copied to the key arena — keys outlive streamed
+//                     chunks — then published), in parallel across the block.
+//                     If a slice overflows it is NOT written back;
 //                     the host splits the table and re-runs only the
 //                     overflowed buckets.
 //  wc_table_split     B -> 2B buckets (rehash into new slices).
@@ -49,17 +51,14 @@ constexpr int RED_UNROLL = WC_RED_UNROLL;  // 12-byte records in flight per lane
 #define WC_RED_UNROLL_24 2
 #endif
 constexpr int RED_UNROLL_24 = WC_RED_UNROLL_24;  // 24-byte records in flight per lane (VGPR budget)
-constexpr int LONGQ = 2048;  // LONG records queued per bucket pass (more: re-scan in batches)
+constexpr uint32_t SREF_POISON = 0xFFFFFFFFu;  // sref_len of a LONG slot whose bytes did not fit the arena
 
 struct RedLds {
   SlotGroup grp[TAB_GROUPS];  // first: 16-B aligned group reads
   uint64_t cnt[TAB_SLOTS];
   uint64_t first[TAB_SLOTS];
-  uint32_t longq[LONGQ];      // record indices of LONG records, then the unmatched ones
   uint32_t occupied;
   uint32_t overflow;
-  uint32_t nlong, nmiss;
-  uint32_t long_ovf;          // more LONG records than LONGQ: re-scan the 24-byte runs
   uint32_t runcnt[RED_MAX_RUNS];  // packed record counts of this bucket's run in every map block
   unsigned long long st[RED_STAMP_N];  // diagnostic counters (WC_RED_STAMPS builds only)
 };
@@ -132,17 +131,31 @@ __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uin
   if (len - c >= 1) dst[c] = src[c];
 }
 
-__device__ __forceinline__ bool bytes_equal(const uint8_t* x, const uint8_t* y, uint64_t len) {
-  uint64_t c = 0;
+// Is the word at text offset o exactly the arena copy [so, so + len)?  The
+// arena copy is 8-byte aligned (claims round the cursor), so it is read in
+// aligned words and the text in unaligned ones; then the byte after the word
+// must end it (a delimiter or the end of the readable text).
+__device__ __forceinline__ bool long_equal(const ReduceArgs& a, uint64_t o, uint64_t so, uint32_t len) {
+  if (o + len > a.avail_len) return false;
+  const uint64_t* ar = reinterpret_cast<const uint64_t*>(a.arena.bytes + so);
+  uint32_t c = 0;
   for (; c + 8 <= len; c += 8) {
-    uint64_t u, v;
-    __builtin_memcpy(&u, x + c, 8);
-    __builtin_memcpy(&v, y + c, 8);
-    if (u != v) return false;
+    uint64_t u;
+    __builtin_memcpy(&u, a.text + o + c, 8);
+    if (u != ar[c / 8]) return false;
   }
-  for (; c < len; ++c)
-    if (x[c] != y[c]) return false;
-  return true;
+  if (c < len) {
+    uint64_t u = 0;
+    const uint32_t r = len - c;
+    if (o + c + 8 <= a.avail_len) {
+      __builtin_memcpy(&u, a.text + o + c, 8);
+    } else {
+      for (uint32_t i = 0; i < r; ++i) u |= (uint64_t)a.text[o + c + i] << (8 * i);
+    }
+    const uint64_t m = (1ull << (8 * r)) - 1ull;
+    if (((u ^ ar[c / 8]) & m) != 0) return false;
+  }
+  return o + len == a.avail_len || is_delim(a.text[o + len]);
 }
 
 // Count + first offset into slot s.
@@ -167,17 +180,90 @@ __device__ __noinline__ uint32_t merge_slow(RedLds& L, uint32_t ph, uint64_t k0,
   return claimed ? 1u : 0u;
 }
 
+// A LONG record (hashed key): find the slot whose stored word equals the
+// record's word byte for byte, or claim one.  Colliding words (same k0, k1,
+// different bytes) keep separate slots, so the probe continues past a slot
+// whose bytes differ.  A claim keeps the slot PENDING while the claimer copies
+// the word to the key arena and writes the slot's arena reference, then
+// publishes the tag (workgroup release); a reader that matched a published
+// tag acquires before reading the reference and the copy.  Probers that see
+// PENDING re-read the group; the claimer finishes inside its iteration, so the
+// lanes of one wave never wait on each other.  Returns 1 for a claim.
+__device__ __noinline__ uint32_t merge_long(RedLds& L, const ReduceArgs& a, uint32_t b, uint32_t ph, uint64_t k0,
+                                            uint64_t k1, uint64_t cnt, uint64_t first, uint64_t off) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const size_t sbase = (size_t)b * TAB_SLOTS;
+  const uint32_t tag = make_tag(ph);
+  const uint32_t g1 = group_of(ph, TAB_GROUPS), g2 = group2_of(ph, TAB_GROUPS);
+  uint32_t g = g1;
+  int steps = 0;
+  if (WC_RED_STAMPS) atomicAdd(&L.st[RS_SLOW_LANES], 1ull);
+  for (;;) {
+    asm volatile("" ::: "memory");
+    SlotGroup& G = L.grp[g];
+    const u32x4 t = *reinterpret_cast<const u32x4*>(G.tag);
+    const uint32_t tv[4] = {t.x, t.y, t.z, t.w};
+    bool pending = false;
+    int e = -1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (tv[i] == TAG_PENDING) {
+        pending = true;
+      } else if (tv[i] == TAG_EMPTY) {
+        if (e < 0) e = i;
+      } else if (tv[i] == tag && G.k1[i] == k1 && G.k0[i] == k0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const int s = 4 * (int)g + i;
+        const uint32_t sl = a.tab.sref_len[sbase + s];
+        if (sl == SREF_POISON || long_equal(a, off, a.tab.sref_off[sbase + s], sl)) {
+          add_to_slot(L, s, cnt, first);
+          return 0;
+        }
+      }
+    }
+    if (WC_RED_STAMPS) atomicAdd(&L.st[RS_PROBE_ITERS], 1ull);
+    if (pending) continue;  // a claim is being published in this group: look again
+    if (e >= 0) {
+      if (atomicCAS(&G.tag[e], TAG_EMPTY, TAG_PENDING) != TAG_EMPTY) continue;  // lost the race: re-read
+      const int s = 4 * (int)g + e;
+      G.k0[e] = k0;
+      G.k1[e] = k1;
+      const uint64_t len = word_len(a, off);
+      const uint64_t p = atomicAdd(a.arena.cursor, (unsigned long long)((len + 7) & ~7ull));
+      if (p + len > a.arena.cap || len >= SREF_POISON) {
+        atomicOr(&a.flags[FLAG_ARENA_OVF], 1u);  // the job fails; the slot still absorbs its word's records
+        a.tab.sref_off[sbase + s] = 0;
+        a.tab.sref_len[sbase + s] = SREF_POISON;
+      } else {
+        copy_bytes(a.arena.bytes + p, a.text + off, len);
+        a.tab.sref_off[sbase + s] = p;
+        a.tab.sref_len[sbase + s] = (uint32_t)len;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __hip_atomic_store(&G.tag[e], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (WC_RED_STAMPS) atomicAdd(&L.st[RS_CLAIMS], 1ull);
+      add_to_slot(L, s, cnt, first);
+      return 1;
+    }
+    if (++steps >= TAB_MAX_GROUP_PROBES) {
+      L.overflow = 1;
+      return 0;
+    }
+    g = probe_group(g1, g2, (uint32_t)steps, TAB_GROUPS);
+  }
+}
+
 // Records [k, k + U * 64) of one run, three phases so a lane keeps all its
 // records' LDS traffic in flight together: (1) load the records, hash them,
 // read the tags of the first two groups of every record's probe sequence (one
 // LDS round trip for all); (2) read k1 / k0 of the first slot whose tag
 // matches (a second round trip); (3) a key match counts with two LDS atomics.
 // A record with no matching slot in those groups — a new key, a key placed
-// further along its sequence, a tag collision — takes merge_slow.  LONG keys (hashed, 24-byte runs
-// only) are queued for the byte comparison.
+// further along its sequence, a tag collision — takes merge_slow.  LONG keys
+// (hashed, 24-byte runs only) take merge_long (byte comparison).
 template <bool R12, int U, class RecT>
 __device__ __forceinline__ void merge_batch(RedLds& L, const ReduceArgs& a, uint32_t b, const RecT (&rr)[U],
-                                            const bool (&valid)[U], const uint32_t (&idx)[U], uint32_t shift,
+                                            const bool (&valid)[U], uint32_t shift,
                                             uint32_t& claims) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const int lane = threadIdx.x & 63;
@@ -203,12 +289,6 @@ __device__ __forceinline__ void merge_batch(RedLds& L, const ReduceArgs& a, uint
     }
     ph[u] = place_hash(k0[u], key1(u));
     mine[u] = valid[u] && (!shift || bucket_of(ph[u], a.tab.log2_buckets) == b);
-    if (!R12 && mine[u] && key_is_hashed(key1(u))) {
-      const uint32_t q = atomicAdd(&L.nlong, 1u);
-      if (q < (uint32_t)LONGQ) L.longq[q] = idx[u];
-      else L.long_ovf = 1;
-      mine[u] = false;
-    }
     tg[u] = *reinterpret_cast<const u32x4*>(L.grp[group_of(ph[u], TAB_GROUPS)].tag);
     tg2[u] = *reinterpret_cast<const u32x4*>(L.grp[group2_of(ph[u], TAB_GROUPS)].tag);
   }
@@ -255,83 +335,14 @@ __device__ __forceinline__ void merge_batch(RedLds& L, const ReduceArgs& a, uint
       off = (uint32_t)rr[u].co;
     }
     const uint64_t first = a.chunk_base + off;
-    if (slot[u] != 0xFFFFFFFFu && c1[u] == key1(u) && c0[u] == k0[u]) {
+    if (!R12 && key_is_hashed(key1(u))) {
+      claims += merge_long(L, a, b, ph[u], k0[u], key1(u), cnt, first, off);
+    } else if (slot[u] != 0xFFFFFFFFu && c1[u] == key1(u) && c0[u] == k0[u]) {
       if (WC_RED_ABLATE != 3) add_to_slot(L, (int)slot[u], cnt, first);
     } else {
       claims += merge_slow(L, ph[u], k0[u], key1(u), cnt, first);
     }
   }
-}
-
-// LONG records longq[0, n) of bucket b (all threads of the block):
-//  A. every thread looks its record up among the slots holding its key and
-//     compares the word bytes with each slot's arena copy -> count it;
-//  B. the unmatched records are taken IN ORDER by wave 0 (claims are rare:
-//     one per new long word per chunk): look up again (a word claimed
-//     earlier in this phase may match), else claim a slot and copy the bytes
-//     to the arena.  Sequential claims need no publication protocol.
-__device__ void long_batch(RedLds& L, const ReduceArgs& a, uint32_t b, uint32_t n) {
-  const size_t sbase = (size_t)b * TAB_SLOTS;
-  if (threadIdx.x == 0) L.nmiss = 0;
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-    const uint32_t idx = L.longq[i];
-    const Rec r = a.rec.recs[idx];
-    const uint32_t off = (uint32_t)r.co;
-    const uint64_t len = word_len(a, off);
-    const uint32_t ph = place_hash(r.k0, r.k1);
-    int s = -1, cur = -1;
-    while ((s = lds_find_next(L.grp, TAB_GROUPS, ph, r.k0, r.k1, cur)) >= 0) {
-      if (a.tab.sref_len[sbase + s] == len && bytes_equal(a.arena.bytes + a.tab.sref_off[sbase + s], a.text + off, len))
-        break;
-    }
-    if (s >= 0) {
-      atomicAdd(reinterpret_cast<unsigned long long*>(&L.cnt[s]), (unsigned long long)(r.co >> 32));
-      atomicMin(reinterpret_cast<unsigned long long*>(&L.first[s]), (unsigned long long)(a.chunk_base + off));
-    } else {
-      L.longq[atomicAdd(&L.nmiss, 1u)] = idx;  // i-th entry already read: compaction in place is safe
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    const uint32_t m = L.nmiss;
-    for (uint32_t i = 0; i < m; ++i) {
-      if (L.overflow) break;
-      if (threadIdx.x != 0) continue;
-      const Rec r = a.rec.recs[L.longq[i]];
-      const uint32_t off = (uint32_t)r.co;
-      const uint64_t len = word_len(a, off);
-      const uint32_t ph = place_hash(r.k0, r.k1);
-      int s = -1, cur = -1;
-      while ((s = lds_find_next(L.grp, TAB_GROUPS, ph, r.k0, r.k1, cur)) >= 0) {
-        if (a.tab.sref_len[sbase + s] == len &&
-            bytes_equal(a.arena.bytes + a.tab.sref_off[sbase + s], a.text + off, len))
-          break;
-      }
-      if (s < 0) {
-        bool claimed;
-        s = lds_find_or_claim(L.grp, TAB_GROUPS, ph, r.k0, r.k1, TAB_MAX_GROUP_PROBES, claimed, false);
-        if (s < 0 || ++L.occupied > (uint32_t)TAB_MAX_OCC) {
-          L.overflow = 1;
-          continue;
-        }
-        const uint64_t p = atomicAdd(a.arena.cursor, (unsigned long long)len);
-        if (p + len > a.arena.cap) {
-          atomicOr(&a.flags[FLAG_ARENA_OVF], 1u);
-          a.tab.sref_off[sbase + s] = 0;
-          a.tab.sref_len[sbase + s] = 0;
-        } else {
-          copy_bytes(a.arena.bytes + p, a.text + off, len);
-          a.tab.sref_off[sbase + s] = p;
-          a.tab.sref_len[sbase + s] = (uint32_t)len;
-        }
-        __threadfence_block();  // this lane re-reads the copy for later words of the batch
-      }
-      L.cnt[s] += r.co >> 32;
-      L.first[s] = min(L.first[s], a.chunk_base + off);
-    }
-  }
-  __syncthreads();
 }
 
 // One record kind's stream over this wave's runs (map blocks p = wave,
@@ -399,14 +410,14 @@ __device__ __forceinline__ void merge_stream(RedLds& L, const ReduceArgs& a, uin
       locate(T0 + B, ib, vb);
       load(rb2, ib, vb);
     }
-    merge_batch<R12, U>(L, a, b, ra, va, ia, shift, claims);
+    merge_batch<R12, U>(L, a, b, ra, va, shift, claims);
     if (!more) return;
     const bool more2 = T0 + 2 * B < N;
     if (more2) {
       locate(T0 + 2 * B, ia, va);
       load(ra, ia, va);
     }
-    merge_batch<R12, U>(L, a, b, rb2, vb, ib, shift, claims);
+    merge_batch<R12, U>(L, a, b, rb2, vb, shift, claims);
     if (!more2) return;
   }
 }
@@ -425,8 +436,6 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   if (tid == 0) {
     L.occupied = a.tab.occupancy[b];
     L.overflow = 0;
-    L.nlong = 0;
-    L.long_ovf = 0;
   }
   if (WC_RED_STAMPS && tid < RED_STAMP_N) L.st[tid] = 0;
   __syncthreads();
@@ -447,27 +456,6 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
     atomicAdd(&L.st[RS_T_RUNS], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
   __syncthreads();
   if (tid == 0 && L.occupied > (uint32_t)TAB_MAX_OCC) L.overflow = 1;  // too full: split and re-run
-  // LONG words: from the queue, or (queue overflow) by re-scanning the 24-byte runs in batches
-  if (!L.long_ovf) {
-    if (L.nlong) long_batch(L, a, b, L.nlong);
-  } else {
-    for (uint32_t p = 0; p < a.map_blocks; ++p) {
-      const uint32_t n = min(a.rec.count[(size_t)p * nrb + rb] >> 16, (uint32_t)sub);
-      const uint64_t sr = ((uint64_t)p * nrb + rb) * sub;
-      for (uint32_t k0 = 0; k0 < n; k0 += RED_THREADS) {
-        if (tid == 0) L.nlong = 0;
-        __syncthreads();
-        const uint32_t k = k0 + tid;
-        if (k < n) {
-          const Rec r = a.rec.recs[sr + k];
-          if (key_is_hashed(r.k1) && (!shift || bucket_of(place_hash(r.k0, r.k1), a.tab.log2_buckets) == b))
-            L.longq[atomicAdd(&L.nlong, 1u)] = (uint32_t)(sr + k);
-        }
-        __syncthreads();
-        if (L.nlong) long_batch(L, a, b, L.nlong);
-      }
-    }
-  }
   __syncthreads();
   if (L.overflow) {
     if (tid == 0) {

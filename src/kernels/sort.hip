@@ -3,15 +3,19 @@
 //
 // Used for: first-occurrence output order (the reference gets that order for
 // free from its serial append, /root/reference/main.cu:97-104) and the
-// deterministic dictionary union of the cross-GPU merge.
+// sort-based-reduce A/B (tools/sort_vs_hash.py).
 //
-// Per digit pass (<= 11 bits): wc_radix_hist (LDS histogram per 2048-item tile, plus
-// the pass's per-digit totals) -> wc_radix_scan (one block per digit: base of
-// the digit + exclusive scan of its row of tile counts; the v8 single-block
-// scan of the whole digit-major array took 195 us at 1M keys, this ~5 us) ->
-// wc_radix_scatter (stable
-// in-tile ranking with 64-lane ballots: lanes with equal digits are matched
-// with 8 ballots, ranked with popcount, waves combined through LDS).
+// Onesweep form: ONE histogram launch counts the digits of every pass
+// (wc_os_hist: per-block LDS histograms, one global add per digit), then ONE
+// launch per 8-bit digit pass (wc_os_pass).  A pass block takes the next tile
+// of 2048 items from a counter (tiles start in order, so a block only ever
+// waits on tiles already running), ranks its items stably in LDS (64-lane
+// ballots match equal digits), publishes its per-digit tile count, and finds
+// the count of every earlier tile by decoupled look-back: a flag/count word per
+// (tile, digit) that is AGGREGATE (this tile only) or INCLUSIVE (all tiles up to
+// it) — summing aggregates backwards until the first inclusive word.  Items go
+// straight to their final slot of the pass.  A 32-bit key sort is 5 launches
+// (round 2: 12 — histogram, scan and scatter per pass).
 #include <algorithm>
 #include <utility>
 
@@ -22,151 +26,122 @@
 namespace wc {
 namespace dev {
 
-constexpr int RS_THREADS = 256;
-// Tiles of ROUNDS x 256 items per block: 2048 for large sorts, 512 below
-// 2^19 items so a 1e5-key sort still spreads over ~200 blocks (A/B: +1.3 % at
-// 100k words; 2048 wins at 1M).
-constexpr int RS_ROUNDS_BIG = 8, RS_ROUNDS_SMALL = 2;
-constexpr uint64_t RS_SMALL_N = 1ull << 19;
-__host__ __device__ constexpr int rs_rounds(uint64_t n) { return n < RS_SMALL_N ? RS_ROUNDS_SMALL : RS_ROUNDS_BIG; }
-constexpr int RS_WAVES = RS_THREADS / 64;
-#ifndef WC_RS_DB
-#define WC_RS_DB 8
-#endif
-constexpr int RS_MAX_DB = WC_RS_DB;              // digit bits per pass (11-bit digits measured slower: the
-                                                  // per-round LDS work on 2048 bins outweighs one pass fewer)
-constexpr int RS_BINS = 1 << RS_MAX_DB;
+constexpr int OS_THREADS = 256;
+constexpr int OS_WAVES = OS_THREADS / 64;
+constexpr int OS_ROUNDS = 8;
+constexpr uint32_t OS_TILE = OS_THREADS * OS_ROUNDS;  // 2048 items per tile
+constexpr int OS_DB = 8;                              // digit bits per pass
+constexpr int OS_BINS = 1 << OS_DB;
+constexpr int OS_MAX_PASSES = 8;                      // 64-bit keys
+constexpr uint32_t OS_AGG = 1u << 30, OS_INC = 2u << 30, OS_VAL = (1u << 30) - 1u;
 
-// dn (nullable): the item count lives on the device and n is only an upper
-// bound: the tiles in use, ceil(*dn / tile), are spread grid-stride over a
-// grid sized from the host's estimate (hist rows keep the stride nb of n).
-__device__ __forceinline__ uint32_t rs_tiles(uint64_t n, const uint64_t* dn, uint64_t tile) {
-  return (uint32_t)(((dn ? *dn : n) + tile - 1) / tile);
-}
+__host__ __device__ inline uint32_t os_tiles(uint64_t n) { return (uint32_t)((n + OS_TILE - 1) / OS_TILE); }
 
-template <int RS_ROUNDS>
-__global__ void __launch_bounds__(RS_THREADS) wc_radix_hist(const uint64_t* keys, uint64_t n, const uint64_t* dn,
-                                                            int shift, int db, uint32_t* hist, uint32_t nblocks,
-                                                            uint32_t* totals) {
-  __shared__ uint32_t h[RS_BINS];
-  constexpr uint64_t TILE = RS_THREADS * RS_ROUNDS;
-  const uint32_t nd = 1u << db, dmask = nd - 1;
-  const uint32_t ntiles = rs_tiles(n, dn, TILE);
+// Digit counts of all passes: ghist[p * 256 + d] = items whose digit p is d.
+__global__ void __launch_bounds__(OS_THREADS) wc_os_hist(const uint64_t* keys, uint64_t n, const uint64_t* dn,
+                                                         int passes, uint32_t* ghist) {
+  __shared__ uint32_t h[OS_MAX_PASSES][OS_BINS];
+  for (int i = threadIdx.x; i < OS_MAX_PASSES * OS_BINS; i += OS_THREADS) (&h[0][0])[i] = 0;
+  __syncthreads();
   if (dn) n = *dn;
-  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    for (uint32_t d = threadIdx.x; d < nd; d += RS_THREADS) h[d] = 0;
-    __syncthreads();
-    const uint64_t base = (uint64_t)tile * TILE;
-    for (int r = 0; r < RS_ROUNDS; ++r) {
-      const uint64_t i = base + (uint64_t)r * RS_THREADS + threadIdx.x;
-      if (i < n) atomicAdd(&h[(keys[i] >> shift) & dmask], 1u);
-    }
-    __syncthreads();
-    for (uint32_t d = threadIdx.x; d < nd; d += RS_THREADS) {
-      hist[(size_t)d * nblocks + tile] = h[d];
-      if (h[d]) atomicAdd(&totals[d], h[d]);
-    }
-    __syncthreads();  // h is cleared for the next tile
+  for (uint64_t i = blockIdx.x * (uint64_t)OS_THREADS + threadIdx.x; i < n; i += (uint64_t)gridDim.x * OS_THREADS) {
+    const uint64_t k = keys[i];
+    for (int p = 0; p < passes; ++p) atomicAdd(&h[p][(k >> (OS_DB * p)) & (OS_BINS - 1)], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < passes * OS_BINS; i += OS_THREADS) {
+    const uint32_t c = (&h[0][0])[i];
+    if (c) atomicAdd(&ghist[i], c);
   }
 }
 
-// Block d: hist row d (tile counts of digit d, nb words) -> exclusive offsets,
-// starting at the total of all smaller digits.
-__global__ void __launch_bounds__(256) wc_radix_scan(uint32_t* hist, uint32_t stride, const uint32_t* totals,
-                                                     uint64_t n, const uint64_t* dn, uint64_t tile_items) {
-  __shared__ uint32_t wsum[4];
-  const uint32_t d = blockIdx.x;
-  const uint32_t nb = rs_tiles(n, dn, tile_items);  // tiles in use
+// One digit pass.  ghist: this pass's 256 digit totals; ctr: tile counter;
+// look: [tiles][256] flag/count words (zeroed).
+__global__ void __launch_bounds__(OS_THREADS) wc_os_pass(const uint64_t* keys, const uint32_t* vals, uint64_t* okeys,
+                                                         uint32_t* ovals, uint64_t n, const uint64_t* dn, int shift,
+                                                         const uint32_t* ghist, uint32_t* ctr, uint32_t* look) {
+  __shared__ uint32_t cnt[OS_ROUNDS][OS_WAVES][OS_BINS];  // per (round, wave) digit counts, then offsets
+  __shared__ uint32_t base[OS_BINS];                      // first output slot of each digit in this tile
+  __shared__ uint32_t wsum[OS_WAVES];
+  __shared__ uint32_t s_tile;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // base of digit d: sum of totals[0, d)
-  uint32_t x = 0;
-  for (uint32_t t = tid; t < d; t += 256) x += totals[t];
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o);
-  if (lane == 0) wsum[wave] = x;
-  __syncthreads();
-  uint32_t run = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-  __syncthreads();
-  uint32_t* row = hist + (size_t)d * stride;
-  for (uint32_t c = 0; c < nb; c += 1024) {  // 4 consecutive words per thread
-    const uint32_t b = c + 4 * tid;
-    uint32_t v[4], t = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      v[k] = b + k < nb ? row[b + k] : 0u;
-      t += v[k];
-    }
-    uint32_t incl = t;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(incl, o);
-      if (lane >= o) incl += y;
-    }
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    uint32_t pre = run + incl - t, chunk = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      pre += w < wave ? wsum[w] : 0u;
-      chunk += wsum[w];
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (b + k < nb) row[b + k] = pre;
-      pre += v[k];
-    }
-    run += chunk;
-    __syncthreads();  // wsum reused by the next chunk
-  }
-}
-
-template <int RS_ROUNDS>
-__global__ void __launch_bounds__(RS_THREADS) wc_radix_scatter(const uint64_t* keys, const uint32_t* vals,
-                                                               uint64_t* okeys, uint32_t* ovals, uint64_t n,
-                                                               const uint64_t* dn, int shift, int db,
-                                                               const uint32_t* hist, uint32_t nblocks) {
-  __shared__ uint32_t run[RS_BINS];             // next output slot per digit
-  __shared__ uint32_t wcnt[RS_WAVES][RS_BINS];  // per-wave digit counts, then offsets
-  constexpr uint64_t TILE = RS_THREADS * RS_ROUNDS;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t nd = 1u << db, dmask = nd - 1;
-  const uint32_t ntiles = rs_tiles(n, dn, TILE);
   if (dn) n = *dn;
+  const uint32_t ntiles = os_tiles(n);
+  if (tid == 0) s_tile = atomicAdd(ctr, 1u);
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  if (tile >= ntiles) return;  // block-uniform: a grid sized for an upper bound of n
+  for (int i = tid; i < OS_ROUNDS * OS_WAVES * OS_BINS; i += OS_THREADS) (&cnt[0][0][0])[i] = 0;
+  // exclusive scan of the digit totals (thread d owns digit d)
+  const uint32_t tot = ghist[tid];
+  uint32_t incl = tot;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  uint32_t dbase = incl - tot;
+  for (int w = 0; w < wave; ++w) dbase += wsum[w];
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    for (uint32_t d = tid; d < nd; d += RS_THREADS) run[d] = hist[(size_t)d * nblocks + tile];
-    const uint64_t base = (uint64_t)tile * TILE;
-    for (int r = 0; r < RS_ROUNDS; ++r) {
-      for (int w = 0; w < RS_WAVES; ++w)
-        for (uint32_t d = tid; d < nd; d += RS_THREADS) wcnt[w][d] = 0;
-      __syncthreads();
-      const uint64_t i = base + (uint64_t)r * RS_THREADS + tid;
-      const bool valid = i < n;
-      const uint64_t k = valid ? keys[i] : 0;
-      const uint32_t d = (uint32_t)(k >> shift) & dmask;
-      uint64_t peers = __ballot(valid);
-      for (int bit = 0; bit < db; ++bit) {  // lanes with equal digits
-        const uint64_t bb = __ballot((d >> bit) & 1);
-        peers &= ((d >> bit) & 1) ? bb : ~bb;
-      }
-      const uint32_t rank = (uint32_t)__popcll(peers & lt);
-      if (valid && rank == 0) wcnt[wave][d] = (uint32_t)__popcll(peers);
-      __syncthreads();
-      for (uint32_t e = tid; e < nd; e += RS_THREADS) {
-        uint32_t acc = run[e];
-        for (int w = 0; w < RS_WAVES; ++w) {
-          const uint32_t c = wcnt[w][e];
-          wcnt[w][e] = acc;
-          acc += c;
-        }
-        run[e] = acc;
-      }
-      __syncthreads();
-      if (valid) {
-        const uint32_t dst = wcnt[wave][d] + rank;
-        okeys[dst] = k;
-        ovals[dst] = vals[i];
-      }
-      __syncthreads();
+  const uint64_t t0 = (uint64_t)tile * OS_TILE;
+  uint64_t k[OS_ROUNDS];
+  uint32_t v[OS_ROUNDS], rank[OS_ROUNDS];
+#pragma unroll
+  for (int r = 0; r < OS_ROUNDS; ++r) {
+    const uint64_t i = t0 + (uint64_t)r * OS_THREADS + tid;
+    const bool valid = i < n;
+    k[r] = valid ? keys[i] : 0;
+    v[r] = valid ? vals[i] : 0;
+    const uint32_t d = (uint32_t)(k[r] >> shift) & (OS_BINS - 1);
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int bit = 0; bit < OS_DB; ++bit) {  // lanes with equal digits
+      const uint64_t bb = __ballot((d >> bit) & 1);
+      peers &= ((d >> bit) & 1) ? bb : ~bb;
     }
+    rank[r] = valid ? (uint32_t)__popcll(peers & lt) : 0xFFFFFFFFu;
+    if (valid && rank[r] == 0) cnt[r][wave][d] = (uint32_t)__popcll(peers);
+  }
+  __syncthreads();
+  // thread d: offsets of digit d inside the tile in item order (round, wave, lane)
+  uint32_t acc = 0;
+#pragma unroll
+  for (int r = 0; r < OS_ROUNDS; ++r)
+#pragma unroll
+    for (int w = 0; w < OS_WAVES; ++w) {
+      const uint32_t c = cnt[r][w][tid];
+      cnt[r][w][tid] = acc;
+      acc += c;
+    }
+  // decoupled look-back for digit d = tid over the tiles before this one
+  uint32_t* my = look + (size_t)tile * OS_BINS + tid;
+  uint32_t excl = 0;
+  if (tile == 0) {
+    __hip_atomic_store(my, OS_INC | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    __hip_atomic_store(my, OS_AGG | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t t = tile - 1;;) {
+      const uint32_t f = __hip_atomic_load(look + (size_t)t * OS_BINS + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (f == 0) {
+        __builtin_amdgcn_s_sleep(1);
+        continue;  // tile t started earlier (tiles are taken in order) and publishes soon
+      }
+      excl += f & OS_VAL;
+      if (f & OS_INC) break;
+      --t;
+    }
+    __hip_atomic_store(my, OS_INC | (excl + acc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  base[tid] = dbase + excl;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < OS_ROUNDS; ++r) {
+    if (rank[r] == 0xFFFFFFFFu) continue;
+    const uint32_t d = (uint32_t)(k[r] >> shift) & (OS_BINS - 1);
+    const uint32_t dst = base[d] + cnt[r][wave][d] + rank[r];
+    okeys[dst] = k[r];
+    ovals[dst] = v[r];
   }
 }
 
@@ -203,47 +178,36 @@ inline dim3 grid_for(uint64_t n) {
 
 }  // namespace dev
 
-constexpr int RS_MAX_PASSES = 8;  // 64-bit keys
-
-size_t radix_hist_words(uint64_t n, uint64_t n_hint) {
-  const uint64_t tile = (uint64_t)dev::RS_THREADS * dev::rs_rounds(n_hint ? n_hint : n);
-  const uint64_t nb = (n + tile - 1) / tile;
-  return (size_t)dev::RS_BINS * (nb ? nb : 1) + (size_t)dev::RS_BINS * RS_MAX_PASSES;  // tile counts + digit totals
+// Workspace (32-bit words): digit totals [8][256] | tile counters [8] (+ pad)
+// | look-back words [passes][tiles][256] — zeroed by one memset per sort.
+size_t radix_hist_words(uint64_t n, uint64_t /*n_hint*/) {
+  const uint64_t tiles = dev::os_tiles(n ? n : 1);
+  return (size_t)dev::OS_MAX_PASSES * dev::OS_BINS + 64 + (size_t)dev::OS_MAX_PASSES * tiles * dev::OS_BINS;
 }
 
-// 8-bit digits (11-bit ones measured slower: the per-round LDS work on 2048
-// bins outweighs one pass fewer).
 void radix_sort_pairs(uint64_t* keys, uint32_t* vals, uint64_t* tmp_keys, uint32_t* tmp_vals, uint32_t* hist,
                       uint64_t n, int bits, hipStream_t s, bool* in_tmp, const uint64_t* dn, uint64_t n_hint) {
   if (in_tmp) *in_tmp = false;
   if (n <= 1 || bits <= 0) return;
-  const uint64_t est = dn && n_hint ? std::min(n, n_hint) : n;  // expected items (tile size, grid)
-  const bool small = dev::rs_rounds(n_hint ? n_hint : n) == dev::RS_ROUNDS_SMALL;
-  const uint64_t tile = (uint64_t)dev::RS_THREADS * (small ? dev::RS_ROUNDS_SMALL : dev::RS_ROUNDS_BIG);
-  const uint32_t nb = (uint32_t)((n + tile - 1) / tile);  // hist row stride (upper bound)
-  const uint32_t grid = dn ? (uint32_t)std::min<uint64_t>(nb, (est + est / 4 + tile - 1) / tile + 1) : nb;
-  const int passes = (bits + dev::RS_MAX_DB - 1) / dev::RS_MAX_DB;
-  const int db = (bits + passes - 1) / passes;
-  uint32_t* totals = hist + (size_t)dev::RS_BINS * nb;  // [passes][2^db]
-  WC_HIP_CHECK(hipMemsetAsync(totals, 0, (size_t)dev::RS_BINS * passes * sizeof(uint32_t), s));
+  WC_CHECK(n < (1ull << 30), "radix_sort_pairs: at most 2^30 items (look-back counts are 30-bit)");
+  const int passes = std::min((bits + dev::OS_DB - 1) / dev::OS_DB, dev::OS_MAX_PASSES);
+  const uint32_t tiles = dev::os_tiles(n);  // upper bound with a device-side count
+  uint32_t* ghist = hist;
+  uint32_t* ctr = hist + dev::OS_MAX_PASSES * dev::OS_BINS;
+  uint32_t* look = ctr + 64;
+  const size_t zero_words = (size_t)dev::OS_MAX_PASSES * dev::OS_BINS + 64 + (size_t)passes * tiles * dev::OS_BINS;
+  WC_HIP_CHECK(hipMemsetAsync(hist, 0, zero_words * sizeof(uint32_t), s));
+  // histogram grid: ~4 tiles of items per block (est: the expected device-side count)
+  const uint64_t est = dn && n_hint ? std::min(n, n_hint) : n;
+  const uint32_t hgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (est + 4 * dev::OS_TILE - 1) / (4 * dev::OS_TILE)));
+  hipLaunchKernelGGL(dev::wc_os_hist, dim3(hgrid), dim3(dev::OS_THREADS), 0, s, keys, n, dn, passes, ghist);
+  // one block per tile of the bound n (with a device-side count the blocks past it exit at once)
+  const uint32_t grid = tiles;
   uint64_t *ki = keys, *ko = tmp_keys;
   uint32_t *vi = vals, *vo = tmp_vals;
   for (int p = 0; p < passes; ++p) {
-    const int shift = db * p;
-    uint32_t* tot = totals + (size_t)dev::RS_BINS * p;
-    if (small)
-      hipLaunchKernelGGL(dev::wc_radix_hist<dev::RS_ROUNDS_SMALL>, dim3(grid), dim3(dev::RS_THREADS), 0, s, ki, n, dn,
-                         shift, db, hist, nb, tot);
-    else
-      hipLaunchKernelGGL(dev::wc_radix_hist<dev::RS_ROUNDS_BIG>, dim3(grid), dim3(dev::RS_THREADS), 0, s, ki, n, dn,
-                         shift, db, hist, nb, tot);
-    hipLaunchKernelGGL(dev::wc_radix_scan, dim3(1u << db), dim3(256), 0, s, hist, nb, tot, n, dn, tile);
-    if (small)
-      hipLaunchKernelGGL(dev::wc_radix_scatter<dev::RS_ROUNDS_SMALL>, dim3(grid), dim3(dev::RS_THREADS), 0, s, ki, vi,
-                         ko, vo, n, dn, shift, db, hist, nb);
-    else
-      hipLaunchKernelGGL(dev::wc_radix_scatter<dev::RS_ROUNDS_BIG>, dim3(grid), dim3(dev::RS_THREADS), 0, s, ki, vi,
-                         ko, vo, n, dn, shift, db, hist, nb);
+    hipLaunchKernelGGL(dev::wc_os_pass, dim3(grid), dim3(dev::OS_THREADS), 0, s, ki, vi, ko, vo, n, dn, dev::OS_DB * p,
+                       ghist + (size_t)p * dev::OS_BINS, ctr + p, look + (size_t)p * tiles * dev::OS_BINS);
     std::swap(ki, ko);
     std::swap(vi, vo);
   }

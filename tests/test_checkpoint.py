@@ -137,7 +137,7 @@ def test_gpu_bench_json_stages(tmp_path):
     assert r.returncode == 0, r.stderr
     d = json.loads((tmp_path / "b.json").read_text())
     assert d["path"] == "gpu" and d["tokens"] == len(data.split()) and d["chunks"] >= 1
-    assert d["stages_ms"]["map_reduce"] > 0 and d["stages_ms"]["finalize"] > 0
+    assert d["device_ms"]["map"] > 0 and d["device_ms"]["reduce"] > 0 and d["device_ms"]["finalize"] > 0
     assert b"[wc debug" in r.stderr and b"finalize" in r.stderr
 
 

@@ -178,6 +178,27 @@ def test_loopback_merge_many_long_words(ranks, merge_mode):
                     want)
 
 
+@pytest.mark.parametrize("merge_mode", [0, 1])
+@pytest.mark.parametrize("ranks", [1, 3, 8])
+@pytest.mark.parametrize("opts", [dict(), dict(log2_rec_buckets=1, log2_tab_buckets=1),
+                                  dict(min_records=16384, records_per_byte=0.001)])
+def test_loopback_merge_speculative(ranks, merge_mode, opts, monkeypatch):
+    """HBM-resident shards: each rank's last pass stays pending and the merged
+    finalize runs behind it (merge_cols_speculative: compaction + owner plan +
+    all-gather, one host wait).  With a 2-bucket starting table (table splits)
+    or tiny shuffle regions (pass re-runs) ranks flag recovery in the gathered
+    matrix and all of them fall back to the synchronous protocol together."""
+    monkeypatch.setenv("WC_MERGE_ROOT_ROWS", "0")  # the owner exchange
+    rng = np.random.default_rng(70 + ranks)
+    text = random_text(rng, 300_000, alphabet=b"abcdefgh  \n", long_words=6) + ops.synth_host(3 << 20, seed=4,
+                                                                                              vocab=40000)
+    want = ops.cpu_count(text)
+    for all_ranks in (False, True):
+        got = ops.loopback_count(text, ranks, merge_mode=merge_mode, all_ranks=all_ranks, resident=True,
+                                 chunk_bytes=8 << 20, **opts)
+        assert_same(got, want)
+
+
 def test_file_stream(tmp_path):
     rng = np.random.default_rng(21)
     text = random_text(rng, 3_000_000, long_words=10)
@@ -302,7 +323,7 @@ def test_pinned_replay_host_staged():
 @pytest.mark.parametrize("n", [1, 2, 5, 2047, 2048, 2049, 100_003, 1_000_000])
 @pytest.mark.parametrize("bits", [8, 13, 30, 64])
 def test_radix_sort_kernel(n, bits):
-    """Kernel unit test: wc_radix_hist / wc_radix_scan / wc_radix_scatter against
+    """Kernel unit test: onesweep wc_os_hist / wc_os_pass (decoupled look-back) against
     numpy's stable argsort (many equal keys, so stability is checked too)."""
     import ctypes
 

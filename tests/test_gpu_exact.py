@@ -153,3 +153,55 @@ def test_host_pool_replay_matches_oracle():
         got = e.result()
     pool.close()
     assert compare_results(got, synthetic_oracle(1, total, 3, 20000, 1.0, pool_bytes=pool_b, chunk=chunk)) == ""
+
+
+@pytest.mark.parametrize("chunk", [128 << 20, 32 << 20])
+def test_long_words_under_load(chunk):
+    """30 % of the vocabulary 16..64-byte words (hashed keys, byte-verified in the
+    reduce), 1M-word Zipf vocabulary, one pass and four: key for key vs the
+    generator-walk oracle."""
+    n = 128 << 20
+    with ops.Engine(device=0, chunk_bytes=chunk) as e:
+        e.synth_device(n, first_segment=0, seed=3, vocab=1_000_000, zipf_s=1.0, long_frac=0.3)
+        e.count_resident(n)
+        got = e.result()
+    want = ops.cpu_count_synth(n, 0, 3, 1_000_000, 1.0, 0, 16, 0.3)
+    long_tokens = sum(int(c) for w, c in zip(want.words, want.counts) if len(w) >= 16)
+    assert long_tokens > 0.2 * want.total
+    assert_same(got, want)
+
+
+def test_many_new_long_words_per_bucket():
+    """More than 2048 distinct new LONG words per table bucket in one pass
+    (the round-2 reducer queued at most 2048 per bucket and re-scanned beyond):
+    every one is claimed in parallel and byte-verified."""
+    n = 192 << 20
+    with ops.Engine(device=0, chunk_bytes=n) as e:
+        e.synth_device(n, first_segment=0, seed=8, vocab=3_000_000, zipf_s=0.6, long_frac=0.7)
+        e.count_resident(n)
+        got = e.result()
+        buckets = 1 << e.stats()["log2_buckets"]
+    want = ops.cpu_count_synth(n, 0, 8, 3_000_000, 0.6, 0, 16, 0.7)
+    distinct_long = sum(1 for w in want.words if len(w) >= 16)
+    assert distinct_long > 2048 * 256, distinct_long
+    assert distinct_long / buckets > 256
+    assert_same(got, want)
+
+
+def test_synth_while_pass_pending():
+    """count_resident leaves its last pass pending; regenerating the resident
+    text before the result must not let a recovery of that pass (overflowing
+    options: table splits / shuffle re-runs) read the new text (advisor)."""
+    from cuda_mapreduce_amd.utils import merge_results
+
+    for opts in (dict(log2_tab_buckets=1, chunk_bytes=8 << 20),
+                 dict(min_records=16384, records_per_byte=0.001, chunk_bytes=1 << 20)):
+        with ops.Engine(device=0, **opts) as e:
+            e.synth_device(24 << 20, seed=5, vocab=50_000)
+            e.count_resident(24 << 20)
+            e.synth_device(24 << 20, seed=6, vocab=70_000)
+            e.count_resident(24 << 20, global_base=24 << 20)  # B follows A in one logical stream
+            got = e.result()
+        want = merge_results([ops.cpu_count_synth(24 << 20, 0, 5, 50_000, 1.0, 0, 16),
+                              ops.cpu_count_synth(24 << 20, 0, 6, 70_000, 1.0, 24 << 20, 16)])
+        assert_same(got, want)

@@ -1,6 +1,7 @@
 """Multi-process data-parallel word count on CPU (gloo, world_size 2, 3 and 8):
-shard ownership + the merge protocol (reduce-scatter / all-gather) must give
-exactly the single-process result."""
+shard ownership + the owner-partitioned merge protocols of src/dist/merge.cpp
+(shuffle: all-to-all to hash owners; dense: owner-numbered dictionary +
+reduce-scatter / all-gather) must give exactly the single-process result."""
 import os
 import socket
 import sys
@@ -19,7 +20,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, path, q, ckpt=""):
+def _worker(rank, world, port, path, q, ckpt="", dense=False):
     sys.path.insert(0, ROOT)
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -28,15 +29,16 @@ def _worker(rank, world, port, path, q, ckpt=""):
     from cuda_mapreduce_amd.parallel import DistributedWordCount, init_from_env
 
     env = init_from_env("gloo")
-    job = DistributedWordCount(env, use_gpu=False)
+    job = DistributedWordCount(env, use_gpu=False, merge_mode=1 if dense else 0)
     res = job.count_file(path, checkpoint=ckpt, interval=20000) if ckpt else job.count_file(path)
     q.put((rank, res.words, [int(c) for c in res.counts], [int(f) for f in res.first_off], res.total))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,ckpt", [(2, False), (3, False), (8, False), (2, True)])
-def test_gloo_data_parallel_matches_single(tmp_path, world, ckpt):
+@pytest.mark.parametrize("world,ckpt,dense", [(2, False, False), (3, False, True), (8, False, False),
+                                              (8, False, True), (2, True, False)])
+def test_gloo_data_parallel_matches_single(tmp_path, world, ckpt, dense):
     from cuda_mapreduce_amd.ops import cpu_count, synth_host
 
     text = synth_host(300_000, seed=5, vocab=4000) + b"tail-without-newline"
@@ -46,7 +48,7 @@ def test_gloo_data_parallel_matches_single(tmp_path, world, ckpt):
     q = ctx.Queue()
     port = _free_port()
     ck = str(tmp_path / "ck") if ckpt else ""
-    procs = [ctx.Process(target=_worker, args=(r, world, port, str(p), q, ck)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, str(p), q, ck, dense)) for r in range(world)]
     for pr in procs:
         pr.start()
     outs = [q.get(timeout=120) for _ in range(world)]

@@ -18,7 +18,7 @@ EOF
 run() {  # name, args...
   local name=$1; shift
   timeout -k 10 180 ./wordcount $F --no-echo --no-list --bench-json /tmp/b.json "$@" > /tmp/w.out || return 1
-  python3 -c "import json,sys; d=json.load(open('/tmp/b.json')); print('%-34s %7.2f GB/s  %.3f s (map+reduce %.0f ms, finalize %.0f ms, %d chunks)  tokens %d keys %d  total=%s' % (sys.argv[1], d['gb_per_s'], d['seconds'], d['stages_ms']['map_reduce'], d['stages_ms']['finalize'], d['chunks'], d['tokens'], d['keys'], open('/tmp/w.out').read().split('Total Count:')[1].strip()))" "$name" >> $OUT
+  python3 -c "import json,sys; d=json.load(open('/tmp/b.json')); print('%-34s %7.2f GB/s  %.3f s (map+reduce %.0f ms, finalize %.0f ms, %d chunks)  tokens %d keys %d  total=%s' % (sys.argv[1], d['gb_per_s'], d['seconds'], d['device_ms']['map'] + d['device_ms']['reduce'], d['device_ms']['finalize'], d['chunks'], d['tokens'], d['keys'], open('/tmp/w.out').read().split('Total Count:')[1].strip()))" "$name" >> $OUT
 }
 WC_IO_THREADS=1 run "plain, 1 read thread" && \
 run "plain (file -> pinned ring)" && \

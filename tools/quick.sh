@@ -8,6 +8,6 @@ for v in 100000 500 1000000; do
   timeout -k 10 120 python bench.py --vocab $v > gpurun_out/q_bench_$v.json 2> gpurun_out/q_bench_$v.err || { tail -5 gpurun_out/q_bench_$v.err; exit 1; }
   python3 -c "
 import json; d=json.loads(open('gpurun_out/q_bench_$v.json').read()); st=d['stages']
-print('vocab $v:', d['value'],'GB/s', d['ms_per_step'],'ms  mr',st['map_reduce_ms'],'fin',st['finalize_ms'],'records',st['records'],'valid',d['validated'])"
+print('vocab $v:', d['value'],'GB/s', d['ms_per_step'],'ms  device',st['device_ms'],'records',st['records'],'valid',d['validated'])"
 done
 WC_MAP_STAMPS=1 timeout -k 10 120 python bench.py --steps 3 --warmup 1 2>&1 | grep "phase clock"
