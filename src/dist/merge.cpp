@@ -115,10 +115,12 @@ void merge_to_root(Engine::Impl& im, Comm& comm, const std::vector<uint64_t>& ra
                        s);
     launch_mrow_compact(recv_rows, state, tcnt, tfirst, T, d_base, d_base + W + 1, (uint32_t)W, merged, d_m, nullptr,
                         s);
-    unsigned long long G = 0;
-    WC_HIP_CHECK(hipMemcpyAsync(&G, d_m, 8, hipMemcpyDeviceToHost, s));
-    comm.sync(s);
+    // no host round trip: columns sized for the rows received (a bound of the
+    // merged count), which stays on the device (KeyCols::dn) through the
+    // first-occurrence sort; the finalize's last wait publishes it
+    const uint64_t G = rr;
     o.n = G;
+    o.dn = d_m;
     o.k0 = take_aligned<uint64_t>(A, G);
     o.k1 = take_aligned<uint64_t>(A, G);
     o.cnt = take_aligned<uint64_t>(A, G);
@@ -128,7 +130,8 @@ void merge_to_root(Engine::Impl& im, Comm& comm, const std::vector<uint64_t>& ra
     uint64_t* d_gbase = d_base + nbase;  // one group: row base 0 .. G, byte base 0
     gb[1] = G;
     WC_HIP_CHECK(hipMemcpyAsync(d_gbase, gb, 4 * 8, hipMemcpyHostToDevice, s));
-    launch_mrow_to_cols(merged, G, d_gbase, d_gbase + 2, 1u, o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len, s);
+    launch_mrow_to_cols(merged, G, d_gbase, d_gbase + 2, 1u, o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len, s,
+                        reinterpret_cast<const uint64_t*>(d_m));
   }
   im.cols = o;  // still in flight: finalize waits under the comm watchdog
   im.cols_arena = recv_bytes;

@@ -64,6 +64,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   if (const char* e = std::getenv("WC_NO_SPECULATE")) speculate = std::atoi(e) == 0;
   if (const char* e = std::getenv("WC_SPIN_WAIT")) spin_wait = std::atoi(e) != 0;
   if (const char* e = std::getenv("WC_STAGE_EVENTS")) stage_events = std::atoi(e) != 0;
+  if (const char* e = std::getenv("WC_HOT_RESAMPLE_EVERY")) hot_resample_every = (uint32_t)std::atoi(e);
   k1_mask = k1_hash_mask(opt.k1_hash_bits);
   if (const char* e = std::getenv("WC_MAP_STAMPS"); e && std::atoi(e)) {
     WC_HIP_CHECK(hipMalloc(&d_stamps, MAP_STAMP_N * 8));
@@ -237,9 +238,14 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   mark(EV_PASS);
   // one zeroing launch: pass counters, sampling state and, after a reset, the
   // table occupancy and the key-arena cursor
+  // reuse the job's hot-table image while it keeps its hit rate (the previous
+  // pass's miss share vs that of the pass that sampled it)
+  const bool sample = !hot_valid || hot_resample_every == 0 || hot_age >= hot_resample_every ||
+                      hot_miss_last > hot_miss_ref * hot_resample_slack;
+  pass_sampled = sample;
   ZeroList z{};
   z.add(d_ctr, sizeof(DevCounters));
-  z.add(hot.fp, hot_clear_bytes);
+  if (sample) z.add(hot.fp, hot_clear_bytes);
   if (reset_pending) {
     z.add(table().occupancy, ((size_t)1 << table().log2_buckets) * 4);
     z.add(d_arena_cursor, sizeof(unsigned long long));
@@ -252,7 +258,7 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   WC_CHECK(pass_rec.subcap > 0, "shuffle record capacity below one record per (map block, bucket)");
   MapArgs m{text, len, avail, prev, log2_rb, pass_rec, d_ctr->flags, &d_ctr->tokens, k1_mask, d_stamps, d_blk};
   if (d_stamps) blocks_stamped += blocks;
-  launch_map(m, hot, blocks, s);
+  launch_map(m, hot, blocks, s, sample);
   mark(EV_MAP);
   if (sync_debug) {  // WC_SYNC_DEBUG: attribute a device fault to a kernel and a chunk
     const hipError_t e = hipStreamSynchronize(s);
@@ -438,6 +444,16 @@ bool Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
   }
   const uint64_t tokens = c.tokens;
   st.records += c.records;
+  {  // hot-table reuse bookkeeping (see launch_pass)
+    const double miss = tokens ? (double)c.records / (double)tokens : 0.0;
+    if (pass_sampled) {
+      hot_valid = true;
+      hot_miss_ref = miss;
+      hot_age = 0;
+    }
+    hot_miss_last = miss;
+    ++hot_age;
+  }
   uint32_t max_occ = c.flags[FLAG_MAX_OCC];
   const bool clean = !c.flags[FLAG_TABLE_OVF];
   while (c.flags[FLAG_TABLE_OVF]) {
@@ -654,10 +670,13 @@ void Engine::Impl::sort_cols_by_first() {
   launch_iota_u32(vals, n, s);
   int bits = 1;
   while (bits < 64 && (max_end >> bits) != 0) ++bits;
+  // cols.dn: the count is on the device (n its bound) — sort and gather on it
+  const uint64_t* dn = reinterpret_cast<const uint64_t*>(cols.dn);
   bool in_tmp = false;
-  radix_sort_pairs(keys, vals, tkeys, tvals, hist, n, bits, s, &in_tmp);
+  radix_sort_pairs(keys, vals, tkeys, tvals, hist, n, bits, s, &in_tmp, dn, dn ? n : 0);
   launch_gather_cols(cols.k0, cols.k1, cols.cnt, cols.first, cols.sref_off, cols.sref_len, in_tmp ? tvals : vals, o.k0,
-                     o.k1, o.cnt, o.first, o.sref_off, o.sref_len, n, s);
+                     o.k1, o.cnt, o.first, o.sref_off, o.sref_len, n, s, dn);
+  o.dn = cols.dn;
   cols = o;
 }
 
@@ -720,6 +739,7 @@ void Engine::reset() {
   im.st = Stats{};
   im.max_end = 0;
   im.ev_n = 0;
+  im.hot_valid = false;  // each job samples its own hot words
 }
 
 void Engine::count_device(const uint8_t* d_text, uint64_t n, uint64_t avail, uint64_t global_base, int prev_byte) {
@@ -990,9 +1010,22 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
     im.finalize_local_sorted();  // sort (first, slot) pairs, gather the columns from the table once
   }
   if (!im.fin_end_marked) im.mark(EV_FIN_END);
+  if (im.cols.dn) {  // the merged count is still on the device: publish it with the last wait
+    if (im.h_fin.size() < 64) im.h_fin = PinnedBuffer(64);
+    PubList pc{};
+    pc.add(im.h_fin.data(), im.cols.dn, 8);
+    launch_publish(pc, im.s);
+  }
   // the merge's last collectives are still in flight: wait under the comm watchdog
   if (merged) comm->sync(im.s);
   else if (!drained) WC_HIP_CHECK(hipStreamSynchronize(im.s));
+  if (im.cols.dn) {
+    uint64_t g = 0;
+    std::memcpy(&g, im.h_fin.data(), 8);
+    WC_CHECK(g <= im.cols.n, "merged key count exceeds its bound");
+    im.cols.n = g;
+    im.cols.dn = nullptr;
+  }
   im.st.host_finalize_ms += (now_seconds() - t0) * 1e3;
   WC_LOG(LOG_INFO, "dev %d: finalize %.3f ms (host), %llu keys, %u chunk(s), %llu records, %u re-run(s)", im.dev,
          (now_seconds() - t0) * 1e3, (unsigned long long)im.cols.n, im.st.chunks, (unsigned long long)im.st.records,

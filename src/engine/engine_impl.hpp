@@ -36,6 +36,9 @@ struct KeyCols {
   uint64_t *k0 = nullptr, *k1 = nullptr, *cnt = nullptr, *first = nullptr, *sref_off = nullptr;
   uint32_t* sref_len = nullptr;
   uint64_t n = 0;
+  // non-null: the row count lives on the device (n is its bound) until the
+  // finalize's last wait publishes it (the merge's rank-0 gather: no host round trip)
+  unsigned long long* dn = nullptr;
 };
 
 struct Engine::Impl {
@@ -68,7 +71,17 @@ struct Engine::Impl {
   // hot-key sampling workspace of the map (HotArgs)
   DeviceArena hot_mem;
   HotArgs hot{};
-  size_t hot_clear_bytes = 0;  // fp, cnt, image, selection state: zeroed before every map pass
+  size_t hot_clear_bytes = 0;  // fp, cnt, image, selection state: zeroed before every sampling pass
+  // Hot-table reuse inside a job (never across jobs: reset() drops it): a pass
+  // keeps the image its job's last sampling pass built while its miss share
+  // (records / tokens) stays within hot_resample_slack of that pass's, and
+  // samples again every hot_resample_every passes (WC_HOT_RESAMPLE_EVERY, 0 =
+  // sample every pass).
+  bool hot_valid = false;
+  double hot_miss_ref = 0, hot_miss_last = 0;
+  uint32_t hot_age = 0, hot_resample_every = 16;
+  double hot_resample_slack = 1.15;
+  bool pass_sampled = false;  // the pass in flight built its own image
 
   // key arena (bytes of LONG words, >= 16 bytes)
   uint8_t* d_arena = nullptr;
@@ -101,6 +114,7 @@ struct Engine::Impl {
   DeviceArena merge_small;  // merge metadata (count matrices)
   PinnedBuffer h_merge;     // merge host words for async H2D copies (no sync before they go out of scope)
   PinnedBuffer h_plan;      // speculative merge: gathered owner-count matrix + key count + sequence word
+  PinnedBuffer h_fin;       // the merged key count (KeyCols::dn) published before the finalize's last wait
   uint32_t plan_seq = 0;
   DeviceArena sort_mem;  // first-occurrence sort + sorted columns
   KeyCols cols;        // local (compact) or merged, sorted by first after finalize

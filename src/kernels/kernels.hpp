@@ -163,8 +163,9 @@ struct SynthVocab {
 };
 
 // ---- launchers (all stream-ordered, no host sync) ----------------------------
-// wc_hot_sample + wc_hot_hist/_threshold/_place + wc_map (HotArgs zeroed first: hot_clear).
-void launch_map(const MapArgs& a, const HotArgs& h, uint32_t map_blocks, hipStream_t s);
+// wc_hot_sample + wc_hot_hist/_threshold/_place + wc_map (HotArgs zeroed first: hot_clear);
+// sample = false: wc_map alone, on the hot-table image an earlier pass of the job built.
+void launch_map(const MapArgs& a, const HotArgs& h, uint32_t map_blocks, hipStream_t s, bool sample = true);
 void launch_reduce(const ReduceArgs& a, hipStream_t s);
 void launch_table_split(const TableView& src, const TableView& dst, hipStream_t s);
 void launch_table_clear(const TableView& t, hipStream_t s);
@@ -197,7 +198,8 @@ void launch_bucket_offsets(const uint32_t* occupancy, uint32_t nb, uint64_t* buc
 // out[i] = in[perm[i]] for the six key-table columns (one launch).
 void launch_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
                         const uint64_t* soff, const uint32_t* slen, const uint32_t* perm, uint64_t* ok0, uint64_t* ok1,
-                        uint64_t* ocnt, uint64_t* ofirst, uint64_t* osoff, uint32_t* oslen, uint64_t n, hipStream_t s);
+                        uint64_t* ocnt, uint64_t* ofirst, uint64_t* osoff, uint32_t* oslen, uint64_t n, hipStream_t s,
+                        const uint64_t* dn = nullptr);
 void launch_iota_u32(uint32_t* v, uint64_t n, hipStream_t s);
 
 // util.hip: zero several device regions / copy several small device regions
@@ -262,7 +264,7 @@ void launch_mrow_compact(const MRow* rows, const uint32_t* state, const unsigned
                          uint32_t W, MRow* out, unsigned long long* out_n, uint32_t* slot_id, hipStream_t s);  // nullable
 void launch_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rbase, const uint64_t* bbase, uint32_t W,
                          uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first, uint64_t* soff, uint32_t* slen,
-                         hipStream_t s);
+                         hipStream_t s, const uint64_t* dn = nullptr);  // dn: device-side row count (n a bound)
 void launch_combine_u64(uint64_t* dst, const uint64_t* src, uint64_t n, int op, hipStream_t s);  // 0 sum 1 min 2 max
 void launch_row_ids(const uint32_t* row_slot, const uint32_t* slot_id, uint64_t R, uint64_t id_base, uint32_t* ids,
                     hipStream_t s);

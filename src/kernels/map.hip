@@ -470,7 +470,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
         emit_record(L.bcur, a, rout, place_hash(k0, k1) & bmask, k0, k1, 1, (uint32_t)(u0 + q));
       }
     }
-    my_direct += ndef;
+    if (ST) my_direct += ndef;
     ndef = 0;
     wave_sync();
   };
@@ -493,127 +493,215 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     uint64_t dm;
     uint32_t bits;
     unit_masks(c0, c1, hb, pv, u0, pbase, a.chunk_len, dm, bits);
-    const uint32_t ntok = __popc(bits);
-    my_tokens += ntok;
-    uint32_t wave_total;
-    uint32_t k = wave_excl_small(ntok, wave_total);
-    wave_total = __builtin_amdgcn_readfirstlane(wave_total);
+    my_tokens += __popc(bits);
+    const uint32_t dlo = (uint32_t)dm, dhi = (uint32_t)(dm >> 32);
+    // delimiter bits from the token start on (i < 32: one funnel shift); none
+    // within 31 bytes -> MAP_LONG: ffbl of 0 is all ones, and the u16 entry
+    // keeps 5 length bits, so (ffbl << 11) needs no clamp
+    static_assert(MAP_LONG == 31, "list entries: 11 position bits + 5 length bits");
+    // One step: two list entries [j, hi) per lane, both probed in one LDS round
+    // trip; a tail of <= 64 entries takes the one-entry step.  General form:
+    // any length (two-word signatures are confirmed by the slot's side word,
+    // LONG words deferred to the round end).
+    auto step = [&](uint32_t j, uint32_t hi, auto two_c) {
+      constexpr bool TWO = decltype(two_c)::value;
+      const bool h1 = j + lane < hi, h2 = TWO && j + 64 + lane < hi;
+      const uint32_t e1 = h1 ? list[j + lane] : 0u, e2 = h2 ? list[j + 64 + lane] : 0u;
+      const uint32_t q1 = e1 & 0x7FFu, q2 = e2 & 0x7FFu, n1 = e1 >> 11, n2 = e2 >> 11;
+      uint64_t w10, w11, w20 = 0, w21 = 0;
+      window16(buf, q1, w10, w11);
+      if (TWO) window16(buf, q2, w20, w21);
+      if (WC_MAP_ABLATE == 1) {
+        sink ^= w10 ^ w21;
+        return;
+      }
+      const bool in1 = h1 && n1 <= KEY_INLINE_MAX, in2 = h2 && n2 <= KEY_INLINE_MAX;
+      uint64_t a0, a1, as, b0 = 0, b1 = 0, bs = 0;
+      inline_key(w10, w11, n1, a0, a1, as);
+      if (TWO) inline_key(w20, w21, n2, b0, b1, bs);
+      const uint32_t ha = place_hash(a0, a1), hb = TWO ? place_hash(b0, b1) : 0u;
+      uint32_t ga1, ga2, gb1 = 0, gb2 = 0;
+      hot_groups(ha, ga1, ga2);
+      if (TWO) hot_groups(hb, gb1, gb2);
+      clk.lap(MS_KEYS);
+      if (WC_MAP_ABLATE == 2) {
+        sink ^= as ^ bs ^ ga2 ^ gb2;
+        return;
+      }
+      const u64x2* S = reinterpret_cast<const u64x2*>(L.sig);
+      int s1 = -1, s2 = -1;
+      if constexpr (GS == 2) {  // S[g]: both slots of group g
+        const u64x2 xa0 = S[ga1], xa1 = S[ga2];
+        if (TWO) {
+          const u64x2 xb0 = S[gb1], xb1 = S[gb2];
+          const int mb = in2 ? sig_match4(xb0, xb1, bs) : -1;
+          s2 = mb < 0 ? -1 : (int)slot_of(mb < GS ? gb1 : gb2, mb & (GS - 1));
+        }
+        const int ma = in1 ? sig_match4(xa0, xa1, as) : -1;
+        s1 = ma < 0 ? -1 : (int)slot_of(ma < GS ? ga1 : ga2, ma & (GS - 1));
+      } else {  // S[g]: slots 0-1, S[NG + g]: slots 2-3
+        const u64x2 xa0 = S[ga1], xa1 = S[NG + ga1], xa2 = S[ga2], xa3 = S[NG + ga2];
+        if (TWO) {
+          const u64x2 xb0 = S[gb1], xb1 = S[NG + gb1], xb2 = S[gb2], xb3 = S[NG + gb2];
+          const int mb = in2 ? sig_match8(xb0, xb1, xb2, xb3, bs) : -1;
+          s2 = mb < 0 ? -1 : (int)slot_of(mb < GS ? gb1 : gb2, mb & (GS - 1));
+        }
+        const int ma = in1 ? sig_match8(xa0, xa1, xa2, xa3, as) : -1;
+        s1 = ma < 0 ? -1 : (int)slot_of(ma < GS ? ga1 : ga2, ma & (GS - 1));
+      }
+      // two-word keys: the matching slot's side word decides
+      const bool ta = two_word(as), tb = TWO && two_word(bs);
+      const uint64_t ca = s1 >= 0 && ta ? L.side[s1] : a0, cb = s2 >= 0 && tb ? L.side[s2] : b0;
+      if (ca != a0) s1 = -1;
+      if (cb != b0) s2 = -1;
+      clk.lap(MS_PROBE);
+      const uint32_t o1 = (uint32_t)(u0 + q1), o2 = (uint32_t)(u0 + q2);
+      if (s1 >= 0) {
+        atomicAdd(&L.cnt[s1], 1u);  // results unused: no-return ds_add / ds_min
+        atomicMin(&L.off[s1], o1);
+      }
+      if (TWO && s2 >= 0) {
+        atomicAdd(&L.cnt[s2], 1u);
+        atomicMin(&L.off[s2], o2);
+      }
+      if (WC_MAP_ABLATE == 3) return;
+      // misses of inline words become records now; LONG words wait for the round end
+      const bool d1 = in1 && s1 < 0, d2 = TWO && in2 && s2 < 0;
+      emit_two(L.bcur, a, rout, d1, ha & bmask, a0, a1, o1, n1, d2, hb & bmask, b0, b1, o2, n2);
+      const bool f1 = h1 && !in1, f2 = TWO && h2 && !in2;
+      const uint64_t mf1 = __ballot(f1), mf2 = TWO ? __ballot(f2) : 0ull;
+      if (mf1 | mf2) {  // entries before j are consumed: ndef <= j
+        const uint32_t r1 =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(mf1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mf1, 0u));
+        const uint32_t r2 =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(mf2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mf2, 0u));
+        const uint32_t n1c = (uint32_t)__popcll(mf1);
+        if (f1) list[ndef + r1] = (uint16_t)e1;
+        if (f2) list[ndef + n1c + r2] = (uint16_t)e2;
+        ndef += n1c + (uint32_t)__popcll(mf2);
+      }
+      if constexpr (ST) {
+        my_direct += (uint32_t)(__popcll(__ballot(d1)) + (TWO ? __popcll(__ballot(d2)) : 0));
+        const uint32_t nh = (uint32_t)(__popcll(__ballot(s1 >= 0)) + __popcll(__ballot(s2 >= 0)));
+        if (lane == 0) {
+          atomicAdd(&st_acc[MS_N_HIT], (unsigned long long)nh);
+          atomicAdd(&st_acc[MS_N_DEFER], (unsigned long long)__popcll(mf1 | mf2));
+        }
+      }
+      clk.lap(MS_EMIT);
+    };
+    // Short step: entries of words of <= 7 bytes only — the signature IS the
+    // key (bytes | len << 56): one 8-byte window (three LDS dwords, two
+    // funnels), no tail, no side-word confirmation, and every miss a 12-byte
+    // record candidate.  3 of 4 tokens of English-like text take it.
+    auto step_short = [&](uint32_t j, uint32_t hi, auto two_c) {
+      constexpr bool TWO = decltype(two_c)::value;
+      const bool h1 = j + lane < hi, h2 = TWO && j + 64 + lane < hi;
+      const uint32_t e1 = h1 ? list[j + lane] : 0u, e2 = h2 ? list[j + 64 + lane] : 0u;
+      const uint32_t q1 = e1 & 0x7FFu, q2 = e2 & 0x7FFu, n1 = e1 >> 11, n2 = e2 >> 11;
+      const uint64_t w1 = window8(buf, q1), w2 = TWO ? window8(buf, q2) : 0ull;
+      // k0: the first n bytes (n <= 7: shift by 64 - 8 n in [8, 56]; n = 0 of an empty lane clamps to 1)
+      const uint32_t sa = 64u - 8u * max(n1, 1u), sb = 64u - 8u * max(n2, 1u);
+      const uint64_t a0 = (w1 << sa) >> sa, b0 = TWO ? (w2 << sb) >> sb : 0ull;
+      const uint64_t as = a0 | ((uint64_t)n1 << 56), bs = b0 | ((uint64_t)n2 << 56);
+      const uint32_t ha = place_hash(a0, n1), hb = TWO ? place_hash(b0, n2) : 0u;
+      uint32_t ga1, ga2, gb1 = 0, gb2 = 0;
+      hot_groups(ha, ga1, ga2);
+      if (TWO) hot_groups(hb, gb1, gb2);
+      clk.lap(MS_KEYS);
+      static_assert(GS == 2, "short step: 2-slot groups");
+      const u64x2* S = reinterpret_cast<const u64x2*>(L.sig);
+      int s1 = -1, s2 = -1;
+      {
+        const u64x2 xa0 = S[ga1], xa1 = S[ga2];
+        if (TWO) {
+          const u64x2 xb0 = S[gb1], xb1 = S[gb2];
+          const int mb = h2 ? sig_match4(xb0, xb1, bs) : -1;
+          s2 = mb < 0 ? -1 : (int)slot_of(mb < GS ? gb1 : gb2, mb & (GS - 1));
+        }
+        const int ma = h1 ? sig_match4(xa0, xa1, as) : -1;
+        s1 = ma < 0 ? -1 : (int)slot_of(ma < GS ? ga1 : ga2, ma & (GS - 1));
+      }
+      clk.lap(MS_PROBE);
+      const uint32_t o1 = (uint32_t)(u0 + q1), o2 = (uint32_t)(u0 + q2);
+      if (s1 >= 0) {
+        atomicAdd(&L.cnt[s1], 1u);
+        atomicMin(&L.off[s1], o1);
+      }
+      if (TWO && s2 >= 0) {
+        atomicAdd(&L.cnt[s2], 1u);
+        atomicMin(&L.off[s2], o2);
+      }
+      const bool d1 = h1 && s1 < 0, d2 = TWO && h2 && s2 < 0;
+      emit_two(L.bcur, a, rout, d1, ha & bmask, a0, n1, o1, n1, d2, hb & bmask, b0, n2, o2, n2);
+      if constexpr (ST) {
+        my_direct += (uint32_t)(__popcll(__ballot(d1)) + (TWO ? __popcll(__ballot(d2)) : 0));
+        const uint32_t nh = (uint32_t)(__popcll(__ballot(s1 >= 0)) + __popcll(__ballot(s2 >= 0)));
+        if (lane == 0) atomicAdd(&st_acc[MS_N_HIT], (unsigned long long)nh);
+      }
+      clk.lap(MS_EMIT);
+    };
+    // short token starts: a delimiter within the next 7 bytes (dm bits i+1..i+7)
+    const uint64_t s1m = dm >> 1, s2m = s1m | (s1m >> 1), s4m = s2m | (s2m >> 2);
+    const uint32_t near7 = (uint32_t)(s4m | (s4m >> 3));
+    const uint32_t sbits = bits & near7, obits = bits & ~near7;
+    uint32_t tot_s, tot_o;
+    const uint32_t ks0 = wave_excl_small((uint32_t)__popc(sbits), tot_s);
+    const uint32_t ko0 = wave_excl_small((uint32_t)__popc(obits), tot_o);
+    tot_s = __builtin_amdgcn_readfirstlane(tot_s);
+    tot_o = __builtin_amdgcn_readfirstlane(tot_o);
+    const uint32_t wave_total = tot_s + tot_o;
     clk.lap(MS_MASK);
-    for (uint32_t base = 0; base < wave_total; base += MAP_LIST) {
-      // ---- list round: entries [base, base + MAP_LIST) of the unit ----
-      const uint32_t lim = base + MAP_LIST;
-      const uint32_t dlo = (uint32_t)dm, dhi = (uint32_t)(dm >> 32);
-      // delimiter bits from the token start on (i < 32: one funnel shift); none
-      // within 31 bytes -> MAP_LONG: ffbl of 0 is all ones, and the u16 entry
-      // keeps 5 length bits, so (ffbl << 11) needs no clamp
-      static_assert(MAP_LONG == 31, "list entries: 11 position bits + 5 length bits");
-      while (bits && k < lim) {
+    if (wave_total <= (uint32_t)MAP_LIST) {
+      // one list round: short entries at [0, tot_s), the others at [tot_s, total)
+      uint32_t ks = ks0, ko = tot_s + ko0;
+      while (bits) {
         const uint32_t i = __ffs(bits) - 1;
         bits &= bits - 1;
         const uint32_t rest = __builtin_amdgcn_alignbit(dhi, dlo, i);
-        list[k - base] = (uint16_t)((pbase + i) | (ffbl_raw(rest) << 11));
-        ++k;
+        const bool sh = (sbits >> i) & 1u;
+        list[sh ? ks : ko] = (uint16_t)((pbase + i) | (ffbl_raw(rest) << 11));
+        ks += sh ? 1u : 0u;
+        ko += sh ? 0u : 1u;
       }
       wave_sync();
-      const uint32_t round_n = min(wave_total - base, (uint32_t)MAP_LIST);
       clk.lap(MS_LIST);
-      // one step: two list entries per lane, both probed in one LDS round trip;
-      // a tail of <= 64 entries takes the one-entry step (no dead second half)
-      auto step = [&](uint32_t j, auto two_c) {
-        constexpr bool TWO = decltype(two_c)::value;
-        const bool h1 = j + lane < round_n, h2 = TWO && j + 64 + lane < round_n;
-        const uint32_t e1 = h1 ? list[j + lane] : 0u, e2 = h2 ? list[j + 64 + lane] : 0u;
-        const uint32_t q1 = e1 & 0x7FFu, q2 = e2 & 0x7FFu, n1 = e1 >> 11, n2 = e2 >> 11;
-        uint64_t w10, w11, w20 = 0, w21 = 0;
-        window16(buf, q1, w10, w11);
-        if (TWO) window16(buf, q2, w20, w21);
-        if (WC_MAP_ABLATE == 1) {
-          sink ^= w10 ^ w21;
-          return;
-        }
-        const bool in1 = h1 && n1 <= KEY_INLINE_MAX, in2 = h2 && n2 <= KEY_INLINE_MAX;
-        uint64_t a0, a1, as, b0 = 0, b1 = 0, bs = 0;
-        inline_key(w10, w11, n1, a0, a1, as);
-        if (TWO) inline_key(w20, w21, n2, b0, b1, bs);
-        const uint32_t ha = place_hash(a0, a1), hb = TWO ? place_hash(b0, b1) : 0u;
-        uint32_t ga1, ga2, gb1 = 0, gb2 = 0;
-        hot_groups(ha, ga1, ga2);
-        if (TWO) hot_groups(hb, gb1, gb2);
-        clk.lap(MS_KEYS);
-        if (WC_MAP_ABLATE == 2) {
-          sink ^= as ^ bs ^ ga2 ^ gb2;
-          return;
-        }
-        const u64x2* S = reinterpret_cast<const u64x2*>(L.sig);
-        int s1 = -1, s2 = -1;
-        if constexpr (GS == 2) {  // S[g]: both slots of group g
-          const u64x2 xa0 = S[ga1], xa1 = S[ga2];
-          if (TWO) {
-            const u64x2 xb0 = S[gb1], xb1 = S[gb2];
-            const int mb = in2 ? sig_match4(xb0, xb1, bs) : -1;
-            s2 = mb < 0 ? -1 : (int)slot_of(mb < GS ? gb1 : gb2, mb & (GS - 1));
-          }
-          const int ma = in1 ? sig_match4(xa0, xa1, as) : -1;
-          s1 = ma < 0 ? -1 : (int)slot_of(ma < GS ? ga1 : ga2, ma & (GS - 1));
-        } else {  // S[g]: slots 0-1, S[NG + g]: slots 2-3
-          const u64x2 xa0 = S[ga1], xa1 = S[NG + ga1], xa2 = S[ga2], xa3 = S[NG + ga2];
-          if (TWO) {
-            const u64x2 xb0 = S[gb1], xb1 = S[NG + gb1], xb2 = S[gb2], xb3 = S[NG + gb2];
-            const int mb = in2 ? sig_match8(xb0, xb1, xb2, xb3, bs) : -1;
-            s2 = mb < 0 ? -1 : (int)slot_of(mb < GS ? gb1 : gb2, mb & (GS - 1));
-          }
-          const int ma = in1 ? sig_match8(xa0, xa1, xa2, xa3, as) : -1;
-          s1 = ma < 0 ? -1 : (int)slot_of(ma < GS ? ga1 : ga2, ma & (GS - 1));
-        }
-        // two-word keys: the matching slot's side word decides
-        const bool ta = two_word(as), tb = TWO && two_word(bs);
-        const uint64_t ca = s1 >= 0 && ta ? L.side[s1] : a0, cb = s2 >= 0 && tb ? L.side[s2] : b0;
-        if (ca != a0) s1 = -1;
-        if (cb != b0) s2 = -1;
-        clk.lap(MS_PROBE);
-        const uint32_t o1 = (uint32_t)(u0 + q1), o2 = (uint32_t)(u0 + q2);
-        if (s1 >= 0) {
-          atomicAdd(&L.cnt[s1], 1u);  // results unused: no-return ds_add / ds_min
-          atomicMin(&L.off[s1], o1);
-        }
-        if (TWO && s2 >= 0) {
-          atomicAdd(&L.cnt[s2], 1u);
-          atomicMin(&L.off[s2], o2);
-        }
-        if (WC_MAP_ABLATE == 3) return;
-        // misses of inline words become records now; LONG words wait for the round end
-        const bool d1 = in1 && s1 < 0, d2 = TWO && in2 && s2 < 0;
-        emit_two(L.bcur, a, rout, d1, ha & bmask, a0, a1, o1, n1, d2, hb & bmask, b0, b1, o2, n2);
-        const bool f1 = h1 && !in1, f2 = TWO && h2 && !in2;
-        const uint64_t mf1 = __ballot(f1), mf2 = TWO ? __ballot(f2) : 0ull;
-        if (mf1 | mf2) {  // entries before j are consumed: ndef <= j
-          const uint32_t r1 =
-              __builtin_amdgcn_mbcnt_hi((uint32_t)(mf1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mf1, 0u));
-          const uint32_t r2 =
-              __builtin_amdgcn_mbcnt_hi((uint32_t)(mf2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mf2, 0u));
-          const uint32_t n1c = (uint32_t)__popcll(mf1);
-          if (f1) list[ndef + r1] = (uint16_t)e1;
-          if (f2) list[ndef + n1c + r2] = (uint16_t)e2;
-          ndef += n1c + (uint32_t)__popcll(mf2);
-        }
-        my_direct += (uint32_t)(__popcll(__ballot(d1)) + (TWO ? __popcll(__ballot(d2)) : 0));
-        if constexpr (ST) {
-          const uint32_t nh = (uint32_t)(__popcll(__ballot(s1 >= 0)) + __popcll(__ballot(s2 >= 0)));
-          if (lane == 0) {
-            atomicAdd(&st_acc[MS_N_HIT], (unsigned long long)nh);
-            atomicAdd(&st_acc[MS_N_DEFER], (unsigned long long)__popcll(mf1 | mf2));
-          }
-        }
-        clk.lap(MS_EMIT);
-      };
       uint32_t j = 0;
-      for (; j + 64 < round_n; j += 128) step(j, std::true_type{});
-      if (j < round_n) step(j, std::false_type{});
+      for (; j + 64 < tot_s; j += 128) step_short(j, tot_s, std::true_type{});
+      if (j < tot_s) step_short(j, tot_s, std::false_type{});
+      const uint32_t total = tot_s + tot_o;
+      for (j = tot_s; j + 64 < total; j += 128) step(j, total, std::true_type{});
+      if (j < total) step(j, total, std::false_type{});
       if (ndef) {
         run_deferred(u0);
         clk.lap(MS_SLOW);
       }
-      wave_sync();  // entries read before the next round overwrites them
+      wave_sync();  // entries read before the next unit's list overwrites them
+    } else {
+      // more than MAP_LIST tokens in the unit (runs of 1-byte words): rounds of
+      // MAP_LIST entries in stream order, every entry on the general step
+      uint32_t k = ks0 + ko0;  // the lane's first entry among all tokens of the unit
+      for (uint32_t base = 0; base < wave_total; base += MAP_LIST) {
+        const uint32_t lim = base + MAP_LIST;
+        while (bits && k < lim) {
+          const uint32_t i = __ffs(bits) - 1;
+          bits &= bits - 1;
+          const uint32_t rest = __builtin_amdgcn_alignbit(dhi, dlo, i);
+          list[k - base] = (uint16_t)((pbase + i) | (ffbl_raw(rest) << 11));
+          ++k;
+        }
+        wave_sync();
+        const uint32_t round_n = min(wave_total - base, (uint32_t)MAP_LIST);
+        clk.lap(MS_LIST);
+        uint32_t j = 0;
+        for (; j + 64 < round_n; j += 128) step(j, round_n, std::true_type{});
+        if (j < round_n) step(j, round_n, std::false_type{});
+        if (ndef) {
+          run_deferred(u0);
+          clk.lap(MS_SLOW);
+        }
+        wave_sync();  // entries read before the next round overwrites them
+      }
     }
     u = nu;
     nu = u == NONE ? NONE : grab();
@@ -621,7 +709,6 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   __syncthreads();
   clk.lap(MS_WAIT);
   // block end: every counted hot slot becomes one record of its bucket
-  uint32_t emitted = 0;
 #pragma unroll
   for (int j = 0; j < SPT; ++j) {
     const int s = tid + j * MAP_THREADS;
@@ -630,7 +717,6 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     uint64_t k0, k1;
     sig_key(L.sig[s], L.side[s], k0, k1);
     emit_record(L.bcur, a, rout, place_hash(k0, k1) & bmask, k0, k1, c, L.off[s]);
-    ++emitted;
   }
   clk.lap(MS_FLUSH);
   if constexpr (ST) {
@@ -649,14 +735,22 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     }
   }
   if (WC_MAP_ABLATE && sink == 0x9E3779B97F4A7C15ull) atomicOr(&a.flags[FLAG_COUNT - 1], 0u);  // never true
-  uint64_t t = my_tokens, e = emitted;
+  // records of the block = the sum of its bucket cursors (no per-step counting)
+  __syncthreads();  // every flush's cursor add is in
+  const uint32_t nb = 1u << a.log2_rec_buckets;
+  uint64_t t = my_tokens, e = 0;
+  for (uint32_t b = tid; b < nb; b += MAP_THREADS) {
+    const uint32_t c = L.bcur[b];
+    a.rec.count[(size_t)blockIdx.x * nb + b] = c;
+    e += (c & 0xFFFFu) + (c >> 16);
+  }
   for (int o = 32; o > 0; o >>= 1) {
     t += __shfl_down(t, o);
     e += __shfl_down(e, o);
   }
   if (lane == 0) {
     atomicAdd(&L.tokens, (unsigned long long)t);
-    atomicAdd(&L.used, (unsigned long long)(e + my_direct));
+    atomicAdd(&L.used, (unsigned long long)e);
   }
   __syncthreads();
   if constexpr (ST) {
@@ -666,18 +760,18 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     atomicAdd(a.tokens, L.tokens);
     atomicAdd(a.rec.cursor, L.used);
   }
-  const uint32_t nb = 1u << a.log2_rec_buckets;
-  for (uint32_t b = tid; b < nb; b += MAP_THREADS) a.rec.count[(size_t)blockIdx.x * nb + b] = L.bcur[b];
 }
 
 }  // namespace dev
 
-void launch_map(const MapArgs& a, const HotArgs& h, uint32_t map_blocks, hipStream_t s) {
-  hipLaunchKernelGGL(dev::wc_hot_sample, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
-  hipLaunchKernelGGL(dev::wc_hot_hist, dim3(HOT_SEL_BLOCKS), dim3(1024), 0, s, h);
-  hipLaunchKernelGGL(dev::wc_hot_threshold, dim3(1), dim3(1024), 0, s, h);
-  for (int p = 0; p < dev::HOT_PLACE_PASSES; ++p)
-    hipLaunchKernelGGL(dev::wc_hot_place, dim3(HOT_SEL_BLOCKS), dim3(1024), 0, s, h, p);
+void launch_map(const MapArgs& a, const HotArgs& h, uint32_t map_blocks, hipStream_t s, bool sample) {
+  if (sample) {
+    hipLaunchKernelGGL(dev::wc_hot_sample, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
+    hipLaunchKernelGGL(dev::wc_hot_hist, dim3(HOT_SEL_BLOCKS), dim3(1024), 0, s, h);
+    hipLaunchKernelGGL(dev::wc_hot_threshold, dim3(1), dim3(1024), 0, s, h);
+    for (int p = 0; p < dev::HOT_PLACE_PASSES; ++p)
+      hipLaunchKernelGGL(dev::wc_hot_place, dim3(HOT_SEL_BLOCKS), dim3(1024), 0, s, h, p);
+  }
   if (a.stamps) hipLaunchKernelGGL(dev::wc_map<true>, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
   else hipLaunchKernelGGL(dev::wc_map<false>, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
 }

@@ -49,6 +49,15 @@ __device__ __forceinline__ void window16(const uint8_t* buf, uint32_t p, uint64_
 #endif
 }
 
+// Bytes [p, p+8) of the LDS text buffer: three dwords from the 4-byte-aligned
+// address below p and two v_alignbyte_b32 funnels.
+__device__ __forceinline__ uint64_t window8(const uint8_t* buf, uint32_t p) {
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(buf + (p & ~3u));
+  const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
+  const uint32_t sh = p & 3u;
+  return (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32);
+}
+
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -135,25 +144,30 @@ __device__ __forceinline__ RecOut rec_out(const MapArgs& a) {
   return RecOut{a.rec.recs12 + first, a.rec.recs + first, a.rec.subcap};
 }
 
-// Store one record at cursor value `packed` of bucket b's sub-region.
+// Store one record at cursor value `packed` of bucket b's sub-region.  The
+// block's store bases are wave-uniform (SGPRs) and a record's byte offset in
+// them fits 32 bits (index < 2^25), so the stores take the SGPR-base + 32-bit
+// VGPR-offset form: one 24-bit multiply per record, no 64-bit address math.
 __device__ __forceinline__ void put_record(const MapArgs& a, const RecOut& o, uint32_t b, uint32_t packed, bool r12,
                                           uint64_t k0, uint64_t k1, uint64_t cnt, uint32_t off) {
   const uint32_t pos = r12 ? (packed & 0xFFFFu) : (packed >> 16);
   const uint32_t idx = __umul24(b, o.sub) + pos;
   if (pos >= o.sub) {
     atomicOr(&a.flags[FLAG_REGION_OVF], 1u);
-  } else if (r12) {
+    return;
+  }
+  if (r12) {
     Rec12 r;
     r.lo = (uint32_t)k0;
     r.hi = (uint32_t)(k0 >> 32);
     r.off = off;
-    o.b12[idx] = r;
+    *reinterpret_cast<Rec12*>(reinterpret_cast<uint8_t*>(o.b12) + __umul24(idx, (uint32_t)sizeof(Rec12))) = r;
   } else {
     Rec r;
     r.k0 = k0;
     r.k1 = k1;
     r.co = (cnt << 32) | off;
-    o.b24[idx] = r;
+    *reinterpret_cast<Rec*>(reinterpret_cast<uint8_t*>(o.b24) + __umul24(idx, (uint32_t)sizeof(Rec))) = r;
   }
 }
 

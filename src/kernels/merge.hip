@@ -301,9 +301,10 @@ __global__ void wc_scatter_ids(const uint32_t* send_pos, const uint32_t* ids_bac
 // Gathered merged rows (grouped by owner) -> key columns; sref_off is made
 // absolute in the gathered byte buffer.  cnt / first may be null (the dense
 // merge takes them from its reduced vectors).
-__global__ void wc_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rbase, const uint64_t* bbase,
-                                uint32_t W, uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first,
-                                uint64_t* soff, uint32_t* slen) {
+__global__ void wc_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* dn, const uint64_t* rbase,
+                                const uint64_t* bbase, uint32_t W, uint64_t* k0, uint64_t* k1, uint64_t* cnt,
+                                uint64_t* first, uint64_t* soff, uint32_t* slen) {
+  if (dn) n = *dn;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     uint32_t o = 0;
     while (o + 1 < W && rbase[o + 1] <= i) ++o;
@@ -350,9 +351,9 @@ void launch_mrow_compact(const MRow* rows, const uint32_t* state, const unsigned
 }
 void launch_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rbase, const uint64_t* bbase, uint32_t W,
                          uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first, uint64_t* soff, uint32_t* slen,
-                         hipStream_t s) {
+                         hipStream_t s, const uint64_t* dn) {
   if (n)
-    hipLaunchKernelGGL(dev::wc_mrow_to_cols, dev::mgrid(n), dim3(256), 0, s, rows, n, rbase, bbase, W, k0, k1, cnt,
+    hipLaunchKernelGGL(dev::wc_mrow_to_cols, dev::mgrid(n), dim3(256), 0, s, rows, n, dn, rbase, bbase, W, k0, k1, cnt,
                        first, soff, slen);
 }
 

@@ -149,7 +149,8 @@ __global__ void __launch_bounds__(OS_THREADS) wc_os_pass(const uint64_t* keys, c
 __global__ void wc_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
                                const uint64_t* soff, const uint32_t* slen, const uint32_t* perm, uint64_t* ok0,
                                uint64_t* ok1, uint64_t* ocnt, uint64_t* ofirst, uint64_t* osoff, uint32_t* oslen,
-                               uint64_t n) {
+                               uint64_t n, const uint64_t* dn) {
+  if (dn) n = *dn;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t j = perm[i];
     ok0[i] = k0[j];
@@ -222,10 +223,11 @@ void radix_sort_pairs(uint64_t* keys, uint32_t* vals, uint64_t* tmp_keys, uint32
 
 void launch_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
                         const uint64_t* soff, const uint32_t* slen, const uint32_t* perm, uint64_t* ok0, uint64_t* ok1,
-                        uint64_t* ocnt, uint64_t* ofirst, uint64_t* osoff, uint32_t* oslen, uint64_t n, hipStream_t s) {
+                        uint64_t* ocnt, uint64_t* ofirst, uint64_t* osoff, uint32_t* oslen, uint64_t n, hipStream_t s,
+                        const uint64_t* dn) {
   if (n)
     hipLaunchKernelGGL(dev::wc_gather_cols, dev::grid_for(n), dim3(256), 0, s, k0, k1, cnt, first, soff, slen, perm,
-                       ok0, ok1, ocnt, ofirst, osoff, oslen, n);
+                       ok0, ok1, ocnt, ofirst, osoff, oslen, n, dn);
 }
 
 void launch_iota_u32(uint32_t* v, uint64_t n, hipStream_t s) {

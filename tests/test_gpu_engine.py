@@ -180,8 +180,8 @@ def test_loopback_merge_many_long_words(ranks, merge_mode):
 
 @pytest.mark.parametrize("merge_mode", [0, 1])
 @pytest.mark.parametrize("ranks", [1, 3, 8])
-@pytest.mark.parametrize("opts", [dict(), dict(log2_rec_buckets=1, log2_tab_buckets=1),
-                                  dict(min_records=16384, records_per_byte=0.001)])
+@pytest.mark.parametrize("opts", [dict(chunk_bytes=8 << 20), dict(log2_rec_buckets=1, log2_tab_buckets=1, chunk_bytes=8 << 20),
+                                  dict(min_records=16384, records_per_byte=0.001, chunk_bytes=1 << 20)])
 def test_loopback_merge_speculative(ranks, merge_mode, opts, monkeypatch):
     """HBM-resident shards: each rank's last pass stays pending and the merged
     finalize runs behind it (merge_cols_speculative: compaction + owner plan +
@@ -194,8 +194,7 @@ def test_loopback_merge_speculative(ranks, merge_mode, opts, monkeypatch):
                                                                                               vocab=40000)
     want = ops.cpu_count(text)
     for all_ranks in (False, True):
-        got = ops.loopback_count(text, ranks, merge_mode=merge_mode, all_ranks=all_ranks, resident=True,
-                                 chunk_bytes=8 << 20, **opts)
+        got = ops.loopback_count(text, ranks, merge_mode=merge_mode, all_ranks=all_ranks, resident=True, **opts)
         assert_same(got, want)
 
 
