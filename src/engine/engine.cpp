@@ -95,6 +95,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   rec.count = rec_mem.take_n<uint32_t>(ncount);
 
   hot_mem.reserve(HOT_TABLE_CAP * (8 + 4) + HOT_TABLE_CAP * 16 + 2 * MAP_SLOTS * 8 + (HOT_SEL_BINS + 3) * 4 +
+                  (size_t)MAP_SLOTS * 64 +
                   HOT_GROUPS * 4 + 8192);
   hot.cap = HOT_TABLE_CAP;
   hot.fp = hot_mem.take_n<unsigned long long>(HOT_TABLE_CAP);
@@ -106,6 +107,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   hot_clear_bytes = (size_t)(reinterpret_cast<uint8_t*>(hot.gocc + HOT_GROUPS) - reinterpret_cast<uint8_t*>(hot.fp));
   hot.sig = hot_mem.take_n<uint64_t>(HOT_TABLE_CAP);
   hot.side = hot_mem.take_n<uint64_t>(HOT_TABLE_CAP);
+  hot.long_bytes = hot_mem.take_n<uint8_t>((size_t)MAP_SLOTS * 64);
   WC_HIP_CHECK(hipMalloc(&d_ctr, sizeof(DevCounters)));
   WC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_ctr), sizeof(DevCounters), hipHostMallocDefault));
   h_pass_seq.resize(256);
@@ -258,6 +260,7 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   WC_CHECK(pass_rec.subcap > 0, "shuffle record capacity below one record per (map block, bucket)");
   MapArgs m{text, len, avail, prev, log2_rb, pass_rec, d_ctr->flags, &d_ctr->tokens, k1_mask, d_stamps, d_blk};
   if (d_stamps) blocks_stamped += blocks;
+  hot.text = text;
   launch_map(m, hot, blocks, s, sample);
   mark(EV_MAP);
   if (sync_debug) {  // WC_SYNC_DEBUG: attribute a device fault to a kernel and a chunk

@@ -114,7 +114,13 @@ struct HotArgs {
   uint64_t* img_side;      // [MAP_SLOTS]
   uint32_t* sel;           // [HOT_SEL_BINS + 3] zeroed: count histogram, threshold, tie quota / counter
   uint32_t* gocc;          // [HOT_GROUPS] zeroed: fill of each image group
+  // Hot LONG words (16..HOT_LONG_MAX bytes): the placement copies each placed
+  // word's bytes (zero-padded) into its slot's 64-byte line; the map verifies
+  // every hit against it byte for byte (persists while the image is reused)
+  uint8_t* long_bytes;     // [MAP_SLOTS * 64]
+  const uint8_t* text;     // the sampling pass's chunk text (placement reads the sampled occurrence)
 };
+constexpr uint32_t HOT_LONG_MAX = 63;
 constexpr uint64_t HOT_TABLE_CAP = 1ull << 18;
 // Map hot-table geometry: 2-choice groups of HOT_GROUP_SLOTS signatures.  Two
 // slots per group (4 candidate compares and two 16-byte probe reads per token)

@@ -34,8 +34,11 @@
 //
 // Signatures: a word of <= 7 bytes is its own 64-bit signature (bytes | len
 // << 56, one compare); 8..15-byte words use len << 56 | low 7 bytes of
-// (k0 ^ tail) plus k0 in `side`.  LONG words (>= 16 bytes, hashed keys) never
-// enter the table: each token is a record, so the reducer compares its bytes.
+// (k0 ^ tail) plus k0 in `side`.  LONG words of 16..63 bytes are hot-table
+// words too (0xFF << 56 | a key hash, `side` = the length): a hit needs the
+// token's bytes to equal the slot's 64-byte copy of the word, so exactness
+// never rests on the hash; every other LONG token is a record whose bytes the
+// reducer compares.
 #include <type_traits>
 
 #include "map_common.hpp"
@@ -119,6 +122,58 @@ __device__ __forceinline__ void hot_groups(uint32_t ph, uint32_t& g1, uint32_t& 
 // 64-bit fingerprint of a sampled word (never 0): keys the global sample table.
 __device__ __forceinline__ uint64_t sample_fp(uint64_t sig, uint64_t side) {
   return fmix64(sig ^ (side * 0x9E3779B97F4A7C15ull)) | 1ull;
+}
+
+// Hot LONG words (16..HOT_LONG_MAX bytes, hashed keys).  Their signature has
+// top byte 0xFF — an inline signature's top byte is its length (<= 15), so the
+// two never meet — and 56 bits of a hash of the key; placement and lookup
+// both take the groups from the signature alone.  A signature match is only a
+// candidate: the token's bytes are compared with the slot's 64-byte copy of
+// the word (HotArgs::long_bytes), so colliding words never merge.
+constexpr uint64_t LONG_SIG_TOP = 0xFFull << 56;
+__device__ __forceinline__ bool is_long_sig(uint64_t sig) { return (sig >> 56) == 0xFF; }
+__device__ __forceinline__ uint64_t long_signature(uint64_t k0, uint64_t k1) {
+  return LONG_SIG_TOP | (fmix64(k0 ^ (k1 * 0x9E3779B97F4A7C15ull)) & LOW7);
+}
+__device__ __forceinline__ uint32_t long_group_hash(uint64_t sig) {
+  return mix32((uint32_t)sig ^ (uint32_t)(sig >> 32));
+}
+
+// Key of a word of known length 16..63 at p of an LDS text buffer (readable
+// to p + len + 12): k0 = first 8 bytes, the tail folded in 8-byte chunks
+// (keys.hpp key_of).
+__device__ __forceinline__ void key_long_len(const uint8_t* buf, uint32_t p, uint32_t len, uint64_t mask, uint64_t& k0,
+                                             uint64_t& k1) {
+  k0 = window8(buf, p);
+  uint64_t h = FNV_OFFSET;
+  for (uint32_t c = 8; c < len; c += 8) {
+    uint64_t x = window8(buf, p + c);
+    if (len - c < 8) x &= (1ull << (8 * (len - c))) - 1ull;
+    h = tail_fold(h, x);
+  }
+  k1 = long_k1(len, h, mask);
+}
+
+// The same from a slot's zero-padded 64-byte line (global, 8-byte words).
+__device__ __forceinline__ void key_long_line(const uint8_t* line, uint32_t len, uint64_t mask, uint64_t& k0,
+                                              uint64_t& k1) {
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(line);
+  k0 = w[0];
+  uint64_t h = FNV_OFFSET;
+  for (uint32_t c = 8; c < len; c += 8) h = tail_fold(h, w[c / 8]);  // padding bytes are zero
+  k1 = long_k1(len, h, mask);
+}
+
+// Token bytes [p, p + len) of the LDS buffer == the slot's line?
+__device__ __forceinline__ bool long_line_equal(const uint8_t* buf, uint32_t p, const uint8_t* line, uint32_t len) {
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(line);
+  bool eq = true;
+  for (uint32_t c = 0; c < len; c += 8) {
+    uint64_t x = window8(buf, p + c);
+    if (len - c < 8) x &= (1ull << (8 * (len - c))) - 1ull;
+    eq &= x == w[c / 8];
+  }
+  return eq;
 }
 
 // Delimiter bits of 16 bytes.
@@ -209,14 +264,24 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs 
       bits &= bits - 1;
       const uint64_t rest = dm >> b;
       const uint32_t len = rest ? (uint32_t)__ffsll((unsigned long long)rest) - 1 : 64u;
-      if (len > KEY_INLINE_MAX) continue;
+      if (len > HOT_LONG_MAX) continue;  // (64: the length is not known inside the lane window)
       const uint32_t p = pbase + b;
-      uint64_t k0, k1, sg, w0, w1;
-      window16(buf, p, w0, w1);
-      inline_key(w0, w1, len, k0, k1, sg);
-      const uint64_t sd = two_word(sg) ? k0 : 0ull;
-      const uint64_t f = sample_fp(sg, sd);
-      uint32_t g = (place_hash(k0, k1) >> 20) & (NG - 1);
+      uint64_t k0, k1, sg, sd, f;
+      uint32_t g;
+      if (len <= KEY_INLINE_MAX) {
+        uint64_t w0, w1;
+        window16(buf, p, w0, w1);
+        inline_key(w0, w1, len, k0, k1, sg);
+        sd = two_word(sg) ? k0 : 0ull;
+        f = sample_fp(sg, sd);
+        g = (place_hash(k0, k1) >> 20) & (NG - 1);
+      } else {  // LONG: side = this occurrence's chunk offset | length (the placement copies its bytes)
+        key_long_len(buf, p, len, a.k1_mask, k0, k1);
+        sg = long_signature(k0, k1);
+        sd = (u0 + p) | ((uint64_t)len << 32);
+        f = sample_fp(sg, k0);
+        g = (uint32_t)(f >> 20) & (NG - 1);
+      }
       for (int st = 0; st < SAMPLE_PROBES * GS; ++st) {
         const uint32_t s = GS * g + (st & (GS - 1));
         uint64_t cur = L.fp[s];
@@ -349,10 +414,15 @@ __global__ void __launch_bounds__(1024) wc_hot_place(HotArgs h, int pass) {
     if (c == 0 || c + 1 < t || tier != (pass == HOT_PLACE_PASSES - 1 ? 2 : pass)) continue;
     if (c < t && atomicAdd(&h.sel[SEL_BINS + 2], 1u) >= ties) continue;
     const uint64_t sg = h.sig[s], sd = h.side[s];
-    uint64_t k0, k1;
-    sig_key(sg, sd, k0, k1);
+    const bool lng = is_long_sig(sg);
     uint32_t g1, g2;
-    hot_groups(place_hash(k0, k1), g1, g2);
+    if (lng) {
+      hot_groups(long_group_hash(sg), g1, g2);
+    } else {
+      uint64_t k0, k1;
+      sig_key(sg, sd, k0, k1);
+      hot_groups(place_hash(k0, k1), g1, g2);
+    }
     if (__hip_atomic_load(&h.gocc[g2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
         __hip_atomic_load(&h.gocc[g1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
       const uint32_t x = g1;
@@ -365,8 +435,20 @@ __global__ void __launch_bounds__(1024) wc_hot_place(HotArgs h, int pass) {
       o = atomicAdd(&h.gocc[g2], 1u);
     }
     if (o >= GS) continue;
-    h.img_sig[slot_of(g, o)] = sg;
-    h.img_side[slot_of(g, o)] = sd;
+    const uint32_t slot = slot_of(g, o);
+    h.img_sig[slot] = sg;
+    if (lng) {  // side = the length; the word's bytes (zero-padded) go to the slot's line
+      const uint32_t len = (uint32_t)(sd >> 32), at = (uint32_t)sd;
+      h.img_side[slot] = len;
+      uint64_t* line = reinterpret_cast<uint64_t*>(h.long_bytes + (size_t)slot * 64);
+      for (uint32_t c = 0; c < 64; c += 8) {
+        uint64_t x = 0;
+        for (uint32_t i = 0; i < 8 && c + i < len; ++i) x |= (uint64_t)h.text[(size_t)at + c + i] << (8 * i);
+        line[c / 8] = x;
+      }
+    } else {
+      h.img_side[slot] = sd;
+    }
   }
 }
 
@@ -465,9 +547,28 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
       const uint32_t q = e & 0x7FFu, n = e >> 11;
       if (hv) {
         uint64_t k0, k1;
+        uint32_t len = n;
         if (n < MAP_LONG) key_long_known(buf, q, n, a.k1_mask, k0, k1);  // 16..30 bytes: length known
-        else key_long_scan(buf, UNIT + HALO, a, q, u0 + q, k0, k1);
-        emit_record(L.bcur, a, rout, place_hash(k0, k1) & bmask, k0, k1, 1, (uint32_t)(u0 + q));
+        else len = (uint32_t)min<uint64_t>(key_long_scan(buf, UNIT + HALO, a, q, u0 + q, k0, k1), 0xFFFFFFFFull);
+        // a hot LONG word: signature candidates, then the bytes against the slot's copy
+        int slot = -1;
+        if (len <= HOT_LONG_MAX) {
+          const uint64_t sg = long_signature(k0, k1);
+          uint32_t g1, g2;
+          hot_groups(long_group_hash(sg), g1, g2);
+          const u64x2* S = reinterpret_cast<const u64x2*>(L.sig);
+          const int m = sig_match4(S[g1], S[g2], sg);
+          if (m >= 0) {
+            const int sl = (int)slot_of(m < GS ? g1 : g2, m & (GS - 1));
+            if (L.side[sl] == len && long_line_equal(buf, q, h.long_bytes + (size_t)sl * 64, len)) slot = sl;
+          }
+        }
+        if (slot >= 0) {
+          atomicAdd(&L.cnt[slot], 1u);
+          atomicMin(&L.off[slot], (uint32_t)(u0 + q));
+        } else {
+          emit_record(L.bcur, a, rout, place_hash(k0, k1) & bmask, k0, k1, 1, (uint32_t)(u0 + q));
+        }
       }
     }
     if (ST) my_direct += ndef;
@@ -715,7 +816,9 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     const uint32_t c = L.cnt[s];
     if (!c) continue;
     uint64_t k0, k1;
-    sig_key(L.sig[s], L.side[s], k0, k1);
+    const uint64_t sg = L.sig[s];
+    if (is_long_sig(sg)) key_long_line(h.long_bytes + (size_t)s * 64, (uint32_t)L.side[s], a.k1_mask, k0, k1);
+    else sig_key(sg, L.side[s], k0, k1);
     emit_record(L.bcur, a, rout, place_hash(k0, k1) & bmask, k0, k1, c, L.off[s]);
   }
   clk.lap(MS_FLUSH);

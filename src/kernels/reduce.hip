@@ -189,7 +189,7 @@ __device__ __noinline__ uint32_t merge_slow(RedLds& L, uint32_t ph, uint64_t k0,
 // tag acquires before reading the reference and the copy.  Probers that see
 // PENDING re-read the group; the claimer finishes inside its iteration, so the
 // lanes of one wave never wait on each other.  Returns 1 for a claim.
-__device__ __noinline__ uint32_t merge_long(RedLds& L, const ReduceArgs& a, uint32_t b, uint32_t ph, uint64_t k0,
+__device__ __forceinline__ uint32_t merge_long(RedLds& L, const ReduceArgs& a, uint32_t b, uint32_t ph, uint64_t k0,
                                             uint64_t k1, uint64_t cnt, uint64_t first, uint64_t off) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const size_t sbase = (size_t)b * TAB_SLOTS;
@@ -260,7 +260,7 @@ __device__ __noinline__ uint32_t merge_long(RedLds& L, const ReduceArgs& a, uint
 // matches (a second round trip); (3) a key match counts with two LDS atomics.
 // A record with no matching slot in those groups — a new key, a key placed
 // further along its sequence, a tag collision — takes merge_slow.  LONG keys
-// (hashed, 24-byte runs only) take merge_long (byte comparison).
+// (hashed, 24-byte runs only) are left to long_stream.
 template <bool R12, int U, class RecT>
 __device__ __forceinline__ void merge_batch(RedLds& L, const ReduceArgs& a, uint32_t b, const RecT (&rr)[U],
                                             const bool (&valid)[U], uint32_t shift,
@@ -288,7 +288,8 @@ __device__ __forceinline__ void merge_batch(RedLds& L, const ReduceArgs& a, uint
       continue;
     }
     ph[u] = place_hash(k0[u], key1(u));
-    mine[u] = valid[u] && (!shift || bucket_of(ph[u], a.tab.log2_buckets) == b);
+    // LONG keys (hashed, 24-byte runs only) are merged by long_stream afterwards
+    mine[u] = valid[u] && (!shift || bucket_of(ph[u], a.tab.log2_buckets) == b) && (R12 || !key_is_hashed(key1(u)));
     tg[u] = *reinterpret_cast<const u32x4*>(L.grp[group_of(ph[u], TAB_GROUPS)].tag);
     tg2[u] = *reinterpret_cast<const u32x4*>(L.grp[group2_of(ph[u], TAB_GROUPS)].tag);
   }
@@ -335,9 +336,7 @@ __device__ __forceinline__ void merge_batch(RedLds& L, const ReduceArgs& a, uint
       off = (uint32_t)rr[u].co;
     }
     const uint64_t first = a.chunk_base + off;
-    if (!R12 && key_is_hashed(key1(u))) {
-      claims += merge_long(L, a, b, ph[u], k0[u], key1(u), cnt, first, off);
-    } else if (slot[u] != 0xFFFFFFFFu && c1[u] == key1(u) && c0[u] == k0[u]) {
+    if (slot[u] != 0xFFFFFFFFu && c1[u] == key1(u) && c0[u] == k0[u]) {
       if (WC_RED_ABLATE != 3) add_to_slot(L, (int)slot[u], cnt, first);
     } else {
       claims += merge_slow(L, ph[u], k0[u], key1(u), cnt, first);
@@ -422,6 +421,26 @@ __device__ __forceinline__ void merge_stream(RedLds& L, const ReduceArgs& a, uin
   }
 }
 
+// LONG records of this wave's runs (a second, lean pass over the 24-byte runs:
+// one record per lane per step, few live registers around the out-of-line
+// merge_long, whose byte comparison needs global reads anyway).
+__device__ __forceinline__ void long_stream(RedLds& L, const ReduceArgs& a, uint32_t b, uint32_t wave, uint32_t nwaves,
+                                            uint32_t nrb, uint32_t rb, uint32_t sub, uint32_t shift, uint32_t& claims) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t p = wave; p < a.map_blocks; p += nwaves) {
+    const uint32_t n = min(L.runcnt[p] >> 16, sub);
+    const Rec* run = a.rec.recs + ((size_t)p * nrb + rb) * sub;
+    for (uint32_t i = lane; i < n; i += 64) {
+      const Rec r = run[i];
+      if (!key_is_hashed(r.k1)) continue;
+      const uint32_t ph = place_hash(r.k0, r.k1);
+      if (shift && bucket_of(ph, a.tab.log2_buckets) != b) continue;
+      const uint32_t off = (uint32_t)r.co;
+      claims += merge_long(L, a, b, ph, r.k0, r.k1, r.co >> 32, a.chunk_base + off, off);
+    }
+  }
+}
+
 __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   __shared__ RedLds L;
   const uint32_t b = blockIdx.x;
@@ -450,6 +469,7 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   uint32_t claims = 0;
   merge_stream<true, RED_UNROLL>(L, a, b, a.rec.recs12, wave, nwaves, nrb, rb, (uint32_t)sub, shift, claims);
   merge_stream<false, RED_UNROLL_24>(L, a, b, a.rec.recs, wave, nwaves, nrb, rb, (uint32_t)sub, shift, claims);
+  long_stream(L, a, b, wave, nwaves, nrb, rb, (uint32_t)sub, shift, claims);
   for (int o = 32; o > 0; o >>= 1) claims += __shfl_down(claims, o);
   if ((tid & 63) == 0 && claims) atomicAdd(&L.occupied, claims);
   if (WC_RED_STAMPS && (tid & 63) == 0)

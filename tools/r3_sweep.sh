@@ -10,6 +10,14 @@ run() {  # name, timeout, args...
   timeout -k 10 $t python bench.py "$@" > $OUT/$name.json 2> $OUT/$name.err || { echo "FAIL $name"; tail -5 $OUT/$name.err; return 1; }
   python3 -c "import json,sys; d=json.loads(open('$OUT/$name.json').read().strip().splitlines()[-1]); st=d['stages']; print('%-28s %8.1f GB/s %8.4f ms/step valid=%s keys=%s dev=%s' % ('$name', d['value'], d['ms_per_step'], d['validated'], d['distinct_words'], st['device_ms']))"
 }
+if [ $# -gt 0 ]; then  # only the named rows
+  for r in "$@"; do
+    line=$(grep -E "(^| )run $r " "$0" | grep -v '^ ' | head -1)
+    [ -n "$line" ] || { echo "no row $r"; exit 1; }
+    eval "$line" || exit 1
+  done
+  exit 0
+fi
 run v100k 120 --steps 300 || exit 1
 run v500 120 --steps 300 --vocab 500 || exit 1
 run v10k 120 --steps 300 --vocab 10000 || exit 1
