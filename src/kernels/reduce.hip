@@ -13,10 +13,12 @@
 //                     is written back.  LONG words (>= 16 bytes, hashed keys)
 //                     are merged only after a byte comparison with the stored
 //                     copy of the word (exact equality, keys.hpp), in line with
-//                     every other record: a new LONG word is claimed by the
-//                     first lane that meets it (slot PENDING while its bytes
-//                     are copied to the key arena — keys outlive streamed
-//                     chunks — then published), in parallel across the block.
+//                     every other record (a second, lean pass over the 24-byte
+//                     runs): a new LONG word is claimed by the first lane that
+//                     meets it, in parallel across the block, and references
+//                     its occurrence in the chunk until the block end copies
+//                     all the pass's new words to the key arena (keys outlive
+//                     streamed chunks) with one arena allocation per block.
 //                     If a slice overflows it is NOT written back;
 //                     the host splits the table and re-runs only the
 //                     overflowed buckets.
@@ -52,11 +54,14 @@ constexpr int RED_UNROLL = WC_RED_UNROLL;  // 12-byte records in flight per lane
 #endif
 constexpr int RED_UNROLL_24 = WC_RED_UNROLL_24;  // 24-byte records in flight per lane (VGPR budget)
 constexpr uint32_t SREF_POISON = 0xFFFFFFFFu;  // sref_len of a LONG slot whose bytes did not fit the arena
+constexpr uint32_t LONGQ = 2048;  // LONG record indices queued per bucket pass (more: the runs are re-scanned)
 
 struct RedLds {
   SlotGroup grp[TAB_GROUPS];  // first: 16-B aligned group reads
   uint64_t cnt[TAB_SLOTS];
   uint64_t first[TAB_SLOTS];
+  uint32_t longq[LONGQ];  // record indices of this pass's LONG records
+  uint32_t nlong;
   uint32_t occupied;
   uint32_t overflow;
   uint32_t runcnt[RED_MAX_RUNS];  // packed record counts of this bucket's run in every map block
@@ -101,21 +106,6 @@ __device__ __forceinline__ void store_slice(const RedLds& L, const TableView& t,
   }
 }
 
-// Length of the word at text offset o: 16-byte chunks with a SWAR delimiter
-// test (unaligned global loads; the byte loop only within 16 B of avail_len).
-__device__ __forceinline__ uint64_t word_len(const ReduceArgs& a, uint64_t o) {
-  uint64_t len = 0;
-  while (o + len + 16 <= a.avail_len) {
-    uint64_t w[2];
-    __builtin_memcpy(w, a.text + o + len, 16);
-    const uint32_t m = (uint32_t)(delim_mask8(w[0]) | (delim_mask8(w[1]) << 8));
-    if (m) return len + (uint64_t)(__ffs(m) - 1);
-    len += 16;
-  }
-  while (o + len < a.avail_len && !is_delim(a.text[o + len])) ++len;
-  return len;
-}
-
 // Copy len bytes text[o..) -> arena[p..): 16-byte pieces, then the tail in
 // 8/4/2/1-byte pieces (never past len: neighbouring words are written concurrently).
 __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uint64_t len) {
@@ -129,33 +119,6 @@ __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uin
   if (len - c >= 4) { uint32_t w; __builtin_memcpy(&w, src + c, 4); __builtin_memcpy(dst + c, &w, 4); c += 4; }
   if (len - c >= 2) { uint16_t w; __builtin_memcpy(&w, src + c, 2); __builtin_memcpy(dst + c, &w, 2); c += 2; }
   if (len - c >= 1) dst[c] = src[c];
-}
-
-// Is the word at text offset o exactly the arena copy [so, so + len)?  The
-// arena copy is 8-byte aligned (claims round the cursor), so it is read in
-// aligned words and the text in unaligned ones; then the byte after the word
-// must end it (a delimiter or the end of the readable text).
-__device__ __forceinline__ bool long_equal(const ReduceArgs& a, uint64_t o, uint64_t so, uint32_t len) {
-  if (o + len > a.avail_len) return false;
-  const uint64_t* ar = reinterpret_cast<const uint64_t*>(a.arena.bytes + so);
-  uint32_t c = 0;
-  for (; c + 8 <= len; c += 8) {
-    uint64_t u;
-    __builtin_memcpy(&u, a.text + o + c, 8);
-    if (u != ar[c / 8]) return false;
-  }
-  if (c < len) {
-    uint64_t u = 0;
-    const uint32_t r = len - c;
-    if (o + c + 8 <= a.avail_len) {
-      __builtin_memcpy(&u, a.text + o + c, 8);
-    } else {
-      for (uint32_t i = 0; i < r; ++i) u |= (uint64_t)a.text[o + c + i] << (8 * i);
-    }
-    const uint64_t m = (1ull << (8 * r)) - 1ull;
-    if (((u ^ ar[c / 8]) & m) != 0) return false;
-  }
-  return o + len == a.avail_len || is_delim(a.text[o + len]);
 }
 
 // Count + first offset into slot s.
@@ -180,19 +143,66 @@ __device__ __noinline__ uint32_t merge_slow(RedLds& L, uint32_t ph, uint64_t k0,
   return claimed ? 1u : 0u;
 }
 
+// What the LONG-word merge reads, passed BY VALUE to the out-of-line
+// merge_long (a reference to ReduceArgs would make the kernel keep its
+// argument block in scratch memory and reload fields from it in the hot loop).
+struct LongCtx {
+  const uint8_t* text;
+  uint64_t avail_len;
+  const uint8_t* arena;
+  uint64_t* sref_off;  // this bucket's slice of the table's arena references
+  uint32_t* sref_len;
+};
+// sref_off of a slot claimed during the current pass: the word's bytes are
+// still in the chunk text (copied to the key arena at the block end, one
+// arena allocation per block instead of one contended atomic per new word).
+constexpr uint64_t SREF_TEXT = 1ull << 63;
+
+__device__ __forceinline__ uint64_t word_len(const uint8_t* text, uint64_t avail_len, uint64_t o) {
+  uint64_t len = 0;
+  while (o + len + 16 <= avail_len) {
+    uint64_t w[2];
+    __builtin_memcpy(w, text + o + len, 16);
+    const uint32_t m = (uint32_t)(delim_mask8(w[0]) | (delim_mask8(w[1]) << 8));
+    if (m) return len + (uint64_t)(__ffs(m) - 1);
+    len += 16;
+  }
+  while (o + len < avail_len && !is_delim(text[o + len])) ++len;
+  return len;
+}
+
+// Is the word at text offset o exactly the stored word (sref so, len)?  The
+// stored copy is 8-byte aligned in the arena, or (SREF_TEXT) the claiming
+// record's occurrence in this chunk's text; then the byte after the word
+// must end it (a delimiter or the end of the readable text).
+__device__ __forceinline__ bool long_equal(const LongCtx& c, uint64_t o, uint64_t so, uint32_t len) {
+  if (o + len > c.avail_len) return false;
+  const bool in_text = (so & SREF_TEXT) != 0;
+  const uint8_t* ref = in_text ? c.text + (so & ~SREF_TEXT) : c.arena + so;
+  uint32_t i = 0;
+  for (; i + 8 <= len; i += 8) {
+    uint64_t u, v;
+    __builtin_memcpy(&u, c.text + o + i, 8);
+    __builtin_memcpy(&v, ref + i, 8);
+    if (u != v) return false;
+  }
+  for (; i < len; ++i)
+    if (c.text[o + i] != ref[i]) return false;
+  return o + len == c.avail_len || is_delim(c.text[o + len]);
+}
+
 // A LONG record (hashed key): find the slot whose stored word equals the
 // record's word byte for byte, or claim one.  Colliding words (same k0, k1,
 // different bytes) keep separate slots, so the probe continues past a slot
-// whose bytes differ.  A claim keeps the slot PENDING while the claimer copies
-// the word to the key arena and writes the slot's arena reference, then
-// publishes the tag (workgroup release); a reader that matched a published
-// tag acquires before reading the reference and the copy.  Probers that see
-// PENDING re-read the group; the claimer finishes inside its iteration, so the
-// lanes of one wave never wait on each other.  Returns 1 for a claim.
-__device__ __forceinline__ uint32_t merge_long(RedLds& L, const ReduceArgs& a, uint32_t b, uint32_t ph, uint64_t k0,
-                                            uint64_t k1, uint64_t cnt, uint64_t first, uint64_t off) {
+// whose bytes differ.  A claim keeps the slot PENDING while the claimer
+// writes the slot's reference (SREF_TEXT | its own text offset, and the
+// length), then publishes the tag (workgroup release); a reader that matched
+// a published tag acquires before reading the reference.  Probers that see
+// PENDING re-read the group; the claimer finishes inside its iteration, so
+// the lanes of one wave never wait on each other.  Returns 1 for a claim.
+__device__ __noinline__ uint32_t merge_long(RedLds& L, LongCtx c, uint32_t ph, uint64_t k0, uint64_t k1, uint64_t cnt,
+                                            uint64_t first, uint64_t off) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  const size_t sbase = (size_t)b * TAB_SLOTS;
   const uint32_t tag = make_tag(ph);
   const uint32_t g1 = group_of(ph, TAB_GROUPS), g2 = group2_of(ph, TAB_GROUPS);
   uint32_t g = g1;
@@ -214,8 +224,8 @@ __device__ __forceinline__ uint32_t merge_long(RedLds& L, const ReduceArgs& a, u
       } else if (tv[i] == tag && G.k1[i] == k1 && G.k0[i] == k0) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         const int s = 4 * (int)g + i;
-        const uint32_t sl = a.tab.sref_len[sbase + s];
-        if (sl == SREF_POISON || long_equal(a, off, a.tab.sref_off[sbase + s], sl)) {
+        const uint32_t sl = c.sref_len[s];
+        if (sl == SREF_POISON || long_equal(c, off, c.sref_off[s], sl)) {
           add_to_slot(L, s, cnt, first);
           return 0;
         }
@@ -228,17 +238,9 @@ __device__ __forceinline__ uint32_t merge_long(RedLds& L, const ReduceArgs& a, u
       const int s = 4 * (int)g + e;
       G.k0[e] = k0;
       G.k1[e] = k1;
-      const uint64_t len = word_len(a, off);
-      const uint64_t p = atomicAdd(a.arena.cursor, (unsigned long long)((len + 7) & ~7ull));
-      if (p + len > a.arena.cap || len >= SREF_POISON) {
-        atomicOr(&a.flags[FLAG_ARENA_OVF], 1u);  // the job fails; the slot still absorbs its word's records
-        a.tab.sref_off[sbase + s] = 0;
-        a.tab.sref_len[sbase + s] = SREF_POISON;
-      } else {
-        copy_bytes(a.arena.bytes + p, a.text + off, len);
-        a.tab.sref_off[sbase + s] = p;
-        a.tab.sref_len[sbase + s] = (uint32_t)len;
-      }
+      const uint64_t len = word_len(c.text, c.avail_len, off);
+      c.sref_off[s] = SREF_TEXT | off;
+      c.sref_len[s] = len < SREF_POISON ? (uint32_t)len : SREF_POISON;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __hip_atomic_store(&G.tag[e], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (WC_RED_STAMPS) atomicAdd(&L.st[RS_CLAIMS], 1ull);
@@ -253,6 +255,61 @@ __device__ __forceinline__ uint32_t merge_long(RedLds& L, const ReduceArgs& a, u
   }
 }
 
+// Block end of a bucket pass: the LONG words claimed during the pass still
+// reference the chunk text; one arena allocation for all of them (a block
+// scan of their 8-byte-rounded lengths, ONE global atomic), then every thread
+// copies its slots' words and rewrites their references.
+__device__ void settle_new_long(RedLds& L, const ReduceArgs& a, uint32_t b) {
+  __shared__ uint32_t wbytes[RED_THREADS / 64];
+  __shared__ unsigned long long base;
+  const size_t sbase = (size_t)b * TAB_SLOTS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  static_assert(TAB_SLOTS == 4 * RED_THREADS, "settle: 4 slots per thread");
+  uint32_t need[4], mine = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int s = 4 * tid + j;
+    need[j] = 0;
+    if (slot_tag(L.grp, s) > TAG_PENDING && key_is_hashed(slot_k1(L.grp, s)) && (a.tab.sref_off[sbase + s] & SREF_TEXT)) {
+      const uint32_t len = a.tab.sref_len[sbase + s];
+      need[j] = len == SREF_POISON ? 0u : ((len + 7u) & ~7u) | 1u;  // | 1: a new word (even of length 0)
+    }
+    mine += need[j] & ~1u;
+  }
+  uint32_t incl = mine;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wbytes[wave] = incl;
+  __syncthreads();
+  uint32_t before = 0, total = 0;
+  for (int w = 0; w < RED_THREADS / 64; ++w) {
+    before += w < wave ? wbytes[w] : 0u;
+    total += wbytes[w];
+  }
+  if (tid == 0) base = total ? atomicAdd(a.arena.cursor, (unsigned long long)total) : 0ull;
+  __syncthreads();
+  const bool ovf = base + total > a.arena.cap;
+  if (ovf && tid == 0) atomicOr(&a.flags[FLAG_ARENA_OVF], 1u);
+  uint64_t p = base + before + incl - mine;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (!need[j]) continue;
+    const int s = 4 * tid + j;
+    const uint64_t to = a.tab.sref_off[sbase + s] & ~SREF_TEXT;
+    const uint32_t len = a.tab.sref_len[sbase + s];
+    if (ovf) {
+      a.tab.sref_off[sbase + s] = 0;
+      a.tab.sref_len[sbase + s] = SREF_POISON;
+      continue;
+    }
+    copy_bytes(a.arena.bytes + p, a.text + to, len);
+    a.tab.sref_off[sbase + s] = p;
+    p += need[j] & ~1u;
+  }
+}
+
 // Records [k, k + U * 64) of one run, three phases so a lane keeps all its
 // records' LDS traffic in flight together: (1) load the records, hash them,
 // read the tags of the first two groups of every record's probe sequence (one
@@ -263,7 +320,7 @@ __device__ __forceinline__ uint32_t merge_long(RedLds& L, const ReduceArgs& a, u
 // (hashed, 24-byte runs only) are left to long_stream.
 template <bool R12, int U, class RecT>
 __device__ __forceinline__ void merge_batch(RedLds& L, const ReduceArgs& a, uint32_t b, const RecT (&rr)[U],
-                                            const bool (&valid)[U], uint32_t shift,
+                                            const bool (&valid)[U], const uint32_t (&idx)[U], uint32_t shift,
                                             uint32_t& claims) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const int lane = threadIdx.x & 63;
@@ -288,8 +345,12 @@ __device__ __forceinline__ void merge_batch(RedLds& L, const ReduceArgs& a, uint
       continue;
     }
     ph[u] = place_hash(k0[u], key1(u));
-    // LONG keys (hashed, 24-byte runs only) are merged by long_stream afterwards
-    mine[u] = valid[u] && (!shift || bucket_of(ph[u], a.tab.log2_buckets) == b) && (R12 || !key_is_hashed(key1(u)));
+    mine[u] = valid[u] && (!shift || bucket_of(ph[u], a.tab.log2_buckets) == b);
+    if (!R12 && mine[u] && key_is_hashed(key1(u))) {  // LONG: queued for merge_long after the streams
+      const uint32_t q = atomicAdd(&L.nlong, 1u);
+      if (q < LONGQ) L.longq[q] = idx[u];
+      mine[u] = false;
+    }
     tg[u] = *reinterpret_cast<const u32x4*>(L.grp[group_of(ph[u], TAB_GROUPS)].tag);
     tg2[u] = *reinterpret_cast<const u32x4*>(L.grp[group2_of(ph[u], TAB_GROUPS)].tag);
   }
@@ -409,21 +470,33 @@ __device__ __forceinline__ void merge_stream(RedLds& L, const ReduceArgs& a, uin
       locate(T0 + B, ib, vb);
       load(rb2, ib, vb);
     }
-    merge_batch<R12, U>(L, a, b, ra, va, shift, claims);
+    merge_batch<R12, U>(L, a, b, ra, va, ia, shift, claims);
     if (!more) return;
     const bool more2 = T0 + 2 * B < N;
     if (more2) {
       locate(T0 + 2 * B, ia, va);
       load(ra, ia, va);
     }
-    merge_batch<R12, U>(L, a, b, rb2, vb, shift, claims);
+    merge_batch<R12, U>(L, a, b, rb2, vb, ib, shift, claims);
     if (!more2) return;
   }
 }
 
-// LONG records of this wave's runs (a second, lean pass over the 24-byte runs:
-// one record per lane per step, few live registers around the out-of-line
-// merge_long, whose byte comparison needs global reads anyway).
+// LONG records of this pass: the queued ones (every thread of the block takes
+// entries), or — more than LONGQ in this bucket — a second, lean pass over the
+// wave's 24-byte runs.  One record per lane per step, few live registers
+// around the out-of-line merge_long, whose byte comparison reads global memory
+// anyway.
+__device__ __forceinline__ void long_queue(RedLds& L, const ReduceArgs& a, uint32_t b, uint32_t n, uint32_t& claims) {
+  const size_t sbase = (size_t)b * TAB_SLOTS;
+  const LongCtx c{a.text, a.avail_len, a.arena.bytes, a.tab.sref_off + sbase, a.tab.sref_len + sbase};
+  for (uint32_t i = threadIdx.x; i < n; i += RED_THREADS) {
+    const Rec r = a.rec.recs[L.longq[i]];
+    const uint32_t off = (uint32_t)r.co;
+    claims += merge_long(L, c, place_hash(r.k0, r.k1), r.k0, r.k1, r.co >> 32, a.chunk_base + off, off);
+  }
+}
+
 __device__ __forceinline__ void long_stream(RedLds& L, const ReduceArgs& a, uint32_t b, uint32_t wave, uint32_t nwaves,
                                             uint32_t nrb, uint32_t rb, uint32_t sub, uint32_t shift, uint32_t& claims) {
   const uint32_t lane = threadIdx.x & 63;
@@ -436,7 +509,9 @@ __device__ __forceinline__ void long_stream(RedLds& L, const ReduceArgs& a, uint
       const uint32_t ph = place_hash(r.k0, r.k1);
       if (shift && bucket_of(ph, a.tab.log2_buckets) != b) continue;
       const uint32_t off = (uint32_t)r.co;
-      claims += merge_long(L, a, b, ph, r.k0, r.k1, r.co >> 32, a.chunk_base + off, off);
+      const size_t sbase = (size_t)b * TAB_SLOTS;
+      const LongCtx c{a.text, a.avail_len, a.arena.bytes, a.tab.sref_off + sbase, a.tab.sref_len + sbase};
+      claims += merge_long(L, c, ph, r.k0, r.k1, r.co >> 32, a.chunk_base + off, off);
     }
   }
 }
@@ -455,6 +530,7 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   if (tid == 0) {
     L.occupied = a.tab.occupancy[b];
     L.overflow = 0;
+    L.nlong = 0;
   }
   if (WC_RED_STAMPS && tid < RED_STAMP_N) L.st[tid] = 0;
   __syncthreads();
@@ -469,7 +545,11 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   uint32_t claims = 0;
   merge_stream<true, RED_UNROLL>(L, a, b, a.rec.recs12, wave, nwaves, nrb, rb, (uint32_t)sub, shift, claims);
   merge_stream<false, RED_UNROLL_24>(L, a, b, a.rec.recs, wave, nwaves, nrb, rb, (uint32_t)sub, shift, claims);
-  long_stream(L, a, b, wave, nwaves, nrb, rb, (uint32_t)sub, shift, claims);
+  __syncthreads();  // every LONG record is queued (or counted past the queue)
+  if (L.nlong) {
+    if (L.nlong <= LONGQ) long_queue(L, a, b, L.nlong, claims);
+    else long_stream(L, a, b, wave, nwaves, nrb, rb, (uint32_t)sub, shift, claims);
+  }
   for (int o = 32; o > 0; o >>= 1) claims += __shfl_down(claims, o);
   if ((tid & 63) == 0 && claims) atomicAdd(&L.occupied, claims);
   if (WC_RED_STAMPS && (tid & 63) == 0)
@@ -484,6 +564,7 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
     }
     return;
   }
+  settle_new_long(L, a, b);
   store_slice(L, a.tab, b);
   if (tid == 0) {
     a.tab.occupancy[b] = L.occupied;

@@ -137,16 +137,33 @@ __global__ void __launch_bounds__(OS_THREADS) wc_os_pass(const uint64_t* keys, c
       __hip_atomic_store(my, OS_INC | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       __hip_atomic_store(my, OS_AGG | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (uint32_t t = tile - 1;;) {
-        const uint32_t f =
-            __hip_atomic_load(look + (size_t)t * OS_BINS + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (f == 0) {
-          __builtin_amdgcn_s_sleep(1);
-          continue;  // tile t started earlier (tiles are taken in order) and publishes soon
+      // the flags of up to OS_LB predecessors are loaded together (one round
+      // trip, not one per tile), then consumed newest first: aggregates add up
+      // until the first inclusive word; an unpublished tile (0) is re-read
+      constexpr int OS_LB = 16;
+      int t = (int)tile - 1;
+      for (;;) {
+        uint32_t f[OS_LB];
+#pragma unroll
+        for (int q = 0; q < OS_LB; ++q)
+          f[q] = t - q >= 0 ? __hip_atomic_load(look + (size_t)(t - q) * OS_BINS + tid, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT)
+                            : OS_INC;  // never reached: tile 0 is inclusive
+        int used = OS_LB;
+        bool done = false;
+#pragma unroll
+        for (int q = 0; q < OS_LB; ++q) {
+          if (done || used < OS_LB) continue;
+          if (f[q] == 0) {
+            used = q;  // tile t - q started earlier (tiles are taken in order) and publishes soon
+          } else {
+            excl += f[q] & OS_VAL;
+            done = (f[q] & OS_INC) != 0;
+          }
         }
-        excl += f & OS_VAL;
-        if (f & OS_INC) break;
-        --t;
+        if (done) break;
+        t -= used;
+        if (used < OS_LB) __builtin_amdgcn_s_sleep(1);
       }
       __hip_atomic_store(my, OS_INC | (excl + acc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
