@@ -35,6 +35,8 @@ int wc_device_count(void);
  * `device`; returns the sorted keys and the permutation (host arrays). */
 int wc_debug_radix_sort(int device, const uint64_t* keys, uint64_t n, int bits, uint64_t* sorted, uint32_t* perm);
 int wc_bench_radix_sort(int device, const uint64_t* keys, uint64_t n, int bits, int reps, double* ms);
+int wc_debug_first_order(int device, const uint64_t* keys, uint64_t n, int reps, uint64_t* sorted, uint32_t* perm,
+                         int* overflow, double* ms);
 void wc_default_options(wc_options* o);
 
 wc_engine* wc_engine_create(const wc_options* o);

@@ -31,6 +31,11 @@ struct Stats {
   uint32_t map_reruns = 0;     // shuffle-region overflow -> chunk halved
   uint32_t table_splits = 0;   // running table grew B -> 2B
   uint32_t log2_buckets = 0;   // final table buckets
+  // first-occurrence order of the last finalize: 1 = sample sort, 2 = radix
+  // sort, 3 = sample sort overflowed and redone by the radix sort, 4 = the
+  // speculative finalize's sample sort (sized by the previous job) overflowed
+  // and the exact-count one did not
+  uint32_t order_path = 0;
   // Host wall clock of the last job's API calls (count_*, finalize / result).
   double host_count_ms = 0, host_finalize_ms = 0;
   // Device time of the last job's stages, from events on the engine stream

@@ -1,5 +1,6 @@
 // capi.cpp — C ABI over the C++ engine (ctypes binding of the Python package).
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <exception>
 #include <memory>
@@ -151,6 +152,106 @@ int wc_bench_radix_sort(int device, const uint64_t* keys, uint64_t n, int bits, 
   });
 }
 
+// first_order (the three-launch sample sort) on n UNIQUE given keys as a key
+// column source: sorted keys, the permutation (source row of each output row)
+// and the overflow word; *ms = device time averaged over `reps` (> 1: the
+// first rep warms up).  Tests + tools/sort_bench.py.
+int wc_debug_first_order(int device, const uint64_t* keys, uint64_t n, int reps, uint64_t* sorted, uint32_t* perm,
+                         int* overflow, double* ms) {
+  return guard([&] {
+    WC_HIP_CHECK(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    const size_t nn = n ? n : 1;
+    wc::OrderSrc src{};
+    src.table = false;
+    src.n = n;
+    const size_t ws = wc::first_order_ws_bytes(src, n);
+    uint8_t* mem = nullptr;
+    WC_HIP_CHECK(hipMalloc(&mem, nn * (8 * 5 + 4) * 2 + ws + 4096));
+    uint8_t* p = mem;
+    auto take = [&](size_t b) {
+      uint8_t* r = p;
+      p += (b + 255) / 256 * 256;
+      return r;
+    };
+    uint64_t* in[5];
+    for (auto& c : in) c = reinterpret_cast<uint64_t*>(take(nn * 8));
+    uint32_t* in_len = reinterpret_cast<uint32_t*>(take(nn * 4));
+    wc::OrderDst d{};
+    d.k0 = reinterpret_cast<uint64_t*>(take(nn * 8));
+    d.k1 = reinterpret_cast<uint64_t*>(take(nn * 8));
+    d.cnt = reinterpret_cast<uint64_t*>(take(nn * 8));
+    d.first = reinterpret_cast<uint64_t*>(take(nn * 8));
+    d.soff = reinterpret_cast<uint64_t*>(take(nn * 8));
+    d.slen = reinterpret_cast<uint32_t*>(take(nn * 4));
+    void* w = take(ws);
+    std::vector<uint64_t> idx(nn);
+    uint64_t kmax = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+      idx[i] = i;
+      kmax = std::max(kmax, keys[i]);
+    }
+    uint32_t kb = 1;
+    while (kb < 64 && (kmax >> kb) != 0) ++kb;
+    WC_HIP_CHECK(hipMemcpy(in[0], idx.data(), n * 8, hipMemcpyHostToDevice));  // k0 = the source row
+    WC_HIP_CHECK(hipMemset(in[1], 0, nn * 8));
+    WC_HIP_CHECK(hipMemset(in[2], 0, nn * 8));
+    WC_HIP_CHECK(hipMemcpy(in[3], keys, n * 8, hipMemcpyHostToDevice));
+    WC_HIP_CHECK(hipMemset(in[4], 0, nn * 8));
+    WC_HIP_CHECK(hipMemset(in_len, 0, nn * 4));
+    src.k0 = in[0];
+    src.k1 = in[1];
+    src.cnt = in[2];
+    src.first = in[3];
+    src.soff = in[4];
+    src.slen = in_len;
+    hipEvent_t e0, e1;
+    WC_HIP_CHECK(hipEventCreate(&e0));
+    WC_HIP_CHECK(hipEventCreate(&e1));
+    float total = 0;
+    uint32_t* ovf = nullptr;
+    unsigned long long* d_st = nullptr;
+    const bool stamps = std::getenv("WC_FO_STAMPS") != nullptr;
+    if (stamps) {
+      WC_HIP_CHECK(hipMalloc(&d_st, 48 * 8));
+      WC_HIP_CHECK(hipMemset(d_st, 0, 48 * 8));
+      wc::first_order_stamps(d_st);
+    }
+    for (int r = 0; r < std::max(reps, 1); ++r) {
+      WC_HIP_CHECK(hipEventRecord(e0, s));
+      if (n) ovf = wc::first_order(src, d, n, kb, w, nullptr, s);
+      WC_HIP_CHECK(hipEventRecord(e1, s));
+      WC_HIP_CHECK(hipEventSynchronize(e1));
+      float t = 0;
+      WC_HIP_CHECK(hipEventElapsedTime(&t, e0, e1));
+      if (r > 0 || reps <= 1) total += t;
+    }
+    *ms = total / (reps > 1 ? reps - 1 : 1);
+    if (stamps) {  // max over reps and blocks, 100 MHz ticks -> us
+      unsigned long long h[48];
+      WC_HIP_CHECK(hipMemcpy(h, d_st, sizeof h, hipMemcpyDeviceToHost));
+      wc::first_order_stamps(nullptr);
+      WC_HIP_CHECK(hipFree(d_st));
+      const char* nm[3] = {"split", "bin", "sort"};
+      for (int k = 0; k < 3; ++k) {
+        std::fprintf(stderr, "fo %-5s n=%llu phase us:", nm[k], (unsigned long long)n);
+        for (int p = 1; p < 6; ++p) std::fprintf(stderr, " %.2f", h[16 * k + p] / 100.0);
+        std::fprintf(stderr, "\n");
+      }
+    }
+    uint32_t o = 0;
+    if (ovf) WC_HIP_CHECK(hipMemcpy(&o, ovf, 4, hipMemcpyDeviceToHost));
+    *overflow = (int)o;
+    std::vector<uint64_t> k0(nn);
+    WC_HIP_CHECK(hipMemcpy(sorted, d.first, n * 8, hipMemcpyDeviceToHost));
+    WC_HIP_CHECK(hipMemcpy(k0.data(), d.k0, n * 8, hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < n; ++i) perm[i] = (uint32_t)k0[i];
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    WC_HIP_CHECK(hipFree(mem));
+  });
+}
+
 int wc_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -266,12 +367,13 @@ int wc_engine_stats_json(wc_engine* e, char* buf, int cap) {
   char tmp[1024];
   const int k = snprintf(tmp, sizeof tmp,
                          "{\"bytes\": %llu, \"tokens\": %llu, \"keys\": %llu, \"records\": %llu, \"chunks\": %u, "
-                         "\"map_reruns\": %u, \"table_splits\": %u, \"log2_buckets\": %u, "
+                         "\"map_reruns\": %u, \"table_splits\": %u, \"log2_buckets\": %u, \"order_path\": %u, "
                          "\"device_ms\": {\"map\": %.4f, \"reduce\": %.4f, \"finalize\": %.4f, \"merge\": %.4f, "
                          "\"idle\": %.4f, \"total\": %.4f}, "
                          "\"host_ms\": {\"count\": %.4f, \"finalize\": %.4f}}",
                          (unsigned long long)s.bytes, (unsigned long long)s.tokens, (unsigned long long)s.keys,
-                         (unsigned long long)s.records, s.chunks, s.map_reruns, s.table_splits, s.log2_buckets, s.map_ms,
+                         (unsigned long long)s.records, s.chunks, s.map_reruns, s.table_splits, s.log2_buckets, s.order_path,
+                         s.map_ms,
                          s.reduce_ms, s.finalize_ms, s.merge_ms, s.idle_ms, s.device_ms, s.host_count_ms,
                          s.host_finalize_ms);
   if (buf && cap > 0) {

@@ -64,6 +64,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   if (const char* e = std::getenv("WC_NO_SPECULATE")) speculate = std::atoi(e) == 0;
   if (const char* e = std::getenv("WC_SPIN_WAIT")) spin_wait = std::atoi(e) != 0;
   if (const char* e = std::getenv("WC_STAGE_EVENTS")) stage_events = std::atoi(e) != 0;
+  if (const char* e = std::getenv("WC_FIRST_ORDER")) order_radix = std::string(e) == "radix";
   if (const char* e = std::getenv("WC_HOT_RESAMPLE_EVERY")) hot_resample_every = (uint32_t)std::atoi(e);
   k1_mask = k1_hash_mask(opt.k1_hash_bits);
   if (const char* e = std::getenv("WC_MAP_STAMPS"); e && std::atoi(e)) {
@@ -552,16 +553,16 @@ bool Engine::Impl::finalize_local_speculative() {
   const size_t nb = (size_t)1 << t.log2_buckets;
   const uint64_t cap = (uint64_t)nb * TAB_SLOTS;
   const uint64_t hint = std::min<uint64_t>(cap, last_keys ? last_keys + last_keys / 8 + 1024 : cap / 4);
+  const bool sample = sample_order(hint);  // sized for the hint; a far larger count -> overflow -> redo
+  OrderSrc src{};
+  src.table = true;
+  src.t = t;
   DeviceArena& A = sort_mem;
-  A.reserve((cap + 1) * (2 * 8 + 2 * 4 + 5 * 8 + 4) + nb * 8 + radix_hist_words(cap, hint) * 4 + 64 * 1024);
+  A.reserve((cap + 1) * (5 * 8 + 4) + 64 * 1024 +
+            (sample ? first_order_ws_bytes(src, hint)
+                    : (cap + 1) * (2 * 8 + 2 * 4) + nb * 8 + radix_hist_words(cap, hint) * 4));
   A.reset();
-  uint64_t* d_boff = A.take_n<uint64_t>(nb);
   uint64_t* d_n = A.take_n<uint64_t>(2);
-  uint64_t* keys = A.take_n<uint64_t>(cap + 1);
-  uint64_t* tkeys = A.take_n<uint64_t>(cap + 1);
-  uint32_t* slots = A.take_n<uint32_t>(cap + 1);
-  uint32_t* tslots = A.take_n<uint32_t>(cap + 1);
-  uint32_t* hist = A.take_n<uint32_t>(radix_hist_words(cap, hint));
   KeyCols o;
   o.k0 = A.take_n<uint64_t>(cap + 1);
   o.k1 = A.take_n<uint64_t>(cap + 1);
@@ -569,14 +570,26 @@ bool Engine::Impl::finalize_local_speculative() {
   o.first = A.take_n<uint64_t>(cap + 1);
   o.sref_off = A.take_n<uint64_t>(cap + 1);
   o.sref_len = A.take_n<uint32_t>(cap + 1);
-  launch_bucket_offsets(t.occupancy, (uint32_t)nb, d_boff, d_n, s);
-  launch_table_keys(t, d_boff, keys, slots, s);
-  int bits = 1;
-  while (bits < 64 && (max_end >> bits) != 0) ++bits;
-  bool in_tmp = false;
-  radix_sort_pairs(keys, slots, tkeys, tslots, hist, cap, bits, s, &in_tmp, d_n, hint);
-  launch_gather_table(t, in_tmp ? tkeys : keys, in_tmp ? tslots : slots, cap, o.k0, o.k1, o.cnt, o.first, o.sref_off,
-                      o.sref_len, s, d_n);
+  uint32_t* ovf = nullptr;
+  if (sample) {
+    ovf = first_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len}, hint, key_bits(),
+                      A.take_n<uint8_t>(first_order_ws_bytes(src, hint)), d_n, s);
+  } else {
+    uint64_t* d_boff = A.take_n<uint64_t>(nb);
+    uint64_t* keys = A.take_n<uint64_t>(cap + 1);
+    uint64_t* tkeys = A.take_n<uint64_t>(cap + 1);
+    uint32_t* slots = A.take_n<uint32_t>(cap + 1);
+    uint32_t* tslots = A.take_n<uint32_t>(cap + 1);
+    uint32_t* hist = A.take_n<uint32_t>(radix_hist_words(cap, hint));
+    launch_bucket_offsets(t.occupancy, (uint32_t)nb, d_boff, d_n, s);
+    launch_table_keys(t, d_boff, keys, slots, s);
+    int bits = 1;
+    while (bits < 64 && (max_end >> bits) != 0) ++bits;
+    bool in_tmp = false;
+    radix_sort_pairs(keys, slots, tkeys, tslots, hist, cap, bits, s, &in_tmp, d_n, hint);
+    launch_gather_table(t, in_tmp ? tkeys : keys, in_tmp ? tslots : slots, cap, o.k0, o.k1, o.cnt, o.first,
+                        o.sref_off, o.sref_len, s, d_n);
+  }
   if (h_spec.size() < 32) {
     h_spec.resize(4096);
     std::memset(h_spec.data(), 0, h_spec.size());  // the sequence word starts below every spec_seq
@@ -587,6 +600,9 @@ bool Engine::Impl::finalize_local_speculative() {
   pc.add(h_spec.data(), d_n, 8);
   pc.add(h_spec.data() + 8, d_arena_cursor, 8);
   uint32_t* seq = reinterpret_cast<uint32_t*>(h_spec.data() + 16);
+  uint32_t* h_ovf = reinterpret_cast<uint32_t*>(h_spec.data() + 24);
+  *h_ovf = 0;
+  if (ovf) pc.add(h_ovf, ovf, 4);
   if (spin_wait) {
     pc.seq_dst = seq;
     pc.seq = ++spec_seq;
@@ -596,6 +612,13 @@ bool Engine::Impl::finalize_local_speculative() {
   else WC_HIP_CHECK(hipStreamSynchronize(s));
   // the pass's counters arrived with this sync: check it (stats, recovery)
   if (!complete_pass(p.text, p.len, p.avail, p.base, p.prev, p.rb, p.blocks, true)) return false;
+  if (*h_ovf) {  // a sample-sort bin overflowed (far more keys than the hint): redo exactly
+    WC_LOG(LOG_INFO, "dev %d: first-occurrence sample sort overflowed (hint %llu keys); redoing", dev,
+           (unsigned long long)hint);
+    last_keys = 0;
+    order_redo = true;
+    return false;
+  }
   uint64_t n = 0, arena_used = 0;
   std::memcpy(&n, h_spec.data(), 8);
   std::memcpy(&arena_used, h_spec.data() + 8, 8);
@@ -605,6 +628,7 @@ bool Engine::Impl::finalize_local_speculative() {
   cols_arena_bytes = std::min<uint64_t>(arena_used, opt.arena_bytes);
   st.keys = n;
   st.log2_buckets = t.log2_buckets;
+  st.order_path = sample ? 1 : 2;
   last_keys = n;
   return true;
 }
@@ -617,30 +641,52 @@ void Engine::Impl::finalize_local_sorted() {
   uint64_t arena_used = 0;
   const uint64_t n = host_occupancy(boff, arena_used);
   DeviceArena& A = sort_mem;
-  A.reserve((n + 1) * (2 * 8 + 2 * 4 + 5 * 8 + 4) + nb * 8 + radix_hist_words(n) * 4 + 64 * 1024);
-  A.reset();
-  uint64_t* d_boff = A.take_n<uint64_t>(nb);
-  uint64_t* keys = A.take_n<uint64_t>(n + 1);
-  uint64_t* tkeys = A.take_n<uint64_t>(n + 1);
-  uint32_t* slots = A.take_n<uint32_t>(n + 1);
-  uint32_t* tslots = A.take_n<uint32_t>(n + 1);
-  uint32_t* hist = A.take_n<uint32_t>(radix_hist_words(n));
   KeyCols o;
-  o.k0 = A.take_n<uint64_t>(n + 1);
-  o.k1 = A.take_n<uint64_t>(n + 1);
-  o.cnt = A.take_n<uint64_t>(n + 1);
-  o.first = A.take_n<uint64_t>(n + 1);
-  o.sref_off = A.take_n<uint64_t>(n + 1);
-  o.sref_len = A.take_n<uint32_t>(n + 1);
-  o.n = n;
-  WC_HIP_CHECK(hipMemcpyAsync(d_boff, boff, nb * 8, hipMemcpyHostToDevice, s));  // pinned: no sync needed
-  launch_table_keys(t, d_boff, keys, slots, s);
-  int bits = 1;
-  while (bits < 64 && (max_end >> bits) != 0) ++bits;
-  bool in_tmp = false;
-  radix_sort_pairs(keys, slots, tkeys, tslots, hist, n, bits, s, &in_tmp);
-  launch_gather_table(t, in_tmp ? tkeys : keys, in_tmp ? tslots : slots, n, o.k0, o.k1, o.cnt, o.first, o.sref_off,
-                      o.sref_len, s);
+  auto take_cols = [&] {
+    o.k0 = A.take_n<uint64_t>(n + 1);
+    o.k1 = A.take_n<uint64_t>(n + 1);
+    o.cnt = A.take_n<uint64_t>(n + 1);
+    o.first = A.take_n<uint64_t>(n + 1);
+    o.sref_off = A.take_n<uint64_t>(n + 1);
+    o.sref_len = A.take_n<uint32_t>(n + 1);
+    o.n = n;
+  };
+  st.order_path = 2;
+  if (sample_order(n)) {
+    OrderSrc src{};
+    src.table = true;
+    src.t = t;
+    A.reserve((n + 1) * (5 * 8 + 4) + first_order_ws_bytes(src, n) + 64 * 1024);
+    A.reset();
+    take_cols();
+    const uint32_t* ovf = first_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len}, n,
+                                      key_bits(), A.take_n<uint8_t>(first_order_ws_bytes(src, n)), nullptr, s);
+    if (h_fin.size() < 64) h_fin = PinnedBuffer(64);
+    WC_HIP_CHECK(hipMemcpyAsync(h_fin.data() + 8, ovf, 4, hipMemcpyDeviceToHost, s));
+    WC_HIP_CHECK(hipStreamSynchronize(s));  // the fallback path: one more wait is fine
+    uint32_t bad = 0;
+    std::memcpy(&bad, h_fin.data() + 8, 4);
+    st.order_path = bad ? 3 : 1;
+  }
+  if (st.order_path != 1) {
+    A.reserve((n + 1) * (2 * 8 + 2 * 4 + 5 * 8 + 4) + nb * 8 + radix_hist_words(n) * 4 + 64 * 1024);
+    A.reset();
+    uint64_t* d_boff = A.take_n<uint64_t>(nb);
+    uint64_t* keys = A.take_n<uint64_t>(n + 1);
+    uint64_t* tkeys = A.take_n<uint64_t>(n + 1);
+    uint32_t* slots = A.take_n<uint32_t>(n + 1);
+    uint32_t* tslots = A.take_n<uint32_t>(n + 1);
+    uint32_t* hist = A.take_n<uint32_t>(radix_hist_words(n));
+    take_cols();
+    WC_HIP_CHECK(hipMemcpyAsync(d_boff, boff, nb * 8, hipMemcpyHostToDevice, s));  // pinned: no sync needed
+    launch_table_keys(t, d_boff, keys, slots, s);
+    int bits = 1;
+    while (bits < 64 && (max_end >> bits) != 0) ++bits;
+    bool in_tmp = false;
+    radix_sort_pairs(keys, slots, tkeys, tslots, hist, n, bits, s, &in_tmp);
+    launch_gather_table(t, in_tmp ? tkeys : keys, in_tmp ? tslots : slots, n, o.k0, o.k1, o.cnt, o.first,
+                        o.sref_off, o.sref_len, s);
+  }
   cols = o;
   cols_arena = d_arena;
   cols_arena_bytes = std::min<uint64_t>(arena_used, opt.arena_bytes);
@@ -649,11 +695,47 @@ void Engine::Impl::finalize_local_sorted() {
   last_keys = n;
 }
 
-void Engine::Impl::sort_cols_by_first() {
+void Engine::Impl::sort_cols_by_first(bool radix) {
   Range r("wc_finalize_sort");
+  fo_ovf = nullptr;
   const uint64_t n = cols.n;
   if (n == 0) return;
+  // cols.dn: the count is on the device (n its bound) — sort and gather on it
+  const uint64_t* dn = reinterpret_cast<const uint64_t*>(cols.dn);
   DeviceArena& A = sort_mem;
+  KeyCols o;
+  auto take_cols = [&] {
+    o.k0 = A.take_n<uint64_t>(n);
+    o.k1 = A.take_n<uint64_t>(n);
+    o.cnt = A.take_n<uint64_t>(n);
+    o.first = A.take_n<uint64_t>(n);
+    o.sref_off = A.take_n<uint64_t>(n);
+    o.sref_len = A.take_n<uint32_t>(n);
+    o.n = n;
+    o.dn = cols.dn;
+  };
+  if (!radix && sample_order(n)) {
+    // the overflow word is read at the finalize's last wait (a rare radix redo follows)
+    OrderSrc src{};
+    src.table = false;
+    src.k0 = cols.k0;
+    src.k1 = cols.k1;
+    src.cnt = cols.cnt;
+    src.first = cols.first;
+    src.soff = cols.sref_off;
+    src.slen = cols.sref_len;
+    src.n = n;
+    src.dn = dn;
+    A.reserve(n * (5 * 8 + 4) + first_order_ws_bytes(src, n) + 64 * 1024);
+    A.reset();
+    take_cols();
+    fo_ovf = first_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len}, n, key_bits(),
+                         A.take_n<uint8_t>(first_order_ws_bytes(src, n)), nullptr, s);
+    cols_unsorted = cols;
+    cols = o;
+    st.order_path = 1;
+    return;
+  }
   A.reserve(n * (2 * 8 + 2 * 4 + 5 * 8 + 4) + radix_hist_words(n) * 4 + 64 * 1024);
   A.reset();
   uint64_t* keys = A.take_n<uint64_t>(n);
@@ -661,26 +743,17 @@ void Engine::Impl::sort_cols_by_first() {
   uint32_t* vals = A.take_n<uint32_t>(n);
   uint32_t* tvals = A.take_n<uint32_t>(n);
   uint32_t* hist = A.take_n<uint32_t>(radix_hist_words(n));
-  KeyCols o;
-  o.k0 = A.take_n<uint64_t>(n);
-  o.k1 = A.take_n<uint64_t>(n);
-  o.cnt = A.take_n<uint64_t>(n);
-  o.first = A.take_n<uint64_t>(n);
-  o.sref_off = A.take_n<uint64_t>(n);
-  o.sref_len = A.take_n<uint32_t>(n);
-  o.n = n;
+  take_cols();
   WC_HIP_CHECK(hipMemcpyAsync(keys, cols.first, n * 8, hipMemcpyDeviceToDevice, s));
   launch_iota_u32(vals, n, s);
   int bits = 1;
   while (bits < 64 && (max_end >> bits) != 0) ++bits;
-  // cols.dn: the count is on the device (n its bound) — sort and gather on it
-  const uint64_t* dn = reinterpret_cast<const uint64_t*>(cols.dn);
   bool in_tmp = false;
   radix_sort_pairs(keys, vals, tkeys, tvals, hist, n, bits, s, &in_tmp, dn, dn ? n : 0);
   launch_gather_cols(cols.k0, cols.k1, cols.cnt, cols.first, cols.sref_off, cols.sref_len, in_tmp ? tvals : vals, o.k0,
                      o.k1, o.cnt, o.first, o.sref_off, o.sref_len, n, s, dn);
-  o.dn = cols.dn;
   cols = o;
+  st.order_path = radix ? 3 : 2;
 }
 
 KeyTable Engine::Impl::download_cols() {
@@ -994,6 +1067,8 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
   im.apply_reset();  // a reset with no pass since: the table reads empty
   im.mark(EV_FIN);
   im.fin_end_marked = false;
+  im.fo_ovf = nullptr;
+  im.order_redo = false;
   bool drained = false;
   if (merged) {
     const bool spec = im.pend.active && im.speculate && !im.sync_debug && merge_cols_speculative(im, *comm, all_ranks);
@@ -1011,17 +1086,31 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
     im.fin_end_marked = false;  // a speculative finalize that needed recovery is redone here
     im.settle();
     im.finalize_local_sorted();  // sort (first, slot) pairs, gather the columns from the table once
+    if (im.order_redo && im.st.order_path == 1) im.st.order_path = 4;
   }
   if (!im.fin_end_marked) im.mark(EV_FIN_END);
-  if (im.cols.dn) {  // the merged count is still on the device: publish it with the last wait
+  // the merged count still on the device and the sample sort's overflow word:
+  // published with the last wait
+  if (im.cols.dn || im.fo_ovf) {
     if (im.h_fin.size() < 64) im.h_fin = PinnedBuffer(64);
     PubList pc{};
-    pc.add(im.h_fin.data(), im.cols.dn, 8);
+    if (im.cols.dn) pc.add(im.h_fin.data(), im.cols.dn, 8);
+    if (im.fo_ovf) pc.add(im.h_fin.data() + 8, im.fo_ovf, 4);
     launch_publish(pc, im.s);
   }
   // the merge's last collectives are still in flight: wait under the comm watchdog
   if (merged) comm->sync(im.s);
   else if (!drained) WC_HIP_CHECK(hipStreamSynchronize(im.s));
+  if (im.fo_ovf) {
+    uint32_t bad = 0;
+    std::memcpy(&bad, im.h_fin.data() + 8, 4);
+    im.fo_ovf = nullptr;
+    if (bad) {  // a sample-sort bin overflowed: redo the order with the radix sort (its input is intact)
+      im.cols = im.cols_unsorted;
+      im.sort_cols_by_first(true);
+      WC_HIP_CHECK(hipStreamSynchronize(im.s));
+    }
+  }
   if (im.cols.dn) {
     uint64_t g = 0;
     std::memcpy(&g, im.h_fin.data(), 8);

@@ -121,6 +121,11 @@ struct Engine::Impl {
   uint8_t* cols_arena = nullptr;   // arena the sref_* of cols point into
   uint64_t cols_arena_bytes = 0;
   uint64_t max_end = 0;  // max global byte offset seen (sort key width)
+  uint32_t key_bits() const {  // first offsets are < max_end < 2^key_bits
+    uint32_t b = 1;
+    while (b < 64 && (max_end >> b) != 0) ++b;
+    return b;
+  }
 
   explicit Impl(const Options& o);
   ~Impl();
@@ -187,7 +192,15 @@ struct Engine::Impl {
   void compact_local();                     // table -> cols (unsorted)
   void finalize_local_sorted();             // table -> cols ordered by first (no merge: no column copy)
   bool finalize_local_speculative();        // same behind a pending pass; false: redo after its recovery
-  void sort_cols_by_first();                // cols ordered by first occurrence
+  void sort_cols_by_first(bool radix = false);  // cols ordered by first occurrence
+  // First-occurrence order: the three-launch sample sort (first_order) up to
+  // FO_MAX_KEYS keys, the onesweep radix sort above it, after a sample-sort
+  // overflow, or always with WC_FIRST_ORDER=radix.
+  bool order_radix = false;
+  bool sample_order(uint64_t bound) const { return !order_radix && bound <= FO_MAX_KEYS; }
+  uint32_t* fo_ovf = nullptr;  // overflow word of the sample sort sort_cols_by_first left in flight
+  KeyCols cols_unsorted;       // its input, kept for a radix redo
+  bool order_redo = false;     // the speculative finalize's sample sort overflowed (Stats::order_path 4)
   KeyTable download_cols();
 };
 

@@ -201,6 +201,33 @@ void launch_gather_table(const TableView& t, const uint64_t* keys, const uint32_
 // key count *n (the speculative finalize: no host round trip after the pass).
 void launch_bucket_offsets(const uint32_t* occupancy, uint32_t nb, uint64_t* bucket_off, uint64_t* n, hipStream_t s);
 
+// First-occurrence order (sort.hip: a three-launch sample sort of UNIQUE
+// keys): rows ordered by first offset, the six output columns written straight
+// from the source — the table's slots (`table`: the single-GPU finalize) or
+// key columns (the merged table, n rows or *dn with n the bound).  `bound` >=
+// the key count; keys < 2^key_bits set the log-bin resolution (a larger key is
+// still ordered); ws = first_order_ws_bytes(src, bound) bytes; *nout (if
+// given) = the key count.  Returns a device word that is nonzero after the stream if a bin
+// overflowed: the output is then invalid and the caller redoes it with
+// radix_sort_pairs (~1e-4 per call for hash-ordered sources).
+struct OrderSrc {
+  bool table;
+  TableView t;
+  const uint64_t *k0, *k1, *cnt, *first, *soff;
+  const uint32_t* slen;
+  uint64_t n;
+  const uint64_t* dn;
+};
+struct OrderDst {
+  uint64_t *k0, *k1, *cnt, *first, *soff;
+  uint32_t* slen;
+};
+constexpr uint64_t FO_MAX_KEYS = 512 * 1000;  // 8x the mean bin still fits the largest (8192-row) LDS bin
+size_t first_order_ws_bytes(const OrderSrc& src, uint64_t bound);
+void first_order_stamps(unsigned long long* d);  // debug: phase clocks of the three kernels (nullptr: off)
+uint32_t* first_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, uint32_t key_bits, void* ws,
+                      uint64_t* nout, hipStream_t s);
+
 // out[i] = in[perm[i]] for the six key-table columns (one launch).
 void launch_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
                         const uint64_t* soff, const uint32_t* slen, const uint32_t* perm, uint64_t* ok0, uint64_t* ok1,

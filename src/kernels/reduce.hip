@@ -191,6 +191,57 @@ __device__ __forceinline__ bool long_equal(const LongCtx& c, uint64_t o, uint64_
   return o + len == c.avail_len || is_delim(c.text[o + len]);
 }
 
+// The first 64 bytes at text offset o as eight words, loaded together (one
+// memory round trip; past the readable text they read as delimiters), and the
+// length of the word there (64: the word is longer).
+__device__ __forceinline__ uint32_t load_word64(const LongCtx& c, uint64_t o, uint64_t (&w)[8]) {
+  if (o + 64 <= c.avail_len) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) __builtin_memcpy(&w[i], c.text + o + 8 * i, 8);
+  } else {  // the last 64 bytes of the readable text (rare): byte by byte
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = 0x2020202020202020ull;
+#pragma unroll 1
+    for (uint32_t k = 0; k < 64 && o + k < c.avail_len; ++k) {
+      const uint64_t x = c.text[o + k];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if ((int)(k >> 3) == i) w[i] = (w[i] & ~(0xFFull << (8 * (k & 7)))) | (x << (8 * (k & 7)));
+    }
+  }
+  uint32_t len = 64;
+#pragma unroll
+  for (int i = 7; i >= 0; --i) {
+    const uint64_t m = delim_mask8(w[i]);
+    if (m) len = 8 * i + (uint32_t)__ffsll((unsigned long long)m) - 1;
+  }
+  return len;
+}
+
+// The record's word (first 64 bytes in w, length wlen < 64) == the stored
+// word (sref so, sl)?  The stored copy's words are loaded together.
+__device__ __forceinline__ bool long_equal64(const LongCtx& c, const uint64_t (&w)[8], uint32_t wlen, uint64_t so,
+                                             uint32_t sl) {
+  if (sl != wlen) return false;
+  const bool in_text = (so & SREF_TEXT) != 0;
+  const uint8_t* ref = in_text ? c.text + (so & ~SREF_TEXT) : c.arena + so;
+  uint64_t r[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    r[i] = 0;
+    if (8 * i < (int)sl) __builtin_memcpy(&r[i], ref + 8 * i, 8);  // the word's last 8-byte piece may read past it
+  }
+  bool eq = true;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (8 * i >= (int)sl) continue;
+    const uint32_t n = sl - 8 * i;
+    const uint64_t m = n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1ull);
+    eq &= ((w[i] ^ r[i]) & m) == 0;
+  }
+  return eq;
+}
+
 // A LONG record (hashed key): find the slot whose stored word equals the
 // record's word byte for byte, or claim one.  Colliding words (same k0, k1,
 // different bytes) keep separate slots, so the probe continues past a slot
@@ -200,7 +251,7 @@ __device__ __forceinline__ bool long_equal(const LongCtx& c, uint64_t o, uint64_
 // a published tag acquires before reading the reference.  Probers that see
 // PENDING re-read the group; the claimer finishes inside its iteration, so
 // the lanes of one wave never wait on each other.  Returns 1 for a claim.
-__device__ __noinline__ uint32_t merge_long(RedLds& L, LongCtx c, uint32_t ph, uint64_t k0, uint64_t k1, uint64_t cnt,
+__device__ __forceinline__ uint32_t merge_long(RedLds& L, const LongCtx& c, uint32_t ph, uint64_t k0, uint64_t k1, uint64_t cnt,
                                             uint64_t first, uint64_t off) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const uint32_t tag = make_tag(ph);
@@ -208,6 +259,9 @@ __device__ __noinline__ uint32_t merge_long(RedLds& L, LongCtx c, uint32_t ph, u
   uint32_t g = g1;
   int steps = 0;
   if (WC_RED_STAMPS) atomicAdd(&L.st[RS_SLOW_LANES], 1ull);
+  // the record's bytes, before the probe needs them (their loads overlap it)
+  uint64_t w[8];
+  const uint32_t wlen = load_word64(c, off, w);
   for (;;) {
     asm volatile("" ::: "memory");
     SlotGroup& G = L.grp[g];
@@ -215,20 +269,23 @@ __device__ __noinline__ uint32_t merge_long(RedLds& L, LongCtx c, uint32_t ph, u
     const uint32_t tv[4] = {t.x, t.y, t.z, t.w};
     bool pending = false;
     int e = -1;
+    uint32_t mm = 0;  // slots holding this key (several only for colliding words)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      if (tv[i] == TAG_PENDING) {
-        pending = true;
-      } else if (tv[i] == TAG_EMPTY) {
-        if (e < 0) e = i;
-      } else if (tv[i] == tag && G.k1[i] == k1 && G.k0[i] == k0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        const int s = 4 * (int)g + i;
-        const uint32_t sl = c.sref_len[s];
-        if (sl == SREF_POISON || long_equal(c, off, c.sref_off[s], sl)) {
-          add_to_slot(L, s, cnt, first);
-          return 0;
-        }
+      if (tv[i] == TAG_PENDING) pending = true;
+      else if (tv[i] == TAG_EMPTY) e = e < 0 ? i : e;
+      else if (tv[i] == tag && G.k1[i] == k1 && G.k0[i] == k0) mm |= 1u << i;
+    }
+    if (mm) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    while (mm) {  // one comparison in the loop body (registers), usually one pass
+      const int i = __ffs(mm) - 1;
+      mm &= mm - 1;
+      const int s = 4 * (int)g + i;
+      const uint32_t sl = c.sref_len[s];
+      const uint64_t so = c.sref_off[s];
+      if (sl == SREF_POISON || (wlen < 64 ? long_equal64(c, w, wlen, so, sl) : long_equal(c, off, so, sl))) {
+        add_to_slot(L, s, cnt, first);
+        return 0;
       }
     }
     if (WC_RED_STAMPS) atomicAdd(&L.st[RS_PROBE_ITERS], 1ull);
@@ -238,7 +295,7 @@ __device__ __noinline__ uint32_t merge_long(RedLds& L, LongCtx c, uint32_t ph, u
       const int s = 4 * (int)g + e;
       G.k0[e] = k0;
       G.k1[e] = k1;
-      const uint64_t len = word_len(c.text, c.avail_len, off);
+      const uint64_t len = wlen < 64 ? wlen : word_len(c.text, c.avail_len, off);
       c.sref_off[s] = SREF_TEXT | off;
       c.sref_len[s] = len < SREF_POISON ? (uint32_t)len : SREF_POISON;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -499,21 +556,52 @@ __device__ __forceinline__ void long_queue(RedLds& L, const ReduceArgs& a, uint3
 
 __device__ __forceinline__ void long_stream(RedLds& L, const ReduceArgs& a, uint32_t b, uint32_t wave, uint32_t nwaves,
                                             uint32_t nrb, uint32_t rb, uint32_t sub, uint32_t shift, uint32_t& claims) {
+  // the queue is unused on this path: each wave compacts its LONG records'
+  // indices into its 128-entry share of it and merges them 64 at a time (full
+  // lanes: a wave's 24-byte runs mix LONG with medium words and hot flushes)
+  static_assert(LONGQ >= 128 * (RED_THREADS / 64), "long_stream: 128 queue entries per wave");
   const uint32_t lane = threadIdx.x & 63;
+  uint32_t* wl = L.longq + wave * 128;
+  const size_t sbase = (size_t)b * TAB_SLOTS;
+  const LongCtx c{a.text, a.avail_len, a.arena.bytes, a.tab.sref_off + sbase, a.tab.sref_len + sbase};
+  auto wsync = [] {  // this wave's LDS writes visible to its other lanes
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  auto merge_first = [&](uint32_t k) {  // wl[0, k), one per lane
+    wsync();
+    if (lane < k) {
+      const Rec r = a.rec.recs[wl[lane]];
+      const uint32_t off = (uint32_t)r.co;
+      claims += merge_long(L, c, place_hash(r.k0, r.k1), r.k0, r.k1, r.co >> 32, a.chunk_base + off, off);
+    }
+    wsync();
+  };
+  uint32_t cnt = 0;  // wave-uniform
   for (uint32_t p = wave; p < a.map_blocks; p += nwaves) {
     const uint32_t n = min(L.runcnt[p] >> 16, sub);
-    const Rec* run = a.rec.recs + ((size_t)p * nrb + rb) * sub;
-    for (uint32_t i = lane; i < n; i += 64) {
-      const Rec r = run[i];
-      if (!key_is_hashed(r.k1)) continue;
-      const uint32_t ph = place_hash(r.k0, r.k1);
-      if (shift && bucket_of(ph, a.tab.log2_buckets) != b) continue;
-      const uint32_t off = (uint32_t)r.co;
-      const size_t sbase = (size_t)b * TAB_SLOTS;
-      const LongCtx c{a.text, a.avail_len, a.arena.bytes, a.tab.sref_off + sbase, a.tab.sref_len + sbase};
-      claims += merge_long(L, c, ph, r.k0, r.k1, r.co >> 32, a.chunk_base + off, off);
+    const uint32_t base = ((uint32_t)p * nrb + rb) * sub;
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      bool isl = false;
+      if (i < n) {
+        const Rec r = a.rec.recs[base + i];
+        isl = key_is_hashed(r.k1) && (!shift || bucket_of(place_hash(r.k0, r.k1), a.tab.log2_buckets) == b);
+      }
+      const uint64_t m = __ballot(isl);
+      if (isl) wl[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = base + i;
+      cnt += (uint32_t)__popcll(m);
+      if (cnt >= 64) {
+        merge_first(64);
+        const uint32_t rest = cnt - 64, moved = lane < rest ? wl[64 + lane] : 0u;
+        wsync();
+        if (lane < rest) wl[lane] = moved;
+        cnt = rest;
+      }
     }
   }
+  if (cnt) merge_first(cnt);
 }
 
 __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {

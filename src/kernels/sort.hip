@@ -18,6 +18,7 @@
 // (round 2: 12 — histogram, scan and scatter per pass).  Tiles of 8192 items
 // (1024-thread blocks) keep the look-back to a dozen hops at 1e5 keys.
 #include <algorithm>
+#include <cstdlib>
 #include <utility>
 
 #include "../common/hip_util.hpp"
@@ -186,6 +187,386 @@ __global__ void __launch_bounds__(OS_THREADS) wc_os_pass(const uint64_t* keys, c
   }
 }
 
+// ---- first-occurrence order: sample sort of UNIQUE keys, three launches ----
+// The keys are first offsets, distinct per word, so no stability is needed.
+// Sorting networks cost ~400-600 cycles per dependent phase on one CU
+// (tools/probe/clock_probe.hip: a 4096-key LDS bitonic sort takes 34 us, a
+// one-wave 512-key register sort 11 us), so no step here sorts with one:
+//   wc_fo_split  one block: a FO_SAMPLE-key sample (strided over the key
+//                column, or every occupied slot of windows spread over the
+//                table) histogrammed over log-scale value bins (exact below
+//                2^M, then 2^M bins per octave); a block scan turns the
+//                histogram into a monotone map log-bin -> one of FO_BINS bins
+//                holding ~1/FO_BINS of the sample each;
+//   wc_fo_bin    one block per 4096 source rows (a table bucket): every row ->
+//                its bin through the map (in LDS), the block's rows written to
+//                its own segment in bin order as 48-byte entries carrying the
+//                whole row, and per bin the block's count and local offset
+//                (bin-major matrices) — no global atomics;
+//   wc_fo_sort   one block per bin: its output offset = the sum of its column
+//                of local offsets, its rows gathered from every block's segment
+//                into LDS, each row's rank in the bin counted directly (small
+//                bins) or after a counting sort into value sub-buckets (larger
+//                ones), the six output columns written from the entries.
+// A bin above its LDS capacity (a pathological value distribution) raises *ovf
+// and the caller redoes the order with the radix sort.
+constexpr int FO_BINS = 512, FO_ROWS = 4096, FO_SAMPLE = 4096, FO_LOGBINS = 16384;
+constexpr uint32_t FO_RANK_MAX = 256;  // bins up to this size count ranks directly
+constexpr int FO_NSUB = 1024;          // value sub-buckets of a larger bin
+
+// WC_FO_STAMPS (debug API): per kernel K, [16 K + p] = the max over blocks of
+// the 100 MHz wall time from the block's start to its phase p.
+__device__ unsigned long long* fo_stamps = nullptr;
+struct FoClock {
+  uint64_t t0;
+  int k;
+  __device__ FoClock(int kernel) : t0(wall_clock64()), k(kernel) {}
+  __device__ void at(int p) {
+    if (fo_stamps && threadIdx.x == 0) atomicMax(&fo_stamps[16 * k + p], (unsigned long long)(wall_clock64() - t0));
+  }
+};
+
+struct alignas(16) FoEntry {
+  uint64_t first, k0, k1, cnt, soff;
+  uint32_t slen, pad;
+};
+static_assert(sizeof(FoEntry) == 48, "48-byte entries");
+
+// Log-scale value bin: k itself below 2^M, else 2^M bins per octave (monotone).
+__device__ __forceinline__ uint32_t fo_logbin(uint64_t k, uint32_t M) {
+  if (k < (1ull << M)) return (uint32_t)k;
+  const uint32_t e = 63u - (uint32_t)__clzll((long long)k);  // >= M
+  const uint32_t lb = ((e - M + 1u) << M) | (uint32_t)((k >> (e - M)) & ((1ull << M) - 1));
+  return min(lb, (uint32_t)FO_LOGBINS - 1);
+}
+
+// Block-wide exclusive scan of `n` (a multiple of T, or < T) LDS counters in
+// place, T threads; returns the total.  `ws`: T / 64 words of scratch.
+template <int T>
+__device__ __forceinline__ uint32_t lds_exclusive_scan(uint32_t* c, int n, uint32_t* ws) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int per = n >= T ? n / T : (tid < n ? 1 : 0);  // n < T: one counter on the first n threads
+  uint32_t own = 0;
+  for (int i = 0; i < per; ++i) own += c[tid * per + i];
+  uint32_t x = own;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) ws[wave] = x;
+  __syncthreads();
+  uint32_t before = 0, total = 0;
+  for (int w = 0; w < T / 64; ++w) {
+    before += w < wave ? ws[w] : 0u;
+    total += ws[w];
+  }
+  uint32_t run = before + x - own;
+  for (int i = 0; i < per; ++i) {
+    const uint32_t v = c[tid * per + i];
+    c[tid * per + i] = run;
+    run += v;
+  }
+  __syncthreads();
+  return total;
+}
+
+__global__ void __launch_bounds__(1024) wc_fo_split(OrderSrc src, uint32_t M, uint16_t* map, uint32_t* ctl) {
+  FoClock clk(0);
+  __shared__ uint32_t hist[FO_LOGBINS];
+  __shared__ uint32_t ws[16];
+  __shared__ uint32_t nvalid;
+  const uint32_t tid = threadIdx.x;
+  if (tid == 0) {
+    ctl[0] = 0;  // the overflow word
+    nvalid = 0;
+  }
+  for (int i = tid; i < FO_LOGBINS; i += 1024) hist[i] = 0;
+  __syncthreads();
+  clk.at(1);
+  constexpr int R = FO_SAMPLE / 1024;
+  if (src.table) {
+    // 1024 windows of 16 slots spread over the table (one per thread, its k1
+    // and first columns read whole: independent loads); every occupied slot in
+    // them is a sample — a sparse table still yields a uniform sample — thinned
+    // to ~0.9 FO_SAMPLE when they hold more.  (One slot per window would bias
+    // the sample: slot order inside a group is claim order.)
+    const uint64_t cap = (uint64_t)1 << (src.t.log2_buckets + TAB_SLOTS_LOG2);
+    const uint64_t p = ((uint64_t)tid * cap / 1024) & ~15ull;
+    uint64_t k1[16], f[16];
+    uint32_t vm = 0;
+    if (src.t.occupancy[p >> TAB_SLOTS_LOG2] != 0) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        k1[j] = src.t.k1[p + j];
+        f[j] = src.t.first[p + j];
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) vm |= (k1[j] != K1_EMPTY ? 1u : 0u) << j;
+    }
+    atomicAdd(&nvalid, (uint32_t)__popc(vm));
+    __syncthreads();
+    const uint32_t V = nvalid;
+    const uint32_t keep = V <= (uint32_t)FO_SAMPLE ? 0xFFFFFFFFu
+                                                    : (uint32_t)(0.9 * (double)FO_SAMPLE / V * 4294967296.0);
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if ((vm >> j) & 1u)
+        if (keep == 0xFFFFFFFFu || (uint32_t)(((tid << 4) + j) * 0x9E3779B1u) < keep)
+          atomicAdd(&hist[fo_logbin(f[j], M)], 1u);
+  } else {
+    const uint64_t n = src.dn ? *src.dn : src.n;
+    const uint64_t m = n < (uint64_t)FO_SAMPLE ? n : (uint64_t)FO_SAMPLE;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t i = (uint32_t)r * 1024 + tid;
+      if (i < m) atomicAdd(&hist[fo_logbin(src.first[i * n / m], M)], 1u);
+    }
+  }
+  __syncthreads();
+  clk.at(2);
+  const uint32_t V = lds_exclusive_scan<1024>(hist, FO_LOGBINS, ws);
+  clk.at(3);
+  // log-bin -> bin: the sample share below it, in FO_BINS equal parts (monotone:
+  // a float scaling, no integer division)
+  const float inv = V ? (float)FO_BINS / (float)V : 0.0f;
+  for (int i = tid; i < FO_LOGBINS; i += 1024)
+    map[i] = (uint16_t)min((uint32_t)FO_BINS - 1, (uint32_t)((float)hist[i] * inv));
+  clk.at(4);
+}
+
+// Block k: source rows [4096 k, 4096 k + 4096) (table: bucket k's slots).
+// cntm / loffm are bin-major: [bin * nblk + k].
+__global__ void __launch_bounds__(1024) wc_fo_bin(OrderSrc src, uint32_t M, const uint16_t* map, uint32_t* cntm,
+                                                  uint32_t* loffm, FoEntry* seg) {
+  FoClock clk(1);
+  __shared__ uint16_t lmap[FO_LOGBINS];
+  __shared__ uint32_t lc[FO_BINS], ws[16];
+  const uint32_t tid = threadIdx.x, k = blockIdx.x, nblk = gridDim.x;
+  const uint64_t i0 = (uint64_t)k * FO_ROWS;
+  uint64_t lim;
+  if (src.table) lim = src.t.occupancy[k] ? i0 + FO_ROWS : i0;  // an empty bucket's slots are undefined
+  else lim = src.dn ? *src.dn : src.n;
+  // rows first (their loads overlap the map copy)
+  FoEntry e[4];
+  bool ok[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint64_t i = i0 + (uint64_t)r * 1024 + tid;
+    ok[r] = i < lim;
+    if (src.table) {
+      const uint64_t k1 = ok[r] ? src.t.k1[i] : K1_EMPTY;
+      ok[r] = k1 != K1_EMPTY;
+      if (ok[r]) {
+        const bool h = key_is_hashed(k1);
+        e[r].first = src.t.first[i];
+        e[r].k0 = src.t.k0[i];
+        e[r].k1 = k1;
+        e[r].cnt = src.t.cnt[i];
+        e[r].soff = h ? src.t.sref_off[i] : 0;
+        e[r].slen = h ? src.t.sref_len[i] : 0;
+      }
+    } else if (ok[r]) {
+      e[r].first = src.first[i];
+      e[r].k0 = src.k0[i];
+      e[r].k1 = src.k1[i];
+      e[r].cnt = src.cnt[i];
+      e[r].soff = src.soff[i];
+      e[r].slen = src.slen[i];
+    }
+    e[r].pad = 0;
+  }
+  {
+    const uint4* g = reinterpret_cast<const uint4*>(map);
+    uint4* l = reinterpret_cast<uint4*>(lmap);
+    for (int i = tid; i < FO_LOGBINS * 2 / 16; i += 1024) l[i] = g[i];
+  }
+  for (uint32_t b = tid; b < FO_BINS; b += 1024) lc[b] = 0;
+  __syncthreads();
+  clk.at(1);
+  uint32_t bb[4], lp[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    bb[r] = FO_BINS;
+    if (ok[r]) {
+      bb[r] = lmap[fo_logbin(e[r].first, M)];
+      lp[r] = atomicAdd(&lc[bb[r]], 1u);
+    }
+  }
+  __syncthreads();
+  clk.at(2);
+  if (tid < FO_BINS) cntm[(size_t)tid * nblk + k] = lc[tid];
+  lds_exclusive_scan<1024>(lc, FO_BINS, ws);  // 0 or 1 bin per thread
+  clk.at(3);
+  if (tid < FO_BINS) loffm[(size_t)tid * nblk + k] = lc[tid];
+  FoEntry* out = seg + i0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    if (bb[r] != FO_BINS) out[lc[bb[r]] + lp[r]] = e[r];
+  clk.at(4);
+}
+
+template <int C, int T>
+__global__ void __launch_bounds__(T) wc_fo_sort(OrderDst dst, const uint32_t* cntm, const uint32_t* loffm,
+                                                const FoEntry* seg, uint32_t nblk, uint32_t* ctl, uint64_t* nout) {
+  FoClock clk(2);
+  __shared__ alignas(16) uint64_t sk[C];
+  __shared__ uint32_t sv[C];
+  __shared__ uint32_t sub[FO_NSUB + 1];
+  __shared__ uint32_t wa[T / 64], wb[T / 64];
+  __shared__ uint32_t carry;
+  __shared__ unsigned long long kmin, kmax;
+  const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t* cc = cntm + (size_t)b * nblk;
+  const uint32_t* ll = loffm + (size_t)b * nblk;
+  // this bin's output offset (sum of the blocks' local offsets) and size
+  uint32_t off = 0, m = 0;
+  {
+    uint32_t so = 0, sm = 0;
+    for (uint32_t k = tid; k < nblk; k += T) {
+      so += ll[k];
+      sm += cc[k];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      so += __shfl_xor(so, o);
+      sm += __shfl_xor(sm, o);
+    }
+    if (lane == 0) {
+      wa[wave] = so;
+      wb[wave] = sm;
+    }
+    if (tid == 0) {
+      carry = 0;
+      kmin = ~0ull;
+      kmax = 0;
+    }
+    __syncthreads();
+    for (int w = 0; w < T / 64; ++w) {
+      off += wa[w];
+      m += wb[w];
+    }
+  }
+  if (b == FO_BINS - 1 && tid == 0 && nout) *nout = (uint64_t)off + m;
+  clk.at(1);
+  if (m == 0) return;
+  if (m > (uint32_t)C) {  // a pathological value distribution: the caller redoes the order
+    if (tid == 0) ctl[0] = 1;
+    return;
+  }
+  // gather (first, entry index) of every block's run: a block scan of the counts
+  for (uint32_t k0 = 0; k0 < nblk; k0 += T) {
+    const uint32_t k = k0 + tid;
+    const uint32_t c = k < nblk ? cc[k] : 0u;
+    uint32_t x = c;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    __syncthreads();  // wa reused
+    if (lane == 63) wa[wave] = x;
+    __syncthreads();
+    uint32_t before = carry;
+    for (uint32_t w = 0; w < wave; ++w) before += wa[w];
+    const uint32_t at = before + x - c;
+    if (c) {
+      const size_t e0 = (size_t)k * FO_ROWS + ll[k];
+      for (uint32_t i = 0; i < c; ++i) {
+        sk[at + i] = seg[e0 + i].first;
+        sv[at + i] = (uint32_t)(e0 + i);
+      }
+    }
+    __syncthreads();
+    if (tid == T - 1) carry = before + x;
+  }
+  clk.at(2);
+  const auto emit = [&](uint32_t at, uint32_t ei) {
+    const FoEntry x = seg[ei];
+    const uint64_t j = (uint64_t)off + at;
+    dst.k0[j] = x.k0;
+    dst.k1[j] = x.k1;
+    dst.cnt[j] = x.cnt;
+    dst.first[j] = x.first;
+    dst.soff[j] = x.soff;
+    dst.slen[j] = x.slen;
+  };
+  typedef uint64_t v2u64 __attribute__((ext_vector_type(2)));
+  if (m <= FO_RANK_MAX) {
+    // small bin: a row's rank = the keys below it (keys are unique), counted
+    // over broadcast LDS reads two at a time
+    if (tid == 0 && (m & 1)) sk[m] = ~0ull;
+    __syncthreads();
+    for (uint32_t t = tid; t < m; t += T) {
+      const uint64_t key = sk[t];
+      uint32_t rank = 0;
+      for (uint32_t j = 0; j < m; j += 2) {
+        const v2u64 w = *reinterpret_cast<const v2u64*>(&sk[j]);
+        rank += (w.x < key ? 1u : 0u) + (w.y < key ? 1u : 0u);
+      }
+      emit(rank, sv[t]);
+    }
+    clk.at(4);
+    return;
+  }
+  // larger bin: counting sort into FO_NSUB value sub-buckets over [min, max]
+  // (sub-bucket = a monotone float scaling of key - min), then each row's rank
+  // = its sub-bucket's start + the keys below it inside the sub-bucket
+  {
+    uint64_t lo = ~0ull, hi = 0;
+    for (uint32_t t = tid; t < m; t += T) {
+      lo = min(lo, sk[t]);
+      hi = max(hi, sk[t]);
+    }
+    atomicMin(&kmin, (unsigned long long)lo);
+    atomicMax(&kmax, (unsigned long long)hi);
+  }
+  for (int i = tid; i <= FO_NSUB; i += T) sub[i] = 0;
+  __syncthreads();
+  const uint64_t base = kmin;
+  const float scale = (float)FO_NSUB / ((float)(kmax - base) + 1.0f);
+  const auto sub_of = [&](uint64_t key) {
+    return min((uint32_t)((float)(key - base) * scale), (uint32_t)FO_NSUB - 1);
+  };
+  for (uint32_t t = tid; t < m; t += T) atomicAdd(&sub[sub_of(sk[t])], 1u);
+  __syncthreads();
+  lds_exclusive_scan<T>(sub, FO_NSUB, wa);
+  // scatter the keys to their sub-bucket ranges (row order inside one is arbitrary)
+  uint64_t* sk2 = sk;  // in place: every row is staged in registers before the barrier
+  constexpr int PER = C / T;
+  uint64_t kk[PER];
+  uint32_t vv[PER], dd[PER];
+#pragma unroll
+  for (int r = 0; r < PER; ++r) {
+    const uint32_t t = (uint32_t)r * T + tid;
+    if (t < m) {
+      kk[r] = sk[t];
+      vv[r] = sv[t];
+      dd[r] = atomicAdd(&sub[sub_of(kk[r])], 1u);  // sub[] now advances to each sub-bucket's end
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < PER; ++r) {
+    const uint32_t t = (uint32_t)r * T + tid;
+    if (t < m) {
+      sk2[dd[r]] = kk[r];
+      sv[dd[r]] = vv[r];
+    }
+  }
+  __syncthreads();
+  // sub[s] = end of sub-bucket s; its start = dd of its first row = end - count:
+  // rank = start + #keys below inside [start, end)
+#pragma unroll
+  for (int r = 0; r < PER; ++r) {
+    const uint32_t t = (uint32_t)r * T + tid;
+    if (t >= m) continue;
+    const uint32_t sb = sub_of(kk[r]);
+    const uint32_t end = sub[sb], start = sb ? sub[sb - 1] : 0u;
+    uint32_t rank = start;
+    for (uint32_t j = start; j < end; ++j) rank += sk2[j] < kk[r] ? 1u : 0u;
+    emit(rank, vv[r]);
+  }
+  clk.at(5);
+}
+
 // out.col[i] = in.col[perm[i]] for all six key-table columns (one launch).
 __global__ void wc_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
                                const uint64_t* soff, const uint32_t* slen, const uint32_t* perm, uint64_t* ok0,
@@ -260,6 +641,59 @@ void radix_sort_pairs(uint64_t* keys, uint32_t* vals, uint64_t* tmp_keys, uint32
     WC_HIP_CHECK(hipMemcpyAsync(keys, ki, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
     WC_HIP_CHECK(hipMemcpyAsync(vals, vi, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   }
+}
+
+
+static uint32_t fo_cap(uint64_t bound) {  // LDS rows per bin: >= 8x the mean bin (+64)
+  if (const char* e = std::getenv("WC_FO_CAP")) {  // tests: a small capacity forces the overflow fallbacks
+    const int c = std::atoi(e);
+    if (c == 512 || c == 2048 || c == 8192) return (uint32_t)c;
+  }
+  const uint64_t want = 8 * (bound / dev::FO_BINS + 1) + 64;
+  return want <= 512 ? 512u : want <= 2048 ? 2048u : 8192u;
+}
+static uint32_t fo_blocks(const OrderSrc& src, uint64_t bound) {
+  return src.table ? (1u << src.t.log2_buckets) : (uint32_t)std::max<uint64_t>(1, (bound + dev::FO_ROWS - 1) / dev::FO_ROWS);
+}
+// Log-bin resolution: the most mantissa bits M with every key < 2^key_bits in FO_LOGBINS bins.
+static uint32_t fo_mbits(uint32_t key_bits) {
+  uint32_t M = 12;
+  while (M > 4 && ((uint64_t)(key_bits > M ? key_bits - M + 1 : 1) << M) > (uint64_t)dev::FO_LOGBINS) --M;
+  return M;
+}
+
+void first_order_stamps(unsigned long long* d) {
+  WC_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(dev::fo_stamps), &d, sizeof d));
+}
+
+size_t first_order_ws_bytes(const OrderSrc& src, uint64_t bound) {
+  const size_t nblk = fo_blocks(src, bound);
+  return 64 * 1024 + 2 * (size_t)dev::FO_BINS * nblk * 4 + 256 + nblk * dev::FO_ROWS * sizeof(dev::FoEntry);
+}
+
+uint32_t* first_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, uint32_t key_bits, void* ws,
+                      uint64_t* nout, hipStream_t s) {
+  WC_CHECK(bound <= FO_MAX_KEYS, "first_order: key bound above FO_MAX_KEYS (use the radix sort)");
+  const uint32_t nblk = fo_blocks(src, bound), C = fo_cap(bound), M = fo_mbits(key_bits);
+  uint8_t* p = static_cast<uint8_t*>(ws);
+  uint16_t* map = reinterpret_cast<uint16_t*>(p);  // FO_LOGBINS entries (32 KiB)
+  uint32_t* ctl = reinterpret_cast<uint32_t*>(p + 48 * 1024);
+  uint32_t* cntm = reinterpret_cast<uint32_t*>(p + 64 * 1024);
+  uint32_t* loffm = cntm + (size_t)dev::FO_BINS * nblk;
+  const size_t mat = 2 * (size_t)dev::FO_BINS * nblk * 4;
+  dev::FoEntry* seg = reinterpret_cast<dev::FoEntry*>(p + 64 * 1024 + (mat + 255) / 256 * 256);
+  hipLaunchKernelGGL(dev::wc_fo_split, dim3(1), dim3(1024), 0, s, src, M, map, ctl);
+  hipLaunchKernelGGL(dev::wc_fo_bin, dim3(nblk), dim3(1024), 0, s, src, M, map, cntm, loffm, seg);
+  if (C == 512)
+    hipLaunchKernelGGL((dev::wc_fo_sort<512, 256>), dim3(dev::FO_BINS), dim3(256), 0, s, dst, cntm, loffm, seg, nblk,
+                       ctl, nout);
+  else if (C == 2048)
+    hipLaunchKernelGGL((dev::wc_fo_sort<2048, 512>), dim3(dev::FO_BINS), dim3(512), 0, s, dst, cntm, loffm, seg, nblk,
+                       ctl, nout);
+  else
+    hipLaunchKernelGGL((dev::wc_fo_sort<8192, 1024>), dim3(dev::FO_BINS), dim3(1024), 0, s, dst, cntm, loffm, seg,
+                       nblk, ctl, nout);
+  return ctl;
 }
 
 void launch_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
