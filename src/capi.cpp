@@ -219,6 +219,7 @@ int wc_debug_first_order(int device, const uint64_t* keys, uint64_t n, int reps,
     }
     for (int r = 0; r < std::max(reps, 1); ++r) {
       WC_HIP_CHECK(hipEventRecord(e0, s));
+      if (stamps && r == 1) WC_HIP_CHECK(hipMemsetAsync(d_st, 0, 48 * 8, s));  // warm reps only
       if (n) ovf = wc::first_order(src, d, n, kb, w, nullptr, s);
       WC_HIP_CHECK(hipEventRecord(e1, s));
       WC_HIP_CHECK(hipEventSynchronize(e1));

@@ -222,7 +222,7 @@ struct OrderDst {
   uint64_t *k0, *k1, *cnt, *first, *soff;
   uint32_t* slen;
 };
-constexpr uint64_t FO_MAX_KEYS = 512 * 1000;  // 8x the mean bin still fits the largest (8192-row) LDS bin
+constexpr uint64_t FO_MAX_KEYS = 400 * 1000;  // bins average <= 800 rows (one wave sorts up to 2048)
 size_t first_order_ws_bytes(const OrderSrc& src, uint64_t bound);
 void first_order_stamps(unsigned long long* d);  // debug: phase clocks of the three kernels (nullptr: off)
 uint32_t* first_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, uint32_t key_bits, void* ws,

@@ -211,8 +211,6 @@ __global__ void __launch_bounds__(OS_THREADS) wc_os_pass(const uint64_t* keys, c
 // A bin above its LDS capacity (a pathological value distribution) raises *ovf
 // and the caller redoes the order with the radix sort.
 constexpr int FO_BINS = 512, FO_ROWS = 4096, FO_SAMPLE = 4096, FO_LOGBINS = 16384;
-constexpr uint32_t FO_RANK_MAX = 256;  // bins up to this size count ranks directly
-constexpr int FO_NSUB = 1024;          // value sub-buckets of a larger bin
 
 // WC_FO_STAMPS (debug API): per kernel K, [16 K + p] = the max over blocks of
 // the 100 MHz wall time from the block's start to its phase p.
@@ -247,7 +245,14 @@ __device__ __forceinline__ uint32_t lds_exclusive_scan(uint32_t* c, int n, uint3
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int per = n >= T ? n / T : (tid < n ? 1 : 0);  // n < T: one counter on the first n threads
   uint32_t own = 0;
-  for (int i = 0; i < per; ++i) own += c[tid * per + i];
+  if (per % 4 == 0) {  // 16-byte reads: 4x fewer LDS trips and bank conflicts
+    for (int i = 0; i < per; i += 4) {
+      const uint4 q = *reinterpret_cast<const uint4*>(&c[tid * per + i]);
+      own += q.x + q.y + q.z + q.w;
+    }
+  } else {
+    for (int i = 0; i < per; ++i) own += c[tid * per + i];
+  }
   uint32_t x = own;
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t y = __shfl_up(x, o);
@@ -261,10 +266,20 @@ __device__ __forceinline__ uint32_t lds_exclusive_scan(uint32_t* c, int n, uint3
     total += ws[w];
   }
   uint32_t run = before + x - own;
-  for (int i = 0; i < per; ++i) {
-    const uint32_t v = c[tid * per + i];
-    c[tid * per + i] = run;
-    run += v;
+  if (per % 4 == 0) {
+    for (int i = 0; i < per; i += 4) {
+      uint4 q = *reinterpret_cast<const uint4*>(&c[tid * per + i]);
+      const uint32_t a = run, b2 = a + q.x, c2 = b2 + q.y, d2 = c2 + q.z;
+      run = d2 + q.w;
+      q = make_uint4(a, b2, c2, d2);
+      *reinterpret_cast<uint4*>(&c[tid * per + i]) = q;
+    }
+  } else {
+    for (int i = 0; i < per; ++i) {
+      const uint32_t v = c[tid * per + i];
+      c[tid * per + i] = run;
+      run += v;
+    }
   }
   __syncthreads();
   return total;
@@ -272,7 +287,7 @@ __device__ __forceinline__ uint32_t lds_exclusive_scan(uint32_t* c, int n, uint3
 
 __global__ void __launch_bounds__(1024) wc_fo_split(OrderSrc src, uint32_t M, uint16_t* map, uint32_t* ctl) {
   FoClock clk(0);
-  __shared__ uint32_t hist[FO_LOGBINS];
+  __shared__ alignas(16) uint32_t hist[FO_LOGBINS];
   __shared__ uint32_t ws[16];
   __shared__ uint32_t nvalid;
   const uint32_t tid = threadIdx.x;
@@ -285,23 +300,27 @@ __global__ void __launch_bounds__(1024) wc_fo_split(OrderSrc src, uint32_t M, ui
   clk.at(1);
   constexpr int R = FO_SAMPLE / 1024;
   if (src.table) {
-    // 1024 windows of 16 slots spread over the table (one per thread, its k1
-    // and first columns read whole: independent loads); every occupied slot in
-    // them is a sample — a sparse table still yields a uniform sample — thinned
-    // to ~0.9 FO_SAMPLE when they hold more.  (One slot per window would bias
-    // the sample: slot order inside a group is claim order.)
+    // 1024 windows of 16 slots spread over the table, one per thread, their
+    // first offsets read whole (16-byte loads; an empty slot of an occupied
+    // bucket holds ~0 — the reducer's slice initialisation — and a stray value
+    // could only skew the sample, never the order): every occupied slot in
+    // them is a sample — a sparse table still yields a uniform sample —
+    // thinned to ~0.9 FO_SAMPLE when they hold more.  (One slot per window
+    // would bias it: slot order inside a group is claim order.)
     const uint64_t cap = (uint64_t)1 << (src.t.log2_buckets + TAB_SLOTS_LOG2);
     const uint64_t p = ((uint64_t)tid * cap / 1024) & ~15ull;
-    uint64_t k1[16], f[16];
+    uint64_t f[16];
     uint32_t vm = 0;
     if (src.t.occupancy[p >> TAB_SLOTS_LOG2] != 0) {
+      const ulonglong2* w = reinterpret_cast<const ulonglong2*>(src.t.first + p);
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        k1[j] = src.t.k1[p + j];
-        f[j] = src.t.first[p + j];
+      for (int j = 0; j < 8; ++j) {
+        const ulonglong2 q = w[j];
+        f[2 * j] = q.x;
+        f[2 * j + 1] = q.y;
       }
 #pragma unroll
-      for (int j = 0; j < 16; ++j) vm |= (k1[j] != K1_EMPTY ? 1u : 0u) << j;
+      for (int j = 0; j < 16; ++j) vm |= (f[j] != ~0ull ? 1u : 0u) << j;
     }
     atomicAdd(&nvalid, (uint32_t)__popc(vm));
     __syncthreads();
@@ -405,79 +424,88 @@ __global__ void __launch_bounds__(1024) wc_fo_bin(OrderSrc src, uint32_t M, cons
   clk.at(4);
 }
 
-template <int C, int T>
-__global__ void __launch_bounds__(T) wc_fo_sort(OrderDst dst, const uint32_t* cntm, const uint32_t* loffm,
-                                                const FoEntry* seg, uint32_t nblk, uint32_t* ctl, uint64_t* nout) {
-  FoClock clk(2);
-  __shared__ alignas(16) uint64_t sk[C];
-  __shared__ uint32_t sv[C];
-  __shared__ uint32_t sub[FO_NSUB + 1];
-  __shared__ uint32_t wa[T / 64], wb[T / 64];
-  __shared__ uint32_t carry;
-  __shared__ unsigned long long kmin, kmax;
-  const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t* cc = cntm + (size_t)b * nblk;
-  const uint32_t* ll = loffm + (size_t)b * nblk;
-  // this bin's output offset (sum of the blocks' local offsets) and size
-  uint32_t off = 0, m = 0;
-  {
-    uint32_t so = 0, sm = 0;
-    for (uint32_t k = tid; k < nblk; k += T) {
-      so += ll[k];
-      sm += cc[k];
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      so += __shfl_xor(so, o);
-      sm += __shfl_xor(sm, o);
-    }
-    if (lane == 0) {
-      wa[wave] = so;
-      wb[wave] = sm;
-    }
-    if (tid == 0) {
-      carry = 0;
-      kmin = ~0ull;
-      kmax = 0;
-    }
-    __syncthreads();
-    for (int w = 0; w < T / 64; ++w) {
-      off += wa[w];
-      m += wb[w];
-    }
-  }
-  if (b == FO_BINS - 1 && tid == 0 && nout) *nout = (uint64_t)off + m;
-  clk.at(1);
-  if (m == 0) return;
-  if (m > (uint32_t)C) {  // a pathological value distribution: the caller redoes the order
-    if (tid == 0) ctl[0] = 1;
-    return;
-  }
-  // gather (first, entry index) of every block's run: a block scan of the counts
-  for (uint32_t k0 = 0; k0 < nblk; k0 += T) {
-    const uint32_t k = k0 + tid;
-    const uint32_t c = k < nblk ? cc[k] : 0u;
-    uint32_t x = c;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o);
-      if (lane >= (uint32_t)o) x += y;
-    }
-    __syncthreads();  // wa reused
-    if (lane == 63) wa[wave] = x;
-    __syncthreads();
-    uint32_t before = carry;
-    for (uint32_t w = 0; w < wave; ++w) before += wa[w];
-    const uint32_t at = before + x - c;
-    if (c) {
-      const size_t e0 = (size_t)k * FO_ROWS + ll[k];
-      for (uint32_t i = 0; i < c; ++i) {
-        sk[at + i] = seg[e0 + i].first;
-        sv[at + i] = (uint32_t)(e0 + i);
+// Per-wave sort of one bin (m <= FO_WAVE_CAP rows), no block barrier: the
+// wave gathers its bin's (first, entry) pairs into its LDS region, counting-
+// sorts them into FO_WSUB value sub-buckets over [min, max] (a monotone float
+// scaling), and each row's rank = its sub-bucket's start + the keys below it
+// inside the sub-bucket.  The block's waves each take a bin; bins above the
+// wave capacity are sorted afterwards by the whole block (LDS bitonic over
+// the block's combined regions, up to FO_BLOCK_CAP rows).
+constexpr int FO_SORT_WAVES = 2, FO_WAVE_CAP = 2048, FO_WSUB = 512;
+constexpr int FO_BLOCK_CAP = FO_SORT_WAVES * FO_WAVE_CAP * 2;  // 12-byte rows in the 24-byte-per-row regions
+
+struct FoWaveLds {
+  alignas(16) uint64_t ka[FO_WAVE_CAP];
+  uint64_t kb[FO_WAVE_CAP];
+  uint32_t va[FO_WAVE_CAP];
+  uint32_t vb[FO_WAVE_CAP];
+  uint32_t sub[FO_WSUB];
+};
+
+// Bitonic sort of P (a power of two) keys + values in LDS, T threads.
+template <int T, bool V>
+__device__ __forceinline__ void lds_bitonic(uint64_t* k, uint32_t* v, uint32_t P) {
+  for (uint32_t size = 2; size <= P; size <<= 1) {
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (uint32_t t = threadIdx.x; t < P / 2; t += T) {
+        const uint32_t i = 2 * t - (t & (stride - 1)), j = i + stride;
+        const uint64_t a = k[i], b = k[j];
+        if ((a > b) == ((i & size) == 0)) {
+          k[i] = b;
+          k[j] = a;
+          if (V) {
+            const uint32_t x = v[i];
+            v[i] = v[j];
+            v[j] = x;
+          }
+        }
       }
     }
-    __syncthreads();
-    if (tid == T - 1) carry = before + x;
   }
-  clk.at(2);
+  __syncthreads();
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  const uint32_t lane = __lane_id();
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  return x;
+}
+
+__global__ void __launch_bounds__(64 * FO_SORT_WAVES) wc_fo_sort(OrderDst dst, const uint32_t* cntm,
+                                                                 const uint32_t* loffm, const FoEntry* seg,
+                                                                 uint32_t nblk, uint32_t cap, uint32_t* ctl,
+                                                                 uint64_t* nout) {
+  constexpr int T = 64 * FO_SORT_WAVES;
+  FoClock clk(2);
+  __shared__ FoWaveLds W[FO_SORT_WAVES];
+  __shared__ uint32_t big_m[FO_SORT_WAVES], big_off[FO_SORT_WAVES];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t b = blockIdx.x * FO_SORT_WAVES + wave;
+  const uint32_t* cc = cntm + (size_t)b * nblk;
+  const uint32_t* ll = loffm + (size_t)b * nblk;
+  FoWaveLds& L = W[wave];
+  // this bin's output offset (sum of the blocks' local offsets) and size
+  uint32_t off = 0, m = 0;
+  for (uint32_t k = lane; k < nblk; k += 64) {
+    off += ll[k];
+    m += cc[k];
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    off += __shfl_xor(off, o);
+    m += __shfl_xor(m, o);
+  }
+  if (b == FO_BINS - 1 && lane == 0 && nout) *nout = (uint64_t)off + m;
+  clk.at(1);
   const auto emit = [&](uint32_t at, uint32_t ei) {
     const FoEntry x = seg[ei];
     const uint64_t j = (uint64_t)off + at;
@@ -488,83 +516,114 @@ __global__ void __launch_bounds__(T) wc_fo_sort(OrderDst dst, const uint32_t* cn
     dst.soff[j] = x.soff;
     dst.slen[j] = x.slen;
   };
-  typedef uint64_t v2u64 __attribute__((ext_vector_type(2)));
-  if (m <= FO_RANK_MAX) {
-    // small bin: a row's rank = the keys below it (keys are unique), counted
-    // over broadcast LDS reads two at a time
-    if (tid == 0 && (m & 1)) sk[m] = ~0ull;
-    __syncthreads();
-    for (uint32_t t = tid; t < m; t += T) {
-      const uint64_t key = sk[t];
-      uint32_t rank = 0;
-      for (uint32_t j = 0; j < m; j += 2) {
-        const v2u64 w = *reinterpret_cast<const v2u64*>(&sk[j]);
-        rank += (w.x < key ? 1u : 0u) + (w.y < key ? 1u : 0u);
+  // gather (first, entry index) of every block's run: lane l owns the blocks
+  // [G l, G l + G) — all their counts / offsets loaded at once, one wave scan,
+  // then all the entry loads (two dependent memory steps, whatever nblk)
+  const auto gather = [&](const uint32_t* gcc, const uint32_t* gll, uint64_t* keys, uint32_t* idx) {
+    const uint32_t G = (nblk + 63) / 64, k0 = lane * G;
+    uint32_t tot = 0;
+    for (uint32_t g = 0; g < G; ++g)
+      if (k0 + g < nblk) tot += gcc[k0 + g];
+    uint32_t at = wave_incl_scan(tot) - tot;
+    for (uint32_t g = 0; g < G; ++g) {
+      const uint32_t k = k0 + g;
+      if (k >= nblk) break;
+      const uint32_t c = gcc[k];
+      if (!c) continue;
+      const size_t e0 = (size_t)k * FO_ROWS + gll[k];
+      for (uint32_t i = 0; i < c; ++i) {
+        keys[at + i] = seg[e0 + i].first;
+        idx[at + i] = (uint32_t)(e0 + i);
       }
-      emit(rank, sv[t]);
+      at += c;
     }
-    clk.at(4);
-    return;
-  }
-  // larger bin: counting sort into FO_NSUB value sub-buckets over [min, max]
-  // (sub-bucket = a monotone float scaling of key - min), then each row's rank
-  // = its sub-bucket's start + the keys below it inside the sub-bucket
-  {
-    uint64_t lo = ~0ull, hi = 0;
-    for (uint32_t t = tid; t < m; t += T) {
-      lo = min(lo, sk[t]);
-      hi = max(hi, sk[t]);
-    }
-    atomicMin(&kmin, (unsigned long long)lo);
-    atomicMax(&kmax, (unsigned long long)hi);
-  }
-  for (int i = tid; i <= FO_NSUB; i += T) sub[i] = 0;
-  __syncthreads();
-  const uint64_t base = kmin;
-  const float scale = (float)FO_NSUB / ((float)(kmax - base) + 1.0f);
-  const auto sub_of = [&](uint64_t key) {
-    return min((uint32_t)((float)(key - base) * scale), (uint32_t)FO_NSUB - 1);
   };
-  for (uint32_t t = tid; t < m; t += T) atomicAdd(&sub[sub_of(sk[t])], 1u);
-  __syncthreads();
-  lds_exclusive_scan<T>(sub, FO_NSUB, wa);
-  // scatter the keys to their sub-bucket ranges (row order inside one is arbitrary)
-  uint64_t* sk2 = sk;  // in place: every row is staged in registers before the barrier
-  constexpr int PER = C / T;
-  uint64_t kk[PER];
-  uint32_t vv[PER], dd[PER];
-#pragma unroll
-  for (int r = 0; r < PER; ++r) {
-    const uint32_t t = (uint32_t)r * T + tid;
-    if (t < m) {
-      kk[r] = sk[t];
-      vv[r] = sv[t];
-      dd[r] = atomicAdd(&sub[sub_of(kk[r])], 1u);  // sub[] now advances to each sub-bucket's end
+  const bool over = m > cap;  // a pathological value distribution: the caller redoes the order
+  if (over && lane == 0) ctl[0] = 1;
+  const bool big = !over && m > (uint32_t)FO_WAVE_CAP;
+  if (m != 0 && !big && !over) {
+    gather(cc, ll, L.ka, L.va);
+    for (uint32_t i = lane; i < FO_WSUB; i += 64) L.sub[i] = 0;
+    wave_sync();
+    clk.at(2);
+    uint64_t lo = ~0ull, hi = 0;
+    for (uint32_t t = lane; t < m; t += 64) {
+      lo = min(lo, L.ka[t]);
+      hi = max(hi, L.ka[t]);
     }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < PER; ++r) {
-    const uint32_t t = (uint32_t)r * T + tid;
-    if (t < m) {
-      sk2[dd[r]] = kk[r];
-      sv[dd[r]] = vv[r];
+    for (int o = 32; o > 0; o >>= 1) {
+      lo = min(lo, (uint64_t)__shfl_xor((unsigned long long)lo, o));
+      hi = max(hi, (uint64_t)__shfl_xor((unsigned long long)hi, o));
     }
+    const float scale = (float)FO_WSUB / ((float)(hi - lo) + 1.0f);
+    const auto sub_of = [&](uint64_t key) { return min((uint32_t)((float)(key - lo) * scale), (uint32_t)FO_WSUB - 1); };
+    for (uint32_t t = lane; t < m; t += 64) atomicAdd(&L.sub[sub_of(L.ka[t])], 1u);
+    wave_sync();
+    {  // exclusive scan of the sub-bucket counts, FO_WSUB / 64 per lane
+      constexpr int PL = FO_WSUB / 64;
+      uint32_t c[PL], own = 0;
+#pragma unroll
+      for (int i = 0; i < PL; ++i) own += c[i] = L.sub[lane * PL + i];
+      uint32_t run = wave_incl_scan(own) - own;
+#pragma unroll
+      for (int i = 0; i < PL; ++i) {
+        L.sub[lane * PL + i] = run;
+        run += c[i];
+      }
+    }
+    wave_sync();
+    for (uint32_t t = lane; t < m; t += 64) {
+      const uint64_t key = L.ka[t];
+      const uint32_t d = atomicAdd(&L.sub[sub_of(key)], 1u);  // sub[s] advances to its end
+      L.kb[d] = key;
+      L.vb[d] = L.va[t];
+    }
+    wave_sync();
+    for (uint32_t t = lane; t < m; t += 64) {
+      const uint64_t key = L.kb[t];
+      const uint32_t sb = sub_of(key);
+      const uint32_t end = L.sub[sb], start = sb ? L.sub[sb - 1] : 0u;
+      uint32_t rank = start;
+      for (uint32_t j = start; j < end; ++j) rank += L.kb[j] < key ? 1u : 0u;
+      emit(rank, L.vb[t]);
+    }
+    clk.at(3);
+  }
+  // bins above the wave capacity: the whole block, one at a time
+  if (lane == 0) {
+    big_m[wave] = big ? m : 0u;
+    big_off[wave] = off;
   }
   __syncthreads();
-  // sub[s] = end of sub-bucket s; its start = dd of its first row = end - count:
-  // rank = start + #keys below inside [start, end)
-#pragma unroll
-  for (int r = 0; r < PER; ++r) {
-    const uint32_t t = (uint32_t)r * T + tid;
-    if (t >= m) continue;
-    const uint32_t sb = sub_of(kk[r]);
-    const uint32_t end = sub[sb], start = sb ? sub[sb - 1] : 0u;
-    uint32_t rank = start;
-    for (uint32_t j = start; j < end; ++j) rank += sk2[j] < kk[r] ? 1u : 0u;
-    emit(rank, vv[r]);
+  uint64_t* sk = reinterpret_cast<uint64_t*>(&W[0]);                                  // FO_BLOCK_CAP keys
+  uint32_t* sv = reinterpret_cast<uint32_t*>(sk + FO_BLOCK_CAP);                      // + values
+  static_assert(sizeof(W) >= (size_t)FO_BLOCK_CAP * 12, "block path fits the wave regions");
+  for (int w = 0; w < FO_SORT_WAVES; ++w) {
+    const uint32_t bm = big_m[w];
+    if (bm == 0) continue;
+    const uint32_t bb = blockIdx.x * FO_SORT_WAVES + w;
+    const uint32_t* bcc = cntm + (size_t)bb * nblk;
+    const uint32_t* bll = loffm + (size_t)bb * nblk;
+    if (wave == 0) gather(bcc, bll, sk, sv);  // by one wave
+    uint32_t P = 64;
+    while (P < bm) P <<= 1;
+    __syncthreads();
+    for (uint32_t i = bm + tid; i < P; i += T) sk[i] = ~0ull;
+    lds_bitonic<T, true>(sk, sv, P);
+    const uint32_t boff = big_off[w];
+    for (uint32_t i = tid; i < bm; i += T) {
+      const FoEntry x = seg[sv[i]];
+      const uint64_t j = (uint64_t)boff + i;
+      dst.k0[j] = x.k0;
+      dst.k1[j] = x.k1;
+      dst.cnt[j] = x.cnt;
+      dst.first[j] = x.first;
+      dst.soff[j] = x.soff;
+      dst.slen[j] = x.slen;
+    }
+    __syncthreads();
   }
-  clk.at(5);
+  clk.at(4);
 }
 
 // out.col[i] = in.col[perm[i]] for all six key-table columns (one launch).
@@ -644,14 +703,6 @@ void radix_sort_pairs(uint64_t* keys, uint32_t* vals, uint64_t* tmp_keys, uint32
 }
 
 
-static uint32_t fo_cap(uint64_t bound) {  // LDS rows per bin: >= 8x the mean bin (+64)
-  if (const char* e = std::getenv("WC_FO_CAP")) {  // tests: a small capacity forces the overflow fallbacks
-    const int c = std::atoi(e);
-    if (c == 512 || c == 2048 || c == 8192) return (uint32_t)c;
-  }
-  const uint64_t want = 8 * (bound / dev::FO_BINS + 1) + 64;
-  return want <= 512 ? 512u : want <= 2048 ? 2048u : 8192u;
-}
 static uint32_t fo_blocks(const OrderSrc& src, uint64_t bound) {
   return src.table ? (1u << src.t.log2_buckets) : (uint32_t)std::max<uint64_t>(1, (bound + dev::FO_ROWS - 1) / dev::FO_ROWS);
 }
@@ -674,7 +725,7 @@ size_t first_order_ws_bytes(const OrderSrc& src, uint64_t bound) {
 uint32_t* first_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, uint32_t key_bits, void* ws,
                       uint64_t* nout, hipStream_t s) {
   WC_CHECK(bound <= FO_MAX_KEYS, "first_order: key bound above FO_MAX_KEYS (use the radix sort)");
-  const uint32_t nblk = fo_blocks(src, bound), C = fo_cap(bound), M = fo_mbits(key_bits);
+  const uint32_t nblk = fo_blocks(src, bound), M = fo_mbits(key_bits);
   uint8_t* p = static_cast<uint8_t*>(ws);
   uint16_t* map = reinterpret_cast<uint16_t*>(p);  // FO_LOGBINS entries (32 KiB)
   uint32_t* ctl = reinterpret_cast<uint32_t*>(p + 48 * 1024);
@@ -684,15 +735,10 @@ uint32_t* first_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, 
   dev::FoEntry* seg = reinterpret_cast<dev::FoEntry*>(p + 64 * 1024 + (mat + 255) / 256 * 256);
   hipLaunchKernelGGL(dev::wc_fo_split, dim3(1), dim3(1024), 0, s, src, M, map, ctl);
   hipLaunchKernelGGL(dev::wc_fo_bin, dim3(nblk), dim3(1024), 0, s, src, M, map, cntm, loffm, seg);
-  if (C == 512)
-    hipLaunchKernelGGL((dev::wc_fo_sort<512, 256>), dim3(dev::FO_BINS), dim3(256), 0, s, dst, cntm, loffm, seg, nblk,
-                       ctl, nout);
-  else if (C == 2048)
-    hipLaunchKernelGGL((dev::wc_fo_sort<2048, 512>), dim3(dev::FO_BINS), dim3(512), 0, s, dst, cntm, loffm, seg, nblk,
-                       ctl, nout);
-  else
-    hipLaunchKernelGGL((dev::wc_fo_sort<8192, 1024>), dim3(dev::FO_BINS), dim3(1024), 0, s, dst, cntm, loffm, seg,
-                       nblk, ctl, nout);
+  uint32_t cap = dev::FO_BLOCK_CAP;
+  if (const char* e = std::getenv("WC_FO_CAP")) cap = std::min<uint32_t>(cap, (uint32_t)std::atoi(e));  // tests
+  hipLaunchKernelGGL(dev::wc_fo_sort, dim3(dev::FO_BINS / dev::FO_SORT_WAVES), dim3(64 * dev::FO_SORT_WAVES), 0, s,
+                     dst, cntm, loffm, seg, nblk, cap, ctl, nout);
   return ctl;
 }
 

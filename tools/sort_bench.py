@@ -20,7 +20,7 @@ def first_offsets(n):
     return rng.permutation(k)
 
 
-for n in [10_000, 100_000, 300_000, 512_000, 1_000_000]:
+for n in [10_000, 100_000, 200_000, 400_000, 1_000_000]:
     keys = first_offsets(n)
     ms = ctypes.c_double(0)
     check(lib.wc_bench_radix_sort(0, keys.ctypes.data_as(P64), len(keys), 30, 5, ctypes.byref(ms)))
@@ -28,7 +28,7 @@ for n in [10_000, 100_000, 300_000, 512_000, 1_000_000]:
     perm = np.empty(len(keys), np.uint32)
     ovf = ctypes.c_int(0)
     ms2 = ctypes.c_double(0)
-    if n > 512_000:
+    if n > 400_000:
         print(f"n={len(keys):>9}: radix {ms.value * 1e3:8.1f} us (no gather)", flush=True)
         continue
     check(lib.wc_debug_first_order(0, keys.ctypes.data_as(P64), len(keys), 6, srt.ctypes.data_as(P64),
