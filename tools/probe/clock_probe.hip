@@ -159,6 +159,32 @@ __global__ void k_read1(const uint64_t* buf, uint64_t* out, unsigned long long* 
   }
 }
 
+// Scattered 12-byte stores: `active` of 64 lanes store per instruction, each to
+// a different bucket region (256 regions of this block, sequential within a
+// region), `total` records per wave either way.
+struct R12 { uint32_t a, b, c; };
+__global__ void __launch_bounds__(1024) k_scatter(R12* out, int active, int total, uint64_t* st) {
+  __shared__ uint32_t cur[256];
+  for (int i = threadIdx.x; i < 256; i += 1024) cur[i] = 0;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  R12* base = out + (size_t)blockIdx.x * 256 * 8192;
+  uint32_t x = threadIdx.x * 2654435761u + blockIdx.x;
+  const int iters = total / active;
+  uint64_t t0 = wall_clock64();
+  for (int it = 0; it < iters; ++it) {
+    x = x * 1664525u + 1013904223u;
+    if ((int)lane < active) {
+      const uint32_t b = x >> 24;
+      const uint32_t pos = atomicAdd(&cur[b], 1u) & 8191u;
+      R12 r{x, x ^ 1u, (uint32_t)it};
+      base[(size_t)b * 8192 + pos] = r;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax((unsigned long long*)st, (unsigned long long)(wall_clock64() - t0));
+}
+
 // busy kernel: keeps every CU at work for a while (clock ramp)
 __global__ void k_busy(uint32_t* out, int iters) {
   uint32_t x = threadIdx.x + blockIdx.x;
@@ -262,6 +288,20 @@ int main() {
       printf("read1 %-26s event %6.2f us | block: load+sync %5.2f us, entry spread %5.2f us, block max %5.2f us\n",
              vn[variant], ms * 1e3, h4[0] / 100.0, (h4[2] - h4[1]) / 100.0, h4[3] / 100.0);
     }
+  }
+  {
+    R12* out;
+    CK(hipMalloc(&out, (size_t)256 * 256 * 8192 * sizeof(R12)));
+    for (int active : {64, 32, 19, 8}) {
+      CK(hipMemset(d_st, 0, 8));
+      hipLaunchKernelGGL(k_scatter, dim3(256), dim3(1024), 0, 0, out, active, 4096, d_st);
+      CK(hipMemset(d_st, 0, 8));
+      hipLaunchKernelGGL(k_scatter, dim3(256), dim3(1024), 0, 0, out, active, 4096, d_st);
+      CK(hipMemcpy(st, d_st, 8, hipMemcpyDeviceToHost));
+      printf("scatter 12B records, %2d active lanes/instr, 4096 per wave x 16 waves x 256 CUs: %8.1f us\n", active,
+             st[0] / 100.0);
+    }
+    CK(hipFree(out));
   }
   std::vector<uint64_t> o(512);
   hipLaunchKernelGGL(k_wsort<8>, dim3(1), dim3(64), 0, 0, d_in, d_out, d_st);
