@@ -41,7 +41,7 @@ T* take_aligned(DeviceArena& A, size_t n) {
 // Pinned host words of one merge (W <= 64): async H2D copies from them need no
 // host sync before the merge returns.  Fixed slots: max offset, source bases,
 // own bytes, gather bases.
-enum : size_t { HW_MX = 0, HW_BASE = 8, HW_OWNB = 160, HW_GBASE = 192, HW_WORDS = 512 };
+enum : size_t { HW_MX = 0, HW_BASE = 8, HW_OWNB = 160, HW_GBASE = 192, HW_SEG = 336, HW_WORDS = 512 };
 uint64_t* host_words(Engine::Impl& im) {
   if (im.h_merge.size() < HW_WORDS * 8) im.h_merge.resize(HW_WORDS * 8);
   return reinterpret_cast<uint64_t*>(im.h_merge.data());
@@ -106,11 +106,17 @@ void merge_to_root(Engine::Impl& im, Comm& comm, const std::vector<uint64_t>& ra
     const size_t nbase = 2 * (size_t)W + 2;
     uint64_t* d_base = take_aligned<uint64_t>(A, nbase + 4);
     unsigned long long* d_m = take_aligned<unsigned long long>(A, 1);
-    WC_HIP_CHECK(hipMemcpyAsync(d_base, base, nbase * 8, hipMemcpyHostToDevice, s));
-    WC_HIP_CHECK(hipMemsetAsync(state, 0, T * 4, s));
-    WC_HIP_CHECK(hipMemsetAsync(tcnt, 0, T * 8, s));
-    launch_fill_u64(reinterpret_cast<uint64_t*>(tfirst), ~0ull, T, s);
-    WC_HIP_CHECK(hipMemsetAsync(d_m, 0, 8, s));
+    uint64_t* d_gbase = d_base + nbase;  // one group: row base 0 .. G, byte base 0
+    const uint64_t G = rr;
+    gb[1] = G;
+    ZeroList z{};  // the owner table's state, the bases from page-locked host words: one launch
+    z.add(state, T * 4);
+    z.add(tcnt, T * 8);
+    z.add(tfirst, T * 8, 0xFFFFFFFFu);
+    z.add(d_m, 8);
+    z.copy(d_base, base, nbase * 8);
+    z.copy(d_gbase, gb, 4 * 8);
+    launch_zero_regions(z, s);
     launch_mrow_insert(recv_rows, rr, recv_bytes, d_base, d_base + W + 1, (uint32_t)W, state, tcnt, tfirst, T, nullptr,
                        s);
     launch_mrow_compact(recv_rows, state, tcnt, tfirst, T, d_base, d_base + W + 1, (uint32_t)W, merged, d_m, nullptr,
@@ -118,7 +124,6 @@ void merge_to_root(Engine::Impl& im, Comm& comm, const std::vector<uint64_t>& ra
     // no host round trip: columns sized for the rows received (a bound of the
     // merged count), which stays on the device (KeyCols::dn) through the
     // first-occurrence sort; the finalize's last wait publishes it
-    const uint64_t G = rr;
     o.n = G;
     o.dn = d_m;
     o.k0 = take_aligned<uint64_t>(A, G);
@@ -127,9 +132,6 @@ void merge_to_root(Engine::Impl& im, Comm& comm, const std::vector<uint64_t>& ra
     o.first = take_aligned<uint64_t>(A, G);
     o.sref_off = take_aligned<uint64_t>(A, G);
     o.sref_len = take_aligned<uint32_t>(A, G);
-    uint64_t* d_gbase = d_base + nbase;  // one group: row base 0 .. G, byte base 0
-    gb[1] = G;
-    WC_HIP_CHECK(hipMemcpyAsync(d_gbase, gb, 4 * 8, hipMemcpyHostToDevice, s));
     launch_mrow_to_cols(merged, G, d_gbase, d_gbase + 2, 1u, o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len, s,
                         reinterpret_cast<const uint64_t*>(d_m));
   }
@@ -175,10 +177,13 @@ void plan_enqueue(Engine::Impl& im, Comm& comm, uint64_t n, const uint64_t* dn, 
   S.reset();
   P.d_cnt = take_aligned<unsigned long long>(S, 2 * C);
   P.d_all = take_aligned<unsigned long long>(S, (size_t)W * C);
-  WC_HIP_CHECK(hipMemsetAsync(P.d_cnt, 0, 2 * C * 8, s));
   uint64_t* mx = host_words(im) + HW_MX;
   *mx = im.max_end;
-  WC_HIP_CHECK(hipMemcpyAsync(P.d_cnt + 2 * W, mx, 8, hipMemcpyHostToDevice, s));
+  ZeroList z{};  // counts | max offset (from a page-locked host word) | cursor: one launch, disjoint regions
+  z.add(P.d_cnt, 2 * (size_t)W * 8);
+  z.add(P.d_cnt + 2 * W + 1, (2 * C - 2 * (size_t)W - 1) * 8);
+  z.copy(P.d_cnt + 2 * W, mx, 8);
+  launch_zero_regions(z, s);
   launch_owner_count(im.cols.k0, im.cols.k1, im.cols.sref_len, n, dn, pass_flags, (uint32_t)W, P.d_cnt, s);
   comm.allgather(P.d_cnt, P.d_all, C * 8, s);
 }
@@ -297,11 +302,15 @@ void merge_cols_owner(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense, 
   }
   base[W] = rr;
   base[2 * W + 1] = rbt;
-  WC_HIP_CHECK(hipMemcpyAsync(d_base, base, (2 * (size_t)W + 2) * 8, hipMemcpyHostToDevice, s));
-  WC_HIP_CHECK(hipMemsetAsync(state, 0, T * 4, s));
-  WC_HIP_CHECK(hipMemsetAsync(tcnt, 0, T * 8, s));
-  launch_fill_u64(reinterpret_cast<uint64_t*>(tfirst), ~0ull, T, s);
-  WC_HIP_CHECK(hipMemsetAsync(d_m, 0, 8, s));
+  {
+    ZeroList z{};  // the owner table's state + the source bases (page-locked host words): one launch
+    z.add(state, T * 4);
+    z.add(tcnt, T * 8);
+    z.add(tfirst, T * 8, 0xFFFFFFFFu);
+    z.add(d_m, 8);
+    z.copy(d_base, base, (2 * (size_t)W + 2) * 8);
+    launch_zero_regions(z, s);
+  }
   launch_mrow_insert(recv_rows, rr, recv_bytes, d_base, d_base + W + 1, (uint32_t)W, state, tcnt, tfirst, T, row_slot,
                      s);
   launch_mrow_compact(recv_rows, state, tcnt, tfirst, T, d_base, d_base + W + 1, (uint32_t)W, merged, d_m, slot_id, s);
@@ -312,9 +321,48 @@ void merge_cols_owner(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense, 
   *own_bytes = rbt;
   unsigned long long* d_own = take_aligned<unsigned long long>(A, 2);
   unsigned long long* d_owns = take_aligned<unsigned long long>(A, 2 * (size_t)W);
-  WC_HIP_CHECK(hipMemcpyAsync(d_own, d_m, 8, hipMemcpyDeviceToDevice, s));
-  WC_HIP_CHECK(hipMemcpyAsync(d_own + 1, own_bytes, 8, hipMemcpyHostToDevice, s));
+  {
+    ZeroList z{};  // (merged rows, bytes): both copies in one launch
+    z.copy(d_own, d_m, 8);
+    z.copy(d_own + 1, own_bytes, 8);
+    launch_zero_regions(z, s);
+  }
+  // dense: number each owner's dictionary (owner-local indices), return them to
+  // the senders in the same RCCL launch as the (rows, bytes) all-gather, then
+  // scatter the local counts into dense vectors sized for the bound (global id
+  // = owner base from the gathered counts + index, on the device) — all
+  // enqueued before the host waits for the counts
+  uint32_t* ids = nullptr;
+  uint32_t* ids_back = nullptr;
+  uint64_t *vc = nullptr, *vf = nullptr;
+  const uint64_t vpad_cap = (P.Gmax + W - 1) / W * W;
+  if (dense) {
+    ids = take_aligned<uint32_t>(A, rr);
+    ids_back = take_aligned<uint32_t>(A, tr);
+    launch_row_ids(row_slot, slot_id, rr, d_owns, 0u, ids, s);  // rank 0: no base
+  }
+  comm.group_begin();
   comm.allgather(d_own, d_owns, 16, s);
+  if (dense) {
+    const auto iro = rescale(P.ro_r, 4), irb = rescale(P.rb_r, 4), iso = rescale(P.so_r, 4), isb = rescale(P.sb_r, 4);
+    comm.alltoallv(ids, iro.data(), irb.data(), ids_back, iso.data(), isb.data(), s);
+  }
+  comm.group_end();
+  if (dense) {
+    vc = take_aligned<uint64_t>(A, vpad_cap);
+    vf = take_aligned<uint64_t>(A, vpad_cap);
+    uint64_t* seg = host_words(im) + HW_SEG;  // send-row starts per owner
+    for (int p = 0; p <= W; ++p) seg[p] = p < W ? P.so_r[p] / sizeof(MRow) : tr;
+    uint64_t* d_seg = take_aligned<uint64_t>(A, (size_t)W + 1);
+    ZeroList z{};
+    if (vpad_cap) {
+      z.add(vc, vpad_cap * 8);
+      z.add(vf, vpad_cap * 8, 0xFFFFFFFFu);
+    }
+    z.copy(d_seg, seg, ((size_t)W + 1) * 8);
+    launch_zero_regions(z, s);
+    launch_scatter_ids(send_pos, ids_back, d_seg, d_owns, (uint32_t)W, im.cols.cnt, im.cols.first, n, vc, vf, s);
+  }
   std::vector<unsigned long long> owns(2 * (size_t)W);
   WC_HIP_CHECK(hipMemcpyAsync(owns.data(), d_owns, owns.size() * 8, hipMemcpyDeviceToHost, s));
   comm.sync(s);
@@ -339,54 +387,48 @@ void merge_cols_owner(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense, 
   gbase[2 * W + 1] = GB;
   WC_CHECK(G < (1ull << 32), "merged dictionary exceeds 2^32 entries");
 
-  // dense: number the dictionary (owner base + compact index), return the ids
-  // to the senders, scatter local counts into dense vectors, reduce-scatter
+  // dense: the vectors' first vpad entries are reduce-scattered (sum, min) and
+  // all-gathered below
   uint64_t* dcnt = nullptr;
   uint64_t* dfirst = nullptr;
   const uint64_t vpad = (G + W - 1) / W * W;
   if (dense) {
-    uint32_t* ids = take_aligned<uint32_t>(A, rr);
-    uint32_t* ids_back = take_aligned<uint32_t>(A, tr);
-    launch_row_ids(row_slot, slot_id, rr, gbase[R], ids, s);
-    const auto iro = rescale(P.ro_r, 4), irb = rescale(P.rb_r, 4), iso = rescale(P.so_r, 4), isb = rescale(P.sb_r, 4);
-    comm.alltoallv(ids, iro.data(), irb.data(), ids_back, iso.data(), isb.data(), s);
-    uint64_t* vc = take_aligned<uint64_t>(A, vpad);
-    uint64_t* vf = take_aligned<uint64_t>(A, vpad);
-    uint64_t* scnt = take_aligned<uint64_t>(A, vpad / W);
-    uint64_t* sfirst = take_aligned<uint64_t>(A, vpad / W);
+    WC_CHECK(vpad <= vpad_cap, "dense merge: dictionary above its bound");
     dcnt = take_aligned<uint64_t>(A, vpad);
     dfirst = take_aligned<uint64_t>(A, vpad);
-    if (vpad) {
-      WC_HIP_CHECK(hipMemsetAsync(vc, 0, vpad * 8, s));
-      launch_fill_u64(vf, ~0ull, vpad, s);
-      launch_scatter_ids(send_pos, ids_back, im.cols.cnt, im.cols.first, n, vc, vf, s);
-      comm.group_begin();  // both reductions in one RCCL launch (independent buffers)
-      comm.reduce_scatter_u64(vc, scnt, vpad / W, RedOp::Sum, s);
-      comm.reduce_scatter_u64(vf, sfirst, vpad / W, RedOp::Min, s);
-      comm.group_end();
-      comm.group_begin();
-      comm.allgather(scnt, dcnt, vpad / W * 8, s);
-      comm.allgather(sfirst, dfirst, vpad / W * 8, s);
-      comm.group_end();
-    }
   }
 
-  // 5. gather the dictionary (merged rows + bytes) to rank 0 (broadcast for all_ranks)
+  // 5. gather the dictionary (merged rows + bytes) to rank 0 (broadcast for
+  // all_ranks) — in the same RCCL launch as the dense reductions
   sr[0] = own[0] * sizeof(MRow);
   sb[0] = own[1];
   const bool have = R == 0 || all_ranks;
   MRow* grows = take_aligned<MRow>(A, G);
   uint8_t* gbytes = take_aligned<uint8_t>(A, GB);
+  uint64_t* scnt = nullptr;
+  uint64_t* sfirst = nullptr;
+  if (dense && vpad) {
+    scnt = take_aligned<uint64_t>(A, vpad / W);
+    sfirst = take_aligned<uint64_t>(A, vpad / W);
+  }
   comm.group_begin();
+  if (dense && vpad) {
+    comm.reduce_scatter_u64(vc, scnt, vpad / W, RedOp::Sum, s);
+    comm.reduce_scatter_u64(vf, sfirst, vpad / W, RedOp::Min, s);
+  }
   comm.alltoallv(merged, zs.data(), sr.data(), grows, go_r.data(), gb_r.data(), s);
   comm.alltoallv(recv_bytes, zs.data(), sb.data(), gbytes, go_b.data(), gb_b.data(), s);
   comm.group_end();
+  comm.group_begin();
+  if (dense && vpad) {
+    comm.allgather(scnt, dcnt, vpad / W * 8, s);
+    comm.allgather(sfirst, dfirst, vpad / W * 8, s);
+  }
   if (all_ranks) {
-    comm.group_begin();
     comm.broadcast(grows, G * sizeof(MRow), 0, s);
     comm.broadcast(gbytes, GB, 0, s);
-    comm.group_end();
   }
+  comm.group_end();
   KeyCols o;
   o.n = have ? G : 0;
   if (have) {

@@ -235,16 +235,28 @@ void launch_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* 
                         const uint64_t* dn = nullptr);
 void launch_iota_u32(uint32_t* v, uint64_t n, hipStream_t s);
 
-// util.hip: zero several device regions / copy several small device regions
-// into page-locked host memory, one launch each (sizes in 32-bit words).
-constexpr int ZERO_MAX_REGIONS = 6, PUB_MAX_REGIONS = 4;
+// util.hip: fill several device regions (+ a few small copies, e.g. host words
+// from page-locked memory into device buffers) / copy several small device
+// regions into page-locked host memory, one launch each (sizes in 32-bit words).
+constexpr int ZERO_MAX_REGIONS = 8, ZERO_MAX_COPIES = 4, PUB_MAX_REGIONS = 4;
 struct ZeroList {
   uint32_t* ptr[ZERO_MAX_REGIONS];
   uint64_t words[ZERO_MAX_REGIONS];
+  uint32_t val[ZERO_MAX_REGIONS];  // the 32-bit fill pattern (0: zeroing)
   int n;
-  void add(void* p, uint64_t bytes) {
+  const uint32_t* csrc[ZERO_MAX_COPIES];  // small copies (device or page-locked host source)
+  uint32_t* cdst[ZERO_MAX_COPIES];
+  uint32_t cwords[ZERO_MAX_COPIES];
+  int nc;
+  void add(void* p, uint64_t bytes, uint32_t pattern = 0) {
     ptr[n] = static_cast<uint32_t*>(p);
+    val[n] = pattern;
     words[n++] = bytes / 4;
+  }
+  void copy(void* dst, const void* src, uint64_t bytes) {
+    cdst[nc] = static_cast<uint32_t*>(dst);
+    csrc[nc] = static_cast<const uint32_t*>(src);
+    cwords[nc++] = (uint32_t)(bytes / 4);
   }
 };
 struct PubList {
@@ -299,9 +311,10 @@ void launch_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rbase, co
                          uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first, uint64_t* soff, uint32_t* slen,
                          hipStream_t s, const uint64_t* dn = nullptr);  // dn: device-side row count (n a bound)
 void launch_combine_u64(uint64_t* dst, const uint64_t* src, uint64_t n, int op, hipStream_t s);  // 0 sum 1 min 2 max
-void launch_row_ids(const uint32_t* row_slot, const uint32_t* slot_id, uint64_t R, uint64_t id_base, uint32_t* ids,
-                    hipStream_t s);
-void launch_scatter_ids(const uint32_t* send_pos, const uint32_t* ids_back, const uint64_t* cnt, const uint64_t* first,
-                        uint64_t n, uint64_t* dcnt, uint64_t* dfirst, hipStream_t s);
+void launch_row_ids(const uint32_t* row_slot, const uint32_t* slot_id, uint64_t R, const unsigned long long* owns,
+                    uint32_t rank, uint32_t* ids, hipStream_t s);  // owns: all-gathered (rows, bytes) per owner
+void launch_scatter_ids(const uint32_t* send_pos, const uint32_t* ids_back, const uint64_t* seg,
+                        const unsigned long long* owns, uint32_t W, const uint64_t* cnt, const uint64_t* first,
+                        uint64_t n, uint64_t* dcnt, uint64_t* dfirst, hipStream_t s);  // ids_back: owner-local
 
 }  // namespace wc

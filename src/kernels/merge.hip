@@ -13,6 +13,7 @@
 // the ids to the senders, and scatters local counts into dense vectors by id
 // (wc_scatter_ids) for the reduce-scatter.  wc_combine_u64 is the loopback
 // communicator's reduction.
+#include "../common/hip_util.hpp"
 #include "kernels.hpp"
 #include "keys.hpp"
 #include "lds_table.hpp"
@@ -280,19 +281,45 @@ __global__ void __launch_bounds__(256) wc_mrow_compact(const MRow* rows, const u
 
 // Dense merge: global id of received row r = this owner's id base + the compact
 // index of the slot the row merged into.
-__global__ void wc_row_ids(const uint32_t* row_slot, const uint32_t* slot_id, uint64_t R, uint64_t id_base,
-                           uint32_t* ids) {
+// id base = the merged rows of the owners before this one, from the all-gathered
+// (rows, bytes) pairs `owns` (no host round trip).
+__global__ void wc_row_ids(const uint32_t* row_slot, const uint32_t* slot_id, uint64_t R,
+                           const unsigned long long* owns, uint32_t rank, uint32_t* ids) {
+  uint64_t id_base = 0;
+  for (uint32_t p = 0; p < rank; ++p) id_base += owns[2 * p];
   for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < R; r += (uint64_t)gridDim.x * blockDim.x)
     ids[r] = (uint32_t)(id_base + slot_id[row_slot[r]]);
 }
 
-// Dense merge: local key i (sent as row send_pos[i], whose id came back in
-// ids_back) stores its count and first offset at its global id — ids of one
+// Dense merge: local key i (sent as row send_pos[i], whose owner-local index
+// came back in ids_back) stores its count and first offset at its global id =
+// the owner's base (merged rows of the owners before it, from the all-gathered
+// (rows, bytes) pairs `owns`) + the index; the owner of send row j is the
+// segment of the send layout (`seg`: W + 1 row starts) holding j.  Ids of one
 // rank's keys are distinct, so plain stores.
-__global__ void wc_scatter_ids(const uint32_t* send_pos, const uint32_t* ids_back, const uint64_t* cnt,
-                               const uint64_t* first, uint64_t n, uint64_t* dcnt, uint64_t* dfirst) {
+__global__ void __launch_bounds__(256) wc_scatter_ids(const uint32_t* send_pos, const uint32_t* ids_back,
+                                                      const uint64_t* seg, const unsigned long long* owns, uint32_t W,
+                                                      const uint64_t* cnt, const uint64_t* first, uint64_t n,
+                                                      uint64_t* dcnt, uint64_t* dfirst) {
+  __shared__ uint64_t lseg[MERGE_MAX_RANKS + 1], lbase[MERGE_MAX_RANKS];
+  if (threadIdx.x == 0) {
+    uint64_t b = 0;
+    for (uint32_t o = 0; o < W; ++o) {
+      lbase[o] = b;
+      b += owns[2 * o];
+    }
+  }
+  for (uint32_t o = threadIdx.x; o <= W; o += blockDim.x) lseg[o] = seg[o];
+  __syncthreads();
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t g = ids_back[send_pos[i]];
+    const uint32_t j = send_pos[i];
+    uint32_t lo = 0, hi = W - 1;  // the last owner whose segment starts at or before j
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (lseg[mid] <= j) lo = mid;
+      else hi = mid - 1;
+    }
+    const uint64_t g = lbase[lo] + ids_back[j];
     dcnt[g] = cnt[i];
     dfirst[g] = first[i];
   }
@@ -357,15 +384,17 @@ void launch_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rbase, co
                        first, soff, slen);
 }
 
-void launch_row_ids(const uint32_t* row_slot, const uint32_t* slot_id, uint64_t R, uint64_t id_base, uint32_t* ids,
-                    hipStream_t s) {
-  if (R) hipLaunchKernelGGL(dev::wc_row_ids, dev::mgrid(R), dim3(256), 0, s, row_slot, slot_id, R, id_base, ids);
+void launch_row_ids(const uint32_t* row_slot, const uint32_t* slot_id, uint64_t R, const unsigned long long* owns,
+                    uint32_t rank, uint32_t* ids, hipStream_t s) {
+  if (R) hipLaunchKernelGGL(dev::wc_row_ids, dev::mgrid(R), dim3(256), 0, s, row_slot, slot_id, R, owns, rank, ids);
 }
-void launch_scatter_ids(const uint32_t* send_pos, const uint32_t* ids_back, const uint64_t* cnt, const uint64_t* first,
+void launch_scatter_ids(const uint32_t* send_pos, const uint32_t* ids_back, const uint64_t* seg,
+                        const unsigned long long* owns, uint32_t W, const uint64_t* cnt, const uint64_t* first,
                         uint64_t n, uint64_t* dcnt, uint64_t* dfirst, hipStream_t s) {
+  WC_CHECK(W >= 1 && W <= MERGE_MAX_RANKS, "scatter_ids: 1..64 ranks");
   if (n)
-    hipLaunchKernelGGL(dev::wc_scatter_ids, dev::mgrid(n), dim3(256), 0, s, send_pos, ids_back, cnt, first, n, dcnt,
-                       dfirst);
+    hipLaunchKernelGGL(dev::wc_scatter_ids, dev::mgrid(n), dim3(256), 0, s, send_pos, ids_back, seg, owns, W, cnt,
+                       first, n, dcnt, dfirst);
 }
 void launch_combine_u64(uint64_t* dst, const uint64_t* src, uint64_t n, int op, hipStream_t s) {
   if (n) hipLaunchKernelGGL(dev::wc_combine_u64, dev::mgrid(n), dim3(256), 0, s, dst, src, n, op);

@@ -1,6 +1,7 @@
 // util.hip — two small launch-count kernels of the pass / finalize plumbing.
 //
-//  wc_zero_regions  zeroes up to ZERO_MAX_REGIONS device regions in ONE launch:
+//  wc_zero_regions  fills up to ZERO_MAX_REGIONS device regions (and does up to
+//                   ZERO_MAX_COPIES small copies) in ONE launch:
 //                   the per-pass counters + hot-key sampling state, and (after
 //                   Engine::reset) the table occupancy and key-arena cursor.  It
 //                   replaces four hipMemsetAsync calls whose host-side enqueue
@@ -27,11 +28,15 @@ __global__ void __launch_bounds__(256) wc_zero_regions(ZeroList z) {
   for (int r = 0; r < z.n; ++r) {
     uint32_t* p = z.ptr[r];
     const uint64_t words = z.words[r];
+    const uint32_t v = z.val[r];
     const uint64_t quads = (reinterpret_cast<uintptr_t>(p) & 15) == 0 ? words / 4 : 0;
     uint4* q = reinterpret_cast<uint4*>(p);
-    for (uint64_t i = tid; i < quads; i += stride) q[i] = make_uint4(0, 0, 0, 0);
-    for (uint64_t i = quads * 4 + tid; i < words; i += stride) p[i] = 0;
+    for (uint64_t i = tid; i < quads; i += stride) q[i] = make_uint4(v, v, v, v);
+    for (uint64_t i = quads * 4 + tid; i < words; i += stride) p[i] = v;
   }
+  if (blockIdx.x == 0)
+    for (int c = 0; c < z.nc; ++c)
+      for (uint32_t i = threadIdx.x; i < z.cwords[c]; i += 256) z.cdst[c][i] = z.csrc[c][i];
 }
 
 __global__ void __launch_bounds__(256) wc_publish(PubList c) {
@@ -50,8 +55,8 @@ __global__ void __launch_bounds__(256) wc_publish(PubList c) {
 }  // namespace dev
 
 void launch_zero_regions(const ZeroList& z, hipStream_t s) {
-  if (z.n == 0) return;
-  WC_CHECK(z.n <= ZERO_MAX_REGIONS, "launch_zero_regions: too many regions");
+  if (z.n == 0 && z.nc == 0) return;
+  WC_CHECK(z.n <= ZERO_MAX_REGIONS && z.nc <= ZERO_MAX_COPIES, "launch_zero_regions: too many regions");
   uint64_t most = 0;
   for (int r = 0; r < z.n; ++r) most = z.words[r] > most ? z.words[r] : most;
   const uint64_t blocks = std::min<uint64_t>(256, std::max<uint64_t>(1, (most / 4 + 255) / 256));

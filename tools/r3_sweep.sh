@@ -27,5 +27,7 @@ WC_MERGE_ALWAYS=1 run merge_shuffle 120 --steps 300 --merge shuffle || exit 1
 WC_MERGE_ALWAYS=1 run merge_dense 120 --steps 300 --merge dense || exit 1
 run c64gb 300 --config 64gb --steps 5 --warmup 1 || exit 1
 WC_HOT_RESAMPLE_EVERY=0 run c64gb_sample_every_pass 300 --config 64gb --steps 5 --warmup 1 || exit 1
+run c64gb_b 300 --config 64gb --steps 5 --warmup 1 --no-oracle || exit 1
+WC_HOT_RESAMPLE_EVERY=0 run c64gb_sample_every_pass_b 300 --config 64gb --steps 5 --warmup 1 --no-oracle || exit 1
 WC_MERGE_ALWAYS=1 run c256gb_rank 400 --config 256gb-8gpu --gpus 1 --steps 3 --warmup 1 || exit 1
 run c1tb_rank 600 --config 1tb-8gpu-host-staged --gpus 1 --steps 2 --warmup 1 || exit 1
