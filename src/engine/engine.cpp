@@ -194,10 +194,13 @@ Engine::Impl::~Impl() {
       fprintf(stderr,
               "[wc] reduce counters: records %llu, slow lanes %llu, slow wave-steps %llu, claim-loop iterations %llu, "
               "CAS failures %llu, PENDING re-reads %llu, claims %llu; run phase / wave lifetime = %.3f; blocks %llu, "
-              "mean wave lifetime %.0f clk, slowest block %llu clk\n",
+              "mean wave lifetime %.0f clk, slowest block %llu clk; record streams / wave lifetime = %.3f, LONG "
+              "records %llu (%llu blocks past the LDS queue), LONG merges / wave lifetime = %.3f\n",
               h[RS_RECORDS], h[RS_SLOW_LANES], h[RS_SLOW_WAVES], h[RS_PROBE_ITERS], h[RS_CAS_FAIL], h[RS_PENDING],
               h[RS_CLAIMS], h[RS_T_WAVE] ? (double)h[RS_T_RUNS] / h[RS_T_WAVE] : 0.0, h[RS_BLOCKS],
-              h[RS_BLOCKS] ? (double)h[RS_T_WAVE] / (h[RS_BLOCKS] * (RED_THREADS / 64)) : 0.0, h[RS_T_BLKMAX]);
+              h[RS_BLOCKS] ? (double)h[RS_T_WAVE] / (h[RS_BLOCKS] * (RED_THREADS / 64)) : 0.0, h[RS_T_BLKMAX],
+              h[RS_T_WAVE] ? (double)h[RS_T_STREAMS] / h[RS_T_WAVE] : 0.0, h[RS_NLONG], h[RS_LONG_STREAMED],
+              h[RS_T_WAVE] ? (double)h[RS_T_SLOW] / h[RS_T_WAVE] : 0.0);
     }
     (void)hipFree(d_red_stamps);
   }

@@ -120,7 +120,7 @@ struct HotArgs {
   uint8_t* long_bytes;     // [MAP_SLOTS * 64]
   const uint8_t* text;     // the sampling pass's chunk text (placement reads the sampled occurrence)
 };
-constexpr uint32_t HOT_LONG_MAX = 63;
+constexpr uint32_t HOT_LONG_MAX = 64;
 constexpr uint64_t HOT_TABLE_CAP = 1ull << 18;
 // Map hot-table geometry: 2-choice groups of HOT_GROUP_SLOTS signatures.  Two
 // slots per group (4 candidate compares and two 16-byte probe reads per token)
@@ -158,7 +158,8 @@ struct ReduceArgs {
 };
 // Reduce diagnostic counters (src/kernels/reduce.hip built with -DWC_RED_STAMPS=1).
 enum : int { RS_RECORDS = 0, RS_SLOW_LANES, RS_SLOW_WAVES, RS_PROBE_ITERS, RS_CAS_FAIL, RS_PENDING, RS_CLAIMS,
-             RS_T_WAVE, RS_T_SLOW, RS_T_RUNS, RS_BLOCKS, RS_T_BLKMAX, RED_STAMP_N };
+             RS_T_WAVE, RS_T_SLOW, RS_T_RUNS, RS_BLOCKS, RS_T_BLKMAX, RS_T_STREAMS, RS_NLONG, RS_LONG_STREAMED,
+             RED_STAMP_N };
 
 struct SynthVocab {
   const uint8_t* bytes;

@@ -34,7 +34,7 @@
 //
 // Signatures: a word of <= 7 bytes is its own 64-bit signature (bytes | len
 // << 56, one compare); 8..15-byte words use len << 56 | low 7 bytes of
-// (k0 ^ tail) plus k0 in `side`.  LONG words of 16..63 bytes are hot-table
+// (k0 ^ tail) plus k0 in `side`.  LONG words of 16..64 bytes are hot-table
 // words too (0xFF << 56 | a key hash, `side` = the length): a hit needs the
 // token's bytes to equal the slot's 64-byte copy of the word, so exactness
 // never rests on the hash; every other LONG token is a record whose bytes the
@@ -139,7 +139,7 @@ __device__ __forceinline__ uint32_t long_group_hash(uint64_t sig) {
   return mix32((uint32_t)sig ^ (uint32_t)(sig >> 32));
 }
 
-// Key of a word of known length 16..63 at p of an LDS text buffer (readable
+// Key of a word of known length 16..64 at p of an LDS text buffer (readable
 // to p + len + 12): k0 = first 8 bytes, the tail folded in 8-byte chunks
 // (keys.hpp key_of).
 __device__ __forceinline__ void key_long_len(const uint8_t* buf, uint32_t p, uint32_t len, uint64_t mask, uint64_t& k0,
@@ -263,9 +263,17 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs 
       const uint32_t b = __ffs(bits) - 1;
       bits &= bits - 1;
       const uint64_t rest = dm >> b;
-      const uint32_t len = rest ? (uint32_t)__ffsll((unsigned long long)rest) - 1 : 64u;
-      if (len > HOT_LONG_MAX) continue;  // (64: the length is not known inside the lane window)
       const uint32_t p = pbase + b;
+      uint32_t len;
+      if (rest) {
+        len = (uint32_t)__ffsll((unsigned long long)rest) - 1;
+      } else {  // the word runs past the lane's 64-byte window: its end in the unit's LDS copy + halo
+        uint32_t q = pbase + 64;
+        while (q < (uint32_t)(UNIT + HALO) && !is_delim(buf[q])) ++q;
+        if (q >= (uint32_t)(UNIT + HALO)) continue;  // past the halo: not a candidate
+        len = q - p;
+      }
+      if (len > HOT_LONG_MAX) continue;
       uint64_t k0, k1, sg, sd, f;
       uint32_t g;
       if (len <= KEY_INLINE_MAX) {

@@ -570,6 +570,7 @@ __device__ __forceinline__ void long_stream(RedLds& L, const ReduceArgs& a, uint
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
   auto merge_first = [&](uint32_t k) {  // wl[0, k), one per lane
+    const uint64_t t0 = WC_RED_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     wsync();
     if (lane < k) {
       const Rec r = a.rec.recs[wl[lane]];
@@ -577,6 +578,7 @@ __device__ __forceinline__ void long_stream(RedLds& L, const ReduceArgs& a, uint
       claims += merge_long(L, c, place_hash(r.k0, r.k1), r.k0, r.k1, r.co >> 32, a.chunk_base + off, off);
     }
     wsync();
+    if (WC_RED_STAMPS && lane == 0) atomicAdd(&L.st[RS_T_SLOW], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
   };
   uint32_t cnt = 0;  // wave-uniform
   for (uint32_t p = wave; p < a.map_blocks; p += nwaves) {
@@ -634,6 +636,12 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   merge_stream<true, RED_UNROLL>(L, a, b, a.rec.recs12, wave, nwaves, nrb, rb, (uint32_t)sub, shift, claims);
   merge_stream<false, RED_UNROLL_24>(L, a, b, a.rec.recs, wave, nwaves, nrb, rb, (uint32_t)sub, shift, claims);
   __syncthreads();  // every LONG record is queued (or counted past the queue)
+  if (WC_RED_STAMPS && (tid & 63) == 0)
+    atomicAdd(&L.st[RS_T_STREAMS], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
+  if (WC_RED_STAMPS && tid == 0) {
+    L.st[RS_NLONG] = L.nlong;
+    L.st[RS_LONG_STREAMED] = L.nlong > LONGQ ? 1 : 0;
+  }
   if (L.nlong) {
     if (L.nlong <= LONGQ) long_queue(L, a, b, L.nlong, claims);
     else long_stream(L, a, b, wave, nwaves, nrb, rb, (uint32_t)sub, shift, claims);
