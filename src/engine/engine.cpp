@@ -95,20 +95,17 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   rec.cap = rec_total;
   rec.count = rec_mem.take_n<uint32_t>(ncount);
 
-  hot_mem.reserve(HOT_TABLE_CAP * (8 + 4) + HOT_TABLE_CAP * 16 + 2 * MAP_SLOTS * 8 + (HOT_SEL_BINS + 3) * 4 +
-                  (size_t)MAP_SLOTS * 64 +
-                  HOT_GROUPS * 4 + 8192);
-  hot.cap = HOT_TABLE_CAP;
-  hot.fp = hot_mem.take_n<unsigned long long>(HOT_TABLE_CAP);
-  hot.cnt = hot_mem.take_n<uint32_t>(HOT_TABLE_CAP);
-  hot.img_sig = hot_mem.take_n<uint64_t>(MAP_SLOTS);  // cleared region: fp .. gocc (one memset)
-  hot.img_side = hot_mem.take_n<uint64_t>(MAP_SLOTS);
-  hot.sel = hot_mem.take_n<uint32_t>(HOT_SEL_BINS + 3);
-  hot.gocc = hot_mem.take_n<uint32_t>(HOT_GROUPS);
-  hot_clear_bytes = (size_t)(reinterpret_cast<uint8_t*>(hot.gocc + HOT_GROUPS) - reinterpret_cast<uint8_t*>(hot.fp));
-  hot.sig = hot_mem.take_n<uint64_t>(HOT_TABLE_CAP);
-  hot.side = hot_mem.take_n<uint64_t>(HOT_TABLE_CAP);
-  hot.long_bytes = hot_mem.take_n<uint8_t>((size_t)MAP_SLOTS * 64);
+  const size_t stage_n = (size_t)HOT_PARTS * map_blocks;
+  hot_mem.reserve(stage_n * HOT_STAGE_CAP * sizeof(HotEnt) + stage_n * 4 +
+                  (size_t)HOT_PARTS * HOT_PART_TOP * (20 + 64) + HOT_PARTS * 4 + 8192);
+  hot.stage = hot_mem.take_n<HotEnt>(stage_n * HOT_STAGE_CAP);
+  hot.stage_n = hot_mem.take_n<uint32_t>(stage_n);
+  hot.cand_sig = hot_mem.take_n<uint64_t>((size_t)HOT_PARTS * HOT_PART_TOP);
+  hot.cand_side = hot_mem.take_n<uint64_t>((size_t)HOT_PARTS * HOT_PART_TOP);
+  hot.cand_cnt = hot_mem.take_n<uint32_t>((size_t)HOT_PARTS * HOT_PART_TOP);
+  hot.cand_n = hot_mem.take_n<uint32_t>(HOT_PARTS);
+  hot.maxb = map_blocks;
+  hot.long_bytes = hot_mem.take_n<uint8_t>((size_t)HOT_PARTS * HOT_PART_TOP * 64);
   WC_HIP_CHECK(hipMalloc(&d_ctr, sizeof(DevCounters)));
   WC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_ctr), sizeof(DevCounters), hipHostMallocDefault));
   h_pass_seq.resize(256);
@@ -242,7 +239,7 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
                                uint32_t log2_rb, uint32_t blocks, bool copy_occupancy) {
   WC_CHECK((reinterpret_cast<uintptr_t>(text) & 15) == 0, "chunk text must be 16-byte aligned");
   mark(EV_PASS);
-  // one zeroing launch: pass counters, sampling state and, after a reset, the
+  // one zeroing launch: pass counters and, after a reset, the
   // table occupancy and the key-arena cursor
   // reuse the job's hot-table image while it keeps its hit rate (the previous
   // pass's miss share vs that of the pass that sampled it)
@@ -251,7 +248,6 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   pass_sampled = sample;
   ZeroList z{};
   z.add(d_ctr, sizeof(DevCounters));
-  if (sample) z.add(hot.fp, hot_clear_bytes);
   if (reset_pending) {
     z.add(table().occupancy, ((size_t)1 << table().log2_buckets) * 4);
     z.add(d_arena_cursor, sizeof(unsigned long long));
@@ -265,6 +261,7 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   MapArgs m{text, len, avail, prev, log2_rb, pass_rec, d_ctr->flags, &d_ctr->tokens, k1_mask, d_stamps, d_blk};
   if (d_stamps) blocks_stamped += blocks;
   hot.text = text;
+  hot.nblk = blocks;
   launch_map(m, hot, blocks, s, sample);
   mark(EV_MAP);
   if (sync_debug) {  // WC_SYNC_DEBUG: attribute a device fault to a kernel and a chunk

@@ -71,7 +71,6 @@ struct Engine::Impl {
   // hot-key sampling workspace of the map (HotArgs)
   DeviceArena hot_mem;
   HotArgs hot{};
-  size_t hot_clear_bytes = 0;  // fp, cnt, image, selection state: zeroed before every sampling pass
   // Hot-table reuse inside a job (never across jobs: reset() drops it): a pass
   // keeps the image its job's last sampling pass built while its miss share
   // (records / tokens) stays within hot_resample_slack of that pass's, and

@@ -101,27 +101,38 @@ struct MapArgs {
   unsigned long long* stamps;  // diagnostic build: per-phase s_memtime sums (MAP_STAMP_N), nullptr = off
   unsigned long long* blk;     // diagnostic: per map block {start, end (s_memrealtime), XCC id, units}, nullable
 };
-// Hot-key sampling workspace (map.hip): a global fingerprint table filled by
-// wc_hot_sample (fp/cnt zeroed before each chunk) and the LDS table image
-// written by wc_hot_select.
+// Hot-key sampling workspace (map.hip).  Two launches, no device-scope
+// atomics and nothing to zero: wc_hot_sample writes every map block's sampled
+// words, split by fingerprint into HOT_PARTS partitions, to its own stage
+// cells; wc_hot_merge (one block per partition) sums them in LDS and keeps the
+// partition's HOT_PART_TOP most frequent words as candidates.  Every wc_map
+// block then selects the HOT_K most frequent candidates and places them in its
+// own LDS table (blocks need not agree: each flushes its slots with full keys).
+struct HotEnt {  // one sampled word (32 B)
+  uint64_t sig, side;
+  uint32_t cnt, pad;
+  uint64_t fp;  // 64-bit fingerprint, never 0; its top byte is the partition
+};
 struct HotArgs {
-  unsigned long long* fp;  // [cap] 0 = empty
-  uint32_t* cnt;           // [cap]
-  uint64_t* sig;           // [cap] signature of the first block's sample of the word
-  uint64_t* side;          // [cap]
-  uint64_t cap;            // power of two
-  uint64_t* img_sig;       // [MAP_SLOTS] zeroed before each chunk
-  uint64_t* img_side;      // [MAP_SLOTS]
-  uint32_t* sel;           // [HOT_SEL_BINS + 3] zeroed: count histogram, threshold, tie quota / counter
-  uint32_t* gocc;          // [HOT_GROUPS] zeroed: fill of each image group
-  // Hot LONG words (16..HOT_LONG_MAX bytes): the placement copies each placed
-  // word's bytes (zero-padded) into its slot's 64-byte line; the map verifies
-  // every hit against it byte for byte (persists while the image is reused)
-  uint8_t* long_bytes;     // [MAP_SLOTS * 64]
-  const uint8_t* text;     // the sampling pass's chunk text (placement reads the sampled occurrence)
+  HotEnt* stage;           // [HOT_PARTS][maxb][HOT_STAGE_CAP] per (partition, map block)
+  uint32_t* stage_n;       // [HOT_PARTS][maxb] entries written (every cell written by its block)
+  uint32_t* cand_cnt;      // [HOT_PARTS][HOT_PART_TOP] candidates of each partition (SoA)
+  uint64_t* cand_sig;
+  uint64_t* cand_side;     // side word; LONG words: the length | candidate index << 32
+  uint32_t* cand_n;        // [HOT_PARTS]
+  uint32_t maxb;           // stage stride: the engine's map grid
+  uint32_t nblk;           // map blocks of the sampling pass (<= maxb)
+  // Hot LONG words (16..HOT_LONG_MAX bytes): wc_hot_merge copies each LONG
+  // candidate's bytes (zero-padded) into the candidate's 64-byte line; the map
+  // verifies every hit against it byte for byte (persists while the candidates
+  // are reused)
+  uint8_t* long_bytes;     // [HOT_PARTS * HOT_PART_TOP * 64]
+  const uint8_t* text;     // the sampling pass's chunk text (the merge reads the sampled occurrence)
 };
 constexpr uint32_t HOT_LONG_MAX = 64;
-constexpr uint64_t HOT_TABLE_CAP = 1ull << 18;
+constexpr int HOT_PARTS = 256;       // fingerprint partitions (one wc_hot_merge block each)
+constexpr int HOT_STAGE_CAP = 8;     // words per (partition, map block) cell; more are dropped (a heuristic)
+constexpr int HOT_PART_TOP = 32;     // candidates kept per partition (the HOT_K words average 14)
 // Map hot-table geometry: 2-choice groups of HOT_GROUP_SLOTS signatures.  Two
 // slots per group (4 candidate compares and two 16-byte probe reads per token)
 // holds 7/8 of the slots at the hit rate that 4-slot groups (8 compares, four
@@ -133,8 +144,7 @@ constexpr uint64_t HOT_TABLE_CAP = 1ull << 18;
 constexpr int HOT_GROUP_SLOTS = WC_HOT_GS;
 constexpr int HOT_GROUPS = MAP_SLOTS / HOT_GROUP_SLOTS;
 static_assert(HOT_GROUP_SLOTS == 2 || HOT_GROUP_SLOTS == 4, "hot-table groups of 2 or 4 slots");
-constexpr int HOT_SEL_BINS = 4096;
-constexpr int HOT_SEL_BLOCKS = 256;
+constexpr int HOT_SEL_BINS = 4096;  // sampled-count histogram bins (counts clamp to the last)
 
 // In-kernel phase stamps of the map (diagnostic build, WC_MAP_STAMPS=1): shares
 // of wave lifetime per phase, then counters.
@@ -170,7 +180,7 @@ struct SynthVocab {
 };
 
 // ---- launchers (all stream-ordered, no host sync) ----------------------------
-// wc_hot_sample + wc_hot_hist/_threshold/_place + wc_map (HotArgs zeroed first: hot_clear);
+// wc_hot_sample + wc_hot_merge + wc_map;
 // sample = false: wc_map alone, on the hot-table image an earlier pass of the job built.
 void launch_map(const MapArgs& a, const HotArgs& h, uint32_t map_blocks, hipStream_t s, bool sample = true);
 void launch_reduce(const ReduceArgs& a, hipStream_t s);

@@ -4,19 +4,20 @@
 // Reference: mapKernel / mapper (/root/reference/main.cu:37-54, 109-117) copy
 // one pre-split line's words per thread with <= 9 threads active; the host
 // tokenizes (main.cu:181-206).  Here the GPU tokenizes and pre-aggregates in
-// three launches per chunk:
+// three launches per sampled chunk:
 //
 //  wc_hot_sample  every map block tokenizes HOT_SAMPLE units spread over its
-//                 range, counts their words in an LDS table and adds the counts
-//                 to a global fingerprint table (one global atomic per distinct
-//                 word per block);
-//  wc_hot_hist / _threshold / _place  keep the HOT_K most frequent sampled
-//                 words and place them in a 2-choice table image of 2-slot groups
-//                 (4096 slots of 64-bit signatures + side words);
+//                 range, counts their words in an LDS table and writes them,
+//                 split into fingerprint partitions, to its own stage cells;
+//  wc_hot_merge   one block per partition sums the cells in LDS and keeps the
+//                 partition's most frequent words as candidates;
 //  wc_map         persistent, ONE 1024-thread block (16 waves) per CU over a
-//                 contiguous range of 2 KiB text units.  The block loads the
-//                 image into LDS; each wave grabs its next unit from an LDS
-//                 cursor and prefetches it into registers (32 B per lane) while
+//                 contiguous range of 2 KiB text units.  The block selects
+//                 the HOT_K most frequent candidates and places them in a
+//                 2-choice table of 2-slot groups in its LDS (4096 slots of
+//                 64-bit signatures + side words; blocks need not agree:
+//                 each flushes its slots with full keys).  Each wave grabs its
+//                 next unit from an LDS cursor and prefetches it into registers (32 B per lane) while
 //                 tokenizing the current one from its private LDS copy:
 //                 SWAR delimiter masks -> token starts `~d & (d << 1 | c)` ->
 //                 ballot-bit prefix sum -> a list of (position, length)
@@ -35,8 +36,9 @@
 // Signatures: a word of <= 7 bytes is its own 64-bit signature (bytes | len
 // << 56, one compare); 8..15-byte words use len << 56 | low 7 bytes of
 // (k0 ^ tail) plus k0 in `side`.  LONG words of 16..64 bytes are hot-table
-// words too (0xFF << 56 | a key hash, `side` = the length): a hit needs the
-// token's bytes to equal the slot's 64-byte copy of the word, so exactness
+// words too (0xFF << 56 | a key hash, `side` = the length | the candidate's
+// index << 32): a hit needs the token's bytes to equal the candidate's 64-byte
+// copy of the word, so exactness
 // never rests on the hash; every other LONG token is a record whose bytes the
 // reducer compares.
 #include <type_traits>
@@ -221,13 +223,19 @@ struct SampleLds {
   uint64_t sig[MAP_SLOTS];
   uint64_t side[MAP_SLOTS];
   uint32_t cnt[MAP_SLOTS];
+  uint32_t pn[HOT_PARTS];  // words of this block in each fingerprint partition
   alignas(16) uint8_t buf[MAP_WAVES][BUF];
 };
 static_assert(sizeof(SampleLds) <= 160 * 1024, "one sample block per CU");
 
 // Each wave takes sampled units (stride over the block's range) and counts
-// their inline words per lane; the block then adds its table into the global
-// fingerprint table (HotArgs::cap slots, linear probing, device atomics).
+// their words per lane in the block's LDS table; the block then writes its
+// words, split by fingerprint partition, to its own stage cells with plain
+// stores (a cell holds HOT_STAGE_CAP words; the rest of a crowded cell is
+// dropped — the table is only an accelerator, exactness never depends on it).
+// The round-2 form added every block's words into one global fingerprint table
+// with device CAS + add: the Zipf head's slots took one atomic pair from each
+// of the 256 blocks in turn, two thirds of a 35 us launch.
 __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs h) {
   __shared__ SampleLds L;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -235,6 +243,7 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs 
     L.fp[s] = 0;
     L.cnt[s] = 0;
   }
+  if (tid < HOT_PARTS) L.pn[tid] = 0;
   __syncthreads();
   uint64_t ub, ue;
   unit_range(a.chunk_len, gridDim.x, blockIdx.x, ub, ue);
@@ -311,88 +320,171 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs 
     wave_sync();
   }
   __syncthreads();
-  const uint64_t gmask = h.cap - 1;
+  const size_t cell0 = (size_t)blockIdx.x * HOT_STAGE_CAP;  // + partition * maxb * HOT_STAGE_CAP
   for (int s = tid; s < MAP_SLOTS; s += MAP_THREADS) {
     const uint32_t c = L.cnt[s];
     if (!c) continue;
     const uint64_t f = L.fp[s];
-    uint64_t gs = (f >> 20) & gmask;
-    for (int n = 0; n < 64; ++n) {  // bounded: a word that finds no room is simply not a candidate
-      const unsigned long long old = atomicCAS(&h.fp[gs], 0ull, (unsigned long long)f);
-      if (old == 0ull || old == f) {
-        atomicAdd(&h.cnt[gs], c);
-        if (old == 0ull) {  // first block to see the word stores it (read by the next launch)
-          h.sig[gs] = L.sig[s];
-          h.side[gs] = L.side[s];
-        }
-        break;
-      }
-      gs = (gs + 1) & gmask;
-    }
+    const uint32_t part = (uint32_t)(f >> 56);
+    const uint32_t at = atomicAdd(&L.pn[part], 1u);
+    if (at >= (uint32_t)HOT_STAGE_CAP) continue;
+    HotEnt e;
+    e.sig = L.sig[s];
+    e.side = L.side[s];
+    e.cnt = c;
+    e.pad = 0;
+    e.fp = f;
+    h.stage[(size_t)part * h.maxb * HOT_STAGE_CAP + cell0 + at] = e;
   }
+  __syncthreads();
+  if (tid < HOT_PARTS) h.stage_n[(size_t)tid * h.maxb + blockIdx.x] = min(L.pn[tid], (uint32_t)HOT_STAGE_CAP);
 }
 
 // ------------------------------------------------------------------ selection
-// Three short launches over the fingerprint table (HOT_SEL_BLOCKS blocks for
-// the two scans): count histogram -> threshold keeping <= HOT_K words (ties
-// at the threshold taken while room remains) -> 2-choice placement into the
-// image (the emptier of the word's two groups, else the other; both full: the
-// word stays out).  HotArgs::sel holds [0, SEL_BINS) histogram, then the
-// threshold, the tie quota and the tie counter; HotArgs::gocc the group fill.
+// Block-wide (1024 threads) selection threshold over a count histogram of
+// HOT_SEL_BINS bins in LDS: t = the smallest count >= 1 whose words (counted
+// >= t) number <= limit (the last bin when even that holds more), cum = the
+// words counted >= t.  Thread i owns bins [4i, 4i + 4); a reverse block scan
+// gives the words counted >= each bin.  sc: 18 words of LDS scratch.
 constexpr int SEL_BINS = HOT_SEL_BINS;
-
-__global__ void __launch_bounds__(1024) wc_hot_hist(HotArgs h) {
-  __shared__ uint32_t hist[SEL_BINS];
-  for (int i = threadIdx.x; i < SEL_BINS; i += 1024) hist[i] = 0;
-  __syncthreads();
-  for (uint64_t s = blockIdx.x * 1024ull + threadIdx.x; s < h.cap; s += (uint64_t)gridDim.x * 1024) {
-    const uint32_t c = h.cnt[s];
-    if (c) atomicAdd(&hist[min(c, (uint32_t)SEL_BINS - 1)], 1u);
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < SEL_BINS; i += 1024)
-    if (hist[i]) atomicAdd(&h.sel[i], hist[i]);
-}
-
-// Threshold t: the smallest count whose words (counted >= t) fit in HOT_K.
-// One block: thread i owns bins [4i, 4i + 4); a reverse block scan gives the
-// number of words counted >= each bin.
-__global__ void __launch_bounds__(1024) wc_hot_threshold(HotArgs h) {
+__device__ void count_threshold(const uint32_t* hist, uint32_t limit, uint32_t* sc, uint32_t& t_out,
+                                uint32_t& cum_out) {
   static_assert(SEL_BINS == 4 * 1024, "threshold: 4 bins per thread");
-  __shared__ uint32_t wsum[16];
-  __shared__ uint32_t best;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   uint32_t b[4], own = 0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) own += b[i] = h.sel[4 * tid + i];
-  // inclusive scan from the top: suffix = words in bins >= 4 tid
-  uint32_t x = own;
+  for (int i = 0; i < 4; ++i) own += b[i] = hist[4 * tid + i];
+  uint32_t x = own;  // inclusive scan from the top: words in bins >= 4 tid within the wave
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t y = __shfl_down(x, o);
     if (lane + o < 64) x += y;
   }
-  if (lane == 0) wsum[wave] = x;
-  if (tid == 0) best = SEL_BINS;
+  if (lane == 0) sc[wave] = x;
+  if (tid == 0) sc[16] = SEL_BINS;
   __syncthreads();
   uint32_t above = 0;  // words in the waves above this one
-  for (int w = wave + 1; w < 16; ++w) above += wsum[w];
+  for (int w = wave + 1; w < 16; ++w) above += sc[w];
   const uint32_t suf0 = x + above;  // words counted >= 4 tid
   uint32_t suf = suf0, t = SEL_BINS;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {  // words counted >= bin 4 tid + i
-    if (t == SEL_BINS && suf <= HOT_K && 4 * tid + i >= 1) t = 4 * tid + i;
+    if (t == SEL_BINS && suf <= limit && 4 * tid + i >= 1) t = 4 * tid + i;
     suf -= b[i];
   }
-  if (t < SEL_BINS) atomicMin(&best, t);
+  if (t < SEL_BINS) atomicMin(&sc[16], t);
   __syncthreads();
-  const uint32_t tt = best == SEL_BINS ? 1u : best;
-  if ((uint32_t)tid == tt / 4) {  // the owner of bin tt: words counted >= tt, then the tie quota
+  const uint32_t tt = sc[16] == SEL_BINS ? SEL_BINS - 1 : sc[16];
+  if ((uint32_t)tid == tt / 4) {
     uint32_t cum = suf0;
     for (uint32_t i = 0; i < tt % 4; ++i) cum -= b[i];
-    h.sel[SEL_BINS] = tt;
-    h.sel[SEL_BINS + 1] = tt > 1 ? HOT_K - min(cum, HOT_K) : 0;
-    h.sel[SEL_BINS + 2] = 0;
+    sc[17] = cum;
   }
+  __syncthreads();
+  t_out = tt;
+  cum_out = sc[17];
+  __syncthreads();  // sc is reusable
+}
+
+// One block per fingerprint partition: every map block's stage cell of the
+// partition is summed into an LDS table, then the HOT_PART_TOP most frequent
+// words (ties at the threshold while room remains) become the partition's
+// candidates.  Two dependent global steps in all (the cells' word counts, then
+// every thread's cell entries at once): a loop that issued one load per
+// iteration behind LDS atomics took 24 us.
+constexpr int MERGE_SLOTS = 4096;
+constexpr int MERGE_CELLS_PER_THREAD = 1024 / HOT_STAGE_CAP;  // cells covered by one pass of the block
+static_assert(1024 % HOT_STAGE_CAP == 0, "merge: whole cells per pass");
+struct HotMergeLds {
+  uint64_t fp[MERGE_SLOTS];
+  uint64_t sig[MERGE_SLOTS];
+  uint64_t side[MERGE_SLOTS];
+  uint32_t cnt[MERGE_SLOTS];
+  uint32_t hist[SEL_BINS];
+  uint32_t sc[18];
+  uint32_t nout, nties;
+};
+__device__ __forceinline__ void merge_insert(HotMergeLds& L, const HotEnt& e) {
+  uint32_t s = (uint32_t)(e.fp >> 20) & (MERGE_SLOTS - 1);
+  for (int k = 0; k < 64; ++k) {  // bounded: a word that finds no slot is dropped
+    uint64_t cur = L.fp[s];
+    if (cur == 0) {
+      cur = atomicCAS(reinterpret_cast<unsigned long long*>(&L.fp[s]), 0ull, (unsigned long long)e.fp);
+      if (cur == 0) {  // claimed: the claimer stores the key (read after the block barrier)
+        L.sig[s] = e.sig;
+        L.side[s] = e.side;
+        cur = e.fp;
+      }
+    }
+    if (cur == e.fp) {
+      atomicAdd(&L.cnt[s], e.cnt);
+      return;
+    }
+    s = (s + 1) & (MERGE_SLOTS - 1);
+  }
+}
+__global__ void __launch_bounds__(1024) wc_hot_merge(HotArgs h) {
+  __shared__ HotMergeLds L;
+  const int tid = threadIdx.x;
+  const uint32_t part = blockIdx.x;
+  for (int s = tid; s < MERGE_SLOTS; s += 1024) {
+    L.fp[s] = 0;
+    L.cnt[s] = 0;
+  }
+  for (int i = tid; i < SEL_BINS; i += 1024) L.hist[i] = 0;
+  if (tid == 0) L.nout = L.nties = 0;
+  __syncthreads();
+  const size_t row = (size_t)part * h.maxb;
+  // thread tid: entry (tid % CAP) of the cells tid / CAP + k * CELLS (all loads of a thread issued together)
+  const uint32_t e = tid % HOT_STAGE_CAP, c0 = tid / HOT_STAGE_CAP;
+  for (uint32_t base = 0; base < h.nblk; base += 4 * MERGE_CELLS_PER_THREAD) {
+    uint32_t n[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t blk = base + c0 + k * MERGE_CELLS_PER_THREAD;
+      n[k] = blk < h.nblk ? h.stage_n[row + blk] : 0u;
+    }
+    HotEnt x[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t blk = base + c0 + k * MERGE_CELLS_PER_THREAD;
+      if (e < n[k]) x[k] = h.stage[(row + blk) * HOT_STAGE_CAP + e];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (e < n[k]) merge_insert(L, x[k]);
+  }
+  __syncthreads();
+  for (int s = tid; s < MERGE_SLOTS; s += 1024)
+    if (L.cnt[s]) atomicAdd(&L.hist[min(L.cnt[s], (uint32_t)SEL_BINS - 1)], 1u);
+  __syncthreads();
+  uint32_t t, cum;
+  count_threshold(L.hist, HOT_PART_TOP, L.sc, t, cum);
+  const uint32_t ties = t > 1 ? HOT_PART_TOP - min(cum, (uint32_t)HOT_PART_TOP) : 0u;
+  for (int s = tid; s < MERGE_SLOTS; s += 1024) {
+    const uint32_t c = L.cnt[s];
+    if (!c || c + 1 < t) continue;
+    if (c < t && atomicAdd(&L.nties, 1u) >= ties) continue;
+    const uint32_t o = atomicAdd(&L.nout, 1u);
+    if (o >= (uint32_t)HOT_PART_TOP) continue;
+    const size_t at = (size_t)part * HOT_PART_TOP + o;
+    const uint64_t sg = L.sig[s], sd = L.side[s];
+    h.cand_cnt[at] = c;
+    h.cand_sig[at] = sg;
+    if (is_long_sig(sg)) {  // the sampled occurrence's bytes (zero-padded) -> the candidate's line
+      const uint32_t len = (uint32_t)(sd >> 32), from = (uint32_t)sd;
+      h.cand_side[at] = len | ((uint64_t)at << 32);
+      uint64_t* line = reinterpret_cast<uint64_t*>(h.long_bytes + at * 64);
+      for (uint32_t c8 = 0; c8 < 64; c8 += 8) {
+        uint64_t x = 0;
+        for (uint32_t j = 0; j < 8 && c8 + j < len; ++j) x |= (uint64_t)h.text[(size_t)from + c8 + j] << (8 * j);
+        line[c8 / 8] = x;
+      }
+    } else {
+      h.cand_side[at] = sd;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) h.cand_n[part] = min(L.nout, (uint32_t)HOT_PART_TOP);
 }
 
 // Placement in count tiers, most frequent first: pass 0 places the words
@@ -412,51 +504,93 @@ __global__ void __launch_bounds__(1024) wc_hot_threshold(HotArgs h) {
 constexpr uint32_t HOT_FIRST_MUL = WC_HOT_FIRST_MUL, HOT_MID_MUL = WC_HOT_MID_MUL;
 constexpr int HOT_PLACE_PASSES = WC_HOT_PLACE_PASSES;
 static_assert(HOT_PLACE_PASSES == 2 || HOT_PLACE_PASSES == 3, "2 or 3 placement tiers");
-__global__ void __launch_bounds__(1024) wc_hot_place(HotArgs h, int pass) {
-  const uint32_t t = h.sel[SEL_BINS], ties = h.sel[SEL_BINS + 1];
+
+constexpr uint32_t CAND_PER_THREAD = HOT_PARTS * HOT_PART_TOP / 1024;
+static_assert(HOT_PARTS * HOT_PART_TOP == 1024 * CAND_PER_THREAD && HOT_PART_TOP % CAND_PER_THREAD == 0,
+              "select: whole candidate rows per thread group");
+static_assert(MAP_THREADS == 1024, "select: one map block of 1024 threads");
+
+// One word into an LDS table image (2-choice: the emptier group, else the
+// other; both full: the word stays out).
+__device__ __forceinline__ void place_hot(uint64_t* isig, uint64_t* iside, uint32_t* gocc, uint64_t sg, uint64_t sd) {
+  uint32_t g1, g2;
+  if (is_long_sig(sg)) {
+    hot_groups(long_group_hash(sg), g1, g2);
+  } else {
+    uint64_t k0, k1;
+    sig_key(sg, sd, k0, k1);
+    hot_groups(place_hash(k0, k1), g1, g2);
+  }
+  if (gocc[g2] < gocc[g1]) {
+    const uint32_t x = g1;
+    g1 = g2;
+    g2 = x;
+  }
+  uint32_t g = g1, o = atomicAdd(&gocc[g1], 1u);
+  if (o >= GS) {
+    g = g2;
+    o = atomicAdd(&gocc[g2], 1u);
+  }
+  if (o >= GS) return;
+  const uint32_t slot = slot_of(g, o);
+  isig[slot] = sg;
+  iside[slot] = sd;
+}
+
+// A map block's table image from the candidates (the block's prologue): the
+// HOT_K most frequent (threshold over every partition's candidates, ties while
+// room remains), placed tier by tier into the LDS image isig / iside (cleared
+// by the caller).  Each thread holds CAND_PER_THREAD candidates in registers:
+// two dependent global steps (counts, then the taken candidates' keys).
+// scratch: >= SEL_BINS + 20 words, gocc: NG words (LDS the main loop reuses).
+__device__ void build_image(const HotArgs& h, uint64_t* isig, uint64_t* iside, uint32_t* scratch, uint32_t* gocc) {
+  const int tid = threadIdx.x;
+  uint32_t* hist = scratch;
+  uint32_t* sc = scratch + SEL_BINS;  // 18 words + the tie counter
+  for (int i = tid; i < SEL_BINS; i += 1024) hist[i] = 0;
+  for (int g = tid; g < NG; g += 1024) gocc[g] = 0;
+  if (tid == 0) sc[18] = 0;
+  constexpr uint32_t TPP = HOT_PART_TOP / CAND_PER_THREAD;  // threads per partition row
+  const uint32_t part = tid / TPP, e0 = (tid % TPP) * CAND_PER_THREAD;
+  const size_t at0 = (size_t)part * HOT_PART_TOP + e0;
+  const uint32_t n = h.cand_n[part];
+  uint32_t c[CAND_PER_THREAD];
+#pragma unroll
+  for (uint32_t i = 0; i < CAND_PER_THREAD; ++i) c[i] = h.cand_cnt[at0 + i];
+#pragma unroll
+  for (uint32_t i = 0; i < CAND_PER_THREAD; ++i) c[i] = e0 + i < n ? c[i] : 0u;  // stale past the row's count
+  __syncthreads();  // scratch cleared
+#pragma unroll
+  for (uint32_t i = 0; i < CAND_PER_THREAD; ++i)
+    if (c[i]) atomicAdd(&hist[min(c[i], (uint32_t)SEL_BINS - 1)], 1u);
+  __syncthreads();
+  uint32_t t, cum;
+  count_threshold(hist, HOT_K, sc, t, cum);
+  const uint32_t ties = t > 1 ? HOT_K - min(cum, HOT_K) : 0u;
+  uint64_t sg[CAND_PER_THREAD], sd[CAND_PER_THREAD];
+#pragma unroll
+  for (uint32_t i = 0; i < CAND_PER_THREAD; ++i) {
+    bool take = c[i] != 0 && c[i] + 1 >= t;
+    if (take && c[i] < t) take = atomicAdd(&sc[18], 1u) < ties;
+    if (!take) c[i] = 0;
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < CAND_PER_THREAD; ++i) {
+    sg[i] = c[i] ? h.cand_sig[at0 + i] : 0ull;
+    sd[i] = c[i] ? h.cand_side[at0 + i] : 0ull;
+  }
   const uint32_t big = min(HOT_FIRST_MUL * t, (uint32_t)SEL_BINS - 1);
   const uint32_t mid = HOT_PLACE_PASSES == 3 ? min(HOT_MID_MUL * t, big) : big;
-  for (uint64_t s = blockIdx.x * 1024ull + threadIdx.x; s < h.cap; s += (uint64_t)gridDim.x * 1024) {
-    const uint32_t c = min(h.cnt[s], (uint32_t)SEL_BINS - 1);
-    const int tier = c >= big ? 0 : (c >= mid ? 1 : 2);
-    if (c == 0 || c + 1 < t || tier != (pass == HOT_PLACE_PASSES - 1 ? 2 : pass)) continue;
-    if (c < t && atomicAdd(&h.sel[SEL_BINS + 2], 1u) >= ties) continue;
-    const uint64_t sg = h.sig[s], sd = h.side[s];
-    const bool lng = is_long_sig(sg);
-    uint32_t g1, g2;
-    if (lng) {
-      hot_groups(long_group_hash(sg), g1, g2);
-    } else {
-      uint64_t k0, k1;
-      sig_key(sg, sd, k0, k1);
-      hot_groups(place_hash(k0, k1), g1, g2);
+  for (int pass = 0; pass < HOT_PLACE_PASSES; ++pass) {
+#pragma unroll
+    for (uint32_t i = 0; i < CAND_PER_THREAD; ++i) {
+      if (!c[i]) continue;
+      const uint32_t cc = min(c[i], (uint32_t)SEL_BINS - 1);
+      const int tier = cc >= big ? 0 : (cc >= mid ? 1 : 2);
+      if (tier != (pass == HOT_PLACE_PASSES - 1 ? 2 : pass)) continue;
+      place_hot(isig, iside, gocc, sg[i], sd[i]);
     }
-    if (__hip_atomic_load(&h.gocc[g2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-        __hip_atomic_load(&h.gocc[g1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-      const uint32_t x = g1;
-      g1 = g2;
-      g2 = x;
-    }
-    uint32_t g = g1, o = atomicAdd(&h.gocc[g1], 1u);
-    if (o >= GS) {
-      g = g2;
-      o = atomicAdd(&h.gocc[g2], 1u);
-    }
-    if (o >= GS) continue;
-    const uint32_t slot = slot_of(g, o);
-    h.img_sig[slot] = sg;
-    if (lng) {  // side = the length; the word's bytes (zero-padded) go to the slot's line
-      const uint32_t len = (uint32_t)(sd >> 32), at = (uint32_t)sd;
-      h.img_side[slot] = len;
-      uint64_t* line = reinterpret_cast<uint64_t*>(h.long_bytes + (size_t)slot * 64);
-      for (uint32_t c = 0; c < 64; c += 8) {
-        uint64_t x = 0;
-        for (uint32_t i = 0; i < 8 && c + i < len; ++i) x |= (uint64_t)h.text[(size_t)at + c + i] << (8 * i);
-        line[c / 8] = x;
-      }
-    } else {
-      h.img_side[slot] = sd;
-    }
+    __syncthreads();
   }
 }
 
@@ -501,12 +635,16 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
 #pragma unroll
   for (int j = 0; j < SPT; ++j) {
     const int s = tid + j * MAP_THREADS;
-    L.sig[s] = h.img_sig[s];
-    L.side[s] = h.img_side[s];
+    L.sig[s] = 0;
+    L.side[s] = 0;
     L.cnt[s] = 0;
     L.off[s] = 0xFFFFFFFFu;
   }
   for (uint32_t b = tid; b < MAX_REC_BUCKETS; b += MAP_THREADS) L.bcur[b] = 0;
+  // the table image, built in this block's LDS (the unit buffers and token
+  // lists are its scratch until the first unit)
+  static_assert(sizeof(L.buf) >= 4 * (SEL_BINS + 20) && sizeof(L.list) >= 4 * NG, "image scratch");
+  build_image(h, L.sig, L.side, reinterpret_cast<uint32_t*>(&L.buf[0][0]), reinterpret_cast<uint32_t*>(&L.list[0][0]));
   uint64_t u_begin, u_end;
   unit_range(a.chunk_len, gridDim.x, blockIdx.x, u_begin, u_end);
   if (tid == 0) {
@@ -568,7 +706,8 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
           const int m = sig_match4(S[g1], S[g2], sg);
           if (m >= 0) {
             const int sl = (int)slot_of(m < GS ? g1 : g2, m & (GS - 1));
-            if (L.side[sl] == len && long_line_equal(buf, q, h.long_bytes + (size_t)sl * 64, len)) slot = sl;
+            const uint64_t sd = L.side[sl];  // length | candidate index << 32
+            if ((uint32_t)sd == len && long_line_equal(buf, q, h.long_bytes + (sd >> 32) * 64, len)) slot = sl;
           }
         }
         if (slot >= 0) {
@@ -825,7 +964,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     if (!c) continue;
     uint64_t k0, k1;
     const uint64_t sg = L.sig[s];
-    if (is_long_sig(sg)) key_long_line(h.long_bytes + (size_t)s * 64, (uint32_t)L.side[s], a.k1_mask, k0, k1);
+    if (is_long_sig(sg)) key_long_line(h.long_bytes + (L.side[s] >> 32) * 64, (uint32_t)L.side[s], a.k1_mask, k0, k1);
     else sig_key(sg, L.side[s], k0, k1);
     emit_record(L.bcur, a, rout, place_hash(k0, k1) & bmask, k0, k1, c, L.off[s]);
   }
@@ -878,10 +1017,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
 void launch_map(const MapArgs& a, const HotArgs& h, uint32_t map_blocks, hipStream_t s, bool sample) {
   if (sample) {
     hipLaunchKernelGGL(dev::wc_hot_sample, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
-    hipLaunchKernelGGL(dev::wc_hot_hist, dim3(HOT_SEL_BLOCKS), dim3(1024), 0, s, h);
-    hipLaunchKernelGGL(dev::wc_hot_threshold, dim3(1), dim3(1024), 0, s, h);
-    for (int p = 0; p < dev::HOT_PLACE_PASSES; ++p)
-      hipLaunchKernelGGL(dev::wc_hot_place, dim3(HOT_SEL_BLOCKS), dim3(1024), 0, s, h, p);
+    hipLaunchKernelGGL(dev::wc_hot_merge, dim3(HOT_PARTS), dim3(1024), 0, s, h);
   }
   if (a.stamps) hipLaunchKernelGGL(dev::wc_map<true>, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
   else hipLaunchKernelGGL(dev::wc_map<false>, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
