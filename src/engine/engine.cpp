@@ -115,6 +115,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   WC_HIP_CHECK(hipMalloc(&d_bucket_en, maxb));
   WC_HIP_CHECK(hipMalloc(&d_arena, std::max<uint64_t>(opt.arena_bytes, 16)));
   WC_HIP_CHECK(hipMalloc(&d_arena_cursor, sizeof(unsigned long long)));
+  WC_HIP_CHECK(hipMalloc(&d_fo_hist, FO_LOGBINS * sizeof(uint32_t)));
   for (int i = 0; i < 2; ++i) {
     WC_HIP_CHECK(hipEventCreateWithFlags(&ev_h2d[i], hipEventDisableTiming));
     WC_HIP_CHECK(hipEventCreateWithFlags(&ev_done[i], hipEventDisableTiming));
@@ -143,6 +144,7 @@ Engine::Impl::~Impl() {
   if (d_bucket_en) (void)hipFree(d_bucket_en);
   if (d_arena) (void)hipFree(d_arena);
   if (d_arena_cursor) (void)hipFree(d_arena_cursor);
+  if (d_fo_hist) (void)hipFree(d_fo_hist);
   if (d_stamps) {
     unsigned long long h[MAP_STAMP_N];
     if (hipMemcpy(h, d_stamps, sizeof h, hipMemcpyDeviceToHost) == hipSuccess && h[MS_TOTAL]) {
@@ -248,6 +250,13 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   pass_sampled = sample;
   ZeroList z{};
   z.add(d_ctr, sizeof(DevCounters));
+  z.add(d_fo_hist, FO_LOGBINS * sizeof(uint32_t));  // rebuilt by this pass's reduce over the whole table
+  {
+    uint32_t kb = 1;
+    while (kb < 64 && (std::max(max_end, base + len) >> kb) != 0) ++kb;
+    fo_hist_m = fo_mbits(kb);
+    fo_hist_ok = true;
+  }
   if (reset_pending) {
     z.add(table().occupancy, ((size_t)1 << table().log2_buckets) * 4);
     z.add(d_arena_cursor, sizeof(unsigned long long));
@@ -272,7 +281,7 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   }
   ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                 avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
-                d_ctr->flags, d_bucket_ovf, nullptr, d_red_stamps};
+                d_ctr->flags, d_bucket_ovf, nullptr, d_red_stamps, d_fo_hist, fo_hist_m};
   launch_reduce(ra, s);
   if (sync_debug) {
     const hipError_t e = hipStreamSynchronize(s);
@@ -473,7 +482,7 @@ bool Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
     WC_HIP_CHECK(hipMemsetAsync(d_ctr, 0, sizeof(DevCounters), s));
     ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                   avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
-                  d_ctr->flags, d_bucket_ovf, d_bucket_en, d_red_stamps};
+                  d_ctr->flags, d_bucket_ovf, d_bucket_en, d_red_stamps, d_fo_hist, fo_hist_m};
     launch_reduce(ra, s);
     PubList pc{};
     pc.add(h_ctr, d_ctr, sizeof(DevCounters));
@@ -573,7 +582,8 @@ bool Engine::Impl::finalize_local_speculative() {
   uint32_t* ovf = nullptr;
   if (sample) {
     ovf = first_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len}, hint, key_bits(),
-                      A.take_n<uint8_t>(first_order_ws_bytes(src, hint)), d_n, s);
+                      A.take_n<uint8_t>(first_order_ws_bytes(src, hint)), d_n, s, fo_hist_ok ? d_fo_hist : nullptr,
+                      fo_hist_m);
   } else {
     uint64_t* d_boff = A.take_n<uint64_t>(nb);
     uint64_t* keys = A.take_n<uint64_t>(cap + 1);
@@ -660,7 +670,8 @@ void Engine::Impl::finalize_local_sorted() {
     A.reset();
     take_cols();
     const uint32_t* ovf = first_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len}, n,
-                                      key_bits(), A.take_n<uint8_t>(first_order_ws_bytes(src, n)), nullptr, s);
+                                      key_bits(), A.take_n<uint8_t>(first_order_ws_bytes(src, n)), nullptr, s,
+                                      fo_hist_ok ? d_fo_hist : nullptr, fo_hist_m);
     if (h_fin.size() < 64) h_fin = PinnedBuffer(64);
     WC_HIP_CHECK(hipMemcpyAsync(h_fin.data() + 8, ovf, 4, hipMemcpyDeviceToHost, s));
     WC_HIP_CHECK(hipStreamSynchronize(s));  // the fallback path: one more wait is fine
@@ -810,6 +821,7 @@ void Engine::reset() {
   // (apply_reset does it first for anything else that reads the table)
   im.reset_pending = true;
   im.occ_valid = false;
+  im.fo_hist_ok = false;
   if (im.copy_used) WC_HIP_CHECK(hipStreamSynchronize(im.copy_s));  // a failed stream may have left copies
   im.copy_used = false;
   im.st = Stats{};

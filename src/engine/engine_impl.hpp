@@ -120,6 +120,9 @@ struct Engine::Impl {
   uint8_t* cols_arena = nullptr;   // arena the sref_* of cols point into
   uint64_t cols_arena_bytes = 0;
   uint64_t max_end = 0;  // max global byte offset seen (sort key width)
+  uint32_t* d_fo_hist = nullptr;  // [FO_LOGBINS] log-bin histogram of the table's first offsets (each reduce)
+  uint32_t fo_hist_m = 0;         // its resolution (fo_mbits of the pass's key width)
+  bool fo_hist_ok = false;        // it describes the current table (a pass ran since the reset)
   uint32_t key_bits() const {  // first offsets are < max_end < 2^key_bits
     uint32_t b = 1;
     while (b < 64 && (max_end >> b) != 0) ++b;

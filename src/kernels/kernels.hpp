@@ -165,6 +165,8 @@ struct ReduceArgs {
   uint32_t* bucket_overflow;      // [n_buckets] set when a slice overflowed
   const uint8_t* bucket_enable;   // nullptr = all
   unsigned long long* stamps;     // [RED_STAMP_N] diagnostic counters (WC_RED_STAMPS builds), nullable
+  uint32_t* fo_hist;              // [FO_LOGBINS] += every stored key's fo_logbin(first, fo_m) (nullable)
+  uint32_t fo_m;
 };
 // Reduce diagnostic counters (src/kernels/reduce.hip built with -DWC_RED_STAMPS=1).
 enum : int { RS_RECORDS = 0, RS_SLOW_LANES, RS_SLOW_WAVES, RS_PROBE_ITERS, RS_CAS_FAIL, RS_PENDING, RS_CLAIMS,
@@ -236,8 +238,11 @@ struct OrderDst {
 constexpr uint64_t FO_MAX_KEYS = 400 * 1000;  // bins average <= 800 rows (one wave sorts up to 2048)
 size_t first_order_ws_bytes(const OrderSrc& src, uint64_t bound);
 void first_order_stamps(unsigned long long* d);  // debug: phase clocks of the three kernels (nullptr: off)
+// key_hist (nullable): a histogram over fo_logbin(first, key_hist_m) of exactly
+// the source's keys (the reducer builds one for the table): used when
+// key_hist_m matches the resolution of key_bits, replacing the sample launch.
 uint32_t* first_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, uint32_t key_bits, void* ws,
-                      uint64_t* nout, hipStream_t s);
+                      uint64_t* nout, hipStream_t s, const uint32_t* key_hist = nullptr, uint32_t key_hist_m = 0);
 
 // out[i] = in[perm[i]] for the six key-table columns (one launch).
 void launch_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,

@@ -131,4 +131,21 @@ WC_HD uint32_t inline_bytes(uint64_t k0, uint64_t k1, uint8_t* out) {
   return len;
 }
 
+// First-occurrence order (sort.hip): log-scale value bin of a first offset k —
+// k itself below 2^M, else 2^M bins per octave (monotone) — over FO_LOGBINS
+// bins, and the most mantissa bits M that keep every key < 2^key_bits inside
+// them.  The reducer histograms its keys with the same function.
+constexpr uint32_t FO_LOGBINS = 16384;
+WC_HD uint32_t fo_logbin(uint64_t k, uint32_t M) {
+  if (k < (1ull << M)) return (uint32_t)k;
+  const uint32_t e = 63u - (uint32_t)__builtin_clzll(k);  // >= M
+  const uint32_t lb = ((e - M + 1u) << M) | (uint32_t)((k >> (e - M)) & ((1ull << M) - 1));
+  return lb < FO_LOGBINS - 1 ? lb : FO_LOGBINS - 1;
+}
+WC_HD uint32_t fo_mbits(uint32_t key_bits) {
+  uint32_t M = 12;
+  while (M > 4 && ((uint64_t)(key_bits > M ? key_bits - M + 1 : 1) << M) > (uint64_t)FO_LOGBINS) --M;
+  return M;
+}
+
 }  // namespace wc

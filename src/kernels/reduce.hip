@@ -662,6 +662,10 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   }
   settle_new_long(L, a, b);
   store_slice(L, a.tab, b);
+  if (a.fo_hist) {  // the finalize's first-occurrence bins come from this exact histogram
+    for (int s = tid; s < TAB_SLOTS; s += RED_THREADS)
+      if (slot_tag(L.grp, s) > TAG_PENDING) atomicAdd(&a.fo_hist[fo_logbin(L.first[s], a.fo_m)], 1u);
+  }
   if (tid == 0) {
     a.tab.occupancy[b] = L.occupied;
     atomicMax(&a.flags[FLAG_MAX_OCC], L.occupied);

@@ -210,7 +210,7 @@ __global__ void __launch_bounds__(OS_THREADS) wc_os_pass(const uint64_t* keys, c
 //                ones), the six output columns written from the entries.
 // A bin above its LDS capacity (a pathological value distribution) raises *ovf
 // and the caller redoes the order with the radix sort.
-constexpr int FO_BINS = 512, FO_ROWS = 4096, FO_SAMPLE = 4096, FO_LOGBINS = 16384;
+constexpr int FO_BINS = 512, FO_ROWS = 4096, FO_SAMPLE = 4096;
 
 // WC_FO_STAMPS (debug API): per kernel K, [16 K + p] = the max over blocks of
 // the 100 MHz wall time from the block's start to its phase p.
@@ -229,14 +229,6 @@ struct alignas(16) FoEntry {
   uint32_t slen, pad;
 };
 static_assert(sizeof(FoEntry) == 48, "48-byte entries");
-
-// Log-scale value bin: k itself below 2^M, else 2^M bins per octave (monotone).
-__device__ __forceinline__ uint32_t fo_logbin(uint64_t k, uint32_t M) {
-  if (k < (1ull << M)) return (uint32_t)k;
-  const uint32_t e = 63u - (uint32_t)__clzll((long long)k);  // >= M
-  const uint32_t lb = ((e - M + 1u) << M) | (uint32_t)((k >> (e - M)) & ((1ull << M) - 1));
-  return min(lb, (uint32_t)FO_LOGBINS - 1);
-}
 
 // Block-wide exclusive scan of `n` (a multiple of T, or < T) LDS counters in
 // place, T threads; returns the total.  `ws`: T / 64 words of scratch.
@@ -355,10 +347,13 @@ __global__ void __launch_bounds__(1024) wc_fo_split(OrderSrc src, uint32_t M, ui
 
 // Block k: source rows [4096 k, 4096 k + 4096) (table: bucket k's slots).
 // cntm / loffm are bin-major: [bin * nblk + k].
-__global__ void __launch_bounds__(1024) wc_fo_bin(OrderSrc src, uint32_t M, const uint16_t* map, uint32_t* cntm,
-                                                  uint32_t* loffm, FoEntry* seg) {
+// phist (nullable): the reducer's histogram of every key's log-bin — each
+// block then builds the log-bin -> bin map itself (no wc_fo_split launch).
+__global__ void __launch_bounds__(1024) wc_fo_bin(OrderSrc src, uint32_t M, const uint16_t* map, const uint32_t* phist,
+                                                  uint32_t* cntm, uint32_t* loffm, FoEntry* seg, uint32_t* ctl) {
   FoClock clk(1);
   __shared__ uint16_t lmap[FO_LOGBINS];
+  __shared__ alignas(16) uint32_t lh[FO_LOGBINS];
   __shared__ uint32_t lc[FO_BINS], ws[16];
   const uint32_t tid = threadIdx.x, k = blockIdx.x, nblk = gridDim.x;
   const uint64_t i0 = (uint64_t)k * FO_ROWS;
@@ -394,7 +389,17 @@ __global__ void __launch_bounds__(1024) wc_fo_bin(OrderSrc src, uint32_t M, cons
     }
     e[r].pad = 0;
   }
-  {
+  if (phist) {  // the map from the exact histogram (as wc_fo_split does from its sample)
+    const uint4* g = reinterpret_cast<const uint4*>(phist);
+    uint4* l = reinterpret_cast<uint4*>(lh);
+    for (int i = tid; i < FO_LOGBINS / 4; i += 1024) l[i] = g[i];
+    if (k == 0 && tid == 0) ctl[0] = 0;  // the overflow word (wc_fo_sort runs after every block)
+    __syncthreads();
+    const uint32_t V = lds_exclusive_scan<1024>(lh, FO_LOGBINS, ws);
+    const float inv = V ? (float)FO_BINS / (float)V : 0.0f;
+    for (int i = tid; i < FO_LOGBINS; i += 1024)
+      lmap[i] = (uint16_t)min((uint32_t)FO_BINS - 1, (uint32_t)((float)lh[i] * inv));
+  } else {
     const uint4* g = reinterpret_cast<const uint4*>(map);
     uint4* l = reinterpret_cast<uint4*>(lmap);
     for (int i = tid; i < FO_LOGBINS * 2 / 16; i += 1024) l[i] = g[i];
@@ -706,13 +711,6 @@ void radix_sort_pairs(uint64_t* keys, uint32_t* vals, uint64_t* tmp_keys, uint32
 static uint32_t fo_blocks(const OrderSrc& src, uint64_t bound) {
   return src.table ? (1u << src.t.log2_buckets) : (uint32_t)std::max<uint64_t>(1, (bound + dev::FO_ROWS - 1) / dev::FO_ROWS);
 }
-// Log-bin resolution: the most mantissa bits M with every key < 2^key_bits in FO_LOGBINS bins.
-static uint32_t fo_mbits(uint32_t key_bits) {
-  uint32_t M = 12;
-  while (M > 4 && ((uint64_t)(key_bits > M ? key_bits - M + 1 : 1) << M) > (uint64_t)dev::FO_LOGBINS) --M;
-  return M;
-}
-
 void first_order_stamps(unsigned long long* d) {
   WC_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(dev::fo_stamps), &d, sizeof d));
 }
@@ -723,7 +721,7 @@ size_t first_order_ws_bytes(const OrderSrc& src, uint64_t bound) {
 }
 
 uint32_t* first_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, uint32_t key_bits, void* ws,
-                      uint64_t* nout, hipStream_t s) {
+                      uint64_t* nout, hipStream_t s, const uint32_t* key_hist, uint32_t key_hist_m) {
   WC_CHECK(bound <= FO_MAX_KEYS, "first_order: key bound above FO_MAX_KEYS (use the radix sort)");
   const uint32_t nblk = fo_blocks(src, bound), M = fo_mbits(key_bits);
   uint8_t* p = static_cast<uint8_t*>(ws);
@@ -733,8 +731,9 @@ uint32_t* first_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, 
   uint32_t* loffm = cntm + (size_t)dev::FO_BINS * nblk;
   const size_t mat = 2 * (size_t)dev::FO_BINS * nblk * 4;
   dev::FoEntry* seg = reinterpret_cast<dev::FoEntry*>(p + 64 * 1024 + (mat + 255) / 256 * 256);
-  hipLaunchKernelGGL(dev::wc_fo_split, dim3(1), dim3(1024), 0, s, src, M, map, ctl);
-  hipLaunchKernelGGL(dev::wc_fo_bin, dim3(nblk), dim3(1024), 0, s, src, M, map, cntm, loffm, seg);
+  const uint32_t* phist = key_hist && key_hist_m == M ? key_hist : nullptr;
+  if (!phist) hipLaunchKernelGGL(dev::wc_fo_split, dim3(1), dim3(1024), 0, s, src, M, map, ctl);
+  hipLaunchKernelGGL(dev::wc_fo_bin, dim3(nblk), dim3(1024), 0, s, src, M, map, phist, cntm, loffm, seg, ctl);
   uint32_t cap = dev::FO_BLOCK_CAP;
   if (const char* e = std::getenv("WC_FO_CAP")) cap = std::min<uint32_t>(cap, (uint32_t)std::atoi(e));  // tests
   hipLaunchKernelGGL(dev::wc_fo_sort, dim3(dev::FO_BINS / dev::FO_SORT_WAVES), dim3(64 * dev::FO_SORT_WAVES), 0, s,

@@ -50,6 +50,8 @@ def test_overflow_falls_back_to_radix(monkeypatch):
     with ops.Engine(device=0) as e:
         assert_same(_resident(e, n, 8, 400_000), want)
         assert e.stats()["order_path"] == 3
+    # bins built from the reducer's exact key histogram are balanced: a smaller cap forces the overflow
+    monkeypatch.setenv("WC_FO_CAP", "128")
     text = ops.synth_host(4 << 20, seed=9, vocab=300_000, zipf_s=0.3)
     with ops.Engine(device=0, chunk_bytes=1 << 20) as e:  # streamed chunks: the non-speculative finalize
         e.count_bytes(text)
