@@ -51,8 +51,11 @@ struct Stats {
 struct Options {
   int device = 0;
   uint64_t chunk_bytes = 1ull << 30;   // device chunk (<= 4 GiB: records carry u32 offsets)
-  uint32_t log2_rec_buckets = 8;       // shuffle partitions
-  uint32_t log2_tab_buckets = 8;       // initial running-table buckets (x4096 slots)
+  // 64 buckets to start: the map appends each record to its bucket's run, and
+  // fewer runs keep their line tails in L2 (256 -> 64 buckets: wc_map -18 % at
+  // 100k words); the reduce then runs several blocks per bucket (split reduce).
+  uint32_t log2_rec_buckets = 6;       // shuffle partitions
+  uint32_t log2_tab_buckets = 6;       // initial running-table buckets (x4096 slots)
   uint32_t max_log2_tab_buckets = 16;
   uint64_t min_records = 1ull << 21;   // floor of shuffle record capacity per chunk
   double records_per_byte = 0.25;      // shuffle record capacity per chunk byte

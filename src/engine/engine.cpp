@@ -58,7 +58,8 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   WC_HIP_CHECK(hipSetDevice(dev));
   WC_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   WC_HIP_CHECK(hipStreamCreateWithFlags(&copy_s, hipStreamNonBlocking));
-  map_blocks = opt.map_blocks ? opt.map_blocks : MAP_BLOCKS_PER_CU * (uint32_t)device_cu_count(dev);
+  n_cu = (uint32_t)device_cu_count(dev);
+  map_blocks = opt.map_blocks ? opt.map_blocks : MAP_BLOCKS_PER_CU * n_cu;
   map_blocks = std::min<uint32_t>(map_blocks, RED_MAX_RUNS);
   if (const char* e = std::getenv("WC_SYNC_DEBUG")) sync_debug = std::atoi(e) != 0;
   if (const char* e = std::getenv("WC_NO_SPECULATE")) speculate = std::atoi(e) == 0;
@@ -76,6 +77,26 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
     WC_HIP_CHECK(hipMemset(d_blk, 0, (size_t)map_blocks * 4 * 8));
   }
 
+  if (const char* e = std::getenv("WC_REC_SHIFT")) rec_shift = (uint32_t)std::atoi(e);  // sweeps only
+  if (const char* e = std::getenv("WC_RED_Q")) red_q_force = (uint32_t)std::atoi(e);    // sweeps only
+  {  // split-reduce partial tables: one per reduce block when buckets < CUs
+    part_blocks = std::max<uint32_t>(n_cu, 256);
+    const size_t rows = (size_t)part_blocks * TAB_SLOTS;
+    part_mem.reserve(rows * (5 * 8 + 4) + part_blocks * 4 + rows * 12 + 16 * 256);
+    part.k0 = part_mem.take_n<uint64_t>(rows);
+    part.k1 = part_mem.take_n<uint64_t>(rows);
+    part.cnt = part_mem.take_n<uint64_t>(rows);
+    part.first = part_mem.take_n<uint64_t>(rows);
+    part.soff = part_mem.take_n<uint64_t>(rows);
+    part.slen = part_mem.take_n<uint32_t>(rows);
+    part.n = part_mem.take_n<uint32_t>(part_blocks);
+    part.qsoff = part_mem.take_n<uint64_t>(rows);
+    part.qslen = part_mem.take_n<uint32_t>(rows);
+  }
+  if (const char* e = std::getenv("WC_LOG2_BUCKETS")) {  // sweeps only: shuffle + table bucket count
+    opt.log2_rec_buckets = (uint32_t)std::atoi(e);
+    opt.log2_tab_buckets = opt.log2_rec_buckets;
+  }
   opt.log2_rec_buckets = std::min<uint32_t>(opt.log2_rec_buckets, MAX_REC_BUCKETS_LOG2);
   opt.max_log2_tab_buckets = std::min<uint32_t>(std::max<uint32_t>(opt.max_log2_tab_buckets, 1), 20);
   opt.log2_tab_buckets = std::max(opt.log2_tab_buckets, opt.log2_rec_buckets);
@@ -281,7 +302,7 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   }
   ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                 avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
-                d_ctr->flags, d_bucket_ovf, nullptr, d_red_stamps, d_fo_hist, fo_hist_m};
+                d_ctr->flags, d_bucket_ovf, nullptr, d_red_stamps, d_fo_hist, fo_hist_m, red_q(), part};
   launch_reduce(ra, s);
   if (sync_debug) {
     const hipError_t e = hipStreamSynchronize(s);
@@ -482,7 +503,7 @@ bool Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
     WC_HIP_CHECK(hipMemsetAsync(d_ctr, 0, sizeof(DevCounters), s));
     ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                   avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
-                  d_ctr->flags, d_bucket_ovf, d_bucket_en, d_red_stamps, d_fo_hist, fo_hist_m};
+                  d_ctr->flags, d_bucket_ovf, d_bucket_en, d_red_stamps, d_fo_hist, fo_hist_m, red_q(), part};
     launch_reduce(ra, s);
     PubList pc{};
     pc.add(h_ctr, d_ctr, sizeof(DevCounters));

@@ -182,8 +182,24 @@ struct Engine::Impl {
   uint32_t blocks_for(uint64_t len) const;
   // Shuffle partitions track the running table (one reduce block reads only
   // its own partition) up to MAX_REC_BUCKETS.
+  uint32_t rec_shift = 0;  // WC_REC_SHIFT (sweeps only): shuffle partitions = table buckets >> shift
+  uint32_t n_cu = 0;         // compute units: reduce blocks per pass
+  uint32_t red_q_force = 0;  // WC_RED_Q (sweeps only): reduce blocks per bucket
+  uint32_t part_blocks = 0;  // split-reduce partial tables allocated
+  ReduceArgs::Parts part{};
+  DeviceArena part_mem;
+  // reduce blocks per table bucket: the split reduce fills the CUs when the
+  // table has fewer buckets than CUs
+  uint32_t red_q() {
+    const uint32_t B = 1u << table().log2_buckets;
+    uint32_t q = red_q_force ? red_q_force : std::max<uint32_t>(1, n_cu / B);
+    q = std::min<uint32_t>(q, RED_SPLIT_MAX_Q);
+    while (q > 1 && (uint64_t)q * B > part_blocks) --q;
+    return q;
+  }
   uint32_t rec_buckets_log2() {
-    return std::min<uint32_t>(std::max(opt.log2_rec_buckets, table().log2_buckets), MAX_REC_BUCKETS_LOG2);
+    const uint32_t tb = table().log2_buckets;
+    return std::min<uint32_t>(std::max(opt.log2_rec_buckets, tb) - std::min(rec_shift, tb), MAX_REC_BUCKETS_LOG2);
   }
   void split_table();
 

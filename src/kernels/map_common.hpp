@@ -200,6 +200,23 @@ __device__ __forceinline__ void emit_two(uint32_t* bcur, const MapArgs& a, const
                                          uint64_t x0, uint64_t x1, uint32_t o1, uint32_t n1, bool d2, uint32_t b2,
                                          uint64_t y0, uint64_t y1, uint32_t o2, uint32_t n2) {
   const bool s1 = rec12_inline(x0, n1), s2 = rec12_inline(y0, n2);
+#if WC_EMIT_ABLATE == 4
+  {  // profiling only: the same number of 12-byte stores, lane-contiguous (coalesced); positions meaningless
+    const uint64_t m1 = __ballot(d1), m2 = __ballot(d2);
+    uint32_t base = 0;
+    if (__lane_id() == 0) base = atomicAdd(&bcur[0], (uint32_t)(__popcll(m1) + __popcll(m2)));
+    base = __builtin_amdgcn_readfirstlane(base);
+    const uint32_t r1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+    const uint32_t r2 = (uint32_t)__popcll(m1) +
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(m2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m2, 0u));
+    Rec12* w = o.b12;
+    if (d1) w[(base + r1) & 0xFFFFFu] = Rec12{(uint32_t)x0, (uint32_t)(x0 >> 32), o1};
+    if (d2) w[(base + r2) & 0xFFFFFu] = Rec12{(uint32_t)y0, (uint32_t)(y0 >> 32), o2};
+    (void)s1;
+    (void)s2;
+    return;
+  }
+#endif
   uint32_t p1 = 0, p2 = 0;
   if (WC_EMIT_ABLATE & 2) {
     p1 = (__lane_id() & 7) * 0x10001u;
@@ -264,12 +281,23 @@ __device__ __forceinline__ uint64_t key_long_scan(const uint8_t* buf, uint32_t b
   return len;
 }
 
+#ifndef WC_TEXT_NT
+#define WC_TEXT_NT 0  // non-temporal text loads (A/B)
+#endif
 // 32 text bytes at global offset g as two 16-B vectors (' ' past avail).
 __device__ __forceinline__ void load32(const MapArgs& a, uint64_t g, uint4& v0, uint4& v1) {
   if (g + MAP_BPL <= a.avail_len) {
     const uint4* src = reinterpret_cast<const uint4*>(a.text + g);
-    v0 = src[0];
-    v1 = src[1];
+    if (WC_TEXT_NT) {
+      typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+      const u4* s4 = reinterpret_cast<const u4*>(src);
+      const u4 x = __builtin_nontemporal_load(s4), y = __builtin_nontemporal_load(s4 + 1);
+      v0 = make_uint4(x.x, x.y, x.z, x.w);
+      v1 = make_uint4(y.x, y.y, y.z, y.w);
+    } else {
+      v0 = src[0];
+      v1 = src[1];
+    }
   } else {
     uint32_t w[8];
     for (int k = 0; k < 8; ++k) {

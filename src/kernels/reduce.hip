@@ -27,6 +27,7 @@
 #include "kernels.hpp"
 
 #include "lds_table.hpp"
+#include "common/hip_util.hpp"
 
 // Diagnostic build (-DWC_RED_STAMPS=1, tools/variants.sh; run with WC_MAP_STAMPS=1):
 // per-block LDS counters of records, slow-path lanes / waves, claim-loop
@@ -71,9 +72,9 @@ static_assert(sizeof(RedLds) <= 160 * 1024, "one reduce block per CU");
 
 // A bucket with occupancy 0 has UNDEFINED slice contents (Engine::reset zeroes
 // only the occupancy): it starts empty without reading the slice.
-__device__ __forceinline__ void load_slice(RedLds& L, const TableView& t, uint32_t b) {
+__device__ __forceinline__ void load_slice(RedLds& L, const TableView& t, uint32_t b, bool empty = false) {
   const size_t base = (size_t)b * TAB_SLOTS;
-  if (t.occupancy[b] == 0) {
+  if (empty || t.occupancy[b] == 0) {
     for (int s = threadIdx.x; s < TAB_SLOTS; s += blockDim.x) {
       SlotGroup& G = L.grp[s >> 2];
       G.k0[s & 3] = 0;
@@ -472,15 +473,16 @@ __device__ __forceinline__ void merge_batch(RedLds& L, const ReduceArgs& a, uint
 // index adjustment ADJ = first record index of run j - P; a record at stream
 // position t of run j sits at t + ADJ_j.
 template <bool R12, int U, class RecT>
-__device__ __forceinline__ void merge_stream(RedLds& L, const ReduceArgs& a, uint32_t b, const RecT* recs, uint32_t wave,
-                                             uint32_t nwaves, uint32_t nrb, uint32_t rb, uint32_t sub, uint32_t shift,
+__device__ __forceinline__ void merge_stream(RedLds& L, const ReduceArgs& a, uint32_t b, const RecT* recs, uint32_t p0,
+                                             uint32_t pstride, uint32_t nrb, uint32_t rb, uint32_t sub, uint32_t shift,
                                              uint32_t& claims) {
   constexpr uint32_t B = U * 64;
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t nj = wave < a.map_blocks ? (a.map_blocks - wave + nwaves - 1) / nwaves : 0u;  // <= 64 (RED_MAX_RUNS)
+  // runs p0, p0 + pstride, ... (pstride >= 16: <= 64 runs, RED_MAX_RUNS)
+  const uint32_t nj = p0 < a.map_blocks ? (a.map_blocks - p0 + pstride - 1) / pstride : 0u;
   uint32_t c = 0;
   if (lane < nj) {
-    const uint32_t packed = L.runcnt[wave + lane * nwaves];
+    const uint32_t packed = L.runcnt[p0 + lane * pstride];
     c = min(R12 ? (packed & 0xFFFFu) : (packed >> 16), sub);
   }
   uint32_t incl = c;
@@ -491,7 +493,7 @@ __device__ __forceinline__ void merge_stream(RedLds& L, const ReduceArgs& a, uin
   const uint32_t N = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   if (N == 0) return;
   const uint32_t P = incl - c;
-  const uint32_t C0 = (wave * nrb + rb) * sub, D = nwaves * nrb * sub;  // < record capacity < 2^32
+  const uint32_t C0 = (p0 * nrb + rb) * sub, D = pstride * nrb * sub;  // < record capacity < 2^32
   const uint32_t ADJ = C0 + lane * D - P;                               // modular: t + ADJ is exact
   uint32_t jlo = 0;  // run holding the current batch start (wave-uniform)
   auto locate = [&](uint32_t T0, uint32_t (&idx)[U], bool (&valid)[U]) {
@@ -544,9 +546,8 @@ __device__ __forceinline__ void merge_stream(RedLds& L, const ReduceArgs& a, uin
 // wave's 24-byte runs.  One record per lane per step, few live registers
 // around the out-of-line merge_long, whose byte comparison reads global memory
 // anyway.
-__device__ __forceinline__ void long_queue(RedLds& L, const ReduceArgs& a, uint32_t b, uint32_t n, uint32_t& claims) {
-  const size_t sbase = (size_t)b * TAB_SLOTS;
-  const LongCtx c{a.text, a.avail_len, a.arena.bytes, a.tab.sref_off + sbase, a.tab.sref_len + sbase};
+__device__ __forceinline__ void long_queue(RedLds& L, const ReduceArgs& a, const LongCtx& c, uint32_t n,
+                                           uint32_t& claims) {
   for (uint32_t i = threadIdx.x; i < n; i += RED_THREADS) {
     const Rec r = a.rec.recs[L.longq[i]];
     const uint32_t off = (uint32_t)r.co;
@@ -554,16 +555,15 @@ __device__ __forceinline__ void long_queue(RedLds& L, const ReduceArgs& a, uint3
   }
 }
 
-__device__ __forceinline__ void long_stream(RedLds& L, const ReduceArgs& a, uint32_t b, uint32_t wave, uint32_t nwaves,
-                                            uint32_t nrb, uint32_t rb, uint32_t sub, uint32_t shift, uint32_t& claims) {
+__device__ __forceinline__ void long_stream(RedLds& L, const ReduceArgs& a, const LongCtx& c, uint32_t b, uint32_t wave,
+                                            uint32_t p0, uint32_t pstride, uint32_t nrb, uint32_t rb, uint32_t sub,
+                                            uint32_t shift, uint32_t& claims) {
   // the queue is unused on this path: each wave compacts its LONG records'
   // indices into its 128-entry share of it and merges them 64 at a time (full
   // lanes: a wave's 24-byte runs mix LONG with medium words and hot flushes)
   static_assert(LONGQ >= 128 * (RED_THREADS / 64), "long_stream: 128 queue entries per wave");
   const uint32_t lane = threadIdx.x & 63;
   uint32_t* wl = L.longq + wave * 128;
-  const size_t sbase = (size_t)b * TAB_SLOTS;
-  const LongCtx c{a.text, a.avail_len, a.arena.bytes, a.tab.sref_off + sbase, a.tab.sref_len + sbase};
   auto wsync = [] {  // this wave's LDS writes visible to its other lanes
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -581,7 +581,7 @@ __device__ __forceinline__ void long_stream(RedLds& L, const ReduceArgs& a, uint
     if (WC_RED_STAMPS && lane == 0) atomicAdd(&L.st[RS_T_SLOW], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
   };
   uint32_t cnt = 0;  // wave-uniform
-  for (uint32_t p = wave; p < a.map_blocks; p += nwaves) {
+  for (uint32_t p = p0; p < a.map_blocks; p += pstride) {
     const uint32_t n = min(L.runcnt[p] >> 16, sub);
     const uint32_t base = ((uint32_t)p * nrb + rb) * sub;
     for (uint32_t i0 = 0; i0 < n; i0 += 64) {
@@ -606,19 +606,74 @@ __device__ __forceinline__ void long_stream(RedLds& L, const ReduceArgs& a, uint
   if (cnt) merge_first(cnt);
 }
 
+// The finalize's first-occurrence bins come from this exact histogram of the
+// stored keys' log-bins (sort.hip wc_fo_bin).
+__device__ __forceinline__ void add_fo_hist(const RedLds& L, const ReduceArgs& a) {
+  if (!a.fo_hist) return;
+  for (int s = threadIdx.x; s < TAB_SLOTS; s += RED_THREADS)
+    if (slot_tag(L.grp, s) > TAG_PENDING) atomicAdd(&a.fo_hist[fo_logbin(L.first[s], a.fo_m)], 1u);
+}
+
+// Split reduce: a quarter's occupied slots -> its part rows (slot order, a
+// block scan places them; LONG rows carry their arena / text reference).
+__device__ void write_partial(const RedLds& L, const ReduceArgs& a, const LongCtx& c, uint32_t pb) {
+  __shared__ uint32_t wsum[RED_THREADS / 64];
+  static_assert(TAB_SLOTS == 4 * RED_THREADS, "partial: 4 slots per thread");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  bool occ[4];
+  uint32_t n = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    occ[j] = slot_tag(L.grp, 4 * tid + j) > TAG_PENDING;
+    n += occ[j] ? 1u : 0u;
+  }
+  uint32_t incl = n;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  uint32_t before = 0, total = 0;
+  for (int w = 0; w < RED_THREADS / 64; ++w) {
+    before += w < wave ? wsum[w] : 0u;
+    total += wsum[w];
+  }
+  size_t o = (size_t)pb * TAB_SLOTS + before + incl - n;
+  const ReduceArgs::Parts& P = a.part;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (!occ[j]) continue;
+    const int s = 4 * tid + j;
+    const uint64_t k1 = slot_k1(L.grp, s);
+    P.k0[o] = slot_k0(L.grp, s);
+    P.k1[o] = k1;
+    P.cnt[o] = L.cnt[s];
+    P.first[o] = L.first[s];
+    if (key_is_hashed(k1)) {
+      P.soff[o] = c.sref_off[s];
+      P.slen[o] = c.sref_len[s];
+    }
+    ++o;
+  }
+  if (tid == 0) P.n[pb] = total;
+}
+
 __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   __shared__ RedLds L;
-  const uint32_t b = blockIdx.x;
+  // block b + B q: bucket b, quarter q (split reduce, a.nq > 1) of the map blocks' runs
+  const uint32_t b = blockIdx.x & ((1u << a.tab.log2_buckets) - 1u), q = blockIdx.x >> a.tab.log2_buckets;
   if (a.bucket_enable && !a.bucket_enable[b]) return;
   if (a.flags[FLAG_REGION_OVF]) return;  // shuffle output incomplete: host re-runs the chunk
   const int tid = threadIdx.x, wave = tid >> 6, nwaves = RED_THREADS / 64;
-  load_slice(L, a.tab, b);
+  const bool split = a.nq > 1;
+  load_slice(L, a.tab, b, q != 0);  // quarters q > 0 start empty
   {
     const uint32_t rb0 = b & ((1u << a.log2_rec_buckets) - 1u), nrb0 = 1u << a.log2_rec_buckets;
     for (uint32_t p = tid; p < a.map_blocks; p += RED_THREADS) L.runcnt[p] = a.rec.count[(size_t)p * nrb0 + rb0];
   }
   if (tid == 0) {
-    L.occupied = a.tab.occupancy[b];
+    L.occupied = q == 0 ? a.tab.occupancy[b] : 0u;
     L.overflow = 0;
     L.nlong = 0;
   }
@@ -633,8 +688,9 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   // one contiguous run per map block: sub-region (p, rb) of the record store;
   // the wave streams the 12-byte records of its runs, then the 24-byte ones
   uint32_t claims = 0;
-  merge_stream<true, RED_UNROLL>(L, a, b, a.rec.recs12, wave, nwaves, nrb, rb, (uint32_t)sub, shift, claims);
-  merge_stream<false, RED_UNROLL_24>(L, a, b, a.rec.recs, wave, nwaves, nrb, rb, (uint32_t)sub, shift, claims);
+  const uint32_t p0 = q + a.nq * wave, pstride = a.nq * nwaves;  // this wave's runs
+  merge_stream<true, RED_UNROLL>(L, a, b, a.rec.recs12, p0, pstride, nrb, rb, (uint32_t)sub, shift, claims);
+  merge_stream<false, RED_UNROLL_24>(L, a, b, a.rec.recs, p0, pstride, nrb, rb, (uint32_t)sub, shift, claims);
   __syncthreads();  // every LONG record is queued (or counted past the queue)
   if (WC_RED_STAMPS && (tid & 63) == 0)
     atomicAdd(&L.st[RS_T_STREAMS], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
@@ -642,9 +698,13 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
     L.st[RS_NLONG] = L.nlong;
     L.st[RS_LONG_STREAMED] = L.nlong > LONGQ ? 1 : 0;
   }
+  // LONG words' arena references: the slice's (q = 0) or the quarter's own scratch
+  const size_t sbase = (size_t)b * TAB_SLOTS, qbase = (size_t)blockIdx.x * TAB_SLOTS;
+  const LongCtx lc{a.text, a.avail_len, a.arena.bytes, q == 0 ? a.tab.sref_off + sbase : a.part.qsoff + qbase,
+                   q == 0 ? a.tab.sref_len + sbase : a.part.qslen + qbase};
   if (L.nlong) {
-    if (L.nlong <= LONGQ) long_queue(L, a, b, L.nlong, claims);
-    else long_stream(L, a, b, wave, nwaves, nrb, rb, (uint32_t)sub, shift, claims);
+    if (L.nlong <= LONGQ) long_queue(L, a, lc, L.nlong, claims);
+    else long_stream(L, a, lc, b, wave, p0, pstride, nrb, rb, (uint32_t)sub, shift, claims);
   }
   for (int o = 32; o > 0; o >>= 1) claims += __shfl_down(claims, o);
   if ((tid & 63) == 0 && claims) atomicAdd(&L.occupied, claims);
@@ -660,15 +720,16 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
     }
     return;
   }
-  settle_new_long(L, a, b);
-  store_slice(L, a.tab, b);
-  if (a.fo_hist) {  // the finalize's first-occurrence bins come from this exact histogram
-    for (int s = tid; s < TAB_SLOTS; s += RED_THREADS)
-      if (slot_tag(L.grp, s) > TAG_PENDING) atomicAdd(&a.fo_hist[fo_logbin(L.first[s], a.fo_m)], 1u);
-  }
-  if (tid == 0) {
-    a.tab.occupancy[b] = L.occupied;
-    atomicMax(&a.flags[FLAG_MAX_OCC], L.occupied);
+  if (split) {
+    write_partial(L, a, lc, blockIdx.x);  // wc_reduce_merge stores the bucket
+  } else {
+    settle_new_long(L, a, b);
+    store_slice(L, a.tab, b);
+    add_fo_hist(L, a);
+    if (tid == 0) {
+      a.tab.occupancy[b] = L.occupied;
+      atomicMax(&a.flags[FLAG_MAX_OCC], L.occupied);
+    }
   }
   if (WC_RED_STAMPS && a.stamps) {
     if ((tid & 63) == 0) atomicAdd(&L.st[RS_T_WAVE], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
@@ -680,6 +741,167 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
     }
     __syncthreads();
     if (tid < RED_STAMP_N) atomicAdd(&a.stamps[tid], L.st[tid]);
+  }
+}
+
+// Split reduce, second step: one block per bucket inserts the nq partial
+// tables' rows (quarter 0's include the running slice) into an empty LDS
+// table — inline keys by key, LONG words by key and then bytes (colliding
+// words keep separate slots) — then stores the slice as the one-block reduce
+// does.  A bucket whose quarter overflowed is left as it was (the host splits
+// the table and re-runs it).
+__device__ __forceinline__ bool refs_equal(const LongCtx& c, uint64_t so1, uint32_t l1, uint64_t so2, uint32_t l2) {
+  if (l1 == SREF_POISON || l2 == SREF_POISON) return true;  // bytes lost (arena overflow): the key decides
+  if (l1 != l2) return false;
+  const uint8_t* p1 = (so1 & SREF_TEXT) ? c.text + (so1 & ~SREF_TEXT) : c.arena + so1;
+  const uint8_t* p2 = (so2 & SREF_TEXT) ? c.text + (so2 & ~SREF_TEXT) : c.arena + so2;
+  uint32_t i = 0;
+  for (; i + 8 <= l1; i += 8) {
+    uint64_t u, v;
+    __builtin_memcpy(&u, p1 + i, 8);
+    __builtin_memcpy(&v, p2 + i, 8);
+    if (u != v) return false;
+  }
+  for (; i < l1; ++i)
+    if (p1[i] != p2[i]) return false;
+  return true;
+}
+
+__device__ __noinline__ void merge_long_row(RedLds& L, const LongCtx c, uint64_t k0, uint64_t k1, uint64_t cnt,
+                                            uint64_t first, uint64_t so, uint32_t sl) {
+  const uint32_t ph = place_hash(k0, k1), tag = make_tag(ph);
+  const uint32_t g1 = group_of(ph, TAB_GROUPS), g2 = group2_of(ph, TAB_GROUPS);
+  uint32_t g = g1;
+  int steps = 0;
+  for (;;) {
+    asm volatile("" ::: "memory");
+    SlotGroup& G = L.grp[g];
+    const uint32_t tv[4] = {G.tag[0], G.tag[1], G.tag[2], G.tag[3]};
+    bool pending = false;
+    int e = -1;
+    uint32_t mm = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (tv[i] == TAG_PENDING) pending = true;
+      else if (tv[i] == TAG_EMPTY) e = e < 0 ? i : e;
+      else if (tv[i] == tag && G.k1[i] == k1 && G.k0[i] == k0) mm |= 1u << i;
+    }
+    if (mm) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    while (mm) {
+      const int i = __ffs(mm) - 1;
+      mm &= mm - 1;
+      const int s = 4 * (int)g + i;
+      if (refs_equal(c, so, sl, c.sref_off[s], c.sref_len[s])) {
+        add_to_slot(L, s, cnt, first);
+        return;
+      }
+    }
+    if (pending) continue;
+    if (e >= 0) {
+      if (atomicCAS(&G.tag[e], TAG_EMPTY, TAG_PENDING) != TAG_EMPTY) continue;
+      const int s = 4 * (int)g + e;
+      G.k0[e] = k0;
+      G.k1[e] = k1;
+      c.sref_off[s] = so;
+      c.sref_len[s] = sl;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __hip_atomic_store(&G.tag[e], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      add_to_slot(L, s, cnt, first);
+      return;
+    }
+    if (++steps >= TAB_MAX_GROUP_PROBES) {
+      L.overflow = 1;
+      return;
+    }
+    g = probe_group(g1, g2, (uint32_t)steps, TAB_GROUPS);
+  }
+}
+
+__global__ void __launch_bounds__(RED_THREADS) wc_reduce_merge(ReduceArgs a) {
+  __shared__ RedLds L;
+  __shared__ uint32_t pn[RED_SPLIT_MAX_Q + 1];
+  const uint32_t b = blockIdx.x, B = 1u << a.tab.log2_buckets;
+  if (a.bucket_enable && !a.bucket_enable[b]) return;
+  if (a.flags[FLAG_REGION_OVF] || a.bucket_overflow[b]) return;
+  const int tid = threadIdx.x;
+  load_slice(L, a.tab, b, true);
+  if (tid == 0) {
+    L.overflow = 0;
+    L.occupied = 0;
+    uint32_t t = 0;
+    for (uint32_t q = 0; q < a.nq; ++q) {
+      pn[q] = t;
+      t += a.part.n[b + B * q];
+    }
+    pn[a.nq] = t;
+  }
+  __syncthreads();
+  // claims reference words in scratch (quarter 0's, which that quarter left
+  // unused): the slice's references change only if the merge stores it — an
+  // overflowed merge must leave the pre-pass slice intact
+  const size_t sbase = (size_t)b * TAB_SLOTS;
+  const LongCtx c{a.text, a.avail_len, a.arena.bytes, a.part.qsoff + sbase, a.part.qslen + sbase};
+  const ReduceArgs::Parts& P = a.part;
+  const uint32_t total = pn[a.nq];
+  constexpr int R = 4;  // rows per thread per round, loaded together
+  for (uint32_t r0 = 0; r0 < total; r0 += R * RED_THREADS) {
+    uint64_t k0[R], k1[R], cnt[R], first[R];
+    size_t at[R];
+    bool v[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const uint32_t i = r0 + j * RED_THREADS + tid;
+      v[j] = i < total;
+      uint32_t q = 0;
+      while (q + 1 < a.nq && pn[q + 1] <= i) ++q;
+      at[j] = (size_t)(b + B * q) * TAB_SLOTS + (i - pn[q]);
+      if (v[j]) {
+        k0[j] = P.k0[at[j]];
+        k1[j] = P.k1[at[j]];
+        cnt[j] = P.cnt[at[j]];
+        first[j] = P.first[at[j]];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      if (!v[j]) continue;
+      if (key_is_hashed(k1[j])) {
+        merge_long_row(L, c, k0[j], k1[j], cnt[j], first[j], P.soff[at[j]], P.slen[at[j]]);
+      } else {
+        bool claimed;
+        const int s = lds_find_or_claim(L.grp, TAB_GROUPS, place_hash(k0[j], k1[j]), k0[j], k1[j],
+                                        TAB_MAX_GROUP_PROBES, claimed, true);
+        if (s < 0) L.overflow = 1;
+        else add_to_slot(L, s, cnt[j], first[j]);
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t occ = 0;
+  for (int s = tid; s < TAB_SLOTS; s += RED_THREADS) occ += slot_tag(L.grp, s) > TAG_PENDING ? 1u : 0u;
+  for (int o = 32; o > 0; o >>= 1) occ += __shfl_down(occ, o);
+  if ((tid & 63) == 0 && occ) atomicAdd(&L.occupied, occ);
+  __syncthreads();
+  if (L.overflow || L.occupied > (uint32_t)TAB_MAX_OCC) {
+    if (tid == 0) {
+      a.bucket_overflow[b] = 1;
+      atomicOr(&a.flags[FLAG_TABLE_OVF], 1u);
+    }
+    return;
+  }
+  for (int s = tid; s < TAB_SLOTS; s += RED_THREADS) {
+    if (slot_tag(L.grp, s) > TAG_PENDING && key_is_hashed(slot_k1(L.grp, s))) {
+      a.tab.sref_off[sbase + s] = c.sref_off[s];
+      a.tab.sref_len[sbase + s] = c.sref_len[s];
+    }
+  }
+  __syncthreads();
+  settle_new_long(L, a, b);
+  store_slice(L, a.tab, b);
+  add_fo_hist(L, a);
+  if (tid == 0) {
+    a.tab.occupancy[b] = L.occupied;
+    atomicMax(&a.flags[FLAG_MAX_OCC], L.occupied);
   }
 }
 
@@ -873,7 +1095,9 @@ void launch_bucket_offsets(const uint32_t* occupancy, uint32_t nb, uint64_t* buc
 }
 
 void launch_reduce(const ReduceArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(dev::wc_reduce_buckets, dim3(1u << a.tab.log2_buckets), dim3(RED_THREADS), 0, s, a);
+  WC_CHECK(a.nq >= 1 && a.nq <= RED_SPLIT_MAX_Q, "reduce: 1..RED_SPLIT_MAX_Q blocks per bucket");
+  hipLaunchKernelGGL(dev::wc_reduce_buckets, dim3((1u << a.tab.log2_buckets) * a.nq), dim3(RED_THREADS), 0, s, a);
+  if (a.nq > 1) hipLaunchKernelGGL(dev::wc_reduce_merge, dim3(1u << a.tab.log2_buckets), dim3(RED_THREADS), 0, s, a);
 }
 
 void launch_table_split(const TableView& src, const TableView& dst, hipStream_t s) {

@@ -16,7 +16,7 @@ for r in $(seq $REPS); do
     if [ $rc -ne 0 ]; then echo "FAILED [$e] rc=$rc"; tail -3 gpurun_out/eb_$i.err; exit 1; fi
     python3 -c "
 import json; d=[json.loads(l) for l in open('gpurun_out/eb_$i.json') if l.startswith('{')][-1]
-print('$i', d['value'])" >> gpurun_out/eb_all.txt
+dm=d['stages']['device_ms']; print('$i', d['value'], dm['map'], dm['reduce'])" >> gpurun_out/eb_all.txt
   done
 done
 python3 - "$*" "${envs[@]}" <<'PY'
@@ -24,8 +24,10 @@ import collections, statistics, sys
 names = sys.argv[2:]
 runs = collections.defaultdict(list)
 for line in open("gpurun_out/eb_all.txt"):
-    i, v = line.split()
-    runs[int(i)].append(float(v))
+    i, v, m, r = line.split()
+    runs[int(i)].append((float(v), float(m), float(r)))
 for i, v in sorted(runs.items()):
-    print("%-28s median %7.1f GB/s  runs %s  %s" % (names[i], statistics.median(v), " ".join("%.1f" % x for x in v), sys.argv[1]))
+    print("%-28s median %7.1f GB/s  map %.4f reduce %.4f ms  runs %s  %s" % (
+        names[i], statistics.median(x[0] for x in v), statistics.median(x[1] for x in v),
+        statistics.median(x[2] for x in v), " ".join("%.1f" % x[0] for x in v), sys.argv[1]))
 PY
