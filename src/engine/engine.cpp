@@ -137,6 +137,8 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   WC_HIP_CHECK(hipMalloc(&d_arena, std::max<uint64_t>(opt.arena_bytes, 16)));
   WC_HIP_CHECK(hipMalloc(&d_arena_cursor, sizeof(unsigned long long)));
   WC_HIP_CHECK(hipMalloc(&d_fo_hist, FO_LOGBINS * sizeof(uint32_t)));
+  WC_HIP_CHECK(hipMalloc(&d_fo_hist_cols, FO_LOGBINS * sizeof(uint32_t)));
+  WC_HIP_CHECK(hipMemsetAsync(d_fo_hist_cols, 0, FO_LOGBINS * sizeof(uint32_t), s));
   for (int i = 0; i < 2; ++i) {
     WC_HIP_CHECK(hipEventCreateWithFlags(&ev_h2d[i], hipEventDisableTiming));
     WC_HIP_CHECK(hipEventCreateWithFlags(&ev_done[i], hipEventDisableTiming));
@@ -166,6 +168,7 @@ Engine::Impl::~Impl() {
   if (d_arena) (void)hipFree(d_arena);
   if (d_arena_cursor) (void)hipFree(d_arena_cursor);
   if (d_fo_hist) (void)hipFree(d_fo_hist);
+  if (d_fo_hist_cols) (void)hipFree(d_fo_hist_cols);
   if (d_stamps) {
     unsigned long long h[MAP_STAMP_N];
     if (hipMemcpy(h, d_stamps, sizeof h, hipMemcpyDeviceToHost) == hipSuccess && h[MS_TOTAL]) {
@@ -762,7 +765,7 @@ void Engine::Impl::sort_cols_by_first(bool radix) {
     A.reset();
     take_cols();
     fo_ovf = first_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len}, n, key_bits(),
-                         A.take_n<uint8_t>(first_order_ws_bytes(src, n)), nullptr, s);
+                         A.take_n<uint8_t>(first_order_ws_bytes(src, n)), nullptr, s, nullptr, 0, d_fo_hist_cols);
     cols_unsorted = cols;
     cols = o;
     st.order_path = 1;

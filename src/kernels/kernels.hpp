@@ -256,8 +256,12 @@ void first_order_stamps(unsigned long long* d);  // debug: phase clocks of the t
 // key_hist (nullable): a histogram over fo_logbin(first, key_hist_m) of exactly
 // the source's keys (the reducer builds one for the table): used when
 // key_hist_m matches the resolution of key_bits, replacing the sample launch.
+// Otherwise hist_ws (nullable: a zeroed FO_LOGBINS-word buffer, left zeroed)
+// receives the exact histogram from a many-block launch; without either, a
+// one-block sample (wc_fo_split) sets the bins.
 uint32_t* first_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, uint32_t key_bits, void* ws,
-                      uint64_t* nout, hipStream_t s, const uint32_t* key_hist = nullptr, uint32_t key_hist_m = 0);
+                      uint64_t* nout, hipStream_t s, const uint32_t* key_hist = nullptr, uint32_t key_hist_m = 0,
+                      uint32_t* hist_ws = nullptr);
 
 // out[i] = in[perm[i]] for the six key-table columns (one launch).
 void launch_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,

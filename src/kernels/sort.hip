@@ -347,6 +347,23 @@ __global__ void __launch_bounds__(1024) wc_fo_split(OrderSrc src, uint32_t M, ui
 
 // Block k: source rows [4096 k, 4096 k + 4096) (table: bucket k's slots).
 // cntm / loffm are bin-major: [bin * nblk + k].
+// Exact log-bin histogram of a column source's keys (the merged table): LDS
+// counts per block, one global add per nonzero bin; hist zeroed by the caller
+// (wc_fo_sort zeroes it again after its use).  Replaces the one-block sample.
+constexpr int FO_HIST_ROWS = 4096;  // rows per block
+__global__ void __launch_bounds__(1024) wc_fo_hist(OrderSrc src, uint32_t M, uint32_t* hist) {
+  __shared__ uint32_t lh[FO_LOGBINS];
+  const uint32_t tid = threadIdx.x;
+  for (int i = tid; i < FO_LOGBINS; i += 1024) lh[i] = 0;
+  __syncthreads();
+  const uint64_t n = src.dn ? *src.dn : src.n;
+  for (uint64_t i = (uint64_t)blockIdx.x * FO_HIST_ROWS + tid; i < n; i += (uint64_t)gridDim.x * FO_HIST_ROWS)
+    for (uint32_t r = 0; r < FO_HIST_ROWS && i + r < n; r += 1024) atomicAdd(&lh[fo_logbin(src.first[i + r], M)], 1u);
+  __syncthreads();
+  for (int i = tid; i < FO_LOGBINS; i += 1024)
+    if (lh[i]) atomicAdd(&hist[i], lh[i]);
+}
+
 // phist (nullable): the reducer's histogram of every key's log-bin — each
 // block then builds the log-bin -> bin map itself (no wc_fo_split launch).
 __global__ void __launch_bounds__(1024) wc_fo_bin(OrderSrc src, uint32_t M, const uint16_t* map, const uint32_t* phist,
@@ -489,9 +506,11 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
 __global__ void __launch_bounds__(64 * FO_SORT_WAVES) wc_fo_sort(OrderDst dst, const uint32_t* cntm,
                                                                  const uint32_t* loffm, const FoEntry* seg,
                                                                  uint32_t nblk, uint32_t cap, uint32_t* ctl,
-                                                                 uint64_t* nout) {
+                                                                 uint64_t* nout, uint32_t* zero_hist) {
   constexpr int T = 64 * FO_SORT_WAVES;
   FoClock clk(2);
+  if (zero_hist)  // wc_fo_bin is done with it: leave it zeroed for the next wc_fo_hist
+    for (uint32_t i = blockIdx.x * T + threadIdx.x; i < FO_LOGBINS; i += gridDim.x * T) zero_hist[i] = 0;
   __shared__ FoWaveLds W[FO_SORT_WAVES];
   __shared__ uint32_t big_m[FO_SORT_WAVES], big_off[FO_SORT_WAVES];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -721,7 +740,8 @@ size_t first_order_ws_bytes(const OrderSrc& src, uint64_t bound) {
 }
 
 uint32_t* first_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, uint32_t key_bits, void* ws,
-                      uint64_t* nout, hipStream_t s, const uint32_t* key_hist, uint32_t key_hist_m) {
+                      uint64_t* nout, hipStream_t s, const uint32_t* key_hist, uint32_t key_hist_m,
+                      uint32_t* hist_ws) {
   WC_CHECK(bound <= FO_MAX_KEYS, "first_order: key bound above FO_MAX_KEYS (use the radix sort)");
   const uint32_t nblk = fo_blocks(src, bound), M = fo_mbits(key_bits);
   uint8_t* p = static_cast<uint8_t*>(ws);
@@ -732,12 +752,18 @@ uint32_t* first_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, 
   const size_t mat = 2 * (size_t)dev::FO_BINS * nblk * 4;
   dev::FoEntry* seg = reinterpret_cast<dev::FoEntry*>(p + 64 * 1024 + (mat + 255) / 256 * 256);
   const uint32_t* phist = key_hist && key_hist_m == M ? key_hist : nullptr;
+  uint32_t* zero_hist = nullptr;
+  if (!phist && hist_ws) {  // the exact histogram of the keys, many blocks (not the one-block sample)
+    const uint32_t hb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(256, (bound + dev::FO_HIST_ROWS - 1) / dev::FO_HIST_ROWS));
+    hipLaunchKernelGGL(dev::wc_fo_hist, dim3(hb), dim3(1024), 0, s, src, M, hist_ws);
+    phist = zero_hist = hist_ws;
+  }
   if (!phist) hipLaunchKernelGGL(dev::wc_fo_split, dim3(1), dim3(1024), 0, s, src, M, map, ctl);
   hipLaunchKernelGGL(dev::wc_fo_bin, dim3(nblk), dim3(1024), 0, s, src, M, map, phist, cntm, loffm, seg, ctl);
   uint32_t cap = dev::FO_BLOCK_CAP;
   if (const char* e = std::getenv("WC_FO_CAP")) cap = std::min<uint32_t>(cap, (uint32_t)std::atoi(e));  // tests
   hipLaunchKernelGGL(dev::wc_fo_sort, dim3(dev::FO_BINS / dev::FO_SORT_WAVES), dim3(64 * dev::FO_SORT_WAVES), 0, s,
-                     dst, cntm, loffm, seg, nblk, cap, ctl, nout);
+                     dst, cntm, loffm, seg, nblk, cap, ctl, nout, zero_hist);
   return ctl;
 }
 
