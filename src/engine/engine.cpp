@@ -82,7 +82,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   {  // split-reduce partial tables: one per reduce block when buckets < CUs
     part_blocks = std::max<uint32_t>(n_cu, 256);
     const size_t rows = (size_t)part_blocks * TAB_SLOTS;
-    part_mem.reserve(rows * (5 * 8 + 4) + part_blocks * 4 + rows * 12 + 16 * 256);
+    part_mem.reserve(rows * (5 * 8 + 4) + part_blocks * 8 + rows * 12 + 16 * 256);
     part.k0 = part_mem.take_n<uint64_t>(rows);
     part.k1 = part_mem.take_n<uint64_t>(rows);
     part.cnt = part_mem.take_n<uint64_t>(rows);
@@ -92,6 +92,8 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
     part.n = part_mem.take_n<uint32_t>(part_blocks);
     part.qsoff = part_mem.take_n<uint64_t>(rows);
     part.qslen = part_mem.take_n<uint32_t>(rows);
+    part.done = part_mem.take_n<uint32_t>(part_blocks);
+    WC_HIP_CHECK(hipMemset(part.done, 0, part_blocks * sizeof(uint32_t)));
   }
   if (const char* e = std::getenv("WC_LOG2_BUCKETS")) {  // sweeps only: shuffle + table bucket count
     opt.log2_rec_buckets = (uint32_t)std::atoi(e);

@@ -170,8 +170,8 @@ struct ReduceArgs {
   // Split reduce (nq > 1: fewer table buckets than CUs).  Block b + B q (q < nq)
   // merges the runs of map blocks p = q mod nq into a partial table of bucket b
   // (q = 0 starting from the running slice, the others empty) and writes its
-  // occupied rows to part slot (b + B q); wc_reduce_merge then combines the nq
-  // partials of each bucket into the slice.
+  // occupied rows to part slot (b + B q); the last quarter of a bucket to finish
+  // merges the other partials into its own table and stores the slice.
   uint32_t nq;
   struct Parts {
     uint64_t *k0, *k1, *cnt, *first, *soff;  // [(b + B q) * TAB_SLOTS + i] rows
@@ -179,9 +179,10 @@ struct ReduceArgs {
     uint32_t* n;                              // [b + B q] rows written
     uint64_t* qsoff;                          // [(b + B q) * TAB_SLOTS + slot] arena references of quarters q > 0
     uint32_t* qslen;
+    uint32_t* done;                           // [b] quarters arrived (zeroed; the last resets it)
   } part;
 };
-// Table buckets below this many per CU run the split reduce (wc_reduce_merge).
+// Most reduce blocks per bucket (split reduce: fewer table buckets than CUs).
 constexpr uint32_t RED_SPLIT_MAX_Q = 16;
 // Reduce diagnostic counters (src/kernels/reduce.hip built with -DWC_RED_STAMPS=1).
 enum : int { RS_RECORDS = 0, RS_SLOW_LANES, RS_SLOW_WAVES, RS_PROBE_ITERS, RS_CAS_FAIL, RS_PENDING, RS_CLAIMS,
@@ -200,7 +201,7 @@ struct SynthVocab {
 // wc_hot_sample + wc_hot_merge + wc_map;
 // sample = false: wc_map alone, on the hot-table image an earlier pass of the job built.
 void launch_map(const MapArgs& a, const HotArgs& h, uint32_t map_blocks, hipStream_t s, bool sample = true);
-void launch_reduce(const ReduceArgs& a, hipStream_t s);  // + wc_reduce_merge when a.nq > 1
+void launch_reduce(const ReduceArgs& a, hipStream_t s);
 void launch_table_split(const TableView& src, const TableView& dst, hipStream_t s);
 void launch_table_clear(const TableView& t, hipStream_t s);
 // Writes occupied entries densely in bucket order; bucket_off[b] = exclusive

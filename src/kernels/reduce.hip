@@ -606,6 +606,172 @@ __device__ __forceinline__ void long_stream(RedLds& L, const ReduceArgs& a, cons
   if (cnt) merge_first(cnt);
 }
 
+// Split reduce, merge step: LONG rows are matched by key and then by bytes
+// (colliding words keep separate slots); the references of both sides point at
+// the chunk text (SREF_TEXT) or the key arena.
+__device__ __forceinline__ bool refs_equal(const LongCtx& c, uint64_t so1, uint32_t l1, uint64_t so2, uint32_t l2) {
+  if (l1 == SREF_POISON || l2 == SREF_POISON) return true;  // bytes lost (arena overflow): the key decides
+  if (l1 != l2) return false;
+  const uint8_t* p1 = (so1 & SREF_TEXT) ? c.text + (so1 & ~SREF_TEXT) : c.arena + so1;
+  const uint8_t* p2 = (so2 & SREF_TEXT) ? c.text + (so2 & ~SREF_TEXT) : c.arena + so2;
+  uint32_t i = 0;
+  for (; i + 8 <= l1; i += 8) {
+    uint64_t u, v;
+    __builtin_memcpy(&u, p1 + i, 8);
+    __builtin_memcpy(&v, p2 + i, 8);
+    if (u != v) return false;
+  }
+  for (; i < l1; ++i)
+    if (p1[i] != p2[i]) return false;
+  return true;
+}
+
+__device__ __noinline__ void merge_long_row(RedLds& L, const LongCtx c, uint64_t k0, uint64_t k1, uint64_t cnt,
+                                            uint64_t first, uint64_t so, uint32_t sl) {
+  const uint32_t ph = place_hash(k0, k1), tag = make_tag(ph);
+  const uint32_t g1 = group_of(ph, TAB_GROUPS), g2 = group2_of(ph, TAB_GROUPS);
+  uint32_t g = g1;
+  int steps = 0;
+  for (;;) {
+    asm volatile("" ::: "memory");
+    SlotGroup& G = L.grp[g];
+    const uint32_t tv[4] = {G.tag[0], G.tag[1], G.tag[2], G.tag[3]};
+    bool pending = false;
+    int e = -1;
+    uint32_t mm = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (tv[i] == TAG_PENDING) pending = true;
+      else if (tv[i] == TAG_EMPTY) e = e < 0 ? i : e;
+      else if (tv[i] == tag && G.k1[i] == k1 && G.k0[i] == k0) mm |= 1u << i;
+    }
+    if (mm) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    while (mm) {
+      const int i = __ffs(mm) - 1;
+      mm &= mm - 1;
+      const int s = 4 * (int)g + i;
+      if (refs_equal(c, so, sl, c.sref_off[s], c.sref_len[s])) {
+        add_to_slot(L, s, cnt, first);
+        return;
+      }
+    }
+    if (pending) continue;
+    if (e >= 0) {
+      if (atomicCAS(&G.tag[e], TAG_EMPTY, TAG_PENDING) != TAG_EMPTY) continue;
+      const int s = 4 * (int)g + e;
+      G.k0[e] = k0;
+      G.k1[e] = k1;
+      c.sref_off[s] = so;
+      c.sref_len[s] = sl;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __hip_atomic_store(&G.tag[e], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      add_to_slot(L, s, cnt, first);
+      return;
+    }
+    if (++steps >= TAB_MAX_GROUP_PROBES) {
+      L.overflow = 1;
+      return;
+    }
+    g = probe_group(g1, g2, (uint32_t)steps, TAB_GROUPS);
+  }
+}
+
+
+// Split reduce: this quarter's partial is published (or it overflowed); count
+// the bucket's arrivals — true for the last quarter, which then sees every
+// other quarter's partial (agent-scope release by each arrival, acquire by the
+// last; the counter is reset for the next launch).
+// One agent-scope acq_rel atomic per block (MI355X_MICROARCH.md: one lane per
+// storing workgroup, behind a workgroup barrier; the other waves load after a
+// barrier that lane joins) — a fence per wave wrote the XCD's L2 back 16 times
+// per block (reduce 214 -> 395 us).
+__device__ bool split_arrive_last(RedLds& L, const ReduceArgs& a, uint32_t b) {
+  __shared__ uint32_t last;
+  __syncthreads();  // every wave's partial rows are written
+  if (threadIdx.x == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(&a.part.done[b], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = old + 1 == a.nq ? 1u : 0u;
+    if (last) a.part.done[b] = 0;
+  }
+  __syncthreads();
+  if (!last) return false;
+  return a.bucket_overflow[b] == 0;  // a quarter overflowed: the host splits the table and re-runs the bucket
+}
+
+// The last quarter inserts the other quarters' partial rows (quarter 0's
+// include the running slice) into its own table — inline keys by key, LONG
+// words by key and bytes — and recounts the occupancy.  False on overflow.
+__device__ bool merge_partials(RedLds& L, const ReduceArgs& a, const LongCtx& c, uint32_t b, uint32_t qself) {
+  __shared__ uint32_t pn[RED_SPLIT_MAX_Q + 1];
+  __shared__ uint32_t pq[RED_SPLIT_MAX_Q];
+  const int tid = threadIdx.x;
+  const uint32_t B = 1u << a.tab.log2_buckets;
+  if (tid == 0) {
+    uint32_t t = 0, k = 0;
+    for (uint32_t q = 0; q < a.nq; ++q) {
+      if (q == qself) continue;
+      pn[k] = t;
+      pq[k++] = q;
+      t += a.part.n[b + B * q];
+    }
+    pn[k] = t;
+    pq[k] = 0;
+    L.occupied = k;  // scratch: the partials merged
+  }
+  __syncthreads();
+  const uint32_t np = L.occupied, total = pn[np];
+  const ReduceArgs::Parts& P = a.part;
+  constexpr int R = 4;  // rows per thread per round, loaded together
+  for (uint32_t r0 = 0; r0 < total; r0 += R * RED_THREADS) {
+    uint64_t k0[R], k1[R], cnt[R], first[R];
+    size_t at[R];
+    bool v[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const uint32_t i = r0 + j * RED_THREADS + tid;
+      v[j] = i < total;
+      uint32_t k = 0;
+      while (k + 1 < np && pn[k + 1] <= i) ++k;
+      at[j] = (size_t)(b + B * pq[k]) * TAB_SLOTS + (i - pn[k]);
+      if (v[j]) {
+        k0[j] = P.k0[at[j]];
+        k1[j] = P.k1[at[j]];
+        cnt[j] = P.cnt[at[j]];
+        first[j] = P.first[at[j]];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      if (!v[j]) continue;
+      if (key_is_hashed(k1[j])) {
+        merge_long_row(L, c, k0[j], k1[j], cnt[j], first[j], P.soff[at[j]], P.slen[at[j]]);
+      } else {
+        bool claimed;
+        const int s = lds_find_or_claim(L.grp, TAB_GROUPS, place_hash(k0[j], k1[j]), k0[j], k1[j],
+                                        TAB_MAX_GROUP_PROBES, claimed, true);
+        if (s < 0) L.overflow = 1;
+        else add_to_slot(L, s, cnt[j], first[j]);
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) L.occupied = 0;
+  __syncthreads();
+  uint32_t occ = 0;
+  for (int s = tid; s < TAB_SLOTS; s += RED_THREADS) occ += slot_tag(L.grp, s) > TAG_PENDING ? 1u : 0u;
+  for (int o = 32; o > 0; o >>= 1) occ += __shfl_down(occ, o);
+  if ((tid & 63) == 0 && occ) atomicAdd(&L.occupied, occ);
+  __syncthreads();
+  if (L.overflow || L.occupied > (uint32_t)TAB_MAX_OCC) {
+    if (tid == 0) {
+      a.bucket_overflow[b] = 1;
+      atomicOr(&a.flags[FLAG_TABLE_OVF], 1u);
+    }
+    return false;
+  }
+  return true;
+}
+
 // The finalize's first-occurrence bins come from this exact histogram of the
 // stored keys' log-bins (sort.hip wc_fo_bin).
 __device__ __forceinline__ void add_fo_hist(const RedLds& L, const ReduceArgs& a) {
@@ -713,16 +879,28 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   __syncthreads();
   if (tid == 0 && L.occupied > (uint32_t)TAB_MAX_OCC) L.overflow = 1;  // too full: split and re-run
   __syncthreads();
-  if (L.overflow) {
-    if (tid == 0) {
-      a.bucket_overflow[b] = 1;
-      atomicOr(&a.flags[FLAG_TABLE_OVF], 1u);
-    }
-    return;
+  if (L.overflow && tid == 0) {
+    a.bucket_overflow[b] = 1;
+    atomicOr(&a.flags[FLAG_TABLE_OVF], 1u);
   }
+  bool store = !L.overflow;
   if (split) {
-    write_partial(L, a, lc, blockIdx.x);  // wc_reduce_merge stores the bucket
-  } else {
+    // every quarter publishes its partial table; the last to arrive merges the
+    // others into its own LDS table and stores the bucket
+    if (!L.overflow) write_partial(L, a, lc, blockIdx.x);
+    store = split_arrive_last(L, a, b);
+    if (store) store = merge_partials(L, a, lc, b, q);
+    if (store && q != 0) {  // the merged table's LONG references: quarter scratch -> the slice
+      for (int s = tid; s < TAB_SLOTS; s += RED_THREADS) {
+        if (slot_tag(L.grp, s) > TAG_PENDING && key_is_hashed(slot_k1(L.grp, s))) {
+          a.tab.sref_off[sbase + s] = lc.sref_off[s];
+          a.tab.sref_len[sbase + s] = lc.sref_len[s];
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (store) {
     settle_new_long(L, a, b);
     store_slice(L, a.tab, b);
     add_fo_hist(L, a);
@@ -741,167 +919,6 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
     }
     __syncthreads();
     if (tid < RED_STAMP_N) atomicAdd(&a.stamps[tid], L.st[tid]);
-  }
-}
-
-// Split reduce, second step: one block per bucket inserts the nq partial
-// tables' rows (quarter 0's include the running slice) into an empty LDS
-// table — inline keys by key, LONG words by key and then bytes (colliding
-// words keep separate slots) — then stores the slice as the one-block reduce
-// does.  A bucket whose quarter overflowed is left as it was (the host splits
-// the table and re-runs it).
-__device__ __forceinline__ bool refs_equal(const LongCtx& c, uint64_t so1, uint32_t l1, uint64_t so2, uint32_t l2) {
-  if (l1 == SREF_POISON || l2 == SREF_POISON) return true;  // bytes lost (arena overflow): the key decides
-  if (l1 != l2) return false;
-  const uint8_t* p1 = (so1 & SREF_TEXT) ? c.text + (so1 & ~SREF_TEXT) : c.arena + so1;
-  const uint8_t* p2 = (so2 & SREF_TEXT) ? c.text + (so2 & ~SREF_TEXT) : c.arena + so2;
-  uint32_t i = 0;
-  for (; i + 8 <= l1; i += 8) {
-    uint64_t u, v;
-    __builtin_memcpy(&u, p1 + i, 8);
-    __builtin_memcpy(&v, p2 + i, 8);
-    if (u != v) return false;
-  }
-  for (; i < l1; ++i)
-    if (p1[i] != p2[i]) return false;
-  return true;
-}
-
-__device__ __noinline__ void merge_long_row(RedLds& L, const LongCtx c, uint64_t k0, uint64_t k1, uint64_t cnt,
-                                            uint64_t first, uint64_t so, uint32_t sl) {
-  const uint32_t ph = place_hash(k0, k1), tag = make_tag(ph);
-  const uint32_t g1 = group_of(ph, TAB_GROUPS), g2 = group2_of(ph, TAB_GROUPS);
-  uint32_t g = g1;
-  int steps = 0;
-  for (;;) {
-    asm volatile("" ::: "memory");
-    SlotGroup& G = L.grp[g];
-    const uint32_t tv[4] = {G.tag[0], G.tag[1], G.tag[2], G.tag[3]};
-    bool pending = false;
-    int e = -1;
-    uint32_t mm = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (tv[i] == TAG_PENDING) pending = true;
-      else if (tv[i] == TAG_EMPTY) e = e < 0 ? i : e;
-      else if (tv[i] == tag && G.k1[i] == k1 && G.k0[i] == k0) mm |= 1u << i;
-    }
-    if (mm) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    while (mm) {
-      const int i = __ffs(mm) - 1;
-      mm &= mm - 1;
-      const int s = 4 * (int)g + i;
-      if (refs_equal(c, so, sl, c.sref_off[s], c.sref_len[s])) {
-        add_to_slot(L, s, cnt, first);
-        return;
-      }
-    }
-    if (pending) continue;
-    if (e >= 0) {
-      if (atomicCAS(&G.tag[e], TAG_EMPTY, TAG_PENDING) != TAG_EMPTY) continue;
-      const int s = 4 * (int)g + e;
-      G.k0[e] = k0;
-      G.k1[e] = k1;
-      c.sref_off[s] = so;
-      c.sref_len[s] = sl;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __hip_atomic_store(&G.tag[e], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      add_to_slot(L, s, cnt, first);
-      return;
-    }
-    if (++steps >= TAB_MAX_GROUP_PROBES) {
-      L.overflow = 1;
-      return;
-    }
-    g = probe_group(g1, g2, (uint32_t)steps, TAB_GROUPS);
-  }
-}
-
-__global__ void __launch_bounds__(RED_THREADS) wc_reduce_merge(ReduceArgs a) {
-  __shared__ RedLds L;
-  __shared__ uint32_t pn[RED_SPLIT_MAX_Q + 1];
-  const uint32_t b = blockIdx.x, B = 1u << a.tab.log2_buckets;
-  if (a.bucket_enable && !a.bucket_enable[b]) return;
-  if (a.flags[FLAG_REGION_OVF] || a.bucket_overflow[b]) return;
-  const int tid = threadIdx.x;
-  load_slice(L, a.tab, b, true);
-  if (tid == 0) {
-    L.overflow = 0;
-    L.occupied = 0;
-    uint32_t t = 0;
-    for (uint32_t q = 0; q < a.nq; ++q) {
-      pn[q] = t;
-      t += a.part.n[b + B * q];
-    }
-    pn[a.nq] = t;
-  }
-  __syncthreads();
-  // claims reference words in scratch (quarter 0's, which that quarter left
-  // unused): the slice's references change only if the merge stores it — an
-  // overflowed merge must leave the pre-pass slice intact
-  const size_t sbase = (size_t)b * TAB_SLOTS;
-  const LongCtx c{a.text, a.avail_len, a.arena.bytes, a.part.qsoff + sbase, a.part.qslen + sbase};
-  const ReduceArgs::Parts& P = a.part;
-  const uint32_t total = pn[a.nq];
-  constexpr int R = 4;  // rows per thread per round, loaded together
-  for (uint32_t r0 = 0; r0 < total; r0 += R * RED_THREADS) {
-    uint64_t k0[R], k1[R], cnt[R], first[R];
-    size_t at[R];
-    bool v[R];
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      const uint32_t i = r0 + j * RED_THREADS + tid;
-      v[j] = i < total;
-      uint32_t q = 0;
-      while (q + 1 < a.nq && pn[q + 1] <= i) ++q;
-      at[j] = (size_t)(b + B * q) * TAB_SLOTS + (i - pn[q]);
-      if (v[j]) {
-        k0[j] = P.k0[at[j]];
-        k1[j] = P.k1[at[j]];
-        cnt[j] = P.cnt[at[j]];
-        first[j] = P.first[at[j]];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      if (!v[j]) continue;
-      if (key_is_hashed(k1[j])) {
-        merge_long_row(L, c, k0[j], k1[j], cnt[j], first[j], P.soff[at[j]], P.slen[at[j]]);
-      } else {
-        bool claimed;
-        const int s = lds_find_or_claim(L.grp, TAB_GROUPS, place_hash(k0[j], k1[j]), k0[j], k1[j],
-                                        TAB_MAX_GROUP_PROBES, claimed, true);
-        if (s < 0) L.overflow = 1;
-        else add_to_slot(L, s, cnt[j], first[j]);
-      }
-    }
-  }
-  __syncthreads();
-  uint32_t occ = 0;
-  for (int s = tid; s < TAB_SLOTS; s += RED_THREADS) occ += slot_tag(L.grp, s) > TAG_PENDING ? 1u : 0u;
-  for (int o = 32; o > 0; o >>= 1) occ += __shfl_down(occ, o);
-  if ((tid & 63) == 0 && occ) atomicAdd(&L.occupied, occ);
-  __syncthreads();
-  if (L.overflow || L.occupied > (uint32_t)TAB_MAX_OCC) {
-    if (tid == 0) {
-      a.bucket_overflow[b] = 1;
-      atomicOr(&a.flags[FLAG_TABLE_OVF], 1u);
-    }
-    return;
-  }
-  for (int s = tid; s < TAB_SLOTS; s += RED_THREADS) {
-    if (slot_tag(L.grp, s) > TAG_PENDING && key_is_hashed(slot_k1(L.grp, s))) {
-      a.tab.sref_off[sbase + s] = c.sref_off[s];
-      a.tab.sref_len[sbase + s] = c.sref_len[s];
-    }
-  }
-  __syncthreads();
-  settle_new_long(L, a, b);
-  store_slice(L, a.tab, b);
-  add_fo_hist(L, a);
-  if (tid == 0) {
-    a.tab.occupancy[b] = L.occupied;
-    atomicMax(&a.flags[FLAG_MAX_OCC], L.occupied);
   }
 }
 
@@ -1097,7 +1114,6 @@ void launch_bucket_offsets(const uint32_t* occupancy, uint32_t nb, uint64_t* buc
 void launch_reduce(const ReduceArgs& a, hipStream_t s) {
   WC_CHECK(a.nq >= 1 && a.nq <= RED_SPLIT_MAX_Q, "reduce: 1..RED_SPLIT_MAX_Q blocks per bucket");
   hipLaunchKernelGGL(dev::wc_reduce_buckets, dim3((1u << a.tab.log2_buckets) * a.nq), dim3(RED_THREADS), 0, s, a);
-  if (a.nq > 1) hipLaunchKernelGGL(dev::wc_reduce_merge, dim3(1u << a.tab.log2_buckets), dim3(RED_THREADS), 0, s, a);
 }
 
 void launch_table_split(const TableView& src, const TableView& dst, hipStream_t s) {
