@@ -210,7 +210,12 @@ __global__ void __launch_bounds__(OS_THREADS) wc_os_pass(const uint64_t* keys, c
 //                ones), the six output columns written from the entries.
 // A bin above its LDS capacity (a pathological value distribution) raises *ovf
 // and the caller redoes the order with the radix sort.
-constexpr int FO_BINS = 512, FO_ROWS = 4096, FO_SAMPLE = 4096;
+#ifndef WC_FO_ROWS
+#define WC_FO_ROWS 1024
+#endif
+constexpr int FO_BINS = 512, FO_ROWS = WC_FO_ROWS, FO_SAMPLE = 4096;
+constexpr int FO_RPT = FO_ROWS / 1024;  // wc_fo_bin rows per thread
+static_assert(FO_ROWS % 1024 == 0 && TAB_SLOTS % FO_ROWS == 0, "fo_bin: whole rows per thread, blocks inside a bucket");
 
 // WC_FO_STAMPS (debug API): per kernel K, [16 K + p] = the max over blocks of
 // the 100 MHz wall time from the block's start to its phase p.
@@ -345,7 +350,7 @@ __global__ void __launch_bounds__(1024) wc_fo_split(OrderSrc src, uint32_t M, ui
   clk.at(4);
 }
 
-// Block k: source rows [4096 k, 4096 k + 4096) (table: bucket k's slots).
+// Block k: source rows [FO_ROWS k, FO_ROWS (k + 1)) (table: slots of bucket FO_ROWS k / TAB_SLOTS).
 // cntm / loffm are bin-major: [bin * nblk + k].
 // Exact log-bin histogram of a column source's keys (the merged table): LDS
 // counts per block, one global add per nonzero bin; hist zeroed by the caller
@@ -375,13 +380,13 @@ __global__ void __launch_bounds__(1024) wc_fo_bin(OrderSrc src, uint32_t M, cons
   const uint32_t tid = threadIdx.x, k = blockIdx.x, nblk = gridDim.x;
   const uint64_t i0 = (uint64_t)k * FO_ROWS;
   uint64_t lim;
-  if (src.table) lim = src.t.occupancy[k] ? i0 + FO_ROWS : i0;  // an empty bucket's slots are undefined
+  if (src.table) lim = src.t.occupancy[i0 >> TAB_SLOTS_LOG2] ? i0 + FO_ROWS : i0;  // an empty bucket's slots are undefined
   else lim = src.dn ? *src.dn : src.n;
   // rows first (their loads overlap the map copy)
-  FoEntry e[4];
-  bool ok[4];
+  FoEntry e[FO_RPT];
+  bool ok[FO_RPT];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
+  for (int r = 0; r < FO_RPT; ++r) {
     const uint64_t i = i0 + (uint64_t)r * 1024 + tid;
     ok[r] = i < lim;
     if (src.table) {
@@ -424,9 +429,9 @@ __global__ void __launch_bounds__(1024) wc_fo_bin(OrderSrc src, uint32_t M, cons
   for (uint32_t b = tid; b < FO_BINS; b += 1024) lc[b] = 0;
   __syncthreads();
   clk.at(1);
-  uint32_t bb[4], lp[4];
+  uint32_t bb[FO_RPT], lp[FO_RPT];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
+  for (int r = 0; r < FO_RPT; ++r) {
     bb[r] = FO_BINS;
     if (ok[r]) {
       bb[r] = lmap[fo_logbin(e[r].first, M)];
@@ -441,7 +446,7 @@ __global__ void __launch_bounds__(1024) wc_fo_bin(OrderSrc src, uint32_t M, cons
   if (tid < FO_BINS) loffm[(size_t)tid * nblk + k] = lc[tid];
   FoEntry* out = seg + i0;
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+  for (int r = 0; r < FO_RPT; ++r)
     if (bb[r] != FO_BINS) out[lc[bb[r]] + lp[r]] = e[r];
   clk.at(4);
 }
@@ -728,7 +733,8 @@ void radix_sort_pairs(uint64_t* keys, uint32_t* vals, uint64_t* tmp_keys, uint32
 
 
 static uint32_t fo_blocks(const OrderSrc& src, uint64_t bound) {
-  return src.table ? (1u << src.t.log2_buckets) : (uint32_t)std::max<uint64_t>(1, (bound + dev::FO_ROWS - 1) / dev::FO_ROWS);
+  return src.table ? (1u << src.t.log2_buckets) * (TAB_SLOTS / dev::FO_ROWS)
+                   : (uint32_t)std::max<uint64_t>(1, (bound + dev::FO_ROWS - 1) / dev::FO_ROWS);
 }
 void first_order_stamps(unsigned long long* d) {
   WC_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(dev::fo_stamps), &d, sizeof d));
