@@ -251,7 +251,10 @@ struct OrderDst {
   uint64_t *k0, *k1, *cnt, *first, *soff;
   uint32_t* slen;
 };
-constexpr uint64_t FO_MAX_KEYS = 400 * 1000;  // bins average <= 800 rows (one wave sorts up to 2048)
+#ifndef WC_FO_MAX_KEYS
+#define WC_FO_MAX_KEYS 400000
+#endif
+constexpr uint64_t FO_MAX_KEYS = WC_FO_MAX_KEYS;  // bins average <= 800 rows (one wave sorts up to 2048)
 size_t first_order_ws_bytes(const OrderSrc& src, uint64_t bound);
 void first_order_stamps(unsigned long long* d);  // debug: phase clocks of the three kernels (nullptr: off)
 // key_hist (nullable): a histogram over fo_logbin(first, key_hist_m) of exactly

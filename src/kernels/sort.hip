@@ -213,7 +213,11 @@ __global__ void __launch_bounds__(OS_THREADS) wc_os_pass(const uint64_t* keys, c
 #ifndef WC_FO_ROWS
 #define WC_FO_ROWS 1024
 #endif
-constexpr int FO_BINS = 512, FO_ROWS = WC_FO_ROWS, FO_SAMPLE = 4096;
+#ifndef WC_FO_BINS
+#define WC_FO_BINS 512
+#endif
+constexpr int FO_BINS = WC_FO_BINS, FO_ROWS = WC_FO_ROWS, FO_SAMPLE = 4096;
+static_assert(FO_BINS <= 1024 && FO_BINS % (2 * 64) == 0, "fo bins: <= one per wc_fo_bin thread, whole wc_fo_sort blocks");
 constexpr int FO_RPT = FO_ROWS / 1024;  // wc_fo_bin rows per thread
 static_assert(FO_ROWS % 1024 == 0 && TAB_SLOTS % FO_ROWS == 0, "fo_bin: whole rows per thread, blocks inside a bucket");
 
