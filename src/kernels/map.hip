@@ -901,16 +901,18 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     const uint32_t wave_total = tot_s + tot_o;
     clk.lap(MS_MASK);
     if (wave_total <= (uint32_t)MAP_LIST) {
-      // one list round: short entries at [0, tot_s), the others at [tot_s, total)
-      uint32_t ks = ks0, ko = tot_s + ko0;
-      while (bits) {
-        const uint32_t i = __ffs(bits) - 1;
-        bits &= bits - 1;
-        const uint32_t rest = __builtin_amdgcn_alignbit(dhi, dlo, i);
-        const bool sh = (sbits >> i) & 1u;
-        list[sh ? ks : ko] = (uint16_t)((pbase + i) | (ffbl_raw(rest) << 11));
-        ks += sh ? 1u : 0u;
-        ko += sh ? 0u : 1u;
+      // one list round: short entries at [0, tot_s), the others at [tot_s, total);
+      // one loop per class (no per-entry class select: 9 instead of 16 VALU per entry)
+      uint32_t ks = ks0, ko = tot_s + ko0, sb = sbits, ob = obits;
+      while (sb) {
+        const uint32_t i = __ffs(sb) - 1;
+        sb &= sb - 1;
+        list[ks++] = (uint16_t)((pbase + i) | (ffbl_raw(__builtin_amdgcn_alignbit(dhi, dlo, i)) << 11));
+      }
+      while (ob) {
+        const uint32_t i = __ffs(ob) - 1;
+        ob &= ob - 1;
+        list[ko++] = (uint16_t)((pbase + i) | (ffbl_raw(__builtin_amdgcn_alignbit(dhi, dlo, i)) << 11));
       }
       wave_sync();
       clk.lap(MS_LIST);
