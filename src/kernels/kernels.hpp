@@ -131,7 +131,10 @@ struct HotArgs {
 };
 constexpr uint32_t HOT_LONG_MAX = 64;
 constexpr int HOT_PARTS = 256;       // fingerprint partitions (one wc_hot_merge block each)
-constexpr int HOT_STAGE_CAP = 8;     // words per (partition, map block) cell; more are dropped (a heuristic)
+#ifndef WC_HOT_STAGE_CAP
+#define WC_HOT_STAGE_CAP 8
+#endif
+constexpr int HOT_STAGE_CAP = WC_HOT_STAGE_CAP;  // words per (partition, map block) cell; more are dropped (a heuristic)
 constexpr int HOT_PART_TOP = 32;     // candidates kept per partition (the HOT_K words average 14)
 // Map hot-table geometry: 2-choice groups of HOT_GROUP_SLOTS signatures.  Two
 // slots per group (4 candidate compares and two 16-byte probe reads per token)
