@@ -754,7 +754,8 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     auto step = [&](uint32_t j, uint32_t hi, auto two_c) {
       constexpr bool TWO = decltype(two_c)::value;
       const bool h1 = j + lane < hi, h2 = TWO && j + 64 + lane < hi;
-      const uint32_t e1 = h1 ? list[j + lane] : 0u, e2 = h2 ? list[j + 64 + lane] : 0u;
+      const uint32_t r1 = list[j + lane], r2 = TWO ? list[j + 64 + lane] : 0u;  // unconditional (see step_short)
+      const uint32_t e1 = h1 ? r1 : 0u, e2 = h2 ? r2 : 0u;
       const uint32_t q1 = e1 & 0x7FFu, q2 = e2 & 0x7FFu, n1 = e1 >> 11, n2 = e2 >> 11;
       uint64_t w10, w11, w20 = 0, w21 = 0;
       window16(buf, q1, w10, w11);
@@ -845,7 +846,10 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     auto step_short = [&](uint32_t j, uint32_t hi, auto two_c) {
       constexpr bool TWO = decltype(two_c)::value;
       const bool h1 = j + lane < hi, h2 = TWO && j + 64 + lane < hi;
-      const uint32_t e1 = h1 ? list[j + lane] : 0u, e2 = h2 ? list[j + 64 + lane] : 0u;
+      // unconditional entry reads (no exec-mask branch): past `hi` they read a
+      // later entry, the next wave's list or bcur — inside MapLds, and masked by h1 / h2
+      const uint32_t r1 = list[j + lane], r2 = TWO ? list[j + 64 + lane] : 0u;
+      const uint32_t e1 = h1 ? r1 : 0u, e2 = h2 ? r2 : 0u;
       const uint32_t q1 = e1 & 0x7FFu, q2 = e2 & 0x7FFu, n1 = e1 >> 11, n2 = e2 >> 11;
       const uint64_t w1 = window8(buf, q1), w2 = TWO ? window8(buf, q2) : 0ull;
       // k0: the first n bytes (n <= 7: shift by 64 - 8 n in [8, 56]; n = 0 of an empty lane clamps to 1)
