@@ -121,9 +121,6 @@ struct PhaseClock {
 #ifndef WC_EMIT_ABLATE
 #define WC_EMIT_ABLATE 0
 #endif
-#ifndef WC_REC_NT
-#define WC_REC_NT 0  // non-temporal record stores (A/B)
-#endif
 
 // Record format of a key with count cnt: 12-byte Rec12 (single occurrence of a
 // short word whose last byte is nonzero, so keys.hpp implied_len(k0) == k1 —

@@ -721,7 +721,10 @@ __device__ bool merge_partials(RedLds& L, const ReduceArgs& a, const LongCtx& c,
   __syncthreads();
   const uint32_t np = L.occupied, total = pn[np];
   const ReduceArgs::Parts& P = a.part;
-  constexpr int R = 4;  // rows per thread per round, loaded together
+#ifndef WC_MERGE_R
+#define WC_MERGE_R 4
+#endif
+  constexpr int R = WC_MERGE_R;  // rows per thread per round, loaded together
   for (uint32_t r0 = 0; r0 < total; r0 += R * RED_THREADS) {
     uint64_t k0[R], k1[R], cnt[R], first[R];
     size_t at[R];
