@@ -211,7 +211,7 @@ __global__ void __launch_bounds__(OS_THREADS) wc_os_pass(const uint64_t* keys, c
 // A bin above its LDS capacity (a pathological value distribution) raises *ovf
 // and the caller redoes the order with the radix sort.
 #ifndef WC_FO_ROWS
-#define WC_FO_ROWS 1024
+#define WC_FO_ROWS 2048
 #endif
 #ifndef WC_FO_BINS
 #define WC_FO_BINS 512

@@ -15,7 +15,7 @@ f = glob.glob(sys.argv[1] + "/**/run_kernel_stats.csv", recursive=True)[0]
 out = []
 for r in csv.DictReader(open(f)):
     nm = r["Name"]
-    for k in ("wc_map", "wc_reduce"):
+    for k in ("wc_map", "wc_reduce", "wc_fo_bin", "wc_fo_sort"):
         if k in nm:
             out.append("%s %.1f us" % (k, float(r["AverageNs"]) / 1e3))
 print("%-12s %s" % (sys.argv[2], "  ".join(out)))
