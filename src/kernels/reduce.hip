@@ -687,7 +687,10 @@ __device__ __noinline__ void merge_long_row(RedLds& L, const LongCtx c, uint64_t
 // per block (reduce 214 -> 395 us).
 __device__ bool split_arrive_last(RedLds& L, const ReduceArgs& a, uint32_t b) {
   __shared__ uint32_t last;
-  __syncthreads();  // every wave's partial rows are written
+  // every storing wave waits for its own partial-row stores before the barrier
+  // behind which one lane signals (MI355X_MICROARCH.md hand-off table, row 1)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t old = __hip_atomic_fetch_add(&a.part.done[b], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     last = old + 1 == a.nq ? 1u : 0u;
