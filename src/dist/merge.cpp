@@ -50,8 +50,10 @@ uint64_t* host_words(Engine::Impl& im) {
 
 // Small-vocabulary variant of the shuffle merge (see merge_cols_owner):
 // pack all local rows (one "owner"), send them to rank 0, merge there.
+// `cursor`: 2 zeroed device words (the owner plan's unused scatter cursor), so
+// the one-owner pack needs no memset launch of its own.
 void merge_to_root(Engine::Impl& im, Comm& comm, const std::vector<uint64_t>& rank_rows,
-                   const std::vector<uint64_t>& rank_bytes, uint64_t gmax_end) {
+                   const std::vector<uint64_t>& rank_bytes, uint64_t gmax_end, unsigned long long* cursor) {
   Range rg("wc_merge_root");
   hipStream_t s = im.s;
   const int W = comm.size(), R = comm.rank();
@@ -86,10 +88,9 @@ void merge_to_root(Engine::Impl& im, Comm& comm, const std::vector<uint64_t>& ra
   uint8_t* send_bytes = take_aligned<uint8_t>(A, my_bytes);
   MRow* recv_rows = take_aligned<MRow>(A, rr);
   uint8_t* recv_bytes = take_aligned<uint8_t>(A, rbt);
-  unsigned long long* d_cur = take_aligned<unsigned long long>(A, 4);  // zero counts (2) | cursor (2)
-  WC_HIP_CHECK(hipMemsetAsync(d_cur, 0, 4 * 8, s));
+  // one owner: the scatter reads no owner count before its own (base 0)
   launch_owner_scatter(im.cols.k0, im.cols.k1, im.cols.cnt, im.cols.first, im.cols.sref_off, im.cols.sref_len,
-                       im.cols_arena, n, 1u, d_cur, d_cur + 2, send_rows, send_bytes, nullptr, s);
+                       im.cols_arena, n, 1u, cursor, cursor, send_rows, send_bytes, nullptr, s);
   comm.group_begin();
   comm.alltoallv(send_rows, zs.data(), sr.data(), recv_rows, ro_r.data(), rb_r.data(), s);
   comm.alltoallv(send_bytes, zs.data(), sb.data(), recv_bytes, ro_b.data(), rb_b.data(), s);
@@ -261,7 +262,7 @@ void merge_cols_owner(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense, 
   uint64_t root_max = MERGE_ROOT_MAX_ROWS;
   if (const char* e = std::getenv("WC_MERGE_ROOT_ROWS")) root_max = std::strtoull(e, nullptr, 10);
   if (!dense && !all_ranks && P.total_rows <= root_max) {
-    merge_to_root(im, comm, P.rank_rows, P.rank_bytes, P.gmax_end);
+    merge_to_root(im, comm, P.rank_rows, P.rank_bytes, P.gmax_end, P.d_cnt + P.C);
     return;
   }
 

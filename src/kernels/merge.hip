@@ -218,11 +218,10 @@ __global__ void __launch_bounds__(256) wc_mrow_insert(const MRow* rows, uint64_t
     const uint8_t* mb = hashed ? bytes + bbase[source_of(rbase, W, r)] + me.aoff : nullptr;
     uint64_t slot = place_hash(me.k0, me.k1) & (T - 1);
     for (;;) {
-      uint32_t s = __hip_atomic_load(&state[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (s == 0) {
-        s = atomicCAS(&state[slot], 0u, (uint32_t)r + 1u);
-        if (s == 0) break;  // claimed
-      }
+      // CAS first: most probes find their slot empty, and a load before the CAS
+      // would add a round trip to every claim
+      const uint32_t s = atomicCAS(&state[slot], 0u, (uint32_t)r + 1u);
+      if (s == 0) break;  // claimed
       const MRow& o = rows[s - 1];
       if (o.k0 == me.k0 && o.k1 == me.k1 &&
           (!hashed || (o.alen == me.alen && mem_equal(bytes + bbase[source_of(rbase, W, s - 1)] + o.aoff, mb, me.alen))))
