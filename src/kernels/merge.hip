@@ -205,7 +205,10 @@ __device__ __forceinline__ uint32_t source_of(const uint64_t* rbase, uint32_t W,
 
 // Owner-side merge: a slot belongs to the first row that CAS-es its id in;
 // later rows of the same key compare against that row (immutable input) and add
-// their counts with device-scope atomics.  LONG keys (hashed) also compare the
+// their counts with device-scope atomics.  The claiming row's own count and
+// first offset are folded in by wc_mrow_compact (which reads that row anyway):
+// a key seen once costs one atomic, not three — device-scope atomics resolve
+// past the per-XCD L2s and bound this kernel.  LONG keys (hashed) also compare the
 // word bytes of the two rows, so colliding words take different slots.  T is a
 // power of two >= 2 R.
 __global__ void __launch_bounds__(256) wc_mrow_insert(const MRow* rows, uint64_t R, const uint8_t* bytes,
@@ -217,25 +220,32 @@ __global__ void __launch_bounds__(256) wc_mrow_insert(const MRow* rows, uint64_t
     const bool hashed = key_is_hashed(me.k1);
     const uint8_t* mb = hashed ? bytes + bbase[source_of(rbase, W, r)] + me.aoff : nullptr;
     uint64_t slot = place_hash(me.k0, me.k1) & (T - 1);
+    bool claimed = false;
     for (;;) {
       // CAS first: most probes find their slot empty, and a load before the CAS
       // would add a round trip to every claim
       const uint32_t s = atomicCAS(&state[slot], 0u, (uint32_t)r + 1u);
-      if (s == 0) break;  // claimed
+      if (s == 0) {
+        claimed = true;
+        break;
+      }
       const MRow& o = rows[s - 1];
       if (o.k0 == me.k0 && o.k1 == me.k1 &&
           (!hashed || (o.alen == me.alen && mem_equal(bytes + bbase[source_of(rbase, W, s - 1)] + o.aoff, mb, me.alen))))
         break;  // same word
       slot = (slot + 1) & (T - 1);
     }
-    atomicAdd(&cnt[slot], (unsigned long long)me.cnt);
-    atomicMin(&first[slot], (unsigned long long)me.first);
+    if (!claimed) {
+      atomicAdd(&cnt[slot], (unsigned long long)me.cnt);
+      atomicMin(&first[slot], (unsigned long long)me.first);
+    }
     if (row_slot) row_slot[r] = (uint32_t)slot;
   }
 }
 
 // Occupied slots -> merged rows; aoff becomes absolute in the received byte
 // buffer (rbase/bbase: exclusive prefixes of rows / bytes received per source).
+// count = the claiming row's + the later rows' sum, first = min of both.
 constexpr int MCOMPACT_PER = 4;  // slots per thread (256-thread blocks: 1024 slots per block)
 __global__ void __launch_bounds__(256) wc_mrow_compact(const MRow* rows, const uint32_t* state,
                                                        const unsigned long long* cnt,
@@ -270,8 +280,9 @@ __global__ void __launch_bounds__(256) wc_mrow_compact(const MRow* rows, const u
     const uint64_t r = state[sl] - 1u;
     const uint32_t src = source_of(rbase, W, r);
     MRow m = rows[r];
-    m.cnt = cnt[sl];
-    m.first = first[sl];
+    m.cnt += cnt[sl];
+    const unsigned long long f = first[sl];
+    if (f < m.first) m.first = f;
     if (m.alen) m.aoff = (uint32_t)(bbase[src] + m.aoff);
     out[blk + local[j]] = m;
     if (slot_id) slot_id[sl] = (uint32_t)(blk + local[j]);
