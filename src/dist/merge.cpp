@@ -8,7 +8,8 @@
 //     bytes per owner, all-gather the W x 2 count matrix (+ max offset)    tiny
 //  2. pack rows (40 B) + long-word bytes by owner, RCCL all-to-all         ~V x 40 B
 //  3. owner merges what it received in a global hash table (row-id claims,
-//     device-scope count / min-offset atomics) and compacts it
+//     device-scope count / min-offset atomics for the rows after the claiming
+//     one, whose own values the compaction folds in) and compacts it
 //  4. gather the merged rows + bytes to rank 0 (broadcast for all_ranks)   ~V x 40 B
 // Each rank merges ~V/W keys instead of sorting all W x V, and only rank 0
 // orders the final table; the merge is a few tens of microseconds of xGMI.
