@@ -65,6 +65,10 @@ def parse(argv=None):
     ap.add_argument("--no-oracle", action="store_true",
                     help="skip the key-for-key check against the generator-walk oracle (sum check only)")
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--virtual-ranks", type=int, default=0,
+                    help="W > 0: W engines (threads) on GPU 0 with the stream-ordered loopback communicator, each "
+                         "on its own shard of the stream, the merge at world size W — a merge-cost curve on one "
+                         "GPU, not a scaling number")
     ap.add_argument("--dry-launch", action="store_true",
                     help="launcher test: ranks report their environment and exit without touching a GPU")
     return ap.parse_args(argv)
@@ -108,6 +112,57 @@ def loaded_runtime() -> dict:
             elif base == "libwc.so":
                 libs["engine"].add(path)
     return {k: sorted(v) if isinstance(v, set) else v for k, v in libs.items()}
+
+
+def run_virtual(a) -> int:
+    """--virtual-ranks W: the merged step at world size W on one GPU (all ranks share it)."""
+    from cuda_mapreduce_amd.models import CONFIGS
+    from cuda_mapreduce_amd.ops import virtual_bench
+    from cuda_mapreduce_amd.utils import compare_results, synthetic_oracle
+
+    cfg = CONFIGS[a.config]
+    gib = 1 << 30
+    W = a.virtual_ranks
+    per = (int(a.gb_per_gpu * gib) if a.gb_per_gpu is not None else cfg.bytes_per_gpu) // 1024 * 1024
+    vocab = a.vocab if a.vocab is not None else cfg.vocab
+    zipf = a.zipf if a.zipf is not None else cfg.zipf_s
+    seed = a.seed if a.seed is not None else cfg.seed
+    long_frac = a.long_frac if a.long_frac is not None else cfg.long_frac
+    chunk = min(int(a.chunk_gb * gib) if a.chunk_gb is not None else cfg.chunk_bytes, per) // 1024 * 1024
+    merge = a.merge or cfg.merge
+    res, ranks = virtual_bench(W, per, seed=seed, vocab=vocab, zipf_s=zipf, long_frac=long_frac, steps=a.steps,
+                               warmup=a.warmup, chunk_bytes=chunk, merge_mode={"shuffle": 0, "dense": 1}[merge])
+    tokens = sum(r["tokens"] for r in ranks)
+    valid = int(res.total) == int(tokens) and int(res.counts.sum()) == int(tokens)
+    check = {"oracle": "skipped (--no-oracle): token-sum check only"}
+    if not a.no_oracle:
+        t1 = time.perf_counter()
+        want = synthetic_oracle(W, per, seed, vocab, zipf, chunk=chunk, long_frac=long_frac)
+        diff = compare_results(res, want)
+        check = {"oracle": "generator word walk (cpu_count_synth)", "identical": not diff,
+                 "seconds": round(time.perf_counter() - t1, 2)}
+        valid = valid and not diff
+        if diff:
+            print(f"bench: VALIDATION FAILED vs oracle: {diff}", file=sys.stderr, flush=True)
+    ms = max(r["ms_per_step"] for r in ranks)
+    out = {
+        "metric": "merged step at W virtual ranks on one GPU (merge-cost curve, not scaling)",
+        "virtual_ranks": W, "value": round(W * per / (ms / 1e3) / 1e9, 3), "unit": "GB/s (all ranks share one GPU)",
+        "ms_per_step": round(ms, 4), "steps": a.steps, "warmup": a.warmup, "validated": valid, "validation": check,
+        "distinct_words": len(res.words),
+        "merge_ms": [round(r["merge"], 4) for r in ranks],
+        "stage_ms_rank0": {k: round(ranks[0][k], 4) for k in ("map", "reduce", "finalize", "merge", "idle")},
+        "keys_per_rank": [int(r["keys"]) for r in ranks],
+        "config": {"model": f"wordcount-mapreduce/{cfg.name}", "bytes_per_rank": per, "chunk_bytes": chunk,
+                   "merge": merge, "vocab": vocab, "long_frac": long_frac,
+                   "communicator": "stream-ordered loopback (src/dist/comm.cpp)"},
+    }
+    line = json.dumps(out)
+    print(line, flush=True)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            f.write(line + "\n")
+    return 0 if valid else 1
 
 
 def run_rank(a) -> int:
@@ -182,9 +237,9 @@ def run_rank(a) -> int:
                 return int(f.read().split()[1]) * os.sysconf("SC_PAGE_SIZE")
 
         rss_before = rss_now()  # interpreter + HIP runtime, before the pool exists
-        pool = HostPool(pool_bytes, first_segment=first_seg, threads=16, **synth)
+        pool = HostPool(pool_bytes, first_segment=first_seg, threads=16, device=local, **synth)
         peak = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024
-        pool_info = {"pool_bytes": pool_bytes, "build_s": round(pool.build_seconds, 3),
+        pool_info = {"pool_bytes": pool_bytes, "build_s": round(pool.build_seconds, 3), "numa_node": pool.numa_node,
                      "rss_before_pool_bytes": rss_before, "peak_rss_bytes": peak,
                      "pool_rss_ratio": round((peak - rss_before) / pool_bytes, 4)}
     else:
@@ -292,6 +347,8 @@ def run_rank(a) -> int:
 
 def main() -> int:
     a = parse()
+    if a.virtual_ranks > 0:
+        return run_virtual(a)
     if "WORLD_SIZE" not in os.environ and (a.gpus > 1 or a.dry_launch):
         return launch(a)
     return run_rank(a)

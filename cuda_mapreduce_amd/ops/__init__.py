@@ -12,6 +12,9 @@ from .engine import (  # noqa: F401
     device_count,
     format_output,
     loopback_count,
+    virtual_bench,
+    numa_of_pci,
+    h2d_bench,
     shard_range,
     shard_range_file,
     synth_host,

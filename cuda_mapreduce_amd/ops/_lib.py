@@ -79,11 +79,17 @@ def _load() -> ctypes.CDLL:
         "wc_format": (c_int, [c_void_p, P8, c_uint64, c_int, c_int, c_uint64, POINTER(c_void_p), P64]),
         "wc_free": (None, [c_void_p]),
         "wc_cpu_count": (c_void_p, [P8, c_uint64, c_uint64]),
+        "wc_key_owner": (c_uint32, [P8, c_uint64, c_uint32]),
+        "wc_debug_comm_counters": (None, [P64, P64]),
+        "wc_debug_loopback_async": (c_int, [c_int, POINTER(c_int), POINTER(c_int), POINTER(c_int)]),
         "wc_cpu_count_compat": (c_void_p, [P8, c_uint64]),
         "wc_synth_host": (c_int, [P8, c_uint64, c_uint64, c_uint64, c_uint32, c_double]),
         "wc_synth_host_mt": (c_int, [P8, c_uint64, c_uint64, c_uint64, c_uint32, c_double, c_double, c_int]),
         "wc_cpu_count_synth": (c_void_p, [c_uint64, c_uint64, c_uint64, c_uint32, c_double, c_double, c_uint64, c_int]),
-        "wc_pool_create": (c_void_p, [c_uint64, c_uint64, c_uint64, c_uint32, c_double, c_double, c_int]),
+        "wc_pool_create": (c_void_p, [c_uint64, c_uint64, c_uint64, c_uint32, c_double, c_double, c_int, c_int]),
+        "wc_pool_numa_node": (c_int, [c_void_p]),
+        "wc_numa_of_pci": (c_int, [c_char_p, c_char_p, POINTER(c_int), POINTER(c_int), c_int]),
+        "wc_h2d_bench": (c_int, [c_int, c_int, c_uint64, c_int, POINTER(c_double), POINTER(c_int)]),
         "wc_pool_destroy": (None, [c_void_p]),
         "wc_pool_build_seconds": (c_double, [c_void_p]),
         "wc_count_pool": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64]),
@@ -95,10 +101,12 @@ def _load() -> ctypes.CDLL:
         "wc_comm_barrier": (c_int, [c_void_p]),
         "wc_comm_allgather_host": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
         "wc_loopback_count": (c_void_p, [P8, c_uint64, c_int, POINTER(c_int), POINTER(Options), c_int, c_int]),
+        "wc_virtual_bench": (c_void_p, [POINTER(Options), c_int, c_int, c_uint64, c_uint64, c_uint32, c_double, c_double,
+                                        c_int, c_int, POINTER(c_double)]),
     }
     for name, (res, args) in sig.items():
-        if name.startswith("wc_debug_") and not hasattr(lib, name):
-            continue  # kernel unit-test hooks: absent from older A/B variant builds (WC_LIB)
+        if not hasattr(lib, name):
+            continue  # an older A/B variant build (WC_LIB) without this entry point: calling it raises
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -278,10 +278,12 @@ class HostPool:
     """Page-locked synthetic replay pool (host-staged configs), generated in place natively."""
 
     def __init__(self, nbytes: int, first_segment: int = 0, seed: int = 1, vocab: int = 100000,
-                 zipf_s: float = 1.0, threads: int = 16, long_frac: float = 0.0):
-        self._p = check_ptr(lib.wc_pool_create(nbytes, first_segment, seed, vocab, zipf_s, long_frac, threads))
+                 zipf_s: float = 1.0, threads: int = 16, long_frac: float = 0.0, device: int = -1):
+        """device >= 0: the pool's pages and generator threads on that GPU's NUMA node."""
+        self._p = check_ptr(lib.wc_pool_create(nbytes, first_segment, seed, vocab, zipf_s, long_frac, threads, device))
         self.nbytes = nbytes
         self.build_seconds = float(lib.wc_pool_build_seconds(self._p))
+        self.numa_node = int(lib.wc_pool_numa_node(self._p))
 
     def close(self) -> None:
         if getattr(self, "_p", None):
@@ -290,6 +292,21 @@ class HostPool:
 
     def __del__(self):
         self.close()
+
+
+def numa_of_pci(bus_id: str, sysfs_root: str = "/sys"):
+    """(node, cpus) of a PCI device from a sysfs tree (src/io/numa.cpp); node -1 if unknown."""
+    node = ctypes.c_int(-1)
+    cpus = (ctypes.c_int * 4096)()
+    n = lib.wc_numa_of_pci(sysfs_root.encode(), bus_id.encode(), ctypes.byref(node), cpus, 4096)
+    return node.value, list(cpus[:min(n, 4096)])
+
+
+def h2d_bench(device: int = 0, node: int = -1, nbytes: int = 1 << 30, reps: int = 8):
+    """Pinned H2D GB/s from a pool on host NUMA node `node` (-1: the GPU's own) -> (GB/s, node used)."""
+    g, used = ctypes.c_double(0), ctypes.c_int(-1)
+    check(lib.wc_h2d_bench(device, node, nbytes, reps, ctypes.byref(g), ctypes.byref(used)))
+    return g.value, used.value
 
 
 def shard_range(data: bytes, rank: int, world: int):
@@ -304,6 +321,20 @@ def shard_range_file(path: str, rank: int, world: int):
     b, e = ctypes.c_uint64(), ctypes.c_uint64()
     check(lib.wc_shard_range_file(path.encode(), rank, world, ctypes.byref(b), ctypes.byref(e)))
     return int(b.value), int(e.value)
+
+
+def virtual_bench(ranks: int, nbytes: int, seed: int = 1, vocab: int = 100000, zipf_s: float = 1.0,
+                  long_frac: float = 0.0, steps: int = 20, warmup: int = 3, device: int = 0, **opts):
+    """`ranks` virtual ranks (threads, stream-ordered loopback communicator) on
+    one GPU run bench.py's step on their own resident shards of one synthetic
+    stream.  Returns (rank 0's merged Result, per-rank dicts of wall ms/step and
+    the last job's device stage times)."""
+    o = default_options(**opts)
+    out = (ctypes.c_double * (8 * ranks))()
+    res = Result._from_native(check_ptr(lib.wc_virtual_bench(ctypes.byref(o), ranks, device, nbytes, seed, vocab,
+                                                             zipf_s, long_frac, steps, warmup, out)))
+    keys = ("ms_per_step", "map", "reduce", "finalize", "merge", "idle", "tokens", "keys")
+    return res, [{k: out[8 * r + i] for i, k in enumerate(keys)} for r in range(ranks)]
 
 
 def loopback_count(data: bytes, ranks: int, devices: Optional[Sequence[int]] = None, all_ranks: bool = False,

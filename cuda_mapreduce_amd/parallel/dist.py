@@ -19,7 +19,6 @@ from __future__ import annotations
 import datetime
 import os
 import struct
-import zlib
 from dataclasses import dataclass
 from typing import Optional
 
@@ -117,8 +116,50 @@ def _reduce_scatter(t, op):
     return out
 
 
+_M32, _M64 = (1 << 32) - 1, (1 << 64) - 1
+_FNV_OFFSET, _FNV_PRIME = 0xCBF29CE484222325, 0x100000001B3
+
+
+def _fmix64(k: int) -> int:
+    k ^= k >> 33
+    k = (k * 0xFF51AFD7ED558CCD) & _M64
+    k ^= k >> 33
+    k = (k * 0xC4CEB9FE1A85EC53) & _M64
+    return k ^ (k >> 33)
+
+
+def key_of(word: bytes):
+    """(k0, k1) of a word: src/kernels/keys.hpp key_of (SHORT / MEDIUM exact, LONG hashed)."""
+    n = len(word)
+    k0 = int.from_bytes(word[:8].ljust(8, b"\0"), "little")
+    if n <= 8:
+        return k0, n
+    if n <= 15:
+        return k0, int.from_bytes(word[8:].ljust(8, b"\0"), "little") | (n << 56)
+    h = _FNV_OFFSET
+    for c in range(8, n, 8):
+        h = ((h ^ int.from_bytes(word[c:c + 8].ljust(8, b"\0"), "little")) * _FNV_PRIME) & _M64
+    return k0, (1 << 63) | (_fmix64(h ^ n) & ((1 << 62) - 1))
+
+
+def _mix32(x: int) -> int:
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & _M32
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & _M32
+    return x ^ (x >> 16)
+
+
+def place_hash(k0: int, k1: int) -> int:
+    """keys.hpp place_hash: 32-bit placement hash of a packed key."""
+    c = (k1 & _M32) ^ (k1 >> 32)
+    return _mix32((k0 & _M32) ^ (((k0 >> 32) * 0x9E3779B1) & _M32) ^ ((c * 0x85EBCA77) & _M32))
+
+
 def _owner(word: bytes, world: int) -> int:
-    return zlib.crc32(word) % world
+    """Merge owner of a word: keys.hpp owner_of, the rule src/dist/merge.cpp partitions by
+    (high bits of the placement hash)."""
+    return (place_hash(*key_of(word)) * world) >> 32
 
 
 def _pack(rows) -> bytes:
@@ -161,9 +202,12 @@ def _alltoallv_bytes(parts) -> list:
 
 def host_merge(local: Result, dense: bool = False) -> Result:
     """Merge per-rank results on the host over torch.distributed (CPU ranks over
-    gloo) with the owner-partitioned protocol of src/dist/merge.cpp:
+    gloo): a Python mirror of the owner-partitioned protocols of
+    src/dist/merge.cpp (the native merge runs HIP kernels and RCCL, so CPU
+    ranks cannot run it):
 
-    1. owner(word) = crc32(word) mod W; rows are packed by owner
+    1. owner(word) = high bits of the word's placement hash (keys.hpp owner_of,
+       the native rule); rows are packed by owner
     2. all-to-all (personalised exchange) of the packed rows
     3. each owner merges what it received (counts add, first offset = min)
     shuffle: 4. the owners' merged rows are gathered to every rank

@@ -55,12 +55,14 @@ int wc_result_merge(wc_result* dst, const wc_result* src);
 int wc_count_replay(wc_engine* e, const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t global_base);
 /* Host-staged benchmark path: pool page-locked once, chunks DMA'd directly. */
 int wc_count_pinned_replay(wc_engine* e, const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t global_base);
-/* Page-locked synthetic replay pool generated in place on `threads` threads (host-staged config). */
+/* Page-locked synthetic replay pool generated in place on `threads` threads (host-staged config);
+ * device >= 0: pages and generator threads on that GPU's NUMA node. */
 typedef struct wc_pool wc_pool;
 wc_pool* wc_pool_create(uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double zipf_s,
-                        double long_frac, int threads);
+                        double long_frac, int threads, int device);
 void wc_pool_destroy(wc_pool* p);
 double wc_pool_build_seconds(const wc_pool* p);
+int wc_pool_numa_node(const wc_pool* p); /* -1: unknown / unbound */
 int wc_count_pool(wc_engine* e, const wc_pool* p, uint64_t total, uint64_t global_base);
 /* Generate synthetic text into the engine's device text buffer (long_frac: share of the
  * vocabulary drawn as 16..64-byte words) ... */

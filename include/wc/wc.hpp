@@ -159,18 +159,22 @@ KeyTable count_reference_compat(const uint8_t* text, uint64_t n, std::string* ec
 // benchmark config): generated in place by `threads` threads, no pageable copy.
 class HostPool {
  public:
-  HostPool(uint64_t n, uint64_t first_segment, const SynthSpec& spec, int threads);
+  // device >= 0: the pool's pages and its generator threads on that GPU's NUMA
+  // node (src/io/numa.hpp); numa_node() reports it (-1: unknown / unbound).
+  HostPool(uint64_t n, uint64_t first_segment, const SynthSpec& spec, int threads, int device = -1);
   ~HostPool();
   HostPool(const HostPool&) = delete;
   HostPool& operator=(const HostPool&) = delete;
   const uint8_t* data() const { return p_; }
   uint64_t size() const { return n_; }
   double build_seconds() const { return secs_; }
+  int numa_node() const { return node_; }
 
  private:
   uint8_t* p_ = nullptr;
   uint64_t n_ = 0;
   double secs_ = 0;
+  int node_ = -1;
 };
 
 // Host copy of the synthetic stream (bit-identical to the device generator).

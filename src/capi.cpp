@@ -1,4 +1,5 @@
 // capi.cpp — C ABI over the C++ engine (ctypes binding of the Python package).
+#include <atomic>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -9,9 +10,11 @@
 #include "common/hip_util.hpp"
 #include "dist/comm.hpp"
 #include "io/checkpoint.hpp"
+#include "io/numa.hpp"
 #include "io/source.hpp"
 #include "io/synth_host.hpp"
 #include "kernels/kernels.hpp"
+#include "kernels/keys.hpp"
 #include "wc/wc.h"
 #include "wc/wc.hpp"
 
@@ -89,6 +92,70 @@ extern "C" {
 
 const char* wc_last_error(void) { return g_err.c_str(); }
 const char* wc_version(void) { return "wc-mi355x 0.1.0"; }
+
+// Stream-ordering check of the loopback communicator (tests): two ranks on
+// `device`, rank 1's stream held by a wait on a page-locked flag.  Both ranks
+// enqueue an allgather of 64 u64 from their own threads; the calls must
+// return while rank 1's stream is held (no host wait inside a collective) and
+// rank 0's stream must still be waiting (nothing is complete before every
+// rank's stream gets there).  Then the flag is released and both results are
+// checked.  *returned = 1 if both calls returned while held, *pending = 1 if
+// rank 0's stream was still busy then, *correct = 1 if both gathers are right.
+int wc_debug_loopback_async(int device, int* returned, int* pending, int* correct) {
+  return guard([&] {
+    WC_HIP_CHECK(hipSetDevice(device));
+    auto comms = wc::make_loopback_comms(2);
+    hipStream_t st[2];
+    for (auto& x : st) WC_HIP_CHECK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+    uint32_t* hold = nullptr;
+    WC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hold), 64, hipHostMallocCoherent));
+    *hold = 0;
+    uint64_t* d = nullptr;
+    WC_HIP_CHECK(hipMalloc(&d, 2 * 192 * 8));
+    std::vector<uint64_t> h(2 * 192);
+    for (int r = 0; r < 2; ++r)
+      for (int i = 0; i < 64; ++i) h[(size_t)r * 192 + i] = (uint64_t)r * 1000003u + (uint64_t)i * 7u;
+    WC_HIP_CHECK(hipMemcpy(d, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+    WC_HIP_CHECK(hipStreamWaitValue32(st[1], hold, 1, hipStreamWaitValueGte, 0xFFFFFFFFu));
+    std::atomic<int> back{0};
+    std::vector<std::thread> th;
+    for (int r = 0; r < 2; ++r)
+      th.emplace_back([&, r] {
+        comms[r]->allgather(d + (size_t)r * 192, d + (size_t)r * 192 + 64, 64 * 8, st[r]);
+        ++back;
+      });
+    const double t0 = wc::now_seconds();
+    while (back.load() < 2 && wc::now_seconds() - t0 < 10.0) std::this_thread::yield();
+    *returned = back.load() == 2;
+    *pending = hipStreamQuery(st[0]) == hipErrorNotReady;
+    __atomic_store_n(hold, 1u, __ATOMIC_SEQ_CST);
+    for (auto& t : th) t.join();
+    for (auto& x : st) WC_HIP_CHECK(hipStreamSynchronize(x));
+    WC_HIP_CHECK(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
+    bool ok = true;
+    for (int r = 0; r < 2; ++r)
+      for (int q = 0; q < 2; ++q)
+        for (int i = 0; i < 64; ++i) ok &= h[(size_t)r * 192 + 64 + (size_t)q * 64 + i] == (uint64_t)q * 1000003u + (uint64_t)i * 7u;
+    *correct = ok;
+    WC_HIP_CHECK(hipFree(d));
+    WC_HIP_CHECK(hipHostFree(hold));
+    for (auto& x : st) WC_HIP_CHECK(hipStreamDestroy(x));
+  });
+}
+
+// Process-wide communicator counters: collectives enqueued, host waits.
+void wc_debug_comm_counters(uint64_t* collectives, uint64_t* host_waits) {
+  *collectives = wc::Comm::collectives_total();
+  *host_waits = wc::Comm::host_waits_total();
+}
+
+// Merge owner of a word among W ranks (keys.hpp owner_of of its placement
+// hash): the native rule the Python merge mirror is tested against.
+uint32_t wc_key_owner(const uint8_t* word, uint64_t len, uint32_t W) {
+  uint64_t k0, k1;
+  wc::key_of(word, len, &k0, &k1);
+  return wc::owner_of(wc::place_hash(k0, k1), W ? W : 1);
+}
 
 int wc_debug_radix_sort(int device, const uint64_t* keys, uint64_t n, int bits, uint64_t* sorted, uint32_t* perm) {
   return guard([&] {
@@ -474,9 +541,11 @@ struct wc_pool {
 };
 
 wc_pool* wc_pool_create(uint64_t n, uint64_t first_segment, uint64_t seed, uint32_t vocab, double s, double long_frac,
-                        int threads) {
+                        int threads, int device) {
   wc_pool* r = new wc_pool;
-  if (guard([&] { r->p.reset(new wc::HostPool(n, first_segment, spec_of(seed, vocab, s, long_frac), threads)); }) != 0) {
+  if (guard([&] {
+        r->p.reset(new wc::HostPool(n, first_segment, spec_of(seed, vocab, s, long_frac), threads, device));
+      }) != 0) {
     delete r;
     return nullptr;
   }
@@ -484,6 +553,47 @@ wc_pool* wc_pool_create(uint64_t n, uint64_t first_segment, uint64_t seed, uint3
 }
 void wc_pool_destroy(wc_pool* p) { delete p; }
 double wc_pool_build_seconds(const wc_pool* p) { return p ? p->p->build_seconds() : 0.0; }
+int wc_pool_numa_node(const wc_pool* p) { return p ? p->p->numa_node() : -1; }
+
+// NUMA resolution against a sysfs tree (tests: a fake root): node of the PCI
+// device and up to `cap` of its CPUs; returns the CPU count.
+int wc_numa_of_pci(const char* sysfs_root, const char* bus_id, int* node, int* cpus, int cap) {
+  const wc::NumaNode n = wc::numa_of_pci(bus_id, sysfs_root);
+  *node = n.node;
+  for (int i = 0; i < cap && i < (int)n.cpus.size(); ++i) cpus[i] = n.cpus[i];
+  return (int)n.cpus.size();
+}
+
+// Pinned-memory H2D bandwidth from a pool on NUMA node `node` (-1: the GPU's
+// own node, numa_of_device) to `device`: `bytes` copied `reps` times after one
+// warm copy.  *node_used = the node the pool was bound to (-1: unbound).
+int wc_h2d_bench(int device, int node, uint64_t bytes, int reps, double* gbps, int* node_used) {
+  return guard([&] {
+    WC_HIP_CHECK(hipSetDevice(device));
+    const wc::NumaNode nn = node >= 0 ? wc::numa_node_cpus(node) : wc::numa_of_device(device);
+    uint8_t* h = nullptr;
+    uint8_t* d = nullptr;
+    {
+      wc::ScopedAffinity bind(nn.cpus);
+      *node_used = bind.active() ? nn.node : -1;
+      WC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h), bytes,
+                                 bind.active() ? hipHostMallocNumaUser : hipHostMallocDefault));
+      std::memset(h, 0x20, bytes);
+    }
+    WC_HIP_CHECK(hipMalloc(&d, bytes));
+    hipStream_t s;
+    WC_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    WC_HIP_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s));
+    WC_HIP_CHECK(hipStreamSynchronize(s));
+    const double t0 = wc::now_seconds();
+    for (int i = 0; i < reps; ++i) WC_HIP_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s));
+    WC_HIP_CHECK(hipStreamSynchronize(s));
+    *gbps = (double)bytes * reps / (wc::now_seconds() - t0) / 1e9;
+    WC_HIP_CHECK(hipStreamDestroy(s));
+    WC_HIP_CHECK(hipFree(d));
+    WC_HIP_CHECK(hipHostFree(h));
+  });
+}
 int wc_count_pool(wc_engine* e, const wc_pool* p, uint64_t total, uint64_t base) {
   return guard([&] { e->e->count_pinned_replay(p->p->data(), p->p->size(), total, base, true); });
 }
@@ -552,6 +662,76 @@ int wc_comm_allgather_host(wc_comm* c, const void* send, uint64_t bytes, void* r
 }
 
 void wc_comm_destroy(wc_comm* c) { delete c; }
+
+// Virtual ranks on one GPU (bench.py --virtual-ranks): `ranks` engines in
+// threads on `device`, each holding its own resident shard of the synthetic
+// stream (rank r: segments [r * nseg, (r + 1) * nseg), global offsets from
+// r * bytes), one stream-ordered loopback group, and bench.py's step — reset,
+// count the shard, merged finalize on the device — `warmup` + `steps` times,
+// the timed loop bracketed by communicator barriers.  out[8 r + i] =
+// {wall ms / step, device ms of the last job: map, reduce, finalize, merge,
+// idle, tokens, local keys}.  Returns rank 0's merged table (one result()
+// after timing) for validation.
+wc_result* wc_virtual_bench(const wc_options* o, int ranks, int device, uint64_t bytes, uint64_t seed, uint32_t vocab,
+                            double zipf, double long_frac, int steps, int warmup, double* out) {
+  wc_result* res = new wc_result;
+  std::vector<std::string> errs(ranks);
+  std::vector<std::unique_ptr<wc::Comm>> comms;
+  if (guard([&] { comms = wc::make_loopback_comms(ranks); }) != 0) {
+    delete res;
+    return nullptr;
+  }
+  const uint64_t seg = 1024, nseg = bytes / seg;
+  std::vector<std::thread> th;
+  for (int r = 0; r < ranks; ++r) {
+    th.emplace_back([&, r] {
+      try {
+        wc::Options opt = to_opts(o);
+        opt.device = device;
+        wc::Engine eng(opt);
+        const uint8_t* d = eng.synth_device(nseg * seg, (uint64_t)r * nseg, spec_of(seed, vocab, zipf, long_frac));
+        wc::Comm* c = comms[r].get();
+        auto step = [&] {
+          eng.reset();
+          eng.count_device(d, nseg * seg, nseg * seg, (uint64_t)r * nseg * seg, ' ');
+          return eng.finalize_device(c);
+        };
+        for (int i = 0; i < warmup; ++i) step();
+        WC_HIP_CHECK(hipDeviceSynchronize());
+        c->barrier(nullptr);
+        const double t0 = wc::now_seconds();
+        uint64_t keys = 0;
+        for (int i = 0; i < steps; ++i) keys = step();
+        WC_HIP_CHECK(hipDeviceSynchronize());
+        c->barrier(nullptr);
+        const double ms = (wc::now_seconds() - t0) * 1e3 / (steps > 0 ? steps : 1);
+        const wc::Stats& st = eng.stats();
+        double* v = out + 8 * (size_t)r;
+        v[0] = ms;
+        v[1] = st.map_ms;
+        v[2] = st.reduce_ms;
+        v[3] = st.finalize_ms;
+        v[4] = st.merge_ms;
+        v[5] = st.idle_ms;
+        v[6] = (double)st.tokens;
+        v[7] = (double)keys;
+        wc::KeyTable t = eng.result(c, false);
+        if (r == 0) res->t = std::move(t);
+      } catch (const std::exception& ex) {
+        errs[r] = ex.what();
+        comms[r]->abort(ex.what());
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int r = 0; r < ranks; ++r)
+    if (!errs[r].empty()) {
+      g_err = "rank " + std::to_string(r) + ": " + errs[r];
+      delete res;
+      return nullptr;
+    }
+  return res;
+}
 
 wc_result* wc_loopback_count(const uint8_t* text, uint64_t n, int ranks, const int* devices, const wc_options* o,
                              int all_ranks, int resident) {

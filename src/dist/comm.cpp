@@ -3,6 +3,7 @@
 
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -10,10 +11,10 @@
 #include <thread>
 
 #include "../common/hip_util.hpp"
+#include "../kernels/kernels.hpp"
 
 namespace wc {
 
-void launch_combine_u64(uint64_t* dst, const uint64_t* src, uint64_t n, int op, hipStream_t s);  // merge.hip
 
 #define WC_NCCL_CHECK(expr)                                                                          \
   do {                                                                                                \
@@ -35,9 +36,17 @@ Comm::Comm() {
   }
 }
 
+namespace {
+std::atomic<uint64_t> g_collectives{0}, g_host_waits{0};
+}
+uint64_t Comm::collectives_total() { return g_collectives.load(); }
+uint64_t Comm::host_waits_total() { return g_host_waits.load(); }
+void Comm::count_host_wait() { ++g_host_waits; }
+
 void Comm::tick(int rank) {
   if (failed()) fail("communicator failed earlier: " + failed_);
   ++calls_;
+  ++g_collectives;
   if (rank == fault_rank_ && calls_ == fault_at_) {
     const std::string why = "injected comm fault (WC_COMM_FAULT) at collective " + std::to_string(calls_) +
                             " of rank " + std::to_string(rank);
@@ -48,6 +57,7 @@ void Comm::tick(int rank) {
 
 void Comm::sync(hipStream_t s) {
   if (failed()) fail("communicator failed earlier: " + failed_);
+  count_host_wait();
   WC_HIP_CHECK(hipStreamSynchronize(s));
 }
 
@@ -109,6 +119,7 @@ class RcclComm final : public Comm {
   // spinning forever under a plain hipStreamSynchronize.
   void sync(hipStream_t s) override {
     if (failed()) fail("communicator failed earlier: " + failed_);
+    count_host_wait();
     const double t0 = now_seconds();
     for (;;) {
       const hipError_t q = hipStreamQuery(s);
@@ -142,19 +153,37 @@ class RcclComm final : public Comm {
   void* scratch_ = nullptr;
 };
 
-// Shared rendezvous for loopback ranks.
+// Shared state of one loopback group: the page-locked metadata the ranks'
+// transfer kernels read (kernels.hpp LbShared, src/kernels/comm.hip), the
+// per-slot ready / done events, and the arrival rendezvous.
 struct Hub {
-  explicit Hub(int n) : n(n), offs(n, nullptr), ptrs(n, nullptr) {}
+  explicit Hub(int n) : n(n) {
+    WC_CHECK(n >= 1 && n <= LB_MAX_RANKS, "loopback: 1..64 ranks");
+    WC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&sh), sizeof(LbShared), hipHostMallocCoherent));
+    std::memset(sh, 0, sizeof(LbShared));
+    ready.resize((size_t)LB_RING * n);
+    done.resize((size_t)LB_RING * n);
+    for (auto* v : {&ready, &done})
+      for (auto& e : *v) WC_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  ~Hub() {
+    for (auto* v : {&ready, &done})
+      for (auto& e : *v)
+        if (e) (void)hipEventDestroy(e);
+    if (sh) (void)hipHostFree(sh);
+  }
   int n;
-  std::vector<const size_t*> offs;  // alltoallv: each rank's send offsets
+  LbShared* sh = nullptr;
+  std::vector<hipEvent_t> ready, done;  // [slot * n + rank]
   std::mutex mu;
   std::condition_variable cv;
   int arrived = 0;
   uint64_t gen = 0;
-  std::vector<const void*> ptrs;
-  bool aborted = false;  // a rank failed: every current and later wait throws
+  bool aborted = false;  // a rank failed: every current and later rendezvous throws
   std::string why;
-  void wait_all() {
+  // Every rank has ENQUEUED up to this point (a host rendezvous on the calls,
+  // never on the GPU: no stream is waited for).
+  void arrive() {
     std::unique_lock<std::mutex> lk(mu);
     if (aborted) fail("loopback peer failed: " + why);
     const uint64_t g = gen;
@@ -167,22 +196,40 @@ struct Hub {
       if (gen == g) fail("loopback peer failed: " + why);
     }
   }
+  bool is_aborted() {
+    std::lock_guard<std::mutex> lk(mu);
+    return aborted;
+  }
   void abort(const std::string& w) {
     std::lock_guard<std::mutex> lk(mu);
     if (!aborted) {
       aborted = true;
       why = w;
+      __atomic_store_n(&sh->aborted, 1u, __ATOMIC_SEQ_CST);  // transfers already queued skip their copies
     }
     cv.notify_all();
   }
 };
 
+// Loopback ranks, one per thread, every rank's stream on one device (or on
+// peer-accessible devices: the transfer kernel reads the peers' buffers
+// directly).  A collective is ENQUEUED like an RCCL collective, never waited
+// for: each rank records "ready" on its stream behind its earlier work; after
+// the arrival rendezvous every peer's ready event exists, so the stream waits
+// on all of them (hipStreamWaitEvent) and runs the transfer kernel, which
+// reads the peers' buffer addresses from the page-locked metadata; then
+// "done" is recorded, a second rendezvous, and the stream waits for every
+// peer's done (a send buffer is reusable once the collective completes on the
+// stream, as with RCCL).  Nothing is complete until the stream gets there: a
+// host read of a collective's output before sync() sees stale data, exactly
+// as with RCCL.  Only arrival rendezvous block the host (for the peers to
+// CALL the collective); every event waited on was recorded before the wait
+// was enqueued, so streams sharing a hardware queue (GPU_MAX_HW_QUEUES) never
+// wait on work queued behind them.
 class LoopbackComm final : public Comm {
  public:
   LoopbackComm(std::shared_ptr<Hub> hub, int rank) : hub_(std::move(hub)), rank_(rank) {}
-  ~LoopbackComm() override {
-    if (scratch_) (void)hipFree(scratch_);
-  }
+  ~LoopbackComm() override = default;
   int rank() const override { return rank_; }
   int size() const override { return hub_->n; }
   const char* backend() const override { return "loopback"; }
@@ -192,74 +239,89 @@ class LoopbackComm final : public Comm {
   }
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
     tick(rank_);
-    WC_HIP_CHECK(hipStreamSynchronize(s));
-    hub_->ptrs[rank_] = send;
-    hub_->wait_all();
-    for (int r = 0; r < hub_->n; ++r)
-      WC_HIP_CHECK(hipMemcpyAsync(static_cast<uint8_t*>(recv) + (size_t)r * bytes, hub_->ptrs[r], bytes,
-                                  hipMemcpyDefault, s));
-    WC_HIP_CHECK(hipStreamSynchronize(s));
-    hub_->wait_all();  // senders may reuse their buffers after everyone copied
+    LbMeta& m = begin();
+    m.send = reinterpret_cast<uint64_t>(send);
+    m.recv = reinterpret_cast<uint64_t>(recv);
+    enqueue(LB_ALLGATHER, bytes, 0, 0, s);
   }
   void reduce_scatter_u64(const uint64_t* send, uint64_t* recv, size_t count, RedOp op, hipStream_t s) override {
     tick(rank_);
-    WC_HIP_CHECK(hipStreamSynchronize(s));
-    hub_->ptrs[rank_] = send;
-    hub_->wait_all();
-    if (count > scratch_n_) {  // grown once, reused: no allocation per collective
-      if (scratch_) WC_HIP_CHECK(hipFree(scratch_));
-      WC_HIP_CHECK(hipMalloc(&scratch_, count * 8));
-      scratch_n_ = count;
-    }
-    uint64_t* tmp = scratch_;
-    for (int r = 0; r < hub_->n; ++r) {
-      const uint64_t* src = static_cast<const uint64_t*>(hub_->ptrs[r]) + (size_t)rank_ * count;
-      if (!count) break;
-      if (r == 0) {
-        WC_HIP_CHECK(hipMemcpyAsync(recv, src, count * 8, hipMemcpyDefault, s));
-      } else {
-        WC_HIP_CHECK(hipMemcpyAsync(tmp, src, count * 8, hipMemcpyDefault, s));
-        launch_combine_u64(recv, tmp, count, (int)op, s);
-      }
-    }
-    WC_HIP_CHECK(hipStreamSynchronize(s));
-    hub_->wait_all();
+    LbMeta& m = begin();
+    m.send = reinterpret_cast<uint64_t>(send);
+    m.recv = reinterpret_cast<uint64_t>(recv);
+    enqueue(LB_REDUCE_SCATTER, count, (uint32_t)op, 0, s);
   }
   void alltoallv(const void* send, const size_t* send_off, const size_t* /*send_bytes*/, void* recv,
                  const size_t* recv_off, const size_t* recv_bytes, hipStream_t s) override {
     tick(rank_);
-    WC_HIP_CHECK(hipStreamSynchronize(s));
-    hub_->ptrs[rank_] = send;
-    hub_->offs[rank_] = send_off;
-    hub_->wait_all();
-    for (int r = 0; r < hub_->n; ++r)
-      if (recv_bytes[r])
-        WC_HIP_CHECK(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[r],
-                                    static_cast<const uint8_t*>(hub_->ptrs[r]) + hub_->offs[r][rank_], recv_bytes[r],
-                                    hipMemcpyDefault, s));
-    WC_HIP_CHECK(hipStreamSynchronize(s));
-    hub_->wait_all();
+    LbMeta& m = begin();
+    m.send = reinterpret_cast<uint64_t>(send);
+    m.recv = reinterpret_cast<uint64_t>(recv);
+    for (int p = 0; p < hub_->n; ++p) {
+      m.soff[p] = send_off[p];
+      m.roff[p] = recv_off[p];
+      m.rbytes[p] = recv_bytes[p];
+    }
+    enqueue(LB_ALLTOALLV, 0, 0, 0, s);
   }
   void broadcast(void* buf, size_t bytes, int root, hipStream_t s) override {
     tick(rank_);
-    WC_HIP_CHECK(hipStreamSynchronize(s));
-    if (rank_ == root) hub_->ptrs[root] = buf;
-    hub_->wait_all();
-    if (rank_ != root && bytes) WC_HIP_CHECK(hipMemcpyAsync(buf, hub_->ptrs[root], bytes, hipMemcpyDefault, s));
-    WC_HIP_CHECK(hipStreamSynchronize(s));
-    hub_->wait_all();
+    LbMeta& m = begin();
+    m.send = reinterpret_cast<uint64_t>(buf);
+    m.recv = reinterpret_cast<uint64_t>(buf);
+    enqueue(LB_BROADCAST, bytes, 0, (uint32_t)root, s);
   }
   void barrier(hipStream_t s) override {
     tick(rank_);
-    WC_HIP_CHECK(hipStreamSynchronize(s));
-    hub_->wait_all();
+    begin();
+    enqueue(~0u, 0, 0, 0, s);  // events only
+    sync(s);
+  }
+  // Watchdog wait, as RcclComm::sync (a failed peer is reported).
+  void sync(hipStream_t s) override {
+    if (failed()) fail("communicator failed earlier: " + failed_);
+    count_host_wait();
+    const double t0 = now_seconds();
+    for (;;) {
+      const hipError_t q = hipStreamQuery(s);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) WC_HIP_CHECK(q);
+      if (now_seconds() - t0 > timeout_s()) {
+        const std::string why = "loopback collective made no progress for " + std::to_string((int)timeout_s()) +
+                                " s (WC_COMM_TIMEOUT_S)";
+        abort(why);
+        fail(why + " on rank " + std::to_string(rank_));
+      }
+      std::this_thread::yield();
+    }
+    if (hub_->is_aborted()) fail("loopback peer failed: " + hub_->why);
   }
 
  private:
+  // Next sequence number and this rank's metadata slot for it (reused
+  // LB_RING collectives later: every rank has enqueued that collective's
+  // waits by then, and the metadata is read by kernels queued before ours).
+  LbMeta& begin() {
+    seq_ = (uint32_t)(seq_ + 1);
+    slot_ = seq_ % LB_RING;
+    return hub_->sh->meta[slot_ * hub_->n + rank_];
+  }
+  void enqueue(uint32_t kind, uint64_t count, uint32_t op, uint32_t root, hipStream_t s) {
+    Hub& h = *hub_;
+    const size_t base = (size_t)slot_ * h.n;
+    WC_HIP_CHECK(hipEventRecord(h.ready[base + rank_], s));
+    h.arrive();  // every peer's metadata is written and its ready event recorded
+    for (int p = 0; p < h.n; ++p)
+      if (p != rank_) WC_HIP_CHECK(hipStreamWaitEvent(s, h.ready[base + p], 0));
+    if (kind != ~0u) launch_loopback_xfer(LbXfer{h.sh, kind, (uint32_t)h.n, (uint32_t)rank_, slot_, op, root, count}, s);
+    WC_HIP_CHECK(hipEventRecord(h.done[base + rank_], s));
+    h.arrive();  // every peer's done event recorded
+    for (int p = 0; p < h.n; ++p)
+      if (p != rank_) WC_HIP_CHECK(hipStreamWaitEvent(s, h.done[base + p], 0));
+  }
   std::shared_ptr<Hub> hub_;
   int rank_;
-  uint64_t* scratch_ = nullptr;  // reduce-scatter staging (device of this rank)
-  size_t scratch_n_ = 0;
+  uint32_t seq_ = 0, slot_ = 0;
 };
 
 }  // namespace

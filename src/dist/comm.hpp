@@ -50,6 +50,11 @@ class Comm {
   virtual void abort(const std::string& why) { failed_ = why.empty() ? "aborted" : why; }
   bool failed() const { return !failed_.empty(); }
   double timeout_s() const { return timeout_s_; }
+  // Process-wide counters (tests): collectives enqueued, and host waits of
+  // the communicators (sync(); barrier() waits through it) — a merge's host
+  // waits must not grow with its collective count.
+  static uint64_t collectives_total();
+  static uint64_t host_waits_total();
 
  protected:
   Comm();
@@ -58,6 +63,7 @@ class Comm {
   // rank <rank> fail its n-th collective (default 1st) as a simulated comm
   // failure, for tests of the failure path.
   void tick(int rank);
+  static void count_host_wait();
   std::string failed_;
 
  private:
@@ -72,7 +78,9 @@ std::string rccl_unique_id();
 std::unique_ptr<Comm> make_rccl_comm(const std::string& unique_id, int rank, int size, int device);
 std::vector<std::unique_ptr<Comm>> make_rccl_comms_all(const std::vector<int>& devices);
 
-// In-process virtual ranks (call each rank's methods from its own thread).
+// In-process virtual ranks (call each rank's methods from its own thread;
+// every rank's stream on one device, or on devices with peer access enabled:
+// the transfer kernel reads the peers' buffers directly).
 std::vector<std::unique_ptr<Comm>> make_loopback_comms(int n);
 
 }  // namespace wc

@@ -51,8 +51,9 @@ uint64_t* host_words(Engine::Impl& im) {
 
 // Small-vocabulary variant of the shuffle merge (see merge_cols_owner):
 // pack all local rows (one "owner"), send them to rank 0, merge there.
-// `cursor`: 2 zeroed device words (the owner plan's unused scatter cursor), so
-// the one-owner pack needs no memset launch of its own.
+// `cursor`: 4 zeroed device words (the owner plan's unused scatter cursor
+// region, >= 4 words), so the one-owner pack needs no memset launch of its own:
+// words 0-1 are the scatter cursor, words 2-3 its (zero) owner counts.
 void merge_to_root(Engine::Impl& im, Comm& comm, const std::vector<uint64_t>& rank_rows,
                    const std::vector<uint64_t>& rank_bytes, uint64_t gmax_end, unsigned long long* cursor) {
   Range rg("wc_merge_root");
@@ -91,7 +92,7 @@ void merge_to_root(Engine::Impl& im, Comm& comm, const std::vector<uint64_t>& ra
   uint8_t* recv_bytes = take_aligned<uint8_t>(A, rbt);
   // one owner: the scatter reads no owner count before its own (base 0)
   launch_owner_scatter(im.cols.k0, im.cols.k1, im.cols.cnt, im.cols.first, im.cols.sref_off, im.cols.sref_len,
-                       im.cols_arena, n, 1u, cursor, cursor, send_rows, send_bytes, nullptr, s);
+                       im.cols_arena, n, 1u, cursor + 2, cursor, send_rows, send_bytes, nullptr, s);
   comm.group_begin();
   comm.alltoallv(send_rows, zs.data(), sr.data(), recv_rows, ro_r.data(), rb_r.data(), s);
   comm.alltoallv(send_bytes, zs.data(), sb.data(), recv_bytes, ro_b.data(), rb_b.data(), s);
@@ -153,7 +154,8 @@ struct OwnerPlan {
   size_t C = 0;
   std::vector<unsigned long long> all;  // W x C
   uint64_t gmax_end = 0;
-  bool any_flags = false;
+  bool any_flags = false;   // some rank's last pass needs recovery (all ranks redo)
+  bool any_arena = false;   // some rank's key arena overflowed (all ranks fail)
   std::vector<uint64_t> rank_rows, rank_bytes;
   uint64_t total_rows = 0, Gmax = 0, GBmax = 0;  // rows / bytes of all ranks (bounds of the merged table)
   std::vector<size_t> so_r, sb_r, so_b, sb_b, ro_r, rb_r, ro_b, rb_b;  // byte offsets / sizes
@@ -198,7 +200,9 @@ void plan_finish(OwnerPlan& P) {
   P.rank_bytes.assign(W, 0);
   for (int r = 0; r < W; ++r) {
     P.gmax_end = std::max<uint64_t>(P.gmax_end, P.all[(size_t)r * C + 2 * W]);
-    if (P.all[(size_t)r * C + 2 * W + 1]) P.any_flags = true;
+    const unsigned long long f = P.all[(size_t)r * C + 2 * W + 1];
+    if (f) P.any_flags = true;
+    if (f & 2) P.any_arena = true;
     for (int p = 0; p < W; ++p) {
       P.rank_rows[r] += P.all[(size_t)r * C + 2 * p];
       P.rank_bytes[r] += P.all[(size_t)r * C + 2 * p + 1];
@@ -515,9 +519,13 @@ bool merge_cols_speculative(Engine::Impl& im, Comm& comm, bool all_ranks) {
     }
     __builtin_ia32_pause();
   }
-  const bool clean = im.complete_pass(p.text, p.len, p.avail, p.base, p.prev, p.rb, p.blocks, true);
   P.all.assign(hp, hp + words);
   plan_finish(P);
+  // a rank whose key arena overflowed would throw in complete_pass while the
+  // others entered the recovery's collectives: every rank fails here instead
+  if (P.any_arena)
+    fail("key arena exhausted on a rank (" + std::to_string(im.opt.arena_bytes) + " bytes each); raise arena_bytes");
+  const bool clean = im.complete_pass(p.text, p.len, p.avail, p.base, p.prev, p.rb, p.blocks, true);
   if (!clean || P.any_flags) return false;  // every rank sees the same flags: all redo
   im.cols.n = hp[words];
   WC_CHECK(im.cols.n == P.rank_rows[P.R], "speculative compaction: key count != owner row counts");

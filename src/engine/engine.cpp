@@ -59,6 +59,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   WC_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   WC_HIP_CHECK(hipStreamCreateWithFlags(&copy_s, hipStreamNonBlocking));
   n_cu = (uint32_t)device_cu_count(dev);
+  numa = numa_of_device(dev);
   map_blocks = opt.map_blocks ? opt.map_blocks : MAP_BLOCKS_PER_CU * n_cu;
   map_blocks = std::min<uint32_t>(map_blocks, RED_MAX_RUNS);
   if (const char* e = std::getenv("WC_SYNC_DEBUG")) sync_debug = std::atoi(e) != 0;
@@ -112,9 +113,9 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   rec_total = std::min<uint64_t>(rec_total, 0xFFFFFFFFull);  // record indices are 32-bit in the reducer
   // record store + per-(block, bucket) counts; partitions follow the table up to the max
   const size_t ncount = (size_t)map_blocks * MAX_REC_BUCKETS;
-  rec_mem.reserve(rec_total * (sizeof(Rec) + sizeof(Rec12)) + ncount * 4 + 8192);
+  rec_mem.reserve(rec_total * (sizeof(Rec) + sizeof(Rec16)) + ncount * 4 + 8192);
   rec.recs = rec_mem.take_n<Rec>(rec_total);
-  rec.recs12 = rec_mem.take_n<Rec12>(rec_total);
+  rec.recs16 = rec_mem.take_n<Rec16>(rec_total);
   rec.cap = rec_total;
   rec.count = rec_mem.take_n<uint32_t>(ncount);
 
@@ -254,6 +255,7 @@ void Engine::Impl::ensure_staging(uint64_t chunk) {
   d_stage[1] = static_cast<uint8_t*>(stage_mem.take(per));
   stage_cap = chunk;
   pinned.clear();
+  ScopedAffinity bind(numa.cpus);  // the staging ring's pages on the GPU's node
   const uint32_t nring = std::max<uint32_t>(2, opt.staging_buffers);
   for (uint32_t i = 0; i < nring; ++i) pinned.emplace_back(chunk);
 }
@@ -908,6 +910,7 @@ void Engine::count_source(ChunkSource& src, uint64_t global_base) {
   const uint64_t C = std::min(im.opt.chunk_bytes, std::max<uint64_t>(1ull << 20, stream / 256 * 256));
   im.ensure_staging(C);
   im.copy_used = true;
+  ScopedAffinity bind(im.numa.cpus);  // the source's reader threads (they inherit the mask) on the GPU's node
   std::vector<uint8_t> carry;
   bool eof = false;
   uint64_t offset = global_base;
@@ -1176,9 +1179,15 @@ KeyTable Engine::result(Comm* comm, bool all_ranks) {
 }  // namespace wc
 
 namespace wc {
-HostPool::HostPool(uint64_t n, uint64_t first_segment, const SynthSpec& spec, int threads) : n_(n) {
+HostPool::HostPool(uint64_t n, uint64_t first_segment, const SynthSpec& spec, int threads, int device) : n_(n) {
   const double t0 = now_seconds();
-  WC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_), std::max<uint64_t>(n, 1), hipHostMallocDefault));
+  // bound to the GPU's node: the page-locked pages (placed at allocation by the
+  // local-node policy) and the generator threads (they inherit the mask)
+  const NumaNode nn = device >= 0 ? numa_of_device(device) : NumaNode{};
+  ScopedAffinity bind(nn.cpus);
+  node_ = bind.active() ? nn.node : -1;
+  WC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_), std::max<uint64_t>(n, 1),
+                             bind.active() ? hipHostMallocNumaUser : hipHostMallocDefault));
   synth_host_into(p_, n, first_segment, spec, build_vocab(spec), threads);
   secs_ = now_seconds() - t0;
 }

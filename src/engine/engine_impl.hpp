@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "../common/hip_util.hpp"
+#include "../io/numa.hpp"
 #include "../io/synth_host.hpp"
 #include "../kernels/kernels.hpp"
 #include "../kernels/keys.hpp"
@@ -185,6 +186,7 @@ struct Engine::Impl {
   // its own partition) up to MAX_REC_BUCKETS.
   uint32_t rec_shift = 0;  // WC_REC_SHIFT (sweeps only): shuffle partitions = table buckets >> shift
   uint32_t n_cu = 0;         // compute units: reduce blocks per pass
+  NumaNode numa;             // the GPU's host NUMA node: pinned staging + reader threads bound there
   uint32_t red_q_force = 0;  // WC_RED_Q (sweeps only): reduce blocks per bucket
   uint32_t part_blocks = 0;  // split-reduce partial tables allocated
   ReduceArgs::Parts part{};

@@ -45,28 +45,32 @@ enum : int { FLAG_REGION_OVF = 0, FLAG_ARENA_OVF = 1, FLAG_TABLE_OVF = 2, FLAG_M
 struct Rec {
   uint64_t k0, k1, co;
 };
-// One occurrence of a short word (k1 = length <= 8) whose last byte is nonzero,
-// so k0 implies the length (keys.hpp implied_len): 12 bytes, count 1.  Every
-// other record — counted hot-slot flushes included — is a 24-byte Rec.
-struct Rec12 {
-  uint32_t lo, hi, off;  // k0 = lo | hi << 32; chunk-relative offset
+// One occurrence of an inline word of <= 12 bytes whose last byte is nonzero:
+// 16 bytes, count 1, one aligned dwordx4.  k0 = lo | hi << 32 (the first 8
+// bytes), t = bytes [8, 12) zero-padded; the length is implied by the highest
+// nonzero byte (of t if t != 0, else of k0: keys.hpp implied_len), so
+// k1 = t ? t | len << 56 : len.  Every other record — counted hot-slot
+// flushes, 13..15-byte and LONG words included — is a 24-byte Rec.
+struct Rec16 {
+  uint32_t lo, hi, t, off;  // off: chunk-relative offset
 };
+static_assert(sizeof(Rec16) == 16, "Rec16 layout");
 
-// Shuffle output.  Two record stores (single short-word occurrences as 12-B
-// Rec12, everything else as 24-B Rec), each split into one sub-region of
+// Shuffle output.  Two record stores (single occurrences of <= 12-byte words as
+// 16-B Rec16, everything else as 24-B Rec), each split into one sub-region of
 // `subcap` records per (map block p, shuffle bucket b):
-//   recs12[(p * nb + b) * subcap + i],  i < count[p * nb + b] & 0xFFFF
+//   recs16[(p * nb + b) * subcap + i],  i < count[p * nb + b] & 0xFFFF
 //   recs  [(p * nb + b) * subcap + i],  i < count[p * nb + b] >> 16
-// A map flush appends each emitted slot to its bucket's sub-region through a
-// per-bucket LDS cursor (no histogram, no scan, no directory); the reducer of
-// bucket b reads one contiguous run per map block.  A full sub-region sets
-// FLAG_REGION_OVF and the host re-runs the chunk in halves.
+// The map appends records to its bucket's sub-region through a per-bucket LDS
+// cursor (no histogram, no scan, no directory) and the reducer of bucket b
+// reads one contiguous run per map block.  A full sub-region sets FLAG_REGION_OVF and
+// the host re-runs the chunk in halves.
 struct Records {
   Rec* recs;                   // 24-byte records
-  Rec12* recs12;               // single short-word occurrences
+  Rec16* recs16;               // single occurrences of <= 12-byte words
   unsigned long long* cursor;  // records emitted (stats)
   uint64_t cap;                // record capacity of each store
-  uint32_t* count;             // [map_blocks * nb] Rec12 (low 16 bits) | Rec (high 16) records appended
+  uint32_t* count;             // [map_blocks * nb] Rec16 (low 16 bits) | Rec (high 16) records appended
   uint32_t subcap;             // records per sub-region, <= 65535 (cap / (map_blocks * nb) of the pass)
 };
 
@@ -281,6 +285,7 @@ void launch_iota_u32(uint32_t* v, uint64_t n, hipStream_t s);
 // from page-locked memory into device buffers) / copy several small device
 // regions into page-locked host memory, one launch each (sizes in 32-bit words).
 constexpr int ZERO_MAX_REGIONS = 8, ZERO_MAX_COPIES = 4, PUB_MAX_REGIONS = 4;
+[[noreturn]] void launch_list_overflow(const char* what);  // util.hip: fails the job (a caller bug)
 struct ZeroList {
   uint32_t* ptr[ZERO_MAX_REGIONS];
   uint64_t words[ZERO_MAX_REGIONS];
@@ -291,11 +296,13 @@ struct ZeroList {
   uint32_t cwords[ZERO_MAX_COPIES];
   int nc;
   void add(void* p, uint64_t bytes, uint32_t pattern = 0) {
+    if (n >= ZERO_MAX_REGIONS) launch_list_overflow("ZeroList: more than ZERO_MAX_REGIONS fills");
     ptr[n] = static_cast<uint32_t*>(p);
     val[n] = pattern;
     words[n++] = bytes / 4;
   }
   void copy(void* dst, const void* src, uint64_t bytes) {
+    if (nc >= ZERO_MAX_COPIES) launch_list_overflow("ZeroList: more than ZERO_MAX_COPIES copies");
     cdst[nc] = static_cast<uint32_t*>(dst);
     csrc[nc] = static_cast<const uint32_t*>(src);
     cwords[nc++] = (uint32_t)(bytes / 4);
@@ -309,6 +316,7 @@ struct PubList {
   uint32_t* seq_dst;  // nullable: written last (system-scope release) with seq, for a host spin-wait
   uint32_t seq;
   void add(void* host_dst, const void* dev_src, uint64_t bytes) {
+    if (n >= PUB_MAX_REGIONS) launch_list_overflow("PubList: more than PUB_MAX_REGIONS regions");
     dst[n] = static_cast<uint32_t*>(host_dst);
     src[n] = static_cast<const uint32_t*>(dev_src);
     words[n++] = (uint32_t)(bytes / 4);
@@ -352,11 +360,30 @@ void launch_mrow_compact(const MRow* rows, const uint32_t* state, const unsigned
 void launch_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rbase, const uint64_t* bbase, uint32_t W,
                          uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first, uint64_t* soff, uint32_t* slen,
                          hipStream_t s, const uint64_t* dn = nullptr);  // dn: device-side row count (n a bound)
-void launch_combine_u64(uint64_t* dst, const uint64_t* src, uint64_t n, int op, hipStream_t s);  // 0 sum 1 min 2 max
 void launch_row_ids(const uint32_t* row_slot, const uint32_t* slot_id, uint64_t R, const unsigned long long* owns,
                     uint32_t rank, uint32_t* ids, hipStream_t s);  // owns: all-gathered (rows, bytes) per owner
 void launch_scatter_ids(const uint32_t* send_pos, const uint32_t* ids_back, const uint64_t* seg,
                         const unsigned long long* owns, uint32_t W, const uint64_t* cnt, const uint64_t* first,
                         uint64_t n, uint64_t* dcnt, uint64_t* dfirst, hipStream_t s);  // ids_back: owner-local
+
+// ---- stream-ordered loopback communicator (src/kernels/comm.hip, dist/comm.cpp) ----
+constexpr int LB_MAX_RANKS = 64, LB_RING = 16, LB_XFER_PARTS = 64;
+enum : uint32_t { LB_ALLGATHER = 0, LB_ALLTOALLV = 1, LB_BROADCAST = 2, LB_REDUCE_SCATTER = 3 };
+struct LbMeta {  // one rank's buffers for one collective (page-locked; read by the peers' transfer kernels)
+  uint64_t send, recv;
+  uint64_t soff[LB_MAX_RANKS];    // alltoallv: where this rank's bytes for rank q start in `send`
+  uint64_t roff[LB_MAX_RANKS];    // alltoallv: where rank q's bytes land in `recv`
+  uint64_t rbytes[LB_MAX_RANKS];  // alltoallv: bytes received from rank q
+};
+struct LbShared {  // page-locked, shared by the ranks of one loopback group
+  uint32_t aborted;                     // a rank failed: queued transfers skip their copies
+  LbMeta meta[LB_RING * LB_MAX_RANKS];  // [slot * world + rank]
+};
+struct LbXfer {
+  const LbShared* shared;
+  uint32_t kind, world, rank, slot, op, root;
+  uint64_t count;  // allgather / broadcast: bytes per rank; reduce-scatter: u64 elements per rank
+};
+void launch_loopback_xfer(const LbXfer& x, hipStream_t s);
 
 }  // namespace wc

@@ -96,6 +96,17 @@ WC_HD uint32_t place_hash(uint64_t k0, uint64_t k1) {
 // Length of a short word implied by its k0: bytes up to the highest nonzero one
 // (0 for k0 = 0).  Equals the length iff the word's last byte is not 0x00.
 WC_HD uint32_t implied_len(uint64_t k0) { return k0 ? (71u - (uint32_t)__builtin_clzll(k0)) >> 3 : 0u; }
+// k1 of a 16-byte single-occurrence record (kernels.hpp Rec16): t = the word's
+// bytes [8, 12) zero-padded, 0 for a word of <= 8 bytes; the length is implied
+// by the highest nonzero byte (the record holds words whose last byte is not 0).
+WC_HD uint64_t rec16_k1(uint64_t k0, uint32_t t) {
+  return t ? medium_k1(t, 9u + ((31u - (uint32_t)__builtin_clz(t)) >> 3)) : implied_len(k0);
+}
+
+// Merge owner of a key among W ranks: the high bits of its placement hash
+// (bucket bits are the low ones), dist/merge.cpp and its Python mirror
+// (cuda_mapreduce_amd/parallel/dist.py _owner).
+WC_HD uint32_t owner_of(uint32_t ph, uint32_t W) { return (uint32_t)(((uint64_t)ph * W) >> 32); }
 
 // Nested: the bucket under 2B buckets is b or b + B for bucket b under B.
 WC_HD uint32_t bucket_of(uint32_t ph, uint32_t log2_buckets) { return ph & ((1u << log2_buckets) - 1u); }

@@ -15,8 +15,9 @@
 //                 contiguous range of 2 KiB text units.  The block selects
 //                 the HOT_K most frequent candidates and places them in a
 //                 2-choice table of 2-slot groups in its LDS (4096 slots of
-//                 64-bit signatures + side words; blocks need not agree:
-//                 each flushes its slots with full keys).  Each wave grabs its
+//                 64-bit signatures, a two-word word's side word in its
+//                 group's second slot; blocks need not agree: each flushes
+//                 its slots with full keys).  Each wave grabs its
 //                 next unit from an LDS cursor and prefetches it into registers (32 B per lane) while
 //                 tokenizing the current one from its private LDS copy:
 //                 SWAR delimiter masks -> token starts `~d & (d << 1 | c)` ->
@@ -34,13 +35,17 @@
 //                 counted hot slot as one record.
 //
 // Signatures: a word of <= 7 bytes is its own 64-bit signature (bytes | len
-// << 56, one compare); 8..15-byte words use len << 56 | low 7 bytes of
-// (k0 ^ tail) plus k0 in `side`.  LONG words of 16..64 bytes are hot-table
-// words too (0xFF << 56 | a key hash, `side` = the length | the candidate's
-// index << 32): a hit needs the token's bytes to equal the candidate's 64-byte
-// copy of the word, so exactness
-// never rests on the hash; every other LONG token is a record whose bytes the
-// reducer compares.
+// << 56, one compare) and takes one slot of a 2-slot group; 8..15-byte words
+// use len << 56 | low 7 bytes of (k0 ^ tail) and take a WHOLE group: the
+// signature in its first slot, k0 (the `side` word) in the second, so the
+// token's one 16-byte probe read confirms it.  LONG words of 16..64 bytes are
+// hot-table words too (0xFF << 56 | a key hash; side = the length | the
+// candidate's index << 32): a hit needs the token's bytes to equal the
+// candidate's 64-byte copy of the word, so exactness never rests on the hash;
+// every other LONG token is a record whose bytes the reducer compares.  A
+// side word never equals a short signature (a short signature's top byte is
+// its length 1..7; two-word words whose k0 has a top byte < 8 are not placed).
+
 #include <type_traits>
 
 #include "map_common.hpp"
@@ -510,16 +515,31 @@ static_assert(HOT_PARTS * HOT_PART_TOP == 1024 * CAND_PER_THREAD && HOT_PART_TOP
               "select: whole candidate rows per thread group");
 static_assert(MAP_THREADS == 1024, "select: one map block of 1024 threads");
 
-// One word into an LDS table image (2-choice: the emptier group, else the
-// other; both full: the word stays out).
-__device__ __forceinline__ void place_hot(uint64_t* isig, uint64_t* iside, uint32_t* gocc, uint64_t sg, uint64_t sd) {
+// One word into an LDS table image.  A one-slot word (<= 7 bytes): 2-choice,
+// the emptier group, else the other.  A two-word or LONG word: a whole empty
+// group (g1, else g2), signature in its first slot and side word in its second
+// (a two-word word whose side word k0 has a top byte < 8 could equal a short
+// signature: it stays out).  Both choices full: the word stays out.
+__device__ __forceinline__ void place_hot(uint64_t* isig, uint32_t* gocc, uint64_t sg, uint64_t sd) {
   uint32_t g1, g2;
-  if (is_long_sig(sg)) {
+  const bool lng = is_long_sig(sg);
+  if (lng) {
     hot_groups(long_group_hash(sg), g1, g2);
   } else {
     uint64_t k0, k1;
     sig_key(sg, sd, k0, k1);
     hot_groups(place_hash(k0, k1), g1, g2);
+  }
+  if (lng || two_word(sg)) {
+    if (!lng && (sd >> 59) == 0) return;
+    uint32_t g = g1;
+    if (atomicCAS(&gocc[g1], 0u, 2u) != 0u) {
+      g = g2;
+      if (atomicCAS(&gocc[g2], 0u, 2u) != 0u) return;
+    }
+    isig[2 * g] = sg;
+    isig[2 * g + 1] = sd;
+    return;
   }
   if (gocc[g2] < gocc[g1]) {
     const uint32_t x = g1;
@@ -532,18 +552,16 @@ __device__ __forceinline__ void place_hot(uint64_t* isig, uint64_t* iside, uint3
     o = atomicAdd(&gocc[g2], 1u);
   }
   if (o >= GS) return;
-  const uint32_t slot = slot_of(g, o);
-  isig[slot] = sg;
-  iside[slot] = sd;
+  isig[slot_of(g, o)] = sg;
 }
 
 // A map block's table image from the candidates (the block's prologue): the
 // HOT_K most frequent (threshold over every partition's candidates, ties while
-// room remains), placed tier by tier into the LDS image isig / iside (cleared
-// by the caller).  Each thread holds CAND_PER_THREAD candidates in registers:
+// room remains), placed tier by tier into the LDS image isig (cleared by the
+// caller).  Each thread holds CAND_PER_THREAD candidates in registers:
 // two dependent global steps (counts, then the taken candidates' keys).
 // scratch: >= SEL_BINS + 20 words, gocc: NG words (LDS the main loop reuses).
-__device__ void build_image(const HotArgs& h, uint64_t* isig, uint64_t* iside, uint32_t* scratch, uint32_t* gocc) {
+__device__ void build_image(const HotArgs& h, uint64_t* isig, uint32_t* scratch, uint32_t* gocc) {
   const int tid = threadIdx.x;
   uint32_t* hist = scratch;
   uint32_t* sc = scratch + SEL_BINS;  // 18 words + the tie counter
@@ -588,7 +606,7 @@ __device__ void build_image(const HotArgs& h, uint64_t* isig, uint64_t* iside, u
       const uint32_t cc = min(c[i], (uint32_t)SEL_BINS - 1);
       const int tier = cc >= big ? 0 : (cc >= mid ? 1 : 2);
       if (tier != (pass == HOT_PLACE_PASSES - 1 ? 2 : pass)) continue;
-      place_hot(isig, iside, gocc, sg[i], sd[i]);
+      place_hot(isig, gocc, sg[i], sd[i]);
     }
     __syncthreads();
   }
@@ -602,14 +620,14 @@ struct alignas(16) MapLds {
   uint32_t cnt[MAP_SLOTS];
   uint32_t off[MAP_SLOTS];              // chunk-relative first offset in the block
   alignas(16) uint64_t sig[MAP_SLOTS];  // hot table image (read-only while tokens stream); 0 = empty
-  uint64_t side[MAP_SLOTS];             // k0 of two-word signatures
   uint16_t list[MAP_WAVES][MAP_LIST];
-  uint32_t bcur[MAX_REC_BUCKETS];       // records appended to each bucket's sub-region (short | long << 16)
+  uint32_t bcur[MAX_REC_BUCKETS];       // records appended to each bucket's sub-region (Rec16 | Rec << 16)
   alignas(16) uint8_t buf[MAP_WAVES][BUF];
   uint32_t next_unit;
   unsigned long long used, tokens;
 };
 static_assert(sizeof(MapLds) + 8 * MAP_STAMP_N <= 160 * 1024, "one map block per CU");
+static_assert(GS == 2, "pair-packed two-word words: 2-slot groups");
 
 // Index (0..3) of the first of a key's four candidate signatures equal to sig, else -1.
 __device__ __forceinline__ int sig_match4(const u64x2& a, const u64x2& b, uint64_t sig) {
@@ -617,12 +635,13 @@ __device__ __forceinline__ int sig_match4(const u64x2& a, const u64x2& b, uint64
   return (int)__ffs(m) - 1;
 }
 
-// Index (0..7) of the first of a key's eight candidate signatures equal to sig, else -1.
-__device__ __forceinline__ int sig_match8(const u64x2& a, const u64x2& b, const u64x2& c, const u64x2& d,
-                                          uint64_t sig) {
-  const uint32_t m = (a.x == sig ? 1u : 0u) | (a.y == sig ? 2u : 0u) | (b.x == sig ? 4u : 0u) |
-                     (b.y == sig ? 8u : 0u) | (c.x == sig ? 16u : 0u) | (c.y == sig ? 32u : 0u) |
-                     (d.x == sig ? 64u : 0u) | (d.y == sig ? 128u : 0u);
+// Hot-table match of an inline token (signature sig, k0) against its two
+// candidate groups: a one-slot word (sig's top byte < 8) in any of the four
+// slots; a two-word word only in a group's first slot with k0 in the second.
+// Returns the slot index 0..3 as sig_match4, or -1.
+__device__ __forceinline__ int inline_match(const u64x2& a, const u64x2& b, uint64_t sig, uint64_t k0) {
+  if (!two_word(sig)) return sig_match4(a, b, sig);
+  const uint32_t m = (a.x == sig && a.y == k0 ? 1u : 0u) | (b.x == sig && b.y == k0 ? 4u : 0u);
   return (int)__ffs(m) - 1;
 }
 
@@ -636,7 +655,6 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   for (int j = 0; j < SPT; ++j) {
     const int s = tid + j * MAP_THREADS;
     L.sig[s] = 0;
-    L.side[s] = 0;
     L.cnt[s] = 0;
     L.off[s] = 0xFFFFFFFFu;
   }
@@ -644,7 +662,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   // the table image, built in this block's LDS (the unit buffers and token
   // lists are its scratch until the first unit)
   static_assert(sizeof(L.buf) >= 4 * (SEL_BINS + 20) && sizeof(L.list) >= 4 * NG, "image scratch");
-  build_image(h, L.sig, L.side, reinterpret_cast<uint32_t*>(&L.buf[0][0]), reinterpret_cast<uint32_t*>(&L.list[0][0]));
+  build_image(h, L.sig, reinterpret_cast<uint32_t*>(&L.buf[0][0]), reinterpret_cast<uint32_t*>(&L.list[0][0]));
   uint64_t u_begin, u_end;
   unit_range(a.chunk_len, gridDim.x, blockIdx.x, u_begin, u_end);
   if (tid == 0) {
@@ -654,6 +672,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   __syncthreads();
 
   const uint32_t bmask = (1u << a.log2_rec_buckets) - 1u;
+  const uint32_t nb = 1u << a.log2_rec_buckets;
   const RecOut rout = rec_out(a);
   uint8_t* buf = L.buf[wave];
   uint16_t* list = L.list[wave];
@@ -696,18 +715,21 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
         uint32_t len = n;
         if (n < MAP_LONG) key_long_known(buf, q, n, a.k1_mask, k0, k1);  // 16..30 bytes: length known
         else len = (uint32_t)min<uint64_t>(key_long_scan(buf, UNIT + HALO, a, q, u0 + q, k0, k1), 0xFFFFFFFFull);
-        // a hot LONG word: signature candidates, then the bytes against the slot's copy
+        // a hot LONG word: the signature in a group's first slot, then the
+        // length and the bytes against the candidate's copy (side word = the
+        // length | the candidate index << 32, in the group's second slot)
         int slot = -1;
         if (len <= HOT_LONG_MAX) {
           const uint64_t sg = long_signature(k0, k1);
           uint32_t g1, g2;
           hot_groups(long_group_hash(sg), g1, g2);
           const u64x2* S = reinterpret_cast<const u64x2*>(L.sig);
-          const int m = sig_match4(S[g1], S[g2], sg);
-          if (m >= 0) {
-            const int sl = (int)slot_of(m < GS ? g1 : g2, m & (GS - 1));
-            const uint64_t sd = L.side[sl];  // length | candidate index << 32
-            if ((uint32_t)sd == len && long_line_equal(buf, q, h.long_bytes + (sd >> 32) * 64, len)) slot = sl;
+          const u64x2 x1 = S[g1], x2 = S[g2];
+          const bool m1 = x1.x == sg, m2 = x2.x == sg;
+          if (m1 || m2) {
+            const uint64_t sd = m1 ? x1.y : x2.y;
+            if ((uint32_t)sd == len && long_line_equal(buf, q, h.long_bytes + (sd >> 32) * 64, len))
+              slot = (int)(2 * (m1 ? g1 : g2));
           }
         }
         if (slot >= 0) {
@@ -749,8 +771,8 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     static_assert(MAP_LONG == 31, "list entries: 11 position bits + 5 length bits");
     // One step: two list entries [j, hi) per lane, both probed in one LDS round
     // trip; a tail of <= 64 entries takes the one-entry step.  General form:
-    // any length (two-word signatures are confirmed by the slot's side word,
-    // LONG words deferred to the round end).
+    // any length (two-word signatures are confirmed by their group's side
+    // word, LONG words deferred to the round end).
     auto step = [&](uint32_t j, uint32_t hi, auto two_c) {
       constexpr bool TWO = decltype(two_c)::value;
       const bool h1 = j + lane < hi, h2 = TWO && j + 64 + lane < hi;
@@ -779,30 +801,16 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
       }
       const u64x2* S = reinterpret_cast<const u64x2*>(L.sig);
       int s1 = -1, s2 = -1;
-      if constexpr (GS == 2) {  // S[g]: both slots of group g
+      {  // S[g]: both slots of group g
         const u64x2 xa0 = S[ga1], xa1 = S[ga2];
         if (TWO) {
           const u64x2 xb0 = S[gb1], xb1 = S[gb2];
-          const int mb = in2 ? sig_match4(xb0, xb1, bs) : -1;
+          const int mb = in2 ? inline_match(xb0, xb1, bs, b0) : -1;
           s2 = mb < 0 ? -1 : (int)slot_of(mb < GS ? gb1 : gb2, mb & (GS - 1));
         }
-        const int ma = in1 ? sig_match4(xa0, xa1, as) : -1;
-        s1 = ma < 0 ? -1 : (int)slot_of(ma < GS ? ga1 : ga2, ma & (GS - 1));
-      } else {  // S[g]: slots 0-1, S[NG + g]: slots 2-3
-        const u64x2 xa0 = S[ga1], xa1 = S[NG + ga1], xa2 = S[ga2], xa3 = S[NG + ga2];
-        if (TWO) {
-          const u64x2 xb0 = S[gb1], xb1 = S[NG + gb1], xb2 = S[gb2], xb3 = S[NG + gb2];
-          const int mb = in2 ? sig_match8(xb0, xb1, xb2, xb3, bs) : -1;
-          s2 = mb < 0 ? -1 : (int)slot_of(mb < GS ? gb1 : gb2, mb & (GS - 1));
-        }
-        const int ma = in1 ? sig_match8(xa0, xa1, xa2, xa3, as) : -1;
+        const int ma = in1 ? inline_match(xa0, xa1, as, a0) : -1;
         s1 = ma < 0 ? -1 : (int)slot_of(ma < GS ? ga1 : ga2, ma & (GS - 1));
       }
-      // two-word keys: the matching slot's side word decides
-      const bool ta = two_word(as), tb = TWO && two_word(bs);
-      const uint64_t ca = s1 >= 0 && ta ? L.side[s1] : a0, cb = s2 >= 0 && tb ? L.side[s2] : b0;
-      if (ca != a0) s1 = -1;
-      if (cb != b0) s2 = -1;
       clk.lap(MS_PROBE);
       const uint32_t o1 = (uint32_t)(u0 + q1), o2 = (uint32_t)(u0 + q2);
       if (s1 >= 0) {
@@ -841,7 +849,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     };
     // Short step: entries of words of <= 7 bytes only — the signature IS the
     // key (bytes | len << 56): one 8-byte window (three LDS dwords, two
-    // funnels), no tail, no side-word confirmation, and every miss a 12-byte
+    // funnels), no tail, no side-word confirmation, and every miss a 16-byte
     // record candidate.  3 of 4 tokens of English-like text take it.
     auto step_short = [&](uint32_t j, uint32_t hi, auto two_c) {
       constexpr bool TWO = decltype(two_c)::value;
@@ -861,10 +869,9 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
       hot_groups(ha, ga1, ga2);
       if (TWO) hot_groups(hb, gb1, gb2);
       clk.lap(MS_KEYS);
-      static_assert(GS == 2, "short step: 2-slot groups");
       const u64x2* S = reinterpret_cast<const u64x2*>(L.sig);
       int s1 = -1, s2 = -1;
-      {
+      {  // a pair's side word never equals a short signature: plain 4-slot match
         const u64x2 xa0 = S[ga1], xa1 = S[ga2];
         if (TWO) {
           const u64x2 xb0 = S[gb1], xb1 = S[gb2];
@@ -962,7 +969,9 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   }
   __syncthreads();
   clk.lap(MS_WAIT);
-  // block end: every counted hot slot becomes one record of its bucket
+  // block end: every counted hot slot becomes one record of its bucket (a
+  // two-word or LONG word counts in its group's first slot; its side word is
+  // the second)
 #pragma unroll
   for (int j = 0; j < SPT; ++j) {
     const int s = tid + j * MAP_THREADS;
@@ -970,8 +979,9 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     if (!c) continue;
     uint64_t k0, k1;
     const uint64_t sg = L.sig[s];
-    if (is_long_sig(sg)) key_long_line(h.long_bytes + (L.side[s] >> 32) * 64, (uint32_t)L.side[s], a.k1_mask, k0, k1);
-    else sig_key(sg, L.side[s], k0, k1);
+    const uint64_t sd = (two_word(sg) || is_long_sig(sg)) ? L.sig[s | 1] : 0ull;
+    if (is_long_sig(sg)) key_long_line(h.long_bytes + (sd >> 32) * 64, (uint32_t)sd, a.k1_mask, k0, k1);
+    else sig_key(sg, sd, k0, k1);
     emit_record(L.bcur, a, rout, place_hash(k0, k1) & bmask, k0, k1, c, L.off[s]);
   }
   clk.lap(MS_FLUSH);
@@ -993,7 +1003,6 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   if (WC_MAP_ABLATE && sink == 0x9E3779B97F4A7C15ull) atomicOr(&a.flags[FLAG_COUNT - 1], 0u);  // never true
   // records of the block = the sum of its bucket cursors (no per-step counting)
   __syncthreads();  // every flush's cursor add is in
-  const uint32_t nb = 1u << a.log2_rec_buckets;
   uint64_t t = my_tokens, e = 0;
   for (uint32_t b = tid; b < nb; b += MAP_THREADS) {
     const uint32_t c = L.bcur[b];

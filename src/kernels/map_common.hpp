@@ -116,49 +116,64 @@ struct PhaseClock {
   }
 };
 
-// Profiling builds only (-DWC_EMIT_ABLATE=N, results NOT valid): 1 no record
-// stores, 2 no cursor atomics (lane-derived positions), 3 neither.
+// Profiling builds only (-DWC_EMIT_ABLATE=1, results NOT valid): no record
+// stores (staged or direct; the cursor atomics stay).
 #ifndef WC_EMIT_ABLATE
 #define WC_EMIT_ABLATE 0
 #endif
 
-// Record format of a key with count cnt: 12-byte Rec12 (single occurrence of a
-// short word whose last byte is nonzero, so keys.hpp implied_len(k0) == k1 —
-// inline keys have zero bytes past the length) or 24-byte Rec.
-__device__ __forceinline__ bool rec12_fits(uint64_t k0, uint64_t k1, uint64_t cnt) {
-  return cnt == 1 && k1 - 1 < 8 && ((k0 >> (8 * (k1 - 1))) & 0xFFu) != 0;
+// Record format of a key with count cnt: 16-byte Rec16 (one occurrence of a
+// word of <= 12 bytes whose last byte is nonzero, so keys.hpp implied_len of
+// k0 / of the tail word gives the length back — inline keys have zero bytes
+// past the length) or 24-byte Rec.
+__device__ __forceinline__ bool rec16_fits(uint64_t k0, uint64_t k1, uint64_t cnt) {
+  if (cnt != 1) return false;
+  if (k1 - 1 < 8) return ((k0 >> (8 * (k1 - 1))) & 0xFFu) != 0;
+  const uint64_t len = k1 >> 56;  // MEDIUM: 9..15; LONG: >= 0x80
+  return len - 9 < 4 && ((k1 >> (8 * (len - 9))) & 0xFFu) != 0;
+}
+
+// rec16_fits for one occurrence of an inline word of known length n (k1 its
+// MEDIUM key word when n > 8): n <= 8 with k0 >> 8 (n - 1) != 0, or 9..12
+// with the tail's byte n - 9 nonzero.  Shifts are masked, so n = 0 of an
+// empty lane is harmless.
+__device__ __forceinline__ bool rec16_inline(uint64_t k0, uint64_t k1, uint32_t n) {
+  if (n - 1u < 8u) return (k0 >> ((8u * n - 8u) & 63u)) != 0;
+  return n - 9u < 4u && ((uint32_t)k1 >> ((8u * n - 72u) & 31u)) != 0;
+}
+
+__device__ __forceinline__ Rec16 make_rec16(uint64_t k0, uint64_t k1, uint32_t off) {
+  return Rec16{(uint32_t)k0, (uint32_t)(k0 >> 32), k1 > 8 ? (uint32_t)k1 : 0u, off};
 }
 
 // This block's record sub-regions: bucket b's run starts at (b * sub) records
 // from the block base (b * sub < 2^25: 32-bit index math, full-rate multiply).
 struct RecOut {
-  Rec12* b12;
+  Rec16* b16;
   Rec* b24;
   uint32_t sub;
 };
 __device__ __forceinline__ RecOut rec_out(const MapArgs& a) {
   const uint64_t first = ((uint64_t)blockIdx.x << a.log2_rec_buckets) * a.rec.subcap;
-  return RecOut{a.rec.recs12 + first, a.rec.recs + first, a.rec.subcap};
+  return RecOut{a.rec.recs16 + first, a.rec.recs + first, a.rec.subcap};
 }
 
 // Store one record at cursor value `packed` of bucket b's sub-region.  The
 // block's store bases are wave-uniform (SGPRs) and a record's byte offset in
 // them fits 32 bits (index < 2^25), so the stores take the SGPR-base + 32-bit
 // VGPR-offset form: one 24-bit multiply per record, no 64-bit address math.
-__device__ __forceinline__ void put_record(const MapArgs& a, const RecOut& o, uint32_t b, uint32_t packed, bool r12,
+__device__ __forceinline__ void put_record(const MapArgs& a, const RecOut& o, uint32_t b, uint32_t packed, bool r16,
                                           uint64_t k0, uint64_t k1, uint64_t cnt, uint32_t off) {
-  const uint32_t pos = r12 ? (packed & 0xFFFFu) : (packed >> 16);
+  const uint32_t pos = r16 ? (packed & 0xFFFFu) : (packed >> 16);
   const uint32_t idx = __umul24(b, o.sub) + pos;
   if (pos >= o.sub) {
     atomicOr(&a.flags[FLAG_REGION_OVF], 1u);
     return;
   }
-  if (r12) {
-    Rec12 r;
-    r.lo = (uint32_t)k0;
-    r.hi = (uint32_t)(k0 >> 32);
-    r.off = off;
-    *reinterpret_cast<Rec12*>(reinterpret_cast<uint8_t*>(o.b12) + __umul24(idx, (uint32_t)sizeof(Rec12))) = r;
+  if (WC_EMIT_ABLATE) return;
+  if (r16) {
+    *reinterpret_cast<Rec16*>(reinterpret_cast<uint8_t*>(o.b16) + idx * (uint32_t)sizeof(Rec16)) =
+        make_rec16(k0, k1, off);
   } else {
     Rec r;
     r.k0 = k0;
@@ -169,63 +184,23 @@ __device__ __forceinline__ void put_record(const MapArgs& a, const RecOut& o, ui
 }
 
 // Append one record (key, count, first offset) to bucket b's sub-region of
-// this block; bcur[b] packs both cursors (Rec12 count | Rec count << 16).
+// this block; bcur[b] packs both cursors (Rec16 count | Rec count << 16).
 __device__ __forceinline__ void emit_record(uint32_t* bcur, const MapArgs& a, const RecOut& o, uint32_t b, uint64_t k0,
                                             uint64_t k1, uint64_t cnt, uint32_t off) {
-  const bool r12 = rec12_fits(k0, k1, cnt);
-  put_record(a, o, b, atomicAdd(&bcur[b], r12 ? 1u : 0x10000u), r12, k0, k1, cnt, off);
+  const bool r16 = rec16_fits(k0, k1, cnt);
+  put_record(a, o, b, atomicAdd(&bcur[b], r16 ? 1u : 0x10000u), r16, k0, k1, cnt, off);
 }
 
-// Profiling builds only (-DWC_EMIT_ABLATE=N, results NOT valid): 1 no record
-// stores, 2 no cursor atomics (lane-derived positions), 3 neither.
-#ifndef WC_EMIT_ABLATE
-#define WC_EMIT_ABLATE 0
-#endif
-
-// rec12_fits for one occurrence of an inline word of known length n: a word
-// of <= 8 bytes whose last byte is nonzero, i.e. k0 >> 8 (n - 1) != 0 (k0
-// holds exactly n bytes).  The shift is masked, so n = 0 of an empty lane is
-// harmless.
-__device__ __forceinline__ bool rec12_inline(uint64_t k0, uint32_t n) {
-  return n - 1u < 8u && (k0 >> ((8u * n - 8u) & 63u)) != 0;
-}
-
-// Two single-occurrence records of one lane (either may be absent): both
-// cursor atomics are issued before either store waits for its position.
-// n1 / n2: the words' lengths (inline keys).
+// Two single-occurrence records of one lane (either may be absent; n1 / n2:
+// the words' lengths, x1 / y1 their key words): both cursor atomics are
+// issued before either store waits for its position.
 __device__ __forceinline__ void emit_two(uint32_t* bcur, const MapArgs& a, const RecOut& o, bool d1, uint32_t b1,
                                          uint64_t x0, uint64_t x1, uint32_t o1, uint32_t n1, bool d2, uint32_t b2,
                                          uint64_t y0, uint64_t y1, uint32_t o2, uint32_t n2) {
-  const bool s1 = rec12_inline(x0, n1), s2 = rec12_inline(y0, n2);
-#if WC_EMIT_ABLATE == 4
-  {  // profiling only: the same number of 12-byte stores, lane-contiguous (coalesced); positions meaningless
-    const uint64_t m1 = __ballot(d1), m2 = __ballot(d2);
-    uint32_t base = 0;
-    if (__lane_id() == 0) base = atomicAdd(&bcur[0], (uint32_t)(__popcll(m1) + __popcll(m2)));
-    base = __builtin_amdgcn_readfirstlane(base);
-    const uint32_t r1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
-    const uint32_t r2 = (uint32_t)__popcll(m1) +
-                        __builtin_amdgcn_mbcnt_hi((uint32_t)(m2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m2, 0u));
-    Rec12* w = o.b12;
-    if (d1) w[(base + r1) & 0xFFFFFu] = Rec12{(uint32_t)x0, (uint32_t)(x0 >> 32), o1};
-    if (d2) w[(base + r2) & 0xFFFFFu] = Rec12{(uint32_t)y0, (uint32_t)(y0 >> 32), o2};
-    (void)s1;
-    (void)s2;
-    return;
-  }
-#endif
+  const bool s1 = rec16_inline(x0, x1, n1), s2 = rec16_inline(y0, y1, n2);
   uint32_t p1 = 0, p2 = 0;
-  if (WC_EMIT_ABLATE & 2) {
-    p1 = (__lane_id() & 7) * 0x10001u;
-    p2 = p1 + 0x80008u;
-  } else {
-    if (d1) p1 = atomicAdd(&bcur[b1], s1 ? 1u : 0x10000u);
-    if (d2) p2 = atomicAdd(&bcur[b2], s2 ? 1u : 0x10000u);
-  }
-  if (WC_EMIT_ABLATE & 1) {
-    if ((p1 ^ p2) == 0xFFFFFFFFu) atomicOr(&a.flags[FLAG_COUNT - 1], 0u);  // never true: keeps the atomics
-    return;
-  }
+  if (d1) p1 = atomicAdd(&bcur[b1], s1 ? 1u : 0x10000u);
+  if (d2) p2 = atomicAdd(&bcur[b2], s2 ? 1u : 0x10000u);
   if (d1) put_record(a, o, b1, p1, s1, x0, x1, 1, o1);
   if (d2) put_record(a, o, b2, p2, s2, y0, y1, 1, o2);
 }

@@ -11,8 +11,7 @@
 // Dense merge (merge_mode 1) runs the same owner partition / exchange / merge
 // to build the dictionary, then numbers each owner's keys (wc_row_ids), returns
 // the ids to the senders, and scatters local counts into dense vectors by id
-// (wc_scatter_ids) for the reduce-scatter.  wc_combine_u64 is the loopback
-// communicator's reduction.
+// (wc_scatter_ids) for the reduce-scatter.
 #include "../common/hip_util.hpp"
 #include "kernels.hpp"
 #include "keys.hpp"
@@ -45,19 +44,9 @@ __device__ __forceinline__ bool mem_equal(const uint8_t* x, const uint8_t* y, ui
   return u == v;
 }
 
-__global__ void wc_combine_u64(uint64_t* dst, const uint64_t* src, uint64_t n, int op) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t a = dst[i], b = src[i];
-    dst[i] = op == 0 ? a + b : (op == 1 ? (a < b ? a : b) : (a > b ? a : b));
-  }
-}
-
 constexpr int OWN_MAX = 64;       // ranks supported by the shuffle merge
 constexpr int OWN_ROWS_PER_BLOCK = 1024;
 
-__device__ __forceinline__ uint32_t owner_of(uint32_t ph, uint32_t W) {
-  return (uint32_t)(((uint64_t)ph * W) >> 32);  // high hash bits (bucket bits are low)
-}
 
 // Wave-aggregated LDS counter adds: lanes with owner `o` (OWN_MAX = none) add 1
 // to ctr[2 o] and `bytes` to ctr[2 o + 1] — two LDS atomics per distinct owner
@@ -103,9 +92,12 @@ __device__ __forceinline__ unsigned long long wave_owner_add(unsigned long long*
   return mine;
 }
 
-// counts[2o] += rows owned by o, counts[2o+1] += their long-word bytes; rows
-// [0, n) or [0, *dn) (device-side count, n the bound); pass_flags (nullable):
-// counts[2W + 1] |= the pass's re-run / table-overflow flags.
+// counts[2o] += rows owned by o, counts[2o+1] += their long-word bytes (each
+// word rounded up to 8 bytes: payloads stay 8-byte aligned, copied and compared
+// a word at a time); rows [0, n) or [0, *dn) (device-side count, n the bound);
+// pass_flags (nullable): counts[2W + 1] |= 1 if the pass needs a re-run (shuffle
+// region / table overflow), |= 2 if the key arena overflowed (every
+// rank then fails the job together instead of one rank throwing alone).
 __global__ void __launch_bounds__(256) wc_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* slen,
                                                       uint64_t n, const uint64_t* dn, const uint32_t* pass_flags,
                                                       uint32_t W, unsigned long long* counts) {
@@ -113,8 +105,9 @@ __global__ void __launch_bounds__(256) wc_owner_count(const uint64_t* k0, const 
   for (uint32_t i = threadIdx.x; i < 2 * W; i += blockDim.x) h[i] = 0;
   if (dn) n = *dn;
   if (pass_flags && blockIdx.x == 0 && threadIdx.x == 0) {
-    const uint32_t f = pass_flags[FLAG_REGION_OVF] | pass_flags[FLAG_TABLE_OVF] | pass_flags[FLAG_ARENA_OVF];
-    if (f) atomicOr(&counts[2 * W + 1], 1ull);
+    const uint32_t rerun = pass_flags[FLAG_REGION_OVF] | pass_flags[FLAG_TABLE_OVF];
+    const unsigned long long f = (rerun ? 1ull : 0ull) | (pass_flags[FLAG_ARENA_OVF] ? 2ull : 0ull);
+    if (f) atomicOr(&counts[2 * W + 1], f);
   }
   __syncthreads();
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -123,7 +116,7 @@ __global__ void __launch_bounds__(256) wc_owner_count(const uint64_t* k0, const 
     uint32_t o = OWN_MAX, nb = 0;
     if (i < n) {
       o = owner_of(place_hash(k0[i], k1[i]), W);
-      if (key_is_hashed(k1[i])) nb = slen[i];
+      if (key_is_hashed(k1[i])) nb = (slen[i] + 7u) & ~7u;
     }
     unsigned long long bo;
     (void)wave_owner_add(h, o, nb, bo);
@@ -135,7 +128,10 @@ __global__ void __launch_bounds__(256) wc_owner_count(const uint64_t* k0, const 
 
 // Pack rows (and long-word bytes) contiguously by owner.  Each block reserves
 // one range per owner (one global atomic per owner per block), then places its
-// rows with LDS atomics.  counts = wc_owner_count output; cursor zeroed.
+// rows with LDS atomics.  counts = wc_owner_count output; cursor zeroed (distinct
+// words: blocks add to the cursor while others read the counts).  A long word
+// is copied in 8-byte words: its arena copy is 8-byte aligned and rounded up
+// (reduce.hip settle_new_long), and its payload slot is rounded the same way.
 __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt,
                                                         const uint64_t* first, const uint64_t* soff,
                                                         const uint32_t* slen, const uint8_t* arena, uint64_t n,
@@ -156,7 +152,7 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
     uint32_t nb = 0;
     if (i < n) {
       own[j] = owner_of(place_hash(k0[i], k1[i]), W);
-      if (key_is_hashed(k1[i])) nb = slen[i];
+      if (key_is_hashed(k1[i])) nb = (slen[i] + 7u) & ~7u;
     }
     lr[j] = wave_owner_add(h, own[j], nb, lb[j]);
   }
@@ -185,7 +181,9 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
     r.alen = 0;
     if (key_is_hashed(r.k1)) {
       const unsigned long long bpos = base[2 * o + 1] + lb[j];
-      for (uint32_t b = 0; b < slen[i]; ++b) bytes[bpos + b] = arena[soff[i] + b];
+      const uint64_t* src = reinterpret_cast<const uint64_t*>(arena + soff[i]);
+      uint64_t* dst = reinterpret_cast<uint64_t*>(bytes + bpos);
+      for (uint32_t c = 0; c < (slen[i] + 7u) / 8u; ++c) dst[c] = src[c];
       unsigned long long bb = 0;  // offset inside owner o's byte payload
       for (uint32_t q = 0; q < o; ++q) bb += counts[2 * q + 1];
       r.aoff = (uint32_t)(bpos - bb);
@@ -405,8 +403,5 @@ void launch_scatter_ids(const uint32_t* send_pos, const uint32_t* ids_back, cons
   if (n)
     hipLaunchKernelGGL(dev::wc_scatter_ids, dev::mgrid(n), dim3(256), 0, s, send_pos, ids_back, seg, owns, W, cnt,
                        first, n, dcnt, dfirst);
-}
-void launch_combine_u64(uint64_t* dst, const uint64_t* src, uint64_t n, int op, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(dev::wc_combine_u64, dev::mgrid(n), dim3(256), 0, s, dst, src, n, op);
 }
 }  // namespace wc

@@ -49,7 +49,7 @@ namespace dev {
 #ifndef WC_RED_UNROLL
 #define WC_RED_UNROLL 4
 #endif
-constexpr int RED_UNROLL = WC_RED_UNROLL;  // 12-byte records in flight per lane
+constexpr int RED_UNROLL = WC_RED_UNROLL;  // 16-byte records in flight per lane
 #ifndef WC_RED_UNROLL_24
 #define WC_RED_UNROLL_24 2
 #endif
@@ -376,23 +376,23 @@ __device__ void settle_new_long(RedLds& L, const ReduceArgs& a, uint32_t b) {
 // A record with no matching slot in those groups — a new key, a key placed
 // further along its sequence, a tag collision — takes merge_slow.  LONG keys
 // (hashed, 24-byte runs only) are left to long_stream.
-template <bool R12, int U, class RecT>
+template <bool R16, int U, class RecT>
 __device__ __forceinline__ void merge_batch(RedLds& L, const ReduceArgs& a, uint32_t b, const RecT (&rr)[U],
                                             const bool (&valid)[U], const uint32_t (&idx)[U], uint32_t shift,
                                             uint32_t& claims) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const int lane = threadIdx.x & 63;
-  uint64_t k0[U], k1[R12 ? 1 : U];  // Rec12: the length is recomputed from k0 (VGPR budget)
+  uint64_t k0[U], k1[R16 ? 1 : U];  // Rec16: k1 is recomputed from k0 and the tail word (VGPR budget)
   uint32_t ph[U], slot[U];
   auto key1 = [&](int u) -> uint64_t {
-    if constexpr (R12) return implied_len(k0[u]);
+    if constexpr (R16) return rec16_k1(k0[u], rr[u].t);
     else return k1[u];
   };
   bool mine[U];
   u32x4 tg[U], tg2[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    if constexpr (R12) {
+    if constexpr (R16) {
       k0[u] = rr[u].lo | ((uint64_t)rr[u].hi << 32);
     } else {
       k0[u] = rr[u].k0;
@@ -404,7 +404,7 @@ __device__ __forceinline__ void merge_batch(RedLds& L, const ReduceArgs& a, uint
     }
     ph[u] = place_hash(k0[u], key1(u));
     mine[u] = valid[u] && (!shift || bucket_of(ph[u], a.tab.log2_buckets) == b);
-    if (!R12 && mine[u] && key_is_hashed(key1(u))) {  // LONG: queued for merge_long after the streams
+    if (!R16 && mine[u] && key_is_hashed(key1(u))) {  // LONG: queued for merge_long after the streams
       const uint32_t q = atomicAdd(&L.nlong, 1u);
       if (q < LONGQ) L.longq[q] = idx[u];
       mine[u] = false;
@@ -447,7 +447,7 @@ __device__ __forceinline__ void merge_batch(RedLds& L, const ReduceArgs& a, uint
     if (!mine[u]) continue;
     uint64_t cnt;
     uint32_t off;
-    if constexpr (R12) {
+    if constexpr (R16) {
       cnt = 1;
       off = rr[u].off;
     } else {
@@ -472,7 +472,7 @@ __device__ __forceinline__ void merge_batch(RedLds& L, const ReduceArgs& a, uint
 // batch AHEAD of its merge.  Lane j holds run j's exclusive prefix P and
 // index adjustment ADJ = first record index of run j - P; a record at stream
 // position t of run j sits at t + ADJ_j.
-template <bool R12, int U, class RecT>
+template <bool R16, int U, class RecT>
 __device__ __forceinline__ void merge_stream(RedLds& L, const ReduceArgs& a, uint32_t b, const RecT* recs, uint32_t p0,
                                              uint32_t pstride, uint32_t nrb, uint32_t rb, uint32_t sub, uint32_t shift,
                                              uint32_t& claims) {
@@ -483,7 +483,7 @@ __device__ __forceinline__ void merge_stream(RedLds& L, const ReduceArgs& a, uin
   uint32_t c = 0;
   if (lane < nj) {
     const uint32_t packed = L.runcnt[p0 + lane * pstride];
-    c = min(R12 ? (packed & 0xFFFFu) : (packed >> 16), sub);
+    c = min(R16 ? (packed & 0xFFFFu) : (packed >> 16), sub);
   }
   uint32_t incl = c;
   for (int o = 1; o < 64; o <<= 1) {
@@ -529,14 +529,14 @@ __device__ __forceinline__ void merge_stream(RedLds& L, const ReduceArgs& a, uin
       locate(T0 + B, ib, vb);
       load(rb2, ib, vb);
     }
-    merge_batch<R12, U>(L, a, b, ra, va, ia, shift, claims);
+    merge_batch<R16, U>(L, a, b, ra, va, ia, shift, claims);
     if (!more) return;
     const bool more2 = T0 + 2 * B < N;
     if (more2) {
       locate(T0 + 2 * B, ia, va);
       load(ra, ia, va);
     }
-    merge_batch<R12, U>(L, a, b, rb2, vb, ib, shift, claims);
+    merge_batch<R16, U>(L, a, b, rb2, vb, ib, shift, claims);
     if (!more2) return;
   }
 }
@@ -858,10 +858,10 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   const uint32_t nrb = 1u << a.log2_rec_buckets;
   const uint64_t sub = a.rec.subcap;
   // one contiguous run per map block: sub-region (p, rb) of the record store;
-  // the wave streams the 12-byte records of its runs, then the 24-byte ones
+  // the wave streams the 16-byte records of its runs, then the 24-byte ones
   uint32_t claims = 0;
   const uint32_t p0 = q + a.nq * wave, pstride = a.nq * nwaves;  // this wave's runs
-  merge_stream<true, RED_UNROLL>(L, a, b, a.rec.recs12, p0, pstride, nrb, rb, (uint32_t)sub, shift, claims);
+  merge_stream<true, RED_UNROLL>(L, a, b, a.rec.recs16, p0, pstride, nrb, rb, (uint32_t)sub, shift, claims);
   merge_stream<false, RED_UNROLL_24>(L, a, b, a.rec.recs, p0, pstride, nrb, rb, (uint32_t)sub, shift, claims);
   __syncthreads();  // every LONG record is queued (or counted past the queue)
   if (WC_RED_STAMPS && (tid & 63) == 0)

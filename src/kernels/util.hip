@@ -54,6 +54,8 @@ __global__ void __launch_bounds__(256) wc_publish(PubList c) {
 
 }  // namespace dev
 
+void launch_list_overflow(const char* what) { fail(std::string(what) + " (raise the list's bound)"); }
+
 void launch_zero_regions(const ZeroList& z, hipStream_t s) {
   if (z.n == 0 && z.nc == 0) return;
   WC_CHECK(z.n <= ZERO_MAX_REGIONS && z.nc <= ZERO_MAX_COPIES, "launch_zero_regions: too many regions");

@@ -187,3 +187,17 @@ def test_host_code_under_asan_ubsan(tmp_path, golden_text):
         assert b"ERROR: AddressSanitizer" not in r.stderr and b"runtime error" not in r.stderr, args
     r = subprocess.run([exe, "--cpu"], cwd=tmp_path, capture_output=True, timeout=120, env=env)
     assert r.stdout == GOLDEN_OUTPUT
+
+
+def test_cli_refuses_more_gpus_than_visible(tmp_path, golden_text):
+    """`wordcount --gpus N` with N above the visible GPUs (none in this CPU
+    container) fails with a clear message instead of silently running on fewer
+    and reporting N; --virtual-ranks is the one-GPU multi-rank form."""
+    exe = os.path.join(ROOT, "wordcount")
+    (tmp_path / "test.txt").write_bytes(golden_text)
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="")
+    out = subprocess.run([exe, "--gpus", "8", "--no-echo"], cwd=tmp_path, capture_output=True, timeout=60, env=env)
+    assert out.returncode != 0
+    assert b"8 GPUs requested" in out.stderr and b"visible" in out.stderr
+    bad = subprocess.run([exe, "--virtual-ranks", "4", "--gpus", "2"], cwd=tmp_path, capture_output=True, timeout=60)
+    assert bad.returncode != 0 and b"--virtual-ranks runs on one GPU" in bad.stderr

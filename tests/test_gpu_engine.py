@@ -163,6 +163,45 @@ def test_loopback_merge(ranks, merge_mode, root_rows, monkeypatch):
         assert_same(got, ops.cpu_count(text))
 
 
+def test_loopback_stream_ordered():
+    """The loopback communicator only enqueues, as RCCL does: with rank 1's
+    stream held, both ranks' allgather calls return on the host, rank 0's
+    stream stays busy until rank 1's stream reaches the collective, and the
+    gathered data is right once it is released (src/dist/comm.cpp LoopbackComm)."""
+    import ctypes
+
+    from cuda_mapreduce_amd.ops import _lib
+
+    ret, pend, ok = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+    _lib.check(_lib.lib.wc_debug_loopback_async(0, ctypes.byref(ret), ctypes.byref(pend), ctypes.byref(ok)))
+    assert ret.value == 1, "a collective call waited on the host for a peer's stream"
+    assert pend.value == 1, "rank 0's collective completed before rank 1's stream reached it"
+    assert ok.value == 1
+
+
+def test_loopback_merge_host_waits():
+    """A merge's host waits do not grow with its collectives: every collective
+    of the stream-ordered loopback is enqueue-only, the merge waits only where
+    the protocol needs host values (owner plan, merged counts, the result)."""
+    import ctypes
+
+    from cuda_mapreduce_amd.ops import _lib
+
+    def counters():
+        c, w = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        _lib.lib.wc_debug_comm_counters(ctypes.byref(c), ctypes.byref(w))
+        return c.value, w.value
+
+    text = ops.synth_host(2 << 20, seed=9, vocab=20000)
+    want = ops.cpu_count(text)
+    for merge_mode in (0, 1):
+        c0, w0 = counters()
+        assert_same(ops.loopback_count(text, 4, chunk_bytes=1 << 20, merge_mode=merge_mode, all_ranks=True), want)
+        c1, w1 = counters()
+        assert c1 - c0 >= 4 * 6, (c1 - c0)  # >= 6 collectives per rank (owner exchange + gather + broadcast)
+        assert (w1 - w0) <= 4 * 4, (w1 - w0)  # <= 4 host waits per rank
+
+
 @pytest.mark.parametrize("merge_mode", [0, 1])
 @pytest.mark.parametrize("ranks", [2, 5, 8])
 def test_loopback_merge_many_long_words(ranks, merge_mode):
@@ -303,6 +342,29 @@ def test_cli_golden(tmp_path, golden_text):
     assert out.stdout == GOLDEN_OUTPUT
     out = subprocess.run([exe, str(tmp_path / "test.txt")], capture_output=True, timeout=120)
     assert out.stdout == GOLDEN_OUTPUT
+
+
+@pytest.mark.parametrize("merge", ["shuffle", "dense"])
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_cli_virtual_ranks(tmp_path, merge, ranks):
+    """The CLI's thread-per-rank path (tools/wordcount.cpp) with W loopback ranks
+    on one GPU: byte-identical output to --cpu, JSON reports 1 GPU and W ranks."""
+    import json
+
+    exe = os.path.join(ROOT, "wordcount")
+    rng = np.random.default_rng(ranks)
+    text = random_text(rng, 300_000, long_words=5) + ops.synth_host(2 << 20, seed=8, vocab=20000)
+    f = tmp_path / "in.txt"
+    f.write_bytes(text)
+    want = subprocess.run([exe, str(f), "--cpu", "--no-echo"], capture_output=True, timeout=120)
+    assert want.returncode == 0, want.stderr
+    bj = tmp_path / "b.json"
+    got = subprocess.run([exe, str(f), "--no-echo", "--virtual-ranks", str(ranks), "--merge", merge, "--chunk-bytes",
+                          "1M", "--bench-json", str(bj)], capture_output=True, timeout=120)
+    assert got.returncode == 0, got.stderr
+    assert got.stdout == want.stdout
+    js = json.loads(bj.read_text())
+    assert js["gpus"] == 1 and js["ranks"] == ranks and js["virtual_ranks"] is True
 
 
 def test_pinned_replay_host_staged():

@@ -1,7 +1,12 @@
 """Multi-process data-parallel word count on CPU (gloo, world_size 2, 3 and 8):
-shard ownership + the owner-partitioned merge protocols of src/dist/merge.cpp
-(shuffle: all-to-all to hash owners; dense: owner-numbered dictionary +
-reduce-scatter / all-gather) must give exactly the single-process result."""
+shard ownership (the native shard splitter, wc_shard_range_*) + the Python
+mirror of the owner-partitioned merge protocols
+(cuda_mapreduce_amd/parallel/dist.py host_merge — shuffle: all-to-all to hash
+owners; dense: owner-numbered dictionary + reduce-scatter / all-gather) must
+give exactly the single-process result.  The mirror partitions by the native
+owner rule (keys.hpp owner_of, checked against the library below); the native
+merge itself (src/dist/merge.cpp: HIP kernels + RCCL) is covered by the GPU
+tests (tests/test_gpu_engine.py loopback ranks, tests/test_gpu_launcher.py)."""
 import os
 import socket
 import sys
@@ -108,3 +113,23 @@ def test_gloo_injected_comm_fault_fails_every_rank(tmp_path):
     assert outs[1][0] == "fault" and "injected comm fault" in outs[1][1]
     assert outs[0][0] == "error"
     assert [pr.exitcode for pr in procs] == [4, 3]
+
+
+def test_owner_rule_matches_native():
+    """dist._owner (Python) == wc_key_owner (keys.hpp owner_of of place_hash), for
+    SHORT, MEDIUM and LONG words and several world sizes."""
+    import ctypes
+    import random
+
+    from cuda_mapreduce_amd.ops import _lib
+    from cuda_mapreduce_amd.parallel import dist
+
+    lib = _lib.lib
+    rng = random.Random(7)
+    words = [b"a", b"Hello", b"12345678", b"123456789", b"fifteen-bytes!!", b"sixteen-bytes!!!",
+             b"x" * 64, b"tab\there", b"nul\0byte", b"\xff" * 23]
+    words += [bytes(rng.randrange(1, 256) for _ in range(rng.randrange(1, 80))) for _ in range(400)]
+    for w in words:
+        buf = (ctypes.c_uint8 * len(w)).from_buffer_copy(w)
+        for world in (1, 2, 3, 8, 64):
+            assert dist._owner(w, world) == lib.wc_key_owner(buf, len(w), world), (w, world)

@@ -24,7 +24,11 @@ namespace {
 const char* kUsage =
     "usage: wordcount [FILE] [options]\n"
     "  FILE                    input text (default: test.txt, as the reference)\n"
-    "  --gpus N                shard across N GPUs, merged with RCCL (default 1)\n"
+    "  --gpus N                shard across N GPUs, merged with RCCL (default 1; more\n"
+    "                          than the visible GPUs is an error)\n"
+    "  --virtual-ranks W       shard across W ranks on GPU 0 (threads), merged with the\n"
+    "                          stream-ordered loopback communicator (tests the W-rank\n"
+    "                          merge on one GPU; not a multi-GPU run)\n"
     "  --merge shuffle|dense   cross-GPU merge: all-to-all by key owner (default) or\n"
     "                          dictionary union + reduce-scatter / all-gather\n"
     "  --cpu                   single-thread CPU oracle (hash map)\n"
@@ -61,6 +65,7 @@ uint64_t parse_size(const std::string& s) {
 struct Cli {
   std::string file = "test.txt";
   int gpus = 1;
+  int virtual_ranks = 0;
   bool cpu = false, compat = false, echo = true, list = true, host_staged = false;
   uint64_t top = 0, chunk = 1ull << 30;
   uint32_t merge_mode = 0;
@@ -86,6 +91,7 @@ Cli parse(int argc, char** argv) {
       std::fputs(kUsage, stdout);
       std::exit(0);
     } else if (a == "--gpus") c.gpus = std::stoi(need("--gpus"));
+    else if (a == "--virtual-ranks") c.virtual_ranks = std::stoi(need("--virtual-ranks"));
     else if (a == "--cpu") c.cpu = true;
     else if (a == "--merge") {
       const std::string m = need("--merge");
@@ -123,6 +129,9 @@ Cli parse(int argc, char** argv) {
   if (c.synthetic) c.echo = false;
   if (!c.ckpt.empty() && (c.synthetic || c.compat)) wc::fail("--checkpoint needs a FILE input and the clean semantics");
   if (c.resume && c.ckpt.empty()) wc::fail("--resume needs --checkpoint PATH");
+  if (c.gpus < 1) wc::fail("--gpus expects N >= 1");
+  if (c.virtual_ranks < 0 || c.virtual_ranks > 64) wc::fail("--virtual-ranks expects 1..64");
+  if (c.virtual_ranks && c.gpus != 1) wc::fail("--virtual-ranks runs on one GPU: drop --gpus");
   return c;
 }
 
@@ -154,6 +163,7 @@ int run(const Cli& c) {
   bool have_text = false;
   const double t0 = wc::now_seconds();
   uint64_t bytes = 0;
+  int gpus_used = 0, ranks_used = 0;
   wc::Stats stages;  // GPU path: stage timings (max over ranks) and counters (sums)
 
   const bool need_host_text = !c.synthetic && (c.echo || c.cpu || c.compat);
@@ -197,12 +207,19 @@ int run(const Cli& c) {
     bytes = host.size();
   } else {
     int ndev = 0;
-    WC_HIP_CHECK(hipGetDeviceCount(&ndev));
-    const int g = std::max(1, std::min(c.gpus, ndev));
+    if (hipGetDeviceCount(&ndev) != hipSuccess) {  // no GPU driver / device: none visible
+      (void)hipGetLastError();
+      ndev = 0;
+    }
+    if (c.gpus > ndev)
+      wc::fail(std::to_string(c.gpus) + " GPUs requested, " + std::to_string(ndev) + " visible");
+    const bool virt = c.virtual_ranks > 0;
+    const int g = virt ? c.virtual_ranks : c.gpus;  // ranks
+    gpus_used = virt ? 1 : g;
     std::vector<int> devs(g);
-    for (int i = 0; i < g; ++i) devs[i] = i;
+    for (int i = 0; i < g; ++i) devs[i] = virt ? 0 : i;
     std::vector<std::unique_ptr<wc::Comm>> comms;
-    if (g > 1) comms = wc::make_rccl_comms_all(devs);
+    if (g > 1) comms = virt ? wc::make_loopback_comms(g) : wc::make_rccl_comms_all(devs);
     std::vector<std::string> errs(g);
     std::vector<wc::KeyTable> rank_tables(g);  // checkpointed runs merge on the host
     std::vector<wc::Stats> rank_stats(g);
@@ -266,8 +283,9 @@ int run(const Cli& c) {
       for (int r = 0; r < g; ++r) th.emplace_back(worker, r);
       for (auto& x : th) x.join();
     }
+    ranks_used = g;
     for (int r = 0; r < g; ++r)
-      if (!errs[r].empty()) wc::fail("GPU " + std::to_string(r) + ": " + errs[r]);
+      if (!errs[r].empty()) wc::fail((virt ? "rank " : "GPU ") + std::to_string(r) + ": " + errs[r]);
     if (!c.ckpt.empty())
       for (int r = 0; r < g; ++r) wc::merge_tables(t, rank_tables[r]);
     for (int r = 0; r < g; ++r) {
@@ -291,12 +309,14 @@ int run(const Cli& c) {
   char js[1024];
   std::snprintf(js, sizeof(js),
                 "{\"bytes\": %llu, \"tokens\": %llu, \"keys\": %zu, \"seconds\": %.6f, \"gb_per_s\": %.3f, "
-                "\"words_per_s\": %.1f, \"gpus\": %d, \"path\": \"%s\", \"chunk_bytes\": %llu, "
+                "\"words_per_s\": %.1f, \"gpus\": %d, \"ranks\": %d, \"virtual_ranks\": %s, \"path\": \"%s\", "
+                "\"chunk_bytes\": %llu, "
                 "\"device_ms\": {\"map\": %.3f, \"reduce\": %.3f, \"finalize\": %.3f, \"merge\": %.3f, "
                 "\"total\": %.3f}, "
                 "\"chunks\": %u, \"records\": %llu, \"map_reruns\": %u, \"table_splits\": %u}",
                 (unsigned long long)bytes, (unsigned long long)t.total, t.size(), secs, bytes / secs / 1e9,
-                t.total / secs, gpu_path ? c.gpus : 0, c.compat ? "compat" : (c.cpu ? "cpu" : "gpu"),
+                t.total / secs, gpu_path ? gpus_used : 0, gpu_path ? ranks_used : 0,
+                c.virtual_ranks > 0 ? "true" : "false", c.compat ? "compat" : (c.cpu ? "cpu" : "gpu"),
                 (unsigned long long)c.chunk, stages.map_ms, stages.reduce_ms, stages.finalize_ms, stages.merge_ms,
                 stages.device_ms,
                 stages.chunks, (unsigned long long)stages.records, stages.map_reruns, stages.table_splits);
