@@ -15,6 +15,7 @@ from .engine import (  # noqa: F401
     virtual_bench,
     numa_of_pci,
     h2d_bench,
+    file_read_bench,
     shard_range,
     shard_range_file,
     synth_host,

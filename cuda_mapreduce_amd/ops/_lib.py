@@ -90,6 +90,7 @@ def _load() -> ctypes.CDLL:
         "wc_pool_numa_node": (c_int, [c_void_p]),
         "wc_numa_of_pci": (c_int, [c_char_p, c_char_p, POINTER(c_int), POINTER(c_int), c_int]),
         "wc_h2d_bench": (c_int, [c_int, c_int, c_uint64, c_int, POINTER(c_double), POINTER(c_int)]),
+        "wc_file_read_bench": (c_int, [c_char_p, c_uint64, c_int, POINTER(c_double), P64]),
         "wc_pool_destroy": (None, [c_void_p]),
         "wc_pool_build_seconds": (c_double, [c_void_p]),
         "wc_count_pool": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64]),

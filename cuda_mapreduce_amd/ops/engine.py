@@ -309,6 +309,13 @@ def h2d_bench(device: int = 0, node: int = -1, nbytes: int = 1 << 30, reps: int 
     return g.value, used.value
 
 
+def file_read_bench(path: str, piece: int = 64 << 20, device: int = 0):
+    """Host read rate of the file path (pread_parallel into page-locked memory, no GPU copy) -> (GB/s, bytes)."""
+    g, n = ctypes.c_double(0), ctypes.c_uint64(0)
+    check(lib.wc_file_read_bench(path.encode(), piece, device, ctypes.byref(g), ctypes.byref(n)))
+    return g.value, n.value
+
+
 def shard_range(data: bytes, rank: int, world: int):
     """Ownership-adjusted [begin, end) of shard `rank` (token owned by its first byte)."""
     ptr, keep = _u8ptr(data)

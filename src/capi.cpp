@@ -143,6 +143,29 @@ int wc_debug_loopback_async(int device, int* returned, int* pending, int* correc
   });
 }
 
+// Raw host side of the file path: the file read with pread_parallel (the
+// FileSource reader) in pieces of `piece` bytes into one page-locked buffer
+// bound to `device`'s NUMA node, nothing copied to the GPU: the ceiling the
+// file-streaming count is measured against (tools/file_path.sh).
+int wc_file_read_bench(const char* path, uint64_t piece, int device, double* gbps, uint64_t* bytes) {
+  return guard([&] {
+    const wc::NumaNode nn = device >= 0 ? wc::numa_of_device(device) : wc::NumaNode{};
+    wc::ScopedAffinity bind(nn.cpus);
+    const uint64_t n = wc::file_size(path);
+    wc::PinnedBuffer buf(std::max<uint64_t>(piece, 1));
+    wc::FileSource src(path, 0, n);
+    const double t0 = wc::now_seconds();
+    uint64_t got = 0;
+    for (;;) {
+      const uint64_t k = src.read(buf.data(), piece);
+      if (!k) break;
+      got += k;
+    }
+    *gbps = (double)got / (wc::now_seconds() - t0) / 1e9;
+    *bytes = got;
+  });
+}
+
 // Process-wide communicator counters: collectives enqueued, host waits.
 void wc_debug_comm_counters(uint64_t* collectives, uint64_t* host_waits) {
   *collectives = wc::Comm::collectives_total();
