@@ -151,6 +151,7 @@ def run_virtual(a) -> int:
         "ms_per_step": round(ms, 4), "steps": a.steps, "warmup": a.warmup, "validated": valid, "validation": check,
         "distinct_words": len(res.words),
         "merge_ms": [round(r["merge"], 4) for r in ranks],
+        "merges_planned_rank0": int(ranks[0]["merges_planned"]), "merge_redos_rank0": int(ranks[0]["merge_redos"]),
         "stage_ms_rank0": {k: round(ranks[0][k], 4) for k in ("map", "reduce", "finalize", "merge", "idle")},
         "keys_per_rank": [int(r["keys"]) for r in ranks],
         "config": {"model": f"wordcount-mapreduce/{cfg.name}", "bytes_per_rank": per, "chunk_bytes": chunk,

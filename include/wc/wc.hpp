@@ -36,6 +36,9 @@ struct Stats {
   // speculative finalize's sample sort (sized by the previous job) overflowed
   // and the exact-count one did not
   uint32_t order_path = 0;
+  // cross-GPU merges of the engine's life run planned (fixed exchange regions,
+  // no host round trip) / redone exactly after a planned one overflowed
+  uint32_t merges_planned = 0, merge_redos = 0;
   // Host wall clock of the last job's API calls (count_*, finalize / result).
   double host_count_ms = 0, host_finalize_ms = 0;
   // Device time of the last job's stages, from events on the engine stream

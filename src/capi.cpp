@@ -459,11 +459,13 @@ int wc_engine_stats_json(wc_engine* e, char* buf, int cap) {
   const int k = snprintf(tmp, sizeof tmp,
                          "{\"bytes\": %llu, \"tokens\": %llu, \"keys\": %llu, \"records\": %llu, \"chunks\": %u, "
                          "\"map_reruns\": %u, \"table_splits\": %u, \"log2_buckets\": %u, \"order_path\": %u, "
+                         "\"merges_planned\": %u, \"merge_redos\": %u, "
                          "\"device_ms\": {\"map\": %.4f, \"reduce\": %.4f, \"finalize\": %.4f, \"merge\": %.4f, "
                          "\"idle\": %.4f, \"total\": %.4f}, "
                          "\"host_ms\": {\"count\": %.4f, \"finalize\": %.4f}}",
                          (unsigned long long)s.bytes, (unsigned long long)s.tokens, (unsigned long long)s.keys,
                          (unsigned long long)s.records, s.chunks, s.map_reruns, s.table_splits, s.log2_buckets, s.order_path,
+                         s.merges_planned, s.merge_redos,
                          s.map_ms,
                          s.reduce_ms, s.finalize_ms, s.merge_ms, s.idle_ms, s.device_ms, s.host_count_ms,
                          s.host_finalize_ms);
@@ -693,8 +695,10 @@ void wc_comm_destroy(wc_comm* c) { delete c; }
 // count the shard, merged finalize on the device — `warmup` + `steps` times,
 // the timed loop bracketed by communicator barriers.  out[8 r + i] =
 // {wall ms / step, device ms of the last job: map, reduce, finalize, merge,
-// idle, tokens, local keys}.  Returns rank 0's merged table (one result()
-// after timing) for validation.
+// idle, tokens, local keys, merges planned, merges redone}.  Returns rank 0's
+// merged table of one more job after timing — the same step ending in
+// result(), so it goes the way the timed jobs went (planned merge once the
+// first job learned its caps) — for validation.
 wc_result* wc_virtual_bench(const wc_options* o, int ranks, int device, uint64_t bytes, uint64_t seed, uint32_t vocab,
                             double zipf, double long_frac, int steps, int warmup, double* out) {
   wc_result* res = new wc_result;
@@ -728,8 +732,12 @@ wc_result* wc_virtual_bench(const wc_options* o, int ranks, int device, uint64_t
         WC_HIP_CHECK(hipDeviceSynchronize());
         c->barrier(nullptr);
         const double ms = (wc::now_seconds() - t0) * 1e3 / (steps > 0 ? steps : 1);
-        const wc::Stats& st = eng.stats();
-        double* v = out + 8 * (size_t)r;
+        const wc::Stats st = eng.stats();
+        eng.reset();
+        eng.count_device(d, nseg * seg, nseg * seg, (uint64_t)r * nseg * seg, ' ');
+        wc::KeyTable t = eng.result(c, false);
+        const wc::Stats& st2 = eng.stats();
+        double* v = out + 10 * (size_t)r;
         v[0] = ms;
         v[1] = st.map_ms;
         v[2] = st.reduce_ms;
@@ -738,7 +746,8 @@ wc_result* wc_virtual_bench(const wc_options* o, int ranks, int device, uint64_t
         v[5] = st.idle_ms;
         v[6] = (double)st.tokens;
         v[7] = (double)keys;
-        wc::KeyTable t = eng.result(c, false);
+        v[8] = (double)st2.merges_planned;
+        v[9] = (double)st2.merge_redos;
         if (r == 0) res->t = std::move(t);
       } catch (const std::exception& ex) {
         errs[r] = ex.what();

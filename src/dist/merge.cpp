@@ -192,6 +192,8 @@ void plan_enqueue(Engine::Impl& im, Comm& comm, uint64_t n, const uint64_t* dn, 
   comm.allgather(P.d_cnt, P.d_all, C * 8, s);
 }
 
+void learn_caps(Engine::Impl& im, const OwnerPlan& P, const std::vector<unsigned long long>& owns, bool dense);
+
 // Host half, from the all-gathered matrix (P.all).
 void plan_finish(OwnerPlan& P) {
   const int W = P.W, R = P.R;
@@ -266,7 +268,11 @@ void merge_cols_owner(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense, 
   // and one host sync fewer.  WC_MERGE_ROOT_ROWS overrides the threshold.
   uint64_t root_max = MERGE_ROOT_MAX_ROWS;
   if (const char* e = std::getenv("WC_MERGE_ROOT_ROWS")) root_max = std::strtoull(e, nullptr, 10);
-  if (!dense && !all_ranks && P.total_rows <= root_max) {
+  static const bool planned_off =
+      std::getenv("WC_MERGE_PLANNED") && std::atoi(std::getenv("WC_MERGE_PLANNED")) == 0;
+  // with planned merges on, the exact merge takes the owner path: it learns
+  // the caps the planned protocol needs (the root path has no owner counts)
+  if (!dense && !all_ranks && P.total_rows <= root_max && (planned_off || std::getenv("WC_MERGE_ROOT_ROWS"))) {
     merge_to_root(im, comm, P.rank_rows, P.rank_bytes, P.gmax_end, P.d_cnt + P.C);
     return;
   }
@@ -372,6 +378,7 @@ void merge_cols_owner(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense, 
   std::vector<unsigned long long> owns(2 * (size_t)W);
   WC_HIP_CHECK(hipMemcpyAsync(owns.data(), d_owns, owns.size() * 8, hipMemcpyDeviceToHost, s));
   comm.sync(s);
+  learn_caps(im, P, owns, dense);  // the next merge of this shape runs planned
   const unsigned long long own[2] = {owns[2 * (size_t)R], rbt};
   std::vector<size_t> go_r(W, 0), gb_r(W, 0), go_b(W, 0), gb_b(W, 0), zs(W, 0);
   std::vector<size_t> sr(W, 0), sb(W, 0);
@@ -453,6 +460,267 @@ void merge_cols_owner(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense, 
   im.cols_arena = gbytes;
   im.cols_arena_bytes = have ? GB : 0;
   im.max_end = P.gmax_end;
+}
+
+// Fixed exchange regions for the next planned merge, from an exact merge's
+// all-gathered count matrix and merged-row counts (identical on every rank):
+// the largest (rank -> owner) rows / bytes and owner merged rows, + 1/8 + 256.
+void learn_caps(Engine::Impl& im, const OwnerPlan& P, const std::vector<unsigned long long>& owns, bool dense) {
+  const int W = P.W;
+  uint64_t rows = 0, bytes = 0, merged = 0;
+  for (int p = 0; p < W; ++p)
+    for (int o = 0; o < W; ++o) {
+      rows = std::max<uint64_t>(rows, P.all[(size_t)p * P.C + 2 * o]);
+      bytes = std::max<uint64_t>(bytes, P.all[(size_t)p * P.C + 2 * o + 1]);
+    }
+  for (int o = 0; o < W; ++o) merged = std::max<uint64_t>(merged, owns[2 * (size_t)o]);
+  auto grow = [](uint64_t x) { return x + x / 8 + 256; };
+  Engine::Impl::MergeCaps& c = im.merge_caps;
+  c.valid = true;
+  c.world = W;
+  c.mode = dense ? 1u : 0u;
+  c.rows = grow(rows);
+  c.bytes = (grow(bytes) + 7) & ~7ull;
+  c.merged = grow(merged);
+  if (const char* e = std::getenv("WC_MERGE_CAP_ROWS")) {  // tests only: force region overflows (the redo path)
+    c.rows = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+    c.merged = c.rows;
+  }
+  c.gmax_end = P.gmax_end;
+}
+
+// Planned merge (both protocols, SURVEY §5.8 with no host round trip): every
+// exchange has sizes fixed in advance (Engine::Impl::MergeCaps) — owner o's
+// rows from each rank in a region of caps.rows rows (+ caps.bytes bytes of
+// long words), owner o's merged rows in a region of caps.merged rows for the
+// gather (dense: padded ids o * caps.merged + index) — padding rows are empty
+// keys that the owner merge skips.  Counts, decisions and the merged key count
+// stay on the device: nothing here waits.  wc_merge_check ORs into
+// im.d_merge_flags, from the all-gathered words every rank reads alike: a
+// last pass needing recovery (1), an arena overflow (2), a region overflow (4)
+// — the finalize reads them after its last wait, and every rank redoes the
+// merge with the exact protocol together when they are set.
+// Columns in: im.cols with n the bound and dn the device count.
+void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense, const uint32_t* pass_flags) {
+  Range rg(dense ? "wc_merge_dense_planned" : "wc_merge_shuffle_planned");
+  hipStream_t s = im.s;
+  const int W = comm.size(), R = comm.rank();
+  WC_CHECK(W <= (int)MERGE_MAX_RANKS, "merge supports at most 64 ranks");
+  const Engine::Impl::MergeCaps cp = im.merge_caps;
+  const uint64_t Cr = cp.rows, Cb = cp.bytes, Gr = cp.merged;
+  const uint64_t nb = im.cols.n;  // bound; the count is *dn
+  const uint64_t* dn = reinterpret_cast<const uint64_t*>(im.cols.dn);
+  const size_t C = 2 * (size_t)W + 2;
+  DeviceArena& S = im.merge_small;
+  S.reserve(((size_t)W * C + 2 * C + 4 * (size_t)W + 64) * 8 + 8 * 1024);
+  S.reset();
+  unsigned long long* d_cnt = take_aligned<unsigned long long>(S, 2 * C);  // counts | max offset | flags | cursor
+  unsigned long long* d_all = take_aligned<unsigned long long>(S, (size_t)W * C);
+  unsigned long long* d_own = take_aligned<unsigned long long>(S, 2);
+  unsigned long long* d_owns = take_aligned<unsigned long long>(S, 2 * (size_t)W);
+  unsigned long long* d_on = take_aligned<unsigned long long>(S, 1);
+  im.d_merge_flags = take_aligned<uint32_t>(S, 2);
+  uint64_t* mx = host_words(im) + HW_MX;
+  *mx = im.max_end;
+  uint64_t* base = host_words(im) + HW_BASE;  // fixed-region bases per source: rows | bytes
+  for (int p = 0; p <= W; ++p) {
+    base[p] = (uint64_t)p * Cr;
+    base[W + 1 + p] = (uint64_t)p * Cb;
+  }
+  uint64_t* seg = host_words(im) + HW_SEG;  // send-row starts per owner (dense id return)
+  for (int p = 0; p <= W; ++p) seg[p] = (uint64_t)p * Cr;
+
+  DeviceArena& A = im.merge_mem;
+  const uint64_t RR = (uint64_t)W * Cr, RB = (uint64_t)W * Cb, GR = (uint64_t)W * Gr;
+  uint64_t T = 1024;
+  while (T < 2 * RR) T <<= 1;
+  const bool have = R == 0 || all_ranks;
+  A.reserve(2 * RR * sizeof(MRow) + 2 * RB + T * (4 + 16) + RR * sizeof(MRow) + (size_t)GR * sizeof(MRow) +
+            (size_t)W * RB + (have ? GR * (5 * 8 + 4) : 0) + (4 * (size_t)W + 8) * 8 + 64 * 1024 +
+            (dense ? (nb + 2 * RR + T) * 4 + GR * 8 * 4 + 16 * 256 : 0));
+  A.reset();
+  MRow* send_rows = take_aligned<MRow>(A, RR);
+  uint8_t* send_bytes = take_aligned<uint8_t>(A, RB);
+  MRow* recv_rows = take_aligned<MRow>(A, RR);
+  uint8_t* recv_bytes = take_aligned<uint8_t>(A, RB);
+  uint32_t* state = take_aligned<uint32_t>(A, T);
+  unsigned long long* tcnt = take_aligned<unsigned long long>(A, T);
+  unsigned long long* tfirst = take_aligned<unsigned long long>(A, T);
+  MRow* merged = take_aligned<MRow>(A, RR);  // compaction writes up to RR rows; the first Gr are sent
+  uint64_t* d_base = take_aligned<uint64_t>(A, 2 * (size_t)W + 2);
+  uint64_t* d_seg = take_aligned<uint64_t>(A, (size_t)W + 1);
+  unsigned long long* d_m = take_aligned<unsigned long long>(A, 1);
+  uint32_t* send_pos = dense ? take_aligned<uint32_t>(A, nb) : nullptr;
+  uint32_t* row_slot = dense ? take_aligned<uint32_t>(A, RR) : nullptr;
+  uint32_t* slot_id = dense ? take_aligned<uint32_t>(A, T) : nullptr;
+  {
+    ZeroList z{};  // counts, flags, cursor, padding rows, the owner table, the merged region: two launches
+    z.add(d_cnt, 2 * (size_t)W * 8);
+    z.add(d_cnt + 2 * W + 1, (2 * C - 2 * (size_t)W - 1) * 8);
+    z.add(im.d_merge_flags, 8);
+    z.add(send_rows, RR * sizeof(MRow));
+    z.add(state, T * 4);
+    z.add(tcnt, T * 8);
+    z.add(tfirst, T * 8, 0xFFFFFFFFu);
+    z.add(merged, Gr * sizeof(MRow));
+    z.copy(d_cnt + 2 * W, mx, 8);
+    z.copy(d_base, base, (2 * (size_t)W + 2) * 8);
+    z.copy(d_seg, seg, ((size_t)W + 1) * 8);
+    launch_zero_regions(z, s);
+    ZeroList z2{};
+    z2.add(d_m, 8);
+    z2.add(d_own + 1, 8);
+    launch_zero_regions(z2, s);
+  }
+  // 1. owner counts (+ max offset, pass flags), all-gathered: the decision words
+  launch_owner_count(im.cols.k0, im.cols.k1, im.cols.sref_len, nb, dn, pass_flags, (uint32_t)W, d_cnt, s);
+  comm.allgather(d_cnt, d_all, C * 8, s);
+  launch_merge_check(d_all, (uint32_t)W, Cr, Cb, nullptr, 0, im.d_merge_flags, s);
+  // 2. pack into the fixed regions and exchange them whole
+  launch_owner_scatter(im.cols.k0, im.cols.k1, im.cols.cnt, im.cols.first, im.cols.sref_off, im.cols.sref_len,
+                       im.cols_arena, nb, (uint32_t)W, nullptr, d_cnt + C, send_rows, send_bytes, send_pos, s, dn, Cr,
+                       Cb, im.d_merge_flags);
+  std::vector<size_t> ro(W), rs(W, Cr * sizeof(MRow)), bo(W), bs(W, Cb), zs(W, 0), gr(W, 0), gb(W, 0), go(W), gbo(W);
+  for (int p = 0; p < W; ++p) {
+    ro[p] = (size_t)p * Cr * sizeof(MRow);
+    bo[p] = (size_t)p * Cb;
+  }
+  comm.group_begin();
+  comm.alltoallv(send_rows, ro.data(), rs.data(), recv_rows, ro.data(), rs.data(), s);
+  comm.alltoallv(send_bytes, bo.data(), bs.data(), recv_bytes, bo.data(), bs.data(), s);
+  comm.group_end();
+  // 3. owner merge (padding rows skipped), merged rows counted on the device
+  launch_mrow_insert(recv_rows, RR, recv_bytes, d_base, d_base + W + 1, (uint32_t)W, state, tcnt, tfirst, T, row_slot,
+                     s);
+  launch_mrow_compact(recv_rows, state, tcnt, tfirst, T, d_base, d_base + W + 1, (uint32_t)W, merged, d_m, slot_id, s);
+  {
+    ZeroList z{};
+    z.copy(d_own, d_m, 8);
+    launch_zero_regions(z, s);
+  }
+  // 4. every owner's merged count (+ dense: the owner-local ids back to the senders)
+  uint32_t* ids = nullptr;
+  uint32_t* ids_back = nullptr;
+  if (dense) {
+    ids = take_aligned<uint32_t>(A, RR);
+    ids_back = take_aligned<uint32_t>(A, RR);
+    launch_row_ids(row_slot, slot_id, RR, d_owns, 0u, ids, s);
+  }
+  comm.group_begin();
+  comm.allgather(d_own, d_owns, 16, s);
+  if (dense) {
+    std::vector<size_t> io(W), is(W, Cr * 4);
+    for (int p = 0; p < W; ++p) io[p] = (size_t)p * Cr * 4;
+    comm.alltoallv(ids, io.data(), is.data(), ids_back, io.data(), is.data(), s);
+  }
+  comm.group_end();
+  launch_merge_check(nullptr, (uint32_t)W, 0, 0, d_owns, Gr, im.d_merge_flags, s);
+  // 5. dense: padded count / first-offset vectors, reduce-scattered (owner o's
+  // slice = its ids) and all-gathered
+  uint64_t *dcnt = nullptr, *dfirst = nullptr;
+  if (dense) {
+    uint64_t* vc = take_aligned<uint64_t>(A, GR);
+    uint64_t* vf = take_aligned<uint64_t>(A, GR);
+    uint64_t* scnt = take_aligned<uint64_t>(A, Gr);
+    uint64_t* sfirst = take_aligned<uint64_t>(A, Gr);
+    dcnt = take_aligned<uint64_t>(A, GR);
+    dfirst = take_aligned<uint64_t>(A, GR);
+    ZeroList z{};
+    z.add(vc, GR * 8);
+    z.add(vf, GR * 8, 0xFFFFFFFFu);
+    launch_zero_regions(z, s);
+    launch_scatter_ids(send_pos, ids_back, d_seg, d_owns, (uint32_t)W, im.cols.cnt, im.cols.first, nb, vc, vf, s, dn, Gr);
+    comm.group_begin();
+    comm.reduce_scatter_u64(vc, scnt, Gr, RedOp::Sum, s);
+    comm.reduce_scatter_u64(vf, sfirst, Gr, RedOp::Min, s);
+    comm.group_end();
+    comm.group_begin();
+    comm.allgather(scnt, dcnt, Gr * 8, s);
+    comm.allgather(sfirst, dfirst, Gr * 8, s);
+    comm.group_end();
+  }
+  // 6. every owner's merged region (+ its whole received byte payload) to rank 0
+  for (int p = 0; p < W; ++p) {
+    go[p] = (size_t)p * Gr * sizeof(MRow);
+    gbo[p] = (size_t)p * RB;
+    if (R == 0) {
+      gr[p] = Gr * sizeof(MRow);
+      gb[p] = RB;
+    }
+  }
+  std::vector<size_t> sr(W, 0), sb(W, 0);
+  sr[0] = Gr * sizeof(MRow);
+  sb[0] = RB;
+  MRow* grows = take_aligned<MRow>(A, GR);
+  uint8_t* gbytes = take_aligned<uint8_t>(A, (uint64_t)W * RB);
+  comm.group_begin();
+  comm.alltoallv(merged, zs.data(), sr.data(), grows, go.data(), gr.data(), s);
+  comm.alltoallv(recv_bytes, zs.data(), sb.data(), gbytes, gbo.data(), gb.data(), s);
+  comm.group_end();
+  if (all_ranks) {
+    comm.group_begin();
+    comm.broadcast(grows, GR * sizeof(MRow), 0, s);
+    comm.broadcast(gbytes, (uint64_t)W * RB, 0, s);
+    comm.group_end();
+  }
+  KeyCols o;
+  if (have) {
+    o.n = GR;
+    o.dn = d_on;
+    o.k0 = take_aligned<uint64_t>(A, GR);
+    o.k1 = take_aligned<uint64_t>(A, GR);
+    o.cnt = take_aligned<uint64_t>(A, GR);
+    o.first = take_aligned<uint64_t>(A, GR);
+    o.sref_off = take_aligned<uint64_t>(A, GR);
+    o.sref_len = take_aligned<uint32_t>(A, GR);
+    launch_mrow_regions_to_cols(grows, (uint32_t)W, Gr, d_owns, RB, dcnt, dfirst, o.k0, o.k1, o.cnt, o.first,
+                                o.sref_off, o.sref_len, d_on, s);
+  }
+  im.cols = o;  // in flight: the finalize's last wait publishes the count and the flags
+  im.cols_arena = gbytes;
+  im.cols_arena_bytes = have ? (uint64_t)W * RB : 0;
+  im.max_end = std::max(im.max_end, cp.gmax_end);
+  im.planned_active = true;
+  im.st.merges_planned++;
+}
+
+// The planned merge launched right behind the pending last pass: device
+// bucket offsets -> compaction sized to the table's capacity -> the planned
+// protocol, nothing waited for.  Needs caps of this world size and protocol.
+bool merge_cols_planned_speculative(Engine::Impl& im, Comm& comm, bool all_ranks) {
+  const Engine::Impl::MergeCaps& cp = im.merge_caps;
+  static const bool off = std::getenv("WC_MERGE_PLANNED") && std::atoi(std::getenv("WC_MERGE_PLANNED")) == 0;
+  if (off || !cp.valid || cp.world != comm.size() || cp.mode != im.opt.merge_mode) return false;
+  Range rg("wc_merge_planned_speculative");
+  im.planned_pass = im.pend;
+  im.pend.active = false;
+  hipStream_t s = im.s;
+  const TableView& t = im.table();
+  const size_t nb = (size_t)1 << t.log2_buckets;
+  const uint64_t cap = (uint64_t)nb * TAB_SLOTS;
+  DeviceArena& F = im.fin_mem;
+  F.reserve((cap + 1) * (5 * 8 + 4) + nb * 8 + 64 * 1024);
+  F.reset();
+  KeyCols c;
+  c.k0 = F.take_n<uint64_t>(cap + 1);
+  c.k1 = F.take_n<uint64_t>(cap + 1);
+  c.cnt = F.take_n<uint64_t>(cap + 1);
+  c.first = F.take_n<uint64_t>(cap + 1);
+  c.sref_off = F.take_n<uint64_t>(cap + 1);
+  c.sref_len = F.take_n<uint32_t>(cap + 1);
+  uint64_t* d_boff = F.take_n<uint64_t>(nb);
+  uint64_t* d_n = F.take_n<uint64_t>(2);
+  launch_bucket_offsets(t.occupancy, (uint32_t)nb, d_boff, d_n, s);
+  launch_table_compact(t, d_boff, c.k0, c.k1, c.cnt, c.first, c.sref_off, c.sref_len, s);
+  c.n = cap;
+  c.dn = reinterpret_cast<unsigned long long*>(d_n);
+  im.d_local_n = d_n;
+  im.cols = c;
+  im.cols_arena = im.d_arena;
+  im.st.log2_buckets = t.log2_buckets;
+  im.mark(Engine::Impl::EV_MERGE0);
+  merge_cols_planned(im, comm, all_ranks, im.opt.merge_mode == 1, im.d_ctr->flags);
+  return true;
 }
 
 void merge_cols(Engine::Impl& im, Comm& comm, bool all_ranks) {

@@ -1111,8 +1111,12 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
   im.fo_ovf = nullptr;
   im.order_redo = false;
   bool drained = false;
+  im.planned_active = false;
   if (merged) {
-    const bool spec = im.pend.active && im.speculate && !im.sync_debug && merge_cols_speculative(im, *comm, all_ranks);
+    // planned (no host round trip) when the last exact merge of this shape
+    // left its caps, else the speculative exact protocol, else the synchronous one
+    const bool spec = im.pend.active && im.speculate && !im.sync_debug &&
+                      (merge_cols_planned_speculative(im, *comm, all_ranks) || merge_cols_speculative(im, *comm, all_ranks));
     if (!spec) {
       im.settle();
       im.compact_local();
@@ -1130,18 +1134,54 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
     if (im.order_redo && im.st.order_path == 1) im.st.order_path = 4;
   }
   if (!im.fin_end_marked) im.mark(EV_FIN_END);
-  // the merged count still on the device and the sample sort's overflow word:
-  // published with the last wait
-  if (im.cols.dn || im.fo_ovf) {
-    if (im.h_fin.size() < 64) im.h_fin = PinnedBuffer(64);
-    PubList pc{};
-    if (im.cols.dn) pc.add(im.h_fin.data(), im.cols.dn, 8);
-    if (im.fo_ovf) pc.add(im.h_fin.data() + 8, im.fo_ovf, 4);
-    launch_publish(pc, im.s);
+  // the merged count still on the device, the sample sort's overflow word and
+  // (planned merge) its decision flags and local key count: published with the last wait
+  auto publish_and_wait = [&] {
+    if (im.cols.dn || im.fo_ovf || im.planned_active) {
+      if (im.h_fin.size() < 64) im.h_fin = PinnedBuffer(64);
+      PubList pc{};
+      if (im.cols.dn) pc.add(im.h_fin.data(), im.cols.dn, 8);
+      if (im.fo_ovf) pc.add(im.h_fin.data() + 8, im.fo_ovf, 4);
+      if (im.planned_active) {
+        std::memset(im.h_fin.data() + 16, 0, 16);
+        pc.add(im.h_fin.data() + 16, im.d_merge_flags, 4);
+        pc.add(im.h_fin.data() + 24, im.d_local_n, 8);
+      }
+      launch_publish(pc, im.s);
+    }
+    // the merge's last collectives are still in flight: wait under the comm watchdog
+    if (merged) comm->sync(im.s);
+    else if (!drained) WC_HIP_CHECK(hipStreamSynchronize(im.s));
+  };
+  publish_and_wait();
+  if (im.planned_active) {
+    // the planned merge's decisions (the same on every rank: all-gathered words)
+    im.planned_active = false;
+    uint32_t f = 0;
+    uint64_t local_n = 0;
+    std::memcpy(&f, im.h_fin.data() + 16, 4);
+    std::memcpy(&local_n, im.h_fin.data() + 24, 8);
+    if (f & 2) fail("key arena exhausted on a rank (" + std::to_string(im.opt.arena_bytes) + " bytes each); raise arena_bytes");
+    const PendingPass p = im.planned_pass;
+    const bool clean = im.complete_pass(p.text, p.len, p.avail, p.base, p.prev, p.rb, p.blocks, true);
+    im.st.keys = local_n;
+    if (!clean || (f & 5)) {
+      // a pass needed recovery (1) or a fixed region overflowed (4): every rank
+      // redoes the merge exactly (the table is intact) and relearns the caps
+      WC_LOG(LOG_INFO, "dev %d: planned merge redone exactly (flags %u)", im.dev, f);
+      im.merge_caps.valid = false;
+      im.st.merge_redos++;
+      im.fo_ovf = nullptr;
+      im.settle();
+      im.compact_local();
+      im.mark(EV_MERGE0);
+      merge_cols(im, *comm, all_ranks);
+      im.mark(EV_MERGE1);
+      im.sort_cols_by_first();
+      im.mark(EV_FIN_END);
+      publish_and_wait();
+    }
   }
-  // the merge's last collectives are still in flight: wait under the comm watchdog
-  if (merged) comm->sync(im.s);
-  else if (!drained) WC_HIP_CHECK(hipStreamSynchronize(im.s));
   if (im.fo_ovf) {
     uint32_t bad = 0;
     std::memcpy(&bad, im.h_fin.data() + 8, 4);

@@ -156,6 +156,21 @@ struct Engine::Impl {
     int prev = -1;
     uint32_t rb = 0, blocks = 0;
   } pend;
+  // Planned merge (dist/merge.cpp merge_cols_planned): fixed exchange regions
+  // learned from the last exact merge of the same shape — identical on every
+  // rank, since they come from all-gathered counts — so the merged finalize
+  // needs no host round trip; its decision flags arrive with the last wait.
+  struct MergeCaps {
+    bool valid = false;
+    int world = 0;
+    uint32_t mode = 0;
+    uint64_t rows = 0, bytes = 0, merged = 0;  // per (rank -> owner) region / per owner in the gather
+    uint64_t gmax_end = 0;                     // the sort key width of the last exact merge
+  } merge_caps;
+  bool planned_active = false;      // a planned merge is in flight: check its flags after the last wait
+  PendingPass planned_pass;         // the pass it ran behind (completed after the last wait)
+  uint32_t* d_merge_flags = nullptr;  // device word of the planned merge's flags (merge_small)
+  uint64_t* d_local_n = nullptr;      // the planned merge's local key count (device, published at the end)
   // Engine::reset() only marks the table empty; the next pass's zeroing kernel
   // (or apply_reset, before anything else reads the table) clears it.
   bool reset_pending = false;
@@ -233,5 +248,8 @@ void merge_cols(Engine::Impl& im, Comm& comm, bool all_ranks);
 // settle, one host wait); false: some rank's pass needs recovery — the caller
 // settles, compacts and runs merge_cols (every rank takes the same branch).
 bool merge_cols_speculative(Engine::Impl& im, Comm& comm, bool all_ranks);
+// The planned merge behind the pending pass (no host round trip; needs
+// MergeCaps of this shape): false = not applicable, nothing enqueued.
+bool merge_cols_planned_speculative(Engine::Impl& im, Comm& comm, bool all_ranks);
 
 }  // namespace wc

@@ -347,10 +347,21 @@ constexpr uint64_t MERGE_ROOT_MAX_ROWS = 1ull << 18;
 // counts of rows [0, n) — or [0, *dn) with n a bound — and (pass_flags) the pass's recovery flags at 2W + 1
 void launch_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* slen, uint64_t n, const uint64_t* dn,
                         const uint32_t* pass_flags, uint32_t W, unsigned long long* counts, hipStream_t s);
+// send_pos (nullable): row index of each local key; dn: device-side row count
+// (n the bound); reg_rows > 0: planned mode — owner o's rows / bytes in fixed
+// regions of reg_rows rows / reg_bytes bytes (counts unused), overflow -> *ovf
 void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
                           const uint64_t* soff, const uint32_t* slen, const uint8_t* arena, uint64_t n, uint32_t W,
                           const unsigned long long* counts, unsigned long long* cursor, MRow* rows, uint8_t* bytes,
-                          uint32_t* send_pos, hipStream_t s);  // send_pos (nullable): row index of each local key
+                          uint32_t* send_pos, hipStream_t s, const uint64_t* dn = nullptr, uint64_t reg_rows = 0,
+                          uint64_t reg_bytes = 0, uint32_t* ovf = nullptr);
+// Planned merge: decision flags from the gathered count matrix / owner counts (merge.hip).
+void launch_merge_check(const unsigned long long* all, uint32_t W, uint64_t reg_rows, uint64_t reg_bytes,
+                        const unsigned long long* owns, uint64_t reg_merged, uint32_t* flags, hipStream_t s);
+void launch_mrow_regions_to_cols(const MRow* rows, uint32_t W, uint64_t reg_merged, const unsigned long long* owns,
+                                 uint64_t byte_stride, const uint64_t* dcnt, const uint64_t* dfirst, uint64_t* k0,
+                                 uint64_t* k1, uint64_t* cnt, uint64_t* first, uint64_t* soff, uint32_t* slen,
+                                 unsigned long long* out_n, hipStream_t s);
 void launch_mrow_insert(const MRow* rows, uint64_t R, const uint8_t* bytes, const uint64_t* rbase,
                         const uint64_t* bbase, uint32_t W, uint32_t* state, unsigned long long* cnt,
                         unsigned long long* first, uint64_t T, uint32_t* row_slot, hipStream_t s);  // row_slot nullable
@@ -364,7 +375,8 @@ void launch_row_ids(const uint32_t* row_slot, const uint32_t* slot_id, uint64_t 
                     uint32_t rank, uint32_t* ids, hipStream_t s);  // owns: all-gathered (rows, bytes) per owner
 void launch_scatter_ids(const uint32_t* send_pos, const uint32_t* ids_back, const uint64_t* seg,
                         const unsigned long long* owns, uint32_t W, const uint64_t* cnt, const uint64_t* first,
-                        uint64_t n, uint64_t* dcnt, uint64_t* dfirst, hipStream_t s);  // ids_back: owner-local
+                        uint64_t n, uint64_t* dcnt, uint64_t* dfirst, hipStream_t s, const uint64_t* dn = nullptr,
+                        uint64_t pad = 0);  // ids_back: owner-local; pad > 0: padded ids (owner base o * pad)
 
 // ---- stream-ordered loopback communicator (src/kernels/comm.hip, dist/comm.cpp) ----
 constexpr int LB_MAX_RANKS = 64, LB_RING = 16, LB_XFER_PARTS = 64;

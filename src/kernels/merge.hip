@@ -132,15 +132,24 @@ __global__ void __launch_bounds__(256) wc_owner_count(const uint64_t* k0, const 
 // words: blocks add to the cursor while others read the counts).  A long word
 // is copied in 8-byte words: its arena copy is 8-byte aligned and rounded up
 // (reduce.hip settle_new_long), and its payload slot is rounded the same way.
+// Planned mode (reg_rows > 0, dist/merge.cpp merge_cols_planned): owner o's
+// rows go to the fixed region [o reg_rows, (o + 1) reg_rows) and its bytes to
+// [o reg_bytes, ...), counts unused; a row past its region (rows or bytes) is
+// dropped and sets bit 2 of *ovf (the job redoes the merge with the exact plan).  Rows
+// [0, n) or [0, *dn) with n the bound.
 __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt,
                                                         const uint64_t* first, const uint64_t* soff,
                                                         const uint32_t* slen, const uint8_t* arena, uint64_t n,
-                                                        uint32_t W, const unsigned long long* counts,
-                                                        unsigned long long* cursor, MRow* rows, uint8_t* bytes,
-                                                        uint32_t* send_pos) {
+                                                        const uint64_t* dn, uint32_t W,
+                                                        const unsigned long long* counts, unsigned long long* cursor,
+                                                        MRow* rows, uint8_t* bytes, uint32_t* send_pos,
+                                                        uint64_t reg_rows, uint64_t reg_bytes, uint32_t* ovf) {
   __shared__ unsigned long long base[2 * OWN_MAX], h[2 * OWN_MAX];
   constexpr int PER = OWN_ROWS_PER_BLOCK / 256;
   const uint64_t r0 = (uint64_t)blockIdx.x * OWN_ROWS_PER_BLOCK;
+  if (dn) n = *dn;
+  if (r0 >= n) return;
+  const bool fixed = reg_rows != 0;
   for (uint32_t i = threadIdx.x; i < 2 * W; i += blockDim.x) h[i] = 0;
   __syncthreads();
   uint32_t own[PER];
@@ -158,12 +167,18 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned long long br = 0, bb = 0;  // exclusive prefix of the global per-owner totals
+    unsigned long long br = 0, bb = 0;  // exclusive prefix of the global per-owner totals (or the regions)
     for (uint32_t o = 0; o < W; ++o) {
+      if (fixed) {
+        br = o * reg_rows;
+        bb = o * reg_bytes;
+      }
       base[2 * o] = br + (h[2 * o] ? atomicAdd(&cursor[2 * o], h[2 * o]) : 0);
       base[2 * o + 1] = bb + (h[2 * o + 1] ? atomicAdd(&cursor[2 * o + 1], h[2 * o + 1]) : 0);
-      br += counts[2 * o];
-      bb += counts[2 * o + 1];
+      if (!fixed) {
+        br += counts[2 * o];
+        bb += counts[2 * o + 1];
+      }
     }
   }
   __syncthreads();
@@ -172,6 +187,16 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
     if (own[j] == OWN_MAX) continue;
     const uint64_t i = r0 + threadIdx.x + (uint64_t)j * 256;
     const uint32_t o = own[j];
+    if (fixed) {  // the row and its bytes must fit the owner's regions
+      const uint64_t rp = base[2 * o] + lr[j] - o * reg_rows;
+      const uint64_t bp = base[2 * o + 1] + lb[j] - o * reg_bytes;
+      const uint64_t nb = key_is_hashed(k1[i]) ? ((slen[i] + 7u) & ~7u) : 0u;
+      if (rp >= reg_rows || bp + nb > reg_bytes) {
+        atomicOr(ovf, 4u);  // wc_merge_check's capacity bit
+        if (send_pos) send_pos[i] = 0xFFFFFFFFu;
+        continue;
+      }
+    }
     MRow r;
     r.k0 = k0[i];
     r.k1 = k1[i];
@@ -184,8 +209,8 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
       const uint64_t* src = reinterpret_cast<const uint64_t*>(arena + soff[i]);
       uint64_t* dst = reinterpret_cast<uint64_t*>(bytes + bpos);
       for (uint32_t c = 0; c < (slen[i] + 7u) / 8u; ++c) dst[c] = src[c];
-      unsigned long long bb = 0;  // offset inside owner o's byte payload
-      for (uint32_t q = 0; q < o; ++q) bb += counts[2 * q + 1];
+      unsigned long long bb = fixed ? o * reg_bytes : 0;  // offset inside owner o's byte payload
+      for (uint32_t q = 0; !fixed && q < o; ++q) bb += counts[2 * q + 1];
       r.aoff = (uint32_t)(bpos - bb);
       r.alen = slen[i];
     }
@@ -215,6 +240,10 @@ __global__ void __launch_bounds__(256) wc_mrow_insert(const MRow* rows, uint64_t
                                                       unsigned long long* first, uint64_t T, uint32_t* row_slot) {
   for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < R; r += (uint64_t)gridDim.x * blockDim.x) {
     const MRow me = rows[r];
+    if (me.k1 == K1_EMPTY) {  // padding of a planned exchange's fixed region
+      if (row_slot) row_slot[r] = 0xFFFFFFFFu;
+      continue;
+    }
     const bool hashed = key_is_hashed(me.k1);
     const uint8_t* mb = hashed ? bytes + bbase[source_of(rbase, W, r)] + me.aoff : nullptr;
     uint64_t slot = place_hash(me.k0, me.k1) & (T - 1);
@@ -291,12 +320,15 @@ __global__ void __launch_bounds__(256) wc_mrow_compact(const MRow* rows, const u
 // index of the slot the row merged into.
 // id base = the merged rows of the owners before this one, from the all-gathered
 // (rows, bytes) pairs `owns` (no host round trip).
+// Padding rows (row_slot all ones, planned exchange) get no id.
 __global__ void wc_row_ids(const uint32_t* row_slot, const uint32_t* slot_id, uint64_t R,
                            const unsigned long long* owns, uint32_t rank, uint32_t* ids) {
   uint64_t id_base = 0;
   for (uint32_t p = 0; p < rank; ++p) id_base += owns[2 * p];
-  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < R; r += (uint64_t)gridDim.x * blockDim.x)
-    ids[r] = (uint32_t)(id_base + slot_id[row_slot[r]]);
+  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < R; r += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t sl = row_slot[r];
+    ids[r] = sl == 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)(id_base + slot_id[sl]);
+  }
 }
 
 // Dense merge: local key i (sent as row send_pos[i], whose owner-local index
@@ -305,22 +337,29 @@ __global__ void wc_row_ids(const uint32_t* row_slot, const uint32_t* slot_id, ui
 // (rows, bytes) pairs `owns`) + the index; the owner of send row j is the
 // segment of the send layout (`seg`: W + 1 row starts) holding j.  Ids of one
 // rank's keys are distinct, so plain stores.
+// Planned exchange (pad > 0): ids are padded (owner o's keys at [o pad,
+// o pad + its count)), so the base of owner o is o pad; rows [0, n) or
+// [0, *dn) with n the bound.
 __global__ void __launch_bounds__(256) wc_scatter_ids(const uint32_t* send_pos, const uint32_t* ids_back,
                                                       const uint64_t* seg, const unsigned long long* owns, uint32_t W,
                                                       const uint64_t* cnt, const uint64_t* first, uint64_t n,
-                                                      uint64_t* dcnt, uint64_t* dfirst) {
+                                                      const uint64_t* dn, uint64_t pad, uint64_t* dcnt,
+                                                      uint64_t* dfirst) {
   __shared__ uint64_t lseg[MERGE_MAX_RANKS + 1], lbase[MERGE_MAX_RANKS];
+  if (dn) n = *dn;
   if (threadIdx.x == 0) {
     uint64_t b = 0;
     for (uint32_t o = 0; o < W; ++o) {
-      lbase[o] = b;
-      b += owns[2 * o];
+      lbase[o] = pad ? o * pad : b;
+      if (!pad) b += owns[2 * o];
     }
   }
   for (uint32_t o = threadIdx.x; o <= W; o += blockDim.x) lseg[o] = seg[o];
   __syncthreads();
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t j = send_pos[i];
+    if (j == 0xFFFFFFFFu) continue;  // a row dropped from an overflowing planned region
+    if (pad && ids_back[j] >= pad) continue;  // past the padded id range: the job redoes the merge
     uint32_t lo = 0, hi = W - 1;  // the last owner whose segment starts at or before j
     while (lo < hi) {
       const uint32_t mid = (lo + hi + 1) >> 1;
@@ -353,7 +392,87 @@ __global__ void wc_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* dn
   }
 }
 
+// Planned merge (dist/merge.cpp merge_cols_planned): flags from the
+// all-gathered count matrix (W rows of C = 2W + 2 words: rows / bytes per
+// owner, max offset, pass flags) — bit 0: a rank's last pass needs recovery,
+// bit 1: a rank's key arena overflowed, bit 2: rows or bytes for some owner
+// past the fixed regions — and, from the all-gathered (merged rows, bytes) of
+// every owner (owns, nullable), bit 2 also for merged rows past reg_merged.
+// Every rank reads the same gathered words, so every rank decides the same.
+__global__ void wc_merge_check(const unsigned long long* all, uint32_t W, uint64_t reg_rows, uint64_t reg_bytes,
+                               const unsigned long long* owns, uint64_t reg_merged, uint32_t* flags) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint64_t C = 2ull * W + 2;
+  uint32_t f = 0;
+  if (all) {
+    for (uint32_t p = 0; p < W; ++p) {
+      const unsigned long long* v = all + p * C;
+      f |= (uint32_t)(v[2 * W + 1] & 3u);
+      for (uint32_t o = 0; o < W; ++o)
+        if (v[2 * o] > reg_rows || v[2 * o + 1] > reg_bytes) f |= 4u;
+    }
+  }
+  if (owns)
+    for (uint32_t o = 0; o < W; ++o)
+      if (owns[2 * o] > reg_merged) f |= 4u;
+  if (f) atomicOr(flags, f);
+}
+
+// Planned merge, rank 0: the gathered merged rows sit in fixed regions of
+// reg_merged rows per owner, owner o's first owns[2 o] rows valid (k1 != 0);
+// they become dense key columns at the exclusive prefix of the owners' counts,
+// the long-word references made absolute in the gathered byte buffer (owner o's
+// payload at o * byte_stride); dense merge: counts / first offsets from the
+// reduced padded vectors (id o * reg_merged + j), else from the rows.
+// *out_n = the key count.
+__global__ void __launch_bounds__(256) wc_mrow_regions_to_cols(const MRow* rows, uint32_t W, uint64_t reg_merged,
+                                                              const unsigned long long* owns, uint64_t byte_stride,
+                                                              const uint64_t* dcnt, const uint64_t* dfirst,
+                                                              uint64_t* k0, uint64_t* k1, uint64_t* cnt,
+                                                              uint64_t* first, uint64_t* soff, uint32_t* slen,
+                                                              unsigned long long* out_n) {
+  __shared__ uint64_t pre[MERGE_MAX_RANKS + 1];
+  if (threadIdx.x == 0) {
+    uint64_t b = 0;
+    for (uint32_t o = 0; o < W; ++o) {
+      pre[o] = b;
+      b += min((uint64_t)owns[2 * o], reg_merged);
+    }
+    pre[W] = b;
+    if (blockIdx.x == 0) *out_n = b;
+  }
+  __syncthreads();
+  const uint64_t N = (uint64_t)W * reg_merged;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < N; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t o = (uint32_t)(i / reg_merged);
+    const uint64_t j = i - (uint64_t)o * reg_merged;
+    if (j >= pre[o + 1] - pre[o]) continue;
+    const MRow m = rows[i];
+    const uint64_t at = pre[o] + j;
+    k0[at] = m.k0;
+    k1[at] = m.k1;
+    cnt[at] = dcnt ? dcnt[i] : m.cnt;
+    first[at] = dfirst ? dfirst[i] : m.first;
+    soff[at] = m.alen ? o * byte_stride + m.aoff : 0;
+    slen[at] = m.alen;
+  }
+}
+
 }  // namespace dev
+
+void launch_merge_check(const unsigned long long* all, uint32_t W, uint64_t reg_rows, uint64_t reg_bytes,
+                        const unsigned long long* owns, uint64_t reg_merged, uint32_t* flags, hipStream_t s) {
+  WC_CHECK(W >= 1 && W <= MERGE_MAX_RANKS, "merge_check: 1..64 ranks");
+  hipLaunchKernelGGL(dev::wc_merge_check, dim3(1), dim3(64), 0, s, all, W, reg_rows, reg_bytes, owns, reg_merged, flags);
+}
+void launch_mrow_regions_to_cols(const MRow* rows, uint32_t W, uint64_t reg_merged, const unsigned long long* owns,
+                                 uint64_t byte_stride, const uint64_t* dcnt, const uint64_t* dfirst, uint64_t* k0,
+                                 uint64_t* k1, uint64_t* cnt, uint64_t* first, uint64_t* soff, uint32_t* slen,
+                                 unsigned long long* out_n, hipStream_t s) {
+  WC_CHECK(W >= 1 && W <= MERGE_MAX_RANKS, "regions_to_cols: 1..64 ranks");
+  hipLaunchKernelGGL(dev::wc_mrow_regions_to_cols, dev::mgrid((uint64_t)W * reg_merged), dim3(256), 0, s, rows, W,
+                     reg_merged, owns, byte_stride, dcnt, dfirst, k0, k1, cnt, first, soff, slen, out_n);
+}
 
 void launch_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* slen, uint64_t n, const uint64_t* dn,
                         const uint32_t* pass_flags, uint32_t W, unsigned long long* counts, hipStream_t s) {
@@ -364,11 +483,12 @@ void launch_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* 
 void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
                           const uint64_t* soff, const uint32_t* slen, const uint8_t* arena, uint64_t n, uint32_t W,
                           const unsigned long long* counts, unsigned long long* cursor, MRow* rows, uint8_t* bytes,
-                          uint32_t* send_pos, hipStream_t s) {
+                          uint32_t* send_pos, hipStream_t s, const uint64_t* dn, uint64_t reg_rows, uint64_t reg_bytes,
+                          uint32_t* ovf) {
   const uint64_t blocks = (n + dev::OWN_ROWS_PER_BLOCK - 1) / dev::OWN_ROWS_PER_BLOCK;
   if (n)
     hipLaunchKernelGGL(dev::wc_owner_scatter, dim3((unsigned)blocks), dim3(256), 0, s, k0, k1, cnt, first, soff, slen,
-                       arena, n, W, counts, cursor, rows, bytes, send_pos);
+                       arena, n, dn, W, counts, cursor, rows, bytes, send_pos, reg_rows, reg_bytes, ovf);
 }
 void launch_mrow_insert(const MRow* rows, uint64_t R, const uint8_t* bytes, const uint64_t* rbase,
                         const uint64_t* bbase, uint32_t W, uint32_t* state, unsigned long long* cnt,
@@ -398,10 +518,10 @@ void launch_row_ids(const uint32_t* row_slot, const uint32_t* slot_id, uint64_t 
 }
 void launch_scatter_ids(const uint32_t* send_pos, const uint32_t* ids_back, const uint64_t* seg,
                         const unsigned long long* owns, uint32_t W, const uint64_t* cnt, const uint64_t* first,
-                        uint64_t n, uint64_t* dcnt, uint64_t* dfirst, hipStream_t s) {
+                        uint64_t n, uint64_t* dcnt, uint64_t* dfirst, hipStream_t s, const uint64_t* dn, uint64_t pad) {
   WC_CHECK(W >= 1 && W <= MERGE_MAX_RANKS, "scatter_ids: 1..64 ranks");
   if (n)
     hipLaunchKernelGGL(dev::wc_scatter_ids, dev::mgrid(n), dim3(256), 0, s, send_pos, ids_back, seg, owns, W, cnt,
-                       first, n, dcnt, dfirst);
+                       first, n, dn, pad, dcnt, dfirst);
 }
 }  // namespace wc

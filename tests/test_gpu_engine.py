@@ -145,15 +145,16 @@ def test_region_overflow_reruns():
     assert_same(got, ops.cpu_count(text))
 
 
-@pytest.mark.parametrize("root_rows", [None, "0"])
+@pytest.mark.parametrize("root_rows", [None, "0", "1000000000"])
 @pytest.mark.parametrize("merge_mode", [0, 1])
 @pytest.mark.parametrize("ranks", [1, 2, 3, 4, 8])
 def test_loopback_merge(ranks, merge_mode, root_rows, monkeypatch):
     """Sharding + cross-rank merge at N virtual ranks: shuffle (all-to-all by key
-    owner, gather to rank 0, broadcast with all_ranks; below WC_MERGE_ROOT_ROWS
-    total rows — the default for this small input — every rank sends straight
-    to rank 0 instead) and dense (dictionary union + reduce-scatter +
-    all-gather) protocols."""
+    owner, gather to rank 0, broadcast with all_ranks; with WC_MERGE_ROOT_ROWS
+    set and fewer total rows, every rank sends straight to rank 0 instead — by
+    default the exact merge takes the owner path, which learns the planned
+    merge's caps) and dense (dictionary union + reduce-scatter + all-gather)
+    protocols."""
     if root_rows is not None:
         monkeypatch.setenv("WC_MERGE_ROOT_ROWS", root_rows)  # 0: always the owner exchange
     rng = np.random.default_rng(ranks)
@@ -177,6 +178,52 @@ def test_loopback_stream_ordered():
     assert ret.value == 1, "a collective call waited on the host for a peer's stream"
     assert pend.value == 1, "rank 0's collective completed before rank 1's stream reached it"
     assert ok.value == 1
+
+
+@pytest.mark.parametrize("merge_mode", [0, 1])
+@pytest.mark.parametrize("ranks", [1, 3, 8])
+def test_planned_merge_virtual_ranks(ranks, merge_mode):
+    """The planned merge (fixed exchange regions learned from the first exact
+    merge, no host round trip; dist/merge.cpp merge_cols_planned) at W virtual
+    ranks: every job after the first runs planned, and the validated job's
+    table equals the oracle of the whole stream (WC_MERGE_ALWAYS covers W = 1
+    in a child process)."""
+    per = 6 << 20
+    code = (
+        "import sys\n"
+        "from cuda_mapreduce_amd import ops\n"
+        f"res, rk = ops.virtual_bench({ranks}, {per}, seed=5, vocab=30000, steps=3, warmup=1, "
+        f"chunk_bytes=2 << 20, merge_mode={merge_mode})\n"
+        f"want = ops.cpu_count_synth({ranks} * {per}, 0, seed=5, vocab=30000)\n"
+        "assert res.words == want.words and res.counts.tolist() == want.counts.tolist(), 'table'\n"
+        "assert res.first_off.tolist() == want.first_off.tolist(), 'first offsets'\n"
+        "assert rk[0]['merges_planned'] >= 4 and rk[0]['merge_redos'] == 0, rk[0]\n"
+        "print('ok')\n"
+    )
+    env = dict(os.environ, WC_MERGE_ALWAYS="1")
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, timeout=120)
+    assert out.returncode == 0 and b"ok" in out.stdout, out.stderr.decode()[-2000:]
+
+
+@pytest.mark.parametrize("merge_mode", [0, 1])
+def test_planned_merge_overflow_redo(merge_mode):
+    """Fixed regions too small (WC_MERGE_CAP_ROWS=64, a test switch): every
+    planned merge overflows, all ranks see it in the gathered words and redo
+    the merge exactly — the result stays exact."""
+    per = 4 << 20
+    code = (
+        "from cuda_mapreduce_amd import ops\n"
+        f"res, rk = ops.virtual_bench(4, {per}, seed=6, vocab=20000, steps=2, warmup=1, chunk_bytes=2 << 20, "
+        f"merge_mode={merge_mode})\n"
+        f"want = ops.cpu_count_synth(4 * {per}, 0, seed=6, vocab=20000)\n"
+        "assert res.words == want.words and res.counts.tolist() == want.counts.tolist(), 'table'\n"
+        "assert res.first_off.tolist() == want.first_off.tolist(), 'first offsets'\n"
+        "assert rk[0]['merge_redos'] >= 3, rk[0]\n"
+        "print('ok')\n"
+    )
+    env = dict(os.environ, WC_MERGE_CAP_ROWS="64")
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, timeout=120)
+    assert out.returncode == 0 and b"ok" in out.stdout, out.stderr.decode()[-2000:]
 
 
 def test_loopback_merge_host_waits():
