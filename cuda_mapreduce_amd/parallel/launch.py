@@ -135,19 +135,43 @@ def _stop(procs: List[subprocess.Popen], ranks, grace_s: float) -> None:
             procs[r].wait()
 
 
+def _proc_start_epoch(pid: int) -> float:
+    """Start time of a process (seconds since the epoch) from /proc; 0 if unknown."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            ticks = int(f.read().rsplit(")", 1)[1].split()[19])
+        with open("/proc/stat") as f:
+            btime = next(int(l.split()[1]) for l in f if l.startswith("btime"))
+        return btime + ticks / os.sysconf("SC_CLK_TCK")
+    except (OSError, ValueError, StopIteration, IndexError):
+        return 0.0
+
+
 def rdzv_dir() -> str:
     d = os.environ.get("WC_RDZV_DIR")
     if d:
         return d
-    # torch.distributed.run: every local rank is a child of the same agent
-    d = os.path.join(tempfile.gettempdir(),
-                     f"wc_rdzv_{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}")
+    # torch.distributed.run: every local rank is a child of the same agent; the
+    # file rendezvous is node-local, so a multi-node job is refused (the RCCL
+    # id would have to travel through the agent's store instead)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if world > local:
+        raise RuntimeError(f"WORLD_SIZE {world} > LOCAL_WORLD_SIZE {local}: the file rendezvous of the RCCL id is "
+                           "single-node only (set WC_RDZV_DIR to a shared directory to override)")
+    run = os.environ.get("TORCHELASTIC_RUN_ID", "")
+    tag = run if run and run != "none" else str(os.getppid())
+    d = os.path.join(tempfile.gettempdir(), f"wc_rdzv_{tag}_{os.environ.get('MASTER_PORT', '0')}")
     os.makedirs(d, exist_ok=True)
     return d
 
 
 def rendezvous_uid(rank: int, make_uid, timeout_s: float = 120.0, name: str = "rccl_uid") -> bytes:
-    """Rank 0 publishes ``make_uid()`` (atomic rename); the others wait for it."""
+    """Rank 0 publishes ``make_uid()`` (atomic rename); the others wait for it.
+
+    A file left by an earlier job with the same directory (same agent pid and
+    port, crashed before its cleanup) is older than this job's agent: ranks
+    ignore any id file written before their parent process started."""
     path = os.path.join(rdzv_dir(), name)
     if rank == 0:
         uid = make_uid()
@@ -156,12 +180,14 @@ def rendezvous_uid(rank: int, make_uid, timeout_s: float = 120.0, name: str = "r
             f.write(uid)
         os.replace(tmp, path)
         return uid
+    not_before = _proc_start_epoch(os.getppid()) - 1.0 if not os.environ.get("WC_RDZV_DIR") else 0.0
     t0 = time.time()
     while True:
         try:
+            fresh = os.stat(path).st_mtime >= not_before
             with open(path, "rb") as f:
                 uid = f.read()
-            if len(uid) == 128:
+            if fresh and len(uid) == 128:
                 return uid
         except FileNotFoundError:
             pass

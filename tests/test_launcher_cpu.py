@@ -106,6 +106,36 @@ def test_file_rendezvous(tmp_path, monkeypatch):
         L.rendezvous_uid(1, lambda: uid, timeout_s=0.2)
 
 
+def test_rendezvous_ignores_stale_id_and_refuses_multinode(tmp_path, monkeypatch):
+    """Under torch.distributed.run (no WC_RDZV_DIR): the directory is keyed on the
+    job (TORCHELASTIC_RUN_ID, else the agent pid) and the port; an id file older
+    than the agent (a crashed earlier job's) is ignored; a multi-node world is
+    refused (the file rendezvous is node-local)."""
+    from cuda_mapreduce_amd.parallel import launch as L
+
+    monkeypatch.delenv("WC_RDZV_DIR", raising=False)
+    monkeypatch.setattr(L.tempfile, "gettempdir", lambda: str(tmp_path))
+    monkeypatch.setenv("MASTER_PORT", "29999")
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "job42")
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    d = L.rdzv_dir()
+    assert os.path.basename(d) == "wc_rdzv_job42_29999"
+    stale = os.path.join(d, "rccl_uid")
+    with open(stale, "wb") as f:
+        f.write(b"s" * 128)
+    os.utime(stale, (1, 1))  # written long before this process's parent started
+    with pytest.raises(TimeoutError):
+        L.rendezvous_uid(1, lambda: b"x" * 128, timeout_s=0.2)
+    fresh = bytes(range(128))
+    assert L.rendezvous_uid(0, lambda: fresh) == fresh
+    assert L.rendezvous_uid(1, lambda: b"x" * 128, timeout_s=2) == fresh
+    monkeypatch.setenv("WORLD_SIZE", "16")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    with pytest.raises(RuntimeError, match="single-node"):
+        L.rdzv_dir()
+
+
 def test_launcher_imports_no_engine():
     # the launcher half of bench.py must not load libwc.so (no HIP runtime in the parent)
     code = ("import sys; sys.path.insert(0, %r); import bench; a = bench.parse(['--gpus', '2']);"
