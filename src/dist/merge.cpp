@@ -537,7 +537,8 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
   const bool have = R == 0 || all_ranks;
   A.reserve(2 * RR * sizeof(MRow) + 2 * RB + T * (4 + 16) + RR * sizeof(MRow) + (size_t)GR * sizeof(MRow) +
             (size_t)W * RB + (have ? GR * (5 * 8 + 4) : 0) + (4 * (size_t)W + 8) * 8 + 64 * 1024 +
-            (dense ? (nb + 2 * RR + T) * 4 + GR * 8 * 4 + 16 * 256 : 0));
+            // dense: send_pos, row_slot, ids, ids_back, slot_id (u32); vc, vf, dcnt, dfirst, scnt, sfirst (u64)
+            (dense ? (nb + 3 * RR + T) * 4 + (4 * GR + 2 * (uint64_t)Gr) * 8 + 16 * 256 : 0));
   A.reset();
   MRow* send_rows = take_aligned<MRow>(A, RR);
   uint8_t* send_bytes = take_aligned<uint8_t>(A, RB);

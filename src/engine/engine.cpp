@@ -852,7 +852,10 @@ void Engine::reset() {
   im.fo_hist_ok = false;
   if (im.copy_used) WC_HIP_CHECK(hipStreamSynchronize(im.copy_s));  // a failed stream may have left copies
   im.copy_used = false;
+  const uint32_t planned = im.st.merges_planned, redos = im.st.merge_redos;  // engine-lifetime counters
   im.st = Stats{};
+  im.st.merges_planned = planned;
+  im.st.merge_redos = redos;
   im.max_end = 0;
   im.ev_n = 0;
   im.hot_valid = false;  // each job samples its own hot words
