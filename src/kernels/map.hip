@@ -892,7 +892,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
         atomicMin(&L.off[s2], o2);
       }
       const bool d1 = h1 && s1 < 0, d2 = TWO && h2 && s2 < 0;
-      emit_two(L.bcur, a, rout, d1, ha & bmask, a0, n1, o1, n1, d2, hb & bmask, b0, n2, o2, n2);
+      emit_two_short(L.bcur, a, rout, d1, ha & bmask, a0, o1, n1, d2, hb & bmask, b0, o2, n2);
       if constexpr (ST) {
         my_direct += (uint32_t)(__popcll(__ballot(d1)) + (TWO ? __popcll(__ballot(d2)) : 0));
         const uint32_t nh = (uint32_t)(__popcll(__ballot(s1 >= 0)) + __popcll(__ballot(s2 >= 0)));
@@ -904,11 +904,12 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     const uint64_t s1m = dm >> 1, s2m = s1m | (s1m >> 1), s4m = s2m | (s2m >> 2);
     const uint32_t near7 = (uint32_t)(s4m | (s4m >> 3));
     const uint32_t sbits = bits & near7, obits = bits & ~near7;
-    uint32_t tot_s, tot_o;
-    const uint32_t ks0 = wave_excl_small((uint32_t)__popc(sbits), tot_s);
-    const uint32_t ko0 = wave_excl_small((uint32_t)__popc(obits), tot_o);
-    tot_s = __builtin_amdgcn_readfirstlane(tot_s);
-    tot_o = __builtin_amdgcn_readfirstlane(tot_o);
+    // both class counts in one packed DPP scan (short | other << 16)
+    const uint32_t cnt2 = (uint32_t)__popc(sbits) | ((uint32_t)__popc(obits) << 16);
+    const uint32_t inc2 = wave_incl_sum(cnt2), exc2 = inc2 - cnt2;
+    const uint32_t tot2 = (uint32_t)__builtin_amdgcn_readlane((int)inc2, 63);
+    const uint32_t ks0 = exc2 & 0xFFFFu, ko0 = exc2 >> 16;
+    const uint32_t tot_s = tot2 & 0xFFFFu, tot_o = tot2 >> 16;
     const uint32_t wave_total = tot_s + tot_o;
     clk.lap(MS_MASK);
     if (wave_total <= (uint32_t)MAP_LIST) {

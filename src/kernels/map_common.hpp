@@ -80,6 +80,22 @@ __device__ __forceinline__ uint32_t delim_bits4(uint32_t x) {
 // per token-list iteration.)
 __device__ __forceinline__ uint32_t ffbl_raw(uint32_t x) { return (uint32_t)__builtin_ctz(x); }
 
+// Wave-wide inclusive prefix sum (wave64) by DPP: four in-row shifts (16-lane
+// rows), then row 15 / row 31 broadcasts — six v_add_u32_dpp, no LDS, no
+// ballots.  The map scans its two token-class counts PACKED in one word
+// (class counts <= 32 per lane, <= 2048 per wave: no carry between halves).
+// (The ballot form below costs five ballots + mbcnt pairs per value: ~4x the
+// VALU cycles at two values per unit, ~5 % of the map's VALU.)
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false); // row_bcast:15 -> rows 1, 3
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false); // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
 // Wave-wide exclusive prefix sum of a small per-lane value v < 32 (bit
 // decomposition over ballots: no cross-lane shuffles); total = wave sum.
 __device__ __forceinline__ uint32_t wave_excl_small(uint32_t v, uint32_t& total) {
@@ -203,6 +219,20 @@ __device__ __forceinline__ void emit_two(uint32_t* bcur, const MapArgs& a, const
   if (d2) p2 = atomicAdd(&bcur[b2], s2 ? 1u : 0x10000u);
   if (d1) put_record(a, o, b1, p1, s1, x0, x1, 1, o1);
   if (d2) put_record(a, o, b2, p2, s2, y0, y1, 1, o2);
+}
+
+// emit_two for words of 1..7 bytes (k1 = the length): a Rec16 unless the
+// word's last byte is 0x00 — one 64-bit shift and compare per word instead of
+// rec16_inline's two length classes (a divergent branch pair in the short step).
+__device__ __forceinline__ void emit_two_short(uint32_t* bcur, const MapArgs& a, const RecOut& o, bool d1, uint32_t b1,
+                                               uint64_t x0, uint32_t o1, uint32_t n1, bool d2, uint32_t b2,
+                                               uint64_t y0, uint32_t o2, uint32_t n2) {
+  const bool s1 = (x0 >> ((8u * n1 - 8u) & 63u)) != 0, s2 = (y0 >> ((8u * n2 - 8u) & 63u)) != 0;
+  uint32_t p1 = 0, p2 = 0;
+  if (d1) p1 = atomicAdd(&bcur[b1], s1 ? 1u : 0x10000u);
+  if (d2) p2 = atomicAdd(&bcur[b2], s2 ? 1u : 0x10000u);
+  if (d1) put_record(a, o, b1, p1, s1, x0, n1, 1, o1);
+  if (d2) put_record(a, o, b2, p2, s2, y0, n2, 1, o2);
 }
 
 // Key of a LONG token (>= 16 bytes) of known length 16..30 from its LDS
