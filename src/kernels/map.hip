@@ -59,6 +59,7 @@ constexpr int HALO = 64;               // bytes past the unit kept in LDS
 // buffer starts 16-byte aligned, so the unit commit's ds_write_b128 are aligned
 // (2136-byte buffers put odd waves at 8 mod 16: SQ_LDS_UNALIGNED_STALL 3.0e7 / GiB)
 constexpr int BUF = (UNIT + HALO + 24 + 15) / 16 * 16;
+constexpr int MAP_DEF_CAP = 256;       // deferred LONG entries per wave and round
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr int GS = HOT_GROUP_SLOTS;    // slots per group
 constexpr int NG = HOT_GROUPS;         // groups
@@ -76,8 +77,10 @@ static_assert(MAP_SLOTS % MAP_THREADS == 0 && (NG & (NG - 1)) == 0, "table geome
 static_assert(UNIT <= 2048, "list entries hold 11-bit unit-relative positions");
 
 // Profiling builds only (tools/variants.sh -DWC_MAP_ABLATE=N; results are NOT
-// valid): 1 tokenize + list only, 2 + keys and hashes, 3 + table probes and
-// hit counts (misses dropped).
+// valid): 5 text stream + LDS commit only, 4 + delimiter masks and token
+// starts, 6 + the token list, 7 + the steps' entry reads, 1 + key windows,
+// 2 + keys and hashes, 3 + table probes and hit counts (misses dropped);
+// 8 / 9: the partial short / general step of each round dropped.
 #ifndef WC_MAP_ABLATE
 #define WC_MAP_ABLATE 0
 #endif
@@ -621,12 +624,14 @@ struct alignas(16) MapLds {
   uint32_t off[MAP_SLOTS];              // chunk-relative first offset in the block
   alignas(16) uint64_t sig[MAP_SLOTS];  // hot table image (read-only while tokens stream); 0 = empty
   uint16_t list[MAP_WAVES][MAP_LIST];
+  uint16_t dlist[MAP_WAVES][MAP_DEF_CAP];  // deferred LONG entries of a round: pos | (len - 16) << 11 | prev << 15
   uint32_t bcur[MAX_REC_BUCKETS];       // records appended to each bucket's sub-region (Rec16 | Rec << 16)
-  alignas(16) uint8_t buf[MAP_WAVES][BUF];
+  alignas(16) uint8_t buf[MAP_WAVES][2][BUF];  // two unit slots per wave: the current unit and the one before
   uint32_t next_unit;
   unsigned long long used, tokens;
 };
 static_assert(sizeof(MapLds) + 8 * MAP_STAMP_N <= 160 * 1024, "one map block per CU");
+static_assert(MAP_DEF_CAP >= 128 + UNIT / 17, "a round defers at most 127 carried + UNIT / 17 LONG tokens");
 static_assert(GS == 2, "pair-packed two-word words: 2-slot groups");
 
 // Index (0..3) of the first of a key's four candidate signatures equal to sig, else -1.
@@ -662,7 +667,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   // the table image, built in this block's LDS (the unit buffers and token
   // lists are its scratch until the first unit)
   static_assert(sizeof(L.buf) >= 4 * (SEL_BINS + 20) && sizeof(L.list) >= 4 * NG, "image scratch");
-  build_image(h, L.sig, reinterpret_cast<uint32_t*>(&L.buf[0][0]), reinterpret_cast<uint32_t*>(&L.list[0][0]));
+  build_image(h, L.sig, reinterpret_cast<uint32_t*>(&L.buf[0][0][0]), reinterpret_cast<uint32_t*>(&L.list[0][0]));
   uint64_t u_begin, u_end;
   unit_range(a.chunk_len, gridDim.x, blockIdx.x, u_begin, u_end);
   if (tid == 0) {
@@ -674,8 +679,9 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   const uint32_t bmask = (1u << a.log2_rec_buckets) - 1u;
   const uint32_t nb = 1u << a.log2_rec_buckets;
   const RecOut rout = rec_out(a);
-  uint8_t* buf = L.buf[wave];
+  uint8_t* const bufw = &L.buf[wave][0][0];  // both unit slots: slot s at s * BUF
   uint16_t* list = L.list[wave];
+  uint16_t* dlist = L.dlist[wave];
   uint32_t my_tokens = 0, my_direct = 0;
   uint64_t sink = 0;  // profiling builds: keeps ablated work alive
   auto grab = [&]() -> uint32_t {
@@ -699,17 +705,24 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   const uint64_t t_begin = clk.t;
   const uint64_t rt_begin = ST ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz, one clock for every XCD
   const uint32_t pbase = lane * MAP_BPL;
-  uint32_t ndef = 0;  // deferred LONG entries of the current round (list[0, ndef))
+  uint32_t ndef = 0;  // deferred LONG entries of the current round (dlist[0, ndef))
+  // Unit slots: the current unit's text at byte cbo of bufw, the previous
+  // unit's (entries carried over from its round) at pbo; their chunk offsets.
+  uint32_t cbo = 0, pbo = BUF;
+  uint64_t cu0 = 0, pu0 = 0;
 
   // LONG words of the round (>= 16 bytes): keys from LDS windows (16..30
-  // bytes) or an 8-byte SWAR scan (>= 31), one record each; 64 per pass, the
-  // unit still in `buf`.
-  auto run_deferred = [&](uint64_t u0) {
+  // bytes) or an 8-byte SWAR scan (>= 31), one record each; 64 per pass, both
+  // unit slots still in LDS.
+  auto run_deferred = [&]() {
     wave_sync();
     for (uint32_t c = 0; c < ndef; c += 64) {
       const bool hv = c + lane < ndef;
-      const uint32_t e = hv ? list[c + lane] : 0u;
-      const uint32_t q = e & 0x7FFu, n = e >> 11;
+      const uint32_t e = hv ? dlist[c + lane] : 0u;
+      const uint32_t q = e & 0x7FFu, n = ((e >> 11) & 0xFu) + 16u;
+      const bool old = (e >> 15) != 0;
+      const uint8_t* buf = bufw + (old ? pbo : cbo);
+      const uint64_t u0 = old ? pu0 : cu0;
       if (hv) {
         uint64_t k0, k1;
         uint32_t len = n;
@@ -745,12 +758,26 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     wave_sync();
   };
 
+  // Carried entries: a round runs only FULL steps (128 entries) of each token
+  // class; the remainder (< 128 entries) waits in the list for the next
+  // round, whose unit goes to the other slot, so every step but the block's
+  // last ones is full.  A remainder holding entries carried from the round
+  // before (two units back: that slot is about to be overwritten) or of the
+  // wave's last unit runs at once.  Carried entries go to the front of their
+  // class in the next list; an entry below a step's `cut` index reads the
+  // previous slot and offsets.
+  uint32_t cs = 0, cs_from = 0, co = 0, co_from = 0;  // carried short / other entries and where they wait
   uint32_t u = grab();
   prefetch(u);
   uint32_t nu = u == NONE ? NONE : grab();
   while (u != NONE) {
-    // ---- commit the prefetched unit, build its masks and token count ----
-    const uint64_t u0 = (uint64_t)u * UNIT;
+    // ---- commit the prefetched unit into the free slot, masks and token count ----
+    pbo = cbo;
+    cbo = BUF - cbo;
+    pu0 = cu0;
+    cu0 = (uint64_t)u * UNIT;
+    const uint64_t u0 = cu0;
+    uint8_t* const buf = bufw + cbo;
     wave_sync();  // the previous unit's reads are done
     reinterpret_cast<uint4*>(&buf[pbase])[0] = p0;
     reinterpret_cast<uint4*>(&buf[pbase])[1] = p1;
@@ -760,10 +787,22 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     const uint32_t hb = halo_bits(ph16);
     prefetch(nu);  // the LDS copy is first read by the steps, behind the list round's wave_sync
     clk.lap(MS_COMMIT);
+    if (WC_MAP_ABLATE == 5) {  // stream + commit only
+      sink ^= c0.x ^ c1.w ^ hb ^ pv;
+      u = nu;
+      nu = u == NONE ? NONE : grab();
+      continue;
+    }
     uint64_t dm;
     uint32_t bits;
     unit_masks(c0, c1, hb, pv, u0, pbase, a.chunk_len, dm, bits);
     my_tokens += __popc(bits);
+    if (WC_MAP_ABLATE == 4) {  // + masks and token starts, no list / steps
+      sink ^= dm ^ wave_incl_sum(bits);
+      u = nu;
+      nu = u == NONE ? NONE : grab();
+      continue;
+    }
     const uint32_t dlo = (uint32_t)dm, dhi = (uint32_t)(dm >> 32);
     // delimiter bits from the token start on (i < 32: one funnel shift); none
     // within 31 bytes -> MAP_LONG: ffbl of 0 is all ones, and the u16 entry
@@ -773,15 +812,20 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     // trip; a tail of <= 64 entries takes the one-entry step.  General form:
     // any length (two-word signatures are confirmed by their group's side
     // word, LONG words deferred to the round end).
-    auto step = [&](uint32_t j, uint32_t hi, auto two_c) {
+    auto step = [&](uint32_t j, uint32_t hi, uint32_t cut, auto two_c) {
       constexpr bool TWO = decltype(two_c)::value;
       const bool h1 = j + lane < hi, h2 = TWO && j + 64 + lane < hi;
       const uint32_t r1 = list[j + lane], r2 = TWO ? list[j + 64 + lane] : 0u;  // unconditional (see step_short)
       const uint32_t e1 = h1 ? r1 : 0u, e2 = h2 ? r2 : 0u;
+      if (WC_MAP_ABLATE == 7) {
+        sink ^= e1 ^ e2;
+        return;
+      }
       const uint32_t q1 = e1 & 0x7FFu, q2 = e2 & 0x7FFu, n1 = e1 >> 11, n2 = e2 >> 11;
+      const bool old1 = j + lane < cut, old2 = TWO && j + 64 + lane < cut;  // carried from the previous unit
       uint64_t w10, w11, w20 = 0, w21 = 0;
-      window16(buf, q1, w10, w11);
-      if (TWO) window16(buf, q2, w20, w21);
+      window16(bufw, q1 + (old1 ? pbo : cbo), w10, w11);
+      if (TWO) window16(bufw, q2 + (old2 ? pbo : cbo), w20, w21);
       if (WC_MAP_ABLATE == 1) {
         sink ^= w10 ^ w21;
         return;
@@ -812,7 +856,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
         s1 = ma < 0 ? -1 : (int)slot_of(ma < GS ? ga1 : ga2, ma & (GS - 1));
       }
       clk.lap(MS_PROBE);
-      const uint32_t o1 = (uint32_t)(u0 + q1), o2 = (uint32_t)(u0 + q2);
+      const uint32_t o1 = (uint32_t)(old1 ? pu0 : cu0) + q1, o2 = (uint32_t)(old2 ? pu0 : cu0) + q2;
       if (s1 >= 0) {
         atomicAdd(&L.cnt[s1], 1u);  // results unused: no-return ds_add / ds_min
         atomicMin(&L.off[s1], o1);
@@ -827,14 +871,14 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
       emit_two(L.bcur, a, rout, d1, ha & bmask, a0, a1, o1, n1, d2, hb & bmask, b0, b1, o2, n2);
       const bool f1 = h1 && !in1, f2 = TWO && h2 && !in2;
       const uint64_t mf1 = __ballot(f1), mf2 = TWO ? __ballot(f2) : 0ull;
-      if (mf1 | mf2) {  // entries before j are consumed: ndef <= j
+      if (mf1 | mf2) {  // LONG entries (length field 16..31) to the round's deferred list
         const uint32_t r1 =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(mf1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mf1, 0u));
         const uint32_t r2 =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(mf2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mf2, 0u));
         const uint32_t n1c = (uint32_t)__popcll(mf1);
-        if (f1) list[ndef + r1] = (uint16_t)e1;
-        if (f2) list[ndef + n1c + r2] = (uint16_t)e2;
+        if (f1) dlist[ndef + r1] = (uint16_t)(q1 | ((n1 - 16u) << 11) | (old1 ? 0x8000u : 0u));
+        if (f2) dlist[ndef + n1c + r2] = (uint16_t)(q2 | ((n2 - 16u) << 11) | (old2 ? 0x8000u : 0u));
         ndef += n1c + (uint32_t)__popcll(mf2);
       }
       if constexpr (ST) {
@@ -851,15 +895,24 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     // key (bytes | len << 56): one 8-byte window (three LDS dwords, two
     // funnels), no tail, no side-word confirmation, and every miss a 16-byte
     // record candidate.  3 of 4 tokens of English-like text take it.
-    auto step_short = [&](uint32_t j, uint32_t hi, auto two_c) {
+    auto step_short = [&](uint32_t j, uint32_t hi, uint32_t cut, auto two_c) {
       constexpr bool TWO = decltype(two_c)::value;
       const bool h1 = j + lane < hi, h2 = TWO && j + 64 + lane < hi;
       // unconditional entry reads (no exec-mask branch): past `hi` they read a
-      // later entry, the next wave's list or bcur — inside MapLds, and masked by h1 / h2
+      // later entry, the next wave's list or the deferred lists — inside MapLds, and masked by h1 / h2
       const uint32_t r1 = list[j + lane], r2 = TWO ? list[j + 64 + lane] : 0u;
       const uint32_t e1 = h1 ? r1 : 0u, e2 = h2 ? r2 : 0u;
+      if (WC_MAP_ABLATE == 7) {
+        sink ^= e1 ^ e2;
+        return;
+      }
       const uint32_t q1 = e1 & 0x7FFu, q2 = e2 & 0x7FFu, n1 = e1 >> 11, n2 = e2 >> 11;
-      const uint64_t w1 = window8(buf, q1), w2 = TWO ? window8(buf, q2) : 0ull;
+      const bool old1 = j + lane < cut, old2 = TWO && j + 64 + lane < cut;  // carried from the previous unit
+      const uint64_t w1 = window8(bufw, q1 + (old1 ? pbo : cbo)), w2 = TWO ? window8(bufw, q2 + (old2 ? pbo : cbo)) : 0ull;
+      if (WC_MAP_ABLATE == 1) {
+        sink ^= w1 ^ w2;
+        return;
+      }
       // k0: the first n bytes (n <= 7: shift by 64 - 8 n in [8, 56]; n = 0 of an empty lane clamps to 1)
       const uint32_t sa = 64u - 8u * max(n1, 1u), sb = 64u - 8u * max(n2, 1u);
       const uint64_t a0 = (w1 << sa) >> sa, b0 = TWO ? (w2 << sb) >> sb : 0ull;
@@ -869,6 +922,10 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
       hot_groups(ha, ga1, ga2);
       if (TWO) hot_groups(hb, gb1, gb2);
       clk.lap(MS_KEYS);
+      if (WC_MAP_ABLATE == 2) {
+        sink ^= as ^ bs ^ ga2 ^ gb2;
+        return;
+      }
       const u64x2* S = reinterpret_cast<const u64x2*>(L.sig);
       int s1 = -1, s2 = -1;
       {  // a pair's side word never equals a short signature: plain 4-slot match
@@ -882,7 +939,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
         s1 = ma < 0 ? -1 : (int)slot_of(ma < GS ? ga1 : ga2, ma & (GS - 1));
       }
       clk.lap(MS_PROBE);
-      const uint32_t o1 = (uint32_t)(u0 + q1), o2 = (uint32_t)(u0 + q2);
+      const uint32_t o1 = (uint32_t)(old1 ? pu0 : cu0) + q1, o2 = (uint32_t)(old2 ? pu0 : cu0) + q2;
       if (s1 >= 0) {
         atomicAdd(&L.cnt[s1], 1u);
         atomicMin(&L.off[s1], o1);
@@ -891,6 +948,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
         atomicAdd(&L.cnt[s2], 1u);
         atomicMin(&L.off[s2], o2);
       }
+      if (WC_MAP_ABLATE == 3) return;
       const bool d1 = h1 && s1 < 0, d2 = TWO && h2 && s2 < 0;
       emit_two_short(L.bcur, a, rout, d1, ha & bmask, a0, o1, n1, d2, hb & bmask, b0, o2, n2);
       if constexpr (ST) {
@@ -912,10 +970,22 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     const uint32_t tot_s = tot2 & 0xFFFFu, tot_o = tot2 >> 16;
     const uint32_t wave_total = tot_s + tot_o;
     clk.lap(MS_MASK);
-    if (wave_total <= (uint32_t)MAP_LIST) {
-      // one list round: short entries at [0, tot_s), the others at [tot_s, total);
-      // one loop per class (no per-entry class select: 9 instead of 16 VALU per entry)
-      uint32_t ks = ks0, ko = tot_s + ko0, sb = sbits, ob = obits;
+    const bool last = nu == NONE;  // the wave's last unit: nothing is carried past it
+    if (cs + co + wave_total <= (uint32_t)MAP_LIST) {
+      // one list round: short entries at [0, ns) — the cs carried ones first —
+      // the others at [ns, no_end) — the co carried ones first; one loop per
+      // class (no per-entry class select: 9 instead of 16 VALU per entry)
+      const uint32_t ns = cs + tot_s, ob0 = ns, no_end = ns + co + tot_o;
+      {  // carried entries to the front of their class (read before any write: one wave, in order)
+        const uint32_t c0 = list[cs_from + lane], c1 = list[cs_from + 64 + lane];
+        const uint32_t d0 = list[co_from + lane], d1 = list[co_from + 64 + lane];
+        wave_sync();
+        if (lane < cs) list[lane] = (uint16_t)c0;
+        if (lane + 64 < cs) list[64 + lane] = (uint16_t)c1;
+        if (lane < co) list[ob0 + lane] = (uint16_t)d0;
+        if (lane + 64 < co) list[ob0 + 64 + lane] = (uint16_t)d1;
+      }
+      uint32_t ks = cs + ks0, ko = ob0 + co + ko0, sb = sbits, ob = obits;
       while (sb) {
         const uint32_t i = __ffs(sb) - 1;
         sb &= sb - 1;
@@ -928,20 +998,53 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
       }
       wave_sync();
       clk.lap(MS_LIST);
+      if (WC_MAP_ABLATE == 6) {  // + the token list, no steps
+        sink ^= list[lane];
+        wave_sync();
+        cs = co = 0;
+        u = nu;
+        nu = u == NONE ? NONE : grab();
+        continue;
+      }
+      // full steps; a remainder waits for the next round unless it holds
+      // carried entries (their slot is overwritten next) or this is the last unit
+      // (explicit loops: the same steps behind a lambda made the kernel spill ~80 VGPRs)
       uint32_t j = 0;
-      for (; j + 64 < tot_s; j += 128) step_short(j, tot_s, std::true_type{});
-      if (j < tot_s) step_short(j, tot_s, std::false_type{});
-      const uint32_t total = tot_s + tot_o;
-      for (j = tot_s; j + 64 < total; j += 128) step(j, total, std::true_type{});
-      if (j < total) step(j, total, std::false_type{});
+      for (; j + 128 <= ns; j += 128) step_short(j, ns, cs, std::true_type{});
+      if (j < ns && (j < cs || last)) {
+        if (j + 64 < ns) step_short(j, ns, cs, std::true_type{});
+        else step_short(j, ns, cs, std::false_type{});
+        j = ns;
+      }
+      cs_from = j;
+      cs = ns - j;
+      const uint32_t ocut = ob0 + co;
+      for (j = ob0; j + 128 <= no_end; j += 128) step(j, no_end, ocut, std::true_type{});
+      if (j < no_end && (j < ocut || last)) {
+        if (j + 64 < no_end) step(j, no_end, ocut, std::true_type{});
+        else step(j, no_end, ocut, std::false_type{});
+        j = no_end;
+      }
+      co_from = j;
+      co = no_end - j;
       if (ndef) {
-        run_deferred(u0);
+        run_deferred();
         clk.lap(MS_SLOW);
       }
       wave_sync();  // entries read before the next unit's list overwrites them
     } else {
-      // more than MAP_LIST tokens in the unit (runs of 1-byte words): rounds of
-      // MAP_LIST entries in stream order, every entry on the general step
+      // more than MAP_LIST tokens with the carried ones (runs of 1-byte
+      // words): the carried entries first, then rounds of MAP_LIST entries of
+      // the unit in stream order, every entry on the general step
+      // all carried: the cut past them (one general step per class, < 128 entries each)
+      if (cs) step(cs_from, cs_from + cs, MAP_LIST, std::true_type{});
+      if (co) step(co_from, co_from + co, MAP_LIST, std::true_type{});
+      cs = co = 0;
+      if (ndef) {
+        run_deferred();
+        clk.lap(MS_SLOW);
+      }
+      wave_sync();
       uint32_t k = ks0 + ko0;  // the lane's first entry among all tokens of the unit
       for (uint32_t base = 0; base < wave_total; base += MAP_LIST) {
         const uint32_t lim = base + MAP_LIST;
@@ -956,10 +1059,10 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
         const uint32_t round_n = min(wave_total - base, (uint32_t)MAP_LIST);
         clk.lap(MS_LIST);
         uint32_t j = 0;
-        for (; j + 64 < round_n; j += 128) step(j, round_n, std::true_type{});
-        if (j < round_n) step(j, round_n, std::false_type{});
+        for (; j + 64 < round_n; j += 128) step(j, round_n, 0u, std::true_type{});
+        if (j < round_n) step(j, round_n, 0u, std::false_type{});
         if (ndef) {
-          run_deferred(u0);
+          run_deferred();
           clk.lap(MS_SLOW);
         }
         wave_sync();  // entries read before the next round overwrites them
