@@ -296,6 +296,7 @@ int run(const Cli& c) {
       stages.finalize_ms = std::max(stages.finalize_ms, x.finalize_ms);
       stages.merge_ms = std::max(stages.merge_ms, x.merge_ms);
       stages.device_ms = std::max(stages.device_ms, x.device_ms);
+      stages.host_count_ms = std::max(stages.host_count_ms, x.host_count_ms);
       stages.records += x.records;
       stages.chunks += x.chunks;
       stages.map_reruns += x.map_reruns;
@@ -306,17 +307,18 @@ int run(const Cli& c) {
   write_out(wc::format_output(t, have_text ? reinterpret_cast<const uint8_t*>(text.data()) : nullptr,
                               have_text ? text.size() : 0, c.echo && have_text, c.list, c.top));
   const bool gpu_path = !(c.cpu || c.compat);
-  char js[1024];
+  char js[1536];
   std::snprintf(js, sizeof(js),
                 "{\"bytes\": %llu, \"tokens\": %llu, \"keys\": %zu, \"seconds\": %.6f, \"gb_per_s\": %.3f, "
                 "\"words_per_s\": %.1f, \"gpus\": %d, \"ranks\": %d, \"virtual_ranks\": %s, \"path\": \"%s\", "
-                "\"chunk_bytes\": %llu, "
+                "\"count_seconds\": %.6f, \"count_gb_per_s\": %.3f, \"chunk_bytes\": %llu, "
                 "\"device_ms\": {\"map\": %.3f, \"reduce\": %.3f, \"finalize\": %.3f, \"merge\": %.3f, "
                 "\"total\": %.3f}, "
                 "\"chunks\": %u, \"records\": %llu, \"map_reruns\": %u, \"table_splits\": %u}",
                 (unsigned long long)bytes, (unsigned long long)t.total, t.size(), secs, bytes / secs / 1e9,
                 t.total / secs, gpu_path ? gpus_used : 0, gpu_path ? ranks_used : 0,
                 c.virtual_ranks > 0 ? "true" : "false", c.compat ? "compat" : (c.cpu ? "cpu" : "gpu"),
+                stages.host_count_ms / 1e3, stages.host_count_ms > 0 ? bytes / (stages.host_count_ms * 1e6) : 0.0,
                 (unsigned long long)c.chunk, stages.map_ms, stages.reduce_ms, stages.finalize_ms, stages.merge_ms,
                 stages.device_ms,
                 stages.chunks, (unsigned long long)stages.records, stages.map_reruns, stages.table_splits);
