@@ -123,10 +123,18 @@ __device__ __forceinline__ uint32_t slot_of(uint32_t g, uint32_t i) {
   return (i < 2 ? 0u : MAP_SLOTS / 2) + 2 * g + (i & 1);
 }
 
-// The two candidate groups of a key (2-choice placement; g2 != g1).
+// The two candidate groups of a key (2-choice placement; g2 != g1: the xor
+// term is odd).
 __device__ __forceinline__ void hot_groups(uint32_t ph, uint32_t& g1, uint32_t& g2) {
   g1 = (ph >> 20) & (NG - 1);
-  g2 = g1 ^ max((ph >> 8) & (NG - 1), 1u);
+  g2 = g1 ^ (((ph >> 8) & (NG - 1)) | 1u);
+}
+// The same as byte offsets of the groups in the signature image (16 * g):
+// right shifts, ands and one bitop3 — all full-rate VALU on gfx950, where the
+// left shifts / max / shift-or forms are half rate (profiles/r4_session3.md §2).
+__device__ __forceinline__ void hot_group_offs(uint32_t ph, uint32_t& o1, uint32_t& o2) {
+  o1 = (ph >> 16) & ((NG - 1) << 4);
+  o2 = o1 ^ (((ph >> 4) & ((NG - 1) << 4)) | 16u);
 }
 
 // 64-bit fingerprint of a sampled word (never 0): keys the global sample table.
@@ -634,20 +642,33 @@ static_assert(sizeof(MapLds) + 8 * MAP_STAMP_N <= 160 * 1024, "one map block per
 static_assert(MAP_DEF_CAP >= 128 + UNIT / 17, "a round defers at most 127 carried + UNIT / 17 LONG tokens");
 static_assert(GS == 2, "pair-packed two-word words: 2-slot groups");
 
-// Index (0..3) of the first of a key's four candidate signatures equal to sig, else -1.
-__device__ __forceinline__ int sig_match4(const u64x2& a, const u64x2& b, uint64_t sig) {
-  const uint32_t m = (a.x == sig ? 1u : 0u) | (a.y == sig ? 2u : 0u) | (b.x == sig ? 4u : 0u) | (b.y == sig ? 8u : 0u);
-  return (int)__ffs(m) - 1;
+// Hot-table slot of a one-slot word's signature in its candidate groups g1 (a)
+// and g2 (b), or -1: a compare + select chain straight to the slot index (a
+// word sits in at most one slot; the old match-mask / ffs / slot decode took
+// twice the VALU).
+// Slot results are BYTE offsets of the slot's counter (4 * slot = 8 * group +
+// 4 * i, from the groups' image offsets o = 16 * group: o / 2 + 4 i).
+__device__ __forceinline__ int sig_slot4(const u64x2& a, const u64x2& b, uint64_t sig, uint32_t o1, uint32_t o2) {
+  const int c1 = (int)(o1 >> 1), c2 = (int)(o2 >> 1);
+  int s = b.y == sig ? c2 + 4 : -1;
+  s = b.x == sig ? c2 : s;
+  s = a.y == sig ? c1 + 4 : s;
+  return a.x == sig ? c1 : s;
 }
 
-// Hot-table match of an inline token (signature sig, k0) against its two
-// candidate groups: a one-slot word (sig's top byte < 8) in any of the four
-// slots; a two-word word only in a group's first slot with k0 in the second.
-// Returns the slot index 0..3 as sig_match4, or -1.
-__device__ __forceinline__ int inline_match(const u64x2& a, const u64x2& b, uint64_t sig, uint64_t k0) {
-  if (!two_word(sig)) return sig_match4(a, b, sig);
-  const uint32_t m = (a.x == sig && a.y == k0 ? 1u : 0u) | (b.x == sig && b.y == k0 ? 4u : 0u);
-  return (int)__ffs(m) - 1;
+// Hot-table slot of an inline token (signature sig, k0): a one-slot word
+// (sig's top byte < 8) in any of the four slots; a two-word word only in a
+// group's first slot with k0 in the second.  -1: not in the table.
+__device__ __forceinline__ int inline_slot(const u64x2& a, const u64x2& b, uint64_t sig, uint64_t k0, uint32_t o1,
+                                           uint32_t o2) {
+  if (!two_word(sig)) return sig_slot4(a, b, sig, o1, o2);
+  const int s = b.x == sig && b.y == k0 ? (int)(o2 >> 1) : -1;
+  return a.x == sig && a.y == k0 ? (int)(o1 >> 1) : s;
+}
+
+// LDS word at byte offset o of an array (the hot table's count / offset arrays).
+__device__ __forceinline__ uint32_t* at_byte(uint32_t* base, int o) {
+  return reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(base) + o);
 }
 
 template <bool ST>
@@ -812,8 +833,8 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     // trip; a tail of <= 64 entries takes the one-entry step.  General form:
     // any length (two-word signatures are confirmed by their group's side
     // word, LONG words deferred to the round end).
-    auto step = [&](uint32_t j, uint32_t hi, uint32_t cut, auto two_c) {
-      constexpr bool TWO = decltype(two_c)::value;
+    auto step = [&](uint32_t j, uint32_t hi, uint32_t cut, auto two_c, auto mixed_c) {
+      constexpr bool TWO = decltype(two_c)::value, MIXED = decltype(mixed_c)::value;
       const bool h1 = j + lane < hi, h2 = TWO && j + 64 + lane < hi;
       const uint32_t r1 = list[j + lane], r2 = TWO ? list[j + 64 + lane] : 0u;  // unconditional (see step_short)
       const uint32_t e1 = h1 ? r1 : 0u, e2 = h2 ? r2 : 0u;
@@ -822,7 +843,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
         return;
       }
       const uint32_t q1 = e1 & 0x7FFu, q2 = e2 & 0x7FFu, n1 = e1 >> 11, n2 = e2 >> 11;
-      const bool old1 = j + lane < cut, old2 = TWO && j + 64 + lane < cut;  // carried from the previous unit
+      const bool old1 = MIXED && j + lane < cut, old2 = MIXED && TWO && j + 64 + lane < cut;  // carried entries
       uint64_t w10, w11, w20 = 0, w21 = 0;
       window16(bufw, q1 + (old1 ? pbo : cbo), w10, w11);
       if (TWO) window16(bufw, q2 + (old2 ? pbo : cbo), w20, w21);
@@ -835,35 +856,33 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
       inline_key(w10, w11, n1, a0, a1, as);
       if (TWO) inline_key(w20, w21, n2, b0, b1, bs);
       const uint32_t ha = place_hash(a0, a1), hb = TWO ? place_hash(b0, b1) : 0u;
-      uint32_t ga1, ga2, gb1 = 0, gb2 = 0;
-      hot_groups(ha, ga1, ga2);
-      if (TWO) hot_groups(hb, gb1, gb2);
+      uint32_t ga1, ga2, gb1 = 0, gb2 = 0;  // group byte offsets in the image
+      hot_group_offs(ha, ga1, ga2);
+      if (TWO) hot_group_offs(hb, gb1, gb2);
       clk.lap(MS_KEYS);
       if (WC_MAP_ABLATE == 2) {
         sink ^= as ^ bs ^ ga2 ^ gb2;
         return;
       }
-      const u64x2* S = reinterpret_cast<const u64x2*>(L.sig);
-      int s1 = -1, s2 = -1;
-      {  // S[g]: both slots of group g
-        const u64x2 xa0 = S[ga1], xa1 = S[ga2];
+      const uint8_t* S = reinterpret_cast<const uint8_t*>(L.sig);
+      int s1 = -1, s2 = -1;  // counter byte offsets
+      {  // both slots of a group in one 16-byte read
+        const u64x2 xa0 = *reinterpret_cast<const u64x2*>(S + ga1), xa1 = *reinterpret_cast<const u64x2*>(S + ga2);
         if (TWO) {
-          const u64x2 xb0 = S[gb1], xb1 = S[gb2];
-          const int mb = in2 ? inline_match(xb0, xb1, bs, b0) : -1;
-          s2 = mb < 0 ? -1 : (int)slot_of(mb < GS ? gb1 : gb2, mb & (GS - 1));
+          const u64x2 xb0 = *reinterpret_cast<const u64x2*>(S + gb1), xb1 = *reinterpret_cast<const u64x2*>(S + gb2);
+          s2 = in2 ? inline_slot(xb0, xb1, bs, b0, gb1, gb2) : -1;
         }
-        const int ma = in1 ? inline_match(xa0, xa1, as, a0) : -1;
-        s1 = ma < 0 ? -1 : (int)slot_of(ma < GS ? ga1 : ga2, ma & (GS - 1));
+        s1 = in1 ? inline_slot(xa0, xa1, as, a0, ga1, ga2) : -1;
       }
       clk.lap(MS_PROBE);
       const uint32_t o1 = (uint32_t)(old1 ? pu0 : cu0) + q1, o2 = (uint32_t)(old2 ? pu0 : cu0) + q2;
       if (s1 >= 0) {
-        atomicAdd(&L.cnt[s1], 1u);  // results unused: no-return ds_add / ds_min
-        atomicMin(&L.off[s1], o1);
+        atomicAdd(at_byte(L.cnt, s1), 1u);  // results unused: no-return ds_add / ds_min
+        atomicMin(at_byte(L.off, s1), o1);
       }
       if (TWO && s2 >= 0) {
-        atomicAdd(&L.cnt[s2], 1u);
-        atomicMin(&L.off[s2], o2);
+        atomicAdd(at_byte(L.cnt, s2), 1u);
+        atomicMin(at_byte(L.off, s2), o2);
       }
       if (WC_MAP_ABLATE == 3) return;
       // misses of inline words become records now; LONG words wait for the round end
@@ -895,8 +914,8 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     // key (bytes | len << 56): one 8-byte window (three LDS dwords, two
     // funnels), no tail, no side-word confirmation, and every miss a 16-byte
     // record candidate.  3 of 4 tokens of English-like text take it.
-    auto step_short = [&](uint32_t j, uint32_t hi, uint32_t cut, auto two_c) {
-      constexpr bool TWO = decltype(two_c)::value;
+    auto step_short = [&](uint32_t j, uint32_t hi, uint32_t cut, auto two_c, auto mixed_c) {
+      constexpr bool TWO = decltype(two_c)::value, MIXED = decltype(mixed_c)::value;
       const bool h1 = j + lane < hi, h2 = TWO && j + 64 + lane < hi;
       // unconditional entry reads (no exec-mask branch): past `hi` they read a
       // later entry, the next wave's list or the deferred lists — inside MapLds, and masked by h1 / h2
@@ -907,46 +926,49 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
         return;
       }
       const uint32_t q1 = e1 & 0x7FFu, q2 = e2 & 0x7FFu, n1 = e1 >> 11, n2 = e2 >> 11;
-      const bool old1 = j + lane < cut, old2 = TWO && j + 64 + lane < cut;  // carried from the previous unit
+      const bool old1 = MIXED && j + lane < cut, old2 = MIXED && TWO && j + 64 + lane < cut;  // carried entries
       const uint64_t w1 = window8(bufw, q1 + (old1 ? pbo : cbo)), w2 = TWO ? window8(bufw, q2 + (old2 ? pbo : cbo)) : 0ull;
       if (WC_MAP_ABLATE == 1) {
         sink ^= w1 ^ w2;
         return;
       }
-      // k0: the first n bytes (n <= 7: shift by 64 - 8 n in [8, 56]; n = 0 of an empty lane clamps to 1)
-      const uint32_t sa = 64u - 8u * max(n1, 1u), sb = 64u - 8u * max(n2, 1u);
-      const uint64_t a0 = (w1 << sa) >> sa, b0 = TWO ? (w2 << sb) >> sb : 0ull;
+      // k0: the first n bytes — the mask -1 >> (64 - 8 n), with 8 n taken from
+      // the entry's length field by a right shift and an and (full-rate ops; an
+      // empty lane's n = 0 shifts by (64 & 63) = 0: garbage, masked by h)
+      const uint32_t sa = (64u - ((e1 >> 8) & 0xF8u)) & 63u, sb = (64u - ((e2 >> 8) & 0xF8u)) & 63u;
+      const uint64_t a0 = w1 & (~0ull >> sa), b0 = TWO ? w2 & (~0ull >> sb) : 0ull;
       const uint64_t as = a0 | ((uint64_t)n1 << 56), bs = b0 | ((uint64_t)n2 << 56);
       const uint32_t ha = place_hash(a0, n1), hb = TWO ? place_hash(b0, n2) : 0u;
-      uint32_t ga1, ga2, gb1 = 0, gb2 = 0;
-      hot_groups(ha, ga1, ga2);
-      if (TWO) hot_groups(hb, gb1, gb2);
+      uint32_t ga1, ga2, gb1 = 0, gb2 = 0;  // group byte offsets in the image
+      hot_group_offs(ha, ga1, ga2);
+      if (TWO) hot_group_offs(hb, gb1, gb2);
       clk.lap(MS_KEYS);
       if (WC_MAP_ABLATE == 2) {
         sink ^= as ^ bs ^ ga2 ^ gb2;
         return;
       }
-      const u64x2* S = reinterpret_cast<const u64x2*>(L.sig);
-      int s1 = -1, s2 = -1;
+      const uint8_t* S = reinterpret_cast<const uint8_t*>(L.sig);
+      int s1 = -1, s2 = -1;  // counter byte offsets
       {  // a pair's side word never equals a short signature: plain 4-slot match
-        const u64x2 xa0 = S[ga1], xa1 = S[ga2];
+        // (an empty lane's signature has top byte 0, like a LONG group's side word: masked by h)
+        const u64x2 xa0 = *reinterpret_cast<const u64x2*>(S + ga1), xa1 = *reinterpret_cast<const u64x2*>(S + ga2);
         if (TWO) {
-          const u64x2 xb0 = S[gb1], xb1 = S[gb2];
-          const int mb = h2 ? sig_match4(xb0, xb1, bs) : -1;
-          s2 = mb < 0 ? -1 : (int)slot_of(mb < GS ? gb1 : gb2, mb & (GS - 1));
+          const u64x2 xb0 = *reinterpret_cast<const u64x2*>(S + gb1), xb1 = *reinterpret_cast<const u64x2*>(S + gb2);
+          const int m2 = sig_slot4(xb0, xb1, bs, gb1, gb2);
+          s2 = h2 ? m2 : -1;
         }
-        const int ma = h1 ? sig_match4(xa0, xa1, as) : -1;
-        s1 = ma < 0 ? -1 : (int)slot_of(ma < GS ? ga1 : ga2, ma & (GS - 1));
+        const int m1 = sig_slot4(xa0, xa1, as, ga1, ga2);
+        s1 = h1 ? m1 : -1;
       }
       clk.lap(MS_PROBE);
       const uint32_t o1 = (uint32_t)(old1 ? pu0 : cu0) + q1, o2 = (uint32_t)(old2 ? pu0 : cu0) + q2;
       if (s1 >= 0) {
-        atomicAdd(&L.cnt[s1], 1u);
-        atomicMin(&L.off[s1], o1);
+        atomicAdd(at_byte(L.cnt, s1), 1u);
+        atomicMin(at_byte(L.off, s1), o1);
       }
       if (TWO && s2 >= 0) {
-        atomicAdd(&L.cnt[s2], 1u);
-        atomicMin(&L.off[s2], o2);
+        atomicAdd(at_byte(L.cnt, s2), 1u);
+        atomicMin(at_byte(L.off, s2), o2);
       }
       if (WC_MAP_ABLATE == 3) return;
       const bool d1 = h1 && s1 < 0, d2 = TWO && h2 && s2 < 0;
@@ -1009,20 +1031,35 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
       // full steps; a remainder waits for the next round unless it holds
       // carried entries (their slot is overwritten next) or this is the last unit
       // (explicit loops: the same steps behind a lambda made the kernel spill ~80 VGPRs)
+      // (only a round's first step of a class can hold carried entries: MIXED
+      // steps select slot and offsets per entry, the others need not)
+      constexpr std::true_type T{}, M{};
+      constexpr std::false_type F{}, P{};
       uint32_t j = 0;
-      for (; j + 128 <= ns; j += 128) step_short(j, ns, cs, std::true_type{});
+      if (cs && ns >= 128) {
+        step_short(0u, ns, cs, T, M);
+        j = 128;
+      }
+      for (; j + 128 <= ns; j += 128) step_short(j, ns, 0u, T, P);
       if (j < ns && (j < cs || last)) {
-        if (j + 64 < ns) step_short(j, ns, cs, std::true_type{});
-        else step_short(j, ns, cs, std::false_type{});
+        if (j < cs) step_short(j, ns, cs, T, M);
+        else if (j + 64 < ns) step_short(j, ns, 0u, T, P);
+        else step_short(j, ns, 0u, F, P);
         j = ns;
       }
       cs_from = j;
       cs = ns - j;
       const uint32_t ocut = ob0 + co;
-      for (j = ob0; j + 128 <= no_end; j += 128) step(j, no_end, ocut, std::true_type{});
+      j = ob0;
+      if (co && no_end >= ob0 + 128) {
+        step(j, no_end, ocut, T, M);
+        j += 128;
+      }
+      for (; j + 128 <= no_end; j += 128) step(j, no_end, 0u, T, P);
       if (j < no_end && (j < ocut || last)) {
-        if (j + 64 < no_end) step(j, no_end, ocut, std::true_type{});
-        else step(j, no_end, ocut, std::false_type{});
+        if (j < ocut) step(j, no_end, ocut, T, M);
+        else if (j + 64 < no_end) step(j, no_end, 0u, T, P);
+        else step(j, no_end, 0u, F, P);
         j = no_end;
       }
       co_from = j;
@@ -1037,8 +1074,8 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
       // words): the carried entries first, then rounds of MAP_LIST entries of
       // the unit in stream order, every entry on the general step
       // all carried: the cut past them (one general step per class, < 128 entries each)
-      if (cs) step(cs_from, cs_from + cs, MAP_LIST, std::true_type{});
-      if (co) step(co_from, co_from + co, MAP_LIST, std::true_type{});
+      if (cs) step(cs_from, cs_from + cs, MAP_LIST, std::true_type{}, std::true_type{});
+      if (co) step(co_from, co_from + co, MAP_LIST, std::true_type{}, std::true_type{});
       cs = co = 0;
       if (ndef) {
         run_deferred();
@@ -1059,8 +1096,8 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
         const uint32_t round_n = min(wave_total - base, (uint32_t)MAP_LIST);
         clk.lap(MS_LIST);
         uint32_t j = 0;
-        for (; j + 64 < round_n; j += 128) step(j, round_n, 0u, std::true_type{});
-        if (j < round_n) step(j, round_n, 0u, std::false_type{});
+        for (; j + 64 < round_n; j += 128) step(j, round_n, 0u, std::true_type{}, std::false_type{});
+        if (j < round_n) step(j, round_n, 0u, std::false_type{}, std::false_type{});
         if (ndef) {
           run_deferred();
           clk.lap(MS_SLOW);
