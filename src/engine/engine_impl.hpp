@@ -233,7 +233,11 @@ struct Engine::Impl {
   // FO_MAX_KEYS keys, the onesweep radix sort above it, after a sample-sort
   // overflow, or always with WC_FIRST_ORDER=radix.
   bool order_radix = false;
-  bool sample_order(uint64_t bound) const { return !order_radix && bound <= FO_MAX_KEYS; }
+  // The sample sort up to 400k keys; above, the radix sort: the 2048-bin sample
+  // sort (first_order handles up to FO_MAX_KEYS) measured no faster at 1M keys
+  // — fo_bin 73 + fo_sort 138 us vs 200 us of radix passes + gather
+  // (profiles/r4_session3.md §7)
+  bool sample_order(uint64_t bound) const { return !order_radix && bound <= 400000; }
   uint32_t* fo_ovf = nullptr;  // overflow word of the sample sort sort_cols_by_first left in flight
   KeyCols cols_unsorted;       // its input, kept for a radix redo
   bool order_redo = false;     // the speculative finalize's sample sort overflowed (Stats::order_path 4)

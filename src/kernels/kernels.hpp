@@ -259,9 +259,9 @@ struct OrderDst {
   uint32_t* slen;
 };
 #ifndef WC_FO_MAX_KEYS
-#define WC_FO_MAX_KEYS 400000
+#define WC_FO_MAX_KEYS 1600000
 #endif
-constexpr uint64_t FO_MAX_KEYS = WC_FO_MAX_KEYS;  // bins average <= 800 rows (one wave sorts up to 2048)
+constexpr uint64_t FO_MAX_KEYS = WC_FO_MAX_KEYS;  // 512 / 2048 bins average <= 800 rows (one wave sorts up to 2048)
 size_t first_order_ws_bytes(const OrderSrc& src, uint64_t bound);
 void first_order_stamps(unsigned long long* d);  // debug: phase clocks of the three kernels (nullptr: off)
 // key_hist (nullable): a histogram over fo_logbin(first, key_hist_m) of exactly

@@ -114,6 +114,18 @@ __device__ __forceinline__ void inline_key(uint64_t w0, uint64_t w1, uint32_t le
   sig = (len <= 7 ? k0 : ((t ^ k0) & LOW7)) | lt;
 }
 
+// inline_key for a token of 8 or more bytes (the map's other-class steps):
+// k0 is the first window whole; len 8..15 -> exact key, longer -> garbage
+// (LONG tokens are deferred, never keyed here).
+__device__ __forceinline__ void inline_key_long8(uint64_t w0, uint64_t w1, uint32_t len, uint64_t& k0, uint64_t& k1,
+                                                 uint64_t& sig) {
+  k0 = w0;
+  const uint64_t t = len > 8 ? w1 & (~0ull >> ((128u - 8u * len) & 63u)) : 0ull;  // the first len - 8 bytes
+  const uint64_t lt = (uint64_t)len << 56;
+  k1 = len == 8 ? 8ull : (t | lt);
+  sig = ((t ^ k0) & LOW7) | lt;
+}
+
 // Slot i of group g.  4-slot groups: slots 0-1 of every group form the first
 // half of the table, slots 2-3 the second, so each 16-byte probe read of a
 // group half lands on bank quad (g mod 16) — all 16 quads — instead of only
@@ -833,8 +845,10 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     // trip; a tail of <= 64 entries takes the one-entry step.  General form:
     // any length (two-word signatures are confirmed by their group's side
     // word, LONG words deferred to the round end).
-    auto step = [&](uint32_t j, uint32_t hi, uint32_t cut, auto two_c, auto mixed_c) {
-      constexpr bool TWO = decltype(two_c)::value, MIXED = decltype(mixed_c)::value;
+    auto step = [&](uint32_t j, uint32_t hi, uint32_t cut, auto two_c, auto mixed_c, auto any_c) {
+      // ANY: entries of any length (the > MAP_LIST rounds); otherwise the
+      // other class only (8 bytes or longer: k0 is the first window as read)
+      constexpr bool TWO = decltype(two_c)::value, MIXED = decltype(mixed_c)::value, ANY = decltype(any_c)::value;
       const bool h1 = j + lane < hi, h2 = TWO && j + 64 + lane < hi;
       const uint32_t r1 = list[j + lane], r2 = TWO ? list[j + 64 + lane] : 0u;  // unconditional (see step_short)
       const uint32_t e1 = h1 ? r1 : 0u, e2 = h2 ? r2 : 0u;
@@ -853,8 +867,13 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
       }
       const bool in1 = h1 && n1 <= KEY_INLINE_MAX, in2 = h2 && n2 <= KEY_INLINE_MAX;
       uint64_t a0, a1, as, b0 = 0, b1 = 0, bs = 0;
-      inline_key(w10, w11, n1, a0, a1, as);
-      if (TWO) inline_key(w20, w21, n2, b0, b1, bs);
+      if (ANY) {
+        inline_key(w10, w11, n1, a0, a1, as);
+        if (TWO) inline_key(w20, w21, n2, b0, b1, bs);
+      } else {
+        inline_key_long8(w10, w11, n1, a0, a1, as);
+        if (TWO) inline_key_long8(w20, w21, n2, b0, b1, bs);
+      }
       const uint32_t ha = place_hash(a0, a1), hb = TWO ? place_hash(b0, b1) : 0u;
       uint32_t ga1, ga2, gb1 = 0, gb2 = 0;  // group byte offsets in the image
       hot_group_offs(ha, ga1, ga2);
@@ -1052,14 +1071,14 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
       const uint32_t ocut = ob0 + co;
       j = ob0;
       if (co && no_end >= ob0 + 128) {
-        step(j, no_end, ocut, T, M);
+        step(j, no_end, ocut, T, M, F);
         j += 128;
       }
-      for (; j + 128 <= no_end; j += 128) step(j, no_end, 0u, T, P);
+      for (; j + 128 <= no_end; j += 128) step(j, no_end, 0u, T, P, F);
       if (j < no_end && (j < ocut || last)) {
-        if (j < ocut) step(j, no_end, ocut, T, M);
-        else if (j + 64 < no_end) step(j, no_end, 0u, T, P);
-        else step(j, no_end, 0u, F, P);
+        if (j < ocut) step(j, no_end, ocut, T, M, F);
+        else if (j + 64 < no_end) step(j, no_end, 0u, T, P, F);
+        else step(j, no_end, 0u, F, P, F);
         j = no_end;
       }
       co_from = j;
@@ -1074,8 +1093,8 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
       // words): the carried entries first, then rounds of MAP_LIST entries of
       // the unit in stream order, every entry on the general step
       // all carried: the cut past them (one general step per class, < 128 entries each)
-      if (cs) step(cs_from, cs_from + cs, MAP_LIST, std::true_type{}, std::true_type{});
-      if (co) step(co_from, co_from + co, MAP_LIST, std::true_type{}, std::true_type{});
+      if (cs) step_short(cs_from, cs_from + cs, MAP_LIST, std::true_type{}, std::true_type{});
+      if (co) step(co_from, co_from + co, MAP_LIST, std::true_type{}, std::true_type{}, std::false_type{});
       cs = co = 0;
       if (ndef) {
         run_deferred();
@@ -1096,8 +1115,8 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
         const uint32_t round_n = min(wave_total - base, (uint32_t)MAP_LIST);
         clk.lap(MS_LIST);
         uint32_t j = 0;
-        for (; j + 64 < round_n; j += 128) step(j, round_n, 0u, std::true_type{}, std::false_type{});
-        if (j < round_n) step(j, round_n, 0u, std::false_type{}, std::false_type{});
+        for (; j + 64 < round_n; j += 128) step(j, round_n, 0u, std::true_type{}, std::false_type{}, std::true_type{});
+        if (j < round_n) step(j, round_n, 0u, std::false_type{}, std::false_type{}, std::true_type{});
         if (ndef) {
           run_deferred();
           clk.lap(MS_SLOW);

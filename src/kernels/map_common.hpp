@@ -34,7 +34,7 @@ __device__ __forceinline__ void window16(const uint8_t* buf, uint32_t p, uint64_
   // 64-bit-shift form (which needs a dword select for shifts >= 4)
   const uint32_t* q = reinterpret_cast<const uint32_t*>(buf + (p & ~3u));
   const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
-  const uint32_t sh = p & 3u;
+  const uint32_t sh = p;  // v_alignbyte_b32 reads only bits [1:0] of the byte shift
   const uint32_t a = __builtin_amdgcn_alignbyte(d1, d0, sh), b = __builtin_amdgcn_alignbyte(d2, d1, sh);
   const uint32_t c = __builtin_amdgcn_alignbyte(d3, d2, sh), d = __builtin_amdgcn_alignbyte(d4, d3, sh);
   w0 = (uint64_t)a | ((uint64_t)b << 32);
@@ -54,7 +54,7 @@ __device__ __forceinline__ void window16(const uint8_t* buf, uint32_t p, uint64_
 __device__ __forceinline__ uint64_t window8(const uint8_t* buf, uint32_t p) {
   const uint32_t* q = reinterpret_cast<const uint32_t*>(buf + (p & ~3u));
   const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
-  const uint32_t sh = p & 3u;
+  const uint32_t sh = p;  // bits [1:0] only (v_alignbyte_b32)
   return (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32);
 }
 
@@ -199,6 +199,29 @@ __device__ __forceinline__ void put_record(const MapArgs& a, const RecOut& o, ui
   }
 }
 
+// put_record for one occurrence of a word of 1..7 bytes (k1 = its length n):
+// a Rec16's tail word is 0 without a compare.
+__device__ __forceinline__ void put_record_short(const MapArgs& a, const RecOut& o, uint32_t b, uint32_t packed,
+                                                 bool r16, uint64_t k0, uint32_t n, uint32_t off) {
+  const uint32_t pos = r16 ? (packed & 0xFFFFu) : (packed >> 16);
+  const uint32_t idx = __umul24(b, o.sub) + pos;
+  if (pos >= o.sub) {
+    atomicOr(&a.flags[FLAG_REGION_OVF], 1u);
+    return;
+  }
+  if (WC_EMIT_ABLATE) return;
+  if (r16) {
+    *reinterpret_cast<Rec16*>(reinterpret_cast<uint8_t*>(o.b16) + idx * (uint32_t)sizeof(Rec16)) =
+        Rec16{(uint32_t)k0, (uint32_t)(k0 >> 32), 0u, off};
+  } else {
+    Rec r;
+    r.k0 = k0;
+    r.k1 = n;
+    r.co = (1ull << 32) | off;
+    *reinterpret_cast<Rec*>(reinterpret_cast<uint8_t*>(o.b24) + __umul24(idx, (uint32_t)sizeof(Rec))) = r;
+  }
+}
+
 // Append one record (key, count, first offset) to bucket b's sub-region of
 // this block; bcur[b] packs both cursors (Rec16 count | Rec count << 16).
 __device__ __forceinline__ void emit_record(uint32_t* bcur, const MapArgs& a, const RecOut& o, uint32_t b, uint64_t k0,
@@ -231,8 +254,8 @@ __device__ __forceinline__ void emit_two_short(uint32_t* bcur, const MapArgs& a,
   uint32_t p1 = 0, p2 = 0;
   if (d1) p1 = atomicAdd(&bcur[b1], s1 ? 1u : 0x10000u);
   if (d2) p2 = atomicAdd(&bcur[b2], s2 ? 1u : 0x10000u);
-  if (d1) put_record(a, o, b1, p1, s1, x0, n1, 1, o1);
-  if (d2) put_record(a, o, b2, p2, s2, y0, n2, 1, o2);
+  if (d1) put_record_short(a, o, b1, p1, s1, x0, n1, o1);
+  if (d2) put_record_short(a, o, b2, p2, s2, y0, n2, o2);
 }
 
 // Key of a LONG token (>= 16 bytes) of known length 16..30 from its LDS

@@ -213,11 +213,12 @@ __global__ void __launch_bounds__(OS_THREADS) wc_os_pass(const uint64_t* keys, c
 #ifndef WC_FO_ROWS
 #define WC_FO_ROWS 2048
 #endif
-#ifndef WC_FO_BINS
-#define WC_FO_BINS 512
-#endif
-constexpr int FO_BINS = WC_FO_BINS, FO_ROWS = WC_FO_ROWS, FO_SAMPLE = 4096;
-static_assert(FO_BINS <= 1024 && FO_BINS % (2 * 64) == 0, "fo bins: <= one per wc_fo_bin thread, whole wc_fo_sort blocks");
+// Bins per order: 512 up to FO_SMALL_KEYS keys, FO_BINS (the maximum, LDS
+// sizing) above — bins average <= 800 rows either way (one wave sorts 2048).
+constexpr int FO_BINS = 2048, FO_BINS_SMALL = 512, FO_ROWS = WC_FO_ROWS, FO_SAMPLE = 4096;
+constexpr uint64_t FO_SMALL_KEYS = 400000;
+static_assert(FO_BINS % 1024 == 0 && FO_BINS_SMALL % (2 * 64) == 0 && FO_BINS_SMALL <= 1024,
+              "fo bins: whole wc_fo_bin scan passes, whole wc_fo_sort blocks");
 constexpr int FO_RPT = FO_ROWS / 1024;  // wc_fo_bin rows per thread
 static_assert(FO_ROWS % 1024 == 0 && TAB_SLOTS % FO_ROWS == 0, "fo_bin: whole rows per thread, blocks inside a bucket");
 
@@ -286,7 +287,7 @@ __device__ __forceinline__ uint32_t lds_exclusive_scan(uint32_t* c, int n, uint3
   return total;
 }
 
-__global__ void __launch_bounds__(1024) wc_fo_split(OrderSrc src, uint32_t M, uint16_t* map, uint32_t* ctl) {
+__global__ void __launch_bounds__(1024) wc_fo_split(OrderSrc src, uint32_t M, uint32_t nb, uint16_t* map, uint32_t* ctl) {
   FoClock clk(0);
   __shared__ alignas(16) uint32_t hist[FO_LOGBINS];
   __shared__ uint32_t ws[16];
@@ -346,11 +347,11 @@ __global__ void __launch_bounds__(1024) wc_fo_split(OrderSrc src, uint32_t M, ui
   clk.at(2);
   const uint32_t V = lds_exclusive_scan<1024>(hist, FO_LOGBINS, ws);
   clk.at(3);
-  // log-bin -> bin: the sample share below it, in FO_BINS equal parts (monotone:
+  // log-bin -> bin: the sample share below it, in nb equal parts (monotone:
   // a float scaling, no integer division)
-  const float inv = V ? (float)FO_BINS / (float)V : 0.0f;
+  const float inv = V ? (float)nb / (float)V : 0.0f;
   for (int i = tid; i < FO_LOGBINS; i += 1024)
-    map[i] = (uint16_t)min((uint32_t)FO_BINS - 1, (uint32_t)((float)hist[i] * inv));
+    map[i] = (uint16_t)min(nb - 1, (uint32_t)((float)hist[i] * inv));
   clk.at(4);
 }
 
@@ -375,8 +376,9 @@ __global__ void __launch_bounds__(1024) wc_fo_hist(OrderSrc src, uint32_t M, uin
 
 // phist (nullable): the reducer's histogram of every key's log-bin — each
 // block then builds the log-bin -> bin map itself (no wc_fo_split launch).
-__global__ void __launch_bounds__(1024) wc_fo_bin(OrderSrc src, uint32_t M, const uint16_t* map, const uint32_t* phist,
-                                                  uint32_t* cntm, uint32_t* loffm, FoEntry* seg, uint32_t* ctl) {
+__global__ void __launch_bounds__(1024) wc_fo_bin(OrderSrc src, uint32_t M, uint32_t nb, const uint16_t* map,
+                                                  const uint32_t* phist, uint32_t* cntm, uint32_t* loffm, FoEntry* seg,
+                                                  uint32_t* ctl) {
   FoClock clk(1);
   __shared__ uint16_t lmap[FO_LOGBINS];
   __shared__ alignas(16) uint32_t lh[FO_LOGBINS];
@@ -422,21 +424,21 @@ __global__ void __launch_bounds__(1024) wc_fo_bin(OrderSrc src, uint32_t M, cons
     if (k == 0 && tid == 0) ctl[0] = 0;  // the overflow word (wc_fo_sort runs after every block)
     __syncthreads();
     const uint32_t V = lds_exclusive_scan<1024>(lh, FO_LOGBINS, ws);
-    const float inv = V ? (float)FO_BINS / (float)V : 0.0f;
+    const float inv = V ? (float)nb / (float)V : 0.0f;
     for (int i = tid; i < FO_LOGBINS; i += 1024)
-      lmap[i] = (uint16_t)min((uint32_t)FO_BINS - 1, (uint32_t)((float)lh[i] * inv));
+      lmap[i] = (uint16_t)min(nb - 1, (uint32_t)((float)lh[i] * inv));
   } else {
     const uint4* g = reinterpret_cast<const uint4*>(map);
     uint4* l = reinterpret_cast<uint4*>(lmap);
     for (int i = tid; i < FO_LOGBINS * 2 / 16; i += 1024) l[i] = g[i];
   }
-  for (uint32_t b = tid; b < FO_BINS; b += 1024) lc[b] = 0;
+  for (uint32_t b = tid; b < nb; b += 1024) lc[b] = 0;
   __syncthreads();
   clk.at(1);
   uint32_t bb[FO_RPT], lp[FO_RPT];
 #pragma unroll
   for (int r = 0; r < FO_RPT; ++r) {
-    bb[r] = FO_BINS;
+    bb[r] = nb;
     if (ok[r]) {
       bb[r] = lmap[fo_logbin(e[r].first, M)];
       lp[r] = atomicAdd(&lc[bb[r]], 1u);
@@ -444,14 +446,14 @@ __global__ void __launch_bounds__(1024) wc_fo_bin(OrderSrc src, uint32_t M, cons
   }
   __syncthreads();
   clk.at(2);
-  if (tid < FO_BINS) cntm[(size_t)tid * nblk + k] = lc[tid];
-  lds_exclusive_scan<1024>(lc, FO_BINS, ws);  // 0 or 1 bin per thread
+  for (uint32_t b = tid; b < nb; b += 1024) cntm[(size_t)b * nblk + k] = lc[b];
+  lds_exclusive_scan<1024>(lc, (int)nb, ws);  // nb < 1024: one bin on each of the first nb threads
   clk.at(3);
-  if (tid < FO_BINS) loffm[(size_t)tid * nblk + k] = lc[tid];
+  for (uint32_t b = tid; b < nb; b += 1024) loffm[(size_t)b * nblk + k] = lc[b];
   FoEntry* out = seg + i0;
 #pragma unroll
   for (int r = 0; r < FO_RPT; ++r)
-    if (bb[r] != FO_BINS) out[lc[bb[r]] + lp[r]] = e[r];
+    if (bb[r] != nb) out[lc[bb[r]] + lp[r]] = e[r];
   clk.at(4);
 }
 
@@ -514,8 +516,8 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
 
 __global__ void __launch_bounds__(64 * FO_SORT_WAVES) wc_fo_sort(OrderDst dst, const uint32_t* cntm,
                                                                  const uint32_t* loffm, const FoEntry* seg,
-                                                                 uint32_t nblk, uint32_t cap, uint32_t* ctl,
-                                                                 uint64_t* nout, uint32_t* zero_hist) {
+                                                                 uint32_t nblk, uint32_t nb, uint32_t cap,
+                                                                 uint32_t* ctl, uint64_t* nout, uint32_t* zero_hist) {
   constexpr int T = 64 * FO_SORT_WAVES;
   FoClock clk(2);
   if (zero_hist)  // wc_fo_bin is done with it: leave it zeroed for the next wc_fo_hist
@@ -537,7 +539,7 @@ __global__ void __launch_bounds__(64 * FO_SORT_WAVES) wc_fo_sort(OrderDst dst, c
     off += __shfl_xor(off, o);
     m += __shfl_xor(m, o);
   }
-  if (b == FO_BINS - 1 && lane == 0 && nout) *nout = (uint64_t)off + m;
+  if (b == nb - 1 && lane == 0 && nout) *nout = (uint64_t)off + m;
   clk.at(1);
   const auto emit = [&](uint32_t at, uint32_t ei) {
     const FoEntry x = seg[ei];
@@ -744,22 +746,24 @@ void first_order_stamps(unsigned long long* d) {
   WC_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(dev::fo_stamps), &d, sizeof d));
 }
 
+static uint32_t fo_nbins(uint64_t bound) { return bound <= dev::FO_SMALL_KEYS ? dev::FO_BINS_SMALL : dev::FO_BINS; }
+
 size_t first_order_ws_bytes(const OrderSrc& src, uint64_t bound) {
   const size_t nblk = fo_blocks(src, bound);
-  return 64 * 1024 + 2 * (size_t)dev::FO_BINS * nblk * 4 + 256 + nblk * dev::FO_ROWS * sizeof(dev::FoEntry);
+  return 64 * 1024 + 2 * (size_t)fo_nbins(bound) * nblk * 4 + 256 + nblk * dev::FO_ROWS * sizeof(dev::FoEntry);
 }
 
 uint32_t* first_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, uint32_t key_bits, void* ws,
                       uint64_t* nout, hipStream_t s, const uint32_t* key_hist, uint32_t key_hist_m,
                       uint32_t* hist_ws) {
   WC_CHECK(bound <= FO_MAX_KEYS, "first_order: key bound above FO_MAX_KEYS (use the radix sort)");
-  const uint32_t nblk = fo_blocks(src, bound), M = fo_mbits(key_bits);
+  const uint32_t nblk = fo_blocks(src, bound), M = fo_mbits(key_bits), nb = fo_nbins(bound);
   uint8_t* p = static_cast<uint8_t*>(ws);
   uint16_t* map = reinterpret_cast<uint16_t*>(p);  // FO_LOGBINS entries (32 KiB)
   uint32_t* ctl = reinterpret_cast<uint32_t*>(p + 48 * 1024);
   uint32_t* cntm = reinterpret_cast<uint32_t*>(p + 64 * 1024);
-  uint32_t* loffm = cntm + (size_t)dev::FO_BINS * nblk;
-  const size_t mat = 2 * (size_t)dev::FO_BINS * nblk * 4;
+  uint32_t* loffm = cntm + (size_t)nb * nblk;
+  const size_t mat = 2 * (size_t)nb * nblk * 4;
   dev::FoEntry* seg = reinterpret_cast<dev::FoEntry*>(p + 64 * 1024 + (mat + 255) / 256 * 256);
   const uint32_t* phist = key_hist && key_hist_m == M ? key_hist : nullptr;
   uint32_t* zero_hist = nullptr;
@@ -768,12 +772,12 @@ uint32_t* first_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, 
     hipLaunchKernelGGL(dev::wc_fo_hist, dim3(hb), dim3(1024), 0, s, src, M, hist_ws);
     phist = zero_hist = hist_ws;
   }
-  if (!phist) hipLaunchKernelGGL(dev::wc_fo_split, dim3(1), dim3(1024), 0, s, src, M, map, ctl);
-  hipLaunchKernelGGL(dev::wc_fo_bin, dim3(nblk), dim3(1024), 0, s, src, M, map, phist, cntm, loffm, seg, ctl);
+  if (!phist) hipLaunchKernelGGL(dev::wc_fo_split, dim3(1), dim3(1024), 0, s, src, M, nb, map, ctl);
+  hipLaunchKernelGGL(dev::wc_fo_bin, dim3(nblk), dim3(1024), 0, s, src, M, nb, map, phist, cntm, loffm, seg, ctl);
   uint32_t cap = dev::FO_BLOCK_CAP;
   if (const char* e = std::getenv("WC_FO_CAP")) cap = std::min<uint32_t>(cap, (uint32_t)std::atoi(e));  // tests
-  hipLaunchKernelGGL(dev::wc_fo_sort, dim3(dev::FO_BINS / dev::FO_SORT_WAVES), dim3(64 * dev::FO_SORT_WAVES), 0, s,
-                     dst, cntm, loffm, seg, nblk, cap, ctl, nout, zero_hist);
+  hipLaunchKernelGGL(dev::wc_fo_sort, dim3(nb / dev::FO_SORT_WAVES), dim3(64 * dev::FO_SORT_WAVES), 0, s, dst, cntm,
+                     loffm, seg, nblk, nb, cap, ctl, nout, zero_hist);
   return ctl;
 }
 

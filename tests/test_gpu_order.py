@@ -1,7 +1,9 @@
 """First-occurrence ordering on the GPU (sort.hip: the three-launch sample sort
 and its radix-sort fallbacks), exact against the CPU oracle.
 
-Stats()["order_path"]: 1 = sample sort, 2 = radix sort (above FO_MAX_KEYS or
+Stats()["order_path"]: 1 = sample sort (the engine uses it up to 400k keys;
+the kernel takes 512 bins up to 400k and 2048 up to FO_MAX_KEYS = 1.6M, tested
+directly below), 2 = radix sort (above 400k keys or
 WC_FIRST_ORDER=radix), 3 = a sample-sort bin overflowed and the radix sort
 redid the order, 4 = the speculative finalize's sample sort (sized from the
 previous job's key count) overflowed and the exact-count redo did not.
@@ -31,7 +33,7 @@ def test_sample_order_sizes(vocab, n):
             got = _resident(e, n, vocab, vocab)
             assert e.stats()["order_path"] in ((1, 2, 4) if job == 0 else (1, 2))
             assert_same(got, want)
-        assert e.stats()["order_path"] == (1 if len(want) <= 390_000 else 2)  # FO_MAX_KEYS
+        assert e.stats()["order_path"] == (1 if len(want) <= 390_000 else 2)  # the engine's sample-sort limit
 
 
 def test_radix_order_forced(monkeypatch):
@@ -105,7 +107,7 @@ def _first_order(keys, reps=1):
     return srt[:n], perm[:n], ovf.value
 
 
-@pytest.mark.parametrize("n", [1, 2, 63, 4095, 4097, 100_000, 300_000, 400_000])
+@pytest.mark.parametrize("n", [1, 2, 63, 4095, 4097, 100_000, 300_000, 400_000, 400_001, 1_000_000, 1_600_000])
 @pytest.mark.parametrize("dist", ["uniform", "crowded", "sorted", "reversed"])
 def test_first_order_kernel(n, dist):
     rng = np.random.default_rng(n)

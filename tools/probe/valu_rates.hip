@@ -76,6 +76,29 @@ __global__ void __launch_bounds__(1024) k_cmp64(uint32_t* out, uint32_t seed) {
   if (a[0] == 0x12345678u) out[threadIdx.x] = 1;
 }
 
+
+__global__ void __launch_bounds__(1024) k_and(uint32_t* out, uint32_t seed) { BODY("v_and_b32 %0, %0, %1") }
+__global__ void __launch_bounds__(1024) k_xor(uint32_t* out, uint32_t seed) { BODY("v_xor_b32 %0, %0, %1") }
+__global__ void __launch_bounds__(1024) k_lshr(uint32_t* out, uint32_t seed) { BODY("v_lshrrev_b32 %0, %1, %0") }
+__global__ void __launch_bounds__(1024) k_lshl(uint32_t* out, uint32_t seed) { BODY("v_lshlrev_b32 %0, %1, %0") }
+__global__ void __launch_bounds__(1024) k_lshrimm(uint32_t* out, uint32_t seed) { BODY("v_lshrrev_b32 %0, 3, %0\n v_xor_b32 %0, %0, %1") }
+__global__ void __launch_bounds__(1024) k_max(uint32_t* out, uint32_t seed) { BODY("v_max_u32 %0, %0, %1") }
+__global__ void __launch_bounds__(1024) k_sub(uint32_t* out, uint32_t seed) { BODY("v_sub_u32 %0, %0, %1") }
+__global__ void __launch_bounds__(1024) k_add3(uint32_t* out, uint32_t seed) { BODY("v_add3_u32 %0, %0, %1, %0") }
+__global__ void __launch_bounds__(1024) k_or3(uint32_t* out, uint32_t seed) { BODY("v_or3_b32 %0, %0, %1, %0") }
+__global__ void __launch_bounds__(1024) k_andor(uint32_t* out, uint32_t seed) { BODY("v_and_or_b32 %0, %0, %1, %0") }
+__global__ void __launch_bounds__(1024) k_lshladd(uint32_t* out, uint32_t seed) { BODY("v_lshl_add_u32 %0, %0, 3, %1") }
+__global__ void __launch_bounds__(1024) k_perm(uint32_t* out, uint32_t seed) { BODY("v_perm_b32 %0, %0, %1, %0") }
+__global__ void __launch_bounds__(1024) k_alignbyte(uint32_t* out, uint32_t seed) { BODY("v_alignbyte_b32 %0, %0, %1, %0") }
+__global__ void __launch_bounds__(1024) k_mul24e32(uint32_t* out, uint32_t seed) { BODY("v_mul_u32_u24_e32 %0, %1, %0") }
+__global__ void __launch_bounds__(1024) k_xorsdwa(uint32_t* out, uint32_t seed) { BODY("v_xor_b32_sdwa %0, %0, %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD") }
+__global__ void __launch_bounds__(1024) k_cmp32(uint32_t* out, uint32_t seed) { BODY("v_cmp_eq_u32 vcc, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc") }
+__global__ void __launch_bounds__(1024) k_cnd(uint32_t* out, uint32_t seed) { BODY("v_cndmask_b32 %0, %0, %1, vcc") }
+__global__ void __launch_bounds__(1024) k_min3(uint32_t* out, uint32_t seed) { BODY("v_min3_u32 %0, %0, %1, %0") }
+__global__ void __launch_bounds__(1024) k_bfi(uint32_t* out, uint32_t seed) { BODY("v_bfi_b32 %0, %0, %1, %0") }
+__global__ void __launch_bounds__(1024) k_mov(uint32_t* out, uint32_t seed) { BODY("v_mov_b32 %0, %1") }
+__global__ void __launch_bounds__(1024) k_pkadd(uint32_t* out, uint32_t seed) { BODY("v_pk_add_u16 %0, %0, %1") }
+
 typedef void (*Kern)(uint32_t*, uint32_t);
 
 int main() {
@@ -93,7 +116,13 @@ int main() {
             {"v_bitop3_b32", k_bitop3},      {"v_xad_u32", k_xad},           {"v_alignbit_b32", k_alignbit},
             {"v_bfe_u32", k_bfe},            {"v_ffbl_b32", k_ffbl},         {"v_bcnt_u32_b32", k_bcnt},
             {"v_lshl_or_b32", k_lshlor},     {"v_add_u32_dpp", k_dppadd},    {"v_lshrrev_b64", k_lshr64},
-            {"v_lshl_add_u64", k_add64},     {"v_cmp_eq_u64 (vcc)", k_cmp64}};
+            {"v_lshl_add_u64", k_add64},     {"v_cmp_eq_u64 (vcc)", k_cmp64},
+            {"v_and_b32", k_and}, {"v_xor_b32", k_xor}, {"v_lshrrev_b32 (vgpr)", k_lshr}, {"v_lshlrev_b32 (vgpr)", k_lshl},
+            {"lshr imm + xor (2 insts)", k_lshrimm}, {"v_max_u32", k_max}, {"v_sub_u32", k_sub}, {"v_add3_u32", k_add3},
+            {"v_or3_b32", k_or3}, {"v_and_or_b32", k_andor}, {"v_lshl_add_u32", k_lshladd}, {"v_perm_b32", k_perm},
+            {"v_alignbyte_b32", k_alignbyte}, {"v_mul_u32_u24_e32", k_mul24e32}, {"v_xor_b32_sdwa", k_xorsdwa},
+            {"v_cmp_eq_u32+cndmask (2)", k_cmp32}, {"v_cndmask_b32 vcc", k_cnd}, {"v_min3_u32", k_min3},
+            {"v_bfi_b32", k_bfi}, {"v_mov_b32", k_mov}, {"v_pk_add_u16", k_pkadd}};
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
