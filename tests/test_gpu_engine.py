@@ -102,11 +102,11 @@ def test_table_split_large_vocab():
     assert_same(got, ops.cpu_count(text))
 
 
-def test_combiner_closed_admission_and_refresh():
-    """A near-flat 1M-word vocabulary over 96 MiB: every map block sees far more
-    distinct keys than its table admits (1024), so most tokens become direct
-    shuffle records and every block refreshes its table many times (> 16 k
-    direct records each); counts and first occurrences must stay exact."""
+def test_combiner_flat_vocabulary():
+    """A near-flat 1M-word vocabulary over 96 MiB: the map blocks' read-only hot
+    tables (the sampled HOT_K most frequent candidates, map.hip wc_map) cover
+    few tokens, so most tokens become shuffle records (> half of them here) and
+    the reduce merges them; counts and first occurrences must stay exact."""
     text = ops.synth_host(96 << 20, seed=21, vocab=1000000, zipf_s=0.4)
     with ops.Engine(device=0) as e:
         e.count_bytes(text)
@@ -117,10 +117,11 @@ def test_combiner_closed_admission_and_refresh():
 
 
 def test_combiner_vocabulary_drift():
-    """The hot keys change half way through every block's share of the text
-    (alternate pieces are upper-cased): retained hot keys are evicted and the
-    new ones admitted while tokens keep flowing — counts and first occurrences
-    must stay exact."""
+    """The frequent keys change every 32 KiB (alternate pieces are upper-cased),
+    so a map block's hot table, sampled once per job from a few units of its
+    range, holds words of both halves and misses the rest: hits and records of
+    the same word mix in every block — counts and first occurrences must stay
+    exact."""
     half = ops.synth_host(48 << 20, seed=5, vocab=20000)
     upper = bytes.maketrans(b"abcdefghijklmnopqrstuvwxyz", b"ABCDEFGHIJKLMNOPQRSTUVWXYZ")
     n = len(half) // 2
