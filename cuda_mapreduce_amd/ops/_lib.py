@@ -54,6 +54,8 @@ def _load() -> ctypes.CDLL:
         "wc_bench_radix_sort": (c_int, [c_int, P64, c_uint64, c_int, c_int, POINTER(ctypes.c_double)]),
         "wc_debug_first_order": (c_int, [c_int, P64, c_uint64, c_int, P64, POINTER(ctypes.c_uint32),
                                          POINTER(c_int), POINTER(ctypes.c_double)]),
+        "wc_debug_order": (c_int, [c_int, c_int, P64, c_uint64, c_int, P64, POINTER(ctypes.c_uint32),
+                                   POINTER(c_int), POINTER(ctypes.c_double), P64]),
         "wc_default_options": (None, [POINTER(Options)]),
         "wc_engine_create": (c_void_p, [POINTER(Options)]),
         "wc_engine_destroy": (None, [c_void_p]),

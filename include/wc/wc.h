@@ -37,6 +37,11 @@ int wc_debug_radix_sort(int device, const uint64_t* keys, uint64_t n, int bits, 
 int wc_bench_radix_sort(int device, const uint64_t* keys, uint64_t n, int bits, int reps, double* ms);
 int wc_debug_first_order(int device, const uint64_t* keys, uint64_t n, int reps, uint64_t* sorted, uint32_t* perm,
                          int* overflow, double* ms);
+/* The same for method 0 (first_order, the sample sort) or 1 (bitmap_order over
+ * the keys themselves: distinct keys, a bitmap of max key + 1 bits); *residue =
+ * nonzero bitmap words left afterwards (0: the bitmap was cleared). */
+int wc_debug_order(int device, int method, const uint64_t* keys, uint64_t n, int reps, uint64_t* sorted,
+                   uint32_t* perm, int* overflow, double* ms, uint64_t* residue);
 void wc_default_options(wc_options* o);
 
 wc_engine* wc_engine_create(const wc_options* o);

@@ -34,7 +34,8 @@ struct Stats {
   // first-occurrence order of the last finalize: 1 = sample sort, 2 = radix
   // sort, 3 = sample sort overflowed and redone by the radix sort, 4 = the
   // speculative finalize's sample sort (sized by the previous job) overflowed
-  // and the exact-count one did not
+  // and the exact-count one did not, 5 = bitmap ranks (above 400k keys),
+  // 6 = the bitmap saw a shared position and the radix sort redid the order
   uint32_t order_path = 0;
   // cross-GPU merges of the engine's life run planned (fixed exchange regions,
   // no host round trip) / redone exactly after a planned one overflowed

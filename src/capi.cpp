@@ -246,8 +246,11 @@ int wc_bench_radix_sort(int device, const uint64_t* keys, uint64_t n, int bits, 
 // column source: sorted keys, the permutation (source row of each output row)
 // and the overflow word; *ms = device time averaged over `reps` (> 1: the
 // first rep warms up).  Tests + tools/sort_bench.py.
-int wc_debug_first_order(int device, const uint64_t* keys, uint64_t n, int reps, uint64_t* sorted, uint32_t* perm,
-                         int* overflow, double* ms) {
+// method 0: first_order (the sample sort); 1: bitmap_order over the keys
+// themselves (shift 0; keys must be distinct, the bitmap spans [0, max key]);
+// *residue = nonzero bitmap words left after the calls (must be 0).
+int wc_debug_order(int device, int method, const uint64_t* keys, uint64_t n, int reps, uint64_t* sorted,
+                   uint32_t* perm, int* overflow, double* ms, uint64_t* residue) {
   return guard([&] {
     WC_HIP_CHECK(hipSetDevice(device));
     hipStream_t s = nullptr;
@@ -255,7 +258,15 @@ int wc_debug_first_order(int device, const uint64_t* keys, uint64_t n, int reps,
     wc::OrderSrc src{};
     src.table = false;
     src.n = n;
-    const size_t ws = wc::first_order_ws_bytes(src, n);
+    uint64_t kmax = 0;
+    for (uint64_t i = 0; i < n; ++i) kmax = std::max(kmax, keys[i]);
+    const size_t ws = method == 1 ? wc::bitmap_order_ws_bytes(nn, kmax + 1, 0) : wc::first_order_ws_bytes(src, n);
+    unsigned long long* bm = nullptr;
+    const size_t bm_words = method == 1 ? wc::bitmap_order_words(kmax + 1, 0) : 0;
+    if (bm_words) {
+      WC_HIP_CHECK(hipMalloc(&bm, bm_words * 8));
+      WC_HIP_CHECK(hipMemset(bm, 0, bm_words * 8));
+    }
     uint8_t* mem = nullptr;
     WC_HIP_CHECK(hipMalloc(&mem, nn * (8 * 5 + 4) * 2 + ws + 4096));
     uint8_t* p = mem;
@@ -276,11 +287,7 @@ int wc_debug_first_order(int device, const uint64_t* keys, uint64_t n, int reps,
     d.slen = reinterpret_cast<uint32_t*>(take(nn * 4));
     void* w = take(ws);
     std::vector<uint64_t> idx(nn);
-    uint64_t kmax = 0;
-    for (uint64_t i = 0; i < n; ++i) {
-      idx[i] = i;
-      kmax = std::max(kmax, keys[i]);
-    }
+    for (uint64_t i = 0; i < n; ++i) idx[i] = i;
     uint32_t kb = 1;
     while (kb < 64 && (kmax >> kb) != 0) ++kb;
     WC_HIP_CHECK(hipMemcpy(in[0], idx.data(), n * 8, hipMemcpyHostToDevice));  // k0 = the source row
@@ -310,7 +317,8 @@ int wc_debug_first_order(int device, const uint64_t* keys, uint64_t n, int reps,
     for (int r = 0; r < std::max(reps, 1); ++r) {
       WC_HIP_CHECK(hipEventRecord(e0, s));
       if (stamps && r == 1) WC_HIP_CHECK(hipMemsetAsync(d_st, 0, 48 * 8, s));  // warm reps only
-      if (n) ovf = wc::first_order(src, d, n, kb, w, nullptr, s);
+      if (n && method == 1) ovf = wc::bitmap_order(src, d, n, kmax + 1, 0, bm, w, nullptr, s);
+      else if (n) ovf = wc::first_order(src, d, n, kb, w, nullptr, s);
       WC_HIP_CHECK(hipEventRecord(e1, s));
       WC_HIP_CHECK(hipEventSynchronize(e1));
       float t = 0;
@@ -337,10 +345,23 @@ int wc_debug_first_order(int device, const uint64_t* keys, uint64_t n, int reps,
     WC_HIP_CHECK(hipMemcpy(sorted, d.first, n * 8, hipMemcpyDeviceToHost));
     WC_HIP_CHECK(hipMemcpy(k0.data(), d.k0, n * 8, hipMemcpyDeviceToHost));
     for (uint64_t i = 0; i < n; ++i) perm[i] = (uint32_t)k0[i];
+    *residue = 0;
+    if (bm) {
+      std::vector<uint64_t> h(bm_words);
+      WC_HIP_CHECK(hipMemcpy(h.data(), bm, bm_words * 8, hipMemcpyDeviceToHost));
+      for (uint64_t x : h) *residue += x != 0;
+      WC_HIP_CHECK(hipFree(bm));
+    }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     WC_HIP_CHECK(hipFree(mem));
   });
+}
+
+int wc_debug_first_order(int device, const uint64_t* keys, uint64_t n, int reps, uint64_t* sorted, uint32_t* perm,
+                         int* overflow, double* ms) {
+  uint64_t residue = 0;
+  return wc_debug_order(device, 0, keys, n, reps, sorted, perm, overflow, ms, &residue);
 }
 
 int wc_device_count(void) {

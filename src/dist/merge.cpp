@@ -495,11 +495,15 @@ void learn_caps(Engine::Impl& im, const OwnerPlan& P, const std::vector<unsigned
 // long words), owner o's merged rows in a region of caps.merged rows for the
 // gather (dense: padded ids o * caps.merged + index) — padding rows are empty
 // keys that the owner merge skips.  Counts, decisions and the merged key count
-// stay on the device: nothing here waits.  wc_merge_check ORs into
-// im.d_merge_flags, from the all-gathered words every rank reads alike: a
-// last pass needing recovery (1), an arena overflow (2), a region overflow (4)
-// — the finalize reads them after its last wait, and every rank redoes the
-// merge with the exact protocol together when they are set.
+// stay on the device: nothing here waits.  Each rank's word quad (merged rows,
+// flags, max first offset, -) travels in ONE all-gather after the owner
+// merge: its scatter sets the flags (a last pass needing recovery 1, an arena
+// overflow 2, a region overflow 4), and wc_merge_check ORs every rank's into
+// im.d_merge_flags (+ 4 for merged rows past their region or a first offset
+// above the key width the order is sized for) — the finalize reads them after
+// its last wait, and every rank redoes the merge with the exact protocol
+// together when they are set.  (Before: an owner-count launch, a count-matrix
+// all-gather and a check ahead of the scatter — one more collective.)
 // Columns in: im.cols with n the bound and dn the device count.
 void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense, const uint32_t* pass_flags) {
   Range rg(dense ? "wc_merge_dense_planned" : "wc_merge_shuffle_planned");
@@ -510,18 +514,18 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
   const uint64_t Cr = cp.rows, Cb = cp.bytes, Gr = cp.merged;
   const uint64_t nb = im.cols.n;  // bound; the count is *dn
   const uint64_t* dn = reinterpret_cast<const uint64_t*>(im.cols.dn);
-  const size_t C = 2 * (size_t)W + 2;
   DeviceArena& S = im.merge_small;
-  S.reserve(((size_t)W * C + 2 * C + 4 * (size_t)W + 64) * 8 + 8 * 1024);
+  S.reserve((8 * (size_t)W + 64) * 8 + 8 * 1024);
   S.reset();
-  unsigned long long* d_cnt = take_aligned<unsigned long long>(S, 2 * C);  // counts | max offset | flags | cursor
-  unsigned long long* d_all = take_aligned<unsigned long long>(S, (size_t)W * C);
-  unsigned long long* d_own = take_aligned<unsigned long long>(S, 2);
-  unsigned long long* d_owns = take_aligned<unsigned long long>(S, 2 * (size_t)W);
+  unsigned long long* d_cur = take_aligned<unsigned long long>(S, 2 * (size_t)W);  // scatter cursor per owner
+  unsigned long long* d_own = take_aligned<unsigned long long>(S, 4);  // merged rows | flags | max offset | -
+  unsigned long long* d_owns = take_aligned<unsigned long long>(S, 4 * (size_t)W);
   unsigned long long* d_on = take_aligned<unsigned long long>(S, 1);
   im.d_merge_flags = take_aligned<uint32_t>(S, 2);
   uint64_t* mx = host_words(im) + HW_MX;
   *mx = im.max_end;
+  // the key width the finalize's order is sized for: every rank's first offsets must fit it
+  const uint64_t key_bound = std::max(im.max_end, cp.gmax_end);
   uint64_t* base = host_words(im) + HW_BASE;  // fixed-region bases per source: rows | bytes
   for (int p = 0; p <= W; ++p) {
     base[p] = (uint64_t)p * Cr;
@@ -550,37 +554,29 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
   MRow* merged = take_aligned<MRow>(A, RR);  // compaction writes up to RR rows; the first Gr are sent
   uint64_t* d_base = take_aligned<uint64_t>(A, 2 * (size_t)W + 2);
   uint64_t* d_seg = take_aligned<uint64_t>(A, (size_t)W + 1);
-  unsigned long long* d_m = take_aligned<unsigned long long>(A, 1);
   uint32_t* send_pos = dense ? take_aligned<uint32_t>(A, nb) : nullptr;
   uint32_t* row_slot = dense ? take_aligned<uint32_t>(A, RR) : nullptr;
   uint32_t* slot_id = dense ? take_aligned<uint32_t>(A, T) : nullptr;
   {
-    ZeroList z{};  // counts, flags, cursor, padding rows, the owner table, the merged region: two launches
-    z.add(d_cnt, 2 * (size_t)W * 8);
-    z.add(d_cnt + 2 * W + 1, (2 * C - 2 * (size_t)W - 1) * 8);
+    ZeroList z{};  // cursor, flags, padding rows, the owner table, the merged region, this rank's quad: ONE launch
+    z.add(d_cur, 2 * (size_t)W * 8);
     z.add(im.d_merge_flags, 8);
     z.add(send_rows, RR * sizeof(MRow));
     z.add(state, T * 4);
     z.add(tcnt, T * 8);
     z.add(tfirst, T * 8, 0xFFFFFFFFu);
     z.add(merged, Gr * sizeof(MRow));
-    z.copy(d_cnt + 2 * W, mx, 8);
+    z.add(d_own, 16);  // merged rows (wc_mrow_compact adds), flags (the scatter ORs)
+    z.copy(d_own + 2, mx, 8);
     z.copy(d_base, base, (2 * (size_t)W + 2) * 8);
     z.copy(d_seg, seg, ((size_t)W + 1) * 8);
     launch_zero_regions(z, s);
-    ZeroList z2{};
-    z2.add(d_m, 8);
-    z2.add(d_own + 1, 8);
-    launch_zero_regions(z2, s);
   }
-  // 1. owner counts (+ max offset, pass flags), all-gathered: the decision words
-  launch_owner_count(im.cols.k0, im.cols.k1, im.cols.sref_len, nb, dn, pass_flags, (uint32_t)W, d_cnt, s);
-  comm.allgather(d_cnt, d_all, C * 8, s);
-  launch_merge_check(d_all, (uint32_t)W, Cr, Cb, nullptr, 0, im.d_merge_flags, s);
-  // 2. pack into the fixed regions and exchange them whole
+  // 1. pack into the fixed regions (this rank's pass flags and region overflow
+  // into its flag word) and exchange them whole
   launch_owner_scatter(im.cols.k0, im.cols.k1, im.cols.cnt, im.cols.first, im.cols.sref_off, im.cols.sref_len,
-                       im.cols_arena, nb, (uint32_t)W, nullptr, d_cnt + C, send_rows, send_bytes, send_pos, s, dn, Cr,
-                       Cb, im.d_merge_flags);
+                       im.cols_arena, nb, (uint32_t)W, nullptr, d_cur, send_rows, send_bytes, send_pos, s, dn, Cr, Cb,
+                       reinterpret_cast<uint32_t*>(d_own + 1), pass_flags);
   std::vector<size_t> ro(W), rs(W, Cr * sizeof(MRow)), bo(W), bs(W, Cb), zs(W, 0), gr(W, 0), gb(W, 0), go(W), gbo(W);
   for (int p = 0; p < W; ++p) {
     ro[p] = (size_t)p * Cr * sizeof(MRow);
@@ -590,16 +586,12 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
   comm.alltoallv(send_rows, ro.data(), rs.data(), recv_rows, ro.data(), rs.data(), s);
   comm.alltoallv(send_bytes, bo.data(), bs.data(), recv_bytes, bo.data(), bs.data(), s);
   comm.group_end();
-  // 3. owner merge (padding rows skipped), merged rows counted on the device
+  // 2. owner merge (padding rows skipped), merged rows counted on the device into the quad
   launch_mrow_insert(recv_rows, RR, recv_bytes, d_base, d_base + W + 1, (uint32_t)W, state, tcnt, tfirst, T, row_slot,
                      s);
-  launch_mrow_compact(recv_rows, state, tcnt, tfirst, T, d_base, d_base + W + 1, (uint32_t)W, merged, d_m, slot_id, s);
-  {
-    ZeroList z{};
-    z.copy(d_own, d_m, 8);
-    launch_zero_regions(z, s);
-  }
-  // 4. every owner's merged count (+ dense: the owner-local ids back to the senders)
+  launch_mrow_compact(recv_rows, state, tcnt, tfirst, T, d_base, d_base + W + 1, (uint32_t)W, merged, d_own, slot_id,
+                      s);
+  // 3. every rank's quad (+ dense: the owner-local ids back to the senders), the decision
   uint32_t* ids = nullptr;
   uint32_t* ids_back = nullptr;
   if (dense) {
@@ -608,15 +600,15 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
     launch_row_ids(row_slot, slot_id, RR, d_owns, 0u, ids, s);
   }
   comm.group_begin();
-  comm.allgather(d_own, d_owns, 16, s);
+  comm.allgather(d_own, d_owns, 32, s);
   if (dense) {
     std::vector<size_t> io(W), is(W, Cr * 4);
     for (int p = 0; p < W; ++p) io[p] = (size_t)p * Cr * 4;
     comm.alltoallv(ids, io.data(), is.data(), ids_back, io.data(), is.data(), s);
   }
   comm.group_end();
-  launch_merge_check(nullptr, (uint32_t)W, 0, 0, d_owns, Gr, im.d_merge_flags, s);
-  // 5. dense: padded count / first-offset vectors, reduce-scattered (owner o's
+  launch_merge_check(d_owns, (uint32_t)W, Gr, key_bound, im.d_merge_flags, s);
+  // 4. dense: padded count / first-offset vectors, reduce-scattered (owner o's
   // slice = its ids) and all-gathered
   uint64_t *dcnt = nullptr, *dfirst = nullptr;
   if (dense) {
@@ -640,7 +632,7 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
     comm.allgather(sfirst, dfirst, Gr * 8, s);
     comm.group_end();
   }
-  // 6. every owner's merged region (+ its whole received byte payload) to rank 0
+  // 5. every owner's merged region (+ its whole received byte payload) to rank 0
   for (int p = 0; p < W; ++p) {
     go[p] = (size_t)p * Gr * sizeof(MRow);
     gbo[p] = (size_t)p * RB;

@@ -66,7 +66,10 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   if (const char* e = std::getenv("WC_NO_SPECULATE")) speculate = std::atoi(e) == 0;
   if (const char* e = std::getenv("WC_SPIN_WAIT")) spin_wait = std::atoi(e) != 0;
   if (const char* e = std::getenv("WC_STAGE_EVENTS")) stage_events = std::atoi(e) != 0;
-  if (const char* e = std::getenv("WC_FIRST_ORDER")) order_radix = std::string(e) == "radix";
+  if (const char* e = std::getenv("WC_FIRST_ORDER")) {
+    order_radix = std::string(e) == "radix";
+    order_bitmap = std::string(e) == "bitmap";
+  }
   if (const char* e = std::getenv("WC_HOT_RESAMPLE_EVERY")) hot_resample_every = (uint32_t)std::atoi(e);
   k1_mask = k1_hash_mask(opt.k1_hash_bits);
   if (const char* e = std::getenv("WC_MAP_STAMPS"); e && std::atoi(e)) {
@@ -172,6 +175,7 @@ Engine::Impl::~Impl() {
   if (d_arena_cursor) (void)hipFree(d_arena_cursor);
   if (d_fo_hist) (void)hipFree(d_fo_hist);
   if (d_fo_hist_cols) (void)hipFree(d_fo_hist_cols);
+  if (d_bm) (void)hipFree(d_bm);
   if (d_stamps) {
     unsigned long long h[MAP_STAMP_N];
     if (hipMemcpy(h, d_stamps, sizeof h, hipMemcpyDeviceToHost) == hipSuccess && h[MS_TOTAL]) {
@@ -549,6 +553,19 @@ void Engine::Impl::process_chunk(const uint8_t* text, uint64_t len, uint64_t ava
   complete_pass(text, len, avail, base, prev, rb, blocks);
 }
 
+unsigned long long* Engine::Impl::ensure_bitmap() {
+  const size_t words = bitmap_order_words(max_end, 1);
+  if (words > bm_words) {
+    if (d_bm) WC_HIP_CHECK(hipFree(d_bm));  // waits for the device: nothing in flight reads it
+    d_bm = nullptr;
+    const size_t w = words + words / 4;  // room for a growing input
+    WC_HIP_CHECK(hipMalloc(&d_bm, w * 8));
+    WC_HIP_CHECK(hipMemsetAsync(d_bm, 0, w * 8, s));  // once: every bitmap_order leaves it zeroed
+    bm_words = w;
+  }
+  return d_bm;
+}
+
 void Engine::Impl::compact_local() {
   Range r("wc_finalize_compact");
   const TableView& t = table();
@@ -591,13 +608,16 @@ bool Engine::Impl::finalize_local_speculative() {
   const uint64_t cap = (uint64_t)nb * TAB_SLOTS;
   const uint64_t hint = std::min<uint64_t>(cap, last_keys ? last_keys + last_keys / 8 + 1024 : cap / 4);
   const bool sample = sample_order(hint);  // sized for the hint; a far larger count -> overflow -> redo
+  const bool bitmap = !sample && bitmap_order_ok(hint);
   OrderSrc src{};
   src.table = true;
   src.t = t;
   DeviceArena& A = sort_mem;
   A.reserve((cap + 1) * (5 * 8 + 4) + 64 * 1024 +
-            (sample ? first_order_ws_bytes(src, hint)
-                    : (cap + 1) * (2 * 8 + 2 * 4) + nb * 8 + radix_hist_words(cap, hint) * 4));
+            (sample   ? first_order_ws_bytes(src, hint)
+             : bitmap ? bitmap_order_ws_bytes(cap + 1, max_end, 1)
+                      : (cap + 1) * (2 * 8 + 2 * 4) + nb * 8 + radix_hist_words(cap, hint) * 4));
+  unsigned long long* bm = bitmap ? ensure_bitmap() : nullptr;
   A.reset();
   uint64_t* d_n = A.take_n<uint64_t>(2);
   KeyCols o;
@@ -612,6 +632,9 @@ bool Engine::Impl::finalize_local_speculative() {
     ovf = first_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len}, hint, key_bits(),
                       A.take_n<uint8_t>(first_order_ws_bytes(src, hint)), d_n, s, fo_hist_ok ? d_fo_hist : nullptr,
                       fo_hist_m);
+  } else if (bitmap) {
+    ovf = bitmap_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len}, cap, max_end, 1, bm,
+                       A.take_n<uint8_t>(bitmap_order_ws_bytes(cap + 1, max_end, 1)), d_n, s);
   } else {
     uint64_t* d_boff = A.take_n<uint64_t>(nb);
     uint64_t* keys = A.take_n<uint64_t>(cap + 1);
@@ -650,9 +673,9 @@ bool Engine::Impl::finalize_local_speculative() {
   else WC_HIP_CHECK(hipStreamSynchronize(s));
   // the pass's counters arrived with this sync: check it (stats, recovery)
   if (!complete_pass(p.text, p.len, p.avail, p.base, p.prev, p.rb, p.blocks, true)) return false;
-  if (*h_ovf) {  // a sample-sort bin overflowed (far more keys than the hint): redo exactly
-    WC_LOG(LOG_INFO, "dev %d: first-occurrence sample sort overflowed (hint %llu keys); redoing", dev,
-           (unsigned long long)hint);
+  if (*h_ovf) {  // a sample-sort bin overflowed (far more keys than the hint) / shared bitmap position: redo exactly
+    WC_LOG(LOG_INFO, "dev %d: first-occurrence %s order overflowed (hint %llu keys); redoing", dev,
+           bitmap ? "bitmap" : "sample", (unsigned long long)hint);
     last_keys = 0;
     order_redo = true;
     return false;
@@ -666,7 +689,7 @@ bool Engine::Impl::finalize_local_speculative() {
   cols_arena_bytes = std::min<uint64_t>(arena_used, opt.arena_bytes);
   st.keys = n;
   st.log2_buckets = t.log2_buckets;
-  st.order_path = sample ? 1 : 2;
+  st.order_path = sample ? 1 : bitmap ? 5 : 2;
   last_keys = n;
   return true;
 }
@@ -706,8 +729,24 @@ void Engine::Impl::finalize_local_sorted() {
     uint32_t bad = 0;
     std::memcpy(&bad, h_fin.data() + 8, 4);
     st.order_path = bad ? 3 : 1;
+  } else if (bitmap_order_ok(n)) {
+    OrderSrc src{};
+    src.table = true;
+    src.t = t;
+    unsigned long long* bm = ensure_bitmap();
+    A.reserve((n + 1) * (5 * 8 + 4) + bitmap_order_ws_bytes(n + 1, max_end, 1) + 64 * 1024);
+    A.reset();
+    take_cols();
+    const uint32_t* ovf = bitmap_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len}, n, max_end,
+                                       1, bm, A.take_n<uint8_t>(bitmap_order_ws_bytes(n + 1, max_end, 1)), nullptr, s);
+    if (h_fin.size() < 64) h_fin = PinnedBuffer(64);
+    WC_HIP_CHECK(hipMemcpyAsync(h_fin.data() + 8, ovf, 4, hipMemcpyDeviceToHost, s));
+    WC_HIP_CHECK(hipStreamSynchronize(s));
+    uint32_t bad = 0;
+    std::memcpy(&bad, h_fin.data() + 8, 4);
+    st.order_path = bad ? 6 : 5;
   }
-  if (st.order_path != 1) {
+  if (st.order_path != 1 && st.order_path != 5) {
     A.reserve((n + 1) * (2 * 8 + 2 * 4 + 5 * 8 + 4) + nb * 8 + radix_hist_words(n) * 4 + 64 * 1024);
     A.reset();
     uint64_t* d_boff = A.take_n<uint64_t>(nb);
@@ -773,6 +812,28 @@ void Engine::Impl::sort_cols_by_first(bool radix) {
     cols_unsorted = cols;
     cols = o;
     st.order_path = 1;
+    return;
+  }
+  if (!radix && bitmap_order_ok(n)) {  // the same in-flight overflow word as the sample sort
+    OrderSrc src{};
+    src.table = false;
+    src.k0 = cols.k0;
+    src.k1 = cols.k1;
+    src.cnt = cols.cnt;
+    src.first = cols.first;
+    src.soff = cols.sref_off;
+    src.slen = cols.sref_len;
+    src.n = n;
+    src.dn = dn;
+    unsigned long long* bm = ensure_bitmap();
+    A.reserve(n * (5 * 8 + 4) + bitmap_order_ws_bytes(n, max_end, 1) + 64 * 1024);
+    A.reset();
+    take_cols();
+    fo_ovf = bitmap_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len}, n, max_end, 1, bm,
+                          A.take_n<uint8_t>(bitmap_order_ws_bytes(n, max_end, 1)), nullptr, s);
+    cols_unsorted = cols;
+    cols = o;
+    st.order_path = 5;
     return;
   }
   A.reserve(n * (2 * 8 + 2 * 4 + 5 * 8 + 4) + radix_hist_words(n) * 4 + 64 * 1024);
@@ -1189,9 +1250,11 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
     uint32_t bad = 0;
     std::memcpy(&bad, im.h_fin.data() + 8, 4);
     im.fo_ovf = nullptr;
-    if (bad) {  // a sample-sort bin overflowed: redo the order with the radix sort (its input is intact)
+    if (bad) {  // a sample-sort bin overflowed / a shared bitmap position: redo the order with the radix sort
+      const bool was_bitmap = im.st.order_path == 5;
       im.cols = im.cols_unsorted;
       im.sort_cols_by_first(true);
+      if (was_bitmap) im.st.order_path = 6;
       WC_HIP_CHECK(hipStreamSynchronize(im.s));
     }
   }

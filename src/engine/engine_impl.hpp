@@ -237,7 +237,17 @@ struct Engine::Impl {
   // sort (first_order handles up to FO_MAX_KEYS) measured no faster at 1M keys
   // — fo_bin 73 + fo_sort 138 us vs 200 us of radix passes + gather
   // (profiles/r4_session3.md §7)
-  bool sample_order(uint64_t bound) const { return !order_radix && bound <= 400000; }
+  bool sample_order(uint64_t bound) const { return !order_radix && !order_bitmap && bound <= 400000; }
+  // Above it the bitmap ranks (bitmap_order: first >> 1 positions, a 64 MiB
+  // bitmap per GiB of text) while the bitmap stays within 128 bytes per key;
+  // WC_FIRST_ORDER=bitmap takes it at every size.
+  bool order_bitmap = false;
+  bool bitmap_order_ok(uint64_t bound) const {
+    return !order_radix && (order_bitmap || (bound > 400000 && (max_end >> 4) <= 128 * bound));
+  }
+  unsigned long long* d_bm = nullptr;  // bitmap_order's bitmap: all zero between calls
+  size_t bm_words = 0;
+  unsigned long long* ensure_bitmap();  // sized for max_end
   uint32_t* fo_ovf = nullptr;  // overflow word of the sample sort sort_cols_by_first left in flight
   KeyCols cols_unsorted;       // its input, kept for a radix redo
   bool order_redo = false;     // the speculative finalize's sample sort overflowed (Stats::order_path 4)

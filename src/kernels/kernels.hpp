@@ -274,6 +274,21 @@ uint32_t* first_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, 
                       uint64_t* nout, hipStream_t s, const uint32_t* key_hist = nullptr, uint32_t key_hist_m = 0,
                       uint32_t* hist_ws = nullptr);
 
+// First-occurrence order by ranks from a bitmap over first >> shift (sort.hip:
+// five launches, no comparison sort; the engine uses it above 400k keys).
+// Positions must be distinct (shift 1: two token starts are >= 2 bytes apart)
+// and first < key_end.  bm: bitmap_order_words(key_end, shift) words, all zero
+// on entry and left all zero (a control word follows the bitmap).  bound >= the
+// key count (a column source: its row bound, *src.dn the count when set; a
+// table source reads every slot).  ws: bitmap_order_ws_bytes(bound, ...).
+// *nout (if given) = the key count.  Returns a device word that is nonzero
+// after the stream if two keys shared a position or one lay beyond key_end:
+// the output is then invalid (redo with radix_sort_pairs).
+size_t bitmap_order_words(uint64_t key_end, uint32_t shift);
+size_t bitmap_order_ws_bytes(uint64_t bound, uint64_t key_end, uint32_t shift);
+uint32_t* bitmap_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, uint64_t key_end, uint32_t shift,
+                       unsigned long long* bm, void* ws, uint64_t* nout, hipStream_t s);
+
 // out[i] = in[perm[i]] for the six key-table columns (one launch).
 void launch_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
                         const uint64_t* soff, const uint32_t* slen, const uint32_t* perm, uint64_t* ok0, uint64_t* ok1,
@@ -350,14 +365,16 @@ void launch_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* 
 // send_pos (nullable): row index of each local key; dn: device-side row count
 // (n the bound); reg_rows > 0: planned mode — owner o's rows / bytes in fixed
 // regions of reg_rows rows / reg_bytes bytes (counts unused), overflow -> *ovf
+// bit 2, and pass_flags (nullable) -> *ovf bits 0 / 1 (rerun / arena overflow)
 void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
                           const uint64_t* soff, const uint32_t* slen, const uint8_t* arena, uint64_t n, uint32_t W,
                           const unsigned long long* counts, unsigned long long* cursor, MRow* rows, uint8_t* bytes,
                           uint32_t* send_pos, hipStream_t s, const uint64_t* dn = nullptr, uint64_t reg_rows = 0,
-                          uint64_t reg_bytes = 0, uint32_t* ovf = nullptr);
-// Planned merge: decision flags from the gathered count matrix / owner counts (merge.hip).
-void launch_merge_check(const unsigned long long* all, uint32_t W, uint64_t reg_rows, uint64_t reg_bytes,
-                        const unsigned long long* owns, uint64_t reg_merged, uint32_t* flags, hipStream_t s);
+                          uint64_t reg_bytes = 0, uint32_t* ovf = nullptr, const uint32_t* pass_flags = nullptr);
+// Planned merge: the decision flags from every rank's gathered word quad
+// (merged rows, flags, max first offset, -) (merge.hip).
+void launch_merge_check(const unsigned long long* owns, uint32_t W, uint64_t reg_merged, uint64_t max_end,
+                        uint32_t* flags, hipStream_t s);
 void launch_mrow_regions_to_cols(const MRow* rows, uint32_t W, uint64_t reg_merged, const unsigned long long* owns,
                                  uint64_t byte_stride, const uint64_t* dcnt, const uint64_t* dfirst, uint64_t* k0,
                                  uint64_t* k1, uint64_t* cnt, uint64_t* first, uint64_t* soff, uint32_t* slen,

@@ -645,7 +645,7 @@ struct alignas(16) MapLds {
   alignas(16) uint64_t sig[MAP_SLOTS];  // hot table image (read-only while tokens stream); 0 = empty
   uint16_t list[MAP_WAVES][MAP_LIST];
   uint16_t dlist[MAP_WAVES][MAP_DEF_CAP];  // deferred LONG entries of a round: pos | (len - 16) << 11 | prev << 15
-  uint32_t bcur[MAX_REC_BUCKETS];       // records appended to each bucket's sub-region (Rec16 | Rec << 16)
+  uint32_t bcur[2 * MAX_REC_BUCKETS];   // record cursors (map_common.hpp cursors_init): Rec16 | Rec per bucket
   alignas(16) uint8_t buf[MAP_WAVES][2][BUF];  // two unit slots per wave: the current unit and the one before
   uint32_t next_unit;
   unsigned long long used, tokens;
@@ -671,11 +671,14 @@ __device__ __forceinline__ int sig_slot4(const u64x2& a, const u64x2& b, uint64_
 // Hot-table slot of an inline token (signature sig, k0): a one-slot word
 // (sig's top byte < 8) in any of the four slots; a two-word word only in a
 // group's first slot with k0 in the second.  -1: not in the table.
-__device__ __forceinline__ int inline_slot(const u64x2& a, const u64x2& b, uint64_t sig, uint64_t k0, uint32_t o1,
-                                           uint32_t o2) {
-  if (!two_word(sig)) return sig_slot4(a, b, sig, o1, o2);
+__device__ __forceinline__ int pair_slot(const u64x2& a, const u64x2& b, uint64_t sig, uint64_t k0, uint32_t o1,
+                                         uint32_t o2) {
   const int s = b.x == sig && b.y == k0 ? (int)(o2 >> 1) : -1;
   return a.x == sig && a.y == k0 ? (int)(o1 >> 1) : s;
+}
+__device__ __forceinline__ int inline_slot(const u64x2& a, const u64x2& b, uint64_t sig, uint64_t k0, uint32_t o1,
+                                           uint32_t o2) {
+  return two_word(sig) ? pair_slot(a, b, sig, k0, o1, o2) : sig_slot4(a, b, sig, o1, o2);
 }
 
 // LDS word at byte offset o of an array (the hot table's count / offset arrays).
@@ -687,7 +690,8 @@ template <bool ST>
 __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   __shared__ MapLds L;
   __shared__ unsigned long long st_acc[ST ? MAP_STAMP_N : 1];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: per-wave LDS bases in SGPRs
   if (ST && tid < MAP_STAMP_N) st_acc[tid] = 0;
 #pragma unroll
   for (int j = 0; j < SPT; ++j) {
@@ -696,7 +700,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     L.cnt[s] = 0;
     L.off[s] = 0xFFFFFFFFu;
   }
-  for (uint32_t b = tid; b < MAX_REC_BUCKETS; b += MAP_THREADS) L.bcur[b] = 0;
+  cursors_init(L.bcur, 1u << a.log2_rec_buckets, a.rec.subcap);
   // the table image, built in this block's LDS (the unit buffers and token
   // lists are its scratch until the first unit)
   static_assert(sizeof(L.buf) >= 4 * (SEL_BINS + 20) && sizeof(L.list) >= 4 * NG, "image scratch");
@@ -782,7 +786,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
           atomicAdd(&L.cnt[slot], 1u);
           atomicMin(&L.off[slot], (uint32_t)(u0 + q));
         } else {
-          emit_record(L.bcur, a, rout, place_hash(k0, k1) & bmask, k0, k1, 1, (uint32_t)(u0 + q));
+          emit_record(L.bcur, rout, place_hash(k0, k1) & bmask, k0, k1, 1, (uint32_t)(u0 + q));
         }
       }
     }
@@ -886,12 +890,13 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
       const uint8_t* S = reinterpret_cast<const uint8_t*>(L.sig);
       int s1 = -1, s2 = -1;  // counter byte offsets
       {  // both slots of a group in one 16-byte read
+        // (other class, 8..15 bytes: always a two-word signature — only the pair match)
         const u64x2 xa0 = *reinterpret_cast<const u64x2*>(S + ga1), xa1 = *reinterpret_cast<const u64x2*>(S + ga2);
         if (TWO) {
           const u64x2 xb0 = *reinterpret_cast<const u64x2*>(S + gb1), xb1 = *reinterpret_cast<const u64x2*>(S + gb2);
-          s2 = in2 ? inline_slot(xb0, xb1, bs, b0, gb1, gb2) : -1;
+          s2 = in2 ? (ANY ? inline_slot(xb0, xb1, bs, b0, gb1, gb2) : pair_slot(xb0, xb1, bs, b0, gb1, gb2)) : -1;
         }
-        s1 = in1 ? inline_slot(xa0, xa1, as, a0, ga1, ga2) : -1;
+        s1 = in1 ? (ANY ? inline_slot(xa0, xa1, as, a0, ga1, ga2) : pair_slot(xa0, xa1, as, a0, ga1, ga2)) : -1;
       }
       clk.lap(MS_PROBE);
       const uint32_t o1 = (uint32_t)(old1 ? pu0 : cu0) + q1, o2 = (uint32_t)(old2 ? pu0 : cu0) + q2;
@@ -906,7 +911,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
       if (WC_MAP_ABLATE == 3) return;
       // misses of inline words become records now; LONG words wait for the round end
       const bool d1 = in1 && s1 < 0, d2 = TWO && in2 && s2 < 0;
-      emit_two(L.bcur, a, rout, d1, ha & bmask, a0, a1, o1, n1, d2, hb & bmask, b0, b1, o2, n2);
+      emit_two(L.bcur, rout, d1, ha & bmask, a0, a1, o1, n1, d2, hb & bmask, b0, b1, o2, n2);
       const bool f1 = h1 && !in1, f2 = TWO && h2 && !in2;
       const uint64_t mf1 = __ballot(f1), mf2 = TWO ? __ballot(f2) : 0ull;
       if (mf1 | mf2) {  // LONG entries (length field 16..31) to the round's deferred list
@@ -991,7 +996,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
       }
       if (WC_MAP_ABLATE == 3) return;
       const bool d1 = h1 && s1 < 0, d2 = TWO && h2 && s2 < 0;
-      emit_two_short(L.bcur, a, rout, d1, ha & bmask, a0, o1, n1, d2, hb & bmask, b0, o2, n2);
+      emit_two_short(L.bcur, rout, d1, ha & bmask, a0, o1, n1, d2, hb & bmask, b0, o2, n2);
       if constexpr (ST) {
         my_direct += (uint32_t)(__popcll(__ballot(d1)) + (TWO ? __popcll(__ballot(d2)) : 0));
         const uint32_t nh = (uint32_t)(__popcll(__ballot(s1 >= 0)) + __popcll(__ballot(s2 >= 0)));
@@ -1142,7 +1147,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     const uint64_t sd = (two_word(sg) || is_long_sig(sg)) ? L.sig[s | 1] : 0ull;
     if (is_long_sig(sg)) key_long_line(h.long_bytes + (sd >> 32) * 64, (uint32_t)sd, a.k1_mask, k0, k1);
     else sig_key(sg, sd, k0, k1);
-    emit_record(L.bcur, a, rout, place_hash(k0, k1) & bmask, k0, k1, c, L.off[s]);
+    emit_record(L.bcur, rout, place_hash(k0, k1) & bmask, k0, k1, c, L.off[s]);
   }
   clk.lap(MS_FLUSH);
   if constexpr (ST) {
@@ -1165,9 +1170,11 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   __syncthreads();  // every flush's cursor add is in
   uint64_t t = my_tokens, e = 0;
   for (uint32_t b = tid; b < nb; b += MAP_THREADS) {
-    const uint32_t c = L.bcur[b];
-    a.rec.count[(size_t)blockIdx.x * nb + b] = c;
-    e += (c & 0xFFFFu) + (c >> 16);
+    const uint32_t sub = rout.sub, c16 = L.bcur[b] - b * sub, c24 = L.bcur[MAX_REC_BUCKETS + b] - b * sub;
+    if (c16 > sub || c24 > sub) atomicOr(&a.flags[FLAG_REGION_OVF], 1u);  // overran into the next sub-region
+    const uint32_t n16 = min(c16, sub), n24 = min(c24, sub);
+    a.rec.count[(size_t)blockIdx.x * nb + b] = n16 | (n24 << 16);  // packed for the reducer (sub <= 0xFFFF)
+    e += n16 + n24;
   }
   for (int o = 32; o > 0; o >>= 1) {
     t += __shfl_down(t, o);

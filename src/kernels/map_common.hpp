@@ -163,99 +163,96 @@ __device__ __forceinline__ Rec16 make_rec16(uint64_t k0, uint64_t k1, uint32_t o
 }
 
 // This block's record sub-regions: bucket b's run starts at (b * sub) records
-// from the block base (b * sub < 2^25: 32-bit index math, full-rate multiply).
+// from the block base (b * sub < 2^25: 32-bit index math).  lim: the last
+// record index of the block's area (nb * sub - 1).
 struct RecOut {
   Rec16* b16;
   Rec* b24;
-  uint32_t sub;
+  uint32_t sub, lim;
 };
 __device__ __forceinline__ RecOut rec_out(const MapArgs& a) {
   const uint64_t first = ((uint64_t)blockIdx.x << a.log2_rec_buckets) * a.rec.subcap;
-  return RecOut{a.rec.recs16 + first, a.rec.recs + first, a.rec.subcap};
+  return RecOut{a.rec.recs16 + first, a.rec.recs + first, a.rec.subcap,
+                (a.rec.subcap << a.log2_rec_buckets) - 1u};
 }
 
-// Store one record at cursor value `packed` of bucket b's sub-region.  The
-// block's store bases are wave-uniform (SGPRs) and a record's byte offset in
-// them fits 32 bits (index < 2^25), so the stores take the SGPR-base + 32-bit
-// VGPR-offset form: one 24-bit multiply per record, no 64-bit address math.
-__device__ __forceinline__ void put_record(const MapArgs& a, const RecOut& o, uint32_t b, uint32_t packed, bool r16,
-                                          uint64_t k0, uint64_t k1, uint64_t cnt, uint32_t off) {
-  const uint32_t pos = r16 ? (packed & 0xFFFFu) : (packed >> 16);
-  const uint32_t idx = __umul24(b, o.sub) + pos;
-  if (pos >= o.sub) {
-    atomicOr(&a.flags[FLAG_REGION_OVF], 1u);
-    return;
+// Record cursors in LDS: cur[b] (Rec16) and cur[MAX_REC_BUCKETS + b] (Rec)
+// start at b * sub, so a cursor atomic returns the record's index in the
+// block's area directly (no select of a packed half, no multiply).  A bucket
+// that outgrows its sub-region writes on into the next bucket's — the block
+// end sees it (cursor - b * sub > sub), raises FLAG_REGION_OVF and the host
+// re-runs the pass, discarding its records; indices are clamped to the block's
+// area, so nothing is written outside it.
+__device__ __forceinline__ void cursors_init(uint32_t* cur, uint32_t nb, uint32_t sub) {
+  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
+    cur[b] = b * sub;
+    cur[MAX_REC_BUCKETS + b] = b * sub;
   }
+}
+
+// Store one record at area index idx.  The block's store bases are
+// wave-uniform (SGPRs) and a record's byte offset fits 32 bits, so the stores
+// take the SGPR-base + 32-bit VGPR-offset form.
+__device__ __forceinline__ void put_rec16(const RecOut& o, uint32_t idx, const Rec16& r) {
   if (WC_EMIT_ABLATE) return;
-  if (r16) {
-    *reinterpret_cast<Rec16*>(reinterpret_cast<uint8_t*>(o.b16) + idx * (uint32_t)sizeof(Rec16)) =
-        make_rec16(k0, k1, off);
-  } else {
-    Rec r;
-    r.k0 = k0;
-    r.k1 = k1;
-    r.co = (cnt << 32) | off;
-    *reinterpret_cast<Rec*>(reinterpret_cast<uint8_t*>(o.b24) + __umul24(idx, (uint32_t)sizeof(Rec))) = r;
-  }
+  idx = min(idx, o.lim);
+  *reinterpret_cast<Rec16*>(reinterpret_cast<uint8_t*>(o.b16) + idx * (uint32_t)sizeof(Rec16)) = r;
 }
-
-// put_record for one occurrence of a word of 1..7 bytes (k1 = its length n):
-// a Rec16's tail word is 0 without a compare.
-__device__ __forceinline__ void put_record_short(const MapArgs& a, const RecOut& o, uint32_t b, uint32_t packed,
-                                                 bool r16, uint64_t k0, uint32_t n, uint32_t off) {
-  const uint32_t pos = r16 ? (packed & 0xFFFFu) : (packed >> 16);
-  const uint32_t idx = __umul24(b, o.sub) + pos;
-  if (pos >= o.sub) {
-    atomicOr(&a.flags[FLAG_REGION_OVF], 1u);
-    return;
-  }
+__device__ __forceinline__ void put_rec24(const RecOut& o, uint32_t idx, uint64_t k0, uint64_t k1, uint64_t cnt,
+                                          uint32_t off) {
   if (WC_EMIT_ABLATE) return;
-  if (r16) {
-    *reinterpret_cast<Rec16*>(reinterpret_cast<uint8_t*>(o.b16) + idx * (uint32_t)sizeof(Rec16)) =
-        Rec16{(uint32_t)k0, (uint32_t)(k0 >> 32), 0u, off};
-  } else {
-    Rec r;
-    r.k0 = k0;
-    r.k1 = n;
-    r.co = (1ull << 32) | off;
-    *reinterpret_cast<Rec*>(reinterpret_cast<uint8_t*>(o.b24) + __umul24(idx, (uint32_t)sizeof(Rec))) = r;
-  }
+  idx = min(idx, o.lim);
+  Rec r;
+  r.k0 = k0;
+  r.k1 = k1;
+  r.co = (cnt << 32) | off;
+  *reinterpret_cast<Rec*>(reinterpret_cast<uint8_t*>(o.b24) + __umul24(idx, (uint32_t)sizeof(Rec))) = r;
 }
 
-// Append one record (key, count, first offset) to bucket b's sub-region of
-// this block; bcur[b] packs both cursors (Rec16 count | Rec count << 16).
-__device__ __forceinline__ void emit_record(uint32_t* bcur, const MapArgs& a, const RecOut& o, uint32_t b, uint64_t k0,
-                                            uint64_t k1, uint64_t cnt, uint32_t off) {
-  const bool r16 = rec16_fits(k0, k1, cnt);
-  put_record(a, o, b, atomicAdd(&bcur[b], r16 ? 1u : 0x10000u), r16, k0, k1, cnt, off);
+// Append one record (key, count, first offset) to bucket b's sub-region.
+__device__ __forceinline__ void emit_record(uint32_t* cur, const RecOut& o, uint32_t b, uint64_t k0, uint64_t k1,
+                                            uint64_t cnt, uint32_t off) {
+  if (rec16_fits(k0, k1, cnt)) put_rec16(o, atomicAdd(&cur[b], 1u), make_rec16(k0, k1, off));
+  else put_rec24(o, atomicAdd(&cur[MAX_REC_BUCKETS + b], 1u), k0, k1, cnt, off);
 }
 
 // Two single-occurrence records of one lane (either may be absent; n1 / n2:
 // the words' lengths, x1 / y1 their key words): both cursor atomics are
-// issued before either store waits for its position.
-__device__ __forceinline__ void emit_two(uint32_t* bcur, const MapArgs& a, const RecOut& o, bool d1, uint32_t b1,
-                                         uint64_t x0, uint64_t x1, uint32_t o1, uint32_t n1, bool d2, uint32_t b2,
-                                         uint64_t y0, uint64_t y1, uint32_t o2, uint32_t n2) {
+// issued before either store waits for its index.
+__device__ __forceinline__ void emit_two(uint32_t* cur, const RecOut& o, bool d1, uint32_t b1, uint64_t x0,
+                                         uint64_t x1, uint32_t o1, uint32_t n1, bool d2, uint32_t b2, uint64_t y0,
+                                         uint64_t y1, uint32_t o2, uint32_t n2) {
   const bool s1 = rec16_inline(x0, x1, n1), s2 = rec16_inline(y0, y1, n2);
   uint32_t p1 = 0, p2 = 0;
-  if (d1) p1 = atomicAdd(&bcur[b1], s1 ? 1u : 0x10000u);
-  if (d2) p2 = atomicAdd(&bcur[b2], s2 ? 1u : 0x10000u);
-  if (d1) put_record(a, o, b1, p1, s1, x0, x1, 1, o1);
-  if (d2) put_record(a, o, b2, p2, s2, y0, y1, 1, o2);
+  if (d1) p1 = atomicAdd(&cur[(s1 ? 0u : (uint32_t)MAX_REC_BUCKETS) + b1], 1u);
+  if (d2) p2 = atomicAdd(&cur[(s2 ? 0u : (uint32_t)MAX_REC_BUCKETS) + b2], 1u);
+  if (d1) {
+    if (s1) put_rec16(o, p1, make_rec16(x0, x1, o1));
+    else put_rec24(o, p1, x0, x1, 1, o1);
+  }
+  if (d2) {
+    if (s2) put_rec16(o, p2, make_rec16(y0, y1, o2));
+    else put_rec24(o, p2, y0, y1, 1, o2);
+  }
 }
 
-// emit_two for words of 1..7 bytes (k1 = the length): a Rec16 unless the
-// word's last byte is 0x00 — one 64-bit shift and compare per word instead of
-// rec16_inline's two length classes (a divergent branch pair in the short step).
-__device__ __forceinline__ void emit_two_short(uint32_t* bcur, const MapArgs& a, const RecOut& o, bool d1, uint32_t b1,
-                                               uint64_t x0, uint32_t o1, uint32_t n1, bool d2, uint32_t b2,
-                                               uint64_t y0, uint32_t o2, uint32_t n2) {
+// emit_two for words of 1..7 bytes (k1 = the length): a Rec16 (tail word 0)
+// unless the word's last byte is 0x00 — one 64-bit shift and compare per word.
+__device__ __forceinline__ void emit_two_short(uint32_t* cur, const RecOut& o, bool d1, uint32_t b1, uint64_t x0,
+                                               uint32_t o1, uint32_t n1, bool d2, uint32_t b2, uint64_t y0,
+                                               uint32_t o2, uint32_t n2) {
   const bool s1 = (x0 >> ((8u * n1 - 8u) & 63u)) != 0, s2 = (y0 >> ((8u * n2 - 8u) & 63u)) != 0;
   uint32_t p1 = 0, p2 = 0;
-  if (d1) p1 = atomicAdd(&bcur[b1], s1 ? 1u : 0x10000u);
-  if (d2) p2 = atomicAdd(&bcur[b2], s2 ? 1u : 0x10000u);
-  if (d1) put_record_short(a, o, b1, p1, s1, x0, n1, o1);
-  if (d2) put_record_short(a, o, b2, p2, s2, y0, n2, o2);
+  if (d1) p1 = atomicAdd(&cur[(s1 ? 0u : (uint32_t)MAX_REC_BUCKETS) + b1], 1u);
+  if (d2) p2 = atomicAdd(&cur[(s2 ? 0u : (uint32_t)MAX_REC_BUCKETS) + b2], 1u);
+  if (d1) {
+    if (s1) put_rec16(o, p1, Rec16{(uint32_t)x0, (uint32_t)(x0 >> 32), 0u, o1});
+    else put_rec24(o, p1, x0, n1, 1, o1);
+  }
+  if (d2) {
+    if (s2) put_rec16(o, p2, Rec16{(uint32_t)y0, (uint32_t)(y0 >> 32), 0u, o2});
+    else put_rec24(o, p2, y0, n2, 1, o2);
+  }
 }
 
 // Key of a LONG token (>= 16 bytes) of known length 16..30 from its LDS

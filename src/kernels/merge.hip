@@ -143,10 +143,16 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
                                                         const uint64_t* dn, uint32_t W,
                                                         const unsigned long long* counts, unsigned long long* cursor,
                                                         MRow* rows, uint8_t* bytes, uint32_t* send_pos,
-                                                        uint64_t reg_rows, uint64_t reg_bytes, uint32_t* ovf) {
+                                                        uint64_t reg_rows, uint64_t reg_bytes, uint32_t* ovf,
+                                                        const uint32_t* pass_flags) {
   __shared__ unsigned long long base[2 * OWN_MAX], h[2 * OWN_MAX];
   constexpr int PER = OWN_ROWS_PER_BLOCK / 256;
   const uint64_t r0 = (uint64_t)blockIdx.x * OWN_ROWS_PER_BLOCK;
+  if (pass_flags && blockIdx.x == 0 && threadIdx.x == 0) {  // planned: this rank's pass flags into its flag word
+    const uint32_t rerun = pass_flags[FLAG_REGION_OVF] | pass_flags[FLAG_TABLE_OVF];
+    const uint32_t f = (rerun ? 1u : 0u) | (pass_flags[FLAG_ARENA_OVF] ? 2u : 0u);
+    if (f) atomicOr(ovf, f);
+  }
   if (dn) n = *dn;
   if (r0 >= n) return;
   const bool fixed = reg_rows != 0;
@@ -392,34 +398,27 @@ __global__ void wc_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* dn
   }
 }
 
-// Planned merge (dist/merge.cpp merge_cols_planned): flags from the
-// all-gathered count matrix (W rows of C = 2W + 2 words: rows / bytes per
-// owner, max offset, pass flags) — bit 0: a rank's last pass needs recovery,
-// bit 1: a rank's key arena overflowed, bit 2: rows or bytes for some owner
-// past the fixed regions — and, from the all-gathered (merged rows, bytes) of
-// every owner (owns, nullable), bit 2 also for merged rows past reg_merged.
-// Every rank reads the same gathered words, so every rank decides the same.
-__global__ void wc_merge_check(const unsigned long long* all, uint32_t W, uint64_t reg_rows, uint64_t reg_bytes,
-                               const unsigned long long* owns, uint64_t reg_merged, uint32_t* flags) {
+// Planned merge (dist/merge.cpp merge_cols_planned): the decision from every
+// rank's all-gathered word quad (merged rows, flags, max first offset, -):
+// flags bit 0 = a rank's last pass needs recovery, bit 1 = its key arena
+// overflowed, bit 2 = rows or bytes past a fixed region (set by its scatter);
+// bit 2 also for merged rows past reg_merged and for a first offset above the
+// bound the host sized the order's key width from (max_end).  Every rank reads
+// the same gathered words, so every rank decides the same.
+__global__ void wc_merge_check(const unsigned long long* owns, uint32_t W, uint64_t reg_merged, uint64_t max_end,
+                               uint32_t* flags) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const uint64_t C = 2ull * W + 2;
   uint32_t f = 0;
-  if (all) {
-    for (uint32_t p = 0; p < W; ++p) {
-      const unsigned long long* v = all + p * C;
-      f |= (uint32_t)(v[2 * W + 1] & 3u);
-      for (uint32_t o = 0; o < W; ++o)
-        if (v[2 * o] > reg_rows || v[2 * o + 1] > reg_bytes) f |= 4u;
-    }
+  for (uint32_t o = 0; o < W; ++o) {
+    const unsigned long long* v = owns + 4 * (size_t)o;
+    f |= (uint32_t)(v[1] & 7u);
+    if (v[0] > reg_merged || v[2] > max_end) f |= 4u;
   }
-  if (owns)
-    for (uint32_t o = 0; o < W; ++o)
-      if (owns[2 * o] > reg_merged) f |= 4u;
   if (f) atomicOr(flags, f);
 }
 
 // Planned merge, rank 0: the gathered merged rows sit in fixed regions of
-// reg_merged rows per owner, owner o's first owns[2 o] rows valid (k1 != 0);
+// reg_merged rows per owner, owner o's first owns[4 o] rows valid (k1 != 0);
 // they become dense key columns at the exclusive prefix of the owners' counts,
 // the long-word references made absolute in the gathered byte buffer (owner o's
 // payload at o * byte_stride); dense merge: counts / first offsets from the
@@ -436,7 +435,7 @@ __global__ void __launch_bounds__(256) wc_mrow_regions_to_cols(const MRow* rows,
     uint64_t b = 0;
     for (uint32_t o = 0; o < W; ++o) {
       pre[o] = b;
-      b += min((uint64_t)owns[2 * o], reg_merged);
+      b += min((uint64_t)owns[4 * o], reg_merged);
     }
     pre[W] = b;
     if (blockIdx.x == 0) *out_n = b;
@@ -460,10 +459,10 @@ __global__ void __launch_bounds__(256) wc_mrow_regions_to_cols(const MRow* rows,
 
 }  // namespace dev
 
-void launch_merge_check(const unsigned long long* all, uint32_t W, uint64_t reg_rows, uint64_t reg_bytes,
-                        const unsigned long long* owns, uint64_t reg_merged, uint32_t* flags, hipStream_t s) {
+void launch_merge_check(const unsigned long long* owns, uint32_t W, uint64_t reg_merged, uint64_t max_end,
+                        uint32_t* flags, hipStream_t s) {
   WC_CHECK(W >= 1 && W <= MERGE_MAX_RANKS, "merge_check: 1..64 ranks");
-  hipLaunchKernelGGL(dev::wc_merge_check, dim3(1), dim3(64), 0, s, all, W, reg_rows, reg_bytes, owns, reg_merged, flags);
+  hipLaunchKernelGGL(dev::wc_merge_check, dim3(1), dim3(64), 0, s, owns, W, reg_merged, max_end, flags);
 }
 void launch_mrow_regions_to_cols(const MRow* rows, uint32_t W, uint64_t reg_merged, const unsigned long long* owns,
                                  uint64_t byte_stride, const uint64_t* dcnt, const uint64_t* dfirst, uint64_t* k0,
@@ -484,11 +483,11 @@ void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t
                           const uint64_t* soff, const uint32_t* slen, const uint8_t* arena, uint64_t n, uint32_t W,
                           const unsigned long long* counts, unsigned long long* cursor, MRow* rows, uint8_t* bytes,
                           uint32_t* send_pos, hipStream_t s, const uint64_t* dn, uint64_t reg_rows, uint64_t reg_bytes,
-                          uint32_t* ovf) {
+                          uint32_t* ovf, const uint32_t* pass_flags) {
   const uint64_t blocks = (n + dev::OWN_ROWS_PER_BLOCK - 1) / dev::OWN_ROWS_PER_BLOCK;
   if (n)
     hipLaunchKernelGGL(dev::wc_owner_scatter, dim3((unsigned)blocks), dim3(256), 0, s, k0, k1, cnt, first, soff, slen,
-                       arena, n, dn, W, counts, cursor, rows, bytes, send_pos, reg_rows, reg_bytes, ovf);
+                       arena, n, dn, W, counts, cursor, rows, bytes, send_pos, reg_rows, reg_bytes, ovf, pass_flags);
 }
 void launch_mrow_insert(const MRow* rows, uint64_t R, const uint8_t* bytes, const uint64_t* rbase,
                         const uint64_t* bbase, uint32_t W, uint32_t* state, unsigned long long* cnt,

@@ -693,6 +693,225 @@ inline dim3 grid_for(uint64_t n) {
   return dim3((unsigned)g);
 }
 
+// ---- first-occurrence order above 400k keys: ranks from a bitmap of first offsets ----
+// Distinct words have distinct first offsets, and two token starts are >= 2
+// bytes apart (a delimiter between them), so first >> 1 indexes a bitmap
+// without collisions: 1 GiB of text is a 64 MiB bitmap.  A key's output row is
+// the number of set bits before its position — no comparison sort at all:
+//   wc_bm_set     set each key's bit (an atomic OR without return) and count
+//                 the keys into the bitmap's control word
+//   wc_bm_count   popcount per 512-bit line (one 64-byte line per thread), the
+//                 lines' exclusive prefix inside each 256-line block + block totals
+//   wc_bm_scan    one block: the block totals' exclusive scan and the key
+//                 count; fewer set bits than keys (two keys at one position)
+//                 or a key beyond the bound raises the overflow word, and the
+//                 caller redoes the order with the radix sort; the control word
+//                 is zeroed again for the next call
+//   wc_bm_place   row = block prefix + line prefix + popcount of the line's
+//                 bits below the key: the key's six columns go to that row as
+//                 ONE 64-byte record (a whole memory sector: six scattered
+//                 8-byte column stores measured 160 us at 1M keys, 6 partial
+//                 lines each)
+//   wc_bm_emit    records -> the six columns in row order (coalesced), and the
+//                 row's bitmap word zeroed: every set bit has a row, so the
+//                 bitmap is left all-zero for the next call
+// The radix path it replaces (4 digit passes + histogram + table keys +
+// gather) measured 200 us at 1M keys (profiles/r4_session3.md §7).
+constexpr uint32_t BM_LINE_BITS = 512;
+constexpr uint32_t BM_BLOCK_LINES = 256;
+constexpr uint64_t BM_BLOCK_WORDS = BM_BLOCK_LINES * BM_LINE_BITS / 64;
+constexpr uint64_t BM_RANGE = 1ull << 63;  // control word: a key beyond the bound (+ the key count below)
+struct alignas(64) BmRow {
+  uint64_t k0, k1, cnt, first, soff;
+  uint32_t slen, pad0;
+  uint64_t pad1, pad2;
+};
+static_assert(sizeof(BmRow) == 64, "one memory sector per row");
+
+// A row of the source: false for an empty table slot (or an empty bucket,
+// whose slots are undefined).
+__device__ inline bool bm_row(const OrderSrc& src, uint64_t i, uint64_t& first) {
+  if (src.table) {
+    if (src.t.occupancy[i >> TAB_SLOTS_LOG2] == 0 || src.t.k1[i] == K1_EMPTY) return false;
+    first = src.t.first[i];
+  } else {
+    first = src.first[i];
+  }
+  return true;
+}
+__device__ inline uint64_t bm_rows(const OrderSrc& src, uint64_t rows) {
+  return !src.table && src.dn ? *src.dn : rows;
+}
+
+__global__ void __launch_bounds__(256) wc_bm_set(OrderSrc src, uint64_t rows, unsigned long long* bm, uint32_t shift,
+                                                 uint64_t pos_end, unsigned long long* ctl) {
+  __shared__ uint32_t wn[4];
+  rows = bm_rows(src, rows);
+  uint32_t n = 0;
+  bool range = false;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < rows; i += (uint64_t)gridDim.x * 256) {
+    uint64_t f;
+    if (!bm_row(src, i, f)) continue;
+    const uint64_t p = f >> shift;
+    ++n;
+    if (p >= pos_end) {  // beyond the bound the caller gave (place skips it too)
+      range = true;
+      continue;
+    }
+    // random 8-byte writes dominate: 1M keys over a 64 MiB bitmap measured 68 us
+    // with 64- or 32-bit, agent- or workgroup-scope ORs, with or without the
+    // return, and 52 us as plain (inexact) stores (tools/bm_probe.py)
+    __hip_atomic_fetch_or(&bm[p >> 6], 1ull << (p & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+  range = __any(range);
+  if ((threadIdx.x & 63) == 0) wn[threadIdx.x >> 6] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t t = (uint64_t)wn[0] + wn[1] + wn[2] + wn[3];
+    if (t) atomicAdd(ctl, (unsigned long long)t);
+  }
+  if (range && (threadIdx.x & 63) == 0) atomicOr(ctl, (unsigned long long)BM_RANGE);
+}
+
+__global__ void __launch_bounds__(BM_BLOCK_LINES) wc_bm_count(const unsigned long long* bm, uint64_t lines,
+                                                              uint32_t* linepre, uint32_t* blocktot) {
+  __shared__ uint32_t wsum[BM_BLOCK_LINES / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t line = (uint64_t)blockIdx.x * BM_BLOCK_LINES + tid;
+  uint32_t c = 0;
+  if (line < lines) {
+    const ulonglong2* q = reinterpret_cast<const ulonglong2*>(bm + line * (BM_LINE_BITS / 64));
+    ulonglong2 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = q[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c += __popcll(v[k].x) + __popcll(v[k].y);
+  }
+  uint32_t incl = c;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o);
+    if ((int)lane >= o) incl += y;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  uint32_t before = 0, tot = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < BM_BLOCK_LINES / 64; ++w) {
+    before += w < wave ? wsum[w] : 0;
+    tot += wsum[w];
+  }
+  if (line < lines) linepre[line] = before + incl - c;
+  if (tid == 0) blocktot[blockIdx.x] = tot;
+}
+
+// One block: blockpre = exclusive scan of blocktot, *n = the total; the
+// overflow word from the control word, which is zeroed for the next call.
+__global__ void __launch_bounds__(1024) wc_bm_scan(const uint32_t* blocktot, uint32_t nblk, uint64_t* blockpre,
+                                                   uint64_t* n, unsigned long long* ctl, uint32_t* ovf) {
+  constexpr int PER = 8;
+  __shared__ uint64_t wsum[16];
+  __shared__ uint64_t carry;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t c = 0; c < nblk; c += 1024 * PER) {
+    uint32_t v[PER];
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const uint32_t b = c + tid * PER + j;
+      v[j] = b < nblk ? blocktot[b] : 0;
+      s += v[j];
+    }
+    uint64_t incl = s;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(incl, o);
+      if ((int)lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint64_t before = carry;
+    for (uint32_t w = 0; w < wave; ++w) before += wsum[w];
+    uint64_t o = before + incl - s;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const uint32_t b = c + tid * PER + j;
+      if (b < nblk) blockpre[b] = o;
+      o += v[j];
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint64_t t = 0;
+      for (int w = 0; w < 16; ++w) t += wsum[w];
+      carry += t;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const unsigned long long k = *ctl;
+    *n = carry;
+    *ovf = (k & BM_RANGE) || (k & ~BM_RANGE) != carry ? 1u : 0u;
+    *ctl = 0;
+  }
+}
+
+__global__ void __launch_bounds__(256) wc_bm_place(OrderSrc src, uint64_t rows, const unsigned long long* bm,
+                                                   uint32_t shift, uint64_t pos_end, const uint32_t* linepre,
+                                                   const uint64_t* blockpre, BmRow* out) {
+  rows = bm_rows(src, rows);
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < rows; i += (uint64_t)gridDim.x * 256) {
+    uint64_t f;
+    if (!bm_row(src, i, f)) continue;
+    const uint64_t p = f >> shift;
+    if (p >= pos_end) continue;
+    const uint64_t line = p / BM_LINE_BITS;
+    const ulonglong2* q = reinterpret_cast<const ulonglong2*>(bm + line * (BM_LINE_BITS / 64));
+    const uint32_t wi = (uint32_t)(p >> 6) & 7, b = (uint32_t)p & 63;
+    const unsigned long long below = (1ull << b) - 1;
+    uint32_t r = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const ulonglong2 v = q[k];
+      r += 2 * k < wi ? __popcll(v.x) : 2 * k == wi ? __popcll(v.x & below) : 0;
+      r += 2 * k + 1 < wi ? __popcll(v.y) : 2 * k + 1 == wi ? __popcll(v.y & below) : 0;
+    }
+    const uint64_t o = blockpre[line / BM_BLOCK_LINES] + linepre[line] + r;
+    ulonglong2 w[4];
+    if (src.table) {
+      const uint64_t k1 = src.t.k1[i];
+      const bool h = key_is_hashed(k1);
+      w[0] = make_ulonglong2(src.t.k0[i], k1);
+      w[1] = make_ulonglong2(src.t.cnt[i], f);
+      w[2] = make_ulonglong2(h ? src.t.sref_off[i] : 0, h ? src.t.sref_len[i] : 0);
+    } else {
+      w[0] = make_ulonglong2(src.k0[i], src.k1[i]);
+      w[1] = make_ulonglong2(src.cnt[i], f);
+      w[2] = make_ulonglong2(src.soff[i], src.slen[i]);
+    }
+    w[3] = make_ulonglong2(0, 0);
+    ulonglong2* d = reinterpret_cast<ulonglong2*>(out + o);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) d[k] = w[k];
+  }
+}
+
+__global__ void __launch_bounds__(256) wc_bm_emit(const BmRow* in, const uint64_t* n, OrderDst dst,
+                                                  unsigned long long* bm, uint32_t shift) {
+  const uint64_t rows = *n;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < rows; i += (uint64_t)gridDim.x * 256) {
+    const ulonglong2* q = reinterpret_cast<const ulonglong2*>(in + i);
+    const ulonglong2 a = q[0], b = q[1], c = q[2];
+    dst.k0[i] = a.x;
+    dst.k1[i] = a.y;
+    dst.cnt[i] = b.x;
+    dst.first[i] = b.y;
+    dst.soff[i] = c.x;
+    dst.slen[i] = (uint32_t)c.y;
+    bm[(b.y >> shift) >> 6] = 0;
+  }
+}
+
 }  // namespace dev
 
 // Workspace (32-bit words): digit totals [8][256] | tile counters [8] (+ pad)
@@ -795,5 +1014,46 @@ void launch_iota_u32(uint32_t* v, uint64_t n, hipStream_t s) {
 }
 void launch_fill_u64(uint64_t* p, uint64_t v, uint64_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(dev::wc_fill_u64, dev::grid_for(n), dim3(256), 0, s, p, v, n);
+}
+
+static uint64_t bm_lines(uint64_t key_end, uint32_t shift) {
+  return ((key_end >> shift) + dev::BM_LINE_BITS) / dev::BM_LINE_BITS;  // positions [0, (key_end >> shift) + 1)
+}
+static uint64_t bm_blocks(uint64_t key_end, uint32_t shift) {
+  return (bm_lines(key_end, shift) + dev::BM_BLOCK_LINES - 1) / dev::BM_BLOCK_LINES;
+}
+// + 8 words: the control word (key count | range flag) after the bitmap
+size_t bitmap_order_words(uint64_t key_end, uint32_t shift) { return bm_blocks(key_end, shift) * dev::BM_BLOCK_WORDS + 8; }
+size_t bitmap_order_ws_bytes(uint64_t bound, uint64_t key_end, uint32_t shift) {
+  return 256 + (bm_lines(key_end, shift) * 4 + 255) / 256 * 256 + bm_blocks(key_end, shift) * 12 + 512 +
+         std::max<uint64_t>(bound, 1) * sizeof(dev::BmRow) + 64;
+}
+
+uint32_t* bitmap_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, uint64_t key_end, uint32_t shift,
+                       unsigned long long* bm, void* ws, uint64_t* nout, hipStream_t s) {
+  const uint64_t lines = bm_lines(key_end, shift), blocks = bm_blocks(key_end, shift);
+  WC_CHECK(blocks < (1ull << 31), "bitmap_order: key bound too large");
+  uint8_t* p = static_cast<uint8_t*>(ws);
+  uint32_t* ovf = reinterpret_cast<uint32_t*>(p);
+  uint64_t* n = nout ? nout : reinterpret_cast<uint64_t*>(p + 64);
+  uint32_t* linepre = reinterpret_cast<uint32_t*>(p + 256);
+  uint8_t* q = p + 256 + (lines * 4 + 255) / 256 * 256;
+  uint64_t* blockpre = reinterpret_cast<uint64_t*>(q);
+  q += (blocks * 8 + 255) / 256 * 256;
+  uint32_t* blocktot = reinterpret_cast<uint32_t*>(q);
+  q += (blocks * 4 + 255) / 256 * 256;
+  dev::BmRow* rows_buf = reinterpret_cast<dev::BmRow*>((reinterpret_cast<uintptr_t>(q) + 63) & ~uintptr_t(63));
+  unsigned long long* ctl = bm + blocks * dev::BM_BLOCK_WORDS;
+  const uint64_t pos_end = (key_end >> shift) + 1;
+  const uint64_t rows = src.table ? ((uint64_t)1 << src.t.log2_buckets) * TAB_SLOTS : bound;
+  const dim3 g((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(4096, (rows + 255) / 256)));
+  hipLaunchKernelGGL(dev::wc_bm_set, g, dim3(256), 0, s, src, rows, bm, shift, pos_end, ctl);
+  hipLaunchKernelGGL(dev::wc_bm_count, dim3((unsigned)blocks), dim3(dev::BM_BLOCK_LINES), 0, s, bm, lines, linepre,
+                     blocktot);
+  hipLaunchKernelGGL(dev::wc_bm_scan, dim3(1), dim3(1024), 0, s, blocktot, (uint32_t)blocks, blockpre, n, ctl, ovf);
+  hipLaunchKernelGGL(dev::wc_bm_place, g, dim3(256), 0, s, src, rows, bm, shift, pos_end, linepre, blockpre, rows_buf);
+  const dim3 ge((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(4096, (bound + 255) / 256)));
+  hipLaunchKernelGGL(dev::wc_bm_emit, ge, dim3(256), 0, s, rows_buf, n, dst, bm, shift);
+  return ovf;
 }
 }  // namespace wc
