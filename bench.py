@@ -256,6 +256,9 @@ def run_rank(a) -> int:
 
     for _ in range(a.warmup):
         step()
+    # stage timing marks cost the GPU ~4.5 us each (profiles/r4_session3.md §9):
+    # off in the timed loop; one more untimed step with them on gives "stages"
+    eng.set_stage_events(False)
     barrier()
     t0 = time.perf_counter()
     keys = 0
@@ -263,6 +266,8 @@ def run_rank(a) -> int:
         keys = step()
     barrier()
     dt = time.perf_counter() - t0
+    eng.set_stage_events(True)
+    step()
     st = eng.stats()
     ms = dt / max(a.steps, 1) * 1e3
     tokens = st["tokens"]
@@ -331,7 +336,7 @@ def run_rank(a) -> int:
             },
             "control_plane": "native RCCL communicator (file rendezvous), no torch" if comm else "single process",
             "runtime": loaded_runtime(),
-            "stages": st,
+            "stages": st,  # from one extra untimed step with the stage marks on
         }
         if pool_info:
             out["host_pool"] = pool_info

@@ -160,6 +160,11 @@ class Engine:
     def reset(self) -> None:
         check(lib.wc_engine_reset(self._p))
 
+    def set_stage_events(self, on: bool) -> None:
+        """Stage timing marks (stats()["device_ms"]); each costs the GPU ~4.5 us."""
+        if hasattr(lib, "wc_engine_set_stage_events"):  # an older A/B variant build (WC_LIB) keeps them on
+            check(lib.wc_engine_set_stage_events(self._p, int(bool(on))))
+
     def count_bytes(self, data: bytes, global_base: int = 0) -> None:
         """Host text, streamed through the pinned ring (H2D overlapped)."""
         ptr, keep = _u8ptr(data)

@@ -111,6 +111,9 @@ class Engine {
   const Options& options() const;
   Stats& stats();
   void reset();  // empty the running table (keeps allocations)
+  // Stage timing marks (Stats::device_ms; default on, WC_STAGE_EVENTS=0 off):
+  // each costs the GPU ~4.5 us between two kernels, so timed loops turn them off
+  void set_stage_events(bool on);
 
   // Text already resident in HBM (16-B aligned).  Tokens owned by this call are
   // those starting in [0, n); bytes in [n, avail) may be read to finish them.

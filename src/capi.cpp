@@ -401,6 +401,7 @@ wc_engine* wc_engine_create(const wc_options* o) {
 void wc_engine_destroy(wc_engine* e) { delete e; }
 
 int wc_engine_reset(wc_engine* e) { return guard([&] { e->e->reset(); }); }
+int wc_engine_set_stage_events(wc_engine* e, int on) { return guard([&] { e->e->set_stage_events(on != 0); }); }
 
 int wc_count_host(wc_engine* e, const uint8_t* text, uint64_t n, uint64_t base) {
   return guard([&] { e->e->count_host(text, n, base); });

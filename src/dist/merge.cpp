@@ -565,8 +565,8 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
     z.add(state, T * 4);
     z.add(tcnt, T * 8);
     z.add(tfirst, T * 8, 0xFFFFFFFFu);
-    z.add(merged, Gr * sizeof(MRow));
     z.add(d_own, 16);  // merged rows (wc_mrow_compact adds), flags (the scatter ORs)
+    if (im.cols.occ) z.add(reinterpret_cast<uint32_t*>(im.d_local_n), 8);  // the scatter counts the table's keys
     z.copy(d_own + 2, mx, 8);
     z.copy(d_base, base, (2 * (size_t)W + 2) * 8);
     z.copy(d_seg, seg, ((size_t)W + 1) * 8);
@@ -576,7 +576,8 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
   // into its flag word) and exchange them whole
   launch_owner_scatter(im.cols.k0, im.cols.k1, im.cols.cnt, im.cols.first, im.cols.sref_off, im.cols.sref_len,
                        im.cols_arena, nb, (uint32_t)W, nullptr, d_cur, send_rows, send_bytes, send_pos, s, dn, Cr, Cb,
-                       reinterpret_cast<uint32_t*>(d_own + 1), pass_flags);
+                       reinterpret_cast<uint32_t*>(d_own + 1), pass_flags, im.cols.occ,
+                       im.cols.occ ? reinterpret_cast<unsigned long long*>(im.d_local_n) : nullptr);
   std::vector<size_t> ro(W), rs(W, Cr * sizeof(MRow)), bo(W), bs(W, Cb), zs(W, 0), gr(W, 0), gb(W, 0), go(W), gbo(W);
   for (int p = 0; p < W; ++p) {
     ro[p] = (size_t)p * Cr * sizeof(MRow);
@@ -687,26 +688,23 @@ bool merge_cols_planned_speculative(Engine::Impl& im, Comm& comm, bool all_ranks
   Range rg("wc_merge_planned_speculative");
   im.planned_pass = im.pend;
   im.pend.active = false;
-  hipStream_t s = im.s;
   const TableView& t = im.table();
   const size_t nb = (size_t)1 << t.log2_buckets;
   const uint64_t cap = (uint64_t)nb * TAB_SLOTS;
   DeviceArena& F = im.fin_mem;
-  F.reserve((cap + 1) * (5 * 8 + 4) + nb * 8 + 64 * 1024);
+  F.reserve(64 * 1024);
   F.reset();
+  // no compaction: the owner scatter reads the table's slots (and counts its keys)
   KeyCols c;
-  c.k0 = F.take_n<uint64_t>(cap + 1);
-  c.k1 = F.take_n<uint64_t>(cap + 1);
-  c.cnt = F.take_n<uint64_t>(cap + 1);
-  c.first = F.take_n<uint64_t>(cap + 1);
-  c.sref_off = F.take_n<uint64_t>(cap + 1);
-  c.sref_len = F.take_n<uint32_t>(cap + 1);
-  uint64_t* d_boff = F.take_n<uint64_t>(nb);
+  c.k0 = t.k0;
+  c.k1 = t.k1;
+  c.cnt = t.cnt;
+  c.first = t.first;
+  c.sref_off = t.sref_off;
+  c.sref_len = t.sref_len;
+  c.occ = t.occupancy;
   uint64_t* d_n = F.take_n<uint64_t>(2);
-  launch_bucket_offsets(t.occupancy, (uint32_t)nb, d_boff, d_n, s);
-  launch_table_compact(t, d_boff, c.k0, c.k1, c.cnt, c.first, c.sref_off, c.sref_len, s);
   c.n = cap;
-  c.dn = reinterpret_cast<unsigned long long*>(d_n);
   im.d_local_n = d_n;
   im.cols = c;
   im.cols_arena = im.d_arena;

@@ -40,6 +40,10 @@ struct KeyCols {
   // non-null: the row count lives on the device (n is its bound) until the
   // finalize's last wait publishes it (the merge's rank-0 gather: no host round trip)
   unsigned long long* dn = nullptr;
+  // non-null: the columns ARE the running table (the planned merge scatters
+  // straight from it): row i is a slot, valid iff occ[i >> TAB_SLOTS_LOG2] != 0
+  // and k1[i] != K1_EMPTY; n = the table's capacity
+  const uint32_t* occ = nullptr;
 };
 
 struct Engine::Impl {

@@ -370,7 +370,11 @@ void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t
                           const uint64_t* soff, const uint32_t* slen, const uint8_t* arena, uint64_t n, uint32_t W,
                           const unsigned long long* counts, unsigned long long* cursor, MRow* rows, uint8_t* bytes,
                           uint32_t* send_pos, hipStream_t s, const uint64_t* dn = nullptr, uint64_t reg_rows = 0,
-                          uint64_t reg_bytes = 0, uint32_t* ovf = nullptr, const uint32_t* pass_flags = nullptr);
+                          uint64_t reg_bytes = 0, uint32_t* ovf = nullptr, const uint32_t* pass_flags = nullptr,
+                          const uint32_t* occ = nullptr, unsigned long long* nvalid = nullptr);
+// occ (nullable): the columns are the running table's (n = its capacity): slot
+// i is a row iff occ[i >> TAB_SLOTS_LOG2] != 0 and k1[i] != K1_EMPTY (an empty
+// slot's send_pos is all ones); nvalid (nullable, zeroed) += the rows seen.
 // Planned merge: the decision flags from every rank's gathered word quad
 // (merged rows, flags, max first offset, -) (merge.hip).
 void launch_merge_check(const unsigned long long* owns, uint32_t W, uint64_t reg_merged, uint64_t max_end,

@@ -144,8 +144,10 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
                                                         const unsigned long long* counts, unsigned long long* cursor,
                                                         MRow* rows, uint8_t* bytes, uint32_t* send_pos,
                                                         uint64_t reg_rows, uint64_t reg_bytes, uint32_t* ovf,
-                                                        const uint32_t* pass_flags) {
+                                                        const uint32_t* pass_flags, const uint32_t* occ,
+                                                        unsigned long long* nvalid) {
   __shared__ unsigned long long base[2 * OWN_MAX], h[2 * OWN_MAX];
+  __shared__ uint32_t nv;
   constexpr int PER = OWN_ROWS_PER_BLOCK / 256;
   const uint64_t r0 = (uint64_t)blockIdx.x * OWN_ROWS_PER_BLOCK;
   if (pass_flags && blockIdx.x == 0 && threadIdx.x == 0) {  // planned: this rank's pass flags into its flag word
@@ -157,8 +159,11 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
   if (r0 >= n) return;
   const bool fixed = reg_rows != 0;
   for (uint32_t i = threadIdx.x; i < 2 * W; i += blockDim.x) h[i] = 0;
+  if (threadIdx.x == 0) nv = 0;
   __syncthreads();
-  uint32_t own[PER];
+  // a table source: one occupancy word per 4096-slot bucket (a block's 1024 rows share it)
+  const bool live = !occ || occ[r0 >> TAB_SLOTS_LOG2] != 0;
+  uint32_t own[PER], mine = 0;
   unsigned long long lr[PER], lb[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -166,12 +171,22 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
     own[j] = OWN_MAX;
     uint32_t nb = 0;
     if (i < n) {
-      own[j] = owner_of(place_hash(k0[i], k1[i]), W);
-      if (key_is_hashed(k1[i])) nb = (slen[i] + 7u) & ~7u;
+      if (live && (!occ || k1[i] != K1_EMPTY)) {
+        own[j] = owner_of(place_hash(k0[i], k1[i]), W);
+        if (key_is_hashed(k1[i])) nb = (slen[i] + 7u) & ~7u;
+        ++mine;
+      } else if (send_pos) {
+        send_pos[i] = 0xFFFFFFFFu;  // an empty slot: no id comes back for it
+      }
     }
     lr[j] = wave_owner_add(h, own[j], nb, lb[j]);
   }
+  if (nvalid) {
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o);
+    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(&nv, mine);
+  }
   __syncthreads();
+  if (nvalid && threadIdx.x == 0 && nv) atomicAdd(nvalid, (unsigned long long)nv);
   if (threadIdx.x == 0) {
     unsigned long long br = 0, bb = 0;  // exclusive prefix of the global per-owner totals (or the regions)
     for (uint32_t o = 0; o < W; ++o) {
@@ -483,11 +498,13 @@ void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t
                           const uint64_t* soff, const uint32_t* slen, const uint8_t* arena, uint64_t n, uint32_t W,
                           const unsigned long long* counts, unsigned long long* cursor, MRow* rows, uint8_t* bytes,
                           uint32_t* send_pos, hipStream_t s, const uint64_t* dn, uint64_t reg_rows, uint64_t reg_bytes,
-                          uint32_t* ovf, const uint32_t* pass_flags) {
+                          uint32_t* ovf, const uint32_t* pass_flags, const uint32_t* occ, unsigned long long* nvalid) {
+  static_assert(TAB_SLOTS % dev::OWN_ROWS_PER_BLOCK == 0, "a scatter block stays inside one table bucket");
   const uint64_t blocks = (n + dev::OWN_ROWS_PER_BLOCK - 1) / dev::OWN_ROWS_PER_BLOCK;
   if (n)
     hipLaunchKernelGGL(dev::wc_owner_scatter, dim3((unsigned)blocks), dim3(256), 0, s, k0, k1, cnt, first, soff, slen,
-                       arena, n, dn, W, counts, cursor, rows, bytes, send_pos, reg_rows, reg_bytes, ovf, pass_flags);
+                       arena, n, dn, W, counts, cursor, rows, bytes, send_pos, reg_rows, reg_bytes, ovf, pass_flags,
+                       occ, nvalid);
 }
 void launch_mrow_insert(const MRow* rows, uint64_t R, const uint8_t* bytes, const uint64_t* rbase,
                         const uint64_t* bbase, uint32_t W, uint32_t* state, unsigned long long* cnt,
