@@ -688,6 +688,7 @@ bool merge_cols_planned_speculative(Engine::Impl& im, Comm& comm, bool all_ranks
   Range rg("wc_merge_planned_speculative");
   im.planned_pass = im.pend;
   im.pend.active = false;
+  im.flush_pass_publish();  // its counters: read after the merge's last wait
   const TableView& t = im.table();
   const size_t nb = (size_t)1 << t.log2_buckets;
   const uint64_t cap = (uint64_t)nb * TAB_SLOTS;
@@ -731,6 +732,7 @@ bool merge_cols_speculative(Engine::Impl& im, Comm& comm, bool all_ranks) {
   Range rg("wc_merge_speculative");
   const Engine::Impl::PendingPass p = im.pend;
   im.pend.active = false;
+  im.flush_pass_publish();
   hipStream_t s = im.s;
   const TableView& t = im.table();
   const size_t nb = (size_t)1 << t.log2_buckets;

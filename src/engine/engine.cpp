@@ -270,7 +270,7 @@ uint32_t Engine::Impl::blocks_for(uint64_t len) const {
 }
 
 void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev,
-                               uint32_t log2_rb, uint32_t blocks, bool copy_occupancy) {
+                               uint32_t log2_rb, uint32_t blocks, bool copy_occupancy, bool defer_publish) {
   WC_CHECK((reinterpret_cast<uintptr_t>(text) & 15) == 0, "chunk text must be 16-byte aligned");
   mark(EV_PASS);
   // one zeroing launch: pass counters and, after a reset, the
@@ -294,7 +294,6 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
     z.add(d_arena_cursor, sizeof(unsigned long long));
     reset_pending = false;
   }
-  launch_zero_regions(z, s);
   pass_rec = rec;
   pass_rec.cursor = &d_ctr->records;
   pass_rec.subcap = (uint32_t)std::min<uint64_t>(rec.cap / ((uint64_t)blocks << log2_rb), 0xFFFFull);
@@ -303,7 +302,7 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   if (d_stamps) blocks_stamped += blocks;
   hot.text = text;
   hot.nblk = blocks;
-  launch_map(m, hot, blocks, s, sample);
+  launch_map(m, hot, blocks, s, sample, z);  // z applied first (inside the sampling launch)
   mark(EV_MAP);
   if (sync_debug) {  // WC_SYNC_DEBUG: attribute a device fault to a kernel and a chunk
     const hipError_t e = hipStreamSynchronize(s);
@@ -331,8 +330,16 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
     c.seq_dst = reinterpret_cast<uint32_t*>(h_pass_seq.data());
     c.seq = ++pass_seq;
   }
-  launch_publish(c, s);
+  pass_pub = c;
+  pass_pub_pending = true;
+  if (!defer_publish) flush_pass_publish();
   mark(EV_REDUCE);
+}
+
+void Engine::Impl::flush_pass_publish() {
+  if (!pass_pub_pending) return;
+  pass_pub_pending = false;
+  launch_publish(pass_pub, s);
 }
 
 void Engine::Impl::mark(int tag) {
@@ -465,6 +472,10 @@ bool Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
                                  uint32_t log2_rb, uint32_t blocks, bool synced) {
   // the pass's publish launch (counters, occupancy) is what this needs: spin on
   // its sequence word; later work already on the stream keeps running
+  if (pass_pub_pending) {  // still held back: launch it now and wait for it
+    flush_pass_publish();
+    synced = false;
+  }
   if (!synced) {
     if (spin_wait) wait_published(reinterpret_cast<const uint32_t*>(h_pass_seq.data()), pass_seq);
     else WC_HIP_CHECK(hipStreamSynchronize(s));
@@ -548,7 +559,7 @@ void Engine::Impl::process_chunk(const uint8_t* text, uint64_t len, uint64_t ava
   const uint32_t blocks = blocks_for(len);
   const uint32_t rb = rec_buckets_log2();
   if (last && speculate && !sync_debug) {
-    launch_pass(text, len, avail, base, prev, rb, blocks, false);
+    launch_pass(text, len, avail, base, prev, rb, blocks, false, true);
     pend = PendingPass{true, text, len, avail, base, prev, rb, blocks};
     occ_valid = false;
     max_end = std::max(max_end, base + len);  // the sort key width of the speculative finalize
@@ -663,6 +674,10 @@ bool Engine::Impl::finalize_local_speculative() {
   mark(EV_FIN_END);
   fin_end_marked = true;
   PubList pc{};
+  if (pass_pub_pending) {  // the pass's counters ride in this launch (complete_pass below reads them)
+    pass_pub_pending = false;
+    for (int i = 0; i < pass_pub.n; ++i) pc.add(pass_pub.dst[i], pass_pub.src[i], (uint64_t)pass_pub.words[i] * 4);
+  }
   pc.add(h_spec.data(), d_n, 8);
   pc.add(h_spec.data() + 8, d_arena_cursor, 8);
   uint32_t* seq = reinterpret_cast<uint32_t*>(h_spec.data() + 16);
@@ -913,6 +928,7 @@ void Engine::reset() {
   // zero only the occupancy: a bucket with occupancy 0 is empty whatever its
   // slice holds (reduce / compact / split never read such a slice)
   im.pend.active = false;  // an unchecked pass of the previous job is discarded with it
+  im.pass_pub_pending = false;
   // no API call: the next pass's zeroing launch clears occupancy + arena cursor
   // (apply_reset does it first for anything else that reads the table)
   im.reset_pending = true;

@@ -150,7 +150,14 @@ struct Engine::Impl {
   // Asynchronous part (map + reduce + counters D2H) and the completion check;
   // complete_pass returns false when the pass needed recovery (re-runs / splits).
   void launch_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev, uint32_t log2_rb,
-                   uint32_t blocks, bool copy_occupancy = true);
+                   uint32_t blocks, bool copy_occupancy = true, bool defer_publish = false);
+  // The pass's counter publish (pinned copies of counters + occupancy), held
+  // back by a speculative last pass: the local finalize folds it into its own
+  // publish launch (one launch, ~4.5 us, fewer per job); anything else that
+  // takes the pending pass launches it first (flush_pass_publish).
+  PubList pass_pub{};
+  bool pass_pub_pending = false;
+  void flush_pass_publish();
   bool complete_pass(const uint8_t* text, uint64_t len, uint64_t avail, uint64_t base, int prev, uint32_t log2_rb,
                      uint32_t blocks, bool synced = false);  // synced: the stream has drained (publish waited)
   struct PendingPass {

@@ -207,7 +207,10 @@ struct SynthVocab {
 // ---- launchers (all stream-ordered, no host sync) ----------------------------
 // wc_hot_sample + wc_hot_merge + wc_map;
 // sample = false: wc_map alone, on the hot-table image an earlier pass of the job built.
-void launch_map(const MapArgs& a, const HotArgs& h, uint32_t map_blocks, hipStream_t s, bool sample = true);
+struct ZeroList;
+// z: the pass's zeroing, applied before the map (inside the sampling launch when `sample`)
+void launch_map(const MapArgs& a, const HotArgs& h, uint32_t map_blocks, hipStream_t s, bool sample,
+                const ZeroList& z);
 void launch_reduce(const ReduceArgs& a, hipStream_t s);
 void launch_table_split(const TableView& src, const TableView& dst, hipStream_t s);
 void launch_table_clear(const TableView& t, hipStream_t s);
@@ -299,7 +302,7 @@ void launch_iota_u32(uint32_t* v, uint64_t n, hipStream_t s);
 // util.hip: fill several device regions (+ a few small copies, e.g. host words
 // from page-locked memory into device buffers) / copy several small device
 // regions into page-locked host memory, one launch each (sizes in 32-bit words).
-constexpr int ZERO_MAX_REGIONS = 8, ZERO_MAX_COPIES = 4, PUB_MAX_REGIONS = 4;
+constexpr int ZERO_MAX_REGIONS = 8, ZERO_MAX_COPIES = 4, PUB_MAX_REGIONS = 8;
 [[noreturn]] void launch_list_overflow(const char* what);  // util.hip: fails the job (a caller bug)
 struct ZeroList {
   uint32_t* ptr[ZERO_MAX_REGIONS];

@@ -49,6 +49,7 @@
 #include <type_traits>
 
 #include "map_common.hpp"
+#include "zero_list.hpp"
 
 namespace wc {
 namespace dev {
@@ -264,9 +265,14 @@ static_assert(sizeof(SampleLds) <= 160 * 1024, "one sample block per CU");
 // The round-2 form added every block's words into one global fingerprint table
 // with device CAS + add: the Zipf head's slots took one atomic pair from each
 // of the 256 blocks in turn, two thirds of a 35 us launch.
-__global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs h) {
+__global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs h, ZeroList z) {
   __shared__ SampleLds L;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // the pass's zeroing (counters, table occupancy after a reset, ...): nothing
+  // here or in wc_hot_merge touches those regions; the map and reduce that read
+  // them run after both launches
+  apply_zero_list(z, blockIdx.x * (uint64_t)MAP_THREADS + tid, (uint64_t)gridDim.x * MAP_THREADS, blockIdx.x == 0,
+                  MAP_THREADS);
   for (int s = tid; s < MAP_SLOTS; s += MAP_THREADS) {
     L.fp[s] = 0;
     L.cnt[s] = 0;
@@ -1196,10 +1202,13 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
 
 }  // namespace dev
 
-void launch_map(const MapArgs& a, const HotArgs& h, uint32_t map_blocks, hipStream_t s, bool sample) {
-  if (sample) {
-    hipLaunchKernelGGL(dev::wc_hot_sample, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
+void launch_map(const MapArgs& a, const HotArgs& h, uint32_t map_blocks, hipStream_t s, bool sample,
+                const ZeroList& z) {
+  if (sample) {  // the zeroing rides in the sampling launch
+    hipLaunchKernelGGL(dev::wc_hot_sample, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h, z);
     hipLaunchKernelGGL(dev::wc_hot_merge, dim3(HOT_PARTS), dim3(1024), 0, s, h);
+  } else {
+    launch_zero_regions(z, s);
   }
   if (a.stamps) hipLaunchKernelGGL(dev::wc_map<true>, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
   else hipLaunchKernelGGL(dev::wc_map<false>, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);

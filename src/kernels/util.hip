@@ -19,24 +19,13 @@
 
 #include "../common/hip_util.hpp"
 #include "kernels.hpp"
+#include "zero_list.hpp"
 
 namespace wc {
 namespace dev {
 
 __global__ void __launch_bounds__(256) wc_zero_regions(ZeroList z) {
-  const uint64_t tid = blockIdx.x * 256ull + threadIdx.x, stride = (uint64_t)gridDim.x * 256;
-  for (int r = 0; r < z.n; ++r) {
-    uint32_t* p = z.ptr[r];
-    const uint64_t words = z.words[r];
-    const uint32_t v = z.val[r];
-    const uint64_t quads = (reinterpret_cast<uintptr_t>(p) & 15) == 0 ? words / 4 : 0;
-    uint4* q = reinterpret_cast<uint4*>(p);
-    for (uint64_t i = tid; i < quads; i += stride) q[i] = make_uint4(v, v, v, v);
-    for (uint64_t i = quads * 4 + tid; i < words; i += stride) p[i] = v;
-  }
-  if (blockIdx.x == 0)
-    for (int c = 0; c < z.nc; ++c)
-      for (uint32_t i = threadIdx.x; i < z.cwords[c]; i += 256) z.cdst[c][i] = z.csrc[c][i];
+  apply_zero_list(z, blockIdx.x * 256ull + threadIdx.x, (uint64_t)gridDim.x * 256, blockIdx.x == 0, 256);
 }
 
 __global__ void __launch_bounds__(256) wc_publish(PubList c) {
