@@ -65,7 +65,10 @@ struct Options {
   double records_per_byte = 0.25;      // shuffle record capacity per chunk byte
   uint64_t arena_bytes = 256ull << 20; // key arena for >8-byte words
   uint32_t map_blocks = 0;             // 0 = 2 per CU
-  uint32_t staging_buffers = 3;        // pinned host ring depth (host-staged path)
+  // pinned host ring depth (host-staged path): 2 suffices — piece k + 2 is
+  // read into piece k's buffer only after pass k (which waited for its H2D)
+  // completed — and each buffer costs ~15 ms of pinning per 64 MiB at start-up
+  uint32_t staging_buffers = 2;
   // Streaming sources (files, host buffers) move through the pinned ring in
   // pieces of min(chunk_bytes, stream_chunk_bytes): small pieces start the
   // pipeline sooner and keep the page-locked ring cheap to allocate (4 GiB

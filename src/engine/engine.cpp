@@ -1084,15 +1084,28 @@ void Engine::count_source(ChunkSource& src, uint64_t global_base) {
     offset += n;
   }
   if (len) issue(0, len);
+  // WC_STREAM_TRACE=1 (diagnostics): host seconds in the reads, the launches and
+  // the completion waits, printed at the end
+  static const bool trace = std::getenv("WC_STREAM_TRACE") && std::atoi(std::getenv("WC_STREAM_TRACE"));
+  double t_fill = 0, t_launch = 0, t_wait = 0;
+  const double t_pre = now_seconds() - t0;  // staging ring + the first piece's read
   for (uint64_t k = 0; len; ++k) {
     const uint8_t* d = im.d_stage[k & 1];
+    const double a0 = trace ? now_seconds() : 0;
     WC_HIP_CHECK(hipStreamWaitEvent(im.s, im.ev_h2d[k & 1], 0));
     const uint32_t blocks = im.blocks_for(len);
     const uint32_t rb = im.rec_buckets_log2();
     im.launch_pass(d, len, len, offset, ' ', rb, blocks);
+    const double a1 = trace ? now_seconds() : 0;
     const uint64_t next = fill(k + 1);  // host reads the next chunk while the GPU works
     if (next) issue(k + 1, next);
+    const double a2 = trace ? now_seconds() : 0;
     im.complete_pass(d, len, len, offset, ' ', rb, blocks);
+    if (trace) {
+      t_launch += a1 - a0;
+      t_fill += a2 - a1;
+      t_wait += now_seconds() - a2;
+    }
     WC_HIP_CHECK(hipEventRecord(im.ev_done[k & 1], im.s));
     offset += len;
     im.st.bytes += len;
@@ -1105,6 +1118,9 @@ void Engine::count_source(ChunkSource& src, uint64_t global_base) {
   }
   WC_HIP_CHECK(hipStreamSynchronize(im.copy_s));
   im.st.host_count_ms += (now_seconds() - t0) * 1e3;
+  if (trace)
+    std::fprintf(stderr, "[wc] stream: %.3f s total, before the loop %.3f s, read %.3f s, launch %.3f s, wait %.3f s, %u pieces\n",
+                 now_seconds() - t0, t_pre, t_fill, t_launch, t_wait, im.st.chunks);
 }
 
 void Engine::count_pinned_replay(const uint8_t* pool, uint64_t pool_bytes, uint64_t total, uint64_t global_base,

@@ -5,7 +5,10 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
+#include <condition_variable>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -80,16 +83,85 @@ FileSource::~FileSource() {
   if (fd_ >= 0) ::close(fd_);
 }
 
+namespace {
+// Persistent reader threads: created on first use (they inherit the caller's
+// CPU mask — the engine binds its streaming loop to the GPU's NUMA node) and
+// woken per read.  Threads spawned per 64 MiB piece cost tens of us each and
+// capped the split at 4 (16 MiB slices); the stream read at 54 GB/s against
+// 75 GB/s standalone (profiles/r4_session3.md §10).
+class ReadPool {
+ public:
+  explicit ReadPool(unsigned n) {
+    for (unsigned i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+  }
+  ~ReadPool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  // f(0) .. f(tasks - 1) over the workers and the caller; returns when all ran.
+  void run(unsigned tasks, const std::function<void(unsigned)>& f) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      job_ = &f;
+      ntasks_.store(tasks);
+      done_.store(0);  // before next_: a worker can take a task as soon as next_ resets
+      next_.store(0);
+      ++gen_;
+    }
+    cv_.notify_all();
+    help();
+    std::unique_lock<std::mutex> lk(m_);
+    done_cv_.wait(lk, [&] { return done_.load() == ntasks_.load(); });
+  }
+
+ private:
+  void help() {
+    for (;;) {
+      const unsigned i = next_.fetch_add(1);
+      if (i >= ntasks_.load()) return;
+      (*job_)(i);
+      if (done_.fetch_add(1) + 1 == ntasks_.load()) {
+        std::lock_guard<std::mutex> g(m_);
+        done_cv_.notify_all();
+      }
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      help();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(unsigned)>* job_ = nullptr;
+  std::atomic<unsigned> ntasks_{0}, next_{~0u}, done_{0};
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+}  // namespace
+
 uint64_t pread_parallel(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
   // One thread copies ~5-8 GB/s out of the page cache, below PCIe Gen5 x16
   // (57 GB/s measured pinned H2D): large reads are split over WC_IO_THREADS
-  // (default 8) threads, 16 MiB minimum per thread.
+  // (default 16) persistent threads, 4 MiB minimum per slice.
   static const unsigned kThreads = [] {
     const char* e = std::getenv("WC_IO_THREADS");
-    const long v = e ? std::strtol(e, nullptr, 10) : 8;
+    const long v = e ? std::strtol(e, nullptr, 10) : 16;
     return (unsigned)std::max(1l, std::min(64l, v));
   }();
-  constexpr uint64_t kMinSlice = 16ull << 20;
+  constexpr uint64_t kMinSlice = 4ull << 20;
   const unsigned t = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(kThreads, n / kMinSlice));
   auto slice = [&](uint64_t b, uint64_t e, uint64_t& got, int& err) {
     got = 0;
@@ -108,14 +180,14 @@ uint64_t pread_parallel(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
   std::vector<uint64_t> got(t), lo(t);
   std::vector<int> err(t);
   const uint64_t per = (n + t - 1) / t;
-  std::vector<std::thread> th;
-  for (unsigned i = 0; i < t; ++i) {
-    lo[i] = std::min(n, (uint64_t)i * per);
-    const uint64_t hi = std::min(n, lo[i] + per);
-    if (i + 1 < t) th.emplace_back(slice, lo[i], hi, std::ref(got[i]), std::ref(err[i]));
-    else slice(lo[i], hi, got[i], err[i]);
+  for (unsigned i = 0; i < t; ++i) lo[i] = std::min(n, (uint64_t)i * per);
+  const std::function<void(unsigned)> task = [&](unsigned i) { slice(lo[i], std::min(n, lo[i] + per), got[i], err[i]); };
+  if (t == 1) {
+    task(0);
+  } else {
+    static ReadPool pool(kThreads - 1);  // + the caller
+    pool.run(t, task);
   }
-  for (auto& x : th) x.join();
   uint64_t total = 0;  // contiguous prefix: a short slice ends the read
   for (unsigned i = 0; i < t; ++i) {
     if (err[i]) fail(std::string("read error: ") + std::strerror(err[i]));
