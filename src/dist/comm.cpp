@@ -84,12 +84,16 @@ class RcclComm final : public Comm {
   int rank() const override { return rank_; }
   int size() const override { return size_; }
   const char* backend() const override { return "rccl"; }
+  // An in-place collective over one rank is the identity: no launch (RCCL
+  // issued a copy kernel for it, ~5 us each).
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
     tick(rank_);
+    if (size_ == 1 && send == recv) return;
     WC_NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, c_, s));
   }
   void reduce_scatter_u64(const uint64_t* send, uint64_t* recv, size_t count, RedOp op, hipStream_t s) override {
     tick(rank_);
+    if (size_ == 1 && send == recv) return;
     WC_NCCL_CHECK(ncclReduceScatter(send, recv, count, ncclUint64, to_nccl(op), c_, s));
   }
   void alltoallv(const void* send, const size_t* send_off, const size_t* send_bytes, void* recv,

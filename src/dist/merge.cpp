@@ -518,8 +518,8 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
   S.reserve((8 * (size_t)W + 64) * 8 + 8 * 1024);
   S.reset();
   unsigned long long* d_cur = take_aligned<unsigned long long>(S, 2 * (size_t)W);  // scatter cursor per owner
-  unsigned long long* d_own = take_aligned<unsigned long long>(S, 4);  // merged rows | flags | max offset | -
   unsigned long long* d_owns = take_aligned<unsigned long long>(S, 4 * (size_t)W);
+  unsigned long long* d_own = d_owns + 4 * (size_t)R;  // merged rows | flags | max offset | -, gathered in place
   unsigned long long* d_on = take_aligned<unsigned long long>(S, 1);
   im.d_merge_flags = take_aligned<uint32_t>(S, 2);
   uint64_t* mx = host_words(im) + HW_MX;
@@ -544,14 +544,22 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
             // dense: send_pos, row_slot, ids, ids_back, slot_id (u32); vc, vf, dcnt, dfirst, scnt, sfirst (u64)
             (dense ? (nb + 3 * RR + T) * 4 + (4 * GR + 2 * (uint64_t)Gr) * 8 + 16 * 256 : 0));
   A.reset();
+  // Nothing travels from a rank to itself: the scatter writes this rank's own
+  // rows and bytes straight into its receive regions, rank 0's compaction
+  // writes into region 0 of the gather buffer and its receive bytes ARE region
+  // 0 of the gathered payload — so at W = 1 no collective moves data at all.
+  MRow* grows = take_aligned<MRow>(A, GR);
+  uint8_t* gbytes = take_aligned<uint8_t>(A, (uint64_t)W * RB);
   MRow* send_rows = take_aligned<MRow>(A, RR);
   uint8_t* send_bytes = take_aligned<uint8_t>(A, RB);
   MRow* recv_rows = take_aligned<MRow>(A, RR);
-  uint8_t* recv_bytes = take_aligned<uint8_t>(A, RB);
+  uint8_t* recv_bytes = R == 0 ? gbytes : take_aligned<uint8_t>(A, RB);
   uint32_t* state = take_aligned<uint32_t>(A, T);
   unsigned long long* tcnt = take_aligned<unsigned long long>(A, T);
   unsigned long long* tfirst = take_aligned<unsigned long long>(A, T);
-  MRow* merged = take_aligned<MRow>(A, RR);  // compaction writes up to RR rows; the first Gr are sent
+  // compaction writes up to RR rows (more than Gr: flagged, the merge is redone); the first Gr are sent
+  MRow* merged = R == 0 ? grows : take_aligned<MRow>(A, RR);
+  const uint64_t merged_cap = R == 0 ? GR : RR;
   uint64_t* d_base = take_aligned<uint64_t>(A, 2 * (size_t)W + 2);
   uint64_t* d_seg = take_aligned<uint64_t>(A, (size_t)W + 1);
   uint32_t* send_pos = dense ? take_aligned<uint32_t>(A, nb) : nullptr;
@@ -561,7 +569,10 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
     ZeroList z{};  // cursor, flags, padding rows, the owner table, the merged region, this rank's quad: ONE launch
     z.add(d_cur, 2 * (size_t)W * 8);
     z.add(im.d_merge_flags, 8);
-    z.add(send_rows, RR * sizeof(MRow));
+    // padding rows read as K1_EMPTY: the send regions to peers, and this rank's own receive region
+    if (R > 0) z.add(send_rows, (uint64_t)R * Cr * sizeof(MRow));
+    if (R + 1 < W) z.add(send_rows + (uint64_t)(R + 1) * Cr, (uint64_t)(W - R - 1) * Cr * sizeof(MRow));
+    z.add(recv_rows + (uint64_t)R * Cr, Cr * sizeof(MRow));
     z.add(state, T * 4);
     z.add(tcnt, T * 8);
     z.add(tfirst, T * 8, 0xFFFFFFFFu);
@@ -574,15 +585,18 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
   }
   // 1. pack into the fixed regions (this rank's pass flags and region overflow
   // into its flag word) and exchange them whole
+  const MergeSelf self{(uint32_t)R, recv_rows, recv_bytes};
   launch_owner_scatter(im.cols.k0, im.cols.k1, im.cols.cnt, im.cols.first, im.cols.sref_off, im.cols.sref_len,
                        im.cols_arena, nb, (uint32_t)W, nullptr, d_cur, send_rows, send_bytes, send_pos, s, dn, Cr, Cb,
                        reinterpret_cast<uint32_t*>(d_own + 1), pass_flags, im.cols.occ,
-                       im.cols.occ ? reinterpret_cast<unsigned long long*>(im.d_local_n) : nullptr);
+                       im.cols.occ ? reinterpret_cast<unsigned long long*>(im.d_local_n) : nullptr, &self);
   std::vector<size_t> ro(W), rs(W, Cr * sizeof(MRow)), bo(W), bs(W, Cb), zs(W, 0), gr(W, 0), gb(W, 0), go(W), gbo(W);
   for (int p = 0; p < W; ++p) {
     ro[p] = (size_t)p * Cr * sizeof(MRow);
     bo[p] = (size_t)p * Cb;
   }
+  rs[R] = 0;  // this rank's own region is already in place
+  bs[R] = 0;
   comm.group_begin();
   comm.alltoallv(send_rows, ro.data(), rs.data(), recv_rows, ro.data(), rs.data(), s);
   comm.alltoallv(send_bytes, bo.data(), bs.data(), recv_bytes, bo.data(), bs.data(), s);
@@ -591,20 +605,21 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
   launch_mrow_insert(recv_rows, RR, recv_bytes, d_base, d_base + W + 1, (uint32_t)W, state, tcnt, tfirst, T, row_slot,
                      s);
   launch_mrow_compact(recv_rows, state, tcnt, tfirst, T, d_base, d_base + W + 1, (uint32_t)W, merged, d_own, slot_id,
-                      s);
+                      s, merged_cap);
   // 3. every rank's quad (+ dense: the owner-local ids back to the senders), the decision
   uint32_t* ids = nullptr;
   uint32_t* ids_back = nullptr;
   if (dense) {
     ids = take_aligned<uint32_t>(A, RR);
     ids_back = take_aligned<uint32_t>(A, RR);
-    launch_row_ids(row_slot, slot_id, RR, d_owns, 0u, ids, s);
+    launch_row_ids(row_slot, slot_id, RR, d_owns, 0u, ids, s, ids_back, (uint32_t)R, Cr);  // own region in place
   }
   comm.group_begin();
   comm.allgather(d_own, d_owns, 32, s);
   if (dense) {
     std::vector<size_t> io(W), is(W, Cr * 4);
     for (int p = 0; p < W; ++p) io[p] = (size_t)p * Cr * 4;
+    is[R] = 0;
     comm.alltoallv(ids, io.data(), is.data(), ids_back, io.data(), is.data(), s);
   }
   comm.group_end();
@@ -613,12 +628,14 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
   // slice = its ids) and all-gathered
   uint64_t *dcnt = nullptr, *dfirst = nullptr;
   if (dense) {
+    // reduce-scatter and all-gather in place: owner R's reduced slice is
+    // region R of the vectors, and the gathered vectors are the vectors
     uint64_t* vc = take_aligned<uint64_t>(A, GR);
     uint64_t* vf = take_aligned<uint64_t>(A, GR);
-    uint64_t* scnt = take_aligned<uint64_t>(A, Gr);
-    uint64_t* sfirst = take_aligned<uint64_t>(A, Gr);
-    dcnt = take_aligned<uint64_t>(A, GR);
-    dfirst = take_aligned<uint64_t>(A, GR);
+    uint64_t* scnt = vc + (uint64_t)R * Gr;
+    uint64_t* sfirst = vf + (uint64_t)R * Gr;
+    dcnt = vc;
+    dfirst = vf;
     ZeroList z{};
     z.add(vc, GR * 8);
     z.add(vf, GR * 8, 0xFFFFFFFFu);
@@ -645,8 +662,10 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
   std::vector<size_t> sr(W, 0), sb(W, 0);
   sr[0] = Gr * sizeof(MRow);
   sb[0] = RB;
-  MRow* grows = take_aligned<MRow>(A, GR);
-  uint8_t* gbytes = take_aligned<uint8_t>(A, (uint64_t)W * RB);
+  if (R == 0) {  // rank 0's own region and payload are in place
+    sr[0] = sb[0] = 0;
+    gr[0] = gb[0] = 0;
+  }
   comm.group_begin();
   comm.alltoallv(merged, zs.data(), sr.data(), grows, go.data(), gr.data(), s);
   comm.alltoallv(recv_bytes, zs.data(), sb.data(), gbytes, gbo.data(), gb.data(), s);

@@ -302,7 +302,7 @@ void launch_iota_u32(uint32_t* v, uint64_t n, hipStream_t s);
 // util.hip: fill several device regions (+ a few small copies, e.g. host words
 // from page-locked memory into device buffers) / copy several small device
 // regions into page-locked host memory, one launch each (sizes in 32-bit words).
-constexpr int ZERO_MAX_REGIONS = 8, ZERO_MAX_COPIES = 4, PUB_MAX_REGIONS = 8;
+constexpr int ZERO_MAX_REGIONS = 12, ZERO_MAX_COPIES = 4, PUB_MAX_REGIONS = 8;
 [[noreturn]] void launch_list_overflow(const char* what);  // util.hip: fails the job (a caller bug)
 struct ZeroList {
   uint32_t* ptr[ZERO_MAX_REGIONS];
@@ -369,15 +369,24 @@ void launch_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* 
 // (n the bound); reg_rows > 0: planned mode — owner o's rows / bytes in fixed
 // regions of reg_rows rows / reg_bytes bytes (counts unused), overflow -> *ovf
 // bit 2, and pass_flags (nullable) -> *ovf bits 0 / 1 (rerun / arena overflow)
+struct MergeSelf {
+  uint32_t rank;
+  MRow* rows;      // the receive row buffer
+  uint8_t* bytes;  // the receive byte buffer
+};
 void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
                           const uint64_t* soff, const uint32_t* slen, const uint8_t* arena, uint64_t n, uint32_t W,
                           const unsigned long long* counts, unsigned long long* cursor, MRow* rows, uint8_t* bytes,
                           uint32_t* send_pos, hipStream_t s, const uint64_t* dn = nullptr, uint64_t reg_rows = 0,
                           uint64_t reg_bytes = 0, uint32_t* ovf = nullptr, const uint32_t* pass_flags = nullptr,
-                          const uint32_t* occ = nullptr, unsigned long long* nvalid = nullptr);
+                          const uint32_t* occ = nullptr, unsigned long long* nvalid = nullptr,
+                          const MergeSelf* self = nullptr);
 // occ (nullable): the columns are the running table's (n = its capacity): slot
 // i is a row iff occ[i >> TAB_SLOTS_LOG2] != 0 and k1[i] != K1_EMPTY (an empty
 // slot's send_pos is all ones); nvalid (nullable, zeroed) += the rows seen.
+// self (nullable, planned mode): this rank's own rows and bytes go straight to
+// its receive regions (same offsets as in the send layout) — nothing to send
+// to itself in the exchange.
 // Planned merge: the decision flags from every rank's gathered word quad
 // (merged rows, flags, max first offset, -) (merge.hip).
 void launch_merge_check(const unsigned long long* owns, uint32_t W, uint64_t reg_merged, uint64_t max_end,
@@ -391,12 +400,14 @@ void launch_mrow_insert(const MRow* rows, uint64_t R, const uint8_t* bytes, cons
                         unsigned long long* first, uint64_t T, uint32_t* row_slot, hipStream_t s);  // row_slot nullable
 void launch_mrow_compact(const MRow* rows, const uint32_t* state, const unsigned long long* cnt,
                          const unsigned long long* first, uint64_t T, const uint64_t* rbase, const uint64_t* bbase,
-                         uint32_t W, MRow* out, unsigned long long* out_n, uint32_t* slot_id, hipStream_t s);  // nullable
+                         uint32_t W, MRow* out, unsigned long long* out_n, uint32_t* slot_id, hipStream_t s,
+                         uint64_t out_cap = ~0ull);  // slot_id nullable; rows past out_cap are counted, not written
 void launch_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rbase, const uint64_t* bbase, uint32_t W,
                          uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first, uint64_t* soff, uint32_t* slen,
                          hipStream_t s, const uint64_t* dn = nullptr);  // dn: device-side row count (n a bound)
 void launch_row_ids(const uint32_t* row_slot, const uint32_t* slot_id, uint64_t R, const unsigned long long* owns,
-                    uint32_t rank, uint32_t* ids, hipStream_t s);  // owns: all-gathered (rows, bytes) per owner
+                    uint32_t rank, uint32_t* ids, hipStream_t s,  // owns: all-gathered (rows, bytes) per owner
+                    uint32_t* ids_self = nullptr, uint32_t self = 0, uint64_t reg = 0);  // rows of region self -> ids_self
 void launch_scatter_ids(const uint32_t* send_pos, const uint32_t* ids_back, const uint64_t* seg,
                         const unsigned long long* owns, uint32_t W, const uint64_t* cnt, const uint64_t* first,
                         uint64_t n, uint64_t* dcnt, uint64_t* dfirst, hipStream_t s, const uint64_t* dn = nullptr,

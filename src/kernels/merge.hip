@@ -145,7 +145,7 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
                                                         MRow* rows, uint8_t* bytes, uint32_t* send_pos,
                                                         uint64_t reg_rows, uint64_t reg_bytes, uint32_t* ovf,
                                                         const uint32_t* pass_flags, const uint32_t* occ,
-                                                        unsigned long long* nvalid) {
+                                                        unsigned long long* nvalid, MergeSelf self) {
   __shared__ unsigned long long base[2 * OWN_MAX], h[2 * OWN_MAX];
   __shared__ uint32_t nv;
   constexpr int PER = OWN_ROWS_PER_BLOCK / 256;
@@ -225,17 +225,18 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
     r.first = first[i];
     r.aoff = 0;
     r.alen = 0;
+    const bool mine = o == self.rank;  // planned: straight into this rank's receive regions
     if (key_is_hashed(r.k1)) {
       const unsigned long long bpos = base[2 * o + 1] + lb[j];
       const uint64_t* src = reinterpret_cast<const uint64_t*>(arena + soff[i]);
-      uint64_t* dst = reinterpret_cast<uint64_t*>(bytes + bpos);
+      uint64_t* dst = reinterpret_cast<uint64_t*>((mine ? self.bytes : bytes) + bpos);
       for (uint32_t c = 0; c < (slen[i] + 7u) / 8u; ++c) dst[c] = src[c];
       unsigned long long bb = fixed ? o * reg_bytes : 0;  // offset inside owner o's byte payload
       for (uint32_t q = 0; !fixed && q < o; ++q) bb += counts[2 * q + 1];
       r.aoff = (uint32_t)(bpos - bb);
       r.alen = slen[i];
     }
-    rows[base[2 * o] + lr[j]] = r;
+    (mine ? self.rows : rows)[base[2 * o] + lr[j]] = r;
     if (send_pos) send_pos[i] = (uint32_t)(base[2 * o] + lr[j]);
   }
 }
@@ -299,7 +300,8 @@ __global__ void __launch_bounds__(256) wc_mrow_compact(const MRow* rows, const u
                                                        const unsigned long long* cnt,
                                                        const unsigned long long* first, uint64_t T,
                                                        const uint64_t* rbase, const uint64_t* bbase, uint32_t W,
-                                                       MRow* out, unsigned long long* out_n, uint32_t* slot_id) {
+                                                       MRow* out, unsigned long long* out_n, uint32_t* slot_id,
+                                                       uint64_t out_cap) {
   __shared__ unsigned long long blk;
   __shared__ uint32_t bcount;
   const int lane = (int)__lane_id();
@@ -332,7 +334,7 @@ __global__ void __launch_bounds__(256) wc_mrow_compact(const MRow* rows, const u
     const unsigned long long f = first[sl];
     if (f < m.first) m.first = f;
     if (m.alen) m.aoff = (uint32_t)(bbase[src] + m.aoff);
-    out[blk + local[j]] = m;
+    if (blk + local[j] < out_cap) out[blk + local[j]] = m;  // past it: counted in out_n (the caller's overflow check)
     if (slot_id) slot_id[sl] = (uint32_t)(blk + local[j]);
   }
 }
@@ -343,12 +345,15 @@ __global__ void __launch_bounds__(256) wc_mrow_compact(const MRow* rows, const u
 // (rows, bytes) pairs `owns` (no host round trip).
 // Padding rows (row_slot all ones, planned exchange) get no id.
 __global__ void wc_row_ids(const uint32_t* row_slot, const uint32_t* slot_id, uint64_t R,
-                           const unsigned long long* owns, uint32_t rank, uint32_t* ids) {
+                           const unsigned long long* owns, uint32_t rank, uint32_t* ids, uint32_t* ids_self,
+                           uint32_t self, uint64_t reg) {
   uint64_t id_base = 0;
   for (uint32_t p = 0; p < rank; ++p) id_base += owns[2 * p];
   for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < R; r += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t sl = row_slot[r];
-    ids[r] = sl == 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)(id_base + slot_id[sl]);
+    // this rank's own region (planned): straight to the returned-id buffer
+    uint32_t* d = ids_self && r / reg == self ? ids_self : ids;
+    d[r] = sl == 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)(id_base + slot_id[sl]);
   }
 }
 
@@ -498,13 +503,15 @@ void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t
                           const uint64_t* soff, const uint32_t* slen, const uint8_t* arena, uint64_t n, uint32_t W,
                           const unsigned long long* counts, unsigned long long* cursor, MRow* rows, uint8_t* bytes,
                           uint32_t* send_pos, hipStream_t s, const uint64_t* dn, uint64_t reg_rows, uint64_t reg_bytes,
-                          uint32_t* ovf, const uint32_t* pass_flags, const uint32_t* occ, unsigned long long* nvalid) {
+                          uint32_t* ovf, const uint32_t* pass_flags, const uint32_t* occ, unsigned long long* nvalid,
+                          const MergeSelf* self) {
+  const MergeSelf me = self ? *self : MergeSelf{~0u, nullptr, nullptr};
   static_assert(TAB_SLOTS % dev::OWN_ROWS_PER_BLOCK == 0, "a scatter block stays inside one table bucket");
   const uint64_t blocks = (n + dev::OWN_ROWS_PER_BLOCK - 1) / dev::OWN_ROWS_PER_BLOCK;
   if (n)
     hipLaunchKernelGGL(dev::wc_owner_scatter, dim3((unsigned)blocks), dim3(256), 0, s, k0, k1, cnt, first, soff, slen,
                        arena, n, dn, W, counts, cursor, rows, bytes, send_pos, reg_rows, reg_bytes, ovf, pass_flags,
-                       occ, nvalid);
+                       occ, nvalid, me);
 }
 void launch_mrow_insert(const MRow* rows, uint64_t R, const uint8_t* bytes, const uint64_t* rbase,
                         const uint64_t* bbase, uint32_t W, uint32_t* state, unsigned long long* cnt,
@@ -515,10 +522,11 @@ void launch_mrow_insert(const MRow* rows, uint64_t R, const uint8_t* bytes, cons
 }
 void launch_mrow_compact(const MRow* rows, const uint32_t* state, const unsigned long long* cnt,
                          const unsigned long long* first, uint64_t T, const uint64_t* rbase, const uint64_t* bbase,
-                         uint32_t W, MRow* out, unsigned long long* out_n, uint32_t* slot_id, hipStream_t s) {
+                         uint32_t W, MRow* out, unsigned long long* out_n, uint32_t* slot_id, hipStream_t s,
+                         uint64_t out_cap) {
   const uint64_t blocks = (T + 256 * dev::MCOMPACT_PER - 1) / (256 * dev::MCOMPACT_PER);
   hipLaunchKernelGGL(dev::wc_mrow_compact, dim3((unsigned)blocks), dim3(256), 0, s, rows, state, cnt, first, T, rbase,
-                     bbase, W, out, out_n, slot_id);
+                     bbase, W, out, out_n, slot_id, out_cap);
 }
 void launch_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rbase, const uint64_t* bbase, uint32_t W,
                          uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first, uint64_t* soff, uint32_t* slen,
@@ -529,8 +537,11 @@ void launch_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rbase, co
 }
 
 void launch_row_ids(const uint32_t* row_slot, const uint32_t* slot_id, uint64_t R, const unsigned long long* owns,
-                    uint32_t rank, uint32_t* ids, hipStream_t s) {
-  if (R) hipLaunchKernelGGL(dev::wc_row_ids, dev::mgrid(R), dim3(256), 0, s, row_slot, slot_id, R, owns, rank, ids);
+                    uint32_t rank, uint32_t* ids, hipStream_t s, uint32_t* ids_self, uint32_t self, uint64_t reg) {
+  WC_CHECK(!ids_self || reg > 0, "row_ids: a region size with ids_self");
+  if (R)
+    hipLaunchKernelGGL(dev::wc_row_ids, dev::mgrid(R), dim3(256), 0, s, row_slot, slot_id, R, owns, rank, ids, ids_self,
+                       self, reg);
 }
 void launch_scatter_ids(const uint32_t* send_pos, const uint32_t* ids_back, const uint64_t* seg,
                         const unsigned long long* owns, uint32_t W, const uint64_t* cnt, const uint64_t* first,
