@@ -246,13 +246,12 @@ def run_rank(a) -> int:
     else:
         eng.synth_device(nbytes, first_segment=first_seg, **synth)
 
-    def step():
-        eng.reset()
+    def step():  # one whole job: reset, count, finalize (ordered device table)
         if host_staged:
+            eng.reset()
             eng.count_pool(pool, nbytes, global_base=base)
-        else:
-            eng.count_resident(nbytes, global_base=base)
-        return eng.finalize_device(comm)
+            return eng.finalize_device(comm)
+        return eng.job_resident(nbytes, global_base=base, comm=comm)
 
     for _ in range(a.warmup):
         step()

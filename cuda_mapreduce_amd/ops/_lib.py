@@ -61,6 +61,7 @@ def _load() -> ctypes.CDLL:
         "wc_engine_destroy": (None, [c_void_p]),
         "wc_engine_reset": (c_int, [c_void_p]),
         "wc_engine_set_stage_events": (c_int, [c_void_p, c_int]),
+        "wc_job_resident": (c_int, [c_void_p, c_uint64, c_uint64, c_void_p, POINTER(c_uint64)]),
         "wc_count_host": (c_int, [c_void_p, P8, c_uint64, c_uint64]),
         "wc_count_file": (c_int, [c_void_p, c_char_p, c_uint64, c_uint64, c_uint64]),
         "wc_count_file_checkpointed": (c_void_p, [c_void_p, c_char_p, c_uint64, c_uint64, c_int, c_int, c_char_p,

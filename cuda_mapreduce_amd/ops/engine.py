@@ -215,6 +215,17 @@ class Engine:
         check(lib.wc_finalize_device(self._p, comm._p if comm else None, ctypes.byref(n)))
         return int(n.value)
 
+    def job_resident(self, nbytes: Optional[int] = None, global_base: int = 0, comm: Optional[Comm] = None) -> int:
+        """reset() + count_resident() + finalize_device() in one native call."""
+        nbytes = self._resident if nbytes is None else nbytes
+        if not hasattr(lib, "wc_job_resident"):  # an older A/B variant build (WC_LIB)
+            self.reset()
+            self.count_resident(nbytes, global_base)
+            return self.finalize_device(comm)
+        n = ctypes.c_uint64(0)
+        check(lib.wc_job_resident(self._p, nbytes, global_base, comm._p if comm else None, ctypes.byref(n)))
+        return int(n.value)
+
     def result(self, comm: Optional[Comm] = None, all_ranks: bool = False) -> Result:
         return Result._from_native(check_ptr(lib.wc_engine_result(self._p, comm._p if comm else None, int(all_ranks))))
 

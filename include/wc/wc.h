@@ -48,6 +48,8 @@ wc_engine* wc_engine_create(const wc_options* o);
 void wc_engine_destroy(wc_engine* e);
 int wc_engine_reset(wc_engine* e);
 int wc_engine_set_stage_events(wc_engine* e, int on);
+/* reset + count the resident text + finalize on the device, in one call */
+int wc_job_resident(wc_engine* e, uint64_t n, uint64_t base, wc_comm* c, uint64_t* n_keys);
 int wc_count_host(wc_engine* e, const uint8_t* text, uint64_t n, uint64_t global_base);
 int wc_count_file(wc_engine* e, const char* path, uint64_t begin, uint64_t end, uint64_t global_base);
 /* Checkpointed count of [begin, end) of a file (rank `rank` of `world`): intervals of

@@ -466,6 +466,17 @@ int wc_finalize_device(wc_engine* e, wc_comm* c, uint64_t* n_keys) {
   return guard([&] { *n_keys = e->e->finalize_device(c ? c->c.get() : nullptr); });
 }
 
+// One whole job on the resident text in one call: reset + count + finalize
+// (the three calls' Python round trips were GPU idle time between jobs).
+int wc_job_resident(wc_engine* e, uint64_t n, uint64_t base, wc_comm* c, uint64_t* n_keys) {
+  return guard([&] {
+    WC_CHECK(e->d_text && n <= e->resident, "no resident text of that size (call wc_synth_device first)");
+    e->e->reset();
+    e->e->count_device(e->d_text, n, e->resident, base, ' ');
+    *n_keys = e->e->finalize_device(c ? c->c.get() : nullptr);
+  });
+}
+
 wc_result* wc_engine_result(wc_engine* e, wc_comm* c, int all_ranks) {
   wc_result* r = new wc_result;
   if (guard([&] { r->t = e->e->result(c ? c->c.get() : nullptr, all_ranks != 0); }) != 0) {

@@ -565,6 +565,9 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
   uint32_t* send_pos = dense ? take_aligned<uint32_t>(A, nb) : nullptr;
   uint32_t* row_slot = dense ? take_aligned<uint32_t>(A, RR) : nullptr;
   uint32_t* slot_id = dense ? take_aligned<uint32_t>(A, T) : nullptr;
+  // dense: padded count / first-offset vectors (zeroed with everything else)
+  uint64_t* vc = dense ? take_aligned<uint64_t>(A, GR) : nullptr;
+  uint64_t* vf = dense ? take_aligned<uint64_t>(A, GR) : nullptr;
   {
     ZeroList z{};  // cursor, flags, padding rows, the owner table, the merged region, this rank's quad: ONE launch
     z.add(d_cur, 2 * (size_t)W * 8);
@@ -578,6 +581,10 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
     z.add(tfirst, T * 8, 0xFFFFFFFFu);
     z.add(d_own, 16);  // merged rows (wc_mrow_compact adds), flags (the scatter ORs)
     if (im.cols.occ) z.add(reinterpret_cast<uint32_t*>(im.d_local_n), 8);  // the scatter counts the table's keys
+    if (dense) {
+      z.add(vc, GR * 8);
+      z.add(vf, GR * 8, 0xFFFFFFFFu);
+    }
     z.copy(d_own + 2, mx, 8);
     z.copy(d_base, base, (2 * (size_t)W + 2) * 8);
     z.copy(d_seg, seg, ((size_t)W + 1) * 8);
@@ -623,23 +630,17 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
     comm.alltoallv(ids, io.data(), is.data(), ids_back, io.data(), is.data(), s);
   }
   comm.group_end();
-  launch_merge_check(d_owns, (uint32_t)W, Gr, key_bound, im.d_merge_flags, s);
+  if (!have) launch_merge_check(d_owns, (uint32_t)W, Gr, key_bound, im.d_merge_flags, s);  // else folded below
   // 4. dense: padded count / first-offset vectors, reduce-scattered (owner o's
   // slice = its ids) and all-gathered
   uint64_t *dcnt = nullptr, *dfirst = nullptr;
   if (dense) {
     // reduce-scatter and all-gather in place: owner R's reduced slice is
     // region R of the vectors, and the gathered vectors are the vectors
-    uint64_t* vc = take_aligned<uint64_t>(A, GR);
-    uint64_t* vf = take_aligned<uint64_t>(A, GR);
     uint64_t* scnt = vc + (uint64_t)R * Gr;
     uint64_t* sfirst = vf + (uint64_t)R * Gr;
     dcnt = vc;
     dfirst = vf;
-    ZeroList z{};
-    z.add(vc, GR * 8);
-    z.add(vf, GR * 8, 0xFFFFFFFFu);
-    launch_zero_regions(z, s);
     launch_scatter_ids(send_pos, ids_back, d_seg, d_owns, (uint32_t)W, im.cols.cnt, im.cols.first, nb, vc, vf, s, dn, Gr);
     comm.group_begin();
     comm.reduce_scatter_u64(vc, scnt, Gr, RedOp::Sum, s);
@@ -677,6 +678,7 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
     comm.group_end();
   }
   KeyCols o;
+  im.max_end = std::max(im.max_end, cp.gmax_end);  // the width the order below is sized for
   if (have) {
     o.n = GR;
     o.dn = d_on;
@@ -686,13 +688,18 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
     o.first = take_aligned<uint64_t>(A, GR);
     o.sref_off = take_aligned<uint64_t>(A, GR);
     o.sref_len = take_aligned<uint32_t>(A, GR);
+    // + the decision flags (wc_merge_check) and, when the sample sort will
+    // order these rows, its exact key histogram: two launches fewer
+    const bool hist = im.sample_order(GR);
+    const uint32_t hm = fo_mbits(im.key_bits());
     launch_mrow_regions_to_cols(grows, (uint32_t)W, Gr, d_owns, RB, dcnt, dfirst, o.k0, o.k1, o.cnt, o.first,
-                                o.sref_off, o.sref_len, d_on, s);
+                                o.sref_off, o.sref_len, d_on, s, im.d_merge_flags, key_bound,
+                                hist ? im.d_fo_hist_cols : nullptr, hm);
+    im.cols_hist_m = hist ? hm : 0;
   }
   im.cols = o;  // in flight: the finalize's last wait publishes the count and the flags
   im.cols_arena = gbytes;
   im.cols_arena_bytes = have ? (uint64_t)W * RB : 0;
-  im.max_end = std::max(im.max_end, cp.gmax_end);
   im.planned_active = true;
   im.st.merges_planned++;
 }

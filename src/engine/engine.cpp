@@ -797,6 +797,10 @@ void Engine::Impl::sort_cols_by_first(bool radix) {
   Range r("wc_finalize_sort");
   fo_ovf = nullptr;
   const uint64_t n = cols.n;
+  if (cols_hist_m && (radix || n == 0 || !sample_order(n))) {  // a histogram the sample sort will not consume
+    WC_HIP_CHECK(hipMemsetAsync(d_fo_hist_cols, 0, FO_LOGBINS * sizeof(uint32_t), s));
+    cols_hist_m = 0;
+  }
   if (n == 0) return;
   // cols.dn: the count is on the device (n its bound) — sort and gather on it
   const uint64_t* dn = reinterpret_cast<const uint64_t*>(cols.dn);
@@ -828,7 +832,9 @@ void Engine::Impl::sort_cols_by_first(bool radix) {
     A.reset();
     take_cols();
     fo_ovf = first_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len}, n, key_bits(),
-                         A.take_n<uint8_t>(first_order_ws_bytes(src, n)), nullptr, s, nullptr, 0, d_fo_hist_cols);
+                         A.take_n<uint8_t>(first_order_ws_bytes(src, n)), nullptr, s, nullptr, 0, d_fo_hist_cols,
+                         cols_hist_m);
+    cols_hist_m = 0;
     cols_unsorted = cols;
     cols = o;
     st.order_path = 1;

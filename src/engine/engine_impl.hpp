@@ -129,6 +129,7 @@ struct Engine::Impl {
   uint32_t fo_hist_m = 0;         // its resolution (fo_mbits of the pass's key width)
   bool fo_hist_ok = false;        // it describes the current table (a pass ran since the reset)
   uint32_t* d_fo_hist_cols = nullptr;  // [FO_LOGBINS] zeroed: exact histogram of merged columns (first_order)
+  uint32_t cols_hist_m = 0;  // nonzero: the planned merge filled d_fo_hist_cols for cols at this resolution
   uint32_t key_bits() const {  // first offsets are < max_end < 2^key_bits
     uint32_t b = 1;
     while (b < 64 && (max_end >> b) != 0) ++b;

@@ -273,9 +273,12 @@ void first_order_stamps(unsigned long long* d);  // debug: phase clocks of the t
 // Otherwise hist_ws (nullable: a zeroed FO_LOGBINS-word buffer, left zeroed)
 // receives the exact histogram from a many-block launch; without either, a
 // one-block sample (wc_fo_split) sets the bins.
+// hist_ready_m (nonzero): hist_ws already holds that exact histogram at
+// resolution hist_ready_m (the planned merge's regions -> columns launch builds
+// it); used when it matches, and left zeroed as usual.
 uint32_t* first_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, uint32_t key_bits, void* ws,
                       uint64_t* nout, hipStream_t s, const uint32_t* key_hist = nullptr, uint32_t key_hist_m = 0,
-                      uint32_t* hist_ws = nullptr);
+                      uint32_t* hist_ws = nullptr, uint32_t hist_ready_m = 0);
 
 // First-occurrence order by ranks from a bitmap over first >> shift (sort.hip:
 // five launches, no comparison sort; the engine uses it above 400k keys).
@@ -391,10 +394,13 @@ void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t
 // (merged rows, flags, max first offset, -) (merge.hip).
 void launch_merge_check(const unsigned long long* owns, uint32_t W, uint64_t reg_merged, uint64_t max_end,
                         uint32_t* flags, hipStream_t s);
+// check_flags (nullable): wc_merge_check folded in (max_end its bound); hist
+// (nullable, zeroed): += fo_logbin(first, hist_m) of every row written.
 void launch_mrow_regions_to_cols(const MRow* rows, uint32_t W, uint64_t reg_merged, const unsigned long long* owns,
                                  uint64_t byte_stride, const uint64_t* dcnt, const uint64_t* dfirst, uint64_t* k0,
                                  uint64_t* k1, uint64_t* cnt, uint64_t* first, uint64_t* soff, uint32_t* slen,
-                                 unsigned long long* out_n, hipStream_t s);
+                                 unsigned long long* out_n, hipStream_t s, uint32_t* check_flags = nullptr,
+                                 uint64_t max_end = 0, uint32_t* hist = nullptr, uint32_t hist_m = 0);
 void launch_mrow_insert(const MRow* rows, uint64_t R, const uint8_t* bytes, const uint64_t* rbase,
                         const uint64_t* bbase, uint32_t W, uint32_t* state, unsigned long long* cnt,
                         unsigned long long* first, uint64_t T, uint32_t* row_slot, hipStream_t s);  // row_slot nullable

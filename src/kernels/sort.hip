@@ -974,7 +974,7 @@ size_t first_order_ws_bytes(const OrderSrc& src, uint64_t bound) {
 
 uint32_t* first_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, uint32_t key_bits, void* ws,
                       uint64_t* nout, hipStream_t s, const uint32_t* key_hist, uint32_t key_hist_m,
-                      uint32_t* hist_ws) {
+                      uint32_t* hist_ws, uint32_t hist_ready_m) {
   WC_CHECK(bound <= FO_MAX_KEYS, "first_order: key bound above FO_MAX_KEYS (use the radix sort)");
   const uint32_t nblk = fo_blocks(src, bound), M = fo_mbits(key_bits), nb = fo_nbins(bound);
   uint8_t* p = static_cast<uint8_t*>(ws);
@@ -986,7 +986,9 @@ uint32_t* first_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, 
   dev::FoEntry* seg = reinterpret_cast<dev::FoEntry*>(p + 64 * 1024 + (mat + 255) / 256 * 256);
   const uint32_t* phist = key_hist && key_hist_m == M ? key_hist : nullptr;
   uint32_t* zero_hist = nullptr;
-  if (!phist && hist_ws) {  // the exact histogram of the keys, many blocks (not the one-block sample)
+  if (!phist && hist_ws && hist_ready_m == M) {  // a producer of the keys already histogrammed them into hist_ws
+    phist = zero_hist = hist_ws;
+  } else if (!phist && hist_ws) {  // the exact histogram of the keys, many blocks (not the one-block sample)
     const uint32_t hb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(256, (bound + dev::FO_HIST_ROWS - 1) / dev::FO_HIST_ROWS));
     hipLaunchKernelGGL(dev::wc_fo_hist, dim3(hb), dim3(1024), 0, s, src, M, hist_ws);
     phist = zero_hist = hist_ws;

@@ -89,6 +89,18 @@ def test_synthetic_device_matches_host():
     assert_same(got, ops.cpu_count(ops.synth_host(n, first_segment=3, seed=11, vocab=20000)))
 
 
+def test_job_resident_one_call():
+    """wc_job_resident (reset + count + finalize in one call, the bench's step)
+    leaves the same ordered table as the three calls, job after job."""
+    n = 8 << 20
+    want = ops.cpu_count(ops.synth_host(n, first_segment=2, seed=5, vocab=30000))
+    with ops.Engine(device=0) as e:
+        e.synth_device(n, first_segment=2, seed=5, vocab=30000)
+        for _ in range(3):
+            assert e.job_resident(n) == len(want)
+            assert_same(e.result(), want)
+
+
 def test_table_split_large_vocab():
     # 2 buckets x 4096 slots to start; ~60k distinct words force several splits
     words = [f"w{i:x}".encode() for i in range(60000)]
