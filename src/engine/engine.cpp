@@ -280,14 +280,34 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   const bool sample = !hot_valid || hot_resample_every == 0 || hot_age >= hot_resample_every ||
                       hot_miss_last > hot_miss_ref * hot_resample_slack;
   pass_sampled = sample;
+  // The last pass of a job, with its finalize launched right behind it: the
+  // finalize's order is known now.  Unless the sample sort will run, the
+  // reducer's key histogram is useless (~1M device atomics at 1M keys); for
+  // the bitmap-rank order the reducer sets the keys' bits instead.
+  bool want_hist = true;
+  unsigned long long* bm = nullptr;
+  uint64_t bm_end = 0;
+  if (defer_publish) {
+    drop_reduce_bits();
+    const uint64_t hint = spec_hint();
+    if (!sample_order(hint)) {
+      want_hist = false;
+      if (bitmap_order_ok(hint)) {
+        bm_end = std::max(max_end, base + len);
+        max_end = bm_end;  // the order's key width (the finalize reads the same value)
+        bm = ensure_bitmap();
+        bm_in_reduce = true;
+      }
+    }
+  }
   ZeroList z{};
   z.add(d_ctr, sizeof(DevCounters));
-  z.add(d_fo_hist, FO_LOGBINS * sizeof(uint32_t));  // rebuilt by this pass's reduce over the whole table
+  if (want_hist) z.add(d_fo_hist, FO_LOGBINS * sizeof(uint32_t));  // rebuilt by this pass's reduce over the whole table
   {
     uint32_t kb = 1;
     while (kb < 64 && (std::max(max_end, base + len) >> kb) != 0) ++kb;
     fo_hist_m = fo_mbits(kb);
-    fo_hist_ok = true;
+    fo_hist_ok = want_hist;
   }
   if (reset_pending) {
     z.add(table().occupancy, ((size_t)1 << table().log2_buckets) * 4);
@@ -312,7 +332,8 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   }
   ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                 avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
-                d_ctr->flags, d_bucket_ovf, nullptr, d_red_stamps, d_fo_hist, fo_hist_m, red_q(), part};
+                d_ctr->flags, d_bucket_ovf, nullptr, d_red_stamps, want_hist ? d_fo_hist : nullptr, fo_hist_m,
+                bm, bm ? bitmap_order_ctl(bm, bm_end, 1) : nullptr, bm ? (bm_end >> 1) + 1 : 0, 1u, red_q(), part};
   launch_reduce(ra, s);
   if (sync_debug) {
     const hipError_t e = hipStreamSynchronize(s);
@@ -380,7 +401,19 @@ void Engine::Impl::collect_stage_times() {
   st.device_ms = st.map_ms + st.reduce_ms + st.merge_ms + st.finalize_ms + st.idle_ms;
 }
 
+void Engine::Impl::drop_reduce_bits() {
+  if (!bm_in_reduce) return;
+  bm_in_reduce = false;
+  WC_HIP_CHECK(hipMemsetAsync(d_bm, 0, bm_words * sizeof(unsigned long long), s));  // bits + control word
+}
+
+uint64_t Engine::Impl::spec_hint() {
+  const uint64_t cap = ((uint64_t)1 << table().log2_buckets) * TAB_SLOTS;
+  return std::min<uint64_t>(cap, last_keys ? last_keys + last_keys / 8 + 1024 : cap / 4);
+}
+
 void Engine::Impl::settle() {
+  drop_reduce_bits();  // a pending pass completed by anything but the speculative local finalize
   if (!pend.active) return;
   const PendingPass p = pend;
   pend.active = false;
@@ -530,7 +563,8 @@ bool Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
     WC_HIP_CHECK(hipMemsetAsync(d_ctr, 0, sizeof(DevCounters), s));
     ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                   avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
-                  d_ctr->flags, d_bucket_ovf, d_bucket_en, d_red_stamps, d_fo_hist, fo_hist_m, red_q(), part};
+                  d_ctr->flags, d_bucket_ovf, d_bucket_en, d_red_stamps, fo_hist_ok ? d_fo_hist : nullptr, fo_hist_m,
+                  nullptr, nullptr, 0, 0u, red_q(), part};
     launch_reduce(ra, s);
     PubList pc{};
     pc.add(h_ctr, d_ctr, sizeof(DevCounters));
@@ -622,9 +656,10 @@ bool Engine::Impl::finalize_local_speculative() {
   const TableView& t = table();
   const size_t nb = (size_t)1 << t.log2_buckets;
   const uint64_t cap = (uint64_t)nb * TAB_SLOTS;
-  const uint64_t hint = std::min<uint64_t>(cap, last_keys ? last_keys + last_keys / 8 + 1024 : cap / 4);
+  const uint64_t hint = spec_hint();  // the same hint launch_pass chose the reducer's extras from
   const bool sample = sample_order(hint);  // sized for the hint; a far larger count -> overflow -> redo
   const bool bitmap = !sample && bitmap_order_ok(hint);
+  if (!bitmap) drop_reduce_bits();  // (cannot be set: the same hint decided the pass's extras)
   OrderSrc src{};
   src.table = true;
   src.t = t;
@@ -650,7 +685,8 @@ bool Engine::Impl::finalize_local_speculative() {
                       fo_hist_m);
   } else if (bitmap) {
     ovf = bitmap_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len}, cap, max_end, 1, bm,
-                       A.take_n<uint8_t>(bitmap_order_ws_bytes(cap + 1, max_end, 1)), d_n, s);
+                       A.take_n<uint8_t>(bitmap_order_ws_bytes(cap + 1, max_end, 1)), d_n, s, bm_in_reduce);
+    bm_in_reduce = false;  // consumed (the order leaves the bitmap zeroed, a failed pass included)
   } else {
     uint64_t* d_boff = A.take_n<uint64_t>(nb);
     uint64_t* keys = A.take_n<uint64_t>(cap + 1);
@@ -934,6 +970,7 @@ void Engine::reset() {
   // zero only the occupancy: a bucket with occupancy 0 is empty whatever its
   // slice holds (reduce / compact / split never read such a slice)
   im.pend.active = false;  // an unchecked pass of the previous job is discarded with it
+  im.drop_reduce_bits();
   im.pass_pub_pending = false;
   // no API call: the next pass's zeroing launch clears occupancy + arena cursor
   // (apply_reset does it first for anything else that reads the table)
@@ -1222,6 +1259,7 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
   bool drained = false;
   im.planned_active = false;
   if (merged) {
+    im.drop_reduce_bits();  // the merged order runs on merged columns
     // planned (no host round trip) when the last exact merge of this shape
     // left its caps, else the speculative exact protocol, else the synchronous one
     const bool spec = im.pend.active && im.speculate && !im.sync_debug &&

@@ -260,6 +260,11 @@ struct Engine::Impl {
   unsigned long long* d_bm = nullptr;  // bitmap_order's bitmap: all zero between calls
   size_t bm_words = 0;
   unsigned long long* ensure_bitmap();  // sized for max_end
+  // The pending last pass's reduce set the bitmap's bits (ReduceArgs::bm): the
+  // speculative finalize's bitmap order consumes them; any other path clears them.
+  bool bm_in_reduce = false;
+  void drop_reduce_bits();
+  uint64_t spec_hint();  // the speculative finalize's key-count hint (sizes its order)
   uint32_t* fo_ovf = nullptr;  // overflow word of the sample sort sort_cols_by_first left in flight
   KeyCols cols_unsorted;       // its input, kept for a radix redo
   bool order_redo = false;     // the speculative finalize's sample sort overflowed (Stats::order_path 4)

@@ -174,6 +174,13 @@ struct ReduceArgs {
   unsigned long long* stamps;     // [RED_STAMP_N] diagnostic counters (WC_RED_STAMPS builds), nullable
   uint32_t* fo_hist;              // [FO_LOGBINS] += every stored key's fo_logbin(first, fo_m) (nullable)
   uint32_t fo_m;
+  // The last pass before a bitmap-rank order (nullable): every stored key sets
+  // its bit and its bucket's key count goes to the control word — the order
+  // then skips its own bit-set launch (sort.hip bitmap_order, bits_set)
+  unsigned long long* bm;
+  unsigned long long* bm_ctl;
+  uint64_t bm_pos_end;
+  uint32_t bm_shift;
   // Split reduce (nq > 1: fewer table buckets than CUs).  Block b + B q (q < nq)
   // merges the runs of map blocks p = q mod nq into a partial table of bucket b
   // (q = 0 starting from the running slice, the others empty) and writes its
@@ -292,8 +299,11 @@ uint32_t* first_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, 
 // the output is then invalid (redo with radix_sort_pairs).
 size_t bitmap_order_words(uint64_t key_end, uint32_t shift);
 size_t bitmap_order_ws_bytes(uint64_t bound, uint64_t key_end, uint32_t shift);
+// bits_set: the reduce already set every key's bit and added the key count
+// (ReduceArgs::bm); bitmap_order_ctl: that control word's address.
 uint32_t* bitmap_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, uint64_t key_end, uint32_t shift,
-                       unsigned long long* bm, void* ws, uint64_t* nout, hipStream_t s);
+                       unsigned long long* bm, void* ws, uint64_t* nout, hipStream_t s, bool bits_set = false);
+unsigned long long* bitmap_order_ctl(unsigned long long* bm, uint64_t key_end, uint32_t shift);
 
 // out[i] = in[perm[i]] for the six key-table columns (one launch).
 void launch_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,

@@ -786,6 +786,24 @@ __device__ __forceinline__ void add_fo_hist(const RedLds& L, const ReduceArgs& a
     if (slot_tag(L.grp, s) > TAG_PENDING) atomicAdd(&a.fo_hist[fo_logbin(L.first[s], a.fo_m)], 1u);
 }
 
+// The last pass before a bitmap-rank order: the stored keys' bits (atomic ORs
+// without return, overlapped with the rest of the reduce) and their count.
+__device__ __forceinline__ void add_bm_bits(const RedLds& L, const ReduceArgs& a) {
+  if (!a.bm) return;
+  bool range = false;
+  for (int s = threadIdx.x; s < TAB_SLOTS; s += RED_THREADS) {
+    if (slot_tag(L.grp, s) <= TAG_PENDING) continue;
+    const uint64_t p = L.first[s] >> a.bm_shift;
+    if (p >= a.bm_pos_end) {
+      range = true;
+      continue;
+    }
+    __hip_atomic_fetch_or(&a.bm[p >> 6], 1ull << (p & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (range) atomicOr(a.bm_ctl, 1ull << 63);  // the order's range flag
+  if (threadIdx.x == 0 && L.occupied) atomicAdd(a.bm_ctl, (unsigned long long)L.occupied);
+}
+
 // Split reduce: a quarter's occupied slots -> its part rows (slot order, a
 // block scan places them; LONG rows carry their arena / text reference).
 __device__ void write_partial(const RedLds& L, const ReduceArgs& a, const LongCtx& c, uint32_t pb) {
@@ -910,6 +928,7 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
     settle_new_long(L, a, b);
     store_slice(L, a.tab, b);
     add_fo_hist(L, a);
+    add_bm_bits(L, a);
     if (tid == 0) {
       a.tab.occupancy[b] = L.occupied;
       atomicMax(&a.flags[FLAG_MAX_OCC], L.occupied);

@@ -1031,8 +1031,12 @@ size_t bitmap_order_ws_bytes(uint64_t bound, uint64_t key_end, uint32_t shift) {
          std::max<uint64_t>(bound, 1) * sizeof(dev::BmRow) + 64;
 }
 
+unsigned long long* bitmap_order_ctl(unsigned long long* bm, uint64_t key_end, uint32_t shift) {
+  return bm + bm_blocks(key_end, shift) * dev::BM_BLOCK_WORDS;
+}
+
 uint32_t* bitmap_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, uint64_t key_end, uint32_t shift,
-                       unsigned long long* bm, void* ws, uint64_t* nout, hipStream_t s) {
+                       unsigned long long* bm, void* ws, uint64_t* nout, hipStream_t s, bool bits_set) {
   const uint64_t lines = bm_lines(key_end, shift), blocks = bm_blocks(key_end, shift);
   WC_CHECK(blocks < (1ull << 31), "bitmap_order: key bound too large");
   uint8_t* p = static_cast<uint8_t*>(ws);
@@ -1049,7 +1053,7 @@ uint32_t* bitmap_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound,
   const uint64_t pos_end = (key_end >> shift) + 1;
   const uint64_t rows = src.table ? ((uint64_t)1 << src.t.log2_buckets) * TAB_SLOTS : bound;
   const dim3 g((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(4096, (rows + 255) / 256)));
-  hipLaunchKernelGGL(dev::wc_bm_set, g, dim3(256), 0, s, src, rows, bm, shift, pos_end, ctl);
+  if (!bits_set) hipLaunchKernelGGL(dev::wc_bm_set, g, dim3(256), 0, s, src, rows, bm, shift, pos_end, ctl);
   hipLaunchKernelGGL(dev::wc_bm_count, dim3((unsigned)blocks), dim3(dev::BM_BLOCK_LINES), 0, s, bm, lines, linepre,
                      blocktot);
   hipLaunchKernelGGL(dev::wc_bm_scan, dim3(1), dim3(1024), 0, s, blocktot, (uint32_t)blocks, blockpre, n, ctl, ovf);

@@ -64,6 +64,25 @@ def test_bitmap_order_forced(vocab, n, chunk, monkeypatch):
             assert e.stats()["order_path"] == 5
 
 
+@pytest.mark.parametrize("vocab", [40, 60000])
+def test_bitmap_order_resident(vocab, monkeypatch):
+    """WC_FIRST_ORDER=bitmap on resident text: the last pass's reduce sets the
+    keys' bits itself (the order skips its bit-set launch); jobs in a row and a
+    count_bytes job in between (which sets its own bits) stay exact."""
+    monkeypatch.setenv("WC_FIRST_ORDER", "bitmap")
+    n = 16 << 20
+    want = ops.cpu_count(ops.synth_host(n, first_segment=1, seed=vocab, vocab=vocab, zipf_s=0.6))
+    other = ops.synth_host(4 << 20, seed=7, vocab=5000)
+    with ops.Engine(device=0) as e:
+        for job in range(3):
+            assert_same(_resident(e, n, vocab, vocab), want)
+            assert e.stats()["order_path"] == 5
+            if job == 1:
+                e.reset()
+                e.count_bytes(other)
+                assert_same(e.result(), ops.cpu_count(other))
+
+
 def test_bitmap_order_merged(monkeypatch):
     """The merged table's order by bitmap ranks (key columns, count on the device)."""
     monkeypatch.setenv("WC_FIRST_ORDER", "bitmap")
