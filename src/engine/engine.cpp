@@ -333,7 +333,8 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                 avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
                 d_ctr->flags, d_bucket_ovf, nullptr, d_red_stamps, want_hist ? d_fo_hist : nullptr, fo_hist_m,
-                bm, bm ? bitmap_order_ctl(bm, bm_end, 1) : nullptr, bm ? (bm_end >> 1) + 1 : 0, 1u, red_q(), part};
+                bm, bm ? bitmap_order_linecnt(bm, bm_end, 1) : nullptr, bm ? bitmap_order_ctl(bm, bm_end, 1) : nullptr,
+                bm ? (bm_end >> 1) + 1 : 0, 1u, red_q(), part};
   launch_reduce(ra, s);
   if (sync_debug) {
     const hipError_t e = hipStreamSynchronize(s);
@@ -564,7 +565,7 @@ bool Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
     ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                   avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
                   d_ctr->flags, d_bucket_ovf, d_bucket_en, d_red_stamps, fo_hist_ok ? d_fo_hist : nullptr, fo_hist_m,
-                  nullptr, nullptr, 0, 0u, red_q(), part};
+                  nullptr, nullptr, nullptr, 0, 0u, red_q(), part};
     launch_reduce(ra, s);
     PubList pc{};
     pc.add(h_ctr, d_ctr, sizeof(DevCounters));

@@ -178,6 +178,7 @@ struct ReduceArgs {
   // its bit and its bucket's key count goes to the control word — the order
   // then skips its own bit-set launch (sort.hip bitmap_order, bits_set)
   unsigned long long* bm;
+  uint32_t* bm_lines;  // per 512-bit line: keys set in it
   unsigned long long* bm_ctl;
   uint64_t bm_pos_end;
   uint32_t bm_shift;
@@ -304,6 +305,7 @@ size_t bitmap_order_ws_bytes(uint64_t bound, uint64_t key_end, uint32_t shift);
 uint32_t* bitmap_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, uint64_t key_end, uint32_t shift,
                        unsigned long long* bm, void* ws, uint64_t* nout, hipStream_t s, bool bits_set = false);
 unsigned long long* bitmap_order_ctl(unsigned long long* bm, uint64_t key_end, uint32_t shift);
+uint32_t* bitmap_order_linecnt(unsigned long long* bm, uint64_t key_end, uint32_t shift);  // per 512-bit line
 
 // out[i] = in[perm[i]] for the six key-table columns (one launch).
 void launch_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,

@@ -798,9 +798,11 @@ __device__ __forceinline__ void add_bm_bits(const RedLds& L, const ReduceArgs& a
       range = true;
       continue;
     }
-    __hip_atomic_fetch_or(&a.bm[p >> 6], 1ull << (p & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long m = 1ull << (p & 63);
+    if (__hip_atomic_fetch_or(&a.bm[p >> 6], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & m) range = true;
+    __hip_atomic_fetch_add(&a.bm_lines[p >> 9], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (range) atomicOr(a.bm_ctl, 1ull << 63);  // the order's range flag
+  if (range) atomicOr(a.bm_ctl, 1ull << 63);  // the order's redo flag (out of bounds, or a shared position)
   if (threadIdx.x == 0 && L.occupied) atomicAdd(a.bm_ctl, (unsigned long long)L.occupied);
 }
 

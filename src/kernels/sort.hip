@@ -698,10 +698,12 @@ inline dim3 grid_for(uint64_t n) {
 // bytes apart (a delimiter between them), so first >> 1 indexes a bitmap
 // without collisions: 1 GiB of text is a 64 MiB bitmap.  A key's output row is
 // the number of set bits before its position — no comparison sort at all:
-//   wc_bm_set     set each key's bit (an atomic OR without return) and count
-//                 the keys into the bitmap's control word
-//   wc_bm_count   popcount per 512-bit line (one 64-byte line per thread), the
-//                 lines' exclusive prefix inside each 256-line block + block totals
+//   wc_bm_set     set each key's bit (an atomic OR; a bit already set = two
+//                 keys at one position: the redo flag), add 1 to its 512-bit
+//                 line's counter, and count the keys into the control word
+//   wc_bm_count   per line its counter (4 bytes, not the 64-byte line: 4 MiB
+//                 read at 1M lines instead of 64 MiB), the lines' exclusive
+//                 prefix inside each 256-line block + block totals
 //   wc_bm_scan    one block: the block totals' exclusive scan and the key
 //                 count; fewer set bits than keys (two keys at one position)
 //                 or a key beyond the bound raises the overflow word, and the
@@ -713,14 +715,16 @@ inline dim3 grid_for(uint64_t n) {
 //                 8-byte column stores measured 160 us at 1M keys, 6 partial
 //                 lines each)
 //   wc_bm_emit    records -> the six columns in row order (coalesced), and the
-//                 row's bitmap word zeroed: every set bit has a row, so the
-//                 bitmap is left all-zero for the next call
+//                 row's bitmap word and line counter zeroed: every set bit has
+//                 a row, so the bitmap is left all-zero for the next call
 // The radix path it replaces (4 digit passes + histogram + table keys +
 // gather) measured 200 us at 1M keys (profiles/r4_session3.md §7).
 constexpr uint32_t BM_LINE_BITS = 512;
 constexpr uint32_t BM_BLOCK_LINES = 256;
 constexpr uint64_t BM_BLOCK_WORDS = BM_BLOCK_LINES * BM_LINE_BITS / 64;
-constexpr uint64_t BM_RANGE = 1ull << 63;  // control word: a key beyond the bound (+ the key count below)
+constexpr uint64_t BM_BLOCK_CNT_WORDS = BM_BLOCK_LINES / 2;  // the block's u32 line counters, in u64 words
+// control word: redo (a key beyond the bound, or two keys at one position) | the key count
+constexpr uint64_t BM_RANGE = 1ull << 63;
 struct alignas(64) BmRow {
   uint64_t k0, k1, cnt, first, soff;
   uint32_t slen, pad0;
@@ -743,8 +747,8 @@ __device__ inline uint64_t bm_rows(const OrderSrc& src, uint64_t rows) {
   return !src.table && src.dn ? *src.dn : rows;
 }
 
-__global__ void __launch_bounds__(256) wc_bm_set(OrderSrc src, uint64_t rows, unsigned long long* bm, uint32_t shift,
-                                                 uint64_t pos_end, unsigned long long* ctl) {
+__global__ void __launch_bounds__(256) wc_bm_set(OrderSrc src, uint64_t rows, unsigned long long* bm, uint32_t* lc,
+                                                 uint32_t shift, uint64_t pos_end, unsigned long long* ctl) {
   __shared__ uint32_t wn[4];
   rows = bm_rows(src, rows);
   uint32_t n = 0;
@@ -761,7 +765,9 @@ __global__ void __launch_bounds__(256) wc_bm_set(OrderSrc src, uint64_t rows, un
     // random 8-byte writes dominate: 1M keys over a 64 MiB bitmap measured 68 us
     // with 64- or 32-bit, agent- or workgroup-scope ORs, with or without the
     // return, and 52 us as plain (inexact) stores (tools/bm_probe.py)
-    __hip_atomic_fetch_or(&bm[p >> 6], 1ull << (p & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long m = 1ull << (p & 63);
+    if (__hip_atomic_fetch_or(&bm[p >> 6], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & m) range = true;
+    __hip_atomic_fetch_add(&lc[p / BM_LINE_BITS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
   range = __any(range);
@@ -774,20 +780,12 @@ __global__ void __launch_bounds__(256) wc_bm_set(OrderSrc src, uint64_t rows, un
   if (range && (threadIdx.x & 63) == 0) atomicOr(ctl, (unsigned long long)BM_RANGE);
 }
 
-__global__ void __launch_bounds__(BM_BLOCK_LINES) wc_bm_count(const unsigned long long* bm, uint64_t lines,
-                                                              uint32_t* linepre, uint32_t* blocktot) {
+__global__ void __launch_bounds__(BM_BLOCK_LINES) wc_bm_count(const uint32_t* lc, uint64_t lines, uint32_t* linepre,
+                                                              uint32_t* blocktot) {
   __shared__ uint32_t wsum[BM_BLOCK_LINES / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t line = (uint64_t)blockIdx.x * BM_BLOCK_LINES + tid;
-  uint32_t c = 0;
-  if (line < lines) {
-    const ulonglong2* q = reinterpret_cast<const ulonglong2*>(bm + line * (BM_LINE_BITS / 64));
-    ulonglong2 v[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = q[k];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) c += __popcll(v[k].x) + __popcll(v[k].y);
-  }
+  const uint32_t c = line < lines ? lc[line] : 0u;
   uint32_t incl = c;
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t y = __shfl_up(incl, o);
@@ -896,8 +894,13 @@ __global__ void __launch_bounds__(256) wc_bm_place(OrderSrc src, uint64_t rows, 
   }
 }
 
+// With two keys at one position (the redo flag) the line counters count more
+// keys than set bits, so some rows below *n were never placed: their stale
+// contents are cleared only inside the bitmap's bounds (ranks of distinct
+// positions stay distinct, so every set bit still has its own placed row).
 __global__ void __launch_bounds__(256) wc_bm_emit(const BmRow* in, const uint64_t* n, OrderDst dst,
-                                                  unsigned long long* bm, uint32_t shift) {
+                                                  unsigned long long* bm, uint32_t* lc, uint32_t shift,
+                                                  uint64_t pos_end) {
   const uint64_t rows = *n;
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < rows; i += (uint64_t)gridDim.x * 256) {
     const ulonglong2* q = reinterpret_cast<const ulonglong2*>(in + i);
@@ -908,7 +911,11 @@ __global__ void __launch_bounds__(256) wc_bm_emit(const BmRow* in, const uint64_
     dst.first[i] = b.y;
     dst.soff[i] = c.x;
     dst.slen[i] = (uint32_t)c.y;
-    bm[(b.y >> shift) >> 6] = 0;
+    const uint64_t p = b.y >> shift;
+    if (p < pos_end) {
+      bm[p >> 6] = 0;
+      lc[p / BM_LINE_BITS] = 0;
+    }
   }
 }
 
@@ -1025,14 +1032,20 @@ static uint64_t bm_blocks(uint64_t key_end, uint32_t shift) {
   return (bm_lines(key_end, shift) + dev::BM_BLOCK_LINES - 1) / dev::BM_BLOCK_LINES;
 }
 // + 8 words: the control word (key count | range flag) after the bitmap
-size_t bitmap_order_words(uint64_t key_end, uint32_t shift) { return bm_blocks(key_end, shift) * dev::BM_BLOCK_WORDS + 8; }
+// bitmap | line counters | 8 control words
+size_t bitmap_order_words(uint64_t key_end, uint32_t shift) {
+  return bm_blocks(key_end, shift) * (dev::BM_BLOCK_WORDS + dev::BM_BLOCK_CNT_WORDS) + 8;
+}
+uint32_t* bitmap_order_linecnt(unsigned long long* bm, uint64_t key_end, uint32_t shift) {
+  return reinterpret_cast<uint32_t*>(bm + bm_blocks(key_end, shift) * dev::BM_BLOCK_WORDS);
+}
 size_t bitmap_order_ws_bytes(uint64_t bound, uint64_t key_end, uint32_t shift) {
   return 256 + (bm_lines(key_end, shift) * 4 + 255) / 256 * 256 + bm_blocks(key_end, shift) * 12 + 512 +
          std::max<uint64_t>(bound, 1) * sizeof(dev::BmRow) + 64;
 }
 
 unsigned long long* bitmap_order_ctl(unsigned long long* bm, uint64_t key_end, uint32_t shift) {
-  return bm + bm_blocks(key_end, shift) * dev::BM_BLOCK_WORDS;
+  return bm + bm_blocks(key_end, shift) * (dev::BM_BLOCK_WORDS + dev::BM_BLOCK_CNT_WORDS);
 }
 
 uint32_t* bitmap_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, uint64_t key_end, uint32_t shift,
@@ -1049,17 +1062,18 @@ uint32_t* bitmap_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound,
   uint32_t* blocktot = reinterpret_cast<uint32_t*>(q);
   q += (blocks * 4 + 255) / 256 * 256;
   dev::BmRow* rows_buf = reinterpret_cast<dev::BmRow*>((reinterpret_cast<uintptr_t>(q) + 63) & ~uintptr_t(63));
-  unsigned long long* ctl = bm + blocks * dev::BM_BLOCK_WORDS;
+  unsigned long long* ctl = bitmap_order_ctl(bm, key_end, shift);
+  uint32_t* lc = bitmap_order_linecnt(bm, key_end, shift);
   const uint64_t pos_end = (key_end >> shift) + 1;
   const uint64_t rows = src.table ? ((uint64_t)1 << src.t.log2_buckets) * TAB_SLOTS : bound;
   const dim3 g((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(4096, (rows + 255) / 256)));
-  if (!bits_set) hipLaunchKernelGGL(dev::wc_bm_set, g, dim3(256), 0, s, src, rows, bm, shift, pos_end, ctl);
-  hipLaunchKernelGGL(dev::wc_bm_count, dim3((unsigned)blocks), dim3(dev::BM_BLOCK_LINES), 0, s, bm, lines, linepre,
+  if (!bits_set) hipLaunchKernelGGL(dev::wc_bm_set, g, dim3(256), 0, s, src, rows, bm, lc, shift, pos_end, ctl);
+  hipLaunchKernelGGL(dev::wc_bm_count, dim3((unsigned)blocks), dim3(dev::BM_BLOCK_LINES), 0, s, lc, lines, linepre,
                      blocktot);
   hipLaunchKernelGGL(dev::wc_bm_scan, dim3(1), dim3(1024), 0, s, blocktot, (uint32_t)blocks, blockpre, n, ctl, ovf);
   hipLaunchKernelGGL(dev::wc_bm_place, g, dim3(256), 0, s, src, rows, bm, shift, pos_end, linepre, blockpre, rows_buf);
   const dim3 ge((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(4096, (bound + 255) / 256)));
-  hipLaunchKernelGGL(dev::wc_bm_emit, ge, dim3(256), 0, s, rows_buf, n, dst, bm, shift);
+  hipLaunchKernelGGL(dev::wc_bm_emit, ge, dim3(256), 0, s, rows_buf, n, dst, bm, lc, shift, pos_end);
   return ovf;
 }
 }  // namespace wc
