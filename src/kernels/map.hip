@@ -69,7 +69,7 @@ constexpr int SPT = MAP_SLOTS / MAP_THREADS;
 #define WC_HOT_K (HOT_GROUP_SLOTS == 2 ? MAP_SLOTS * 7 / 8 : MAP_SLOTS * 3 / 4)
 #endif
 #ifndef WC_HOT_SAMPLE
-#define WC_HOT_SAMPLE 8  // 8 vs 4: wc_hot_sample +4 us, wc_map -16 us at v100k (profiles/r4_session3.md §13)
+#define WC_HOT_SAMPLE 4  // 8: +0.3-1 % at v100k but long30_v1m 388 -> 245 GB/s (profiles/r4_session3.md §13)
 #endif
 constexpr uint32_t HOT_K = WC_HOT_K;            // words placed in the hot table
 constexpr uint32_t HOT_SAMPLE = WC_HOT_SAMPLE;  // units sampled per map block
