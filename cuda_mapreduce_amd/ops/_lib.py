@@ -54,6 +54,7 @@ def _load() -> ctypes.CDLL:
         "wc_bench_radix_sort": (c_int, [c_int, P64, c_uint64, c_int, c_int, POINTER(ctypes.c_double)]),
         "wc_debug_first_order": (c_int, [c_int, P64, c_uint64, c_int, P64, POINTER(ctypes.c_uint32),
                                          POINTER(c_int), POINTER(ctypes.c_double)]),
+        "wc_debug_read_file": (c_int, [c_char_p, c_uint64, c_uint64, c_uint64, P8, POINTER(c_uint64)]),
         "wc_debug_order": (c_int, [c_int, c_int, P64, c_uint64, c_int, P64, POINTER(ctypes.c_uint32),
                                    POINTER(c_int), POINTER(ctypes.c_double), P64]),
         "wc_default_options": (None, [POINTER(Options)]),

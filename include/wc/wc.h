@@ -31,6 +31,8 @@ typedef struct wc_options {
 const char* wc_last_error(void);
 const char* wc_version(void);
 int wc_device_count(void);
+/* Host-only test hook: bytes [begin, end) of a file through the parallel reader, `piece` bytes per read. */
+int wc_debug_read_file(const char* path, uint64_t begin, uint64_t end, uint64_t piece, uint8_t* dst, uint64_t* got);
 /* Kernel test hook: stable LSD radix sort of n u64 keys (low `bits` bits) on
  * `device`; returns the sorted keys and the permutation (host arrays). */
 int wc_debug_radix_sort(int device, const uint64_t* keys, uint64_t n, int bits, uint64_t* sorted, uint32_t* perm);

@@ -147,6 +147,21 @@ int wc_debug_loopback_async(int device, int* returned, int* pending, int* correc
 // FileSource reader) in pieces of `piece` bytes into one page-locked buffer
 // bound to `device`'s NUMA node, nothing copied to the GPU: the ceiling the
 // file-streaming count is measured against (tools/file_path.sh).
+// Host-only test hook: read bytes [begin, end) of a file through FileSource
+// (the parallel reader pool) in pieces of `piece` bytes into dst.
+int wc_debug_read_file(const char* path, uint64_t begin, uint64_t end, uint64_t piece, uint8_t* dst, uint64_t* got) {
+  return guard([&] {
+    wc::FileSource src(path, begin, end);
+    uint64_t n = 0;
+    for (;;) {
+      const uint64_t k = src.read(dst + n, std::min<uint64_t>(piece, end - begin - n));
+      if (k == 0) break;
+      n += k;
+    }
+    *got = n;
+  });
+}
+
 int wc_file_read_bench(const char* path, uint64_t piece, int device, double* gbps, uint64_t* bytes) {
   return guard([&] {
     const wc::NumaNode nn = device >= 0 ? wc::numa_of_device(device) : wc::NumaNode{};

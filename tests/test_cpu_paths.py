@@ -201,3 +201,26 @@ def test_cli_refuses_more_gpus_than_visible(tmp_path, golden_text):
     assert b"8 GPUs requested" in out.stderr and b"visible" in out.stderr
     bad = subprocess.run([exe, "--virtual-ranks", "4", "--gpus", "2"], cwd=tmp_path, capture_output=True, timeout=60)
     assert bad.returncode != 0 and b"--virtual-ranks runs on one GPU" in bad.stderr
+
+
+@pytest.mark.parametrize("piece", [65521, 1 << 20, (4 << 20) + 7, 48 << 20])
+def test_parallel_file_reader(tmp_path, piece):
+    """FileSource through pread_parallel's persistent reader pool (16 threads,
+    4 MiB slices; src/io/source.cpp): every byte of [begin, end) in order, for
+    pieces below, at and above the slice size, and a range that starts and ends
+    mid-file."""
+    import ctypes
+
+    from cuda_mapreduce_amd.ops._lib import check, lib
+
+    rng = np.random.default_rng(piece)
+    data = rng.integers(0, 256, (40 << 20) + 12345, dtype=np.uint8)
+    path = tmp_path / "f.bin"
+    data.tofile(path)
+    for begin, end in ((0, len(data)), (777, len(data) - 999)):
+        out = np.zeros(end - begin, np.uint8)
+        got = ctypes.c_uint64(0)
+        check(lib.wc_debug_read_file(str(path).encode(), begin, end, piece,
+                                     out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(got)))
+        assert got.value == end - begin
+        assert np.array_equal(out, data[begin:end])
