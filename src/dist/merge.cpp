@@ -522,17 +522,8 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
   unsigned long long* d_own = d_owns + 4 * (size_t)R;  // merged rows | flags | max offset | -, gathered in place
   unsigned long long* d_on = take_aligned<unsigned long long>(S, 1);
   im.d_merge_flags = take_aligned<uint32_t>(S, 2);
-  uint64_t* mx = host_words(im) + HW_MX;
-  *mx = im.max_end;
   // the key width the finalize's order is sized for: every rank's first offsets must fit it
   const uint64_t key_bound = std::max(im.max_end, cp.gmax_end);
-  uint64_t* base = host_words(im) + HW_BASE;  // fixed-region bases per source: rows | bytes
-  for (int p = 0; p <= W; ++p) {
-    base[p] = (uint64_t)p * Cr;
-    base[W + 1 + p] = (uint64_t)p * Cb;
-  }
-  uint64_t* seg = host_words(im) + HW_SEG;  // send-row starts per owner (dense id return)
-  for (int p = 0; p <= W; ++p) seg[p] = (uint64_t)p * Cr;
 
   DeviceArena& A = im.merge_mem;
   const uint64_t RR = (uint64_t)W * Cr, RB = (uint64_t)W * Cb, GR = (uint64_t)W * Gr;
@@ -585,14 +576,13 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
       z.add(vc, GR * 8);
       z.add(vf, GR * 8, 0xFFFFFFFFu);
     }
-    z.copy(d_own + 2, mx, 8);
-    z.copy(d_base, base, (2 * (size_t)W + 2) * 8);
-    z.copy(d_seg, seg, ((size_t)W + 1) * 8);
-    launch_zero_regions(z, s);
+    launch_zero_regions(z, s);  // (region bases and the max offset: written by the scatter's block 0)
   }
   // 1. pack into the fixed regions (this rank's pass flags and region overflow
   // into its flag word) and exchange them whole
-  const MergeSelf self{(uint32_t)R, recv_rows, recv_bytes};
+  // + the fixed-region bases per source (rows | bytes), the send-row starts per
+  // owner (dense id return) and this rank's max first offset, from block 0
+  const MergeSelf self{(uint32_t)R, recv_rows, recv_bytes, d_base, d_seg, d_own, im.max_end};
   launch_owner_scatter(im.cols.k0, im.cols.k1, im.cols.cnt, im.cols.first, im.cols.sref_off, im.cols.sref_len,
                        im.cols_arena, nb, (uint32_t)W, nullptr, d_cur, send_rows, send_bytes, send_pos, s, dn, Cr, Cb,
                        reinterpret_cast<uint32_t*>(d_own + 1), pass_flags, im.cols.occ,

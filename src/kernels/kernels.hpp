@@ -388,6 +388,13 @@ struct MergeSelf {
   uint32_t rank;
   MRow* rows;      // the receive row buffer
   uint8_t* bytes;  // the receive byte buffer
+  // planned-merge words the scatter's block 0 writes (nullable): region bases
+  // per source (rows p * reg_rows | bytes p * reg_bytes, p <= W), send-row
+  // starts per owner, and this rank's max first offset into quad[2]
+  uint64_t* base;
+  uint64_t* seg;
+  unsigned long long* quad;
+  uint64_t max_end;
 };
 void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
                           const uint64_t* soff, const uint32_t* slen, const uint8_t* arena, uint64_t n, uint32_t W,

@@ -157,6 +157,14 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
     const uint32_t f = (rerun ? 1u : 0u) | (pass_flags[FLAG_ARENA_OVF] ? 2u : 0u);
     if (f) atomicOr(ovf, f);
   }
+  if (self.base && blockIdx.x == 0) {  // planned: the fixed-region words (no host copies in the zeroing launch)
+    for (uint32_t p = threadIdx.x; p <= W; p += blockDim.x) {
+      self.base[p] = p * reg_rows;
+      self.base[W + 1 + p] = p * reg_bytes;
+      self.seg[p] = p * reg_rows;
+    }
+    if (threadIdx.x == 0) self.quad[2] = self.max_end;
+  }
   if (dn) n = *dn;
   if (r0 >= n) return;
   const bool fixed = reg_rows != 0;
@@ -540,7 +548,7 @@ void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t
                           uint32_t* send_pos, hipStream_t s, const uint64_t* dn, uint64_t reg_rows, uint64_t reg_bytes,
                           uint32_t* ovf, const uint32_t* pass_flags, const uint32_t* occ, unsigned long long* nvalid,
                           const MergeSelf* self) {
-  const MergeSelf me = self ? *self : MergeSelf{~0u, nullptr, nullptr};
+  const MergeSelf me = self ? *self : MergeSelf{~0u, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
   static_assert(TAB_SLOTS % dev::OWN_ROWS_PER_BLOCK == 0, "a scatter block stays inside one table bucket");
   const uint64_t blocks = (n + dev::OWN_ROWS_PER_BLOCK - 1) / dev::OWN_ROWS_PER_BLOCK;
   if (n)

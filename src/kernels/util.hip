@@ -50,7 +50,8 @@ void launch_zero_regions(const ZeroList& z, hipStream_t s) {
   WC_CHECK(z.n <= ZERO_MAX_REGIONS && z.nc <= ZERO_MAX_COPIES, "launch_zero_regions: too many regions");
   uint64_t most = 0;
   for (int r = 0; r < z.n; ++r) most = z.words[r] > most ? z.words[r] : most;
-  const uint64_t blocks = std::min<uint64_t>(256, std::max<uint64_t>(1, (most / 4 + 255) / 256));
+  // up to 4 blocks per CU: a merge list fills ~10 MB (owner table, padding rows)
+  const uint64_t blocks = std::min<uint64_t>(1024, std::max<uint64_t>(1, (most / 4 + 255) / 256));
   hipLaunchKernelGGL(dev::wc_zero_regions, dim3((unsigned)blocks), dim3(256), 0, s, z);
 }
 
