@@ -1,9 +1,9 @@
-// sort.hip — stable LSD radix sort of (u64 key, u32 value) pairs + small
+// sort.hip — the first-occurrence output order (the reference gets that order
+// for free from its serial append, /root/reference/main.cu:97-104): the
+// three-launch sample sort (up to 400k keys), ranks from a bitmap of first
+// offsets (above), the stable LSD radix sort of (u64 key, u32 value) pairs
+// (fallbacks; also the sort-based-reduce A/B, tools/sort_vs_hash.py), and small
 // column kernels used by finalisation and the multi-GPU merge.
-//
-// Used for: first-occurrence output order (the reference gets that order for
-// free from its serial append, /root/reference/main.cu:97-104) and the
-// sort-based-reduce A/B (tools/sort_vs_hash.py).
 //
 // Onesweep form: ONE histogram launch counts the digits of every pass
 // (wc_os_hist: per-block LDS histograms, one global add per digit), then ONE
