@@ -85,6 +85,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   if (const char* e = std::getenv("WC_RED_Q")) red_q_force = (uint32_t)std::atoi(e);    // sweeps only
   {  // split-reduce partial tables: one per reduce block when buckets < CUs
     part_blocks = std::max<uint32_t>(n_cu, 256);
+    if (red_q_force) part_blocks = std::max<uint32_t>(part_blocks, 512u * red_q_force);  // sweeps: Q above 512 buckets
     const size_t rows = (size_t)part_blocks * TAB_SLOTS;
     part_mem.reserve(rows * (5 * 8 + 4) + part_blocks * 8 + rows * 12 + 16 * 256);
     part.k0 = part_mem.take_n<uint64_t>(rows);
