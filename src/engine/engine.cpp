@@ -973,6 +973,14 @@ void Engine::reset() {
   // slice holds (reduce / compact / split never read such a slice)
   im.pend.active = false;  // an unchecked pass of the previous job is discarded with it
   im.drop_reduce_bits();
+  // WC_STAMPS_PER_JOB=1 (diagnostics): the map / reduce stamp sums printed at
+  // teardown cover the last job only (the first job's table growth excluded)
+  static const bool stamps_per_job = std::getenv("WC_STAMPS_PER_JOB") && std::atoi(std::getenv("WC_STAMPS_PER_JOB"));
+  if (stamps_per_job && im.d_stamps) {
+    WC_HIP_CHECK(hipMemsetAsync(im.d_stamps, 0, MAP_STAMP_N * 8, im.s));
+    WC_HIP_CHECK(hipMemsetAsync(im.d_red_stamps, 0, RED_STAMP_N * 8, im.s));
+    im.blocks_stamped = 0;
+  }
   im.pass_pub_pending = false;
   // no API call: the next pass's zeroing launch clears occupancy + arena cursor
   // (apply_reset does it first for anything else that reads the table)
