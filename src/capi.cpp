@@ -653,7 +653,7 @@ int wc_h2d_bench(int device, int node, uint64_t bytes, int reps, double* gbps, i
                                  bind.active() ? hipHostMallocNumaUser : hipHostMallocDefault));
       std::memset(h, 0x20, bytes);
     }
-    WC_HIP_CHECK(hipMalloc(&d, bytes));
+    wc::dev_malloc(&d, bytes);
     hipStream_t s;
     WC_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     WC_HIP_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s));
@@ -757,6 +757,10 @@ wc_result* wc_virtual_bench(const wc_options* o, int ranks, int device, uint64_t
     return nullptr;
   }
   const uint64_t seg = 1024, nseg = bytes / seg;
+  // tests only: the LAST rank's validation job counts this many more segments
+  // than the timed jobs (the stream stays contiguous: [0, (ranks * nseg + grow) * seg)),
+  // so it outgrows the planned merge's learned caps
+  const uint64_t grow = std::getenv("WC_VB_GROW_SEGS") ? std::strtoull(std::getenv("WC_VB_GROW_SEGS"), nullptr, 10) : 0;
   std::vector<std::thread> th;
   for (int r = 0; r < ranks; ++r) {
     th.emplace_back([&, r] {
@@ -764,7 +768,8 @@ wc_result* wc_virtual_bench(const wc_options* o, int ranks, int device, uint64_t
         wc::Options opt = to_opts(o);
         opt.device = device;
         wc::Engine eng(opt);
-        const uint8_t* d = eng.synth_device(nseg * seg, (uint64_t)r * nseg, spec_of(seed, vocab, zipf, long_frac));
+        const uint64_t vseg = nseg + (r == ranks - 1 ? grow : 0);  // the validation job's segments
+        const uint8_t* d = eng.synth_device(vseg * seg, (uint64_t)r * nseg, spec_of(seed, vocab, zipf, long_frac));
         wc::Comm* c = comms[r].get();
         auto step = [&] {
           eng.reset();
@@ -782,7 +787,7 @@ wc_result* wc_virtual_bench(const wc_options* o, int ranks, int device, uint64_t
         const double ms = (wc::now_seconds() - t0) * 1e3 / (steps > 0 ? steps : 1);
         const wc::Stats st = eng.stats();
         eng.reset();
-        eng.count_device(d, nseg * seg, nseg * seg, (uint64_t)r * nseg * seg, ' ');
+        eng.count_device(d, vseg * seg, vseg * seg, (uint64_t)r * nseg * seg, ' ');
         wc::KeyTable t = eng.result(c, false);
         const wc::Stats& st2 = eng.stats();
         double* v = out + 10 * (size_t)r;
@@ -819,7 +824,11 @@ wc_result* wc_loopback_count(const uint8_t* text, uint64_t n, int ranks, const i
   std::vector<std::string> errs(ranks);
   std::vector<wc::KeyTable> tables(ranks);
   std::vector<std::unique_ptr<wc::Comm>> comms;
-  if (guard([&] { comms = wc::make_loopback_comms(ranks); }) != 0) {
+  if (guard([&] {
+        std::vector<int> devs;
+        if (devices) devs.assign(devices, devices + ranks);
+        comms = wc::make_loopback_comms(ranks, devs);
+      }) != 0) {
     delete out;
     return nullptr;
   }
@@ -837,7 +846,7 @@ wc_result* wc_loopback_count(const uint8_t* text, uint64_t n, int ranks, const i
           // speculatively behind it (merge_cols_speculative)
           const uint64_t len = sr.end - sr.begin;
           WC_HIP_CHECK(hipSetDevice(opt.device));
-          WC_HIP_CHECK(hipMalloc(&d, len + 64));
+          wc::dev_malloc(&d, len + 64);
           WC_HIP_CHECK(hipMemcpy(d, text + sr.begin, len, hipMemcpyHostToDevice));
           eng.count_device(d, len, len, sr.begin, sr.begin ? text[sr.begin - 1] : ' ');
         } else if (sr.end > sr.begin) {

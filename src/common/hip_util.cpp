@@ -12,6 +12,26 @@ namespace wc {
 
 void fail(const std::string& msg) { throw Error(msg); }
 
+int poison_level() {
+  static const int v = std::getenv("WC_POISON") ? std::atoi(std::getenv("WC_POISON")) : 0;
+  return v;
+}
+
+namespace {
+void poison(void* p, size_t bytes) {
+  if (!p || !bytes) return;
+  WC_HIP_CHECK(hipDeviceSynchronize());  // nothing queued still uses the region (arena reuse)
+  WC_HIP_CHECK(hipMemset(p, 0xA5, bytes));
+  WC_HIP_CHECK(hipDeviceSynchronize());
+}
+}  // namespace
+
+void dev_malloc(void** p, size_t bytes) {
+  *p = nullptr;
+  WC_HIP_CHECK(hipMalloc(p, bytes));
+  if (poison_level() >= 1) poison(*p, bytes);
+}
+
 DeviceArena::~DeviceArena() {
   if (base_) (void)hipFree(base_);
 }
@@ -24,8 +44,13 @@ void DeviceArena::reserve(size_t bytes) {
   if (base_) WC_HIP_CHECK(hipFree(base_));
   base_ = nullptr;
   cap_ = used_ = 0;
-  WC_HIP_CHECK(hipMalloc(&base_, bytes));
+  dev_malloc(&base_, bytes);
   cap_ = bytes;
+}
+
+void DeviceArena::reset() {
+  if (poison_level() >= 2 && used_) poison(base_, used_);
+  used_ = 0;
 }
 
 void* DeviceArena::take(size_t bytes, size_t align) {

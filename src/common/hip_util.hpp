@@ -33,6 +33,22 @@ struct Error : std::runtime_error {
                             std::to_string(__LINE__));                                          \
   } while (0)
 
+// Debug mode WC_POISON=1 (a test switch, off by default): every device
+// allocation of the engine, the merge and the communicators is filled with
+// the byte 0xA5 when it is made, and with WC_POISON=2 every DeviceArena region
+// also when the arena is reset for reuse — so no kernel or host path can
+// silently depend on fresh memory reading as zeros (the reference's own bug
+// class: dev_pairs never initialised, main.cu:144).
+int poison_level();
+// hipMalloc + (WC_POISON) the fill, device-synchronous.
+void dev_malloc(void** p, size_t bytes);
+template <class T>
+inline void dev_malloc(T** p, size_t bytes) {
+  void* v = nullptr;
+  dev_malloc(&v, bytes);
+  *p = static_cast<T*>(v);
+}
+
 // Bump allocator over ONE hipMalloc: nothing in the hot path allocates
 // (cdna_hip_programming.md Guideline 9).
 class DeviceArena {
@@ -47,7 +63,7 @@ class DeviceArena {
   T* take_n(size_t n) {
     return static_cast<T*>(take(n * sizeof(T)));
   }
-  void reset() { used_ = 0; }
+  void reset();  // WC_POISON=2: the regions handed out so far are poisoned
   size_t capacity() const { return cap_; }
   size_t used() const { return used_; }
 

@@ -75,7 +75,7 @@ class RcclComm final : public Comm {
  public:
   RcclComm(ncclComm_t c, int rank, int size, int device) : c_(c), rank_(rank), size_(size), dev_(device) {
     WC_HIP_CHECK(hipSetDevice(device));
-    WC_HIP_CHECK(hipMalloc(&scratch_, 8));
+    dev_malloc(&scratch_, 8);
   }
   ~RcclComm() override {
     (void)hipFree(scratch_);
@@ -299,16 +299,23 @@ class LoopbackComm final : public Comm {
       std::this_thread::yield();
     }
     if (hub_->is_aborted()) fail("loopback peer failed: " + hub_->why);
+    since_sync_ = 0;
   }
 
  private:
-  // Next sequence number and this rank's metadata slot for it (reused
-  // LB_RING collectives later: every rank has enqueued that collective's
-  // waits by then, and the metadata is read by kernels queued before ours).
+  // Next sequence number and this rank's metadata slot for it.  The slot's previous collective was begun LB_RING collectives ago: if this
+  // rank has not completed a sync() since then, the peers' transfer kernels of
+  // that collective (which read this metadata when they RUN, not when they are
+  // enqueued) may still be queued — wait for its done events before
+  // overwriting it.  After a sync() every earlier collective is complete on
+  // every peer (this rank's stream waited for all their done events).
   LbMeta& begin() {
     seq_ = (uint32_t)(seq_ + 1);
     slot_ = seq_ % LB_RING;
-    return hub_->sh->meta[slot_ * hub_->n + rank_];
+    Hub& h = *hub_;
+    if (++since_sync_ > (uint32_t)LB_RING)
+      for (int p = 0; p < h.n; ++p) WC_HIP_CHECK(hipEventSynchronize(h.done[(size_t)slot_ * h.n + p]));
+    return h.sh->meta[slot_ * h.n + rank_];
   }
   void enqueue(uint32_t kind, uint64_t count, uint32_t op, uint32_t root, hipStream_t s) {
     Hub& h = *hub_;
@@ -326,6 +333,7 @@ class LoopbackComm final : public Comm {
   std::shared_ptr<Hub> hub_;
   int rank_;
   uint32_t seq_ = 0, slot_ = 0;
+  uint32_t since_sync_ = 0;  // collectives begun since this rank's last completed sync()
 };
 
 }  // namespace
@@ -356,7 +364,23 @@ std::vector<std::unique_ptr<Comm>> make_rccl_comms_all(const std::vector<int>& d
   return out;
 }
 
-std::vector<std::unique_ptr<Comm>> make_loopback_comms(int n) {
+std::vector<std::unique_ptr<Comm>> make_loopback_comms(int n, const std::vector<int>& devices) {
+  WC_CHECK(devices.empty() || (int)devices.size() == n, "loopback: one device per rank");
+  int prev = 0;
+  WC_HIP_CHECK(hipGetDevice(&prev));
+  for (int a : devices)
+    for (int b : devices) {
+      if (a == b) continue;
+      int ok = 0;
+      WC_HIP_CHECK(hipDeviceCanAccessPeer(&ok, a, b));
+      WC_CHECK(ok, "loopback ranks on devices " + std::to_string(a) + " and " + std::to_string(b) +
+                       ": no peer access between them (the transfer kernel reads peer buffers directly)");
+      WC_HIP_CHECK(hipSetDevice(a));
+      const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+      if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();  // not an error: clear it
+      else WC_HIP_CHECK(e);
+    }
+  WC_HIP_CHECK(hipSetDevice(prev));
   auto hub = std::make_shared<Hub>(n);
   std::vector<std::unique_ptr<Comm>> out;
   for (int r = 0; r < n; ++r) out.emplace_back(new LoopbackComm(hub, r));

@@ -81,6 +81,9 @@ std::vector<std::unique_ptr<Comm>> make_rccl_comms_all(const std::vector<int>& d
 // In-process virtual ranks (call each rank's methods from its own thread;
 // every rank's stream on one device, or on devices with peer access enabled:
 // the transfer kernel reads the peers' buffers directly).
-std::vector<std::unique_ptr<Comm>> make_loopback_comms(int n);
+// devices (optional, one per rank): distinct devices must be peer-accessible —
+// the transfer kernel reads the peers' buffers directly — and peer access is
+// enabled between every pair here (refused with an error when unsupported).
+std::vector<std::unique_ptr<Comm>> make_loopback_comms(int n, const std::vector<int>& devices = {});
 
 }  // namespace wc

@@ -156,6 +156,7 @@ struct OwnerPlan {
   uint64_t gmax_end = 0;
   bool any_flags = false;   // some rank's last pass needs recovery (all ranks redo)
   bool any_arena = false;   // some rank's key arena overflowed (all ranks fail)
+  bool count_mismatch = false;  // some rank's row count != its owner-count sum (all ranks fail)
   std::vector<uint64_t> rank_rows, rank_bytes;
   uint64_t total_rows = 0, Gmax = 0, GBmax = 0;  // rows / bytes of all ranks (bounds of the merged table)
   std::vector<size_t> so_r, sb_r, so_b, sb_b, ro_r, rb_r, ro_b, rb_b;  // byte offsets / sizes
@@ -174,7 +175,7 @@ void plan_enqueue(Engine::Impl& im, Comm& comm, uint64_t n, const uint64_t* dn, 
   P.R = comm.rank();
   const int W = P.W;
   WC_CHECK(W <= (int)MERGE_MAX_RANKS, "merge supports at most 64 ranks");
-  P.C = 2 * (size_t)W + 2;
+  P.C = 2 * (size_t)W + 3;  // per owner (rows, bytes) | max offset | pass flags | row count
   const size_t C = P.C;
   DeviceArena& S = im.merge_small;  // small buffers: own arena
   S.reserve(((size_t)W * C + 2 * C + 16) * 8 + 8 * 1024);
@@ -188,7 +189,9 @@ void plan_enqueue(Engine::Impl& im, Comm& comm, uint64_t n, const uint64_t* dn, 
   z.add(P.d_cnt + 2 * W + 1, (2 * C - 2 * (size_t)W - 1) * 8);
   z.copy(P.d_cnt + 2 * W, mx, 8);
   launch_zero_regions(z, s);
-  launch_owner_count(im.cols.k0, im.cols.k1, im.cols.sref_len, n, dn, pass_flags, (uint32_t)W, P.d_cnt, s);
+  static const int fault_rank = std::getenv("WC_MERGE_FAULT_COUNT") ? std::atoi(std::getenv("WC_MERGE_FAULT_COUNT")) : -1;
+  launch_owner_count(im.cols.k0, im.cols.k1, im.cols.sref_len, n, dn, pass_flags, (uint32_t)W, P.d_cnt, s,
+                     P.R == fault_rank ? 1u : 0u);
   comm.allgather(P.d_cnt, P.d_all, C * 8, s);
 }
 
@@ -209,6 +212,7 @@ void plan_finish(OwnerPlan& P) {
       P.rank_rows[r] += P.all[(size_t)r * C + 2 * p];
       P.rank_bytes[r] += P.all[(size_t)r * C + 2 * p + 1];
     }
+    if (P.all[(size_t)r * C + 2 * W + 2] != P.rank_rows[r]) P.count_mismatch = true;
     P.total_rows += P.rank_rows[r];
     P.GBmax += P.rank_bytes[r];
   }
@@ -242,6 +246,7 @@ OwnerPlan plan_owners(Engine::Impl& im, Comm& comm) {
   WC_HIP_CHECK(hipMemcpyAsync(P.all.data(), P.d_all, P.all.size() * 8, hipMemcpyDeviceToHost, im.s));
   comm.sync(im.s);
   plan_finish(P);
+  if (P.count_mismatch) fail("owner plan: a rank's key count != its owner row counts");  // every rank sees it
   return P;
 }
 
@@ -522,8 +527,14 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
   unsigned long long* d_own = d_owns + 4 * (size_t)R;  // merged rows | flags | max offset | -, gathered in place
   unsigned long long* d_on = take_aligned<unsigned long long>(S, 1);
   im.d_merge_flags = take_aligned<uint32_t>(S, 2);
-  // the key width the finalize's order is sized for: every rank's first offsets must fit it
-  const uint64_t key_bound = std::max(im.max_end, cp.gmax_end);
+  // The bound every rank's gathered max first offset is checked against.  It
+  // must be IDENTICAL on every rank — each rank decides "redo" from it on its
+  // own, and a rank that disagrees skips the redo's collectives (a hang):
+  // the caps' global max end (the last exact merge's), not this rank's own
+  // max_end.  It is <= the width rank 0's order is sized for below
+  // (max(max_end, gmax_end)), so a job that outgrows it redoes exactly, on
+  // every rank together.
+  const uint64_t key_bound = cp.gmax_end;
 
   DeviceArena& A = im.merge_mem;
   const uint64_t RR = (uint64_t)W * Cr, RB = (uint64_t)W * Cb, GR = (uint64_t)W * Gr;
@@ -798,14 +809,17 @@ bool merge_cols_speculative(Engine::Impl& im, Comm& comm, bool all_ranks) {
   }
   P.all.assign(hp, hp + words);
   plan_finish(P);
-  // a rank whose key arena overflowed would throw in complete_pass while the
-  // others entered the recovery's collectives: every rank fails here instead
+  // Decisions that end or redo the job come from the gathered matrix only, so
+  // every rank takes them together: a rank whose key arena overflowed would
+  // throw in complete_pass while the others entered the recovery's
+  // collectives, and a row count that disagrees with its owner counts (a
+  // compaction bug) used to throw on that rank alone — both fail every rank here
   if (P.any_arena)
     fail("key arena exhausted on a rank (" + std::to_string(im.opt.arena_bytes) + " bytes each); raise arena_bytes");
+  if (P.count_mismatch) fail("speculative compaction: a rank's key count != its owner row counts");
   const bool clean = im.complete_pass(p.text, p.len, p.avail, p.base, p.prev, p.rb, p.blocks, true);
   if (!clean || P.any_flags) return false;  // every rank sees the same flags: all redo
-  im.cols.n = hp[words];
-  WC_CHECK(im.cols.n == P.rank_rows[P.R], "speculative compaction: key count != owner row counts");
+  im.cols.n = P.all[(size_t)P.R * P.C + 2 * (size_t)P.W + 2];
   im.st.keys = im.cols.n;
   im.st.log2_buckets = t.log2_buckets;
   merge_cols_owner(im, comm, all_ranks, im.opt.merge_mode == 1, P);

@@ -35,7 +35,7 @@ void TableStore::alloc(uint32_t log2_buckets) {
   mem = nullptr;
   const size_t nb = (size_t)1 << log2_buckets, n = nb * TAB_SLOTS;
   const size_t bytes = n * (5 * sizeof(uint64_t) + sizeof(uint32_t)) + nb * sizeof(uint32_t) + 1024;
-  WC_HIP_CHECK(hipMalloc(&mem, bytes));
+  dev_malloc(&mem, bytes);
   uint8_t* p = static_cast<uint8_t*>(mem);
   auto take = [&](size_t b) {
     uint8_t* r = p;
@@ -73,11 +73,11 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   if (const char* e = std::getenv("WC_HOT_RESAMPLE_EVERY")) hot_resample_every = (uint32_t)std::atoi(e);
   k1_mask = k1_hash_mask(opt.k1_hash_bits);
   if (const char* e = std::getenv("WC_MAP_STAMPS"); e && std::atoi(e)) {
-    WC_HIP_CHECK(hipMalloc(&d_stamps, MAP_STAMP_N * 8));
+    dev_malloc(&d_stamps, MAP_STAMP_N * 8);
     WC_HIP_CHECK(hipMemset(d_stamps, 0, MAP_STAMP_N * 8));
-    WC_HIP_CHECK(hipMalloc(&d_red_stamps, RED_STAMP_N * 8));
+    dev_malloc(&d_red_stamps, RED_STAMP_N * 8);
     WC_HIP_CHECK(hipMemset(d_red_stamps, 0, RED_STAMP_N * 8));
-    WC_HIP_CHECK(hipMalloc(&d_blk, (size_t)map_blocks * 4 * 8));
+    dev_malloc(&d_blk, (size_t)map_blocks * 4 * 8);
     WC_HIP_CHECK(hipMemset(d_blk, 0, (size_t)map_blocks * 4 * 8));
   }
 
@@ -134,17 +134,17 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   hot.cand_n = hot_mem.take_n<uint32_t>(HOT_PARTS);
   hot.maxb = map_blocks;
   hot.long_bytes = hot_mem.take_n<uint8_t>((size_t)HOT_PARTS * HOT_PART_TOP * 64);
-  WC_HIP_CHECK(hipMalloc(&d_ctr, sizeof(DevCounters)));
+  dev_malloc(&d_ctr, sizeof(DevCounters));
   WC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_ctr), sizeof(DevCounters), hipHostMallocDefault));
   h_pass_seq.resize(256);
   std::memset(h_pass_seq.data(), 0, h_pass_seq.size());
   const size_t maxb = (size_t)1 << opt.max_log2_tab_buckets;
-  WC_HIP_CHECK(hipMalloc(&d_bucket_ovf, maxb * sizeof(uint32_t)));
-  WC_HIP_CHECK(hipMalloc(&d_bucket_en, maxb));
-  WC_HIP_CHECK(hipMalloc(&d_arena, std::max<uint64_t>(opt.arena_bytes, 16)));
-  WC_HIP_CHECK(hipMalloc(&d_arena_cursor, sizeof(unsigned long long)));
-  WC_HIP_CHECK(hipMalloc(&d_fo_hist, FO_LOGBINS * sizeof(uint32_t)));
-  WC_HIP_CHECK(hipMalloc(&d_fo_hist_cols, FO_LOGBINS * sizeof(uint32_t)));
+  dev_malloc(&d_bucket_ovf, maxb * sizeof(uint32_t));
+  dev_malloc(&d_bucket_en, maxb);
+  dev_malloc(&d_arena, std::max<uint64_t>(opt.arena_bytes, 16));
+  dev_malloc(&d_arena_cursor, sizeof(unsigned long long));
+  dev_malloc(&d_fo_hist, FO_LOGBINS * sizeof(uint32_t));
+  dev_malloc(&d_fo_hist_cols, FO_LOGBINS * sizeof(uint32_t));
   WC_HIP_CHECK(hipMemsetAsync(d_fo_hist_cols, 0, FO_LOGBINS * sizeof(uint32_t), s));
   for (int i = 0; i < 2; ++i) {
     WC_HIP_CHECK(hipEventCreateWithFlags(&ev_h2d[i], hipEventDisableTiming));
@@ -611,7 +611,7 @@ unsigned long long* Engine::Impl::ensure_bitmap() {
     if (d_bm) WC_HIP_CHECK(hipFree(d_bm));  // waits for the device: nothing in flight reads it
     d_bm = nullptr;
     const size_t w = words + words / 4;  // room for a growing input
-    WC_HIP_CHECK(hipMalloc(&d_bm, w * 8));
+    dev_malloc(&d_bm, w * 8);
     WC_HIP_CHECK(hipMemsetAsync(d_bm, 0, w * 8, s));  // once: every bitmap_order leaves it zeroed
     bm_words = w;
   }

@@ -84,11 +84,18 @@ FileSource::~FileSource() {
 }
 
 namespace {
-// Persistent reader threads: created on first use (they inherit the caller's
-// CPU mask — the engine binds its streaming loop to the GPU's NUMA node) and
-// woken per read.  Threads spawned per 64 MiB piece cost tens of us each and
-// capped the split at 4 (16 MiB slices); the stream read at 54 GB/s against
-// 75 GB/s standalone (profiles/r4_session3.md §10).
+// Persistent reader threads, one pool PER CALLING THREAD (thread_local below):
+// the CLI runs one streaming thread per GPU, each bound to its GPU's NUMA node,
+// and its pool's workers inherit that CPU mask; concurrent callers never share
+// a pool.  Threads spawned per 64 MiB piece cost tens of us each and capped the
+// split at 4 (16 MiB slices); the stream read at 54 GB/s against 75 GB/s
+// standalone (profiles/r4_session3.md §10).
+//
+// Task claims go through ONE 64-bit ticket = generation << 32 | next index,
+// advanced by compare-exchange only while its generation is the caller's: a
+// worker still inside help() of an earlier run can never claim (or count) a
+// task of the next run, and run() returns only when every task of its own
+// generation has finished (the tasks' captures live on the caller's stack).
 class ReadPool {
  public:
   explicit ReadPool(unsigned n) {
@@ -104,27 +111,35 @@ class ReadPool {
   }
   // f(0) .. f(tasks - 1) over the workers and the caller; returns when all ran.
   void run(unsigned tasks, const std::function<void(unsigned)>& f) {
+    std::lock_guard<std::mutex> one(run_m_);  // one run at a time (re-entry from another thread waits)
+    uint64_t gen;
     {
       std::lock_guard<std::mutex> g(m_);
       job_ = &f;
-      ntasks_.store(tasks);
-      done_.store(0);  // before next_: a worker can take a task as soon as next_ resets
-      next_.store(0);
-      ++gen_;
+      ntasks_ = tasks;
+      done_.store(0);
+      gen = ++gen_;
+      ticket_.store(gen << 32);
     }
     cv_.notify_all();
-    help();
+    help(gen);
     std::unique_lock<std::mutex> lk(m_);
-    done_cv_.wait(lk, [&] { return done_.load() == ntasks_.load(); });
+    done_cv_.wait(lk, [&] { return done_.load() == tasks; });
+    job_ = nullptr;
   }
 
  private:
-  void help() {
+  void help(uint64_t gen) {
     for (;;) {
-      const unsigned i = next_.fetch_add(1);
-      if (i >= ntasks_.load()) return;
-      (*job_)(i);
-      if (done_.fetch_add(1) + 1 == ntasks_.load()) {
+      uint64_t t = ticket_.load();
+      unsigned i;
+      do {
+        if ((t >> 32) != gen) return;  // a later run: not ours
+        i = (unsigned)t;
+        if (i >= ntasks_) return;      // ntasks_ is this generation's while t's generation is
+      } while (!ticket_.compare_exchange_weak(t, t + 1));
+      (*job_)(i);  // the run cannot end (nor job_ change) before this task is counted
+      if (done_.fetch_add(1) + 1 == ntasks_) {
         std::lock_guard<std::mutex> g(m_);
         done_cv_.notify_all();
       }
@@ -133,20 +148,23 @@ class ReadPool {
   void loop() {
     uint64_t seen = 0;
     for (;;) {
+      uint64_t gen;
       {
         std::unique_lock<std::mutex> lk(m_);
         cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
         if (stop_) return;
-        seen = gen_;
+        gen = seen = gen_;
       }
-      help();
+      help(gen);
     }
   }
   std::vector<std::thread> th_;
-  std::mutex m_;
+  std::mutex m_, run_m_;
   std::condition_variable cv_, done_cv_;
   const std::function<void(unsigned)>* job_ = nullptr;
-  std::atomic<unsigned> ntasks_{0}, next_{~0u}, done_{0};
+  std::atomic<uint64_t> ticket_{0};
+  std::atomic<unsigned> done_{0};
+  std::atomic<unsigned> ntasks_{0};
   uint64_t gen_ = 0;
   bool stop_ = false;
 };
@@ -185,7 +203,7 @@ uint64_t pread_parallel(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
   if (t == 1) {
     task(0);
   } else {
-    static ReadPool pool(kThreads - 1);  // + the caller
+    thread_local ReadPool pool(kThreads - 1);  // + the caller; this thread's own pool (its CPU mask)
     pool.run(t, task);
   }
   uint64_t total = 0;  // contiguous prefix: a short slice ends the read

@@ -377,9 +377,11 @@ constexpr uint32_t MERGE_MAX_RANKS = 64;
 // V / W x W; the owner path costs one more exchange + host sync (~50 us at one
 // rank, tools/merge_cost.py) — the insert + compact of ~2.5e5 rows.
 constexpr uint64_t MERGE_ROOT_MAX_ROWS = 1ull << 18;
-// counts of rows [0, n) — or [0, *dn) with n a bound — and (pass_flags) the pass's recovery flags at 2W + 1
+// counts of rows [0, n) — or [0, *dn) with n a bound — (pass_flags) the pass's recovery flags at 2W + 1,
+// and the row count itself (+ count_bias, a fault-injection switch) at 2W + 2
 void launch_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* slen, uint64_t n, const uint64_t* dn,
-                        const uint32_t* pass_flags, uint32_t W, unsigned long long* counts, hipStream_t s);
+                        const uint32_t* pass_flags, uint32_t W, unsigned long long* counts, hipStream_t s,
+                        uint32_t count_bias = 0);
 // send_pos (nullable): row index of each local key; dn: device-side row count
 // (n the bound); reg_rows > 0: planned mode — owner o's rows / bytes in fixed
 // regions of reg_rows rows / reg_bytes bytes (counts unused), overflow -> *ovf

@@ -102,10 +102,14 @@ __device__ __forceinline__ unsigned long long wave_owner_add(unsigned long long*
 // rank then fails the job together instead of one rank throwing alone).
 __global__ void __launch_bounds__(256) wc_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* slen,
                                                       uint64_t n, const uint64_t* dn, const uint32_t* pass_flags,
-                                                      uint32_t W, unsigned long long* counts) {
+                                                      uint32_t W, unsigned long long* counts, uint32_t count_bias) {
   __shared__ unsigned long long h[2 * OWN_MAX];
   for (uint32_t i = threadIdx.x; i < 2 * W; i += blockDim.x) h[i] = 0;
   if (dn) n = *dn;
+  // the row count counted here, next to the owner counts: every rank checks
+  // every rank's count against its owner-count sum from the gathered matrix
+  // (count_bias: fault injection, WC_MERGE_FAULT_COUNT)
+  if (blockIdx.x == 0 && threadIdx.x == 0) counts[2 * W + 2] = n + count_bias;
   if (pass_flags && blockIdx.x == 0 && threadIdx.x == 0) {
     const uint32_t rerun = pass_flags[FLAG_REGION_OVF] | pass_flags[FLAG_TABLE_OVF];
     const unsigned long long f = (rerun ? 1ull : 0ull) | (pass_flags[FLAG_ARENA_OVF] ? 2ull : 0ull);
@@ -537,10 +541,11 @@ void launch_mrow_regions_to_cols(const MRow* rows, uint32_t W, uint64_t reg_merg
 }
 
 void launch_owner_count(const uint64_t* k0, const uint64_t* k1, const uint32_t* slen, uint64_t n, const uint64_t* dn,
-                        const uint32_t* pass_flags, uint32_t W, unsigned long long* counts, hipStream_t s) {
+                        const uint32_t* pass_flags, uint32_t W, unsigned long long* counts, hipStream_t s,
+                        uint32_t count_bias) {
   // with a device-side count the grid is sized for the bound (grid-stride inside)
   hipLaunchKernelGGL(dev::wc_owner_count, dev::mgrid(n ? n : 1), dim3(256), 0, s, k0, k1, slen, n, dn, pass_flags, W,
-                     counts);
+                     counts, count_bias);
 }
 void launch_owner_scatter(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
                           const uint64_t* soff, const uint32_t* slen, const uint8_t* arena, uint64_t n, uint32_t W,

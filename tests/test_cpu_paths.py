@@ -224,3 +224,44 @@ def test_parallel_file_reader(tmp_path, piece):
                                      out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(got)))
         assert got.value == end - begin
         assert np.array_equal(out, data[begin:end])
+
+
+def test_parallel_file_reader_concurrent_callers(tmp_path):
+    """Several threads stream through FileSource at once (the CLI's one
+    streaming thread per GPU): each caller has its own reader pool
+    (src/io/source.cpp, thread_local) and its tasks are claimed through a
+    generation-tagged ticket, so no caller runs another's slices, returns early
+    or hangs.  ctypes drops the GIL for the native calls: the reads overlap."""
+    import ctypes
+    import threading
+
+    from cuda_mapreduce_amd.ops._lib import check, lib
+
+    rng = np.random.default_rng(11)
+    data = rng.integers(0, 256, (48 << 20) + 4321, dtype=np.uint8)
+    path = tmp_path / "f.bin"
+    data.tofile(path)
+    errors = []
+
+    def reader(k):
+        try:
+            for rep in range(6):
+                begin = (k * 5 + rep) * 1_000_003 % (8 << 20)
+                end = len(data) - (k * 7 + rep) * 999_983 % (8 << 20)
+                piece = (4 << 20) * (1 + (k + rep) % 3) + k
+                out = np.zeros(end - begin, np.uint8)
+                got = ctypes.c_uint64(0)
+                check(lib.wc_debug_read_file(str(path).encode(), begin, end, piece,
+                                             out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(got)))
+                assert got.value == end - begin, (k, rep, got.value)
+                assert np.array_equal(out, data[begin:end]), (k, rep)
+        except Exception as ex:  # noqa: BLE001 - surfaced below
+            errors.append(repr(ex))
+
+    th = [threading.Thread(target=reader, args=(k,)) for k in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th), "a reader hung"
+    assert not errors, errors

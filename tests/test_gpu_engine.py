@@ -219,6 +219,56 @@ def test_planned_merge_virtual_ranks(ranks, merge_mode):
 
 
 @pytest.mark.parametrize("merge_mode", [0, 1])
+def test_planned_merge_larger_job_redoes_on_every_rank(merge_mode):
+    """A job larger than the one the planned merge learned its caps from
+    (WC_VB_GROW_SEGS: the last rank's validation job counts 2 MiB more): its
+    max first offset passes the caps' global max end.  Every rank checks the
+    gathered offsets against that SAME bound (dist/merge.cpp key_bound), so all
+    of them redo exactly together — before, ranks whose own max end was lower
+    redid alone and waited in collectives the last rank never joined."""
+    per, grow = 4 << 20, 2048
+    code = (
+        "from cuda_mapreduce_amd import ops\n"
+        f"res, rk = ops.virtual_bench(3, {per}, seed=8, vocab=20000, steps=2, warmup=1, chunk_bytes=2 << 20, "
+        f"merge_mode={merge_mode})\n"
+        f"want = ops.cpu_count_synth(3 * {per} + {grow} * 1024, 0, seed=8, vocab=20000)\n"
+        "assert res.words == want.words and res.counts.tolist() == want.counts.tolist(), 'table'\n"
+        "assert res.first_off.tolist() == want.first_off.tolist(), 'first offsets'\n"
+        "assert rk[0]['merge_redos'] >= 1, rk[0]\n"
+        "print('ok')\n"
+    )
+    env = dict(os.environ, WC_VB_GROW_SEGS=str(grow), WC_COMM_TIMEOUT_S="20")
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, timeout=110)
+    assert out.returncode == 0 and b"ok" in out.stdout, out.stderr.decode()[-2000:]
+
+
+@pytest.mark.parametrize("resident", [True, False])
+def test_loopback_count_mismatch_fails_every_rank(resident):
+    """A rank whose compacted key count disagrees with its owner-count sum
+    (injected: WC_MERGE_FAULT_COUNT=1 biases rank 1's count word) is seen by
+    EVERY rank in the gathered plan matrix, so all of them fail at once — the
+    speculative finalize used to throw on that rank alone while the peers
+    entered the merge's collectives and waited for the watchdog."""
+    code = (
+        "import time\n"
+        "from cuda_mapreduce_amd import ops\n"
+        "text = ops.synth_host(3 << 20, seed=4, vocab=20000)\n"
+        "t0 = time.time()\n"
+        "try:\n"
+        f"    ops.loopback_count(text, 3, chunk_bytes=1 << 20, resident={resident})\n"
+        "    print('no error')\n"
+        "except RuntimeError as ex:\n"
+        "    print('failed', round(time.time() - t0, 2), str(ex)[:200])\n"
+    )
+    env = dict(os.environ, WC_MERGE_FAULT_COUNT="1", WC_COMM_TIMEOUT_S="60")
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, timeout=100)
+    line = out.stdout.decode().strip().splitlines()[-1] if out.stdout.strip() else out.stderr.decode()[-1500:]
+    assert line.startswith("failed"), line
+    assert "key count" in line, line
+    assert float(line.split()[1]) < 5.0, line
+
+
+@pytest.mark.parametrize("merge_mode", [0, 1])
 def test_planned_merge_overflow_redo(merge_mode):
     """Fixed regions too small (WC_MERGE_CAP_ROWS=64, a test switch): every
     planned merge overflows, all ranks see it in the gathered words and redo
