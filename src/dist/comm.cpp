@@ -61,6 +61,37 @@ void Comm::sync(hipStream_t s) {
   WC_HIP_CHECK(hipStreamSynchronize(s));
 }
 
+void Comm::wait_word(const uint32_t* word, uint32_t want, hipStream_t s) {
+  if (failed()) fail("communicator failed earlier: " + failed_);
+  count_host_wait();
+  const double t0 = now_seconds();
+  for (uint64_t it = 1;; ++it) {
+    if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == want) break;
+    if ((it & 0x3FFF) == 0) {
+      const hipError_t q = hipStreamQuery(s);
+      if (q != hipErrorNotReady) {
+        WC_HIP_CHECK(q);
+        if (__atomic_load_n(word, __ATOMIC_ACQUIRE) != want) fail("publish launch completed without its sequence word");
+        break;
+      }
+      std::string why;
+      if (!poll_error(why) && now_seconds() - t0 > timeout_s())
+        why = std::string(backend()) + " collective made no progress for " + std::to_string((int)timeout_s()) +
+              " s (WC_COMM_TIMEOUT_S)";
+      if (!why.empty()) {
+        abort(why);
+        fail(why + "; communicator aborted");
+      }
+    }
+    __builtin_ia32_pause();
+  }
+  std::string why;
+  if (poll_error(why)) {
+    abort(why);
+    fail(why + "; communicator aborted");
+  }
+}
+
 namespace {
 
 ncclRedOp_t to_nccl(RedOp op) {
@@ -141,6 +172,14 @@ class RcclComm final : public Comm {
       }
       std::this_thread::yield();
     }
+  }
+  bool poll_error(std::string& why) override {
+    if (!c_) return false;
+    ncclResult_t ar = ncclSuccess;
+    WC_NCCL_CHECK(ncclCommGetAsyncError(c_, &ar));
+    if (ar == ncclSuccess || ar == ncclInProgress) return false;
+    why = std::string("RCCL async error: ") + ncclGetErrorString(ar);
+    return true;
   }
   void abort(const std::string& why) override {
     Comm::abort(why);
@@ -280,6 +319,11 @@ class LoopbackComm final : public Comm {
     begin();
     enqueue(~0u, 0, 0, 0, s);  // events only
     sync(s);
+  }
+  bool poll_error(std::string& why) override {
+    if (!hub_->is_aborted()) return false;
+    why = "loopback peer failed: " + hub_->why;
+    return true;
   }
   // Watchdog wait, as RcclComm::sync (a failed peer is reported).
   void sync(hipStream_t s) override {

@@ -45,6 +45,12 @@ class Comm {
   // async error, or no progress within timeout_s(), aborts the communicator
   // (ncclCommAbort) and throws instead of hanging the job.
   virtual void sync(hipStream_t s);
+  // Wait for a page-locked word that a publish launch on s stores last
+  // (system-scope release): a host spin wakes within a microsecond of the
+  // store, where sync()'s stream query waits for the completion signal (~20-30
+  // us of GPU idle between merged jobs).  The same watchdog as sync(): the
+  // backend's async error and the timeout are polled while spinning.
+  void wait_word(const uint32_t* word, uint32_t want, hipStream_t s);
   // Mark the communicator failed: later calls throw, and peers blocked in a
   // collective of the loopback backend wake up and throw.
   virtual void abort(const std::string& why) { failed_ = why.empty() ? "aborted" : why; }
@@ -58,6 +64,12 @@ class Comm {
 
  protected:
   Comm();
+  // A failure the backend knows of without waiting (RCCL: ncclCommGetAsyncError;
+  // loopback: a peer aborted) -> true and the reason.
+  virtual bool poll_error(std::string& why) {
+    (void)why;
+    return false;
+  }
   // Called at the top of every collective: throws once the communicator has
   // failed, and implements fault injection — WC_COMM_FAULT=<rank>[:<n>] makes
   // rank <rank> fail its n-th collective (default 1st) as a simulated comm

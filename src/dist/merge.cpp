@@ -715,7 +715,8 @@ bool merge_cols_planned_speculative(Engine::Impl& im, Comm& comm, bool all_ranks
   Range rg("wc_merge_planned_speculative");
   im.planned_pass = im.pend;
   im.pend.active = false;
-  im.flush_pass_publish();  // its counters: read after the merge's last wait
+  // the pass's counter publish stays held back: it rides in the finalize's
+  // last publish (read after that wait) — one launch fewer
   const TableView& t = im.table();
   const size_t nb = (size_t)1 << t.log2_buckets;
   const uint64_t cap = (uint64_t)nb * TAB_SLOTS;

@@ -77,6 +77,9 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
     WC_HIP_CHECK(hipMemset(d_stamps, 0, MAP_STAMP_N * 8));
     dev_malloc(&d_red_stamps, RED_STAMP_N * 8);
     WC_HIP_CHECK(hipMemset(d_red_stamps, 0, RED_STAMP_N * 8));
+    red_blk_n = 16384;  // reduce grids up to this many blocks are profiled
+    dev_malloc(&d_red_blk, red_blk_n * RED_BLK_WORDS * 8);
+    WC_HIP_CHECK(hipMemset(d_red_blk, 0, red_blk_n * RED_BLK_WORDS * 8));
     dev_malloc(&d_blk, (size_t)map_blocks * 4 * 8);
     WC_HIP_CHECK(hipMemset(d_blk, 0, (size_t)map_blocks * 4 * 8));
   }
@@ -235,6 +238,37 @@ Engine::Impl::~Impl() {
     }
     (void)hipFree(d_red_stamps);
   }
+  if (d_red_blk && red_blk_grid) {  // the last reduce launch, block by block (100 MHz realtime ticks -> us)
+    std::vector<unsigned long long> h(red_blk_grid * RED_BLK_WORDS);
+    if (hipMemcpy(h.data(), d_red_blk, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+      struct B { double start, dur; uint32_t b, q; unsigned long long n16, n24, nl; };
+      std::vector<B> v;
+      unsigned long long t0 = ~0ull, t1 = 0;
+      for (size_t i = 0; i < red_blk_grid; ++i) {
+        const unsigned long long* r = &h[i * RED_BLK_WORDS];
+        if (!r[2]) continue;
+        t0 = std::min(t0, r[1]);
+        t1 = std::max(t1, r[2]);
+        v.push_back(B{(double)r[1], (r[2] - r[1]) / 100.0, (uint32_t)r[0], (uint32_t)(r[0] >> 32), r[3] & 0xFFFFFFFFull,
+                      r[3] >> 32, r[4]});
+      }
+      if (!v.empty()) {
+        double sum = 0;
+        for (auto& x : v) sum += x.dur;
+        std::sort(v.begin(), v.end(), [](const B& a, const B& b) { return a.dur > b.dur; });
+        fprintf(stderr, "[wc] reduce blocks (last launch): %zu blocks, span %.1f us, duration mean %.1f max %.1f us\n",
+                v.size(), (t1 - t0) / 100.0, sum / v.size(), v[0].dur);
+        for (size_t i = 0; i < v.size() && i < 8; ++i)
+          fprintf(stderr, "[wc]   #%zu bucket %u q %u: %.1f us from %.1f us, records 16B %llu 24B %llu, LONG %llu\n", i,
+                  v[i].b, v[i].q, v[i].dur, (v[i].start - t0) / 100.0, v[i].n16, v[i].n24, v[i].nl);
+        double m16 = 0, m24 = 0, ml = 0;
+        for (auto& x : v) m16 += x.n16, m24 += x.n24, ml += (double)x.nl;
+        fprintf(stderr, "[wc]   mean records 16B %.0f 24B %.0f LONG %.0f\n", m16 / v.size(), m24 / v.size(),
+                ml / v.size());
+      }
+    }
+  }
+  if (d_red_blk) (void)hipFree(d_red_blk);
   if (registered) (void)hipHostUnregister(const_cast<uint8_t*>(registered));
   if (s) (void)hipStreamDestroy(s);
   if (copy_s) (void)hipStreamDestroy(copy_s);
@@ -333,7 +367,7 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   }
   ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                 avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
-                d_ctr->flags, d_bucket_ovf, nullptr, d_red_stamps, want_hist ? d_fo_hist : nullptr, fo_hist_m,
+                d_ctr->flags, d_bucket_ovf, nullptr, d_red_stamps, red_blk(), want_hist ? d_fo_hist : nullptr, fo_hist_m,
                 bm, bm ? bitmap_order_linecnt(bm, bm_end, 1) : nullptr, bm ? bitmap_order_ctl(bm, bm_end, 1) : nullptr,
                 bm ? (bm_end >> 1) + 1 : 0, 1u, red_q(), part};
   launch_reduce(ra, s);
@@ -565,7 +599,7 @@ bool Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
     WC_HIP_CHECK(hipMemsetAsync(d_ctr, 0, sizeof(DevCounters), s));
     ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                   avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
-                  d_ctr->flags, d_bucket_ovf, d_bucket_en, d_red_stamps, fo_hist_ok ? d_fo_hist : nullptr, fo_hist_m,
+                  d_ctr->flags, d_bucket_ovf, d_bucket_en, d_red_stamps, red_blk(), fo_hist_ok ? d_fo_hist : nullptr, fo_hist_m,
                   nullptr, nullptr, nullptr, 0, 0u, red_q(), part};
     launch_reduce(ra, s);
     PubList pc{};
@@ -781,7 +815,10 @@ void Engine::Impl::finalize_local_sorted() {
     const uint32_t* ovf = first_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len}, n,
                                       key_bits(), A.take_n<uint8_t>(first_order_ws_bytes(src, n)), nullptr, s,
                                       fo_hist_ok ? d_fo_hist : nullptr, fo_hist_m);
-    if (h_fin.size() < 64) h_fin = PinnedBuffer(64);
+    if (h_fin.size() < 64) {
+      h_fin = PinnedBuffer(64);
+      std::memset(h_fin.data(), 0, 64);
+    }
     WC_HIP_CHECK(hipMemcpyAsync(h_fin.data() + 8, ovf, 4, hipMemcpyDeviceToHost, s));
     WC_HIP_CHECK(hipStreamSynchronize(s));  // the fallback path: one more wait is fine
     uint32_t bad = 0;
@@ -797,7 +834,10 @@ void Engine::Impl::finalize_local_sorted() {
     take_cols();
     const uint32_t* ovf = bitmap_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len}, n, max_end,
                                        1, bm, A.take_n<uint8_t>(bitmap_order_ws_bytes(n + 1, max_end, 1)), nullptr, s);
-    if (h_fin.size() < 64) h_fin = PinnedBuffer(64);
+    if (h_fin.size() < 64) {
+      h_fin = PinnedBuffer(64);
+      std::memset(h_fin.data(), 0, 64);
+    }
     WC_HIP_CHECK(hipMemcpyAsync(h_fin.data() + 8, ovf, 4, hipMemcpyDeviceToHost, s));
     WC_HIP_CHECK(hipStreamSynchronize(s));
     uint32_t bad = 0;
@@ -1294,9 +1334,17 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
   // the merged count still on the device, the sample sort's overflow word and
   // (planned merge) its decision flags and local key count: published with the last wait
   auto publish_and_wait = [&] {
-    if (im.cols.dn || im.fo_ovf || im.planned_active) {
-      if (im.h_fin.size() < 64) im.h_fin = PinnedBuffer(64);
+    if (im.cols.dn || im.fo_ovf || im.planned_active || im.pass_pub_pending) {
+      if (im.h_fin.size() < 64) {
+        im.h_fin = PinnedBuffer(64);
+        std::memset(im.h_fin.data(), 0, 64);  // the sequence word starts below every fin_seq
+      }
       PubList pc{};
+      if (im.pass_pub_pending) {  // the planned merge's pending pass: its counters ride here
+        im.pass_pub_pending = false;
+        for (int i = 0; i < im.pass_pub.n; ++i)
+          pc.add(im.pass_pub.dst[i], im.pass_pub.src[i], (uint64_t)im.pass_pub.words[i] * 4);
+      }
       if (im.cols.dn) pc.add(im.h_fin.data(), im.cols.dn, 8);
       if (im.fo_ovf) pc.add(im.h_fin.data() + 8, im.fo_ovf, 4);
       if (im.planned_active) {
@@ -1304,9 +1352,17 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
         pc.add(im.h_fin.data() + 16, im.d_merge_flags, 4);
         pc.add(im.h_fin.data() + 24, im.d_local_n, 8);
       }
+      if (merged && im.spin_wait) {  // a sequence word stored last: the host spins on it (below)
+        pc.seq_dst = reinterpret_cast<uint32_t*>(im.h_fin.data() + 32);
+        pc.seq = ++im.fin_seq;
+      }
       launch_publish(pc, im.s);
+      // the merge's last collectives are still in flight: wait under the comm watchdog
+      if (merged && im.spin_wait) {
+        comm->wait_word(reinterpret_cast<const uint32_t*>(im.h_fin.data() + 32), im.fin_seq, im.s);
+        return;
+      }
     }
-    // the merge's last collectives are still in flight: wait under the comm watchdog
     if (merged) comm->sync(im.s);
     else if (!drained) WC_HIP_CHECK(hipStreamSynchronize(im.s));
   };

@@ -57,6 +57,18 @@ struct Engine::Impl {
   unsigned long long* d_stamps = nullptr;  // WC_MAP_STAMPS: map phase clock sums
   unsigned long long* d_blk = nullptr;     // WC_MAP_STAMPS: per-block timing of the last map pass
   unsigned long long* d_red_stamps = nullptr;  // WC_MAP_STAMPS: reduce counters (WC_RED_STAMPS builds)
+  unsigned long long* d_red_blk = nullptr;     // WC_MAP_STAMPS: per reduce block profile (RED_BLK_WORDS each)
+  size_t red_blk_n = 0;
+  // the profile buffer when the next reduce grid fits it (its last launch's blocks are printed at teardown)
+  unsigned long long* red_blk() {
+    if (!d_red_blk || ((size_t)table().log2_buckets >= 63)) return nullptr;
+    const size_t grid = ((size_t)1 << table().log2_buckets) * red_q();
+    if (grid > red_blk_n) return nullptr;
+    red_blk_grid = grid;
+    return d_red_blk;
+  }
+  size_t red_blk_grid = 0;
+  uint32_t fin_seq = 0;  // sequence word of the merged finalize's last publish (h_fin + 32)
   uint64_t blocks_stamped = 0;             // map blocks launched with stamps (block-duration mean)
 
   // shuffle records

@@ -172,6 +172,9 @@ struct ReduceArgs {
   uint32_t* bucket_overflow;      // [n_buckets] set when a slice overflowed
   const uint8_t* bucket_enable;   // nullptr = all
   unsigned long long* stamps;     // [RED_STAMP_N] diagnostic counters (WC_RED_STAMPS builds), nullable
+  // diagnostic (WC_RED_STAMPS builds, nullable): per reduce block RED_BLK_WORDS words
+  // {bucket | quarter << 32, start, end (s_memrealtime), Rec16 | Rec records << 32 of its runs, LONG records}
+  unsigned long long* blk;
   uint32_t* fo_hist;              // [FO_LOGBINS] += every stored key's fo_logbin(first, fo_m) (nullable)
   uint32_t fo_m;
   // The last pass before a bitmap-rank order (nullable): every stored key sets
@@ -200,6 +203,7 @@ struct ReduceArgs {
 // Most reduce blocks per bucket (split reduce: fewer table buckets than CUs).
 constexpr uint32_t RED_SPLIT_MAX_Q = 16;
 // Reduce diagnostic counters (src/kernels/reduce.hip built with -DWC_RED_STAMPS=1).
+constexpr int RED_BLK_WORDS = 5;
 enum : int { RS_RECORDS = 0, RS_SLOW_LANES, RS_SLOW_WAVES, RS_PROBE_ITERS, RS_CAS_FAIL, RS_PENDING, RS_CLAIMS,
              RS_T_WAVE, RS_T_SLOW, RS_T_RUNS, RS_BLOCKS, RS_T_BLKMAX, RS_T_STREAMS, RS_NLONG, RS_LONG_STREAMED,
              RED_STAMP_N };

@@ -872,6 +872,7 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   if (WC_RED_STAMPS && tid < RED_STAMP_N) L.st[tid] = 0;
   __syncthreads();
   const uint64_t t_start = WC_RED_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+  const uint64_t rt_start = WC_RED_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz, one clock for every XCD
 
   const uint32_t shift = a.tab.log2_buckets - a.log2_rec_buckets;  // table buckets per record bucket (log2)
   const uint32_t rb = b & ((1u << a.log2_rec_buckets) - 1u);       // buckets nest on the low bits
@@ -946,6 +947,21 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
     }
     __syncthreads();
     if (tid < RED_STAMP_N) atomicAdd(&a.stamps[tid], L.st[tid]);
+    if (a.blk && tid == 0) {  // where the reduce's time goes, block by block
+      const uint32_t nrb0 = 1u << a.log2_rec_buckets;
+      unsigned long long n16 = 0, n24 = 0;
+      for (uint32_t p = q; p < a.map_blocks; p += a.nq) {
+        n16 += L.runcnt[p] & 0xFFFFu;
+        n24 += L.runcnt[p] >> 16;
+      }
+      (void)nrb0;
+      unsigned long long* r = a.blk + (size_t)RED_BLK_WORDS * blockIdx.x;
+      r[0] = b | ((unsigned long long)q << 32);
+      r[1] = rt_start;
+      r[2] = __builtin_amdgcn_s_memrealtime();
+      r[3] = n16 | (n24 << 32);
+      r[4] = L.st[RS_NLONG];
+    }
   }
 }
 
