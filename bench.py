@@ -154,6 +154,8 @@ def run_virtual(a) -> int:
         "merges_planned_rank0": int(ranks[0]["merges_planned"]), "merge_redos_rank0": int(ranks[0]["merge_redos"]),
         "stage_ms_rank0": {k: round(ranks[0][k], 4) for k in ("map", "reduce", "finalize", "merge", "idle")},
         "keys_per_rank": [int(r["keys"]) for r in ranks],
+        "merge_wire": [{k: int(r[k]) for k in ("merge_collectives", "merge_sent_bytes", "merge_peer_bytes",
+                                               "merge_root_recv_bytes")} for r in ranks],
         "config": {"model": f"wordcount-mapreduce/{cfg.name}", "bytes_per_rank": per, "chunk_bytes": chunk,
                    "merge": merge, "vocab": vocab, "long_frac": long_frac,
                    "communicator": "stream-ordered loopback (src/dist/comm.cpp)"},

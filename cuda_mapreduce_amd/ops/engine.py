@@ -353,12 +353,12 @@ def virtual_bench(ranks: int, nbytes: int, seed: int = 1, vocab: int = 100000, z
     stream.  Returns (rank 0's merged Result, per-rank dicts of wall ms/step and
     the last job's device stage times)."""
     o = default_options(**opts)
-    out = (ctypes.c_double * (10 * ranks))()
+    out = (ctypes.c_double * (14 * ranks))()
     res = Result._from_native(check_ptr(lib.wc_virtual_bench(ctypes.byref(o), ranks, device, nbytes, seed, vocab,
                                                              zipf_s, long_frac, steps, warmup, out)))
     keys = ("ms_per_step", "map", "reduce", "finalize", "merge", "idle", "tokens", "keys", "merges_planned",
-            "merge_redos")
-    return res, [{k: out[10 * r + i] for i, k in enumerate(keys)} for r in range(ranks)]
+            "merge_redos", "merge_collectives", "merge_sent_bytes", "merge_peer_bytes", "merge_root_recv_bytes")
+    return res, [{k: out[14 * r + i] for i, k in enumerate(keys)} for r in range(ranks)]
 
 
 def loopback_count(data: bytes, ranks: int, devices: Optional[Sequence[int]] = None, all_ranks: bool = False,

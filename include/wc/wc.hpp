@@ -40,6 +40,14 @@ struct Stats {
   // cross-GPU merges of the engine's life run planned (fixed exchange regions,
   // no host round trip) / redone exactly after a planned one overflowed
   uint32_t merges_planned = 0, merge_redos = 0;
+  // Wire traffic of the last merge, this rank's side (what a W-GPU xGMI run
+  // would move; profiles/r5_merge_rank_cost.md): collectives issued, bytes sent
+  // to peers in all of them, and the sum over collectives of the largest
+  // amount sent to ONE peer (each peer pair has its own xGMI link, so that is
+  // the link-bound part of a point-to-point exchange); bytes received by rank 0
+  // in the gather.
+  uint32_t merge_collectives = 0;
+  uint64_t merge_sent_bytes = 0, merge_peer_bytes = 0, merge_root_recv_bytes = 0;
   // Host wall clock of the last job's API calls (count_*, finalize / result).
   double host_count_ms = 0, host_finalize_ms = 0;
   // Device time of the last job's stages, from events on the engine stream

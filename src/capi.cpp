@@ -741,9 +741,11 @@ void wc_comm_destroy(wc_comm* c) { delete c; }
 // stream (rank r: segments [r * nseg, (r + 1) * nseg), global offsets from
 // r * bytes), one stream-ordered loopback group, and bench.py's step — reset,
 // count the shard, merged finalize on the device — `warmup` + `steps` times,
-// the timed loop bracketed by communicator barriers.  out[8 r + i] =
+// the timed loop bracketed by communicator barriers.  out[14 r + i] =
 // {wall ms / step, device ms of the last job: map, reduce, finalize, merge,
-// idle, tokens, local keys, merges planned, merges redone}.  Returns rank 0's
+// idle, tokens, local keys, merges planned, merges redone, merge collectives,
+// merge bytes sent to peers, sum over collectives of the largest per-peer
+// amount, bytes rank 0 received in the gather} (14 doubles per rank).  Returns rank 0's
 // merged table of one more job after timing — the same step ending in
 // result(), so it goes the way the timed jobs went (planned merge once the
 // first job learned its caps) — for validation.
@@ -790,7 +792,7 @@ wc_result* wc_virtual_bench(const wc_options* o, int ranks, int device, uint64_t
         eng.count_device(d, vseg * seg, vseg * seg, (uint64_t)r * nseg * seg, ' ');
         wc::KeyTable t = eng.result(c, false);
         const wc::Stats& st2 = eng.stats();
-        double* v = out + 10 * (size_t)r;
+        double* v = out + 14 * (size_t)r;
         v[0] = ms;
         v[1] = st.map_ms;
         v[2] = st.reduce_ms;
@@ -801,6 +803,10 @@ wc_result* wc_virtual_bench(const wc_options* o, int ranks, int device, uint64_t
         v[7] = (double)keys;
         v[8] = (double)st2.merges_planned;
         v[9] = (double)st2.merge_redos;
+        v[10] = (double)st.merge_collectives;
+        v[11] = (double)st.merge_sent_bytes;
+        v[12] = (double)st.merge_peer_bytes;
+        v[13] = (double)st.merge_root_recv_bytes;
         if (r == 0) res->t = std::move(t);
       } catch (const std::exception& ex) {
         errs[r] = ex.what();

@@ -510,8 +510,27 @@ void learn_caps(Engine::Impl& im, const OwnerPlan& P, const std::vector<unsigned
 // together when they are set.  (Before: an owner-count launch, a count-matrix
 // all-gather and a check ahead of the scatter — one more collective.)
 // Columns in: im.cols with n the bound and dn the device count.
+// Wire-traffic accounting of one collective (Stats::merge_*): bytes this rank
+// sends to each peer (vector over ranks; its own entry ignored).
+void account(Engine::Impl& im, int R, const std::vector<size_t>& to_peer) {
+  uint64_t mx = 0, tot = 0;
+  for (size_t p = 0; p < to_peer.size(); ++p) {
+    if ((int)p == R) continue;
+    mx = std::max<uint64_t>(mx, to_peer[p]);
+    tot += to_peer[p];
+  }
+  im.st.merge_collectives++;
+  im.st.merge_sent_bytes += tot;
+  im.st.merge_peer_bytes += mx;
+}
+void account_uniform(Engine::Impl& im, int R, int W, uint64_t bytes_each) {
+  account(im, R, std::vector<size_t>((size_t)W, (size_t)bytes_each));
+}
+
 void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense, const uint32_t* pass_flags) {
   Range rg(dense ? "wc_merge_dense_planned" : "wc_merge_shuffle_planned");
+  im.st.merge_collectives = 0;
+  im.st.merge_sent_bytes = im.st.merge_peer_bytes = im.st.merge_root_recv_bytes = 0;
   hipStream_t s = im.s;
   const int W = comm.size(), R = comm.rank();
   WC_CHECK(W <= (int)MERGE_MAX_RANKS, "merge supports at most 64 ranks");
@@ -609,6 +628,11 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
   comm.alltoallv(send_rows, ro.data(), rs.data(), recv_rows, ro.data(), rs.data(), s);
   comm.alltoallv(send_bytes, bo.data(), bs.data(), recv_bytes, bo.data(), bs.data(), s);
   comm.group_end();
+  {
+    std::vector<size_t> per(W);
+    for (int p = 0; p < W; ++p) per[p] = rs[p] + bs[p];
+    account(im, R, per);  // the owner exchange (rows + LONG bytes, one grouped launch)
+  }
   // 2. owner merge (padding rows skipped), merged rows counted on the device into the quad
   launch_mrow_insert(recv_rows, RR, recv_bytes, d_base, d_base + W + 1, (uint32_t)W, state, tcnt, tfirst, T, row_slot,
                      s);
@@ -631,6 +655,7 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
     comm.alltoallv(ids, io.data(), is.data(), ids_back, io.data(), is.data(), s);
   }
   comm.group_end();
+  account_uniform(im, R, W, 32 + (dense ? Cr * 4 : 0));  // the quads (+ dense: the ids back)
   if (!have) launch_merge_check(d_owns, (uint32_t)W, Gr, key_bound, im.d_merge_flags, s);  // else folded below
   // 4. dense: padded count / first-offset vectors, reduce-scattered (owner o's
   // slice = its ids) and all-gathered
@@ -647,10 +672,12 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
     comm.reduce_scatter_u64(vc, scnt, Gr, RedOp::Sum, s);
     comm.reduce_scatter_u64(vf, sfirst, Gr, RedOp::Min, s);
     comm.group_end();
+    account_uniform(im, R, W, 2 * Gr * 8);  // reduce-scatter: owner p's slice of both vectors to p
     comm.group_begin();
     comm.allgather(scnt, dcnt, Gr * 8, s);
     comm.allgather(sfirst, dfirst, Gr * 8, s);
     comm.group_end();
+    account_uniform(im, R, W, 2 * Gr * 8);  // all-gather: this rank's slice to every peer
   }
   // 5. every owner's merged region (+ its whole received byte payload) to rank 0
   for (int p = 0; p < W; ++p) {
@@ -672,11 +699,19 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
   comm.alltoallv(merged, zs.data(), sr.data(), grows, go.data(), gr.data(), s);
   comm.alltoallv(recv_bytes, zs.data(), sb.data(), gbytes, gbo.data(), gb.data(), s);
   comm.group_end();
+  {
+    std::vector<size_t> per(W, 0);
+    per[0] = sr[0] + sb[0];
+    account(im, R, per);  // the gather to rank 0
+    if (R == 0)
+      for (int p = 1; p < W; ++p) im.st.merge_root_recv_bytes += gr[p] + gb[p];
+  }
   if (all_ranks) {
     comm.group_begin();
     comm.broadcast(grows, GR * sizeof(MRow), 0, s);
     comm.broadcast(gbytes, (uint64_t)W * RB, 0, s);
     comm.group_end();
+    if (R == 0) account_uniform(im, R, W, GR * sizeof(MRow) + (uint64_t)W * RB);
   }
   KeyCols o;
   im.max_end = std::max(im.max_end, cp.gmax_end);  // the width the order below is sized for

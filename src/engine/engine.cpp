@@ -86,11 +86,13 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
 
   if (const char* e = std::getenv("WC_REC_SHIFT")) rec_shift = (uint32_t)std::atoi(e);  // sweeps only
   if (const char* e = std::getenv("WC_RED_Q")) red_q_force = (uint32_t)std::atoi(e);    // sweeps only
-  {  // split-reduce partial tables: one per reduce block when buckets < CUs
-    part_blocks = std::max<uint32_t>(n_cu, 256);
+  if (const char* e = std::getenv("WC_RED_PLAN")) red_plan = std::atoi(e) != 0;  // A/B: 0 = the uniform split
+  {  // split-reduce partial tables: one per reduce block when buckets < CUs,
+     // two per block of the balanced reduce (its grid is one block per CU)
+    part_blocks = 2 * std::max<uint32_t>(n_cu, 256);
     if (red_q_force) part_blocks = std::max<uint32_t>(part_blocks, 512u * red_q_force);  // sweeps: Q above 512 buckets
     const size_t rows = (size_t)part_blocks * TAB_SLOTS;
-    part_mem.reserve(rows * (5 * 8 + 4) + part_blocks * 8 + rows * 12 + 16 * 256);
+    part_mem.reserve(rows * (5 * 8 + 4) + part_blocks * 8 + rows * 12 + MAX_REC_BUCKETS * 4 + 16 * 256);
     part.k0 = part_mem.take_n<uint64_t>(rows);
     part.k1 = part_mem.take_n<uint64_t>(rows);
     part.cnt = part_mem.take_n<uint64_t>(rows);
@@ -100,8 +102,10 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
     part.n = part_mem.take_n<uint32_t>(part_blocks);
     part.qsoff = part_mem.take_n<uint64_t>(rows);
     part.qslen = part_mem.take_n<uint32_t>(rows);
-    part.done = part_mem.take_n<uint32_t>(part_blocks);
-    WC_HIP_CHECK(hipMemset(part.done, 0, part_blocks * sizeof(uint32_t)));
+    const size_t ndone = std::max<size_t>(part_blocks, MAX_REC_BUCKETS);  // indexed by bucket
+    part.done = part_mem.take_n<uint32_t>(ndone);
+    WC_HIP_CHECK(hipMemset(part.done, 0, ndone * sizeof(uint32_t)));
+    dev_malloc(&d_bucket_w, MAX_REC_BUCKETS * sizeof(uint32_t));
   }
   if (const char* e = std::getenv("WC_LOG2_BUCKETS")) {  // sweeps only: shuffle + table bucket count
     opt.log2_rec_buckets = (uint32_t)std::atoi(e);
@@ -178,6 +182,7 @@ Engine::Impl::~Impl() {
   if (d_arena) (void)hipFree(d_arena);
   if (d_arena_cursor) (void)hipFree(d_arena_cursor);
   if (d_fo_hist) (void)hipFree(d_fo_hist);
+  if (d_bucket_w) (void)hipFree(d_bucket_w);
   if (d_fo_hist_cols) (void)hipFree(d_fo_hist_cols);
   if (d_bm) (void)hipFree(d_bm);
   if (d_stamps) {
@@ -335,8 +340,14 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
       }
     }
   }
+  // the balanced reduce: one record bucket per table bucket (no split since
+  // the records were bucketed), its weights from this map
+  const uint32_t nbk = 1u << table().log2_buckets;
+  const bool planned = red_plan && !red_q_force && log2_rb == table().log2_buckets && blocks <= (uint32_t)RED_MAX_RUNS &&
+                       nbk <= (uint32_t)MAX_REC_BUCKETS && part_blocks >= 2 * n_cu;
   ZeroList z{};
   z.add(d_ctr, sizeof(DevCounters));
+  if (planned) z.add(d_bucket_w, nbk * sizeof(uint32_t));
   if (want_hist) z.add(d_fo_hist, FO_LOGBINS * sizeof(uint32_t));  // rebuilt by this pass's reduce over the whole table
   {
     uint32_t kb = 1;
@@ -353,7 +364,8 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   pass_rec.cursor = &d_ctr->records;
   pass_rec.subcap = (uint32_t)std::min<uint64_t>(rec.cap / ((uint64_t)blocks << log2_rb), 0xFFFFull);
   WC_CHECK(pass_rec.subcap > 0, "shuffle record capacity below one record per (map block, bucket)");
-  MapArgs m{text, len, avail, prev, log2_rb, pass_rec, d_ctr->flags, &d_ctr->tokens, k1_mask, d_stamps, d_blk};
+  MapArgs m{text,     len,          avail,          prev,     log2_rb, pass_rec, d_ctr->flags, &d_ctr->tokens,
+            k1_mask,  d_stamps,     d_blk,          planned ? d_bucket_w : nullptr};
   if (d_stamps) blocks_stamped += blocks;
   hot.text = text;
   hot.nblk = blocks;
@@ -369,8 +381,13 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
                 avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
                 d_ctr->flags, d_bucket_ovf, nullptr, d_red_stamps, red_blk(), want_hist ? d_fo_hist : nullptr, fo_hist_m,
                 bm, bm ? bitmap_order_linecnt(bm, bm_end, 1) : nullptr, bm ? bitmap_order_ctl(bm, bm_end, 1) : nullptr,
-                bm ? (bm_end >> 1) + 1 : 0, 1u, red_q(), part};
-  launch_reduce(ra, s);
+                bm ? (bm_end >> 1) + 1 : 0, 1u, red_q(), planned ? d_bucket_w : nullptr, part, part_blocks};
+  if (planned) {
+    if (ra.blk) red_blk_grid = n_cu;
+    launch_reduce_planned(ra, n_cu, s);
+  } else {
+    launch_reduce(ra, s);
+  }
   if (sync_debug) {
     const hipError_t e = hipStreamSynchronize(s);
     fprintf(stderr, "[wc] reduce base=%llu buckets=%u -> %s\n", (unsigned long long)base, 1u << table().log2_buckets,
@@ -600,7 +617,7 @@ bool Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
     ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                   avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
                   d_ctr->flags, d_bucket_ovf, d_bucket_en, d_red_stamps, red_blk(), fo_hist_ok ? d_fo_hist : nullptr, fo_hist_m,
-                  nullptr, nullptr, nullptr, 0, 0u, red_q(), part};
+                  nullptr, nullptr, nullptr, 0, 0u, red_q(), nullptr, part, part_blocks};
     launch_reduce(ra, s);
     PubList pc{};
     pc.add(h_ctr, d_ctr, sizeof(DevCounters));

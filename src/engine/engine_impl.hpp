@@ -68,7 +68,9 @@ struct Engine::Impl {
     return d_red_blk;
   }
   size_t red_blk_grid = 0;
-  uint32_t fin_seq = 0;  // sequence word of the merged finalize's last publish (h_fin + 32)
+  uint32_t fin_seq = 0;
+  bool red_plan = true;             // the balanced reduce (WC_RED_PLAN=0: the uniform split)
+  uint32_t* d_bucket_w = nullptr;   // its per-bucket weights (the map adds them)  // sequence word of the merged finalize's last publish (h_fin + 32)
   uint64_t blocks_stamped = 0;             // map blocks launched with stamps (block-duration mean)
 
   // shuffle records

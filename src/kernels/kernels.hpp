@@ -104,7 +104,15 @@ struct MapArgs {
   uint64_t k1_mask;            // LONG-key hash bits kept (K1_HASH_MASK; collision tests truncate)
   unsigned long long* stamps;  // diagnostic build: per-phase s_memtime sums (MAP_STAMP_N), nullptr = off
   unsigned long long* blk;     // diagnostic: per map block {start, end (s_memrealtime), XCC id, units}, nullable
+  // nullable (zeroed per pass): per shuffle bucket, += the reduce-cost weight of
+  // every map block's run (Rec16 records + RED_W24 x 24-byte records) — the
+  // balanced reduce's plan (ReduceArgs::bucket_w)
+  uint32_t* bucket_w;
 };
+// Reduce cost of a 24-byte record relative to a Rec16 one in the balanced
+// plan: 24-byte runs carry the LONG words, whose byte comparison (a random
+// 64-byte text read) costs ~10-20x a Rec16 merge (profiles/r5_reduce_balance.md)
+constexpr uint32_t RED_W24 = 12;
 // Hot-key sampling workspace (map.hip).  Two launches, no device-scope
 // atomics and nothing to zero: wc_hot_sample writes every map block's sampled
 // words, split by fingerprint into HOT_PARTS partitions, to its own stage
@@ -191,6 +199,14 @@ struct ReduceArgs {
   // occupied rows to part slot (b + B q); the last quarter of a bucket to finish
   // merges the other partials into its own table and stores the slice.
   uint32_t nq;
+  // Balanced reduce (nullable: the uniform split above): the map's per-bucket
+  // weights (MapArgs::bucket_w; record buckets == table buckets).  The grid's
+  // G blocks cut the buckets' concatenated weight W (+1 per bucket) into G equal
+  // intervals: block i takes [W i / G, W (i + 1) / G) — a tail of one bucket,
+  // whole buckets, a head of another — as record ranges of the buckets'
+  // concatenated runs; a bucket cut into pieces is merged by its last piece to
+  // finish (partial slots 2 i / 2 i + 1, done[b] counts the pieces).
+  const uint32_t* bucket_w;
   struct Parts {
     uint64_t *k0, *k1, *cnt, *first, *soff;  // [(b + B q) * TAB_SLOTS + i] rows
     uint32_t* slen;
@@ -199,9 +215,11 @@ struct ReduceArgs {
     uint32_t* qslen;
     uint32_t* done;                           // [b] quarters arrived (zeroed; the last resets it)
   } part;
+  uint32_t part_slots;  // partial-table slots allocated (the balanced plan needs 2 x its grid)
 };
 // Most reduce blocks per bucket (split reduce: fewer table buckets than CUs).
 constexpr uint32_t RED_SPLIT_MAX_Q = 16;
+// launch_reduce_planned: the balanced reduce over `grid` blocks (ReduceArgs::bucket_w set)
 // Reduce diagnostic counters (src/kernels/reduce.hip built with -DWC_RED_STAMPS=1).
 constexpr int RED_BLK_WORDS = 5;
 enum : int { RS_RECORDS = 0, RS_SLOW_LANES, RS_SLOW_WAVES, RS_PROBE_ITERS, RS_CAS_FAIL, RS_PENDING, RS_CLAIMS,
@@ -224,6 +242,7 @@ struct ZeroList;
 void launch_map(const MapArgs& a, const HotArgs& h, uint32_t map_blocks, hipStream_t s, bool sample,
                 const ZeroList& z);
 void launch_reduce(const ReduceArgs& a, hipStream_t s);
+void launch_reduce_planned(const ReduceArgs& a, uint32_t grid, hipStream_t s);
 void launch_table_split(const TableView& src, const TableView& dst, hipStream_t s);
 void launch_table_clear(const TableView& t, hipStream_t s);
 // Writes occupied entries densely in bucket order; bucket_off[b] = exclusive

@@ -1180,6 +1180,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     if (c16 > sub || c24 > sub) atomicOr(&a.flags[FLAG_REGION_OVF], 1u);  // overran into the next sub-region
     const uint32_t n16 = min(c16, sub), n24 = min(c24, sub);
     a.rec.count[(size_t)blockIdx.x * nb + b] = n16 | (n24 << 16);  // packed for the reducer (sub <= 0xFFFF)
+    if (a.bucket_w && (n16 | n24)) atomicAdd(&a.bucket_w[b], n16 + RED_W24 * n24);  // the balanced reduce's plan
     e += n16 + n24;
   }
   for (int o = 32; o > 0; o >>= 1) {
