@@ -255,8 +255,9 @@ __device__ __forceinline__ bool long_equal64(const LongCtx& c, const uint64_t (&
 // a published tag acquires before reading the reference.  Probers that see
 // PENDING re-read the group; the claimer finishes inside its iteration, so
 // the lanes of one wave never wait on each other.  Returns 1 for a claim.
-__device__ __forceinline__ uint32_t merge_long(RedLds& L, const LongCtx& c, uint32_t ph, uint64_t k0, uint64_t k1, uint64_t cnt,
-                                            uint64_t first, uint64_t off) {
+__device__ __forceinline__ int find_long(RedLds& L, const LongCtx& c, uint32_t ph, uint64_t k0, uint64_t k1, uint64_t off,
+                                         bool& claimed) {
+  claimed = false;
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const uint32_t tag = make_tag(ph);
   const uint32_t g1 = group_of(ph, TAB_GROUPS), g2 = group2_of(ph, TAB_GROUPS);
@@ -287,10 +288,7 @@ __device__ __forceinline__ uint32_t merge_long(RedLds& L, const LongCtx& c, uint
       const int s = 4 * (int)g + i;
       const uint32_t sl = c.sref_len[s];
       const uint64_t so = c.sref_off[s];
-      if (sl == SREF_POISON || (wlen < 64 ? long_equal64(c, w, wlen, so, sl) : long_equal(c, off, so, sl))) {
-        add_to_slot(L, s, cnt, first);
-        return 0;
-      }
+      if (sl == SREF_POISON || (wlen < 64 ? long_equal64(c, w, wlen, so, sl) : long_equal(c, off, so, sl))) return s;
     }
     if (WC_RED_STAMPS) atomicAdd(&L.st[RS_PROBE_ITERS], 1ull);
     if (pending) continue;  // a claim is being published in this group: look again
@@ -305,15 +303,45 @@ __device__ __forceinline__ uint32_t merge_long(RedLds& L, const LongCtx& c, uint
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __hip_atomic_store(&G.tag[e], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (WC_RED_STAMPS) atomicAdd(&L.st[RS_CLAIMS], 1ull);
-      add_to_slot(L, s, cnt, first);
-      return 1;
+      claimed = true;
+      return s;
     }
     if (++steps >= TAB_MAX_GROUP_PROBES) {
       L.overflow = 1;
-      return 0;
+      return -1;
     }
     g = probe_group(g1, g2, (uint32_t)steps, TAB_GROUPS);
   }
+}
+
+// A wave's LONG records after find_long (slot s, or -1 for none / no room),
+// EVERY lane of the wave converged here: the records of the first valid
+// lane's slot — a frequent LONG word — add once, summed in registers (one
+// pair of LDS atomics instead of one per lane on the same address); the
+// others add for themselves.  Each record is counted exactly once: by its own
+// lane (s != the lead slot) or inside the lead's sum (s == the lead slot);
+// lanes with s < 0 hold no record (the sum takes 0 / ~0 from them).
+__device__ __forceinline__ void wave_add_long(RedLds& L, int s, uint64_t cnt, uint64_t first) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t valid = __ballot(s >= 0);
+  if (!valid) return;
+  const int lead = __ffsll((unsigned long long)valid) - 1;
+  const int ls = __builtin_amdgcn_readlane(s, lead);
+  const bool same = s == ls;
+  if (s >= 0 && !same) add_to_slot(L, s, cnt, first);
+  if (__popcll(__ballot(same)) == 1) {
+    if (lane == lead) add_to_slot(L, ls, cnt, first);
+    return;
+  }
+  uint64_t c = same ? cnt : 0ull, f = same ? first : ~0ull;
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t clo = (uint32_t)__shfl_xor((int)(uint32_t)c, o), chi = (uint32_t)__shfl_xor((int)(uint32_t)(c >> 32), o);
+    const uint32_t flo = (uint32_t)__shfl_xor((int)(uint32_t)f, o), fhi = (uint32_t)__shfl_xor((int)(uint32_t)(f >> 32), o);
+    c += (uint64_t)clo | ((uint64_t)chi << 32);
+    const uint64_t g = (uint64_t)flo | ((uint64_t)fhi << 32);
+    f = g < f ? g : f;
+  }
+  if (lane == lead) add_to_slot(L, ls, c, f);
 }
 
 // Block end of a bucket pass: the LONG words claimed during the pass still
@@ -551,10 +579,21 @@ __device__ __forceinline__ void merge_stream(RedLds& L, const ReduceArgs& a, uin
 // anyway.
 __device__ __forceinline__ void long_queue(RedLds& L, const ReduceArgs& a, const LongCtx& c, uint32_t n,
                                            uint32_t& claims) {
-  for (uint32_t i = threadIdx.x; i < n; i += RED_THREADS) {
-    const Rec r = a.rec.recs[L.longq[i]];
-    const uint32_t off = (uint32_t)r.co;
-    claims += merge_long(L, c, place_hash(r.k0, r.k1), r.k0, r.k1, r.co >> 32, a.chunk_base + off, off);
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t i0 = threadIdx.x - lane; i0 < n; i0 += RED_THREADS) {  // wave-uniform: lanes stay converged
+    const uint32_t i = i0 + lane;
+    int s = -1;
+    uint64_t cnt = 0, first = ~0ull;
+    if (i < n) {
+      const Rec r = a.rec.recs[L.longq[i]];
+      const uint32_t off = (uint32_t)r.co;
+      bool cl;
+      s = find_long(L, c, place_hash(r.k0, r.k1), r.k0, r.k1, off, cl);
+      claims += cl ? 1u : 0u;
+      cnt = r.co >> 32;
+      first = a.chunk_base + off;
+    }
+    wave_add_long(L, s, cnt, first);
   }
 }
 
@@ -575,11 +614,18 @@ __device__ __forceinline__ void long_stream(RedLds& L, const ReduceArgs& a, cons
   auto merge_first = [&](uint32_t k) {  // wl[0, k), one per lane
     const uint64_t t0 = WC_RED_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     wsync();
+    int s = -1;
+    uint64_t cnt = 0, first = ~0ull;
     if (lane < k) {
       const Rec r = a.rec.recs[wl[lane]];
       const uint32_t off = (uint32_t)r.co;
-      claims += merge_long(L, c, place_hash(r.k0, r.k1), r.k0, r.k1, r.co >> 32, a.chunk_base + off, off);
+      bool cl;
+      s = find_long(L, c, place_hash(r.k0, r.k1), r.k0, r.k1, off, cl);
+      claims += cl ? 1u : 0u;
+      cnt = r.co >> 32;
+      first = a.chunk_base + off;
     }
+    wave_add_long(L, s, cnt, first);
     wsync();
     if (WC_RED_STAMPS && lane == 0) atomicAdd(&L.st[RS_T_SLOW], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
   };
@@ -1001,11 +1047,18 @@ __device__ __forceinline__ void long_range(RedLds& L, const ReduceArgs& a, const
   };
   auto merge_first = [&](uint32_t k) {  // wl[0, k), one per lane
     wsync();
+    int s = -1;
+    uint64_t cnt = 0, first = ~0ull;
     if (lane < k) {
       const Rec r = a.rec.recs[wl[lane]];
       const uint32_t off = (uint32_t)r.co;
-      claims += merge_long(L, c, place_hash(r.k0, r.k1), r.k0, r.k1, r.co >> 32, a.chunk_base + off, off);
+      bool cl;
+      s = find_long(L, c, place_hash(r.k0, r.k1), r.k0, r.k1, off, cl);
+      claims += cl ? 1u : 0u;
+      cnt = r.co >> 32;
+      first = a.chunk_base + off;
     }
+    wave_add_long(L, s, cnt, first);
     wsync();
   };
   auto pre = [&](uint32_t k) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)L.runcnt[k]); };
