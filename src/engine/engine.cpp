@@ -87,6 +87,10 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   if (const char* e = std::getenv("WC_REC_SHIFT")) rec_shift = (uint32_t)std::atoi(e);  // sweeps only
   if (const char* e = std::getenv("WC_RED_Q")) red_q_force = (uint32_t)std::atoi(e);    // sweeps only
   if (const char* e = std::getenv("WC_RED_PLAN")) red_plan = std::atoi(e) != 0;  // A/B: 0 = the uniform split
+  if (const char* e = std::getenv("WC_CHECK_TABLE"); e && std::atoi(e)) {
+    dev_malloc(&d_tab_err, 4 * sizeof(unsigned long long));
+    WC_HIP_CHECK(hipMemset(d_tab_err, 0, 4 * sizeof(unsigned long long)));
+  }
   {  // split-reduce partial tables: one per reduce block when buckets < CUs,
      // two per block of the balanced reduce (its grid is one block per CU)
     part_blocks = 2 * std::max<uint32_t>(n_cu, 256);
@@ -183,6 +187,7 @@ Engine::Impl::~Impl() {
   if (d_arena_cursor) (void)hipFree(d_arena_cursor);
   if (d_fo_hist) (void)hipFree(d_fo_hist);
   if (d_bucket_w) (void)hipFree(d_bucket_w);
+  if (d_tab_err) (void)hipFree(d_tab_err);
   if (d_fo_hist_cols) (void)hipFree(d_fo_hist_cols);
   if (d_bm) (void)hipFree(d_bm);
   if (d_stamps) {
@@ -388,6 +393,7 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   } else {
     launch_reduce(ra, s);
   }
+  check_table(planned ? "the balanced reduce" : "the reduce");
   if (sync_debug) {
     const hipError_t e = hipStreamSynchronize(s);
     fprintf(stderr, "[wc] reduce base=%llu buckets=%u -> %s\n", (unsigned long long)base, 1u << table().log2_buckets,
@@ -408,6 +414,18 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   pass_pub_pending = true;
   if (!defer_publish) flush_pass_publish();
   mark(EV_REDUCE);
+}
+
+void Engine::Impl::check_table(const char* where) {
+  if (!d_tab_err) return;
+  launch_check_table(table(), d_tab_err, s);
+  unsigned long long h[4] = {};
+  WC_HIP_CHECK(hipMemcpyAsync(h, d_tab_err, sizeof h, hipMemcpyDeviceToHost, s));
+  WC_HIP_CHECK(hipStreamSynchronize(s));
+  if (h[0])
+    fail(std::string("WC_CHECK_TABLE: table invariant broken after ") + where + ": bucket " + std::to_string(h[0] - 1) +
+         " of " + std::to_string(1u << table().log2_buckets) + " holds " + std::to_string(h[1]) + " keys, occupancy " +
+         std::to_string(h[2]) + ", " + std::to_string(h[3]) + " misplaced");
 }
 
 void Engine::Impl::flush_pass_publish() {
@@ -550,6 +568,7 @@ void Engine::Impl::split_table() {
   launch_table_clear(dst.v, s);
   launch_table_split(table(), dst.v, s);
   cur ^= 1;
+  check_table("a table split");
   st.table_splits++;
   WC_LOG(LOG_INFO, "dev %d: key table split %u -> %u buckets", dev, 1u << lg, 2u << lg);
 }
@@ -619,6 +638,7 @@ bool Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
                   d_ctr->flags, d_bucket_ovf, d_bucket_en, d_red_stamps, red_blk(), fo_hist_ok ? d_fo_hist : nullptr, fo_hist_m,
                   nullptr, nullptr, nullptr, 0, 0u, red_q(), nullptr, part, part_blocks};
     launch_reduce(ra, s);
+    check_table("a split re-run's reduce");
     PubList pc{};
     pc.add(h_ctr, d_ctr, sizeof(DevCounters));
     add_occupancy(pc);

@@ -69,7 +69,12 @@ struct Engine::Impl {
   }
   size_t red_blk_grid = 0;
   uint32_t fin_seq = 0;
-  bool red_plan = true;             // the balanced reduce (WC_RED_PLAN=0: the uniform split)
+  bool red_plan = true;
+  // WC_CHECK_TABLE=1 (debug): after every reduce and split the table's
+  // invariants are checked on the device and a violation fails the job naming
+  // the stage (engine.cpp check_table)
+  unsigned long long* d_tab_err = nullptr;
+  void check_table(const char* where);             // the balanced reduce (WC_RED_PLAN=0: the uniform split)
   uint32_t* d_bucket_w = nullptr;   // its per-bucket weights (the map adds them)  // sequence word of the merged finalize's last publish (h_fin + 32)
   uint64_t blocks_stamped = 0;             // map blocks launched with stamps (block-duration mean)
 

@@ -245,6 +245,8 @@ void launch_reduce(const ReduceArgs& a, hipStream_t s);
 void launch_reduce_planned(const ReduceArgs& a, uint32_t grid, hipStream_t s);
 void launch_table_split(const TableView& src, const TableView& dst, hipStream_t s);
 void launch_table_clear(const TableView& t, hipStream_t s);
+// debug: err (4 words, zeroed) <- the first bucket breaking the table's invariants (reduce.hip wc_check_table)
+void launch_check_table(const TableView& t, unsigned long long* err, hipStream_t s);
 // Writes occupied entries densely in bucket order; bucket_off[b] = exclusive
 // prefix of the per-bucket occupancy (device array of 2^log2_buckets).
 void launch_table_compact(const TableView& t, const uint64_t* bucket_off, uint64_t* k0, uint64_t* k1, uint64_t* cnt,

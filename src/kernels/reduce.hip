@@ -1392,6 +1392,35 @@ __global__ void __launch_bounds__(RED_THREADS) wc_table_split(TableView src, Tab
   if (threadIdx.x == 0) dst.occupancy[nb] = L.occupied;
 }
 
+// Debug (WC_CHECK_TABLE=1, Engine::Impl::check_table): the running table's
+// invariants — a bucket with occupancy > 0 holds exactly that many keys (k1 !=
+// K1_EMPTY: the compaction, the order and the gather size their output from
+// the occupancy) and every key hashes to its own bucket.  err = {1 + the first
+// bad bucket (0: none), keys found, its occupancy, misplaced keys}.
+__global__ void __launch_bounds__(1024) wc_check_table(TableView t, unsigned long long* err) {
+  __shared__ uint32_t cnt, bad;
+  const uint32_t b = blockIdx.x;
+  const uint32_t occ = t.occupancy[b];
+  if (occ == 0) return;  // contents undefined (see load_slice)
+  if (threadIdx.x == 0) cnt = bad = 0;
+  __syncthreads();
+  const size_t base = (size_t)b * TAB_SLOTS;
+  for (int s = threadIdx.x; s < TAB_SLOTS; s += blockDim.x) {
+    const uint64_t k1 = t.k1[base + s];
+    if (k1 == K1_EMPTY) continue;
+    atomicAdd(&cnt, 1u);
+    if (bucket_of(place_hash(t.k0[base + s], k1), t.log2_buckets) != b) atomicAdd(&bad, 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && (cnt != occ || bad)) {
+    if (atomicCAS(&err[0], 0ull, (unsigned long long)b + 1) == 0ull) {
+      err[1] = cnt;
+      err[2] = occ;
+      err[3] = bad;
+    }
+  }
+}
+
 __global__ void wc_table_clear(TableView t, size_t n) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     t.k1[i] = K1_EMPTY;
@@ -1561,6 +1590,10 @@ void launch_reduce_planned(const ReduceArgs& a, uint32_t grid, hipStream_t s) {
 
 void launch_table_split(const TableView& src, const TableView& dst, hipStream_t s) {
   hipLaunchKernelGGL(dev::wc_table_split, dim3(1u << dst.log2_buckets), dim3(RED_THREADS), 0, s, src, dst);
+}
+
+void launch_check_table(const TableView& t, unsigned long long* err, hipStream_t s) {
+  hipLaunchKernelGGL(dev::wc_check_table, dim3(1u << t.log2_buckets), dim3(1024), 0, s, t, err);
 }
 
 void launch_table_clear(const TableView& t, hipStream_t s) {
