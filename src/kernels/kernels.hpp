@@ -201,7 +201,7 @@ struct ReduceArgs {
   uint32_t nq;
   // Balanced reduce (nullable: the uniform split above): the map's per-bucket
   // weights (MapArgs::bucket_w; record buckets == table buckets).  The grid's
-  // G blocks cut the buckets' concatenated weight W (+1 per bucket) into G equal
+  // G blocks cut the buckets' concatenated weight W (+ceil(G / buckets) per bucket) into G equal
   // intervals: block i takes [W i / G, W (i + 1) / G) — a tail of one bucket,
   // whole buckets, a head of another — as record ranges of the buckets'
   // concatenated runs; a bucket cut into pieces is merged by its last piece to

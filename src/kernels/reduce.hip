@@ -1096,8 +1096,12 @@ __device__ __forceinline__ void reduce_planned(RedLds& L, const ReduceArgs& a) {
   const int tid = threadIdx.x, wave = tid >> 6, nwaves = RED_THREADS / 64;
   const uint32_t nb = 1u << a.tab.log2_buckets, G = gridDim.x, i = blockIdx.x;
   const uint32_t sub = a.rec.subcap;
-  {  // the plan: exclusive prefix of the bucket weights (+1 each: every bucket has a non-empty interval)
-    const uint32_t w = (uint32_t)tid < nb ? a.bucket_w[tid] + 1u : 0u;
+  {  // the plan: exclusive prefix of the bucket weights, each + ceil(G / nb): every bucket's
+     // interval is non-empty and W >= G, so every block's interval is too — a
+     // bucket's pieces are then exactly the blocks [first, last] its interval
+     // meets, and all of them arrive on its counter (an empty block would not)
+    const uint32_t pad = (G + nb - 1) / nb;
+    const uint32_t w = (uint32_t)tid < nb ? a.bucket_w[tid] + pad : 0u;
     uint32_t tot;
     const uint32_t ex = block_scan_excl(w, tot);
     if ((uint32_t)tid < nb) L.wpre[tid] = ex;
@@ -1127,7 +1131,7 @@ __device__ __forceinline__ void reduce_planned(RedLds& L, const ReduceArgs& a) {
     runs_prefix<true>(L, a, b, nb, sub);
     const uint32_t n16 = uni(L.tot16), n24 = uni(L.tot24);
     // weight -> record ranges: [0, n16) Rec16 records of weight 1, then n24 of
-    // weight RED_W24, then the bucket's +1 (no records); the first and last
+    // weight RED_W24, then the bucket's pad (no records); the first and last
     // pieces take the ends exactly
     auto r24 = [&](uint32_t x) {
       return x <= n16 ? 0u : min(n24, (x - n16 + RED_W24 - 1) / RED_W24);
