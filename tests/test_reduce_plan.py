@@ -30,7 +30,7 @@ def r24(x, n16, n24):
 
 def test_plan_pieces_and_ranges():
     rnd = random.Random(5)
-    for _ in range(1500):
+    for _ in range(300):
         nb = rnd.choice([64, 128, 256, 512])
         G = rnd.choice([1, 3, 64, 256, 300])
         n16s = [rnd.choice([0, 0, 1, 7, 300, 5000]) for _ in range(nb)]
