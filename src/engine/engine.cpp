@@ -93,7 +93,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   }
   {  // split-reduce partial tables: one per reduce block when buckets < CUs,
      // two per block of the balanced reduce (its grid is one block per CU)
-    part_blocks = 2 * std::max<uint32_t>(n_cu, 256);
+    part_blocks = std::max<uint32_t>(n_cu, 256) + MAX_REC_BUCKETS;
     if (red_q_force) part_blocks = std::max<uint32_t>(part_blocks, 512u * red_q_force);  // sweeps: Q above 512 buckets
     const size_t rows = (size_t)part_blocks * TAB_SLOTS;
     part_mem.reserve(rows * (5 * 8 + 4) + part_blocks * 8 + rows * 12 + MAX_REC_BUCKETS * 4 + 16 * 256);
@@ -345,11 +345,13 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
       }
     }
   }
-  // the balanced reduce: one record bucket per table bucket (no split since
-  // the records were bucketed), its weights from this map
+  // the reduce's dispatch plan (heavy buckets split, heaviest first) for
+  // tables of >= CUs buckets: one record bucket per table bucket (no split
+  // since the records were bucketed), its weights from this map
   const uint32_t nbk = 1u << table().log2_buckets;
-  const bool planned = red_plan && !red_q_force && log2_rb == table().log2_buckets && blocks <= (uint32_t)RED_MAX_RUNS &&
-                       nbk <= (uint32_t)MAX_REC_BUCKETS && part_blocks >= 2 * n_cu;
+  const uint32_t plan_extra = std::min<uint32_t>(RED_PLAN_EXTRA, part_blocks - std::min(part_blocks, nbk));
+  const bool planned = red_plan && !red_q_force && red_q() == 1 && log2_rb == table().log2_buckets &&
+                       nbk <= (uint32_t)MAX_REC_BUCKETS && nbk + plan_extra <= part_blocks;
   ZeroList z{};
   z.add(d_ctr, sizeof(DevCounters));
   if (planned) z.add(d_bucket_w, nbk * sizeof(uint32_t));
@@ -387,13 +389,9 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
                 d_ctr->flags, d_bucket_ovf, nullptr, d_red_stamps, red_blk(), want_hist ? d_fo_hist : nullptr, fo_hist_m,
                 bm, bm ? bitmap_order_linecnt(bm, bm_end, 1) : nullptr, bm ? bitmap_order_ctl(bm, bm_end, 1) : nullptr,
                 bm ? (bm_end >> 1) + 1 : 0, 1u, red_q(), planned ? d_bucket_w : nullptr, part, part_blocks};
-  if (planned) {
-    if (ra.blk) red_blk_grid = n_cu;
-    launch_reduce_planned(ra, n_cu, s);
-  } else {
-    launch_reduce(ra, s);
-  }
-  check_table(planned ? "the balanced reduce" : "the reduce");
+  if (planned && ra.blk) red_blk_grid = nbk + plan_extra;
+  launch_reduce(ra, s, plan_extra);
+  check_table("the reduce");
   if (sync_debug) {
     const hipError_t e = hipStreamSynchronize(s);
     fprintf(stderr, "[wc] reduce base=%llu buckets=%u -> %s\n", (unsigned long long)base, 1u << table().log2_buckets,

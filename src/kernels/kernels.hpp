@@ -109,7 +109,7 @@ struct MapArgs {
   // balanced reduce's plan (ReduceArgs::bucket_w)
   uint32_t* bucket_w;
 };
-// Reduce cost of a 24-byte record relative to a Rec16 one in the balanced
+// Reduce cost of a 24-byte record relative to a Rec16 one in the dispatch
 // plan: 24-byte runs carry the LONG words, whose byte comparison (a random
 // 64-byte text read) costs ~10-20x a Rec16 merge (profiles/r5_reduce_balance.md)
 constexpr uint32_t RED_W24 = 12;
@@ -199,13 +199,11 @@ struct ReduceArgs {
   // occupied rows to part slot (b + B q); the last quarter of a bucket to finish
   // merges the other partials into its own table and stores the slice.
   uint32_t nq;
-  // Balanced reduce (nullable: the uniform split above): the map's per-bucket
-  // weights (MapArgs::bucket_w; record buckets == table buckets).  The grid's
-  // G blocks cut the buckets' concatenated weight W (+ceil(G / buckets) per bucket) into G equal
-  // intervals: block i takes [W i / G, W (i + 1) / G) — a tail of one bucket,
-  // whole buckets, a head of another — as record ranges of the buckets'
-  // concatenated runs; a bucket cut into pieces is merged by its last piece to
-  // finish (partial slots 2 i / 2 i + 1, done[b] counts the pieces).
+  // Dispatch plan (nullable: one block per bucket / the uniform split above):
+  // the map's per-bucket weights (MapArgs::bucket_w; record buckets == table
+  // buckets >= CUs, nq = 1).  Heavy buckets are split into quarters and the
+  // pieces dispatched heaviest first (reduce.hip lpt_piece); a piece's partial
+  // slot is its block index.
   const uint32_t* bucket_w;
   struct Parts {
     uint64_t *k0, *k1, *cnt, *first, *soff;  // [(b + B q) * TAB_SLOTS + i] rows
@@ -215,11 +213,11 @@ struct ReduceArgs {
     uint32_t* qslen;
     uint32_t* done;                           // [b] quarters arrived (zeroed; the last resets it)
   } part;
-  uint32_t part_slots;  // partial-table slots allocated (the balanced plan needs 2 x its grid)
+  uint32_t part_slots;  // partial-table slots allocated (the dispatch plan needs one per block)
 };
 // Most reduce blocks per bucket (split reduce: fewer table buckets than CUs).
 constexpr uint32_t RED_SPLIT_MAX_Q = 16;
-// launch_reduce_planned: the balanced reduce over `grid` blocks (ReduceArgs::bucket_w set)
+constexpr uint32_t RED_PLAN_EXTRA = 64;  // dispatch plan: blocks for split heavy buckets past one per bucket
 // Reduce diagnostic counters (src/kernels/reduce.hip built with -DWC_RED_STAMPS=1).
 constexpr int RED_BLK_WORDS = 5;
 enum : int { RS_RECORDS = 0, RS_SLOW_LANES, RS_SLOW_WAVES, RS_PROBE_ITERS, RS_CAS_FAIL, RS_PENDING, RS_CLAIMS,
@@ -241,8 +239,9 @@ struct ZeroList;
 // z: the pass's zeroing, applied before the map (inside the sampling launch when `sample`)
 void launch_map(const MapArgs& a, const HotArgs& h, uint32_t map_blocks, hipStream_t s, bool sample,
                 const ZeroList& z);
-void launch_reduce(const ReduceArgs& a, hipStream_t s);
-void launch_reduce_planned(const ReduceArgs& a, uint32_t grid, hipStream_t s);
+// extra: with ReduceArgs::bucket_w, blocks past one per bucket for the dispatch
+// plan's split heavy buckets (reduce.hip lpt_piece)
+void launch_reduce(const ReduceArgs& a, hipStream_t s, uint32_t extra = 0);
 void launch_table_split(const TableView& src, const TableView& dst, hipStream_t s);
 void launch_table_clear(const TableView& t, hipStream_t s);
 // debug: err (4 words, zeroed) <- the first bucket breaking the table's invariants (reduce.hip wc_check_table)

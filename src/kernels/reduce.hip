@@ -66,9 +66,6 @@ struct RedLds {
   uint32_t occupied;
   uint32_t overflow;
   uint32_t runcnt[RED_MAX_RUNS];  // packed record counts of this bucket's run in every map block
-                                  // (balanced reduce: the inclusive prefix of one record kind's counts)
-  uint32_t wpre[MAX_REC_BUCKETS + 1];  // balanced reduce: exclusive prefix of the bucket weights (+1 each)
-  uint32_t tot16, tot24;               // balanced reduce: the bucket's clamped record totals
   unsigned long long st[RED_STAMP_N];  // diagnostic counters (WC_RED_STAMPS builds only)
 };
 static_assert(sizeof(RedLds) <= 160 * 1024, "one reduce block per CU");
@@ -921,331 +918,95 @@ __device__ void write_partial(const RedLds& L, const ReduceArgs& a, const LongCt
   if (tid == 0) P.n[pb] = total;
 }
 
-// ------------------------------------------------------------ balanced reduce
-// (ReduceArgs::bucket_w; profiles/r5_reduce_balance.md).  One 1024-thread block
-// per CU cuts the buckets' concatenated weight — Rec16 records 1, 24-byte
-// records RED_W24 (they carry the LONG words), +1 per bucket — into G equal
-// intervals: every block does the same work however skewed the buckets are
-// (the uniform split's slowest block ran 1.19x the mean at v100k; at 30 % LONG
-// vocabulary one bucket ran 2.4x the mean, dispatched in the second wave).
-
-__device__ __forceinline__ uint32_t plan_lo(uint32_t W, uint32_t G, uint32_t i) {
-  return (uint32_t)(((uint64_t)W * i) / G);
-}
-// The block whose interval holds weight position y < W.
-__device__ __forceinline__ uint32_t plan_block(uint32_t W, uint32_t G, uint32_t y) {
-  uint32_t i = (uint32_t)(((uint64_t)y * G) / W);
-  while (i + 1 < G && plan_lo(W, G, i + 1) <= y) ++i;
-  while (i > 0 && plan_lo(W, G, i) > y) --i;
-  return i;
-}
-// The bucket holding weight position y < W: the largest b with wpre[b] <= y
-// (every bucket weighs >= 1, so it is unique).
-__device__ __forceinline__ uint32_t plan_bucket(const uint32_t* wpre, uint32_t nb, uint32_t y) {
-  uint32_t lo = 0, hi = nb - 1;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi + 1) >> 1;
-    if (wpre[mid] <= y) lo = mid;
-    else hi = mid - 1;
+// Exclusive block-wide prefix of a 64-bit value per thread (every thread calls).
+__device__ __forceinline__ uint64_t block_scan_excl64(uint64_t v, uint64_t& total) {
+  __shared__ uint64_t ws[RED_THREADS / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t incl = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
   }
-  return lo;
-}
-
-// Inclusive prefix over the map blocks of bucket rb's clamped record counts of
-// one kind into L.runcnt (runs past the last map block repeat the total);
-// L.tot16 / L.tot24 = both kinds' totals.  Every thread calls.
-template <bool R16>
-__device__ __forceinline__ void runs_prefix(RedLds& L, const ReduceArgs& a, uint32_t rb, uint32_t nrb, uint32_t sub) {
-  static_assert(RED_MAX_RUNS == RED_THREADS, "one run per thread");
-  const int tid = threadIdx.x;
-  uint32_t c16 = 0, c24 = 0;
-  if ((uint32_t)tid < a.map_blocks) {
-    const uint32_t packed = a.rec.count[(size_t)tid * nrb + rb];
-    c16 = min(packed & 0xFFFFu, sub);
-    c24 = min(packed >> 16, sub);
-  }
-  uint32_t t16, t24;
-  const uint32_t e16 = block_scan_excl(c16, t16);
-  const uint32_t e24 = block_scan_excl(c24, t24);
-  L.runcnt[tid] = R16 ? e16 + c16 : e24 + c24;
-  if (tid == 0) {
-    L.tot16 = t16;
-    L.tot24 = t24;
+  if (lane == 63) ws[wave] = incl;
+  __syncthreads();
+  uint64_t before = 0;
+  total = 0;
+  for (int w = 0; w < RED_THREADS / 64; ++w) {
+    before += w < wave ? ws[w] : 0ull;
+    total += ws[w];
   }
   __syncthreads();
+  return before + incl - v;
 }
 
-// Records [T0, T1) of one kind of bucket rb's runs concatenated in map-block
-// order (L.runcnt: their inclusive prefix): batches of U x 64 consecutive
-// records, each loaded one batch ahead of its merge (as merge_stream).
-template <bool R16, int U, class RecT>
-__device__ __forceinline__ void merge_range(RedLds& L, const ReduceArgs& a, uint32_t b, const RecT* recs, uint32_t nrb,
-                                            uint32_t rb, uint32_t sub, uint32_t T0, uint32_t T1, uint32_t& claims) {
-  constexpr uint32_t B = U * 64;
-  if (T0 >= T1) return;
-  const uint32_t lane = threadIdx.x & 63, P = a.map_blocks;
-  const uint32_t D = nrb * sub, C0 = rb * sub;  // run p's first record: C0 + p D (< record capacity < 2^32)
-  uint32_t j = 0;                               // the run holding the batch start (wave-uniform, advances)
-  auto pre = [&](uint32_t k) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)L.runcnt[k]); };
-  auto locate = [&](uint32_t T, uint32_t (&idx)[U], bool (&valid)[U]) {
-    while (j + 1 < P && pre(j) <= T) ++j;
-    const uint32_t adj = C0 + j * D - (j ? pre(j - 1) : 0u);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t t = T + u * 64 + lane;
-      idx[u] = t + adj;
-      valid[u] = t < T1;
-    }
-    for (uint32_t jj = j + 1; jj < P; ++jj) {  // runs starting inside this batch (usually 0-2)
-      const uint32_t ej = pre(jj - 1);
-      if (ej >= T + B || ej >= T1) break;
-      const uint32_t aj = C0 + jj * D - ej;
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (T + u * 64 + lane >= ej) idx[u] = T + u * 64 + lane + aj;
-    }
-  };
-  auto load = [&](RecT (&rr)[U], const uint32_t (&idx)[U], const bool (&valid)[U]) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) rr[u] = recs[valid[u] ? idx[u] : C0];  // C0: inside the store
-  };
-  RecT ra[U], rb2[U];
-  uint32_t ia[U], ib[U];
-  bool va[U], vb[U];
-  locate(T0, ia, va);
-  load(ra, ia, va);
-  for (uint32_t T = T0;; T += 2 * B) {  // unrolled by two: the register sets swap roles without copies
-    const bool more = T + B < T1;
-    if (more) {
-      locate(T + B, ib, vb);
-      load(rb2, ib, vb);
-    }
-    merge_batch<R16, U>(L, a, b, ra, va, ia, 0u, claims);
-    if (!more) return;
-    const bool more2 = T + 2 * B < T1;
-    if (more2) {
-      locate(T + 2 * B, ia, va);
-      load(ra, ia, va);
-    }
-    merge_batch<R16, U>(L, a, b, rb2, vb, ib, 0u, claims);
-    if (!more2) return;
+// The reduce's dispatch plan for tables of >= CUs buckets (ReduceArgs::
+// bucket_w; profiles/r5_reduce_balance.md): every block derives the same plan
+// from the map's per-bucket weights.  A bucket above 1.5x the mean weight is
+// split into ceil(w / (1.1 mean)) pieces (the split reduce's quarters, <=
+// RED_SPLIT_MAX_Q, as long as the extra pieces fit the grid), and the pieces
+// are dispatched heaviest first (8 classes of a quarter mean each, then bucket
+// order): with 2+ waves of blocks per CU, the one bucket at 2.4x the mean no
+// longer starts in the second wave.  Block i -> (bucket, piece, pieces, the
+// bucket's first piece = the block index of its quarter 0); false: no piece.
+__device__ __forceinline__ bool lpt_piece(const ReduceArgs& a, uint32_t& b, uint32_t& q, uint32_t& nq, uint32_t& base) {
+  __shared__ uint32_t pl[4];
+  const uint32_t tid = threadIdx.x, nb = 1u << a.tab.log2_buckets, i = blockIdx.x;
+  const uint32_t w = tid < nb ? a.bucket_w[tid] + 1u : 0u;
+  uint32_t W;
+  (void)block_scan_excl(w, W);
+  const uint64_t wn = (uint64_t)w * nb;  // w / mean = wn / W
+  uint32_t n = tid < nb ? 1u : 0u;
+  if (tid < nb && 2 * wn > 3ull * W) n = (uint32_t)min<uint64_t>(RED_SPLIT_MAX_Q, (10 * wn + 11ull * W - 1) / (11ull * W));
+  uint32_t extra;
+  (void)block_scan_excl(n > 1 ? n - 1 : 0u, extra);
+  if (nb + extra > gridDim.x && tid < nb) n = 1;  // no room for the extra pieces: order only
+  // class of the piece weight in quarter means (7: >= 1.75 mean), heaviest first
+  const uint32_t cls = tid < nb ? (uint32_t)min<uint64_t>(7, 4 * wn / ((uint64_t)W * n)) : 0u;
+  // pieces before b inside its class: two 64-bit scans of 16-bit per-class counters
+  const uint64_t v = (uint64_t)n << (16 * (cls & 3));
+  uint64_t tlo, thi;
+  const uint64_t plo = block_scan_excl64(cls < 4 ? v : 0ull, tlo);
+  const uint64_t phi = block_scan_excl64(cls >= 4 ? v : 0ull, thi);
+  uint32_t before = 0;  // pieces of the heavier classes
+  for (uint32_t k = 7; k > cls; --k) before += (uint32_t)(((k < 4 ? tlo : thi) >> (16 * (k & 3))) & 0xFFFFu);
+  const uint32_t mine = (uint32_t)(((cls < 4 ? plo : phi) >> (16 * (cls & 3))) & 0xFFFFu);
+  const uint32_t first = before + mine;
+  if (tid == 0) pl[0] = ~0u;
+  __syncthreads();
+  if (tid < nb && first <= i && i < first + n) {
+    pl[0] = tid;
+    pl[1] = i - first;
+    pl[2] = n;
+    pl[3] = first;
   }
-}
-
-// More LONG records than the LDS queue holds: the wave re-scans its 24-byte
-// range [s0, s1) (L.runcnt: the 24-byte prefix) and merges its LONG records 64
-// at a time (as long_stream).
-__device__ __forceinline__ void long_range(RedLds& L, const ReduceArgs& a, const LongCtx& c, uint32_t wave, uint32_t nrb,
-                                           uint32_t rb, uint32_t sub, uint32_t s0, uint32_t s1, uint32_t& claims) {
-  const uint32_t lane = threadIdx.x & 63, P = a.map_blocks;
-  const uint32_t D = nrb * sub, C0 = rb * sub;
-  uint32_t* wl = L.longq + wave * 128;
-  auto wsync = [] {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  };
-  auto merge_first = [&](uint32_t k) {  // wl[0, k), one per lane
-    wsync();
-    int s = -1;
-    uint64_t cnt = 0, first = ~0ull;
-    if (lane < k) {
-      const Rec r = a.rec.recs[wl[lane]];
-      const uint32_t off = (uint32_t)r.co;
-      bool cl;
-      s = find_long(L, c, place_hash(r.k0, r.k1), r.k0, r.k1, off, cl);
-      claims += cl ? 1u : 0u;
-      cnt = r.co >> 32;
-      first = a.chunk_base + off;
-    }
-    wave_add_long(L, s, cnt, first);
-    wsync();
-  };
-  auto pre = [&](uint32_t k) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)L.runcnt[k]); };
-  uint32_t j = 0, cnt = 0;
-  for (uint32_t T = s0; T < s1; T += 64) {
-    while (j + 1 < P && pre(j) <= T) ++j;
-    const uint32_t t = T + lane;
-    uint32_t idx = t + C0 + j * D - (j ? pre(j - 1) : 0u);
-    for (uint32_t jj = j + 1; jj < P; ++jj) {
-      const uint32_t ej = pre(jj - 1);
-      if (ej >= T + 64 || ej >= s1) break;
-      if (t >= ej) idx = t + C0 + jj * D - ej;
-    }
-    bool isl = false;
-    if (t < s1) isl = key_is_hashed(a.rec.recs[idx].k1);
-    const uint64_t m = __ballot(isl);
-    if (isl) wl[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = idx;
-    cnt += (uint32_t)__popcll(m);
-    if (cnt >= 64) {
-      merge_first(64);
-      const uint32_t rest = cnt - 64, moved = lane < rest ? wl[64 + lane] : 0u;
-      wsync();
-      if (lane < rest) wl[lane] = moved;
-      cnt = rest;
-    }
-  }
-  if (cnt) merge_first(cnt);
-}
-
-// Block-uniform values read from LDS: in SGPRs, not VGPRs (the compiler cannot
-// tell they are uniform; as VGPRs they are live across the record streams).
-__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-
-__device__ __forceinline__ void reduce_planned(RedLds& L, const ReduceArgs& a) {
-  const int tid = threadIdx.x, wave = tid >> 6, nwaves = RED_THREADS / 64;
-  const uint32_t nb = 1u << a.tab.log2_buckets, G = gridDim.x, i = blockIdx.x;
-  const uint32_t sub = a.rec.subcap;
-  {  // the plan: exclusive prefix of the bucket weights, each + ceil(G / nb): every bucket's
-     // interval is non-empty and W >= G, so every block's interval is too — a
-     // bucket's pieces are then exactly the blocks [first, last] its interval
-     // meets, and all of them arrive on its counter (an empty block would not)
-    const uint32_t pad = (G + nb - 1) / nb;
-    const uint32_t w = (uint32_t)tid < nb ? a.bucket_w[tid] + pad : 0u;
-    uint32_t tot;
-    const uint32_t ex = block_scan_excl(w, tot);
-    if ((uint32_t)tid < nb) L.wpre[tid] = ex;
-    if (tid == 0) L.wpre[nb] = tot;
-    if (WC_RED_STAMPS && tid < RED_STAMP_N) L.st[tid] = 0;
-    __syncthreads();
-  }
-  const uint32_t W = uni(L.wpre[nb]);
-  const uint32_t lo = plan_lo(W, G, i), hi = plan_lo(W, G, i + 1);
-  if (lo >= hi) return;
-  const uint32_t bf = uni(plan_bucket(L.wpre, nb, lo)), bl = uni(plan_bucket(L.wpre, nb, hi - 1));
-  const uint64_t t_start = WC_RED_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
-  const uint64_t rt_start = WC_RED_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;
-  unsigned long long s16 = 0, s24 = 0;  // stamps: this block's records
-  for (uint32_t b = bf; b <= bl; ++b) {
-    const uint32_t wb0 = uni(L.wpre[b]), wb1 = uni(L.wpre[b + 1]);
-    const uint32_t fb = plan_block(W, G, wb0), lb = plan_block(W, G, wb1 - 1);
-    const bool first = fb == i, last = lb == i, whole = first && last;
-    const uint32_t x0 = max(lo, wb0) - wb0, x1 = min(hi, wb1) - wb0;  // this piece, in the bucket's weight units
-    const uint32_t slot = 2 * i + (b == bf ? 0u : 1u);                 // partial slot of (block i, bucket b)
-    load_slice(L, a.tab, b, !first);  // the bucket's first piece continues the running slice
-    if (tid == 0) {
-      L.occupied = first ? a.tab.occupancy[b] : 0u;
-      L.overflow = 0;
-      L.nlong = 0;
-    }
-    runs_prefix<true>(L, a, b, nb, sub);
-    const uint32_t n16 = uni(L.tot16), n24 = uni(L.tot24);
-    // weight -> record ranges: [0, n16) Rec16 records of weight 1, then n24 of
-    // weight RED_W24, then the bucket's pad (no records); the first and last
-    // pieces take the ends exactly
-    auto r24 = [&](uint32_t x) {
-      return x <= n16 ? 0u : min(n24, (x - n16 + RED_W24 - 1) / RED_W24);
-    };
-    const uint32_t a16 = first ? 0u : min(x0, n16), b16 = last ? n16 : min(x1, n16);
-    const uint32_t a24 = first ? 0u : r24(x0), b24 = last ? n24 : r24(x1);
-    uint32_t claims = 0;
-    merge_range<true, RED_UNROLL>(L, a, b, a.rec.recs16, nb, b, sub,
-                                  a16 + (uint32_t)((uint64_t)(b16 - a16) * wave / nwaves),
-                                  a16 + (uint32_t)((uint64_t)(b16 - a16) * (wave + 1) / nwaves), claims);
-    __syncthreads();  // every wave is done with the Rec16 prefix
-    runs_prefix<false>(L, a, b, nb, sub);
-    const uint32_t v0 = a24 + (uint32_t)((uint64_t)(b24 - a24) * wave / nwaves);
-    const uint32_t v1 = a24 + (uint32_t)((uint64_t)(b24 - a24) * (wave + 1) / nwaves);
-    merge_range<false, RED_UNROLL_24>(L, a, b, a.rec.recs, nb, b, sub, v0, v1, claims);
-    __syncthreads();  // every LONG record is queued (or counted past the queue)
-    if (WC_RED_STAMPS && tid == 0) L.st[RS_NLONG] += L.nlong;
-    s16 += b16 - a16;
-    s24 += b24 - a24;
-    // LONG words' arena references: the slice's (first piece) or this piece's scratch
-    const size_t sbase = (size_t)b * TAB_SLOTS, qbase = (size_t)slot * TAB_SLOTS;
-    const LongCtx lc{a.text, a.avail_len, a.arena.bytes, first ? a.tab.sref_off + sbase : a.part.qsoff + qbase,
-                     first ? a.tab.sref_len + sbase : a.part.qslen + qbase};
-    const uint32_t nlong = uni(L.nlong);
-    if (nlong) {
-      if (nlong <= LONGQ) long_queue(L, a, lc, nlong, claims);
-      else long_range(L, a, lc, wave, nb, b, sub, v0, v1, claims);
-    }
-    for (int o = 32; o > 0; o >>= 1) claims += __shfl_down(claims, o);
-    if ((tid & 63) == 0 && claims) atomicAdd(&L.occupied, claims);
-    __syncthreads();
-    if (tid == 0 && L.occupied > (uint32_t)TAB_MAX_OCC) L.overflow = 1;  // too full: split and re-run
-    __syncthreads();
-    const bool ovf = uni(L.overflow) != 0;
-    if (ovf && tid == 0) {
-      a.bucket_overflow[b] = 1;
-      atomicOr(&a.flags[FLAG_TABLE_OVF], 1u);
-    }
-    bool store = !ovf;
-    if (!whole) {
-      // every piece publishes its partial table; the last to finish merges the
-      // others' into its own LDS table and stores the bucket
-      if (!ovf) write_partial(L, a, lc, slot);
-      store = split_arrive_last(L, a, b, lb - fb + 1);
-      if (store) {
-        for (uint32_t k = tid; fb + k <= lb; k += RED_THREADS) {  // the other pieces' slots
-          const uint32_t jb = fb + k;
-          if (jb == i) continue;
-          const uint32_t js = 2 * jb + (b == plan_bucket(L.wpre, nb, plan_lo(W, G, jb)) ? 0u : 1u);
-          L.longq[jb < i ? k : k - 1] = js;
-        }
-        __syncthreads();
-        store = merge_partials(L, a, lc, b, L.longq, lb - fb);
-      }
-      if (store && !first) {  // the merged table's LONG references: piece scratch -> the slice
-        for (int s = tid; s < TAB_SLOTS; s += RED_THREADS) {
-          if (slot_tag(L.grp, s) > TAG_PENDING && key_is_hashed(slot_k1(L.grp, s))) {
-            a.tab.sref_off[sbase + s] = lc.sref_off[s];
-            a.tab.sref_len[sbase + s] = lc.sref_len[s];
-          }
-        }
-        __syncthreads();
-      }
-    }
-    if (store) {
-      settle_new_long(L, a, b);
-      store_slice(L, a.tab, b);
-      add_fo_hist(L, a);
-      add_bm_bits(L, a);
-      if (tid == 0) {
-        a.tab.occupancy[b] = L.occupied;
-        atomicMax(&a.flags[FLAG_MAX_OCC], L.occupied);
-      }
-    }
-    __syncthreads();  // the next bucket reuses the LDS table
-  }
-  if (WC_RED_STAMPS && a.stamps) {
-    if ((tid & 63) == 0) atomicAdd(&L.st[RS_T_WAVE], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
-    __syncthreads();
-    if (tid == 0) {
-      L.st[RS_BLOCKS] = 1;
-      L.st[RS_T_BLKMAX] = 0;
-      atomicMax(&a.stamps[RS_T_BLKMAX], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
-    }
-    __syncthreads();
-    if (tid < RED_STAMP_N) atomicAdd(&a.stamps[tid], L.st[tid]);
-    if (a.blk && tid == 0) {
-      unsigned long long* r = a.blk + (size_t)RED_BLK_WORDS * blockIdx.x;
-      r[0] = bf | ((unsigned long long)(bl - bf + 1) << 32);  // first bucket | buckets touched
-      r[1] = rt_start;
-      r[2] = __builtin_amdgcn_s_memrealtime();
-      r[3] = s16 | (s24 << 32);
-      r[4] = L.st[RS_NLONG];
-    }
-  }
-}
-
-// Its own kernel: inlined beside the uniform split, the two paths' register
-// allocation spilled (and a non-inlined callee taking the arguments by
-// reference moves the argument block to scratch).
-__global__ void __launch_bounds__(RED_THREADS) wc_reduce_balanced(ReduceArgs a) {
-  __shared__ RedLds L;
-  if (a.flags[FLAG_REGION_OVF]) return;  // shuffle output incomplete: host re-runs the chunk
-  reduce_planned(L, a);
+  __syncthreads();
+  if (pl[0] == ~0u) return false;
+  b = pl[0];
+  q = pl[1];
+  nq = pl[2];
+  base = pl[3];
+  return true;
 }
 
 __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   __shared__ RedLds L;
-  // block b + B q: bucket b, quarter q (split reduce, a.nq > 1) of the map blocks' runs
-  const uint32_t b = blockIdx.x & ((1u << a.tab.log2_buckets) - 1u), q = blockIdx.x >> a.tab.log2_buckets;
-  if (a.bucket_enable && !a.bucket_enable[b]) return;
   if (a.flags[FLAG_REGION_OVF]) return;  // shuffle output incomplete: host re-runs the chunk
+  // block b + B q: bucket b, quarter q (split reduce, a.nq > 1) of the map blocks' runs;
+  // with bucket weights, the dispatch plan's piece instead (lpt_piece)
+  uint32_t b = blockIdx.x & ((1u << a.tab.log2_buckets) - 1u), q = blockIdx.x >> a.tab.log2_buckets;
+  uint32_t nq = a.nq, pbase = b, pstep = 1u << a.tab.log2_buckets;  // partial slot of quarter q': pbase + q' pstep
+  if (a.bucket_w) {
+    uint32_t base;
+    if (!lpt_piece(a, b, q, nq, base)) return;
+    b = __builtin_amdgcn_readfirstlane(b);
+    q = __builtin_amdgcn_readfirstlane(q);
+    nq = __builtin_amdgcn_readfirstlane(nq);
+    pbase = __builtin_amdgcn_readfirstlane(base);
+    pstep = 1;
+  }
+  if (a.bucket_enable && !a.bucket_enable[b]) return;
   const int tid = threadIdx.x, wave = tid >> 6, nwaves = RED_THREADS / 64;
-  const bool split = a.nq > 1;
+  const bool split = nq > 1;
   load_slice(L, a.tab, b, q != 0);  // quarters q > 0 start empty
   {
     const uint32_t rb0 = b & ((1u << a.log2_rec_buckets) - 1u), nrb0 = 1u << a.log2_rec_buckets;
@@ -1268,7 +1029,7 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   // one contiguous run per map block: sub-region (p, rb) of the record store;
   // the wave streams the 16-byte records of its runs, then the 24-byte ones
   uint32_t claims = 0;
-  const uint32_t p0 = q + a.nq * wave, pstride = a.nq * nwaves;  // this wave's runs
+  const uint32_t p0 = q + nq * wave, pstride = nq * nwaves;  // this wave's runs
   merge_stream<true, RED_UNROLL>(L, a, b, a.rec.recs16, p0, pstride, nrb, rb, (uint32_t)sub, shift, claims);
   merge_stream<false, RED_UNROLL_24>(L, a, b, a.rec.recs, p0, pstride, nrb, rb, (uint32_t)sub, shift, claims);
   __syncthreads();  // every LONG record is queued (or counted past the queue)
@@ -1302,12 +1063,12 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
     // every quarter publishes its partial table; the last to arrive merges the
     // others into its own LDS table and stores the bucket
     if (!L.overflow) write_partial(L, a, lc, blockIdx.x);
-    store = split_arrive_last(L, a, b, a.nq);
+    store = split_arrive_last(L, a, b, nq);
     if (store) {
       if (tid == 0) {  // the other quarters' partial slots
         uint32_t k = 0;
-        for (uint32_t qq = 0; qq < a.nq; ++qq)
-          if (qq != q) L.longq[k++] = b + (1u << a.tab.log2_buckets) * qq;
+        for (uint32_t qq = 0; qq < nq; ++qq)
+          if (qq != q) L.longq[k++] = pbase + pstep * qq;
         L.nlong = k;  // scratch: the slot count
       }
       __syncthreads();
@@ -1346,7 +1107,7 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
     if (a.blk && tid == 0) {  // where the reduce's time goes, block by block
       const uint32_t nrb0 = 1u << a.log2_rec_buckets;
       unsigned long long n16 = 0, n24 = 0;
-      for (uint32_t p = q; p < a.map_blocks; p += a.nq) {
+      for (uint32_t p = q; p < a.map_blocks; p += nq) {
         n16 += L.runcnt[p] & 0xFFFFu;
         n24 += L.runcnt[p] >> 16;
       }
@@ -1579,17 +1340,13 @@ void launch_bucket_offsets(const uint32_t* occupancy, uint32_t nb, uint64_t* buc
   hipLaunchKernelGGL(dev::wc_bucket_offsets, dim3(1), dim3(1024), 0, s, occupancy, nb, bucket_off, n);
 }
 
-void launch_reduce(const ReduceArgs& a, hipStream_t s) {
+void launch_reduce(const ReduceArgs& a, hipStream_t s, uint32_t extra) {
   WC_CHECK(a.nq >= 1 && a.nq <= RED_SPLIT_MAX_Q, "reduce: 1..RED_SPLIT_MAX_Q blocks per bucket");
-  hipLaunchKernelGGL(dev::wc_reduce_buckets, dim3((1u << a.tab.log2_buckets) * a.nq), dim3(RED_THREADS), 0, s, a);
-}
-
-void launch_reduce_planned(const ReduceArgs& a, uint32_t grid, hipStream_t s) {
-  WC_CHECK(a.bucket_w && (a.tab.log2_buckets == a.log2_rec_buckets) && a.map_blocks <= (uint32_t)RED_MAX_RUNS &&
-               (1u << a.tab.log2_buckets) <= (uint32_t)MAX_REC_BUCKETS && 2 * grid <= a.part_slots &&
-               a.part_slots >= (1u << a.tab.log2_buckets),
-           "balanced reduce: one record bucket per table bucket, <= RED_MAX_RUNS map blocks, 2 partial slots per block");
-  hipLaunchKernelGGL(dev::wc_reduce_balanced, dim3(grid), dim3(RED_THREADS), 0, s, a);
+  const uint32_t grid = (1u << a.tab.log2_buckets) * a.nq + (a.bucket_w ? extra : 0u);
+  WC_CHECK(!a.bucket_w || (a.nq == 1 && a.tab.log2_buckets == a.log2_rec_buckets && !a.bucket_enable &&
+                           (1u << a.tab.log2_buckets) <= (uint32_t)MAX_REC_BUCKETS && grid <= a.part_slots),
+           "reduce dispatch plan: one record bucket per table bucket, <= MAX_REC_BUCKETS, a partial slot per block");
+  hipLaunchKernelGGL(dev::wc_reduce_buckets, dim3(grid), dim3(RED_THREADS), 0, s, a);
 }
 
 void launch_table_split(const TableView& src, const TableView& dst, hipStream_t s) {
