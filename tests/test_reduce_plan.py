@@ -1,67 +1,68 @@
-"""CPU mirror of the balanced reduce's plan (src/kernels/reduce.hip
-reduce_planned / plan_lo / plan_block / the weight -> record-range map): with
-each bucket padded by ceil(G / buckets), every block's weight interval is
-non-empty, a bucket's pieces are exactly the blocks [first, last] its interval
-meets (so the piece counter the last piece waits for is reached), and the
-pieces' record ranges cover each bucket's Rec16 and 24-byte records exactly
-once.  (The first GPU run without the pad lost every bucket of a 56-byte input:
-blocks with empty intervals never arrived.)"""
+"""CPU mirror of the reduce's dispatch plan (src/kernels/reduce.hip lpt_piece):
+every block derives, from the map's per-bucket weights, which bucket piece it
+reduces.  Checked here for random and skewed weights: every bucket is reduced
+exactly once — all its pieces (quarters) present, each on one block, a
+bucket's pieces on consecutive blocks starting at its `base` (the partial
+slots the last piece merges), nothing past the grid — heavy buckets are split
+only while the extra pieces fit the grid, and pieces run heaviest class first."""
 import random
 
-W24 = 12  # kernels.hpp RED_W24
+RED_SPLIT_MAX_Q = 16
 
 
-def plan_lo(W, G, i):
-    return W * i // G
+def plan(weights, grid):
+    nb = len(weights)
+    w = [x + 1 for x in weights]
+    W = sum(w)
+    n = []
+    for x in w:
+        wn = x * nb
+        k = 1
+        if 2 * wn > 3 * W:
+            k = min(RED_SPLIT_MAX_Q, (10 * wn + 11 * W - 1) // (11 * W))
+        n.append(k)
+    extra = sum(k - 1 for k in n)
+    if nb + extra > grid:
+        n = [1] * nb
+    cls = [min(7, 4 * x * nb // (W * k)) for x, k in zip(w, n)]
+    tot = [0] * 8
+    first = [0] * nb
+    within = [0] * 8
+    for b in range(nb):
+        first[b] = within[cls[b]]
+        within[cls[b]] += n[b]
+        tot[cls[b]] += n[b]
+    base = []
+    for b in range(nb):
+        before = sum(tot[k] for k in range(7, cls[b], -1))
+        base.append(before + first[b])
+    blocks = {}
+    for i in range(grid):
+        hit = [(b, i - base[b], n[b], base[b]) for b in range(nb) if base[b] <= i < base[b] + n[b]]
+        assert len(hit) <= 1
+        if hit:
+            blocks[i] = hit[0]
+    return blocks, n, cls
 
 
-def plan_block(W, G, y):
-    i = y * G // W
-    while i + 1 < G and plan_lo(W, G, i + 1) <= y:
-        i += 1
-    while i > 0 and plan_lo(W, G, i) > y:
-        i -= 1
-    return i
-
-
-def r24(x, n16, n24):
-    return 0 if x <= n16 else min(n24, (x - n16 + W24 - 1) // W24)
-
-
-def test_plan_pieces_and_ranges():
-    rnd = random.Random(5)
-    for _ in range(300):
-        nb = rnd.choice([64, 128, 256, 512])
-        G = rnd.choice([1, 3, 64, 256, 300])
-        n16s = [rnd.choice([0, 0, 1, 7, 300, 5000]) for _ in range(nb)]
-        n24s = [rnd.choice([0, 0, 1, 3, 40]) for _ in range(nb)]
-        pad = (G + nb - 1) // nb
-        w = [a + W24 * b + pad for a, b in zip(n16s, n24s)]
-        pre = [0]
-        for x in w:
-            pre.append(pre[-1] + x)
-        W = pre[-1]
-        assert W >= G
-        arrivals = [0] * nb
-        got16 = [[] for _ in range(nb)]
-        got24 = [[] for _ in range(nb)]
-        for i in range(G):
-            lo, hi = plan_lo(W, G, i), plan_lo(W, G, i + 1)
-            assert lo < hi
-            for b in range(nb):
-                if not (pre[b] < hi and pre[b + 1] > lo):
-                    continue
-                arrivals[b] += 1
-                fb, lb = plan_block(W, G, pre[b]), plan_block(W, G, pre[b + 1] - 1)
-                first, last = fb == i, lb == i
-                x0, x1 = max(lo, pre[b]) - pre[b], min(hi, pre[b + 1]) - pre[b]
-                n16, n24 = n16s[b], n24s[b]
-                a16, b16 = (0 if first else min(x0, n16)), (n16 if last else min(x1, n16))
-                a24, b24 = (0 if first else r24(x0, n16, n24)), (n24 if last else r24(x1, n16, n24))
-                got16[b] += range(a16, b16)
-                got24[b] += range(a24, b24)
-        for b in range(nb):
-            fb, lb = plan_block(W, G, pre[b]), plan_block(W, G, pre[b + 1] - 1)
-            assert arrivals[b] == lb - fb + 1
-            assert sorted(got16[b]) == list(range(n16s[b]))
-            assert sorted(got24[b]) == list(range(n24s[b]))
+def test_dispatch_plan():
+    rnd = random.Random(7)
+    for trial in range(300):
+        nb = rnd.choice([256, 512])
+        extra = rnd.choice([0, 16, 64])
+        if trial % 3 == 0:  # skewed: a few buckets far above the mean (LONG-heavy buckets)
+            weights = [rnd.randint(900, 1100) for _ in range(nb)]
+            for _ in range(rnd.randint(1, 6)):
+                weights[rnd.randrange(nb)] *= rnd.choice([2, 3, 8, 40])
+        else:
+            weights = [rnd.choice([0, 1, 50, 1000, 1200]) for _ in range(nb)]
+        blocks, n, cls = plan(weights, nb + extra)
+        seen = {}
+        for i, (b, q, nq, base) in blocks.items():
+            assert 0 <= q < nq and i == base + q
+            seen.setdefault(b, set()).add(q)
+        assert sorted(seen) == list(range(nb))
+        assert all(seen[b] == set(range(n[b])) for b in range(nb))
+        assert sum(n) <= nb + extra
+        order = [cls[blocks[i][0]] for i in sorted(blocks)]
+        assert order == sorted(order, reverse=True)  # heaviest class first
