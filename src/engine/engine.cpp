@@ -345,13 +345,15 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
       }
     }
   }
-  // the reduce's dispatch plan (heavy buckets split, heaviest first) for
-  // tables of >= CUs buckets: one record bucket per table bucket (no split
-  // since the records were bucketed), its weights from this map
+  // the reduce's dispatch plan (pieces sized by the buckets' weights,
+  // heaviest first): one record bucket per table bucket (no split since the
+  // records were bucketed), its weights from this map.  Grid: 2 pieces per CU
+  // below CUs buckets, else one block per bucket + RED_PLAN_EXTRA
   const uint32_t nbk = 1u << table().log2_buckets;
-  const uint32_t plan_extra = std::min<uint32_t>(RED_PLAN_EXTRA, part_blocks - std::min(part_blocks, nbk));
-  const bool planned = red_plan && !red_q_force && red_q() == 1 && log2_rb == table().log2_buckets &&
-                       nbk <= (uint32_t)MAX_REC_BUCKETS && nbk + plan_extra <= part_blocks;
+  const uint32_t plan_grid = nbk < n_cu ? 2 * n_cu : nbk + RED_PLAN_EXTRA;
+  const bool planned = red_plan && !red_q_force && log2_rb == table().log2_buckets &&
+                       nbk <= (uint32_t)MAX_REC_BUCKETS && plan_grid <= part_blocks;
+  const uint32_t plan_extra = plan_grid - nbk;
   ZeroList z{};
   z.add(d_ctr, sizeof(DevCounters));
   if (planned) z.add(d_bucket_w, nbk * sizeof(uint32_t));
@@ -388,7 +390,8 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
                 avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
                 d_ctr->flags, d_bucket_ovf, nullptr, d_red_stamps, red_blk(), want_hist ? d_fo_hist : nullptr, fo_hist_m,
                 bm, bm ? bitmap_order_linecnt(bm, bm_end, 1) : nullptr, bm ? bitmap_order_ctl(bm, bm_end, 1) : nullptr,
-                bm ? (bm_end >> 1) + 1 : 0, 1u, red_q(), planned ? d_bucket_w : nullptr, part, part_blocks};
+                bm ? (bm_end >> 1) + 1 : 0, 1u, planned ? 1u : red_q(), planned ? d_bucket_w : nullptr, part,
+                part_blocks};
   if (planned && ra.blk) red_blk_grid = nbk + plan_extra;
   launch_reduce(ra, s, plan_extra);
   check_table("the reduce");

@@ -939,29 +939,39 @@ __device__ __forceinline__ uint64_t block_scan_excl64(uint64_t v, uint64_t& tota
   return before + incl - v;
 }
 
-// The reduce's dispatch plan for tables of >= CUs buckets (ReduceArgs::
-// bucket_w; profiles/r5_reduce_balance.md): every block derives the same plan
-// from the map's per-bucket weights.  A bucket above 1.5x the mean weight is
-// split into ceil(w / (1.1 mean)) pieces (the split reduce's quarters, <=
-// RED_SPLIT_MAX_Q, as long as the extra pieces fit the grid), and the pieces
-// are dispatched heaviest first (8 classes of a quarter mean each, then bucket
-// order): with 2+ waves of blocks per CU, the one bucket at 2.4x the mean no
-// longer starts in the second wave.  Block i -> (bucket, piece, pieces, the
-// bucket's first piece = the block index of its quarter 0); false: no piece.
+// The reduce's dispatch plan (ReduceArgs::bucket_w; profiles/r5_reduce_balance.md):
+// every block derives the same plan from the map's per-bucket weights.
+// * fewer buckets than the grid (the split reduce's regime): bucket b gets
+//   floor(w_b (G - B) / W) + 1 pieces (quarters, <= RED_SPLIT_MAX_Q) — pieces
+//   of about W / G each instead of CUs / B per bucket whatever its weight (the
+//   uniform split's slowest quarter ran 1.19x the mean at v100k);
+// * otherwise one piece per bucket, a bucket above 1.5x the mean weight split
+//   into ceil(w / (1.1 mean)) pieces while the extra ones fit the grid.
+// Pieces are dispatched heaviest first (8 classes of a quarter of the mean
+// piece each, then bucket order): with more pieces than CUs the heavy ones no
+// longer start in the last wave (at 30 % LONG vocabulary one bucket at 2.4x
+// the mean did).  Block i -> (bucket, piece, pieces, the block index of the
+// bucket's piece 0 = its partial slots); false: no piece.
 __device__ __forceinline__ bool lpt_piece(const ReduceArgs& a, uint32_t& b, uint32_t& q, uint32_t& nq, uint32_t& base) {
   __shared__ uint32_t pl[4];
-  const uint32_t tid = threadIdx.x, nb = 1u << a.tab.log2_buckets, i = blockIdx.x;
+  const uint32_t tid = threadIdx.x, nb = 1u << a.tab.log2_buckets, i = blockIdx.x, G = gridDim.x;
   const uint32_t w = tid < nb ? a.bucket_w[tid] + 1u : 0u;
   uint32_t W;
   (void)block_scan_excl(w, W);
   const uint64_t wn = (uint64_t)w * nb;  // w / mean = wn / W
   uint32_t n = tid < nb ? 1u : 0u;
-  if (tid < nb && 2 * wn > 3ull * W) n = (uint32_t)min<uint64_t>(RED_SPLIT_MAX_Q, (10 * wn + 11ull * W - 1) / (11ull * W));
-  uint32_t extra;
-  (void)block_scan_excl(n > 1 ? n - 1 : 0u, extra);
-  if (nb + extra > gridDim.x && tid < nb) n = 1;  // no room for the extra pieces: order only
-  // class of the piece weight in quarter means (7: >= 1.75 mean), heaviest first
-  const uint32_t cls = tid < nb ? (uint32_t)min<uint64_t>(7, 4 * wn / ((uint64_t)W * n)) : 0u;
+  if (tid < nb) {
+    if (nb < G) n = (uint32_t)min<uint64_t>(RED_SPLIT_MAX_Q, (uint64_t)w * (G - nb) / W + 1);
+    else if (2 * wn > 3ull * W) n = (uint32_t)min<uint64_t>(RED_SPLIT_MAX_Q, (10 * wn + 11ull * W - 1) / (11ull * W));
+  }
+  uint32_t P;
+  (void)block_scan_excl(n, P);
+  if (P > G) {  // no room for the extra pieces: one per bucket, order only
+    n = tid < nb ? 1u : 0u;
+    P = nb;
+  }
+  // class of the piece weight in quarters of the mean piece (7: >= 1.75x), heaviest first
+  const uint32_t cls = tid < nb ? (uint32_t)min<uint64_t>(7, 4ull * w * P / ((uint64_t)W * n)) : 0u;
   // pieces before b inside its class: two 64-bit scans of 16-bit per-class counters
   const uint64_t v = (uint64_t)n << (16 * (cls & 3));
   uint64_t tlo, thi;
@@ -1344,7 +1354,8 @@ void launch_reduce(const ReduceArgs& a, hipStream_t s, uint32_t extra) {
   WC_CHECK(a.nq >= 1 && a.nq <= RED_SPLIT_MAX_Q, "reduce: 1..RED_SPLIT_MAX_Q blocks per bucket");
   const uint32_t grid = (1u << a.tab.log2_buckets) * a.nq + (a.bucket_w ? extra : 0u);
   WC_CHECK(!a.bucket_w || (a.nq == 1 && a.tab.log2_buckets == a.log2_rec_buckets && !a.bucket_enable &&
-                           (1u << a.tab.log2_buckets) <= (uint32_t)MAX_REC_BUCKETS && grid <= a.part_slots),
+                           (1u << a.tab.log2_buckets) <= (uint32_t)MAX_REC_BUCKETS && grid <= a.part_slots &&
+                           (1u << a.tab.log2_buckets) <= (uint32_t)RED_THREADS),
            "reduce dispatch plan: one record bucket per table bucket, <= MAX_REC_BUCKETS, a partial slot per block");
   hipLaunchKernelGGL(dev::wc_reduce_buckets, dim3(grid), dim3(RED_THREADS), 0, s, a);
 }

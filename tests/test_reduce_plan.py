@@ -18,13 +18,16 @@ def plan(weights, grid):
     for x in w:
         wn = x * nb
         k = 1
-        if 2 * wn > 3 * W:
+        if nb < grid:
+            k = min(RED_SPLIT_MAX_Q, x * (grid - nb) // W + 1)
+        elif 2 * wn > 3 * W:
             k = min(RED_SPLIT_MAX_Q, (10 * wn + 11 * W - 1) // (11 * W))
         n.append(k)
-    extra = sum(k - 1 for k in n)
-    if nb + extra > grid:
+    P = sum(n)
+    if P > grid:
         n = [1] * nb
-    cls = [min(7, 4 * x * nb // (W * k)) for x, k in zip(w, n)]
+        P = nb
+    cls = [min(7, 4 * x * P // (W * k)) for x, k in zip(w, n)]
     tot = [0] * 8
     first = [0] * nb
     within = [0] * 8
@@ -48,8 +51,8 @@ def plan(weights, grid):
 def test_dispatch_plan():
     rnd = random.Random(7)
     for trial in range(300):
-        nb = rnd.choice([256, 512])
-        extra = rnd.choice([0, 16, 64])
+        nb = rnd.choice([64, 128, 256, 512])
+        extra = rnd.choice([0, 16, 64]) if nb >= 256 else 512 - nb
         if trial % 3 == 0:  # skewed: a few buckets far above the mean (LONG-heavy buckets)
             weights = [rnd.randint(900, 1100) for _ in range(nb)]
             for _ in range(rnd.randint(1, 6)):
@@ -64,5 +67,9 @@ def test_dispatch_plan():
         assert sorted(seen) == list(range(nb))
         assert all(seen[b] == set(range(n[b])) for b in range(nb))
         assert sum(n) <= nb + extra
+        if nb < 256 and trial % 3:  # the split regime: pieces of about W / grid each
+            W = sum(x + 1 for x in weights)
+            for b in range(nb):
+                assert (weights[b] + 1) / n[b] <= W / (nb + extra - nb) + 1 or n[b] == RED_SPLIT_MAX_Q
         order = [cls[blocks[i][0]] for i in sorted(blocks)]
         assert order == sorted(order, reverse=True)  # heaviest class first
