@@ -345,13 +345,15 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
       }
     }
   }
-  // the reduce's dispatch plan (pieces sized by the buckets' weights,
-  // heaviest first): one record bucket per table bucket (no split since the
-  // records were bucketed), its weights from this map.  Grid: 2 pieces per CU
-  // below CUs buckets, else one block per bucket + RED_PLAN_EXTRA
+  // the reduce's dispatch plan (heavy buckets split, pieces heaviest first)
+  // for tables of >= CUs buckets: one record bucket per table bucket (no
+  // split since the records were bucketed), its weights from this map.
+  // Below CUs buckets the uniform split stays: weight-sized pieces at 2 per CU
+  // cost 11 % more block time in partial tables than their balance saved
+  // (v100k reduce 0.244 -> 0.307 ms; profiles/r5_reduce_balance.md)
   const uint32_t nbk = 1u << table().log2_buckets;
-  const uint32_t plan_grid = nbk < n_cu ? 2 * n_cu : nbk + RED_PLAN_EXTRA;
-  const bool planned = red_plan && !red_q_force && log2_rb == table().log2_buckets &&
+  const uint32_t plan_grid = nbk + RED_PLAN_EXTRA;
+  const bool planned = red_plan && !red_q_force && nbk >= n_cu && log2_rb == table().log2_buckets &&
                        nbk <= (uint32_t)MAX_REC_BUCKETS && plan_grid <= part_blocks;
   const uint32_t plan_extra = plan_grid - nbk;
   ZeroList z{};
