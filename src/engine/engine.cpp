@@ -128,11 +128,12 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   rec_total = std::min<uint64_t>(rec_total, 0xFFFFFFFFull);  // record indices are 32-bit in the reducer
   // record store + per-(block, bucket) counts; partitions follow the table up to the max
   const size_t ncount = (size_t)map_blocks * MAX_REC_BUCKETS;
-  rec_mem.reserve(rec_total * (sizeof(Rec) + sizeof(Rec16)) + ncount * 4 + 8192);
+  rec_mem.reserve(rec_total * (sizeof(Rec) + sizeof(Rec16)) + 2 * ncount * 4 + 8192);
   rec.recs = rec_mem.take_n<Rec>(rec_total);
   rec.recs16 = rec_mem.take_n<Rec16>(rec_total);
   rec.cap = rec_total;
   rec.count = rec_mem.take_n<uint32_t>(ncount);
+  rec.count_long = rec_mem.take_n<uint32_t>(ncount);
 
   const size_t stage_n = (size_t)HOT_PARTS * map_blocks;
   hot_mem.reserve(stage_n * HOT_STAGE_CAP * sizeof(HotEnt) + stage_n * 4 +

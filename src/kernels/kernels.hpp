@@ -72,6 +72,11 @@ struct Records {
   uint64_t cap;                // record capacity of each store
   uint32_t* count;             // [map_blocks * nb] Rec16 (low 16 bits) | Rec (high 16) records appended
   uint32_t subcap;             // records per sub-region, <= 65535 (cap / (map_blocks * nb) of the pass)
+  // LONG-word records (hashed keys: their bytes are compared in the reduce)
+  // fill the same 24-byte sub-region from its TOP down — recs[(p nb + b + 1)
+  // subcap - 1 - i], i < count_long[p nb + b] — so the reducer streams them
+  // directly instead of re-scanning the 24-byte runs for them
+  uint32_t* count_long;        // [map_blocks * nb]
 };
 
 // Running key table: n_buckets x TAB_SLOTS open-addressing slices.
@@ -109,10 +114,11 @@ struct MapArgs {
   // balanced reduce's plan (ReduceArgs::bucket_w)
   uint32_t* bucket_w;
 };
-// Reduce cost of a 24-byte record relative to a Rec16 one in the dispatch
-// plan: 24-byte runs carry the LONG words, whose byte comparison (a random
-// 64-byte text read) costs ~10-20x a Rec16 merge (profiles/r5_reduce_balance.md)
-constexpr uint32_t RED_W24 = 12;
+// Reduce cost of a record relative to a Rec16 one in the dispatch plan: a
+// LONG word's byte comparison (a random 64-byte text read) costs ~10-20x a
+// Rec16 merge (profiles/r5_reduce_balance.md)
+constexpr uint32_t RED_W24 = 2;     // a 24-byte inline-key record (a counted hot slot, a 13..15-byte word)
+constexpr uint32_t RED_WLONG = 16;  // a LONG-word record
 // Hot-key sampling workspace (map.hip).  Two launches, no device-scope
 // atomics and nothing to zero: wc_hot_sample writes every map block's sampled
 // words, split by fingerprint into HOT_PARTS partitions, to its own stage

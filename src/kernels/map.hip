@@ -60,7 +60,7 @@ constexpr int HALO = 64;               // bytes past the unit kept in LDS
 // buffer starts 16-byte aligned, so the unit commit's ds_write_b128 are aligned
 // (2136-byte buffers put odd waves at 8 mod 16: SQ_LDS_UNALIGNED_STALL 3.0e7 / GiB)
 constexpr int BUF = (UNIT + HALO + 24 + 15) / 16 * 16;
-constexpr int MAP_DEF_CAP = 256;       // deferred LONG entries per wave and round
+constexpr int MAP_DEF_CAP = 248;       // deferred LONG entries per wave and round (>= 128 + UNIT / 17)
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr int GS = HOT_GROUP_SLOTS;    // slots per group
 constexpr int NG = HOT_GROUPS;         // groups
@@ -652,6 +652,8 @@ struct alignas(16) MapLds {
   uint16_t list[MAP_WAVES][MAP_LIST];
   uint16_t dlist[MAP_WAVES][MAP_DEF_CAP];  // deferred LONG entries of a round: pos | (len - 16) << 11 | prev << 15
   uint32_t bcur[2 * MAX_REC_BUCKETS];   // record cursors (map_common.hpp cursors_init): Rec16 | Rec per bucket
+  uint32_t lcur[MAX_REC_BUCKETS / 2];   // LONG-record counts, 16 bits per bucket (map_common.hpp emit_long)
+  uint32_t lovf;                        // a LONG count reached its sub-region
   alignas(16) uint8_t buf[MAP_WAVES][2][BUF];  // two unit slots per wave: the current unit and the one before
   uint32_t next_unit;
   unsigned long long used, tokens;
@@ -706,7 +708,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     L.cnt[s] = 0;
     L.off[s] = 0xFFFFFFFFu;
   }
-  cursors_init(L.bcur, 1u << a.log2_rec_buckets, a.rec.subcap);
+  cursors_init(L.bcur, L.lcur, 1u << a.log2_rec_buckets, a.rec.subcap);
   // the table image, built in this block's LDS (the unit buffers and token
   // lists are its scratch until the first unit)
   static_assert(sizeof(L.buf) >= 4 * (SEL_BINS + 20) && sizeof(L.list) >= 4 * NG, "image scratch");
@@ -716,6 +718,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   if (tid == 0) {
     L.next_unit = 0;
     L.used = L.tokens = 0;
+    L.lovf = 0;
   }
   __syncthreads();
 
@@ -792,7 +795,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
           atomicAdd(&L.cnt[slot], 1u);
           atomicMin(&L.off[slot], (uint32_t)(u0 + q));
         } else {
-          emit_record(L.bcur, rout, place_hash(k0, k1) & bmask, k0, k1, 1, (uint32_t)(u0 + q));
+          emit_record(L.bcur, L.lcur, &L.lovf, rout, place_hash(k0, k1) & bmask, k0, k1, 1, (uint32_t)(u0 + q));
         }
       }
     }
@@ -1153,7 +1156,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     const uint64_t sd = (two_word(sg) || is_long_sig(sg)) ? L.sig[s | 1] : 0ull;
     if (is_long_sig(sg)) key_long_line(h.long_bytes + (sd >> 32) * 64, (uint32_t)sd, a.k1_mask, k0, k1);
     else sig_key(sg, sd, k0, k1);
-    emit_record(L.bcur, rout, place_hash(k0, k1) & bmask, k0, k1, c, L.off[s]);
+    emit_record(L.bcur, L.lcur, &L.lovf, rout, place_hash(k0, k1) & bmask, k0, k1, c, L.off[s]);
   }
   clk.lap(MS_FLUSH);
   if constexpr (ST) {
@@ -1177,11 +1180,14 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   uint64_t t = my_tokens, e = 0;
   for (uint32_t b = tid; b < nb; b += MAP_THREADS) {
     const uint32_t sub = rout.sub, c16 = L.bcur[b] - b * sub, c24 = L.bcur[MAX_REC_BUCKETS + b] - b * sub;
-    if (c16 > sub || c24 > sub) atomicOr(&a.flags[FLAG_REGION_OVF], 1u);  // overran into the next sub-region
-    const uint32_t n16 = min(c16, sub), n24 = min(c24, sub);
+    const uint32_t cl = (L.lcur[b >> 1] >> (16u * (b & 1u))) & 0xFFFFu;
+    // overran into the next sub-region (24-byte records grow up, LONG ones down)
+    if (c16 > sub || c24 + cl > sub || L.lovf) atomicOr(&a.flags[FLAG_REGION_OVF], 1u);
+    const uint32_t n16 = min(c16, sub), n24 = min(c24, sub), nl = min(cl, sub);
     a.rec.count[(size_t)blockIdx.x * nb + b] = n16 | (n24 << 16);  // packed for the reducer (sub <= 0xFFFF)
-    if (a.bucket_w && (n16 | n24)) atomicAdd(&a.bucket_w[b], n16 + RED_W24 * n24);  // the balanced reduce's plan
-    e += n16 + n24;
+    a.rec.count_long[(size_t)blockIdx.x * nb + b] = nl;
+    if (a.bucket_w && (n16 | n24 | nl)) atomicAdd(&a.bucket_w[b], n16 + RED_W24 * n24 + RED_WLONG * nl);  // dispatch plan
+    e += n16 + n24 + nl;
   }
   for (int o = 32; o > 0; o >>= 1) {
     t += __shfl_down(t, o);

@@ -183,11 +183,12 @@ __device__ __forceinline__ RecOut rec_out(const MapArgs& a) {
 // end sees it (cursor - b * sub > sub), raises FLAG_REGION_OVF and the host
 // re-runs the pass, discarding its records; indices are clamped to the block's
 // area, so nothing is written outside it.
-__device__ __forceinline__ void cursors_init(uint32_t* cur, uint32_t nb, uint32_t sub) {
+__device__ __forceinline__ void cursors_init(uint32_t* cur, uint32_t* lcur, uint32_t nb, uint32_t sub) {
   for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
     cur[b] = b * sub;
     cur[MAX_REC_BUCKETS + b] = b * sub;
   }
+  for (uint32_t w = threadIdx.x; w < (nb + 1) / 2; w += blockDim.x) lcur[w] = 0;
 }
 
 // Store one record at area index idx.  The block's store bases are
@@ -209,10 +210,24 @@ __device__ __forceinline__ void put_rec24(const RecOut& o, uint32_t idx, uint64_
   *reinterpret_cast<Rec*>(reinterpret_cast<uint8_t*>(o.b24) + __umul24(idx, (uint32_t)sizeof(Rec))) = r;
 }
 
+// LONG-word record cursors: 16-bit counts, two buckets per LDS word (bucket b
+// in half b & 1 of word b >> 1), counting down from the top of the 24-byte
+// sub-region.  A count reaching the sub-region size raises the block's
+// overflow word (ovf) at once — a count past 0xFFFF would carry into its
+// neighbour — and the block end checks 24-byte + LONG counts against it.
+__device__ __forceinline__ void emit_long(uint32_t* lcur, uint32_t* ovf, const RecOut& o, uint32_t b, uint64_t k0,
+                                          uint64_t k1, uint64_t cnt, uint32_t off) {
+  const uint32_t sh = 16u * (b & 1u);
+  const uint32_t c = (atomicAdd(&lcur[b >> 1], 1u << sh) >> sh) & 0xFFFFu;
+  if (c >= o.sub) *ovf = 1u;
+  put_rec24(o, b * o.sub + (o.sub - 1u) - min(c, o.sub - 1u), k0, k1, cnt, off);
+}
+
 // Append one record (key, count, first offset) to bucket b's sub-region.
-__device__ __forceinline__ void emit_record(uint32_t* cur, const RecOut& o, uint32_t b, uint64_t k0, uint64_t k1,
-                                            uint64_t cnt, uint32_t off) {
+__device__ __forceinline__ void emit_record(uint32_t* cur, uint32_t* lcur, uint32_t* ovf, const RecOut& o, uint32_t b,
+                                            uint64_t k0, uint64_t k1, uint64_t cnt, uint32_t off) {
   if (rec16_fits(k0, k1, cnt)) put_rec16(o, atomicAdd(&cur[b], 1u), make_rec16(k0, k1, off));
+  else if (key_is_hashed(k1)) emit_long(lcur, ovf, o, b, k0, k1, cnt, off);
   else put_rec24(o, atomicAdd(&cur[MAX_REC_BUCKETS + b], 1u), k0, k1, cnt, off);
 }
 

@@ -66,6 +66,7 @@ struct RedLds {
   uint32_t occupied;
   uint32_t overflow;
   uint32_t runcnt[RED_MAX_RUNS];  // packed record counts of this bucket's run in every map block
+  uint16_t runlong[RED_MAX_RUNS]; // LONG records of this bucket's sub-region in every map block (Records::count_long)
   unsigned long long st[RED_STAMP_N];  // diagnostic counters (WC_RED_STAMPS builds only)
 };
 static_assert(sizeof(RedLds) <= 160 * 1024, "one reduce block per CU");
@@ -252,8 +253,10 @@ __device__ __forceinline__ bool long_equal64(const LongCtx& c, const uint64_t (&
 // a published tag acquires before reading the reference.  Probers that see
 // PENDING re-read the group; the claimer finishes inside its iteration, so
 // the lanes of one wave never wait on each other.  Returns 1 for a claim.
-__device__ __forceinline__ int find_long(RedLds& L, const LongCtx& c, uint32_t ph, uint64_t k0, uint64_t k1, uint64_t off,
-                                         bool& claimed) {
+// w / wlen: the record's first 64 bytes and length (load_word64), loaded by
+// the caller — long_direct issues them one batch ahead.
+__device__ __forceinline__ int find_long_w(RedLds& L, const LongCtx& c, uint32_t ph, uint64_t k0, uint64_t k1,
+                                           uint64_t off, const uint64_t (&w)[8], uint32_t wlen, bool& claimed) {
   claimed = false;
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const uint32_t tag = make_tag(ph);
@@ -261,9 +264,6 @@ __device__ __forceinline__ int find_long(RedLds& L, const LongCtx& c, uint32_t p
   uint32_t g = g1;
   int steps = 0;
   if (WC_RED_STAMPS) atomicAdd(&L.st[RS_SLOW_LANES], 1ull);
-  // the record's bytes, before the probe needs them (their loads overlap it)
-  uint64_t w[8];
-  const uint32_t wlen = load_word64(c, off, w);
   for (;;) {
     asm volatile("" ::: "memory");
     SlotGroup& G = L.grp[g];
@@ -309,6 +309,13 @@ __device__ __forceinline__ int find_long(RedLds& L, const LongCtx& c, uint32_t p
     }
     g = probe_group(g1, g2, (uint32_t)steps, TAB_GROUPS);
   }
+}
+
+__device__ __forceinline__ int find_long(RedLds& L, const LongCtx& c, uint32_t ph, uint64_t k0, uint64_t k1, uint64_t off,
+                                         bool& claimed) {
+  uint64_t w[8];  // the record's bytes, before the probe needs them (their loads overlap it)
+  const uint32_t wlen = load_word64(c, off, w);
+  return find_long_w(L, c, ph, k0, k1, off, w, wlen, claimed);
 }
 
 // A wave's LONG records after find_long (slot s, or -1 for none / no room),
@@ -565,6 +572,81 @@ __device__ __forceinline__ void merge_stream(RedLds& L, const ReduceArgs& a, uin
       load(ra, ia, va);
     }
     merge_batch<R16, U>(L, a, b, rb2, vb, ib, shift, claims);
+    if (!more2) return;
+  }
+}
+
+// The LONG records of this wave's runs (map blocks p0, p0 + pstride, ...): each
+// run fills its 24-byte sub-region from the top down (Records::count_long), so
+// they stream straight in, one record per lane, batches of 64 concatenated
+// across runs (as merge_stream: lane j holds run j's prefix P_j and the index
+// of its record 0, TOP_j, so stream position t of run j is record TOP_j + P_j - t).
+// The next batch's records and their first 64 text bytes are loaded before
+// this batch's slots are resolved: the random text read — the LONG merge's
+// cost — overlaps the probe and the byte comparison of the batch before.
+__device__ __forceinline__ void long_direct(RedLds& L, const ReduceArgs& a, const LongCtx& c, uint32_t b, uint32_t p0,
+                                            uint32_t pstride, uint32_t nrb, uint32_t rb, uint32_t sub, uint32_t shift,
+                                            uint32_t& claims) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t nj = p0 < a.map_blocks ? (a.map_blocks - p0 + pstride - 1) / pstride : 0u;  // <= 64 (pstride >= 16)
+  const uint32_t cnt = lane < nj ? (uint32_t)L.runlong[p0 + lane * pstride] : 0u;
+  uint32_t incl = cnt;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+    if ((int)lane >= o) incl += y;
+  }
+  const uint32_t N = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  if (N == 0) return;
+  const uint32_t P = incl - cnt;
+  const uint32_t TOP = ((p0 + lane * pstride) * nrb + rb + 1) * sub - 1 + P;  // modular: TOP_j - t is exact
+  const uint32_t SAFE = rb * sub;                                            // an index inside the store
+  uint32_t jlo = 0;
+  auto locate = [&](uint32_t T0, uint32_t& idx, bool& valid) {
+    while (jlo + 1 < nj && (uint32_t)__builtin_amdgcn_readlane((int)P, (int)(jlo + 1)) <= T0) ++jlo;
+    const uint32_t t = T0 + lane;
+    idx = (uint32_t)__builtin_amdgcn_readlane((int)TOP, (int)jlo) - t;
+    for (uint32_t jj = jlo + 1; jj < nj; ++jj) {  // runs starting inside this batch
+      const uint32_t pj = (uint32_t)__builtin_amdgcn_readlane((int)P, (int)jj);
+      if (pj >= T0 + 64) break;
+      if (t >= pj) idx = (uint32_t)__builtin_amdgcn_readlane((int)TOP, (int)jj) - t;
+    }
+    valid = t < N;
+  };
+  auto load = [&](uint32_t idx, bool valid, Rec& r, uint64_t (&w)[8], uint32_t& wlen) {
+    r = a.rec.recs[valid ? idx : SAFE];
+    wlen = 0;
+    if (valid) wlen = load_word64(c, (uint32_t)r.co, w);
+  };
+  auto merge = [&](const Rec& r, const uint64_t (&w)[8], uint32_t wlen, bool valid) {
+    const uint32_t ph = place_hash(r.k0, r.k1), off = (uint32_t)r.co;
+    int s = -1;
+    if (valid && (!shift || bucket_of(ph, a.tab.log2_buckets) == b)) {
+      bool cl;
+      s = find_long_w(L, c, ph, r.k0, r.k1, off, w, wlen, cl);
+      claims += cl ? 1u : 0u;
+    }
+    wave_add_long(L, s, r.co >> 32, a.chunk_base + off);
+  };
+  Rec ra, rb2;
+  uint64_t wa[8], wb[8];
+  uint32_t la, lb, ia, ib;
+  bool va, vb;
+  locate(0, ia, va);
+  load(ia, va, ra, wa, la);
+  for (uint32_t T0 = 0;; T0 += 128) {  // unrolled by two: the register sets swap roles without copies
+    const bool more = T0 + 64 < N;
+    if (more) {
+      locate(T0 + 64, ib, vb);
+      load(ib, vb, rb2, wb, lb);
+    }
+    merge(ra, wa, la, va);
+    if (!more) return;
+    const bool more2 = T0 + 128 < N;
+    if (more2) {
+      locate(T0 + 128, ia, va);
+      load(ia, va, ra, wa, la);
+    }
+    merge(rb2, wb, lb, vb);
     if (!more2) return;
   }
 }
@@ -1020,7 +1102,10 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   load_slice(L, a.tab, b, q != 0);  // quarters q > 0 start empty
   {
     const uint32_t rb0 = b & ((1u << a.log2_rec_buckets) - 1u), nrb0 = 1u << a.log2_rec_buckets;
-    for (uint32_t p = tid; p < a.map_blocks; p += RED_THREADS) L.runcnt[p] = a.rec.count[(size_t)p * nrb0 + rb0];
+    for (uint32_t p = tid; p < a.map_blocks; p += RED_THREADS) {
+      L.runcnt[p] = a.rec.count[(size_t)p * nrb0 + rb0];
+      L.runlong[p] = (uint16_t)a.rec.count_long[(size_t)p * nrb0 + rb0];
+    }
   }
   if (tid == 0) {
     L.occupied = q == 0 ? a.tab.occupancy[b] : 0u;
@@ -1053,10 +1138,11 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   const size_t sbase = (size_t)b * TAB_SLOTS, qbase = (size_t)blockIdx.x * TAB_SLOTS;
   const LongCtx lc{a.text, a.avail_len, a.arena.bytes, q == 0 ? a.tab.sref_off + sbase : a.part.qsoff + qbase,
                    q == 0 ? a.tab.sref_len + sbase : a.part.qslen + qbase};
-  if (L.nlong) {
+  if (L.nlong) {  // LONG records inside the 24-byte runs (none since the map fills LONG ones top-down)
     if (L.nlong <= LONGQ) long_queue(L, a, lc, L.nlong, claims);
     else long_stream(L, a, lc, b, wave, p0, pstride, nrb, rb, (uint32_t)sub, shift, claims);
   }
+  long_direct(L, a, lc, b, p0, pstride, nrb, rb, (uint32_t)sub, shift, claims);
   for (int o = 32; o > 0; o >>= 1) claims += __shfl_down(claims, o);
   if ((tid & 63) == 0 && claims) atomicAdd(&L.occupied, claims);
   if (WC_RED_STAMPS && (tid & 63) == 0)
