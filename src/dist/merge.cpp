@@ -813,7 +813,7 @@ bool merge_cols_speculative(Engine::Impl& im, Comm& comm, bool all_ranks) {
   uint64_t* d_boff = A.take_n<uint64_t>(nb);
   uint64_t* d_n = A.take_n<uint64_t>(2);
   launch_bucket_offsets(t.occupancy, (uint32_t)nb, d_boff, d_n, s);
-  launch_table_compact(t, d_boff, c.k0, c.k1, c.cnt, c.first, c.sref_off, c.sref_len, s);
+  launch_table_compact(t, d_boff, c.k0, c.k1, c.cnt, c.first, c.sref_off, c.sref_len, s, im.bounds(cap + 1));
   im.cols = c;
   im.cols_arena = im.d_arena;
   im.mark(Engine::Impl::EV_MERGE0);

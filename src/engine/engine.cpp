@@ -87,6 +87,10 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   if (const char* e = std::getenv("WC_REC_SHIFT")) rec_shift = (uint32_t)std::atoi(e);  // sweeps only
   if (const char* e = std::getenv("WC_RED_Q")) red_q_force = (uint32_t)std::atoi(e);    // sweeps only
   if (const char* e = std::getenv("WC_RED_PLAN")) red_plan = std::atoi(e) != 0;  // A/B: 0 = the uniform split
+  if (const char* e = std::getenv("WC_RED_STEAL")) red_steal = std::atoi(e) != 0;  // A/B: 0 = the uniform split
+  if (const char* e = std::getenv("WC_FAULT_OCC_UNDER")) fault_occ_under = std::strtoull(e, nullptr, 10);  // tests
+  dev_malloc(&d_bounds, 64);
+  WC_HIP_CHECK(hipMemset(d_bounds, 0, 64));
   if (const char* e = std::getenv("WC_CHECK_TABLE"); e && std::atoi(e)) {
     dev_malloc(&d_tab_err, 4 * sizeof(unsigned long long));
     WC_HIP_CHECK(hipMemset(d_tab_err, 0, 4 * sizeof(unsigned long long)));
@@ -110,6 +114,11 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
     part.done = part_mem.take_n<uint32_t>(ndone);
     WC_HIP_CHECK(hipMemset(part.done, 0, ndone * sizeof(uint32_t)));
     dev_malloc(&d_bucket_w, MAX_REC_BUCKETS * sizeof(uint32_t));
+    // work-stealing split reduce state (zeroed per pass: next, word, slot counter)
+    dev_malloc(&steal.next, MAX_REC_BUCKETS * sizeof(uint32_t));
+    dev_malloc(&steal.word, MAX_REC_BUCKETS * sizeof(unsigned long long));
+    dev_malloc(&steal.plist, (size_t)MAX_REC_BUCKETS * RED_STEAL_PL * sizeof(uint32_t));
+    dev_malloc(&steal.slot_ctr, 64);
   }
   if (const char* e = std::getenv("WC_LOG2_BUCKETS")) {  // sweeps only: shuffle + table bucket count
     opt.log2_rec_buckets = (uint32_t)std::atoi(e);
@@ -188,7 +197,10 @@ Engine::Impl::~Impl() {
   if (d_arena_cursor) (void)hipFree(d_arena_cursor);
   if (d_fo_hist) (void)hipFree(d_fo_hist);
   if (d_bucket_w) (void)hipFree(d_bucket_w);
+  for (void* p : {(void*)steal.next, (void*)steal.word, (void*)steal.plist, (void*)steal.slot_ctr})
+    if (p) (void)hipFree(p);
   if (d_tab_err) (void)hipFree(d_tab_err);
+  if (d_bounds) (void)hipFree(d_bounds);
   if (d_fo_hist_cols) (void)hipFree(d_fo_hist_cols);
   if (d_bm) (void)hipFree(d_bm);
   if (d_stamps) {
@@ -357,9 +369,18 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   const bool planned = red_plan && !red_q_force && nbk >= n_cu && log2_rb == table().log2_buckets &&
                        nbk <= (uint32_t)MAX_REC_BUCKETS && plan_grid <= part_blocks;
   const uint32_t plan_extra = plan_grid - nbk;
+  // below CUs buckets: the work-stealing split (blocks of a finished bucket take runs of the fullest one)
+  const bool stealing = red_steal && !planned && !red_q_force && nbk < n_cu && red_q() > 1 &&
+                        log2_rb == table().log2_buckets && blocks <= (uint32_t)RED_MAX_RUNS &&
+                        nbk * red_q() <= part_blocks;
   ZeroList z{};
   z.add(d_ctr, sizeof(DevCounters));
   if (planned) z.add(d_bucket_w, nbk * sizeof(uint32_t));
+  if (stealing) {
+    z.add(steal.next, nbk * sizeof(uint32_t));
+    z.add(steal.word, nbk * sizeof(unsigned long long));
+    z.add(steal.slot_ctr, sizeof(uint32_t));
+  }
   if (want_hist) z.add(d_fo_hist, FO_LOGBINS * sizeof(uint32_t));  // rebuilt by this pass's reduce over the whole table
   {
     uint32_t kb = 1;
@@ -394,9 +415,10 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
                 d_ctr->flags, d_bucket_ovf, nullptr, d_red_stamps, red_blk(), want_hist ? d_fo_hist : nullptr, fo_hist_m,
                 bm, bm ? bitmap_order_linecnt(bm, bm_end, 1) : nullptr, bm ? bitmap_order_ctl(bm, bm_end, 1) : nullptr,
                 bm ? (bm_end >> 1) + 1 : 0, 1u, planned ? 1u : red_q(), planned ? d_bucket_w : nullptr, part,
-                part_blocks};
+                part_blocks, stealing ? steal : ReduceArgs::Steal{}};
   if (planned && ra.blk) red_blk_grid = nbk + plan_extra;
-  launch_reduce(ra, s, plan_extra);
+  if (stealing) launch_reduce_steal(ra, s);
+  else launch_reduce(ra, s, plan_extra);
   check_table("the reduce");
   if (sync_debug) {
     const hipError_t e = hipStreamSynchronize(s);
@@ -430,6 +452,19 @@ void Engine::Impl::check_table(const char* where) {
     fail(std::string("WC_CHECK_TABLE: table invariant broken after ") + where + ": bucket " + std::to_string(h[0] - 1) +
          " of " + std::to_string(1u << table().log2_buckets) + " holds " + std::to_string(h[1]) + " keys, occupancy " +
          std::to_string(h[2]) + ", " + std::to_string(h[3]) + " misplaced");
+}
+
+// A finalize writer met a row at or past its buffer's capacity (the word
+// published with the finalize's last wait): the row was not written, so the
+// output is incomplete — fail, naming the kernel and the row, and re-arm.
+void Engine::Impl::check_bounds(uint64_t word, const char* where) {
+  if (!word) return;
+  WC_HIP_CHECK(hipMemsetAsync(d_bounds, 0, 8, s));
+  if (d_bm) WC_HIP_CHECK(hipMemsetAsync(d_bm, 0, bm_words * 8, s));  // rows not emitted left their bits set
+  WC_HIP_CHECK(hipStreamSynchronize(s));
+  fail(std::string("bounds guard: ") + bounds_kernel_name((uint32_t)(word >> 56)) + " reached row " +
+       std::to_string(word & ((1ull << 56) - 1)) + " past its buffer's capacity in " + where +
+       " (the key count it was sized for is short; output discarded)");
 }
 
 void Engine::Impl::flush_pass_publish() {
@@ -558,7 +593,7 @@ uint64_t Engine::Impl::host_occupancy(uint64_t*& boff, uint64_t& arena_used) {
     boff[b] = n;
     n += occ[b];
   }
-  return n;
+  return n - std::min(n, fault_occ_under);
 }
 
 void Engine::Impl::split_table() {
@@ -640,7 +675,7 @@ bool Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
     ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                   avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
                   d_ctr->flags, d_bucket_ovf, d_bucket_en, d_red_stamps, red_blk(), fo_hist_ok ? d_fo_hist : nullptr, fo_hist_m,
-                  nullptr, nullptr, nullptr, 0, 0u, red_q(), nullptr, part, part_blocks};
+                  nullptr, nullptr, nullptr, 0, 0u, red_q(), nullptr, part, part_blocks, ReduceArgs::Steal{}};
     launch_reduce(ra, s);
     check_table("a split re-run's reduce");
     PubList pc{};
@@ -713,7 +748,8 @@ void Engine::Impl::compact_local() {
   cols.sref_len = fin_mem.take_n<uint32_t>(n + 1);
   uint64_t* d_boff = fin_mem.take_n<uint64_t>(nb);
   WC_HIP_CHECK(hipMemcpyAsync(d_boff, boff, nb * 8, hipMemcpyHostToDevice, s));  // pinned: no sync needed
-  launch_table_compact(t, d_boff, cols.k0, cols.k1, cols.cnt, cols.first, cols.sref_off, cols.sref_len, s);
+  launch_table_compact(t, d_boff, cols.k0, cols.k1, cols.cnt, cols.first, cols.sref_off, cols.sref_len, s,
+                       bounds(n + 1));
   cols.n = n;
   cols_arena = d_arena;
   cols_arena_bytes = std::min<uint64_t>(arena_used, opt.arena_bytes);
@@ -757,11 +793,12 @@ bool Engine::Impl::finalize_local_speculative() {
   o.sref_len = A.take_n<uint32_t>(cap + 1);
   uint32_t* ovf = nullptr;
   if (sample) {
-    ovf = first_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len}, hint, key_bits(),
+    ovf = first_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len, bounds(cap + 1)}, hint, key_bits(),
                       A.take_n<uint8_t>(first_order_ws_bytes(src, hint)), d_n, s, fo_hist_ok ? d_fo_hist : nullptr,
                       fo_hist_m);
   } else if (bitmap) {
-    ovf = bitmap_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len}, cap, max_end, 1, bm,
+    ovf = bitmap_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len, bounds(cap + 1)}, cap, max_end,
+                       1, bm,
                        A.take_n<uint8_t>(bitmap_order_ws_bytes(cap + 1, max_end, 1)), d_n, s, bm_in_reduce);
     bm_in_reduce = false;  // consumed (the order leaves the bitmap zeroed, a failed pass included)
   } else {
@@ -772,13 +809,13 @@ bool Engine::Impl::finalize_local_speculative() {
     uint32_t* tslots = A.take_n<uint32_t>(cap + 1);
     uint32_t* hist = A.take_n<uint32_t>(radix_hist_words(cap, hint));
     launch_bucket_offsets(t.occupancy, (uint32_t)nb, d_boff, d_n, s);
-    launch_table_keys(t, d_boff, keys, slots, s);
+    launch_table_keys(t, d_boff, keys, slots, s, bounds(cap + 1));
     int bits = 1;
     while (bits < 64 && (max_end >> bits) != 0) ++bits;
     bool in_tmp = false;
     radix_sort_pairs(keys, slots, tkeys, tslots, hist, cap, bits, s, &in_tmp, d_n, hint);
     launch_gather_table(t, in_tmp ? tkeys : keys, in_tmp ? tslots : slots, cap, o.k0, o.k1, o.cnt, o.first,
-                        o.sref_off, o.sref_len, s, d_n);
+                        o.sref_off, o.sref_len, s, d_n, bounds(cap + 1));
   }
   if (h_spec.size() < 32) {
     h_spec.resize(4096);
@@ -793,6 +830,7 @@ bool Engine::Impl::finalize_local_speculative() {
   }
   pc.add(h_spec.data(), d_n, 8);
   pc.add(h_spec.data() + 8, d_arena_cursor, 8);
+  pc.add(h_spec.data() + 40, d_bounds, 8);
   uint32_t* seq = reinterpret_cast<uint32_t*>(h_spec.data() + 16);
   uint32_t* h_ovf = reinterpret_cast<uint32_t*>(h_spec.data() + 24);
   *h_ovf = 0;
@@ -813,6 +851,9 @@ bool Engine::Impl::finalize_local_speculative() {
     order_redo = true;
     return false;
   }
+  uint64_t bw = 0;
+  std::memcpy(&bw, h_spec.data() + 40, 8);
+  check_bounds(bw, "the speculative local finalize");
   uint64_t n = 0, arena_used = 0;
   std::memcpy(&n, h_spec.data(), 8);
   std::memcpy(&arena_used, h_spec.data() + 8, 8);
@@ -853,8 +894,8 @@ void Engine::Impl::finalize_local_sorted() {
     A.reserve((n + 1) * (5 * 8 + 4) + first_order_ws_bytes(src, n) + 64 * 1024);
     A.reset();
     take_cols();
-    const uint32_t* ovf = first_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len}, n,
-                                      key_bits(), A.take_n<uint8_t>(first_order_ws_bytes(src, n)), nullptr, s,
+    const uint32_t* ovf = first_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len, bounds(n + 1)},
+                                      n, key_bits(), A.take_n<uint8_t>(first_order_ws_bytes(src, n)), nullptr, s,
                                       fo_hist_ok ? d_fo_hist : nullptr, fo_hist_m);
     if (h_fin.size() < 64) {
       h_fin = PinnedBuffer(64);
@@ -873,8 +914,8 @@ void Engine::Impl::finalize_local_sorted() {
     A.reserve((n + 1) * (5 * 8 + 4) + bitmap_order_ws_bytes(n + 1, max_end, 1) + 64 * 1024);
     A.reset();
     take_cols();
-    const uint32_t* ovf = bitmap_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len}, n, max_end,
-                                       1, bm, A.take_n<uint8_t>(bitmap_order_ws_bytes(n + 1, max_end, 1)), nullptr, s);
+    const uint32_t* ovf = bitmap_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len, bounds(n + 1)},
+                                       n, max_end, 1, bm, A.take_n<uint8_t>(bitmap_order_ws_bytes(n + 1, max_end, 1)), nullptr, s);
     if (h_fin.size() < 64) {
       h_fin = PinnedBuffer(64);
       std::memset(h_fin.data(), 0, 64);
@@ -896,13 +937,13 @@ void Engine::Impl::finalize_local_sorted() {
     uint32_t* hist = A.take_n<uint32_t>(radix_hist_words(n));
     take_cols();
     WC_HIP_CHECK(hipMemcpyAsync(d_boff, boff, nb * 8, hipMemcpyHostToDevice, s));  // pinned: no sync needed
-    launch_table_keys(t, d_boff, keys, slots, s);
+    launch_table_keys(t, d_boff, keys, slots, s, bounds(n + 1));
     int bits = 1;
     while (bits < 64 && (max_end >> bits) != 0) ++bits;
     bool in_tmp = false;
     radix_sort_pairs(keys, slots, tkeys, tslots, hist, n, bits, s, &in_tmp);
     launch_gather_table(t, in_tmp ? tkeys : keys, in_tmp ? tslots : slots, n, o.k0, o.k1, o.cnt, o.first,
-                        o.sref_off, o.sref_len, s);
+                        o.sref_off, o.sref_len, s, nullptr, bounds(n + 1));
   }
   cols = o;
   cols_arena = d_arena;
@@ -950,7 +991,7 @@ void Engine::Impl::sort_cols_by_first(bool radix) {
     A.reserve(n * (5 * 8 + 4) + first_order_ws_bytes(src, n) + 64 * 1024);
     A.reset();
     take_cols();
-    fo_ovf = first_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len}, n, key_bits(),
+    fo_ovf = first_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len, bounds(n)}, n, key_bits(),
                          A.take_n<uint8_t>(first_order_ws_bytes(src, n)), nullptr, s, nullptr, 0, d_fo_hist_cols,
                          cols_hist_m);
     cols_hist_m = 0;
@@ -974,7 +1015,7 @@ void Engine::Impl::sort_cols_by_first(bool radix) {
     A.reserve(n * (5 * 8 + 4) + bitmap_order_ws_bytes(n, max_end, 1) + 64 * 1024);
     A.reset();
     take_cols();
-    fo_ovf = bitmap_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len}, n, max_end, 1, bm,
+    fo_ovf = bitmap_order(src, OrderDst{o.k0, o.k1, o.cnt, o.first, o.sref_off, o.sref_len, bounds(n)}, n, max_end, 1, bm,
                           A.take_n<uint8_t>(bitmap_order_ws_bytes(n, max_end, 1)), nullptr, s);
     cols_unsorted = cols;
     cols = o;
@@ -996,7 +1037,7 @@ void Engine::Impl::sort_cols_by_first(bool radix) {
   bool in_tmp = false;
   radix_sort_pairs(keys, vals, tkeys, tvals, hist, n, bits, s, &in_tmp, dn, dn ? n : 0);
   launch_gather_cols(cols.k0, cols.k1, cols.cnt, cols.first, cols.sref_off, cols.sref_len, in_tmp ? tvals : vals, o.k0,
-                     o.k1, o.cnt, o.first, o.sref_off, o.sref_len, n, s, dn);
+                     o.k1, o.cnt, o.first, o.sref_off, o.sref_len, n, s, dn, bounds(n));
   cols = o;
   st.order_path = radix ? 3 : 2;
 }
@@ -1375,7 +1416,7 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
   // the merged count still on the device, the sample sort's overflow word and
   // (planned merge) its decision flags and local key count: published with the last wait
   auto publish_and_wait = [&] {
-    if (im.cols.dn || im.fo_ovf || im.planned_active || im.pass_pub_pending) {
+    if (!drained) {  // the bounds word rides in every finalize's last publish
       if (im.h_fin.size() < 64) {
         im.h_fin = PinnedBuffer(64);
         std::memset(im.h_fin.data(), 0, 64);  // the sequence word starts below every fin_seq
@@ -1387,6 +1428,7 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
           pc.add(im.pass_pub.dst[i], im.pass_pub.src[i], (uint64_t)im.pass_pub.words[i] * 4);
       }
       if (im.cols.dn) pc.add(im.h_fin.data(), im.cols.dn, 8);
+      pc.add(im.h_fin.data() + 40, im.d_bounds, 8);
       if (im.fo_ovf) pc.add(im.h_fin.data() + 8, im.fo_ovf, 4);
       if (im.planned_active) {
         std::memset(im.h_fin.data() + 16, 0, 16);
@@ -1408,6 +1450,12 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
     else if (!drained) WC_HIP_CHECK(hipStreamSynchronize(im.s));
   };
   publish_and_wait();
+  const auto bounds_word = [&] {
+    uint64_t w = 0;
+    if (!drained) std::memcpy(&w, im.h_fin.data() + 40, 8);
+    return w;
+  };
+  im.check_bounds(bounds_word(), merged ? "the merged finalize" : "the local finalize");
   if (im.planned_active) {
     // the planned merge's decisions (the same on every rank: all-gathered words)
     im.planned_active = false;
@@ -1434,6 +1482,7 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
       im.sort_cols_by_first();
       im.mark(EV_FIN_END);
       publish_and_wait();
+      im.check_bounds(bounds_word(), "the redone merged finalize");
     }
   }
   if (im.fo_ovf) {
@@ -1445,7 +1494,10 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
       im.cols = im.cols_unsorted;
       im.sort_cols_by_first(true);
       if (was_bitmap) im.st.order_path = 6;
+      uint64_t w = 0;
+      WC_HIP_CHECK(hipMemcpyAsync(&w, im.d_bounds, 8, hipMemcpyDeviceToHost, im.s));
       WC_HIP_CHECK(hipStreamSynchronize(im.s));
+      im.check_bounds(w, "the radix order redo");
     }
   }
   if (im.cols.dn) {

@@ -70,10 +70,18 @@ struct Engine::Impl {
   size_t red_blk_grid = 0;
   uint32_t fin_seq = 0;
   bool red_plan = true;
+  bool red_steal = false;           // the work-stealing split reduce (WC_RED_STEAL=1; A/B pending)
+  ReduceArgs::Steal steal{};
   // WC_CHECK_TABLE=1 (debug): after every reduce and split the table's
   // invariants are checked on the device and a violation fails the job naming
   // the stage (engine.cpp check_table)
   unsigned long long* d_tab_err = nullptr;
+  // the finalize writers' bounds guard (kernels.hpp Bounds): one word, zero
+  // unless a writer met a row past its buffer; checked at every finalize
+  unsigned long long* d_bounds = nullptr;
+  uint64_t fault_occ_under = 0;  // WC_FAULT_OCC_UNDER (tests): host key count short by this many
+  Bounds bounds(uint64_t cap) const { return Bounds{d_bounds, cap}; }
+  void check_bounds(uint64_t word, const char* where);
   void check_table(const char* where);             // the balanced reduce (WC_RED_PLAN=0: the uniform split)
   uint32_t* d_bucket_w = nullptr;   // its per-bucket weights (the map adds them)  // sequence word of the merged finalize's last publish (h_fin + 32)
   uint64_t blocks_stamped = 0;             // map blocks launched with stamps (block-duration mean)

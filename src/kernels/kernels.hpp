@@ -220,10 +220,25 @@ struct ReduceArgs {
     uint32_t* done;                           // [b] quarters arrived (zeroed; the last resets it)
   } part;
   uint32_t part_slots;  // partial-table slots allocated (the dispatch plan needs one per block)
+  // Work-stealing split reduce (nullable `next`: off; fewer table buckets than
+  // CUs): blocks grab a bucket's runs RED_STEAL_CH at a time and, their bucket
+  // exhausted, start a piece of the bucket with the most runs left; a piece
+  // registers (slot) before it grabs, and the arrival that completes the
+  // bucket's runs with every registered piece arrived merges them (reduce.hip
+  // wc_reduce_steal).  Zeroed per pass: next, word, slot_ctr.
+  struct Steal {
+    uint32_t* next;            // [nb] runs grabbed
+    unsigned long long* word;  // [nb] runs done << 32 | pieces arrived << 16 | pieces registered
+    uint32_t* plist;           // [nb][RED_STEAL_PL] partial slots of the registered pieces
+    uint32_t* slot_ctr;        // partial slots handed out
+  } steal;
 };
 // Most reduce blocks per bucket (split reduce: fewer table buckets than CUs).
 constexpr uint32_t RED_SPLIT_MAX_Q = 16;
 constexpr uint32_t RED_PLAN_EXTRA = 64;  // dispatch plan: blocks for split heavy buckets past one per bucket
+constexpr uint32_t RED_STEAL_CH = 32;    // work-stealing reduce: runs per grab (2 per wave)
+constexpr uint32_t RED_STEAL_PL = 32;    // pieces per bucket at most
+constexpr uint32_t RED_STEAL_MIN = 16;   // runs left for a steal to start a piece
 // Reduce diagnostic counters (src/kernels/reduce.hip built with -DWC_RED_STAMPS=1).
 constexpr int RED_BLK_WORDS = 5;
 enum : int { RS_RECORDS = 0, RS_SLOW_LANES, RS_SLOW_WAVES, RS_PROBE_ITERS, RS_CAS_FAIL, RS_PENDING, RS_CLAIMS,
@@ -247,7 +262,30 @@ void launch_map(const MapArgs& a, const HotArgs& h, uint32_t map_blocks, hipStre
                 const ZeroList& z);
 // extra: with ReduceArgs::bucket_w, blocks past one per bucket for the dispatch
 // plan's split heavy buckets (reduce.hip lpt_piece)
+// Bounds guard on the finalize's row writers (profiles/r5_fault_hunt.md): a
+// write at or past `cap` rows is skipped and the first one recorded in *err as
+// (kernel id << 56 | row); the engine fails naming the kernel and the row at
+// the finalize's wait (Engine::Impl::check_bounds) instead of faulting the GPU.
+// err == nullptr: unchecked.
+enum BoundsKernel : uint32_t {
+  BND_NONE = 0,
+  BND_FO_SORT,       // sort.hip wc_fo_sort: output rows
+  BND_BM_PLACE,      // sort.hip wc_bm_place: record rows
+  BND_BM_EMIT,       // sort.hip wc_bm_emit: output rows
+  BND_GATHER_COLS,   // sort.hip wc_gather_cols: output rows and source rows
+  BND_TABLE_KEYS,    // reduce.hip wc_table_keys: (first, slot) rows
+  BND_GATHER_TABLE,  // reduce.hip wc_gather_table: output rows and table slots
+  BND_COMPACT,       // reduce.hip wc_table_compact: output rows
+  BND_KERNELS
+};
+struct Bounds {
+  unsigned long long* err = nullptr;
+  uint64_t cap = ~0ull;
+};
+const char* bounds_kernel_name(uint32_t k);
+
 void launch_reduce(const ReduceArgs& a, hipStream_t s, uint32_t extra = 0);
+void launch_reduce_steal(const ReduceArgs& a, hipStream_t s);  // ReduceArgs::steal set
 void launch_table_split(const TableView& src, const TableView& dst, hipStream_t s);
 void launch_table_clear(const TableView& t, hipStream_t s);
 // debug: err (4 words, zeroed) <- the first bucket breaking the table's invariants (reduce.hip wc_check_table)
@@ -255,7 +293,8 @@ void launch_check_table(const TableView& t, unsigned long long* err, hipStream_t
 // Writes occupied entries densely in bucket order; bucket_off[b] = exclusive
 // prefix of the per-bucket occupancy (device array of 2^log2_buckets).
 void launch_table_compact(const TableView& t, const uint64_t* bucket_off, uint64_t* k0, uint64_t* k1, uint64_t* cnt,
-                          uint64_t* first, uint64_t* sref_off, uint32_t* sref_len, hipStream_t s);
+                          uint64_t* first, uint64_t* sref_off, uint32_t* sref_len, hipStream_t s,
+                          const Bounds& bnd = {});
 
 // LSD radix sort of (key, value) by the low `bits` bits of key; stable.
 // tmp_* must hold n items; hist must hold radix_hist_words(n) words.  With
@@ -270,10 +309,11 @@ void radix_sort_pairs(uint64_t* keys, uint32_t* vals, uint64_t* tmp_keys, uint32
 // Local finalize without the column copy: occupied slots -> (first offset,
 // global slot index) pairs at host-computed bucket offsets; after the sort,
 // the six output columns are gathered straight from the table.
-void launch_table_keys(const TableView& t, const uint64_t* bucket_off, uint64_t* keys, uint32_t* slots, hipStream_t s);
+void launch_table_keys(const TableView& t, const uint64_t* bucket_off, uint64_t* keys, uint32_t* slots, hipStream_t s,
+                       const Bounds& bnd = {});
 void launch_gather_table(const TableView& t, const uint64_t* keys, const uint32_t* slots, uint64_t n, uint64_t* ok0,
                          uint64_t* ok1, uint64_t* ocnt, uint64_t* ofirst, uint64_t* osoff, uint32_t* oslen,
-                         hipStream_t s, const uint64_t* dn = nullptr);
+                         hipStream_t s, const uint64_t* dn = nullptr, const Bounds& bnd = {});
 // Exclusive scan of the bucket occupancy on the device: bucket_off[b] and the
 // key count *n (the speculative finalize: no host round trip after the pass).
 void launch_bucket_offsets(const uint32_t* occupancy, uint32_t nb, uint64_t* bucket_off, uint64_t* n, hipStream_t s);
@@ -298,6 +338,7 @@ struct OrderSrc {
 struct OrderDst {
   uint64_t *k0, *k1, *cnt, *first, *soff;
   uint32_t* slen;
+  Bounds bnd;  // the columns' row capacity (the bitmap order's record rows too)
 };
 #ifndef WC_FO_MAX_KEYS
 #define WC_FO_MAX_KEYS 1600000
@@ -341,7 +382,7 @@ uint32_t* bitmap_order_linecnt(unsigned long long* bm, uint64_t key_end, uint32_
 void launch_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
                         const uint64_t* soff, const uint32_t* slen, const uint32_t* perm, uint64_t* ok0, uint64_t* ok1,
                         uint64_t* ocnt, uint64_t* ofirst, uint64_t* osoff, uint32_t* oslen, uint64_t n, hipStream_t s,
-                        const uint64_t* dn = nullptr);
+                        const uint64_t* dn = nullptr, const Bounds& bnd = {});
 void launch_iota_u32(uint32_t* v, uint64_t n, hipStream_t s);
 
 // util.hip: fill several device regions (+ a few small copies, e.g. host words

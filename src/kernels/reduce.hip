@@ -26,6 +26,7 @@
 //  wc_table_compact   occupied slots -> dense columns (per-bucket block scan).
 #include "kernels.hpp"
 
+#include "bounds.hpp"
 #include "lds_table.hpp"
 #include "common/hip_util.hpp"
 
@@ -510,11 +511,12 @@ __device__ __forceinline__ void merge_batch(RedLds& L, const ReduceArgs& a, uint
 template <bool R16, int U, class RecT>
 __device__ __forceinline__ void merge_stream(RedLds& L, const ReduceArgs& a, uint32_t b, const RecT* recs, uint32_t p0,
                                              uint32_t pstride, uint32_t nrb, uint32_t rb, uint32_t sub, uint32_t shift,
-                                             uint32_t& claims) {
+                                             uint32_t& claims, uint32_t p_end = ~0u) {
   constexpr uint32_t B = U * 64;
   const uint32_t lane = threadIdx.x & 63;
-  // runs p0, p0 + pstride, ... (pstride >= 16: <= 64 runs, RED_MAX_RUNS)
-  const uint32_t nj = p0 < a.map_blocks ? (a.map_blocks - p0 + pstride - 1) / pstride : 0u;
+  // runs p0, p0 + pstride, ... below p_end (pstride >= 16: <= 64 runs, RED_MAX_RUNS)
+  const uint32_t pe = min(p_end, a.map_blocks);
+  const uint32_t nj = p0 < pe ? (pe - p0 + pstride - 1) / pstride : 0u;
   uint32_t c = 0;
   if (lane < nj) {
     const uint32_t packed = L.runcnt[p0 + lane * pstride];
@@ -586,9 +588,10 @@ __device__ __forceinline__ void merge_stream(RedLds& L, const ReduceArgs& a, uin
 // cost — overlaps the probe and the byte comparison of the batch before.
 __device__ __forceinline__ void long_direct(RedLds& L, const ReduceArgs& a, const LongCtx& c, uint32_t b, uint32_t p0,
                                             uint32_t pstride, uint32_t nrb, uint32_t rb, uint32_t sub, uint32_t shift,
-                                            uint32_t& claims) {
+                                            uint32_t& claims, uint32_t p_end = ~0u) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t nj = p0 < a.map_blocks ? (a.map_blocks - p0 + pstride - 1) / pstride : 0u;  // <= 64 (pstride >= 16)
+  const uint32_t pe = min(p_end, a.map_blocks);
+  const uint32_t nj = p0 < pe ? (pe - p0 + pstride - 1) / pstride : 0u;  // <= 64 (pstride >= 16)
   const uint32_t cnt = lane < nj ? (uint32_t)L.runlong[p0 + lane * pstride] : 0u;
   uint32_t incl = cnt;
   for (int o = 1; o < 64; o <<= 1) {
@@ -1218,6 +1221,185 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------- work-stealing split reduce
+// (ReduceArgs::steal; fewer table buckets than CUs — the headline's 64).  The
+// uniform split gives each of a bucket's CUs / B blocks the runs p = q mod
+// (CUs / B); its slowest block ran 1.19x the mean (bucket sizes and run sizes
+// vary: profiles/r5_session.md §4).  Here a block grabs RED_STEAL_CH runs of
+// its bucket at a time from the bucket's run cursor; when its bucket has none
+// left it starts a piece of the bucket with the most runs left, so the blocks
+// end together.  Every piece starts EMPTY and ends as a partial table; the
+// piece whose arrival completes the bucket's runs with every registered piece
+// arrived (one packed 64-bit word per bucket, acq_rel) merges its own table
+// with the running slice and the other pieces' partials and stores the slice.
+// A piece registers (partial slot, CAS while the bucket's runs are not all
+// done) BEFORE it grabs, so no run is processed by an unregistered piece and
+// no piece registers after the bucket completed: exactly one merger.
+
+// Rows of the running slice b (the table's occupied slots) into this block's
+// LDS table — the steal reduce's pieces all start empty.
+__device__ __forceinline__ void merge_slice(RedLds& L, const ReduceArgs& a, const LongCtx& c, uint32_t b) {
+  if (a.tab.occupancy[b] == 0) return;  // contents undefined (see load_slice)
+  const size_t base = (size_t)b * TAB_SLOTS;
+  for (int s = threadIdx.x; s < TAB_SLOTS; s += RED_THREADS) {
+    const uint64_t k1 = a.tab.k1[base + s];
+    if (k1 == K1_EMPTY) continue;
+    const uint64_t k0 = a.tab.k0[base + s], cnt = a.tab.cnt[base + s], first = a.tab.first[base + s];
+    if (key_is_hashed(k1)) {
+      merge_long_row(L, c, k0, k1, cnt, first, a.tab.sref_off[base + s], a.tab.sref_len[base + s]);
+    } else {
+      bool claimed;
+      const int d = lds_find_or_claim(L.grp, TAB_GROUPS, place_hash(k0, k1), k0, k1, TAB_MAX_GROUP_PROBES, claimed, true);
+      if (d < 0) L.overflow = 1;
+      else add_to_slot(L, d, cnt, first);
+    }
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(RED_THREADS) wc_reduce_steal(ReduceArgs a) {
+  __shared__ RedLds L;
+  __shared__ uint32_t sh[4];
+  __shared__ unsigned long long best;
+  if (a.flags[FLAG_REGION_OVF]) return;  // shuffle output incomplete: host re-runs the chunk
+  const int tid = threadIdx.x, wave = tid >> 6, nwaves = RED_THREADS / 64;
+  const uint32_t nb = 1u << a.tab.log2_buckets, P = a.map_blocks, sub = a.rec.subcap;
+  const ReduceArgs::Steal& S = a.steal;
+  uint32_t b = blockIdx.x & (nb - 1);
+  for (bool own = true;; own = false) {
+    // 1. register a piece of bucket b: a partial slot (its own block index for a block's first piece — every
+    //    bucket gets its first pieces whatever the stealers took — then past the grid), then the bucket's
+    //    count (CAS while runs remain undone)
+    if (tid == 0) {
+      uint32_t ok = 0, slot = 0;
+      if (__hip_atomic_load(&S.next[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < P) {
+        slot = own ? blockIdx.x : gridDim.x + atomicAdd(S.slot_ctr, 1u);
+        if (slot < a.part_slots) {
+          unsigned long long w = __hip_atomic_load(&S.word[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          while ((w >> 32) < P && (w & 0xFFFFull) < RED_STEAL_PL) {
+            const unsigned long long seen = atomicCAS(&S.word[b], w, w + 1);
+            if (seen == w) {
+              S.plist[b * RED_STEAL_PL + (uint32_t)(w & 0xFFFFull)] = slot;
+              ok = 1;
+              break;
+            }
+            w = seen;
+          }
+        }
+      }
+      sh[0] = ok;
+      sh[1] = slot;
+    }
+    __syncthreads();
+    const bool ok = __builtin_amdgcn_readfirstlane(sh[0]) != 0;  // block-uniform: SGPRs, not VGPRs
+    const uint32_t slot = __builtin_amdgcn_readfirstlane(sh[1]);
+    if (ok) {
+      // 2. the piece: an empty table, runs grabbed RED_STEAL_CH at a time (two per wave)
+      load_slice(L, a.tab, b, true);
+      for (uint32_t p = tid; p < P; p += RED_THREADS) {
+        L.runcnt[p] = a.rec.count[(size_t)p * nb + b];
+        L.runlong[p] = (uint16_t)a.rec.count_long[(size_t)p * nb + b];
+      }
+      if (tid == 0) {
+        L.occupied = 0;
+        L.overflow = 0;
+        L.nlong = 0;
+      }
+      __syncthreads();
+      const size_t qbase = (size_t)slot * TAB_SLOTS, sbase = (size_t)b * TAB_SLOTS;
+      const LongCtx lc{a.text, a.avail_len, a.arena.bytes, a.part.qsoff + qbase, a.part.qslen + qbase};
+      uint32_t claims = 0, runs = 0;
+      for (;;) {
+        if (tid == 0) sh[2] = atomicAdd(&S.next[b], RED_STEAL_CH);
+        __syncthreads();
+        const uint32_t r0 = __builtin_amdgcn_readfirstlane(sh[2]);
+        __syncthreads();  // every wave has read sh[2] before the next grab
+        if (r0 >= P) break;
+        const uint32_t re = min(r0 + RED_STEAL_CH, P);
+        merge_stream<true, RED_UNROLL>(L, a, b, a.rec.recs16, r0 + wave, nwaves, nb, b, sub, 0u, claims, re);
+        merge_stream<false, RED_UNROLL_24>(L, a, b, a.rec.recs, r0 + wave, nwaves, nb, b, sub, 0u, claims, re);
+        long_direct(L, a, lc, b, r0 + wave, nwaves, nb, b, sub, 0u, claims, re);
+        runs += re - r0;
+      }
+      __syncthreads();
+      // LONG records inside 24-byte runs: none since the map fills LONG ones top-down; past the
+      // queue (no run list to re-scan here) the bucket re-runs after a split, exactly
+      if (L.nlong > LONGQ) {
+        if (tid == 0) L.overflow = 1;
+      } else if (L.nlong) {
+        long_queue(L, a, lc, L.nlong, claims);
+      }
+      for (int o = 32; o > 0; o >>= 1) claims += __shfl_down(claims, o);
+      if ((tid & 63) == 0 && claims) atomicAdd(&L.occupied, claims);
+      __syncthreads();
+      if (tid == 0 && L.occupied > (uint32_t)TAB_MAX_OCC) L.overflow = 1;
+      __syncthreads();
+      const bool ovf = __builtin_amdgcn_readfirstlane(L.overflow) != 0;
+      if (ovf && tid == 0) {
+        a.bucket_overflow[b] = 1;
+        atomicOr(&a.flags[FLAG_TABLE_OVF], 1u);
+      }
+      if (!ovf) write_partial(L, a, lc, slot);
+      // 3. arrive: runs done and one piece; the arrival completing both counts merges
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const unsigned long long add = ((unsigned long long)runs << 32) | (1ull << 16);
+        const unsigned long long nw =
+            __hip_atomic_fetch_add(&S.word[b], add, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + add;
+        const uint32_t reg = (uint32_t)(nw & 0xFFFFull), arr = (uint32_t)((nw >> 16) & 0xFFFFull);
+        sh[3] = (nw >> 32) == P && arr == reg ? reg : 0u;
+      }
+      __syncthreads();
+      const uint32_t reg = __builtin_amdgcn_readfirstlane(sh[3]);
+      if (reg && !a.bucket_overflow[b]) {
+        // the merger: the running slice and the other pieces' partials into this table
+        merge_slice(L, a, lc, b);
+        if (tid == 0) {
+          uint32_t k = 0;
+          for (uint32_t i = 0; i < reg; ++i) {
+            const uint32_t sl = S.plist[b * RED_STEAL_PL + i];
+            if (sl != slot) L.longq[k++] = sl;
+          }
+          L.nlong = k;  // scratch: the partial count
+        }
+        __syncthreads();
+        if (merge_partials(L, a, lc, b, L.longq, L.nlong)) {
+          for (int s = tid; s < TAB_SLOTS; s += RED_THREADS) {  // LONG references: piece scratch -> the slice
+            if (slot_tag(L.grp, s) > TAG_PENDING && key_is_hashed(slot_k1(L.grp, s))) {
+              a.tab.sref_off[sbase + s] = lc.sref_off[s];
+              a.tab.sref_len[sbase + s] = lc.sref_len[s];
+            }
+          }
+          __syncthreads();
+          settle_new_long(L, a, b);
+          store_slice(L, a.tab, b);
+          add_fo_hist(L, a);
+          add_bm_bits(L, a);
+          if (tid == 0) {
+            a.tab.occupancy[b] = L.occupied;
+            atomicMax(&a.flags[FLAG_MAX_OCC], L.occupied);
+          }
+        }
+      }
+      __syncthreads();
+    }
+    // 4. next: the bucket with the most runs left (at least RED_STEAL_MIN)
+    if (tid == 0) best = 0;
+    __syncthreads();
+    if ((uint32_t)tid < nb) {
+      const uint32_t g = __hip_atomic_load(&S.next[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t left = g < P ? P - g : 0u;
+      if (left >= RED_STEAL_MIN) atomicMax(&best, ((unsigned long long)left << 32) | (uint32_t)(~tid));
+    }
+    __syncthreads();
+    const unsigned long long bb = best;
+    if (!bb) return;
+    b = __builtin_amdgcn_readfirstlane(~(uint32_t)bb);
+  }
+}
+
 // Rehash parent slice (new_b mod B) of `src` into slice new_b of `dst` (2B
 // buckets).  Source slots hold distinct words, so every one claims a fresh
 // slot (colliding LONG keys stay apart).
@@ -1297,7 +1479,7 @@ __global__ void wc_table_clear(TableView t, size_t n) {
 // one-counter-per-wave form serialised ~16k waves on one address (~200 us).
 __global__ void __launch_bounds__(1024) wc_table_compact(TableView t, const uint64_t* bucket_off, uint64_t* k0,
                                                          uint64_t* k1, uint64_t* cnt, uint64_t* first,
-                                                         uint64_t* sref_off, uint32_t* sref_len) {
+                                                         uint64_t* sref_off, uint32_t* sref_len, Bounds bnd) {
   static_assert(TAB_SLOTS == 4 * 1024, "compact: 4 slots per thread");
   __shared__ uint32_t wsum[16];
   const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1325,6 +1507,7 @@ __global__ void __launch_bounds__(1024) wc_table_compact(TableView t, const uint
     if (kk1[j] == K1_EMPTY) continue;
     const size_t i = base + j;
     const bool h = key_is_hashed(kk1[j]);
+    if (!bounds_ok(bnd, BND_COMPACT, o)) break;
     k0[o] = t.k0[i];
     k1[o] = kk1[j];
     cnt[o] = t.cnt[i];
@@ -1337,7 +1520,7 @@ __global__ void __launch_bounds__(1024) wc_table_compact(TableView t, const uint
 
 // As wc_table_compact, but only (first offset, global slot index) per key.
 __global__ void __launch_bounds__(1024) wc_table_keys(TableView t, const uint64_t* bucket_off, uint64_t* keys,
-                                                      uint32_t* slots) {
+                                                      uint32_t* slots, Bounds bnd) {
   __shared__ uint32_t wsum[16];
   const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const size_t base = (size_t)b * TAB_SLOTS + 4 * tid;
@@ -1362,6 +1545,7 @@ __global__ void __launch_bounds__(1024) wc_table_keys(TableView t, const uint64_
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     if (!occ[j]) continue;
+    if (!bounds_ok(bnd, BND_TABLE_KEYS, o)) break;
     keys[o] = t.first[base + j];
     slots[o] = (uint32_t)(base + j);
     ++o;
@@ -1403,10 +1587,12 @@ __global__ void __launch_bounds__(1024) wc_bucket_offsets(const uint32_t* occ, u
 // Sorted (first, slot) pairs -> the six key columns, read from the table.
 __global__ void wc_gather_table(TableView t, const uint64_t* keys, const uint32_t* slots, uint64_t n,
                                 const uint64_t* dn, uint64_t* ok0, uint64_t* ok1, uint64_t* ocnt, uint64_t* ofirst,
-                                uint64_t* osoff, uint32_t* oslen) {
+                                uint64_t* osoff, uint32_t* oslen, Bounds bnd) {
   if (dn) n = *dn;
+  const Bounds tab{bnd.err, (uint64_t)TAB_SLOTS << t.log2_buckets};
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t j = slots[i];
+    if (!bounds_ok(bnd, BND_GATHER_TABLE, i) || !bounds_ok(tab, BND_GATHER_TABLE, j)) continue;
     const uint64_t k1 = t.k1[j];
     const bool h = key_is_hashed(k1);
     ok0[i] = t.k0[j];
@@ -1420,17 +1606,18 @@ __global__ void wc_gather_table(TableView t, const uint64_t* keys, const uint32_
 
 }  // namespace dev
 
-void launch_table_keys(const TableView& t, const uint64_t* bucket_off, uint64_t* keys, uint32_t* slots, hipStream_t s) {
-  hipLaunchKernelGGL(dev::wc_table_keys, dim3(1u << t.log2_buckets), dim3(1024), 0, s, t, bucket_off, keys, slots);
+void launch_table_keys(const TableView& t, const uint64_t* bucket_off, uint64_t* keys, uint32_t* slots, hipStream_t s,
+                       const Bounds& bnd) {
+  hipLaunchKernelGGL(dev::wc_table_keys, dim3(1u << t.log2_buckets), dim3(1024), 0, s, t, bucket_off, keys, slots, bnd);
 }
 void launch_gather_table(const TableView& t, const uint64_t* keys, const uint32_t* slots, uint64_t n, uint64_t* ok0,
                          uint64_t* ok1, uint64_t* ocnt, uint64_t* ofirst, uint64_t* osoff, uint32_t* oslen,
-                         hipStream_t s, const uint64_t* dn) {
+                         hipStream_t s, const uint64_t* dn, const Bounds& bnd) {
   if (!n) return;
   uint64_t g = (n + 255) / 256;
   g = g > 4096 ? 4096 : g;
   hipLaunchKernelGGL(dev::wc_gather_table, dim3((unsigned)g), dim3(256), 0, s, t, keys, slots, n, dn, ok0, ok1, ocnt,
-                     ofirst, osoff, oslen);
+                     ofirst, osoff, oslen, bnd);
 }
 void launch_bucket_offsets(const uint32_t* occupancy, uint32_t nb, uint64_t* bucket_off, uint64_t* n, hipStream_t s) {
   hipLaunchKernelGGL(dev::wc_bucket_offsets, dim3(1), dim3(1024), 0, s, occupancy, nb, bucket_off, n);
@@ -1444,6 +1631,14 @@ void launch_reduce(const ReduceArgs& a, hipStream_t s, uint32_t extra) {
                            (1u << a.tab.log2_buckets) <= (uint32_t)RED_THREADS),
            "reduce dispatch plan: one record bucket per table bucket, <= MAX_REC_BUCKETS, a partial slot per block");
   hipLaunchKernelGGL(dev::wc_reduce_buckets, dim3(grid), dim3(RED_THREADS), 0, s, a);
+}
+
+void launch_reduce_steal(const ReduceArgs& a, hipStream_t s) {
+  const uint32_t nb = 1u << a.tab.log2_buckets;
+  WC_CHECK(a.steal.next && a.nq > 1 && !a.bucket_enable && !a.bucket_w && a.tab.log2_buckets == a.log2_rec_buckets &&
+               nb * a.nq <= a.part_slots && a.map_blocks <= (uint32_t)RED_MAX_RUNS,
+           "work-stealing reduce: fewer buckets than CUs, one record bucket per table bucket, a slot per block");
+  hipLaunchKernelGGL(dev::wc_reduce_steal, dim3(nb * a.nq), dim3(RED_THREADS), 0, s, a);
 }
 
 void launch_table_split(const TableView& src, const TableView& dst, hipStream_t s) {
@@ -1460,9 +1655,15 @@ void launch_table_clear(const TableView& t, hipStream_t s) {
 }
 
 void launch_table_compact(const TableView& t, const uint64_t* bucket_off, uint64_t* k0, uint64_t* k1, uint64_t* cnt,
-                          uint64_t* first, uint64_t* sref_off, uint32_t* sref_len, hipStream_t s) {
+                          uint64_t* first, uint64_t* sref_off, uint32_t* sref_len, hipStream_t s, const Bounds& bnd) {
   hipLaunchKernelGGL(dev::wc_table_compact, dim3(1u << t.log2_buckets), dim3(1024), 0, s, t, bucket_off, k0, k1, cnt,
-                     first, sref_off, sref_len);
+                     first, sref_off, sref_len, bnd);
+}
+
+const char* bounds_kernel_name(uint32_t k) {
+  static const char* names[BND_KERNELS] = {"none",           "wc_fo_sort",    "wc_bm_place",      "wc_bm_emit",
+                                           "wc_gather_cols", "wc_table_keys", "wc_gather_table", "wc_table_compact"};
+  return k < BND_KERNELS ? names[k] : "unknown";
 }
 
 }  // namespace wc

@@ -23,6 +23,7 @@
 
 #include "../common/hip_util.hpp"
 #include "kernels.hpp"
+#include "bounds.hpp"
 #include "lds_table.hpp"
 
 namespace wc {
@@ -544,6 +545,7 @@ __global__ void __launch_bounds__(64 * FO_SORT_WAVES) wc_fo_sort(OrderDst dst, c
   const auto emit = [&](uint32_t at, uint32_t ei) {
     const FoEntry x = seg[ei];
     const uint64_t j = (uint64_t)off + at;
+    if (!bounds_ok(dst.bnd, BND_FO_SORT, j)) return;
     dst.k0[j] = x.k0;
     dst.k1[j] = x.k1;
     dst.cnt[j] = x.cnt;
@@ -649,6 +651,7 @@ __global__ void __launch_bounds__(64 * FO_SORT_WAVES) wc_fo_sort(OrderDst dst, c
     for (uint32_t i = tid; i < bm; i += T) {
       const FoEntry x = seg[sv[i]];
       const uint64_t j = (uint64_t)boff + i;
+      if (!bounds_ok(dst.bnd, BND_FO_SORT, j)) continue;
       dst.k0[j] = x.k0;
       dst.k1[j] = x.k1;
       dst.cnt[j] = x.cnt;
@@ -665,10 +668,11 @@ __global__ void __launch_bounds__(64 * FO_SORT_WAVES) wc_fo_sort(OrderDst dst, c
 __global__ void wc_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
                                const uint64_t* soff, const uint32_t* slen, const uint32_t* perm, uint64_t* ok0,
                                uint64_t* ok1, uint64_t* ocnt, uint64_t* ofirst, uint64_t* osoff, uint32_t* oslen,
-                               uint64_t n, const uint64_t* dn) {
+                               uint64_t n, const uint64_t* dn, Bounds bnd) {
   if (dn) n = *dn;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t j = perm[i];
+    if (!bounds_ok(bnd, BND_GATHER_COLS, i) || !bounds_ok(bnd, BND_GATHER_COLS, j)) continue;
     ok0[i] = k0[j];
     ok1[i] = k1[j];
     ocnt[i] = cnt[j];
@@ -856,7 +860,7 @@ __global__ void __launch_bounds__(1024) wc_bm_scan(const uint32_t* blocktot, uin
 
 __global__ void __launch_bounds__(256) wc_bm_place(OrderSrc src, uint64_t rows, const unsigned long long* bm,
                                                    uint32_t shift, uint64_t pos_end, const uint32_t* linepre,
-                                                   const uint64_t* blockpre, BmRow* out) {
+                                                   const uint64_t* blockpre, BmRow* out, Bounds bnd) {
   rows = bm_rows(src, rows);
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < rows; i += (uint64_t)gridDim.x * 256) {
     uint64_t f;
@@ -875,6 +879,7 @@ __global__ void __launch_bounds__(256) wc_bm_place(OrderSrc src, uint64_t rows, 
       r += 2 * k + 1 < wi ? __popcll(v.y) : 2 * k + 1 == wi ? __popcll(v.y & below) : 0;
     }
     const uint64_t o = blockpre[line / BM_BLOCK_LINES] + linepre[line] + r;
+    if (!bounds_ok(bnd, BND_BM_PLACE, o)) continue;
     ulonglong2 w[4];
     if (src.table) {
       const uint64_t k1 = src.t.k1[i];
@@ -901,7 +906,11 @@ __global__ void __launch_bounds__(256) wc_bm_place(OrderSrc src, uint64_t rows, 
 __global__ void __launch_bounds__(256) wc_bm_emit(const BmRow* in, const uint64_t* n, OrderDst dst,
                                                   unsigned long long* bm, uint32_t* lc, uint32_t shift,
                                                   uint64_t pos_end) {
-  const uint64_t rows = *n;
+  uint64_t rows = *n;
+  if (rows > dst.bnd.cap) {  // more set bits than rows: record once, emit what fits
+    if (blockIdx.x == 0 && threadIdx.x == 0) (void)bounds_ok(dst.bnd, BND_BM_EMIT, rows - 1);
+    rows = dst.bnd.cap;
+  }
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < rows; i += (uint64_t)gridDim.x * 256) {
     const ulonglong2* q = reinterpret_cast<const ulonglong2*>(in + i);
     const ulonglong2 a = q[0], b = q[1], c = q[2];
@@ -1012,10 +1021,10 @@ uint32_t* first_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound, 
 void launch_gather_cols(const uint64_t* k0, const uint64_t* k1, const uint64_t* cnt, const uint64_t* first,
                         const uint64_t* soff, const uint32_t* slen, const uint32_t* perm, uint64_t* ok0, uint64_t* ok1,
                         uint64_t* ocnt, uint64_t* ofirst, uint64_t* osoff, uint32_t* oslen, uint64_t n, hipStream_t s,
-                        const uint64_t* dn) {
+                        const uint64_t* dn, const Bounds& bnd) {
   if (n)
     hipLaunchKernelGGL(dev::wc_gather_cols, dev::grid_for(n), dim3(256), 0, s, k0, k1, cnt, first, soff, slen, perm,
-                       ok0, ok1, ocnt, ofirst, osoff, oslen, n, dn);
+                       ok0, ok1, ocnt, ofirst, osoff, oslen, n, dn, bnd);
 }
 
 void launch_iota_u32(uint32_t* v, uint64_t n, hipStream_t s) {
@@ -1071,7 +1080,8 @@ uint32_t* bitmap_order(const OrderSrc& src, const OrderDst& dst, uint64_t bound,
   hipLaunchKernelGGL(dev::wc_bm_count, dim3((unsigned)blocks), dim3(dev::BM_BLOCK_LINES), 0, s, lc, lines, linepre,
                      blocktot);
   hipLaunchKernelGGL(dev::wc_bm_scan, dim3(1), dim3(1024), 0, s, blocktot, (uint32_t)blocks, blockpre, n, ctl, ovf);
-  hipLaunchKernelGGL(dev::wc_bm_place, g, dim3(256), 0, s, src, rows, bm, shift, pos_end, linepre, blockpre, rows_buf);
+  hipLaunchKernelGGL(dev::wc_bm_place, g, dim3(256), 0, s, src, rows, bm, shift, pos_end, linepre, blockpre, rows_buf,
+                     dst.bnd);
   const dim3 ge((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(4096, (bound + 255) / 256)));
   hipLaunchKernelGGL(dev::wc_bm_emit, ge, dim3(256), 0, s, rows_buf, n, dst, bm, lc, shift, pos_end);
   return ovf;

@@ -98,6 +98,28 @@ def test_reset_ignores_stale_slices():
     assert_same(again, first)
 
 
+@pytest.mark.parametrize("order,kernel", [("", "wc_fo_sort"), ("radix", "wc_table_keys"), ("bitmap", "wc_bm_place")])
+def test_bounds_guard_names_the_writer(order, kernel, monkeypatch):
+    """The finalize's row writers are bounds-guarded (kernels.hpp Bounds,
+    profiles/r5_fault_hunt.md): a host key count short of the table's keys —
+    the output columns sized too small, the class of the round-4 illegal
+    access — ends in a clean error naming the kernel, not a GPU fault, and the
+    next engine on the device counts exactly."""
+    text = ops.synth_host(4 << 20, seed=3, vocab=20_000)
+    monkeypatch.setenv("WC_FAULT_OCC_UNDER", "3000")  # read at engine creation
+    monkeypatch.setenv("WC_NO_SPECULATE", "1")  # the host-sized finalize
+    if order:
+        monkeypatch.setenv("WC_FIRST_ORDER", order)
+    with ops.Engine(device=0) as e:
+        e.count_bytes(text)
+        with pytest.raises(ops.WcError, match="bounds guard: " + kernel):
+            e.result()
+    monkeypatch.delenv("WC_FAULT_OCC_UNDER")
+    with ops.Engine(device=0) as e:
+        e.count_bytes(text)
+        assert_same(e.result(), ops.cpu_count(text))
+
+
 @pytest.mark.parametrize("opts", [dict(log2_tab_buckets=1, chunk_bytes=8 << 20),
                                   dict(min_records=16384, records_per_byte=0.001, chunk_bytes=1 << 20)])
 def test_speculative_finalize_recovers(opts):
