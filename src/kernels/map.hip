@@ -652,7 +652,7 @@ struct alignas(16) MapLds {
   uint16_t list[MAP_WAVES][MAP_LIST];
   uint16_t dlist[MAP_WAVES][MAP_DEF_CAP];  // deferred LONG entries of a round: pos | (len - 16) << 11 | prev << 15
   uint32_t bcur[2 * MAX_REC_BUCKETS];   // record cursors (map_common.hpp cursors_init): Rec16 | Rec per bucket
-  uint32_t lcur[MAX_REC_BUCKETS / 2];   // LONG-record counts, 16 bits per bucket (map_common.hpp emit_record)
+  uint32_t lcur[MAX_REC_BUCKETS / 2];   // LONG-record counts, 16 bits per bucket (map_common.hpp emit_long)
   uint32_t lovf;                        // a LONG count reached its sub-region
   alignas(16) uint8_t buf[MAP_WAVES][2][BUF];  // two unit slots per wave: the current unit and the one before
   uint32_t next_unit;
@@ -795,7 +795,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
           atomicAdd(&L.cnt[slot], 1u);
           atomicMin(&L.off[slot], (uint32_t)(u0 + q));
         } else {
-          emit_record(L.bcur, L.lcur, &L.lovf, rout, place_hash(k0, k1) & bmask, k0, k1, 1, (uint32_t)(u0 + q));
+          emit_long(L.lcur, &L.lovf, rout, place_hash(k0, k1) & bmask, k0, k1, 1, (uint32_t)(u0 + q));
         }
       }
     }

@@ -215,26 +215,23 @@ __device__ __forceinline__ void put_rec24(const RecOut& o, uint32_t idx, uint64_
 // sub-region.  A count reaching the sub-region size raises the block's
 // overflow word (ovf) at once — a count past 0xFFFF would carry into its
 // neighbour — and the block end checks 24-byte + LONG counts against it.
-// Append one record (key, count, first offset) to bucket b's sub-region.
-// LONG and other 24-byte records share one cursor atomic and one store (a
-// lane-selected address, increment and index): a wave mixing the three kinds
-// runs two divergent emit paths, not three.
+// The deferred-LONG pass calls this directly (every key there is hashed): no
+// Rec16 / 24-byte paths in the unit loop's register budget.
+__device__ __forceinline__ void emit_long(uint32_t* lcur, uint32_t* ovf, const RecOut& o, uint32_t b, uint64_t k0,
+                                          uint64_t k1, uint64_t cnt, uint32_t off) {
+  const uint32_t sh = 16u * (b & 1u);
+  const uint32_t c = (atomicAdd(&lcur[b >> 1], 1u << sh) >> sh) & 0xFFFFu;
+  if (c >= o.sub) *ovf = 1u;
+  put_rec24(o, b * o.sub + (o.sub - 1u) - min(c, o.sub - 1u), k0, k1, cnt, off);
+}
+
+// Append one record (key, count, first offset) to bucket b's sub-region (the
+// hot-table flush: any kind).
 __device__ __forceinline__ void emit_record(uint32_t* cur, uint32_t* lcur, uint32_t* ovf, const RecOut& o, uint32_t b,
                                             uint64_t k0, uint64_t k1, uint64_t cnt, uint32_t off) {
-  if (rec16_fits(k0, k1, cnt)) {
-    put_rec16(o, atomicAdd(&cur[b], 1u), make_rec16(k0, k1, off));
-    return;
-  }
-  const bool lg = key_is_hashed(k1);
-  const uint32_t sh = lg ? 16u * (b & 1u) : 0u;
-  const uint32_t c = atomicAdd(lg ? &lcur[b >> 1] : &cur[MAX_REC_BUCKETS + b], 1u << sh);
-  uint32_t idx = c;
-  if (lg) {
-    const uint32_t n = (c >> sh) & 0xFFFFu;
-    if (n >= o.sub) *ovf = 1u;
-    idx = b * o.sub + (o.sub - 1u) - min(n, o.sub - 1u);
-  }
-  put_rec24(o, idx, k0, k1, cnt, off);
+  if (rec16_fits(k0, k1, cnt)) put_rec16(o, atomicAdd(&cur[b], 1u), make_rec16(k0, k1, off));
+  else if (key_is_hashed(k1)) emit_long(lcur, ovf, o, b, k0, k1, cnt, off);
+  else put_rec24(o, atomicAdd(&cur[MAX_REC_BUCKETS + b], 1u), k0, k1, cnt, off);
 }
 
 // Two single-occurrence records of one lane (either may be absent; n1 / n2:
