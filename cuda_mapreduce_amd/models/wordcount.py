@@ -46,10 +46,12 @@ CONFIGS = {
                   "N > 1: shuffle merge — all-to-all to hash owners over xGMI)"),
         JobConfig("64gb", "64 GB synthetic text, single MI355X (HBM-resident, chunked)", bytes_per_gpu=64 * GiB,
                   chunk_bytes=2 * GiB),
-        # the config names the reduce-scatter merge: dense protocol (modelled at W = 8, 100k keys/rank:
-        # ~0.06 ms per job more than the shuffle's all-to-all, profiles/merge_cost.md; unmeasured at W = 8)
-        JobConfig("256gb-8gpu", "256 GB synthetic text sharded across 8x MI355X, RCCL reduce-scatter merge",
-                  bytes_per_gpu=32 * GiB, gpus=8, chunk_bytes=2 * GiB, merge="dense"),
+        # shuffle merge: per-rank merge cost measured at W = 1 / 2 / 4 / 8 (kernel traces + wire bytes,
+        # profiles/r5_merge_rank_cost.md) predicts it 26-34 % below the dense reduce-scatter protocol at
+        # 100k and 1M keys / rank on an 8-GPU xGMI node (fewer kernels, 3 collectives instead of 5,
+        # 30-45 % fewer bytes); --merge dense still selects the reduce-scatter protocol
+        JobConfig("256gb-8gpu", "256 GB synthetic text sharded across 8x MI355X, RCCL all-to-all (shuffle) merge",
+                  bytes_per_gpu=32 * GiB, gpus=8, chunk_bytes=2 * GiB, merge="shuffle"),
         JobConfig("1tb-8gpu-host-staged", "1 TB synthetic text, 8x MI355X, host-staged pinned hipMemcpyAsync",
                   bytes_per_gpu=128 * GiB, gpus=8, source="host-staged", chunk_bytes=GiB),
     ]

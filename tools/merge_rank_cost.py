@@ -10,6 +10,14 @@ per rank: device time + sum over collectives of the largest per-peer amount /
 one xGMI link (~153 GB/s, each peer pair on its own link) + ~10 us launch
 latency per collective.
 
+The W virtual ranks share ONE GPU: their merge kernels run beside the other
+ranks' map / reduce kernels, so their traced durations include waiting for CUs
+(the max rank's merge reads 2-8x the W = 1 cost).  The second prediction
+takes the uncontended device time from the W = 1 run of the same vocabulary
+and protocol (the protocol forced on: WC_MERGE_ALWAYS=1): with a shared Zipf
+vocabulary each owner receives about one rank's key count whatever W, so an
+owner's kernels do the W = 1 work; the wire term is the W-rank one.
+
 usage: python tools/merge_rank_cost.py DIR   (markdown table on stdout)
 """
 import csv
@@ -71,15 +79,20 @@ def main(d):
         sent = max((w["merge_sent_bytes"] for w in wire), default=0)
         dev = max(per_rank) if per_rank else float("nan")
         pred = dev + peer / (LINK_GBS * 1e3) + COLL_US * coll
-        rows.append((info["virtual_ranks"], info["config"]["vocab"], info["config"]["merge"], dev,
-                     statistics.mean(per_rank) if per_rank else float("nan"), coll, sent, peer, pred,
-                     info["validated"], info["merges_planned_rank0"], info["merge_redos_rank0"]))
-    rows.sort(key=lambda r: (r[1], r[2], r[0]))
-    print("| W | keys/rank | protocol | merge kernels us (max rank) | (mean rank) | collectives | bytes sent / rank |"
-          " largest per-peer bytes (sum) | predicted 8-GPU-node merge us | validated | planned / redos |")
-    print("|---:|---:|---|---:|---:|---:|---:|---:|---:|---|---|")
+        rows.append([info.get("virtual_ranks", 1), info["config"]["vocab"], info["config"]["merge"], dev,
+                     statistics.mean(per_rank) if per_rank else float("nan"), coll, sent, peer, pred, float("nan"),
+                     info["validated"], info.get("merges_planned_rank0", 0), info.get("merge_redos_rank0", 0)])
+    solo = {(r[1], r[2]): r[3] for r in rows if r[0] == 1}
     for r in rows:
-        print("| %d | %d | %s | %.1f | %.1f | %d | %d | %d | %.1f | %s | %d / %d |" % r)
+        if (r[1], r[2]) in solo:
+            r[9] = solo[(r[1], r[2])] + r[7] / (LINK_GBS * 1e3) + COLL_US * r[5]
+    rows.sort(key=lambda r: (r[1], r[2], r[0]))
+    print("| W | keys/rank | protocol | merge kernels us (max rank, contended) | (mean rank) | collectives |"
+          " bytes sent / rank | largest per-peer bytes (sum) | predicted: contended kernels + wire, us |"
+          " predicted: W=1 kernels + wire, us | validated | planned / redos |")
+    print("|---:|---:|---|---:|---:|---:|---:|---:|---:|---:|---|---|")
+    for r in rows:
+        print("| %d | %d | %s | %.1f | %.1f | %d | %d | %d | %.1f | %.1f | %s | %d / %d |" % tuple(r))
 
 
 if __name__ == "__main__":
