@@ -264,7 +264,7 @@ Engine::Impl::~Impl() {
   if (d_red_blk && red_blk_grid) {  // the last reduce launch, block by block (100 MHz realtime ticks -> us)
     std::vector<unsigned long long> h(red_blk_grid * RED_BLK_WORDS);
     if (hipMemcpy(h.data(), d_red_blk, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-      struct B { double start, dur; uint32_t b, q; unsigned long long n16, n24, nl; };
+      struct B { double start, dur; uint32_t b, q; unsigned long long n16, n24, nl; double streams, arrive; };
       std::vector<B> v;
       unsigned long long t0 = ~0ull, t1 = 0;
       for (size_t i = 0; i < red_blk_grid; ++i) {
@@ -273,7 +273,7 @@ Engine::Impl::~Impl() {
         t0 = std::min(t0, r[1]);
         t1 = std::max(t1, r[2]);
         v.push_back(B{(double)r[1], (r[2] - r[1]) / 100.0, (uint32_t)r[0], (uint32_t)(r[0] >> 32), r[3] & 0xFFFFFFFFull,
-                      r[3] >> 32, r[4]});
+                      r[3] >> 32, r[4], (r[5] - r[1]) / 100.0, (r[6] - r[1]) / 100.0});
       }
       if (!v.empty()) {
         double sum = 0;
@@ -281,9 +281,13 @@ Engine::Impl::~Impl() {
         std::sort(v.begin(), v.end(), [](const B& a, const B& b) { return a.dur > b.dur; });
         fprintf(stderr, "[wc] reduce blocks (last launch): %zu blocks, span %.1f us, duration mean %.1f max %.1f us\n",
                 v.size(), (t1 - t0) / 100.0, sum / v.size(), v[0].dur);
-        for (size_t i = 0; i < v.size() && i < 8; ++i)
-          fprintf(stderr, "[wc]   #%zu bucket %u q %u: %.1f us from %.1f us, records 16B %llu 24B %llu, LONG %llu\n", i,
-                  v[i].b, v[i].q, v[i].dur, (v[i].start - t0) / 100.0, v[i].n16, v[i].n24, v[i].nl);
+        const size_t show = std::getenv("WC_RED_BLK_ALL") ? v.size() : 8;  // tools/red_blocks.sh: every block
+        for (size_t i = 0; i < v.size() && i < show; ++i)
+          fprintf(stderr,
+                  "[wc]   #%zu bucket %u q %u: %.1f us from %.1f us, records 16B %llu 24B %llu, LONG %llu; streams end "
+                  "%.1f, arrival %.1f us\n",
+                  i, v[i].b, v[i].q, v[i].dur, (v[i].start - t0) / 100.0, v[i].n16, v[i].n24, v[i].nl, v[i].streams,
+                  v[i].arrive);
         double m16 = 0, m24 = 0, ml = 0;
         for (auto& x : v) m16 += x.n16, m24 += x.n24, ml += (double)x.nl;
         fprintf(stderr, "[wc]   mean records 16B %.0f 24B %.0f LONG %.0f\n", m16 / v.size(), m24 / v.size(),

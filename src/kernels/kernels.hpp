@@ -240,7 +240,7 @@ constexpr uint32_t RED_STEAL_CH = 32;    // work-stealing reduce: runs per grab 
 constexpr uint32_t RED_STEAL_PL = 32;    // pieces per bucket at most
 constexpr uint32_t RED_STEAL_MIN = 16;   // runs left for a steal to start a piece
 // Reduce diagnostic counters (src/kernels/reduce.hip built with -DWC_RED_STAMPS=1).
-constexpr int RED_BLK_WORDS = 5;
+constexpr int RED_BLK_WORDS = 7;  // bucket | q, start, end, n16 | n24, LONG, streams end, arrival
 enum : int { RS_RECORDS = 0, RS_SLOW_LANES, RS_SLOW_WAVES, RS_PROBE_ITERS, RS_CAS_FAIL, RS_PENDING, RS_CLAIMS,
              RS_T_WAVE, RS_T_SLOW, RS_T_RUNS, RS_BLOCKS, RS_T_BLKMAX, RS_T_STREAMS, RS_NLONG, RS_LONG_STREAMED,
              RED_STAMP_N };

@@ -1158,11 +1158,14 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
     atomicOr(&a.flags[FLAG_TABLE_OVF], 1u);
   }
   bool store = !L.overflow;
+  const uint64_t rt_streams = WC_RED_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;
+  uint64_t rt_arrive = rt_streams;
   if (split) {
     // every quarter publishes its partial table; the last to arrive merges the
     // others into its own LDS table and stores the bucket
     if (!L.overflow) write_partial(L, a, lc, blockIdx.x);
     store = split_arrive_last(L, a, b, nq);
+    if (WC_RED_STAMPS) rt_arrive = __builtin_amdgcn_s_memrealtime();
     if (store) {
       if (tid == 0) {  // the other quarters' partial slots
         uint32_t k = 0;
@@ -1217,6 +1220,8 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
       r[2] = __builtin_amdgcn_s_memrealtime();
       r[3] = n16 | (n24 << 32);
       r[4] = L.st[RS_NLONG];
+      r[5] = rt_streams;
+      r[6] = rt_arrive;
     }
   }
 }
