@@ -1102,6 +1102,22 @@ void Engine::reset() {
   // WC_STAMPS_PER_JOB=1 (diagnostics): the map / reduce stamp sums printed at
   // teardown cover the last job only (the first job's table growth excluded)
   static const bool stamps_per_job = std::getenv("WC_STAMPS_PER_JOB") && std::atoi(std::getenv("WC_STAMPS_PER_JOB"));
+  // WC_MAP_CLOCK=1 (with the stamps build path): the previous job's effective
+  // shader clock during the map — s_memtime ticks over 100 MHz realtime ticks,
+  // summed over the map blocks (tools/ramp_probe.py: is the short-run ramp the clock?)
+  static const bool map_clock = std::getenv("WC_MAP_CLOCK") && std::atoi(std::getenv("WC_MAP_CLOCK"));
+  if (map_clock && im.d_stamps && im.d_blk) {
+    WC_HIP_CHECK(hipStreamSynchronize(im.s));
+    unsigned long long st[MAP_STAMP_N];
+    std::vector<unsigned long long> blk((size_t)im.map_blocks * 4);
+    WC_HIP_CHECK(hipMemcpy(st, im.d_stamps, sizeof st, hipMemcpyDeviceToHost));
+    WC_HIP_CHECK(hipMemcpy(blk.data(), im.d_blk, blk.size() * 8, hipMemcpyDeviceToHost));
+    double rt = 0;
+    for (size_t i = 0; i < im.map_blocks; ++i) rt += (double)(blk[4 * i + 1] - blk[4 * i]);
+    if (rt > 0 && st[MS_BLKSUM])
+      fprintf(stderr, "[wc] job map clock %.0f MHz (memtime %.3e / realtime %.3e), mean map block %.1f us\n",
+              (double)st[MS_BLKSUM] / rt * 100.0, (double)st[MS_BLKSUM], rt, rt / im.map_blocks / 100.0);
+  }
   if (stamps_per_job && im.d_stamps) {
     WC_HIP_CHECK(hipMemsetAsync(im.d_stamps, 0, MAP_STAMP_N * 8, im.s));
     WC_HIP_CHECK(hipMemsetAsync(im.d_red_stamps, 0, RED_STAMP_N * 8, im.s));
