@@ -505,14 +505,16 @@ int wc_engine_stats_json(wc_engine* e, char* buf, int cap) {
   const wc::Stats& s = e->e->stats();
   char tmp[1024];
   const int k = snprintf(tmp, sizeof tmp,
-                         "{\"bytes\": %llu, \"tokens\": %llu, \"keys\": %llu, \"records\": %llu, \"chunks\": %u, "
+                         "{\"bytes\": %llu, \"tokens\": %llu, \"keys\": %llu, \"records\": %llu, "
+                         "\"long_tokens\": %llu, \"long_direct\": %u, \"chunks\": %u, "
                          "\"map_reruns\": %u, \"table_splits\": %u, \"log2_buckets\": %u, \"order_path\": %u, "
                          "\"merges_planned\": %u, \"merge_redos\": %u, "
                          "\"device_ms\": {\"map\": %.4f, \"reduce\": %.4f, \"finalize\": %.4f, \"merge\": %.4f, "
                          "\"idle\": %.4f, \"total\": %.4f}, "
                          "\"host_ms\": {\"count\": %.4f, \"finalize\": %.4f}}",
                          (unsigned long long)s.bytes, (unsigned long long)s.tokens, (unsigned long long)s.keys,
-                         (unsigned long long)s.records, s.chunks, s.map_reruns, s.table_splits, s.log2_buckets, s.order_path,
+                         (unsigned long long)s.records, (unsigned long long)s.long_tokens, s.long_direct, s.chunks,
+                         s.map_reruns, s.table_splits, s.log2_buckets, s.order_path,
                          s.merges_planned, s.merge_redos,
                          s.map_ms,
                          s.reduce_ms, s.finalize_ms, s.merge_ms, s.idle_ms, s.device_ms, s.host_count_ms,

@@ -88,6 +88,8 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   if (const char* e = std::getenv("WC_RED_Q")) red_q_force = (uint32_t)std::atoi(e);    // sweeps only
   if (const char* e = std::getenv("WC_RED_PLAN")) red_plan = std::atoi(e) != 0;  // A/B: 0 = the uniform split
   if (const char* e = std::getenv("WC_RED_STEAL")) red_steal = std::atoi(e) != 0;  // A/B: 0 = the uniform split
+  if (const char* e = std::getenv("WC_LONG_DIRECT")) long_direct_force = std::atoi(e) != 0 ? 1 : 0;  // A/B
+  long_direct = long_direct_force == 1;
   if (const char* e = std::getenv("WC_FAULT_OCC_UNDER")) fault_occ_under = std::strtoull(e, nullptr, 10);  // tests
   dev_malloc(&d_bounds, 64);
   WC_HIP_CHECK(hipMemset(d_bounds, 0, 64));
@@ -403,6 +405,9 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   WC_CHECK(pass_rec.subcap > 0, "shuffle record capacity below one record per (map block, bucket)");
   MapArgs m{text,     len,          avail,          prev,     log2_rb, pass_rec, d_ctr->flags, &d_ctr->tokens,
             k1_mask,  d_stamps,     d_blk,          planned ? d_bucket_w : nullptr};
+  pass_ld = long_direct;
+  m.long_direct = pass_ld;
+  m.long_tokens = &d_ctr->long_tokens;
   if (d_stamps) blocks_stamped += blocks;
   hot.text = text;
   hot.nblk = blocks;
@@ -420,6 +425,7 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
                 bm, bm ? bitmap_order_linecnt(bm, bm_end, 1) : nullptr, bm ? bitmap_order_ctl(bm, bm_end, 1) : nullptr,
                 bm ? (bm_end >> 1) + 1 : 0, 1u, planned ? 1u : red_q(), planned ? d_bucket_w : nullptr, part,
                 part_blocks, stealing ? steal : ReduceArgs::Steal{}};
+  ra.long_direct = pass_ld;
   if (planned && ra.blk) red_blk_grid = nbk + plan_extra;
   if (stealing) launch_reduce_steal(ra, s);
   else launch_reduce(ra, s, plan_extra);
@@ -653,6 +659,10 @@ bool Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
   }
   const uint64_t tokens = c.tokens;
   st.records += c.records;
+  st.long_tokens += c.long_tokens;
+  st.long_direct = pass_ld ? 1u : 0u;
+  // the next pass's LONG-record layout, from this pass's LONG share
+  long_direct = long_direct_force >= 0 ? long_direct_force == 1 : c.long_tokens * 64 > c.records;
   {  // hot-table reuse bookkeeping (see launch_pass)
     const double miss = tokens ? (double)c.records / (double)tokens : 0.0;
     if (pass_sampled) {
@@ -680,6 +690,7 @@ bool Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
                   avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
                   d_ctr->flags, d_bucket_ovf, d_bucket_en, d_red_stamps, red_blk(), fo_hist_ok ? d_fo_hist : nullptr, fo_hist_m,
                   nullptr, nullptr, nullptr, 0, 0u, red_q(), nullptr, part, part_blocks, ReduceArgs::Steal{}};
+    ra.long_direct = pass_ld;  // the pass's records: its map's LONG layout
     launch_reduce(ra, s);
     check_table("a split re-run's reduce");
     PubList pc{};

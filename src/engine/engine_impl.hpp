@@ -21,6 +21,7 @@ struct DevCounters {
   uint32_t flags[FLAG_COUNT];
   unsigned long long tokens;
   unsigned long long records;
+  unsigned long long long_tokens;  // LONG-word tokens of the pass (MapArgs::long_tokens)
 };
 
 // Running table storage (own allocation: it grows by splitting).
@@ -70,7 +71,15 @@ struct Engine::Impl {
   size_t red_blk_grid = 0;
   uint32_t fin_seq = 0;
   bool red_plan = true;
-  bool red_steal = false;           // the work-stealing split reduce (WC_RED_STEAL=1; A/B pending)
+  bool red_steal = false;           // the work-stealing split reduce (WC_RED_STEAL=1; measured slower)
+  // LONG-word records top-down + streamed by the reduce (MapArgs::long_direct):
+  // chosen per pass from the LONG share of the pass before (LONG tokens > 1/64
+  // of its records; the first pass of an engine: off); both modes are exact for any
+  // text — the instances without the LONG stream run the LONG-free headline
+  // text ~1 % faster (profiles/r5_session.md §5).  WC_LONG_DIRECT=0|1 forces.
+  bool long_direct = false;
+  int long_direct_force = -1;
+  bool pass_ld = false;  // the mode of the pass in flight (its map, its reduce and any re-run of it)
   ReduceArgs::Steal steal{};
   // WC_CHECK_TABLE=1 (debug): after every reduce and split the table's
   // invariants are checked on the device and a violation fails the job naming

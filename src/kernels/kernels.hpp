@@ -113,6 +113,14 @@ struct MapArgs {
   // every map block's run (Rec16 records + RED_W24 x 24-byte records) — the
   // balanced reduce's plan (ReduceArgs::bucket_w)
   uint32_t* bucket_w;
+  // LONG-word records (hashed keys): true = into the top of their 24-byte
+  // sub-region (Records::count_long, streamed by the reduce's long_direct);
+  // false = appended to the 24-byte run like any 24-byte record (the reduce
+  // queues them while it streams).  The engine picks per pass from the LONG
+  // token share of the pass before (Engine::Impl::long_direct); every pass's reduce
+  // runs the same mode (ReduceArgs::long_direct).
+  bool long_direct = false;
+  unsigned long long* long_tokens = nullptr;  // nullable: += LONG-word tokens of the pass (hot hits included)
 };
 // Reduce cost of a record relative to a Rec16 one in the dispatch plan: a
 // LONG word's byte comparison (a random 64-byte text read) costs ~10-20x a
@@ -232,6 +240,7 @@ struct ReduceArgs {
     uint32_t* plist;           // [nb][RED_STEAL_PL] partial slots of the registered pieces
     uint32_t* slot_ctr;        // partial slots handed out
   } steal;
+  bool long_direct = false;  // the pass's map wrote LONG records top-down (MapArgs::long_direct)
 };
 // Most reduce blocks per bucket (split reduce: fewer table buckets than CUs).
 constexpr uint32_t RED_SPLIT_MAX_Q = 16;

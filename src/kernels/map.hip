@@ -654,6 +654,7 @@ struct alignas(16) MapLds {
   uint32_t bcur[2 * MAX_REC_BUCKETS];   // record cursors (map_common.hpp cursors_init): Rec16 | Rec per bucket
   uint32_t lcur[MAX_REC_BUCKETS / 2];   // LONG-record counts, 16 bits per bucket (map_common.hpp emit_long)
   uint32_t lovf;                        // a LONG count reached its sub-region
+  uint32_t nltok;                       // LONG-word tokens of this block (MapArgs::long_tokens)
   alignas(16) uint8_t buf[MAP_WAVES][2][BUF];  // two unit slots per wave: the current unit and the one before
   uint32_t next_unit;
   unsigned long long used, tokens;
@@ -694,7 +695,7 @@ __device__ __forceinline__ uint32_t* at_byte(uint32_t* base, int o) {
   return reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(base) + o);
 }
 
-template <bool ST>
+template <bool ST, bool LD>
 __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   __shared__ MapLds L;
   __shared__ unsigned long long st_acc[ST ? MAP_STAMP_N : 1];
@@ -719,6 +720,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     L.next_unit = 0;
     L.used = L.tokens = 0;
     L.lovf = 0;
+    L.nltok = 0;
   }
   __syncthreads();
 
@@ -761,6 +763,9 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   // bytes) or an 8-byte SWAR scan (>= 31), one record each; 64 per pass, both
   // unit slots still in LDS.
   auto run_deferred = [&]() {
+    // the pass's LONG share picks the next pass's record layout: an LDS count of
+    // the round's LONG tokens (ndef is wave-uniform; no register held across the loop)
+    if (lane == 0 && ndef) atomicAdd(&L.nltok, ndef);
     wave_sync();
     for (uint32_t c = 0; c < ndef; c += 64) {
       const bool hv = c + lane < ndef;
@@ -795,7 +800,9 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
           atomicAdd(&L.cnt[slot], 1u);
           atomicMin(&L.off[slot], (uint32_t)(u0 + q));
         } else {
-          emit_long(L.lcur, &L.lovf, rout, place_hash(k0, k1) & bmask, k0, k1, 1, (uint32_t)(u0 + q));
+          const uint32_t bk = place_hash(k0, k1) & bmask;
+          if constexpr (LD) emit_long(L.lcur, &L.lovf, rout, bk, k0, k1, 1, (uint32_t)(u0 + q));
+          else put_rec24(rout, atomicAdd(&L.bcur[MAX_REC_BUCKETS + bk], 1u), k0, k1, 1, (uint32_t)(u0 + q));
         }
       }
     }
@@ -1156,7 +1163,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     const uint64_t sd = (two_word(sg) || is_long_sig(sg)) ? L.sig[s | 1] : 0ull;
     if (is_long_sig(sg)) key_long_line(h.long_bytes + (sd >> 32) * 64, (uint32_t)sd, a.k1_mask, k0, k1);
     else sig_key(sg, sd, k0, k1);
-    emit_record(L.bcur, L.lcur, &L.lovf, rout, place_hash(k0, k1) & bmask, k0, k1, c, L.off[s]);
+    emit_record<LD>(L.bcur, L.lcur, &L.lovf, rout, place_hash(k0, k1) & bmask, k0, k1, c, L.off[s]);
   }
   clk.lap(MS_FLUSH);
   if constexpr (ST) {
@@ -1204,6 +1211,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   if (tid == 0) {
     atomicAdd(a.tokens, L.tokens);
     atomicAdd(a.rec.cursor, L.used);
+    if (L.nltok && a.long_tokens) atomicAdd(a.long_tokens, (unsigned long long)L.nltok);
   }
 }
 
@@ -1217,8 +1225,13 @@ void launch_map(const MapArgs& a, const HotArgs& h, uint32_t map_blocks, hipStre
   } else {
     launch_zero_regions(z, s);
   }
-  if (a.stamps) hipLaunchKernelGGL(dev::wc_map<true>, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
-  else hipLaunchKernelGGL(dev::wc_map<false>, dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
+  if (a.stamps) {
+    if (a.long_direct) hipLaunchKernelGGL((dev::wc_map<true, true>), dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
+    else hipLaunchKernelGGL((dev::wc_map<true, false>), dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
+  } else {
+    if (a.long_direct) hipLaunchKernelGGL((dev::wc_map<false, true>), dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
+    else hipLaunchKernelGGL((dev::wc_map<false, false>), dim3(map_blocks), dim3(MAP_THREADS), 0, s, a, h);
+  }
 }
 
 }  // namespace wc

@@ -226,11 +226,12 @@ __device__ __forceinline__ void emit_long(uint32_t* lcur, uint32_t* ovf, const R
 }
 
 // Append one record (key, count, first offset) to bucket b's sub-region (the
-// hot-table flush: any kind).
+// hot-table flush: any kind).  LD: LONG records top-down (emit_long).
+template <bool LD>
 __device__ __forceinline__ void emit_record(uint32_t* cur, uint32_t* lcur, uint32_t* ovf, const RecOut& o, uint32_t b,
                                             uint64_t k0, uint64_t k1, uint64_t cnt, uint32_t off) {
   if (rec16_fits(k0, k1, cnt)) put_rec16(o, atomicAdd(&cur[b], 1u), make_rec16(k0, k1, off));
-  else if (key_is_hashed(k1)) emit_long(lcur, ovf, o, b, k0, k1, cnt, off);
+  else if (LD && key_is_hashed(k1)) emit_long(lcur, ovf, o, b, k0, k1, cnt, off);
   else put_rec24(o, atomicAdd(&cur[MAX_REC_BUCKETS + b], 1u), k0, k1, cnt, off);
 }
 

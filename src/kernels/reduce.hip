@@ -27,6 +27,7 @@
 #include "kernels.hpp"
 
 #include "bounds.hpp"
+#include "map_common.hpp"  // wave_incl_sum (DPP wave scan)
 #include "lds_table.hpp"
 #include "common/hip_util.hpp"
 
@@ -522,11 +523,7 @@ __device__ __forceinline__ void merge_stream(RedLds& L, const ReduceArgs& a, uin
     const uint32_t packed = L.runcnt[p0 + lane * pstride];
     c = min(R16 ? (packed & 0xFFFFu) : (packed >> 16), sub);
   }
-  uint32_t incl = c;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
-    if ((int)lane >= o) incl += y;
-  }
+  const uint32_t incl = wave_incl_sum(c);  // DPP: no bpermute lane addresses held across the stream
   const uint32_t N = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   if (N == 0) return;
   const uint32_t P = incl - c;
@@ -593,11 +590,7 @@ __device__ __forceinline__ void long_direct(RedLds& L, const ReduceArgs& a, cons
   const uint32_t pe = min(p_end, a.map_blocks);
   const uint32_t nj = p0 < pe ? (pe - p0 + pstride - 1) / pstride : 0u;  // <= 64 (pstride >= 16)
   const uint32_t cnt = lane < nj ? (uint32_t)L.runlong[p0 + lane * pstride] : 0u;
-  uint32_t incl = cnt;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
-    if ((int)lane >= o) incl += y;
-  }
+  const uint32_t incl = wave_incl_sum(cnt);
   const uint32_t N = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   if (N == 0) return;
   const uint32_t P = incl - cnt;
@@ -1083,6 +1076,10 @@ __device__ __forceinline__ bool lpt_piece(const ReduceArgs& a, uint32_t& b, uint
   return true;
 }
 
+// LD: the pass's map wrote LONG records top-down (MapArgs::long_direct) and
+// they stream through long_direct; otherwise they sit in the 24-byte runs and
+// merge_batch queues them (an instance without long_direct's code).
+template <bool LD>
 __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   __shared__ RedLds L;
   if (a.flags[FLAG_REGION_OVF]) return;  // shuffle output incomplete: host re-runs the chunk
@@ -1107,7 +1104,7 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
     const uint32_t rb0 = b & ((1u << a.log2_rec_buckets) - 1u), nrb0 = 1u << a.log2_rec_buckets;
     for (uint32_t p = tid; p < a.map_blocks; p += RED_THREADS) {
       L.runcnt[p] = a.rec.count[(size_t)p * nrb0 + rb0];
-      L.runlong[p] = (uint16_t)a.rec.count_long[(size_t)p * nrb0 + rb0];
+      if (LD) L.runlong[p] = (uint16_t)a.rec.count_long[(size_t)p * nrb0 + rb0];
     }
   }
   if (tid == 0) {
@@ -1145,7 +1142,7 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
     if (L.nlong <= LONGQ) long_queue(L, a, lc, L.nlong, claims);
     else long_stream(L, a, lc, b, wave, p0, pstride, nrb, rb, (uint32_t)sub, shift, claims);
   }
-  long_direct(L, a, lc, b, p0, pstride, nrb, rb, (uint32_t)sub, shift, claims);
+  if constexpr (LD) long_direct(L, a, lc, b, p0, pstride, nrb, rb, (uint32_t)sub, shift, claims);
   for (int o = 32; o > 0; o >>= 1) claims += __shfl_down(claims, o);
   if ((tid & 63) == 0 && claims) atomicAdd(&L.occupied, claims);
   if (WC_RED_STAMPS && (tid & 63) == 0)
@@ -1635,7 +1632,8 @@ void launch_reduce(const ReduceArgs& a, hipStream_t s, uint32_t extra) {
                            (1u << a.tab.log2_buckets) <= (uint32_t)MAX_REC_BUCKETS && grid <= a.part_slots &&
                            (1u << a.tab.log2_buckets) <= (uint32_t)RED_THREADS),
            "reduce dispatch plan: one record bucket per table bucket, <= MAX_REC_BUCKETS, a partial slot per block");
-  hipLaunchKernelGGL(dev::wc_reduce_buckets, dim3(grid), dim3(RED_THREADS), 0, s, a);
+  if (a.long_direct) hipLaunchKernelGGL(dev::wc_reduce_buckets<true>, dim3(grid), dim3(RED_THREADS), 0, s, a);
+  else hipLaunchKernelGGL(dev::wc_reduce_buckets<false>, dim3(grid), dim3(RED_THREADS), 0, s, a);
 }
 
 void launch_reduce_steal(const ReduceArgs& a, hipStream_t s) {
