@@ -61,6 +61,7 @@ constexpr int HALO = 64;               // bytes past the unit kept in LDS
 // (2136-byte buffers put odd waves at 8 mod 16: SQ_LDS_UNALIGNED_STALL 3.0e7 / GiB)
 constexpr int BUF = (UNIT + HALO + 24 + 15) / 16 * 16;
 constexpr int MAP_DEF_CAP = 248;       // deferred LONG entries per wave and round (>= 128 + UNIT / 17)
+constexpr int MAP_DEF_CAP_Q = 256;     // the same, queue layout (no LONG cursors in its LDS)
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr int GS = HOT_GROUP_SLOTS;    // slots per group
 constexpr int NG = HOT_GROUPS;         // groups
@@ -645,21 +646,25 @@ __device__ void build_image(const HotArgs& h, uint64_t* isig, uint32_t* scratch,
 // cnt / off first: every per-token LDS address (the two hit atomics at 4 s
 // and 16 KiB + 4 s, the probe reads at 32 KiB + 16 g) is one VGPR plus an
 // immediate ds offset (< 64 KiB) — no VALU add per token
+// LD: the top-down LONG layout's LDS (its 16-bit LONG cursors take what the
+// deferred lists give up); the queue layout keeps round 4's layout exactly.
+template <bool LD>
 struct alignas(16) MapLds {
   uint32_t cnt[MAP_SLOTS];
   uint32_t off[MAP_SLOTS];              // chunk-relative first offset in the block
   alignas(16) uint64_t sig[MAP_SLOTS];  // hot table image (read-only while tokens stream); 0 = empty
   uint16_t list[MAP_WAVES][MAP_LIST];
-  uint16_t dlist[MAP_WAVES][MAP_DEF_CAP];  // deferred LONG entries of a round: pos | (len - 16) << 11 | prev << 15
+  uint16_t dlist[MAP_WAVES][LD ? MAP_DEF_CAP : MAP_DEF_CAP_Q];  // deferred LONG entries of a round: pos | (len - 16) << 11 | prev << 15
   uint32_t bcur[2 * MAX_REC_BUCKETS];   // record cursors (map_common.hpp cursors_init): Rec16 | Rec per bucket
-  uint32_t lcur[MAX_REC_BUCKETS / 2];   // LONG-record counts, 16 bits per bucket (map_common.hpp emit_long)
+  uint32_t lcur[LD ? MAX_REC_BUCKETS / 2 : 1];  // LONG-record counts, 16 bits per bucket (map_common.hpp emit_long)
   uint32_t lovf;                        // a LONG count reached its sub-region
   uint32_t nltok;                       // LONG-word tokens of this block (MapArgs::long_tokens)
   alignas(16) uint8_t buf[MAP_WAVES][2][BUF];  // two unit slots per wave: the current unit and the one before
   uint32_t next_unit;
   unsigned long long used, tokens;
 };
-static_assert(sizeof(MapLds) + 8 * MAP_STAMP_N <= 160 * 1024, "one map block per CU");
+static_assert(sizeof(MapLds<true>) + 8 * MAP_STAMP_N <= 160 * 1024, "one map block per CU");
+static_assert(sizeof(MapLds<false>) + 8 * MAP_STAMP_N <= 160 * 1024, "one map block per CU");
 static_assert(MAP_DEF_CAP >= 128 + UNIT / 17, "a round defers at most 127 carried + UNIT / 17 LONG tokens");
 static_assert(GS == 2, "pair-packed two-word words: 2-slot groups");
 
@@ -697,7 +702,7 @@ __device__ __forceinline__ uint32_t* at_byte(uint32_t* base, int o) {
 
 template <bool ST, bool LD>
 __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
-  __shared__ MapLds L;
+  __shared__ MapLds<LD> L;
   __shared__ unsigned long long st_acc[ST ? MAP_STAMP_N : 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: per-wave LDS bases in SGPRs
@@ -709,7 +714,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
     L.cnt[s] = 0;
     L.off[s] = 0xFFFFFFFFu;
   }
-  cursors_init(L.bcur, L.lcur, 1u << a.log2_rec_buckets, a.rec.subcap);
+  cursors_init(L.bcur, LD ? L.lcur : nullptr, 1u << a.log2_rec_buckets, a.rec.subcap);
   // the table image, built in this block's LDS (the unit buffers and token
   // lists are its scratch until the first unit)
   static_assert(sizeof(L.buf) >= 4 * (SEL_BINS + 20) && sizeof(L.list) >= 4 * NG, "image scratch");
@@ -1187,9 +1192,9 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   uint64_t t = my_tokens, e = 0;
   for (uint32_t b = tid; b < nb; b += MAP_THREADS) {
     const uint32_t sub = rout.sub, c16 = L.bcur[b] - b * sub, c24 = L.bcur[MAX_REC_BUCKETS + b] - b * sub;
-    const uint32_t cl = (L.lcur[b >> 1] >> (16u * (b & 1u))) & 0xFFFFu;
+    const uint32_t cl = LD ? (L.lcur[b >> 1] >> (16u * (b & 1u))) & 0xFFFFu : 0u;
     // overran into the next sub-region (24-byte records grow up, LONG ones down)
-    if (c16 > sub || c24 + cl > sub || L.lovf) atomicOr(&a.flags[FLAG_REGION_OVF], 1u);
+    if (c16 > sub || c24 + cl > sub || (LD && L.lovf)) atomicOr(&a.flags[FLAG_REGION_OVF], 1u);
     const uint32_t n16 = min(c16, sub), n24 = min(c24, sub), nl = min(cl, sub);
     a.rec.count[(size_t)blockIdx.x * nb + b] = n16 | (n24 << 16);  // packed for the reducer (sub <= 0xFFFF)
     a.rec.count_long[(size_t)blockIdx.x * nb + b] = nl;

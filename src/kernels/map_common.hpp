@@ -188,7 +188,8 @@ __device__ __forceinline__ void cursors_init(uint32_t* cur, uint32_t* lcur, uint
     cur[b] = b * sub;
     cur[MAX_REC_BUCKETS + b] = b * sub;
   }
-  for (uint32_t w = threadIdx.x; w < (nb + 1) / 2; w += blockDim.x) lcur[w] = 0;
+  if (lcur)
+    for (uint32_t w = threadIdx.x; w < (nb + 1) / 2; w += blockDim.x) lcur[w] = 0;
 }
 
 // Store one record at area index idx.  The block's store bases are
