@@ -98,6 +98,27 @@ def test_reset_ignores_stale_slices():
     assert_same(again, first)
 
 
+def test_long_layout_follows_the_pass_before():
+    """The LONG-record layout is picked per pass from the LONG token share of
+    the pass before (Engine::Impl::long_direct): a fresh engine queues LONG
+    records from the 24-byte runs, a LONG-heavy pass switches the next one to
+    the top-down layout streamed by long_direct, a LONG-free pass switches back.
+    Every job is exact whichever layout ran."""
+    heavy = colliding_text(21, n_words=80000, distinct=3000)  # ~60 % LONG tokens
+    light = ops.synth_host(2 << 20, seed=2, vocab=5000)  # no word reaches 16 bytes
+    want_h, want_l = ops.cpu_count(heavy), ops.cpu_count(light)
+    layouts = []
+    with ops.Engine(device=0) as e:
+        for text, want in ((heavy, want_h), (heavy, want_h), (light, want_l), (light, want_l), (heavy, want_h)):
+            e.reset()
+            e.count_bytes(text)
+            assert_same(e.result(), want)
+            st = e.stats()
+            layouts.append(st["long_direct"])
+            assert st["long_tokens"] > 0 if text is heavy else st["long_tokens"] == 0
+    assert layouts == [0, 1, 1, 0, 0]
+
+
 @pytest.mark.parametrize("order,kernel", [("", "wc_fo_sort"), ("radix", "wc_table_keys"), ("bitmap", "wc_bm_place")])
 def test_bounds_guard_names_the_writer(order, kernel, monkeypatch):
     """The finalize's row writers are bounds-guarded (kernels.hpp Bounds,
