@@ -266,7 +266,7 @@ Engine::Impl::~Impl() {
   if (d_red_blk && red_blk_grid) {  // the last reduce launch, block by block (100 MHz realtime ticks -> us)
     std::vector<unsigned long long> h(red_blk_grid * RED_BLK_WORDS);
     if (hipMemcpy(h.data(), d_red_blk, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-      struct B { double start, dur; uint32_t b, q; unsigned long long n16, n24, nl; double streams, arrive; };
+      struct B { double start, dur; uint32_t b, q; unsigned long long n16, n24, nl; double streams, arrive, merged, stored; };
       std::vector<B> v;
       unsigned long long t0 = ~0ull, t1 = 0;
       for (size_t i = 0; i < red_blk_grid; ++i) {
@@ -275,7 +275,8 @@ Engine::Impl::~Impl() {
         t0 = std::min(t0, r[1]);
         t1 = std::max(t1, r[2]);
         v.push_back(B{(double)r[1], (r[2] - r[1]) / 100.0, (uint32_t)r[0], (uint32_t)(r[0] >> 32), r[3] & 0xFFFFFFFFull,
-                      r[3] >> 32, r[4], (r[5] - r[1]) / 100.0, (r[6] - r[1]) / 100.0});
+                      r[3] >> 32, r[4], (r[5] - r[1]) / 100.0, (r[6] - r[1]) / 100.0, (r[7] - r[1]) / 100.0,
+                      (r[8] - r[1]) / 100.0});
       }
       if (!v.empty()) {
         double sum = 0;
@@ -287,9 +288,9 @@ Engine::Impl::~Impl() {
         for (size_t i = 0; i < v.size() && i < show; ++i)
           fprintf(stderr,
                   "[wc]   #%zu bucket %u q %u: %.1f us from %.1f us, records 16B %llu 24B %llu, LONG %llu; streams end "
-                  "%.1f, arrival %.1f us\n",
+                  "%.1f, arrival %.1f, merged %.1f, stored %.1f us\n",
                   i, v[i].b, v[i].q, v[i].dur, (v[i].start - t0) / 100.0, v[i].n16, v[i].n24, v[i].nl, v[i].streams,
-                  v[i].arrive);
+                  v[i].arrive, v[i].merged, v[i].stored);
         double m16 = 0, m24 = 0, ml = 0;
         for (auto& x : v) m16 += x.n16, m24 += x.n24, ml += (double)x.nl;
         fprintf(stderr, "[wc]   mean records 16B %.0f 24B %.0f LONG %.0f\n", m16 / v.size(), m24 / v.size(),
@@ -369,7 +370,7 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   // split since the records were bucketed), its weights from this map.
   // Below CUs buckets the uniform split stays: weight-sized pieces at 2 per CU
   // cost 11 % more block time in partial tables than their balance saved
-  // (v100k reduce 0.244 -> 0.307 ms; profiles/r5_reduce_balance.md)
+  // (v100k reduce 0.244 -> 0.307 ms; profiles/r5_session.md §4)
   const uint32_t nbk = 1u << table().log2_buckets;
   const uint32_t plan_grid = nbk + RED_PLAN_EXTRA;
   const bool planned = red_plan && !red_q_force && nbk >= n_cu && log2_rb == table().log2_buckets &&

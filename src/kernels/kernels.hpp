@@ -124,7 +124,7 @@ struct MapArgs {
 };
 // Reduce cost of a record relative to a Rec16 one in the dispatch plan: a
 // LONG word's byte comparison (a random 64-byte text read) costs ~10-20x a
-// Rec16 merge (profiles/r5_reduce_balance.md)
+// Rec16 merge (profiles/r5_session.md §4)
 constexpr uint32_t RED_W24 = 2;     // a 24-byte inline-key record (a counted hot slot, a 13..15-byte word)
 constexpr uint32_t RED_WLONG = 16;  // a LONG-word record
 // Hot-key sampling workspace (map.hip).  Two launches, no device-scope
@@ -249,7 +249,7 @@ constexpr uint32_t RED_STEAL_CH = 32;    // work-stealing reduce: runs per grab 
 constexpr uint32_t RED_STEAL_PL = 32;    // pieces per bucket at most
 constexpr uint32_t RED_STEAL_MIN = 16;   // runs left for a steal to start a piece
 // Reduce diagnostic counters (src/kernels/reduce.hip built with -DWC_RED_STAMPS=1).
-constexpr int RED_BLK_WORDS = 7;  // bucket | q, start, end, n16 | n24, LONG, streams end, arrival
+constexpr int RED_BLK_WORDS = 9;  // bucket | q, start, end, n16 | n24, LONG, streams end, arrival, merged, stored
 enum : int { RS_RECORDS = 0, RS_SLOW_LANES, RS_SLOW_WAVES, RS_PROBE_ITERS, RS_CAS_FAIL, RS_PENDING, RS_CLAIMS,
              RS_T_WAVE, RS_T_SLOW, RS_T_RUNS, RS_BLOCKS, RS_T_BLKMAX, RS_T_STREAMS, RS_NLONG, RS_LONG_STREAMED,
              RED_STAMP_N };

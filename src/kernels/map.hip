@@ -196,6 +196,32 @@ __device__ __forceinline__ void key_long_line(const uint8_t* line, uint32_t len,
   k1 = long_k1(len, h, mask);
 }
 
+// The same with the whole 64-byte line loaded in one round trip (four 16-byte
+// loads, then the compares): the top-down LONG layout's instance only — its
+// extra registers spilled the main loop of the LONG-free one (-2.5 % at v100k,
+// profiles/r3_session2.md §5), which keeps the loop above.
+__device__ __forceinline__ bool long_line_equal_1rt(const uint8_t* buf, uint32_t p, const uint8_t* line, uint32_t len) {
+  const uint4* l4 = reinterpret_cast<const uint4*>(line);
+  const uint4 v0 = l4[0], v1 = l4[1], v2 = l4[2], v3 = l4[3];
+  const uint64_t w[8] = {v0.x | (uint64_t)v0.y << 32, v0.z | (uint64_t)v0.w << 32, v1.x | (uint64_t)v1.y << 32,
+                         v1.z | (uint64_t)v1.w << 32, v2.x | (uint64_t)v2.y << 32, v2.z | (uint64_t)v2.w << 32,
+                         v3.x | (uint64_t)v3.y << 32, v3.z | (uint64_t)v3.w << 32};
+  bool eq = true;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i) {
+    const uint32_t c = 8 * i;
+    if (c >= len) break;
+    uint64_t x = window8(buf, p + c);
+    if (len - c < 8) x &= (1ull << (8 * (len - c))) - 1ull;
+    eq &= x == w[i];
+  }
+  return eq;
+}
+
+#ifndef WC_LONG_1RT
+#define WC_LONG_1RT 1  // A/B
+#endif
+
 // Token bytes [p, p + len) of the LDS buffer == the slot's line?
 __device__ __forceinline__ bool long_line_equal(const uint8_t* buf, uint32_t p, const uint8_t* line, uint32_t len) {
   const uint64_t* w = reinterpret_cast<const uint64_t*>(line);
@@ -797,8 +823,11 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
           const bool m1 = x1.x == sg, m2 = x2.x == sg;
           if (m1 || m2) {
             const uint64_t sd = m1 ? x1.y : x2.y;
-            if ((uint32_t)sd == len && long_line_equal(buf, q, h.long_bytes + (sd >> 32) * 64, len))
-              slot = (int)(2 * (m1 ? g1 : g2));
+            const uint8_t* line = h.long_bytes + (sd >> 32) * 64;
+            bool eq;
+            if constexpr (LD && WC_LONG_1RT) eq = (uint32_t)sd == len && long_line_equal_1rt(buf, q, line, len);
+            else eq = (uint32_t)sd == len && long_line_equal(buf, q, line, len);
+            if (eq) slot = (int)(2 * (m1 ? g1 : g2));
           }
         }
         if (slot >= 0) {

@@ -1017,14 +1017,13 @@ __device__ __forceinline__ uint64_t block_scan_excl64(uint64_t v, uint64_t& tota
   return before + incl - v;
 }
 
-// The reduce's dispatch plan (ReduceArgs::bucket_w; profiles/r5_reduce_balance.md):
+// The reduce's dispatch plan (ReduceArgs::bucket_w; profiles/r5_session.md §4):
 // every block derives the same plan from the map's per-bucket weights.
-// * fewer buckets than the grid (the split reduce's regime): bucket b gets
-//   floor(w_b (G - B) / W) + 1 pieces (quarters, <= RED_SPLIT_MAX_Q) — pieces
-//   of about W / G each instead of CUs / B per bucket whatever its weight (the
-//   uniform split's slowest quarter ran 1.19x the mean at v100k);
-// * otherwise one piece per bucket, a bucket above 1.5x the mean weight split
-//   into ceil(w / (1.1 mean)) pieces while the extra ones fit the grid.
+// bucket b gets floor(w_b (G - B) / W) + 1 pieces (<= RED_SPLIT_MAX_Q): the
+// G - B extra blocks go to the buckets by weight share, so only a bucket above
+// W / (G - B) is split.  (Splitting every bucket above 1.5x the mean at
+// long30_v1m — 512 buckets, 2 dispatch rounds on 256 CUs — pushed the pieces
+// past 2 x CUs into a third round: 446.9 vs 451.0 GB/s, profiles/r5_session.md §12.)
 // Pieces are dispatched heaviest first (8 classes of a quarter of the mean
 // piece each, then bucket order): with more pieces than CUs the heavy ones no
 // longer start in the last wave (at 30 % LONG vocabulary one bucket at 2.4x
@@ -1036,12 +1035,8 @@ __device__ __forceinline__ bool lpt_piece(const ReduceArgs& a, uint32_t& b, uint
   const uint32_t w = tid < nb ? a.bucket_w[tid] + 1u : 0u;
   uint32_t W;
   (void)block_scan_excl(w, W);
-  const uint64_t wn = (uint64_t)w * nb;  // w / mean = wn / W
   uint32_t n = tid < nb ? 1u : 0u;
-  if (tid < nb) {
-    if (nb < G) n = (uint32_t)min<uint64_t>(RED_SPLIT_MAX_Q, (uint64_t)w * (G - nb) / W + 1);
-    else if (2 * wn > 3ull * W) n = (uint32_t)min<uint64_t>(RED_SPLIT_MAX_Q, (10 * wn + 11ull * W - 1) / (11ull * W));
-  }
+  if (tid < nb) n = (uint32_t)min<uint64_t>(RED_SPLIT_MAX_Q, (uint64_t)w * (G - nb) / W + 1);
   uint32_t P;
   (void)block_scan_excl(n, P);
   if (P > G) {  // no room for the extra pieces: one per bucket, order only
@@ -1183,9 +1178,12 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
       __syncthreads();
     }
   }
+  const uint64_t rt_merged = WC_RED_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;
+  uint64_t rt_stored = rt_merged;
   if (store) {
     settle_new_long(L, a, b);
     store_slice(L, a.tab, b);
+    if (WC_RED_STAMPS) rt_stored = __builtin_amdgcn_s_memrealtime();
     add_fo_hist(L, a);
     add_bm_bits(L, a);
     if (tid == 0) {
@@ -1205,10 +1203,11 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
     if (tid < RED_STAMP_N) atomicAdd(&a.stamps[tid], L.st[tid]);
     if (a.blk && tid == 0) {  // where the reduce's time goes, block by block
       const uint32_t nrb0 = 1u << a.log2_rec_buckets;
-      unsigned long long n16 = 0, n24 = 0;
+      unsigned long long n16 = 0, n24 = 0, nl = L.st[RS_NLONG];
       for (uint32_t p = q; p < a.map_blocks; p += nq) {
         n16 += L.runcnt[p] & 0xFFFFu;
         n24 += L.runcnt[p] >> 16;
+        if (LD) nl += L.runlong[p];  // top-down LONG records (inside the 24-byte count)
       }
       (void)nrb0;
       unsigned long long* r = a.blk + (size_t)RED_BLK_WORDS * blockIdx.x;
@@ -1216,9 +1215,11 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
       r[1] = rt_start;
       r[2] = __builtin_amdgcn_s_memrealtime();
       r[3] = n16 | (n24 << 32);
-      r[4] = L.st[RS_NLONG];
+      r[4] = nl;
       r[5] = rt_streams;
       r[6] = rt_arrive;
+      r[7] = rt_merged;
+      r[8] = rt_stored;
     }
   }
 }

@@ -16,13 +16,7 @@ def plan(weights, grid):
     W = sum(w)
     n = []
     for x in w:
-        wn = x * nb
-        k = 1
-        if nb < grid:
-            k = min(RED_SPLIT_MAX_Q, x * (grid - nb) // W + 1)
-        elif 2 * wn > 3 * W:
-            k = min(RED_SPLIT_MAX_Q, (10 * wn + 11 * W - 1) // (11 * W))
-        n.append(k)
+        n.append(min(RED_SPLIT_MAX_Q, x * (grid - nb) // W + 1))
     P = sum(n)
     if P > grid:
         n = [1] * nb
