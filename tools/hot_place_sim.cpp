@@ -8,7 +8,10 @@
 // MODE 0 greedy by count (the kernel's order), 1 two-word words first,
 // 3 cuckoo (BFS displacement), 4 every selected word placed (the capacity
 // bound), 5 / 6 tiered greedy + one- / two-level displacement repairs,
-// 7 the kernel: BUDGET words by sampled count (not slots), tiered greedy.
+// 7 the kernel: BUDGET words by sampled count (not slots), tiered greedy,
+// 8 slot-valued selection, 9 = 7 with two-word words first in each tier.
+// SIM_ONE_SLOT8=1: 8-byte words as one-slot words; SIM_FIRST_SLOT8=1: only in
+// an empty group's first slot.
 // profiles/r5_session.md §12.
 #include "io/synth_host.hpp"
 #include "kernels/keys.hpp"
@@ -17,6 +20,7 @@
 #include <vector>
 #include <random>
 #include <algorithm>
+#include <cstdlib>
 using namespace wc;
 int main(int argc, char** argv) {
   SynthSpec sp; sp.vocab = argc > 3 ? atoi(argv[3]) : 100000;
@@ -36,13 +40,20 @@ int main(int argc, char** argv) {
     std::poisson_distribution<int> pd(SAMPLE * p[i] / z);
     c[i] = pd(rng);
   }
-  auto slots = [&](uint32_t i) { return v.len[i] >= 8 ? 2u : 1u; };
+  const uint32_t two_from = getenv("SIM_ONE_SLOT8") ? 9u : 8u;  // 8-byte words as one-slot words (raw k0 signature)
+  auto slots = [&](uint32_t i) { return v.len[i] >= two_from ? 2u : 1u; };
   std::vector<uint32_t> cand; for (uint32_t i = 0; i < n; ++i) if (c[i]) cand.push_back(i);
   std::shuffle(cand.begin(), cand.end(), rng);
   // selection by value per slot (c / slots), budget in slots
   std::stable_sort(cand.begin(), cand.end(), [&](uint32_t a, uint32_t b) { return (double)c[a] / slots(a) > (double)c[b] / slots(b); });
   std::vector<uint32_t> take; uint32_t used = 0;
-  if (mode == 7) {  // the kernel's selection (count_threshold): BUDGET words by sampled count, ties at t - 1 while room
+  if (mode == 8) {  // slot-valued selection: histogram key c / slots, each word weighing its slots, BUDGET slots
+    std::vector<uint32_t> hist(4096, 0);
+    for (auto i : cand) hist[std::min(c[i] / slots(i), 4095u)] += slots(i);
+    uint32_t t = 4095, suf = 0;
+    for (int b = 4095; b >= 1; --b) { if (suf + hist[b] > BUDGET) { t = b + 1; break; } suf += hist[b]; t = b; }
+    for (auto i : cand) if (c[i] / slots(i) >= t) take.push_back(i);
+  } else if (mode == 7 || mode == 9) {  // the kernel's selection (count_threshold): BUDGET words by sampled count, ties at t - 1 while room
     std::vector<uint32_t> hist(4096, 0);
     for (auto i : cand) hist[std::min(c[i], 4095u)]++;
     uint32_t t = 4095, suf = 0;
@@ -93,7 +104,7 @@ int main(int argc, char** argv) {
   };
   std::vector<uint32_t> towner(NG, ~0u);
   if (mode == 4) { for (auto i : take) placed[i] = 1; ord.clear(); }
-  if (mode == 5 || mode == 6 || mode == 7) {
+  if (mode >= 5) {
     // thresholds as the GPU: t from counts; tiers big=8t, mid=2t
     uint32_t mn = ~0u; for (auto i : take) mn = std::min(mn, c[i]);
     const uint32_t t = mn + 1, big = 8 * t, mid = 2 * t;
@@ -106,6 +117,10 @@ int main(int argc, char** argv) {
       uint32_t g1, g2; groups(i, g1, g2);
       if (slots(i) == 2) {
         for (uint32_t g : {g1, g2}) if (!two[g] && nocc(g) == 0) { two[g] = 1; towner[g] = i; return true; }
+        return false;
+      }
+      if (getenv("SIM_FIRST_SLOT8") && v.len[i] == 8) {  // one-slot 8-byte word, first slot of an empty group only
+        for (uint32_t g : {g1, g2}) if (!two[g] && nocc(g) == 0) { occ1[2*g] = i; return true; }
         return false;
       }
       if (nocc(g2) < nocc(g1)) std::swap(g1, g2);
@@ -142,9 +157,10 @@ int main(int argc, char** argv) {
       std::vector<uint32_t> tier;
       for (auto i : take) { int tr = c[i] >= big ? 0 : (c[i] >= mid ? 1 : 2); if (tr == pass) tier.push_back(i); }
       std::shuffle(tier.begin(), tier.end(), rng);
+      if (mode == 9) std::stable_sort(tier.begin(), tier.end(), [&](uint32_t a, uint32_t b) { return slots(a) > slots(b); });
       std::vector<uint32_t> f;
       for (auto i : tier) if (!place(i)) f.push_back(i);
-      if (mode != 7) for (auto i : f) repair(i);
+      if (mode == 5 || mode == 6) for (auto i : f) repair(i);
     }
     for (uint32_t s = 0; s < 2 * NG; ++s) if (occ1[s] != ~0u) placed[occ1[s]] = 1;
     for (uint32_t g = 0; g < NG; ++g) if (towner[g] != ~0u) placed[towner[g]] = 1;
