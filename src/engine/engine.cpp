@@ -428,7 +428,10 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
                 part_blocks, stealing ? steal : ReduceArgs::Steal{}};
   ra.long_direct = pass_ld;
   if (planned && ra.blk) red_blk_grid = nbk + plan_extra;
-  if (stealing) launch_reduce_steal(ra, s);
+  if (stealing) {
+    launch_reduce_steal(ra, s);
+    st.steal_passes++;
+  }
   else launch_reduce(ra, s, plan_extra);
   check_table("the reduce");
   if (sync_debug) {
