@@ -189,6 +189,14 @@ def run_rank(a) -> int:
     if local >= ndev:
         print(f"bench: rank {rank}: LOCAL_RANK {local} but {ndev} GPU(s) visible", file=sys.stderr, flush=True)
         return 2
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if world > 1 and local_world > ndev:
+        # RCCL refuses two ranks on one GPU ("Duplicate GPU detected", ncclInvalidUsage:
+        # profiles/r6_rccl_one_gpu.md): fail before any rank waits in the rendezvous
+        print(f"bench: rank {rank}: {local_world} local ranks but {ndev} GPU(s) visible; RCCL allows one rank per "
+              f"GPU (\"Duplicate GPU detected\") — use --virtual-ranks for several ranks on one GPU",
+              file=sys.stderr, flush=True)
+        return 2
 
     cfg = CONFIGS[a.config]
     gib = 1 << 30

@@ -29,7 +29,6 @@ struct Stats {
   uint64_t records = 0;   // shuffle records after the LDS combiner
   uint64_t long_tokens = 0;   // LONG-word (>= 16-byte, hashed-key) tokens
   uint32_t long_direct = 0;   // the last pass wrote LONG records top-down (Engine::Impl::long_direct)
-  uint32_t steal_passes = 0;  // passes reduced by the work-stealing split reduce (WC_RED_STEAL=1)
   uint32_t chunks = 0;    // map/reduce chunk passes
   uint32_t map_reruns = 0;     // shuffle-region overflow -> chunk halved
   uint32_t table_splits = 0;   // running table grew B -> 2B

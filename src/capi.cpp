@@ -506,14 +506,14 @@ int wc_engine_stats_json(wc_engine* e, char* buf, int cap) {
   char tmp[2048];
   const int k = snprintf(tmp, sizeof tmp,
                          "{\"bytes\": %llu, \"tokens\": %llu, \"keys\": %llu, \"records\": %llu, "
-                         "\"long_tokens\": %llu, \"long_direct\": %u, \"steal_passes\": %u, \"chunks\": %u, "
+                         "\"long_tokens\": %llu, \"long_direct\": %u, \"chunks\": %u, "
                          "\"map_reruns\": %u, \"table_splits\": %u, \"log2_buckets\": %u, \"order_path\": %u, "
                          "\"merges_planned\": %u, \"merge_redos\": %u, "
                          "\"device_ms\": {\"map\": %.4f, \"reduce\": %.4f, \"finalize\": %.4f, \"merge\": %.4f, "
                          "\"idle\": %.4f, \"total\": %.4f}, "
                          "\"host_ms\": {\"count\": %.4f, \"finalize\": %.4f}}",
                          (unsigned long long)s.bytes, (unsigned long long)s.tokens, (unsigned long long)s.keys,
-                         (unsigned long long)s.records, (unsigned long long)s.long_tokens, s.long_direct, s.steal_passes, s.chunks,
+                         (unsigned long long)s.records, (unsigned long long)s.long_tokens, s.long_direct, s.chunks,
                          s.map_reruns, s.table_splits, s.log2_buckets, s.order_path,
                          s.merges_planned, s.merge_redos,
                          s.map_ms,

@@ -395,7 +395,16 @@ std::unique_ptr<Comm> make_rccl_comm(const std::string& unique_id, int rank, int
   std::memcpy(&id, unique_id.data(), sizeof id);
   WC_HIP_CHECK(hipSetDevice(device));
   ncclComm_t c;
-  WC_NCCL_CHECK(ncclCommInitRank(&c, size, id, rank));
+  const ncclResult_t r = ncclCommInitRank(&c, size, id, rank);
+  // Two ranks on one GPU: RCCL 2.27 refuses them at init with
+  // "NCCL WARN Duplicate GPU detected : rank 0 and rank 1 both on CUDA device
+  // 8e000" and ncclInvalidUsage (measured on MI355X, profiles/r6_rccl_one_gpu.md)
+  // — one rank per GPU; the loopback communicator shares a GPU instead
+  if (r == ncclInvalidUsage)
+    fail("RCCL refused rank " + std::to_string(rank) + " of " + std::to_string(size) + " on device " +
+         std::to_string(device) + " (ncclInvalidUsage): RCCL allows one rank per GPU (\"Duplicate GPU detected\" when "
+         "two ranks share one); give every rank its own GPU, or use --virtual-ranks (loopback) on one GPU");
+  if (r != ncclSuccess) fail(std::string("RCCL error ") + ncclGetErrorString(r) + " in ncclCommInitRank");
   return std::unique_ptr<Comm>(new RcclComm(c, rank, size, device));
 }
 

@@ -212,6 +212,8 @@ void plan_finish(OwnerPlan& P) {
       P.rank_rows[r] += P.all[(size_t)r * C + 2 * p];
       P.rank_bytes[r] += P.all[(size_t)r * C + 2 * p + 1];
     }
+    // rows counted vs the owner-count sum of the same rows: an owner-count /
+    // gather consistency check (not an independent check of the compaction)
     if (P.all[(size_t)r * C + 2 * W + 2] != P.rank_rows[r]) P.count_mismatch = true;
     P.total_rows += P.rank_rows[r];
     P.GBmax += P.rank_bytes[r];

@@ -87,7 +87,6 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   if (const char* e = std::getenv("WC_REC_SHIFT")) rec_shift = (uint32_t)std::atoi(e);  // sweeps only
   if (const char* e = std::getenv("WC_RED_Q")) red_q_force = (uint32_t)std::atoi(e);    // sweeps only
   if (const char* e = std::getenv("WC_RED_PLAN")) red_plan = std::atoi(e) != 0;  // A/B: 0 = the uniform split
-  if (const char* e = std::getenv("WC_RED_STEAL")) red_steal = std::atoi(e) != 0;  // A/B: 0 = the uniform split
   if (const char* e = std::getenv("WC_LONG_DIRECT")) long_direct_force = std::atoi(e) != 0 ? 1 : 0;  // A/B
   long_direct = long_direct_force == 1;
   if (const char* e = std::getenv("WC_FAULT_OCC_UNDER")) fault_occ_under = std::strtoull(e, nullptr, 10);  // tests
@@ -116,11 +115,6 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
     part.done = part_mem.take_n<uint32_t>(ndone);
     WC_HIP_CHECK(hipMemset(part.done, 0, ndone * sizeof(uint32_t)));
     dev_malloc(&d_bucket_w, MAX_REC_BUCKETS * sizeof(uint32_t));
-    // work-stealing split reduce state (zeroed per pass: next, word, slot counter)
-    dev_malloc(&steal.next, MAX_REC_BUCKETS * sizeof(uint32_t));
-    dev_malloc(&steal.word, MAX_REC_BUCKETS * sizeof(unsigned long long));
-    dev_malloc(&steal.plist, (size_t)MAX_REC_BUCKETS * RED_STEAL_PL * sizeof(uint32_t));
-    dev_malloc(&steal.slot_ctr, 64);
   }
   if (const char* e = std::getenv("WC_LOG2_BUCKETS")) {  // sweeps only: shuffle + table bucket count
     opt.log2_rec_buckets = (uint32_t)std::atoi(e);
@@ -199,8 +193,6 @@ Engine::Impl::~Impl() {
   if (d_arena_cursor) (void)hipFree(d_arena_cursor);
   if (d_fo_hist) (void)hipFree(d_fo_hist);
   if (d_bucket_w) (void)hipFree(d_bucket_w);
-  for (void* p : {(void*)steal.next, (void*)steal.word, (void*)steal.plist, (void*)steal.slot_ctr})
-    if (p) (void)hipFree(p);
   if (d_tab_err) (void)hipFree(d_tab_err);
   if (d_bounds) (void)hipFree(d_bounds);
   if (d_fo_hist_cols) (void)hipFree(d_fo_hist_cols);
@@ -376,18 +368,9 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   const bool planned = red_plan && !red_q_force && nbk >= n_cu && log2_rb == table().log2_buckets &&
                        nbk <= (uint32_t)MAX_REC_BUCKETS && plan_grid <= part_blocks;
   const uint32_t plan_extra = plan_grid - nbk;
-  // below CUs buckets: the work-stealing split (blocks of a finished bucket take runs of the fullest one)
-  const bool stealing = red_steal && !planned && !red_q_force && nbk < n_cu && red_q() > 1 &&
-                        log2_rb == table().log2_buckets && blocks <= (uint32_t)RED_MAX_RUNS &&
-                        nbk * red_q() <= part_blocks;
   ZeroList z{};
   z.add(d_ctr, sizeof(DevCounters));
   if (planned) z.add(d_bucket_w, nbk * sizeof(uint32_t));
-  if (stealing) {
-    z.add(steal.next, nbk * sizeof(uint32_t));
-    z.add(steal.word, nbk * sizeof(unsigned long long));
-    z.add(steal.slot_ctr, sizeof(uint32_t));
-  }
   if (want_hist) z.add(d_fo_hist, FO_LOGBINS * sizeof(uint32_t));  // rebuilt by this pass's reduce over the whole table
   {
     uint32_t kb = 1;
@@ -425,14 +408,10 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
                 d_ctr->flags, d_bucket_ovf, nullptr, d_red_stamps, red_blk(), want_hist ? d_fo_hist : nullptr, fo_hist_m,
                 bm, bm ? bitmap_order_linecnt(bm, bm_end, 1) : nullptr, bm ? bitmap_order_ctl(bm, bm_end, 1) : nullptr,
                 bm ? (bm_end >> 1) + 1 : 0, 1u, planned ? 1u : red_q(), planned ? d_bucket_w : nullptr, part,
-                part_blocks, stealing ? steal : ReduceArgs::Steal{}};
+                part_blocks};
   ra.long_direct = pass_ld;
   if (planned && ra.blk) red_blk_grid = nbk + plan_extra;
-  if (stealing) {
-    launch_reduce_steal(ra, s);
-    st.steal_passes++;
-  }
-  else launch_reduce(ra, s, plan_extra);
+  launch_reduce(ra, s, plan_extra);
   check_table("the reduce");
   if (sync_debug) {
     const hipError_t e = hipStreamSynchronize(s);
@@ -693,7 +672,7 @@ bool Engine::Impl::complete_pass(const uint8_t* text, uint64_t len, uint64_t ava
     ReduceArgs ra{pass_rec, blocks,       log2_rb,       table(), text,
                   avail,    base,         Arena{d_arena, d_arena_cursor, opt.arena_bytes},
                   d_ctr->flags, d_bucket_ovf, d_bucket_en, d_red_stamps, red_blk(), fo_hist_ok ? d_fo_hist : nullptr, fo_hist_m,
-                  nullptr, nullptr, nullptr, 0, 0u, red_q(), nullptr, part, part_blocks, ReduceArgs::Steal{}};
+                  nullptr, nullptr, nullptr, 0, 0u, red_q(), nullptr, part, part_blocks};
     ra.long_direct = pass_ld;  // the pass's records: its map's LONG layout
     launch_reduce(ra, s);
     check_table("a split re-run's reduce");
@@ -861,13 +840,19 @@ bool Engine::Impl::finalize_local_speculative() {
   launch_publish(pc, s);
   if (spin_wait) wait_published(seq, spec_seq);
   else WC_HIP_CHECK(hipStreamSynchronize(s));
-  // the pass's counters arrived with this sync: check it (stats, recovery)
-  if (!complete_pass(p.text, p.len, p.avail, p.base, p.prev, p.rb, p.blocks, true)) return false;
+  // the pass's counters arrived with this sync: check it (stats, recovery).  A
+  // discarded attempt re-arms the bounds word: whatever it recorded belongs to
+  // output that is thrown away, not to the redo that publishes it next
+  if (!complete_pass(p.text, p.len, p.avail, p.base, p.prev, p.rb, p.blocks, true)) {
+    WC_HIP_CHECK(hipMemsetAsync(d_bounds, 0, 8, s));
+    return false;
+  }
   if (*h_ovf) {  // a sample-sort bin overflowed (far more keys than the hint) / shared bitmap position: redo exactly
     WC_LOG(LOG_INFO, "dev %d: first-occurrence %s order overflowed (hint %llu keys); redoing", dev,
            bitmap ? "bitmap" : "sample", (unsigned long long)hint);
     last_keys = 0;
     order_redo = true;
+    WC_HIP_CHECK(hipMemsetAsync(d_bounds, 0, 8, s));
     return false;
   }
   uint64_t bw = 0;
@@ -1490,7 +1475,10 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
     if (!drained) std::memcpy(&w, im.h_fin.data() + 40, 8);
     return w;
   };
-  im.check_bounds(bounds_word(), merged ? "the merged finalize" : "the local finalize");
+  // the planned merge decides first whether this attempt is redone: a redone
+  // attempt's bounds word is discarded with its output (re-armed before the redo)
+  const uint64_t bw_first = bounds_word();
+  if (!im.planned_active) im.check_bounds(bw_first, merged ? "the merged finalize" : "the local finalize");
   if (im.planned_active) {
     // the planned merge's decisions (the same on every rank: all-gathered words)
     im.planned_active = false;
@@ -1502,10 +1490,12 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
     const PendingPass p = im.planned_pass;
     const bool clean = im.complete_pass(p.text, p.len, p.avail, p.base, p.prev, p.rb, p.blocks, true);
     im.st.keys = local_n;
+    if (clean && !(f & 5)) im.check_bounds(bw_first, "the merged finalize");
     if (!clean || (f & 5)) {
       // a pass needed recovery (1) or a fixed region overflowed (4): every rank
       // redoes the merge exactly (the table is intact) and relearns the caps
       WC_LOG(LOG_INFO, "dev %d: planned merge redone exactly (flags %u)", im.dev, f);
+      if (bw_first) WC_HIP_CHECK(hipMemsetAsync(im.d_bounds, 0, 8, im.s));
       im.merge_caps.valid = false;
       im.st.merge_redos++;
       im.fo_ovf = nullptr;

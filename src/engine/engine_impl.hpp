@@ -71,7 +71,6 @@ struct Engine::Impl {
   size_t red_blk_grid = 0;
   uint32_t fin_seq = 0;
   bool red_plan = true;
-  bool red_steal = false;           // the work-stealing split reduce (WC_RED_STEAL=1; measured slower)
   // LONG-word records top-down + streamed by the reduce (MapArgs::long_direct):
   // chosen per pass from the LONG share of the pass before (LONG tokens > 1/64
   // of its records; the first pass of an engine: off); both modes are exact for any
@@ -80,7 +79,6 @@ struct Engine::Impl {
   bool long_direct = false;
   int long_direct_force = -1;
   bool pass_ld = false;  // the mode of the pass in flight (its map, its reduce and any re-run of it)
-  ReduceArgs::Steal steal{};
   // WC_CHECK_TABLE=1 (debug): after every reduce and split the table's
   // invariants are checked on the device and a violation fails the job naming
   // the stage (engine.cpp check_table)

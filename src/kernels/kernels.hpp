@@ -18,13 +18,18 @@ namespace wc {
 // ---- geometry (gfx950: wave64, 256 CUs, 160 KiB LDS per CU) -------------------
 #ifndef WC_MAP_THREADS
 #define WC_MAP_THREADS 1024
+#endif
+#ifndef WC_MAP_BLOCKS_PER_CU
 #define WC_MAP_BLOCKS_PER_CU 1
+#endif
+#ifndef WC_MAP_SLOTS
 #define WC_MAP_SLOTS 4096
 #endif
 constexpr int MAP_THREADS = WC_MAP_THREADS;          // 16 waves, one block per CU
 constexpr int MAP_BLOCKS_PER_CU = WC_MAP_BLOCKS_PER_CU;
 constexpr int MAP_BPL = 32;                          // text bytes per lane
-constexpr int MAP_TILE = MAP_THREADS * MAP_BPL;      // 32 KiB: chunk-length granule of the engine
+constexpr int MAP_TILE = 1024 * MAP_BPL;             // 32 KiB: chunk-length granule of the engine (16 wave units)
+static_assert(MAP_THREADS % 256 == 0 && MAP_THREADS <= 1024, "map block: the same wave count on every SIMD");
 constexpr int MAP_SLOTS = WC_MAP_SLOTS;              // LDS combiner slots (groups of 4)
 constexpr int MAX_REC_BUCKETS_LOG2 = 9;              // shuffle partitions <= 512
 constexpr int MAX_REC_BUCKETS = 1 << MAX_REC_BUCKETS_LOG2;
@@ -228,26 +233,11 @@ struct ReduceArgs {
     uint32_t* done;                           // [b] quarters arrived (zeroed; the last resets it)
   } part;
   uint32_t part_slots;  // partial-table slots allocated (the dispatch plan needs one per block)
-  // Work-stealing split reduce (nullable `next`: off; fewer table buckets than
-  // CUs): blocks grab a bucket's runs RED_STEAL_CH at a time and, their bucket
-  // exhausted, start a piece of the bucket with the most runs left; a piece
-  // registers (slot) before it grabs, and the arrival that completes the
-  // bucket's runs with every registered piece arrived merges them (reduce.hip
-  // wc_reduce_steal).  Zeroed per pass: next, word, slot_ctr.
-  struct Steal {
-    uint32_t* next;            // [nb] runs grabbed
-    unsigned long long* word;  // [nb] runs done << 32 | pieces arrived << 16 | pieces registered
-    uint32_t* plist;           // [nb][RED_STEAL_PL] partial slots of the registered pieces
-    uint32_t* slot_ctr;        // partial slots handed out
-  } steal;
   bool long_direct = false;  // the pass's map wrote LONG records top-down (MapArgs::long_direct)
 };
 // Most reduce blocks per bucket (split reduce: fewer table buckets than CUs).
 constexpr uint32_t RED_SPLIT_MAX_Q = 16;
 constexpr uint32_t RED_PLAN_EXTRA = 64;  // dispatch plan: blocks for split heavy buckets past one per bucket
-constexpr uint32_t RED_STEAL_CH = 32;    // work-stealing reduce: runs per grab (2 per wave)
-constexpr uint32_t RED_STEAL_PL = 32;    // pieces per bucket at most
-constexpr uint32_t RED_STEAL_MIN = 16;   // runs left for a steal to start a piece
 // Reduce diagnostic counters (src/kernels/reduce.hip built with -DWC_RED_STAMPS=1).
 constexpr int RED_BLK_WORDS = 9;  // bucket | q, start, end, n16 | n24, LONG, streams end, arrival, merged, stored
 enum : int { RS_RECORDS = 0, RS_SLOW_LANES, RS_SLOW_WAVES, RS_PROBE_ITERS, RS_CAS_FAIL, RS_PENDING, RS_CLAIMS,
@@ -294,7 +284,6 @@ struct Bounds {
 const char* bounds_kernel_name(uint32_t k);
 
 void launch_reduce(const ReduceArgs& a, hipStream_t s, uint32_t extra = 0);
-void launch_reduce_steal(const ReduceArgs& a, hipStream_t s);  // ReduceArgs::steal set
 void launch_table_split(const TableView& src, const TableView& dst, hipStream_t s);
 void launch_table_clear(const TableView& t, hipStream_t s);
 // debug: err (4 words, zeroed) <- the first bucket breaking the table's invariants (reduce.hip wc_check_table)

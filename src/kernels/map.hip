@@ -65,7 +65,6 @@ constexpr int MAP_DEF_CAP_Q = 256;     // the same, queue layout (no LONG cursor
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr int GS = HOT_GROUP_SLOTS;    // slots per group
 constexpr int NG = HOT_GROUPS;         // groups
-constexpr int SPT = MAP_SLOTS / MAP_THREADS;
 #ifndef WC_HOT_K
 #define WC_HOT_K (HOT_GROUP_SLOTS == 2 ? MAP_SLOTS * 7 / 8 : MAP_SLOTS * 3 / 4)
 #endif
@@ -75,7 +74,13 @@ constexpr int SPT = MAP_SLOTS / MAP_THREADS;
 constexpr uint32_t HOT_K = WC_HOT_K;            // words placed in the hot table
 constexpr uint32_t HOT_SAMPLE = WC_HOT_SAMPLE;  // units sampled per map block
 constexpr int SAMPLE_PROBES = 8;
-static_assert(MAP_SLOTS % MAP_THREADS == 0 && (NG & (NG - 1)) == 0, "table geometry");
+// A power-of-two group count takes its groups from hash bit fields; any
+// other (e.g. 3072 groups: the 6144-slot table of 512-thread blocks) scales a
+// 12-bit field by NG (g1) and steps g2 a nonzero distance below NG from it.
+constexpr bool NG_POW2 = (NG & (NG - 1)) == 0;
+static_assert(NG_POW2 || (NG > 2048 && NG <= 4096), "table geometry: 2^k groups, or 2049..4096");
+// The sampling table keeps 4096 slots whatever the map table holds.
+constexpr int SAMPLE_SLOTS = 4096, SNG = SAMPLE_SLOTS / GS;
 static_assert(UNIT <= 2048, "list entries hold 11-bit unit-relative positions");
 
 // Profiling builds only (tools/variants.sh -DWC_MAP_ABLATE=N; results are NOT
@@ -140,15 +145,27 @@ __device__ __forceinline__ uint32_t slot_of(uint32_t g, uint32_t i) {
 // The two candidate groups of a key (2-choice placement; g2 != g1: the xor
 // term is odd).
 __device__ __forceinline__ void hot_groups(uint32_t ph, uint32_t& g1, uint32_t& g2) {
-  g1 = (ph >> 20) & (NG - 1);
-  g2 = g1 ^ (((ph >> 8) & (NG - 1)) | 1u);
+  if constexpr (NG_POW2) {
+    g1 = (ph >> 20) & (NG - 1);
+    g2 = g1 ^ (((ph >> 8) & (NG - 1)) | 1u);
+  } else {
+    g1 = __umul24(ph >> 20, (uint32_t)NG) >> 12;
+    g2 = g1 + ((ph >> 8) & 2047u) + 1u;  // 1..2048 groups on, < NG
+    g2 = min(g2, g2 - (uint32_t)NG);     // mod NG (unsigned: wraps high below NG)
+  }
 }
 // The same as byte offsets of the groups in the signature image (16 * g):
 // right shifts, ands and one bitop3 — all full-rate VALU on gfx950, where the
 // left shifts / max / shift-or forms are half rate (profiles/r4_session3.md §2).
 __device__ __forceinline__ void hot_group_offs(uint32_t ph, uint32_t& o1, uint32_t& o2) {
-  o1 = (ph >> 16) & ((NG - 1) << 4);
-  o2 = o1 ^ (((ph >> 4) & ((NG - 1) << 4)) | 16u);
+  if constexpr (NG_POW2) {
+    o1 = (ph >> 16) & ((NG - 1) << 4);
+    o2 = o1 ^ (((ph >> 4) & ((NG - 1) << 4)) | 16u);
+  } else {  // hot_groups' g1 / g2 times 16
+    o1 = (__umul24(ph >> 20, (uint32_t)NG) >> 8) & ~15u;
+    o2 = o1 + ((ph >> 4) & (2047u << 4)) + 16u;
+    o2 = min(o2, o2 - 16u * (uint32_t)NG);
+  }
 }
 
 // 64-bit fingerprint of a sampled word (never 0): keys the global sample table.
@@ -275,10 +292,10 @@ __device__ __forceinline__ void unit_range(uint64_t chunk_len, uint32_t grid, ui
 
 // ------------------------------------------------------------------ sampling
 struct SampleLds {
-  uint64_t fp[MAP_SLOTS];  // 0 empty, else the word's fingerprint
-  uint64_t sig[MAP_SLOTS];
-  uint64_t side[MAP_SLOTS];
-  uint32_t cnt[MAP_SLOTS];
+  uint64_t fp[SAMPLE_SLOTS];  // 0 empty, else the word's fingerprint
+  uint64_t sig[SAMPLE_SLOTS];
+  uint64_t side[SAMPLE_SLOTS];
+  uint32_t cnt[SAMPLE_SLOTS];
   uint32_t pn[HOT_PARTS];  // words of this block in each fingerprint partition
   alignas(16) uint8_t buf[MAP_WAVES][BUF];
 };
@@ -300,7 +317,7 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs 
   // them run after both launches
   apply_zero_list(z, blockIdx.x * (uint64_t)MAP_THREADS + tid, (uint64_t)gridDim.x * MAP_THREADS, blockIdx.x == 0,
                   MAP_THREADS);
-  for (int s = tid; s < MAP_SLOTS; s += MAP_THREADS) {
+  for (int s = tid; s < SAMPLE_SLOTS; s += MAP_THREADS) {
     L.fp[s] = 0;
     L.cnt[s] = 0;
   }
@@ -352,13 +369,13 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs 
         inline_key(w0, w1, len, k0, k1, sg);
         sd = two_word(sg) ? k0 : 0ull;
         f = sample_fp(sg, sd);
-        g = (place_hash(k0, k1) >> 20) & (NG - 1);
+        g = (place_hash(k0, k1) >> 20) & (SNG - 1);
       } else {  // LONG: side = this occurrence's chunk offset | length (the placement copies its bytes)
         key_long_len(buf, p, len, a.k1_mask, k0, k1);
         sg = long_signature(k0, k1);
         sd = (u0 + p) | ((uint64_t)len << 32);
         f = sample_fp(sg, k0);
-        g = (uint32_t)(f >> 20) & (NG - 1);
+        g = (uint32_t)(f >> 20) & (SNG - 1);
       }
       for (int st = 0; st < SAMPLE_PROBES * GS; ++st) {
         const uint32_t s = GS * g + (st & (GS - 1));
@@ -375,14 +392,14 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs 
           atomicAdd(&L.cnt[s], 1u);
           break;
         }
-        if ((st & (GS - 1)) == GS - 1) g = (g + 1) & (NG - 1);
+        if ((st & (GS - 1)) == GS - 1) g = (g + 1) & (SNG - 1);
       }
     }
     wave_sync();
   }
   __syncthreads();
   const size_t cell0 = (size_t)blockIdx.x * HOT_STAGE_CAP;  // + partition * maxb * HOT_STAGE_CAP
-  for (int s = tid; s < MAP_SLOTS; s += MAP_THREADS) {
+  for (int s = tid; s < SAMPLE_SLOTS; s += MAP_THREADS) {
     const uint32_t c = L.cnt[s];
     if (!c) continue;
     const uint64_t f = L.fp[s];
@@ -402,19 +419,22 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs 
 }
 
 // ------------------------------------------------------------------ selection
-// Block-wide (1024 threads) selection threshold over a count histogram of
+// Block-wide (NT threads) selection threshold over a count histogram of
 // HOT_SEL_BINS bins in LDS: t = the smallest count >= 1 whose words (counted
 // >= t) number <= limit (the last bin when even that holds more), cum = the
-// words counted >= t.  Thread i owns bins [4i, 4i + 4); a reverse block scan
-// gives the words counted >= each bin.  sc: 18 words of LDS scratch.
+// words counted >= t.  Thread i owns bins [B i, B i + B), B = ceil(bins / NT)
+// (bins past the histogram count 0); a reverse block scan gives the words
+// counted >= each bin.  sc: 18 words of LDS scratch.
 constexpr int SEL_BINS = HOT_SEL_BINS;
+template <int NT>
 __device__ void count_threshold(const uint32_t* hist, uint32_t limit, uint32_t* sc, uint32_t& t_out,
                                 uint32_t& cum_out) {
-  static_assert(SEL_BINS == 4 * 1024, "threshold: 4 bins per thread");
+  constexpr int B = (SEL_BINS + NT - 1) / NT, NW = NT / 64;
+  static_assert(NT % 64 == 0 && NW <= 16, "threshold: whole waves, <= 16");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  uint32_t b[4], own = 0;
+  uint32_t b[B], own = 0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) own += b[i] = hist[4 * tid + i];
+  for (int i = 0; i < B; ++i) own += b[i] = B * tid + i < SEL_BINS ? hist[B * tid + i] : 0u;
   uint32_t x = own;  // inclusive scan from the top: words in bins >= 4 tid within the wave
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t y = __shfl_down(x, o);
@@ -424,20 +444,20 @@ __device__ void count_threshold(const uint32_t* hist, uint32_t limit, uint32_t* 
   if (tid == 0) sc[16] = SEL_BINS;
   __syncthreads();
   uint32_t above = 0;  // words in the waves above this one
-  for (int w = wave + 1; w < 16; ++w) above += sc[w];
-  const uint32_t suf0 = x + above;  // words counted >= 4 tid
+  for (int w = wave + 1; w < NW; ++w) above += sc[w];
+  const uint32_t suf0 = x + above;  // words counted >= B tid
   uint32_t suf = suf0, t = SEL_BINS;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {  // words counted >= bin 4 tid + i
-    if (t == SEL_BINS && suf <= limit && 4 * tid + i >= 1) t = 4 * tid + i;
+  for (int i = 0; i < B; ++i) {  // words counted >= bin B tid + i
+    if (t == SEL_BINS && suf <= limit && B * tid + i >= 1 && B * tid + i < SEL_BINS) t = B * tid + i;
     suf -= b[i];
   }
   if (t < SEL_BINS) atomicMin(&sc[16], t);
   __syncthreads();
   const uint32_t tt = sc[16] == SEL_BINS ? SEL_BINS - 1 : sc[16];
-  if ((uint32_t)tid == tt / 4) {
+  if ((uint32_t)tid == tt / B) {
     uint32_t cum = suf0;
-    for (uint32_t i = 0; i < tt % 4; ++i) cum -= b[i];
+    for (uint32_t i = 0; i < tt % B; ++i) cum -= b[i];
     sc[17] = cum;
   }
   __syncthreads();
@@ -519,7 +539,7 @@ __global__ void __launch_bounds__(1024) wc_hot_merge(HotArgs h) {
     if (L.cnt[s]) atomicAdd(&L.hist[min(L.cnt[s], (uint32_t)SEL_BINS - 1)], 1u);
   __syncthreads();
   uint32_t t, cum;
-  count_threshold(L.hist, HOT_PART_TOP, L.sc, t, cum);
+  count_threshold<1024>(L.hist, HOT_PART_TOP, L.sc, t, cum);
   const uint32_t ties = t > 1 ? HOT_PART_TOP - min(cum, (uint32_t)HOT_PART_TOP) : 0u;
   for (int s = tid; s < MERGE_SLOTS; s += 1024) {
     const uint32_t c = L.cnt[s];
@@ -566,10 +586,8 @@ constexpr uint32_t HOT_FIRST_MUL = WC_HOT_FIRST_MUL, HOT_MID_MUL = WC_HOT_MID_MU
 constexpr int HOT_PLACE_PASSES = WC_HOT_PLACE_PASSES;
 static_assert(HOT_PLACE_PASSES == 2 || HOT_PLACE_PASSES == 3, "2 or 3 placement tiers");
 
-constexpr uint32_t CAND_PER_THREAD = HOT_PARTS * HOT_PART_TOP / 1024;
-static_assert(HOT_PARTS * HOT_PART_TOP == 1024 * CAND_PER_THREAD && HOT_PART_TOP % CAND_PER_THREAD == 0,
-              "select: whole candidate rows per thread group");
-static_assert(MAP_THREADS == 1024, "select: one map block of 1024 threads");
+// candidates per map thread: candidate tid + k MAP_THREADS, k < CAND_PER_THREAD
+constexpr uint32_t CAND_PER_THREAD = (HOT_PARTS * HOT_PART_TOP + MAP_THREADS - 1) / MAP_THREADS;
 
 // One word into an LDS table image.  A one-slot word (<= 7 bytes): 2-choice,
 // the emptier group, else the other.  A two-word or LONG word: a whole empty
@@ -621,25 +639,27 @@ __device__ void build_image(const HotArgs& h, uint64_t* isig, uint32_t* scratch,
   const int tid = threadIdx.x;
   uint32_t* hist = scratch;
   uint32_t* sc = scratch + SEL_BINS;  // 18 words + the tie counter
-  for (int i = tid; i < SEL_BINS; i += 1024) hist[i] = 0;
-  for (int g = tid; g < NG; g += 1024) gocc[g] = 0;
+  for (int i = tid; i < SEL_BINS; i += MAP_THREADS) hist[i] = 0;
+  for (int g = tid; g < NG; g += MAP_THREADS) gocc[g] = 0;
   if (tid == 0) sc[18] = 0;
-  constexpr uint32_t TPP = HOT_PART_TOP / CAND_PER_THREAD;  // threads per partition row
-  const uint32_t part = tid / TPP, e0 = (tid % TPP) * CAND_PER_THREAD;
-  const size_t at0 = (size_t)part * HOT_PART_TOP + e0;
-  const uint32_t n = h.cand_n[part];
-  uint32_t c[CAND_PER_THREAD];
+  constexpr uint32_t NCAND = HOT_PARTS * HOT_PART_TOP;
+  uint32_t c[CAND_PER_THREAD], n[CAND_PER_THREAD];
 #pragma unroll
-  for (uint32_t i = 0; i < CAND_PER_THREAD; ++i) c[i] = h.cand_cnt[at0 + i];
+  for (uint32_t i = 0; i < CAND_PER_THREAD; ++i) {
+    const uint32_t at = tid + i * MAP_THREADS;
+    n[i] = at < NCAND ? h.cand_n[at / HOT_PART_TOP] : 0u;
+    c[i] = at < NCAND ? h.cand_cnt[at] : 0u;
+  }
 #pragma unroll
-  for (uint32_t i = 0; i < CAND_PER_THREAD; ++i) c[i] = e0 + i < n ? c[i] : 0u;  // stale past the row's count
+  for (uint32_t i = 0; i < CAND_PER_THREAD; ++i)  // stale past the row's count
+    c[i] = (tid + i * MAP_THREADS) % HOT_PART_TOP < n[i] ? c[i] : 0u;
   __syncthreads();  // scratch cleared
 #pragma unroll
   for (uint32_t i = 0; i < CAND_PER_THREAD; ++i)
     if (c[i]) atomicAdd(&hist[min(c[i], (uint32_t)SEL_BINS - 1)], 1u);
   __syncthreads();
   uint32_t t, cum;
-  count_threshold(hist, HOT_K, sc, t, cum);
+  count_threshold<MAP_THREADS>(hist, HOT_K, sc, t, cum);
   const uint32_t ties = t > 1 ? HOT_K - min(cum, HOT_K) : 0u;
   uint64_t sg[CAND_PER_THREAD], sd[CAND_PER_THREAD];
 #pragma unroll
@@ -650,8 +670,8 @@ __device__ void build_image(const HotArgs& h, uint64_t* isig, uint32_t* scratch,
   }
 #pragma unroll
   for (uint32_t i = 0; i < CAND_PER_THREAD; ++i) {
-    sg[i] = c[i] ? h.cand_sig[at0 + i] : 0ull;
-    sd[i] = c[i] ? h.cand_side[at0 + i] : 0ull;
+    sg[i] = c[i] ? h.cand_sig[tid + i * MAP_THREADS] : 0ull;
+    sd[i] = c[i] ? h.cand_side[tid + i * MAP_THREADS] : 0ull;
   }
   const uint32_t big = min(HOT_FIRST_MUL * t, (uint32_t)SEL_BINS - 1);
   const uint32_t mid = HOT_PLACE_PASSES == 3 ? min(HOT_MID_MUL * t, big) : big;
@@ -727,15 +747,13 @@ __device__ __forceinline__ uint32_t* at_byte(uint32_t* base, int o) {
 }
 
 template <bool ST, bool LD>
-__global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
+__global__ void __launch_bounds__(MAP_THREADS, MAP_WAVES / 4) wc_map(MapArgs a, HotArgs h) {
   __shared__ MapLds<LD> L;
   __shared__ unsigned long long st_acc[ST ? MAP_STAMP_N : 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: per-wave LDS bases in SGPRs
   if (ST && tid < MAP_STAMP_N) st_acc[tid] = 0;
-#pragma unroll
-  for (int j = 0; j < SPT; ++j) {
-    const int s = tid + j * MAP_THREADS;
+  for (int s = tid; s < MAP_SLOTS; s += MAP_THREADS) {
     L.sig[s] = 0;
     L.cnt[s] = 0;
     L.off[s] = 0xFFFFFFFFu;
@@ -743,8 +761,13 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   cursors_init(L.bcur, LD ? L.lcur : nullptr, 1u << a.log2_rec_buckets, a.rec.subcap);
   // the table image, built in this block's LDS (the unit buffers and token
   // lists are its scratch until the first unit)
-  static_assert(sizeof(L.buf) >= 4 * (SEL_BINS + 20) && sizeof(L.list) >= 4 * NG, "image scratch");
-  build_image(h, L.sig, reinterpret_cast<uint32_t*>(&L.buf[0][0][0]), reinterpret_cast<uint32_t*>(&L.list[0][0]));
+  // (group occupancy in the token lists, or after the histogram in the unit
+  // buffers when the lists are too small: 512-thread blocks of a 6144-slot table)
+  constexpr bool GOCC_IN_LIST = sizeof(L.list) >= 4 * NG;
+  static_assert(sizeof(L.buf) >= 4 * (SEL_BINS + 20 + (GOCC_IN_LIST ? 0 : NG)), "image scratch");
+  uint32_t* const img_scratch = reinterpret_cast<uint32_t*>(&L.buf[0][0][0]);
+  build_image(h, L.sig, img_scratch,
+              GOCC_IN_LIST ? reinterpret_cast<uint32_t*>(&L.list[0][0]) : img_scratch + SEL_BINS + 20);
   uint64_t u_begin, u_end;
   unit_range(a.chunk_len, gridDim.x, blockIdx.x, u_begin, u_end);
   if (tid == 0) {
@@ -1187,9 +1210,7 @@ __global__ void __launch_bounds__(MAP_THREADS, 4) wc_map(MapArgs a, HotArgs h) {
   // block end: every counted hot slot becomes one record of its bucket (a
   // two-word or LONG word counts in its group's first slot; its side word is
   // the second)
-#pragma unroll
-  for (int j = 0; j < SPT; ++j) {
-    const int s = tid + j * MAP_THREADS;
+  for (int s = tid; s < MAP_SLOTS; s += MAP_THREADS) {
     const uint32_t c = L.cnt[s];
     if (!c) continue;
     uint64_t k0, k1;

@@ -108,7 +108,10 @@ __global__ void __launch_bounds__(256) wc_owner_count(const uint64_t* k0, const 
   if (dn) n = *dn;
   // the row count counted here, next to the owner counts: every rank checks
   // every rank's count against its owner-count sum from the gathered matrix
-  // (count_bias: fault injection, WC_MERGE_FAULT_COUNT)
+  // (count_bias: fault injection, WC_MERGE_FAULT_COUNT).  Both come from the
+  // same rows [0, n), so this guards the owner counting and the gathered
+  // matrix only — it cannot see a compaction that wrote fewer rows than the
+  // occupancy promised (WC_CHECK_TABLE and the finalize's bounds guard do)
   if (blockIdx.x == 0 && threadIdx.x == 0) counts[2 * W + 2] = n + count_bias;
   if (pass_flags && blockIdx.x == 0 && threadIdx.x == 0) {
     const uint32_t rerun = pass_flags[FLAG_REGION_OVF] | pass_flags[FLAG_TABLE_OVF];

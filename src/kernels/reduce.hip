@@ -1032,11 +1032,14 @@ __device__ __forceinline__ uint64_t block_scan_excl64(uint64_t v, uint64_t& tota
 __device__ __forceinline__ bool lpt_piece(const ReduceArgs& a, uint32_t& b, uint32_t& q, uint32_t& nq, uint32_t& base) {
   __shared__ uint32_t pl[4];
   const uint32_t tid = threadIdx.x, nb = 1u << a.tab.log2_buckets, i = blockIdx.x, G = gridDim.x;
-  const uint32_t w = tid < nb ? a.bucket_w[tid] + 1u : 0u;
-  uint32_t W;
-  (void)block_scan_excl(w, W);
+  // a bucket's weight stays below 2^32 (<= 1024 map blocks x 65535 records x
+  // RED_WLONG per run), the sum over 512 buckets does not: 64-bit total, and
+  // every bucket weighs >= 1, so W > 0
+  const uint64_t w = tid < nb ? (uint64_t)a.bucket_w[tid] + 1u : 0u;
+  uint64_t W;
+  (void)block_scan_excl64(w, W);
   uint32_t n = tid < nb ? 1u : 0u;
-  if (tid < nb) n = (uint32_t)min<uint64_t>(RED_SPLIT_MAX_Q, (uint64_t)w * (G - nb) / W + 1);
+  if (tid < nb) n = (uint32_t)min<uint64_t>(RED_SPLIT_MAX_Q, w * (G - nb) / W + 1);
   uint32_t P;
   (void)block_scan_excl(n, P);
   if (P > G) {  // no room for the extra pieces: one per bucket, order only
@@ -1044,7 +1047,7 @@ __device__ __forceinline__ bool lpt_piece(const ReduceArgs& a, uint32_t& b, uint
     P = nb;
   }
   // class of the piece weight in quarters of the mean piece (7: >= 1.75x), heaviest first
-  const uint32_t cls = tid < nb ? (uint32_t)min<uint64_t>(7, 4ull * w * P / ((uint64_t)W * n)) : 0u;
+  const uint32_t cls = tid < nb ? (uint32_t)min<uint64_t>(7, 4ull * w * P / (W * n)) : 0u;
   // pieces before b inside its class: two 64-bit scans of 16-bit per-class counters
   const uint64_t v = (uint64_t)n << (16 * (cls & 3));
   uint64_t tlo, thi;
@@ -1224,184 +1227,6 @@ __global__ void __launch_bounds__(RED_THREADS) wc_reduce_buckets(ReduceArgs a) {
   }
 }
 
-
-// ---------------------------------------------------------- work-stealing split reduce
-// (ReduceArgs::steal; fewer table buckets than CUs — the headline's 64).  The
-// uniform split gives each of a bucket's CUs / B blocks the runs p = q mod
-// (CUs / B); its slowest block ran 1.19x the mean (bucket sizes and run sizes
-// vary: profiles/r5_session.md §4).  Here a block grabs RED_STEAL_CH runs of
-// its bucket at a time from the bucket's run cursor; when its bucket has none
-// left it starts a piece of the bucket with the most runs left, so the blocks
-// end together.  Every piece starts EMPTY and ends as a partial table; the
-// piece whose arrival completes the bucket's runs with every registered piece
-// arrived (one packed 64-bit word per bucket, acq_rel) merges its own table
-// with the running slice and the other pieces' partials and stores the slice.
-// A piece registers (partial slot, CAS while the bucket's runs are not all
-// done) BEFORE it grabs, so no run is processed by an unregistered piece and
-// no piece registers after the bucket completed: exactly one merger.
-
-// Rows of the running slice b (the table's occupied slots) into this block's
-// LDS table — the steal reduce's pieces all start empty.
-__device__ __forceinline__ void merge_slice(RedLds& L, const ReduceArgs& a, const LongCtx& c, uint32_t b) {
-  if (a.tab.occupancy[b] == 0) return;  // contents undefined (see load_slice)
-  const size_t base = (size_t)b * TAB_SLOTS;
-  for (int s = threadIdx.x; s < TAB_SLOTS; s += RED_THREADS) {
-    const uint64_t k1 = a.tab.k1[base + s];
-    if (k1 == K1_EMPTY) continue;
-    const uint64_t k0 = a.tab.k0[base + s], cnt = a.tab.cnt[base + s], first = a.tab.first[base + s];
-    if (key_is_hashed(k1)) {
-      merge_long_row(L, c, k0, k1, cnt, first, a.tab.sref_off[base + s], a.tab.sref_len[base + s]);
-    } else {
-      bool claimed;
-      const int d = lds_find_or_claim(L.grp, TAB_GROUPS, place_hash(k0, k1), k0, k1, TAB_MAX_GROUP_PROBES, claimed, true);
-      if (d < 0) L.overflow = 1;
-      else add_to_slot(L, d, cnt, first);
-    }
-  }
-  __syncthreads();
-}
-
-__global__ void __launch_bounds__(RED_THREADS) wc_reduce_steal(ReduceArgs a) {
-  __shared__ RedLds L;
-  __shared__ uint32_t sh[4];
-  __shared__ unsigned long long best;
-  if (a.flags[FLAG_REGION_OVF]) return;  // shuffle output incomplete: host re-runs the chunk
-  const int tid = threadIdx.x, wave = tid >> 6, nwaves = RED_THREADS / 64;
-  const uint32_t nb = 1u << a.tab.log2_buckets, P = a.map_blocks, sub = a.rec.subcap;
-  const ReduceArgs::Steal& S = a.steal;
-  uint32_t b = blockIdx.x & (nb - 1);
-  for (bool own = true;; own = false) {
-    // 1. register a piece of bucket b: a partial slot (its own block index for a block's first piece — every
-    //    bucket gets its first pieces whatever the stealers took — then past the grid), then the bucket's
-    //    count (CAS while runs remain undone)
-    if (tid == 0) {
-      uint32_t ok = 0, slot = 0;
-      if (__hip_atomic_load(&S.next[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < P) {
-        slot = own ? blockIdx.x : gridDim.x + atomicAdd(S.slot_ctr, 1u);
-        if (slot < a.part_slots) {
-          unsigned long long w = __hip_atomic_load(&S.word[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          while ((w >> 32) < P && (w & 0xFFFFull) < RED_STEAL_PL) {
-            const unsigned long long seen = atomicCAS(&S.word[b], w, w + 1);
-            if (seen == w) {
-              S.plist[b * RED_STEAL_PL + (uint32_t)(w & 0xFFFFull)] = slot;
-              ok = 1;
-              break;
-            }
-            w = seen;
-          }
-        }
-      }
-      sh[0] = ok;
-      sh[1] = slot;
-    }
-    __syncthreads();
-    const bool ok = __builtin_amdgcn_readfirstlane(sh[0]) != 0;  // block-uniform: SGPRs, not VGPRs
-    const uint32_t slot = __builtin_amdgcn_readfirstlane(sh[1]);
-    if (ok) {
-      // 2. the piece: an empty table, runs grabbed RED_STEAL_CH at a time (two per wave)
-      load_slice(L, a.tab, b, true);
-      for (uint32_t p = tid; p < P; p += RED_THREADS) {
-        L.runcnt[p] = a.rec.count[(size_t)p * nb + b];
-        L.runlong[p] = (uint16_t)a.rec.count_long[(size_t)p * nb + b];
-      }
-      if (tid == 0) {
-        L.occupied = 0;
-        L.overflow = 0;
-        L.nlong = 0;
-      }
-      __syncthreads();
-      const size_t qbase = (size_t)slot * TAB_SLOTS, sbase = (size_t)b * TAB_SLOTS;
-      const LongCtx lc{a.text, a.avail_len, a.arena.bytes, a.part.qsoff + qbase, a.part.qslen + qbase};
-      uint32_t claims = 0, runs = 0;
-      for (;;) {
-        if (tid == 0) sh[2] = atomicAdd(&S.next[b], RED_STEAL_CH);
-        __syncthreads();
-        const uint32_t r0 = __builtin_amdgcn_readfirstlane(sh[2]);
-        __syncthreads();  // every wave has read sh[2] before the next grab
-        if (r0 >= P) break;
-        const uint32_t re = min(r0 + RED_STEAL_CH, P);
-        merge_stream<true, RED_UNROLL>(L, a, b, a.rec.recs16, r0 + wave, nwaves, nb, b, sub, 0u, claims, re);
-        merge_stream<false, RED_UNROLL_24>(L, a, b, a.rec.recs, r0 + wave, nwaves, nb, b, sub, 0u, claims, re);
-        long_direct(L, a, lc, b, r0 + wave, nwaves, nb, b, sub, 0u, claims, re);
-        runs += re - r0;
-      }
-      __syncthreads();
-      // LONG records inside 24-byte runs: none since the map fills LONG ones top-down; past the
-      // queue (no run list to re-scan here) the bucket re-runs after a split, exactly
-      if (L.nlong > LONGQ) {
-        if (tid == 0) L.overflow = 1;
-      } else if (L.nlong) {
-        long_queue(L, a, lc, L.nlong, claims);
-      }
-      for (int o = 32; o > 0; o >>= 1) claims += __shfl_down(claims, o);
-      if ((tid & 63) == 0 && claims) atomicAdd(&L.occupied, claims);
-      __syncthreads();
-      if (tid == 0 && L.occupied > (uint32_t)TAB_MAX_OCC) L.overflow = 1;
-      __syncthreads();
-      const bool ovf = __builtin_amdgcn_readfirstlane(L.overflow) != 0;
-      if (ovf && tid == 0) {
-        a.bucket_overflow[b] = 1;
-        atomicOr(&a.flags[FLAG_TABLE_OVF], 1u);
-      }
-      if (!ovf) write_partial(L, a, lc, slot);
-      // 3. arrive: runs done and one piece; the arrival completing both counts merges
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        const unsigned long long add = ((unsigned long long)runs << 32) | (1ull << 16);
-        const unsigned long long nw =
-            __hip_atomic_fetch_add(&S.word[b], add, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + add;
-        const uint32_t reg = (uint32_t)(nw & 0xFFFFull), arr = (uint32_t)((nw >> 16) & 0xFFFFull);
-        sh[3] = (nw >> 32) == P && arr == reg ? reg : 0u;
-      }
-      __syncthreads();
-      const uint32_t reg = __builtin_amdgcn_readfirstlane(sh[3]);
-      if (reg && !a.bucket_overflow[b]) {
-        // the merger: the running slice and the other pieces' partials into this table
-        merge_slice(L, a, lc, b);
-        if (tid == 0) {
-          uint32_t k = 0;
-          for (uint32_t i = 0; i < reg; ++i) {
-            const uint32_t sl = S.plist[b * RED_STEAL_PL + i];
-            if (sl != slot) L.longq[k++] = sl;
-          }
-          L.nlong = k;  // scratch: the partial count
-        }
-        __syncthreads();
-        if (merge_partials(L, a, lc, b, L.longq, L.nlong)) {
-          for (int s = tid; s < TAB_SLOTS; s += RED_THREADS) {  // LONG references: piece scratch -> the slice
-            if (slot_tag(L.grp, s) > TAG_PENDING && key_is_hashed(slot_k1(L.grp, s))) {
-              a.tab.sref_off[sbase + s] = lc.sref_off[s];
-              a.tab.sref_len[sbase + s] = lc.sref_len[s];
-            }
-          }
-          __syncthreads();
-          settle_new_long(L, a, b);
-          store_slice(L, a.tab, b);
-          add_fo_hist(L, a);
-          add_bm_bits(L, a);
-          if (tid == 0) {
-            a.tab.occupancy[b] = L.occupied;
-            atomicMax(&a.flags[FLAG_MAX_OCC], L.occupied);
-          }
-        }
-      }
-      __syncthreads();
-    }
-    // 4. next: the bucket with the most runs left (at least RED_STEAL_MIN)
-    if (tid == 0) best = 0;
-    __syncthreads();
-    if ((uint32_t)tid < nb) {
-      const uint32_t g = __hip_atomic_load(&S.next[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t left = g < P ? P - g : 0u;
-      if (left >= RED_STEAL_MIN) atomicMax(&best, ((unsigned long long)left << 32) | (uint32_t)(~tid));
-    }
-    __syncthreads();
-    const unsigned long long bb = best;
-    if (!bb) return;
-    b = __builtin_amdgcn_readfirstlane(~(uint32_t)bb);
-  }
-}
 
 // Rehash parent slice (new_b mod B) of `src` into slice new_b of `dst` (2B
 // buckets).  Source slots hold distinct words, so every one claims a fresh
@@ -1637,13 +1462,6 @@ void launch_reduce(const ReduceArgs& a, hipStream_t s, uint32_t extra) {
   else hipLaunchKernelGGL(dev::wc_reduce_buckets<false>, dim3(grid), dim3(RED_THREADS), 0, s, a);
 }
 
-void launch_reduce_steal(const ReduceArgs& a, hipStream_t s) {
-  const uint32_t nb = 1u << a.tab.log2_buckets;
-  WC_CHECK(a.steal.next && a.nq > 1 && !a.bucket_enable && !a.bucket_w && a.tab.log2_buckets == a.log2_rec_buckets &&
-               nb * a.nq <= a.part_slots && a.map_blocks <= (uint32_t)RED_MAX_RUNS,
-           "work-stealing reduce: fewer buckets than CUs, one record bucket per table bucket, a slot per block");
-  hipLaunchKernelGGL(dev::wc_reduce_steal, dim3(nb * a.nq), dim3(RED_THREADS), 0, s, a);
-}
 
 void launch_table_split(const TableView& src, const TableView& dst, hipStream_t s) {
   hipLaunchKernelGGL(dev::wc_table_split, dim3(1u << dst.log2_buckets), dim3(RED_THREADS), 0, s, src, dst);

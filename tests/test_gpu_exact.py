@@ -248,26 +248,3 @@ def test_synth_while_pass_pending():
         want = merge_results([ops.cpu_count_synth(24 << 20, 0, 5, 50_000, 1.0, 0, 16),
                               ops.cpu_count_synth(24 << 20, 0, 6, 70_000, 1.0, 24 << 20, 16)])
         assert_same(got, want)
-
-
-@pytest.mark.parametrize("case", ["zipf", "long", "multipass"])
-def test_stealing_reduce_exact(case, monkeypatch):
-    """The work-stealing split reduce (off by default, `WC_RED_STEAL=1`,
-    profiles/r5_session.md §6) stays exact: a Zipf text, LONG-heavy jobs in both
-    LONG layouts (the second job takes the top-down one), and a multi-pass
-    stream whose pieces merge with the running slice."""
-    monkeypatch.setenv("WC_RED_STEAL", "1")  # read at engine creation
-    opts = {"chunk_bytes": 4 << 20} if case == "multipass" else {}
-    if case == "long":
-        texts = [colliding_text(31, n_words=80000, distinct=3000)] * 2
-    else:
-        texts = [ops.synth_host(16 << 20 if case == "multipass" else 24 << 20, seed=5, vocab=100_000)]
-    with ops.Engine(device=0, **opts) as e:
-        for text in texts:
-            e.reset()
-            e.count_bytes(text)
-            assert_same(e.result(), ops.cpu_count(text))
-            st = e.stats()
-            assert st["steal_passes"] >= 1
-            if case == "multipass":
-                assert st["chunks"] >= 4 and st["steal_passes"] >= st["chunks"]

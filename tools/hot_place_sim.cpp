@@ -9,7 +9,8 @@
 // 3 cuckoo (BFS displacement), 4 every selected word placed (the capacity
 // bound), 5 / 6 tiered greedy + one- / two-level displacement repairs,
 // 7 the kernel: BUDGET words by sampled count (not slots), tiered greedy,
-// 8 slot-valued selection, 9 = 7 with two-word words first in each tier.
+// 8 slot-valued selection, 9 = 7 with two-word words first in each tier,
+// 10 the round-6 image builder (priority random-walk cuckoo, one block per job).
 // SIM_ONE_SLOT8=1: 8-byte words as one-slot words; SIM_FIRST_SLOT8=1: only in
 // an empty group's first slot.
 // profiles/r5_session.md §12.
@@ -104,7 +105,7 @@ int main(int argc, char** argv) {
   };
   std::vector<uint32_t> towner(NG, ~0u);
   if (mode == 4) { for (auto i : take) placed[i] = 1; ord.clear(); }
-  if (mode >= 5) {
+  if (mode >= 5 && mode != 10) {
     // thresholds as the GPU: t from counts; tiers big=8t, mid=2t
     uint32_t mn = ~0u; for (auto i : take) mn = std::min(mn, c[i]);
     const uint32_t t = mn + 1, big = 8 * t, mid = 2 * t;
@@ -165,6 +166,86 @@ int main(int argc, char** argv) {
     for (uint32_t s = 0; s < 2 * NG; ++s) if (occ1[s] != ~0u) placed[occ1[s]] = 1;
     for (uint32_t g = 0; g < NG; ++g) if (towner[g] != ~0u) placed[towner[g]] = 1;
     ord.clear();
+  }
+  if (mode == 10) {
+    // the round-6 image builder (map.hip build_image_once): BUDGET words by sampled
+    // count (ties while room); per count tier (8t, 2t, rest): two-word words into an
+    // empty group (2-choice) else evicting a lower-count two-word owner, then one-slot
+    // words by a random walk that takes a free slot or evicts a lower-count one-slot
+    // occupant (<= 64 moves), the last item of a walk dropped
+    std::vector<uint32_t> hist(4096, 0);
+    for (auto i : cand) hist[std::min(c[i], 4095u)]++;
+    uint32_t t = 4095, suf = 0;
+    for (int b = 4095; b >= 1; --b) { if (suf + hist[b] > BUDGET) { t = b + 1; break; } suf += hist[b]; t = b; }
+    uint32_t cum = 0; for (uint32_t b = t; b < 4096; ++b) cum += hist[b];
+    uint32_t ties = t > 1 ? BUDGET - std::min(cum, BUDGET) : 0;
+    take.clear();
+    for (auto i : cand) if (c[i] >= t) take.push_back(i);
+    for (auto i : cand) if (c[i] + 1 == t && ties) { take.push_back(i); --ties; }
+    const uint32_t tt = t, big = 8 * tt, mid = 2 * tt;
+    std::vector<uint32_t> two(NG, ~0u), occ(2 * NG, ~0u);
+    auto other = [&](uint32_t i, uint32_t g) { uint32_t g1, g2; groups(i, g1, g2); return g1 == g ? g2 : g1; };
+    // one walk: place `item`, evicting strictly lower-count occupants; returns when placed or dropped
+    auto walk = [&](uint32_t item) {
+      for (int it = 0; it < 64; ++it) {
+        uint32_t g1, g2; groups(item, g1, g2);
+        auto nf = [&](uint32_t g) { return two[g] != ~0u ? 0 : (occ[2*g] == ~0u) + (occ[2*g+1] == ~0u); };
+        if (slots(item) == 2) {
+          bool done = false;
+          for (uint32_t g : {g1, g2}) if (!done && nf(g) == 2) { two[g] = item; done = true; }
+          if (done) return;
+          // evict: a lower-count two-word owner, or a lone lower-count one-slot occupant
+          uint32_t bg = ~0u, bc = ~0u;
+          for (uint32_t g : {g1, g2}) {
+            uint32_t o = two[g] != ~0u ? two[g] : (nf(g) == 1 ? (occ[2*g] != ~0u ? occ[2*g] : occ[2*g+1]) : ~0u);
+            if (o != ~0u && c[o] < c[item] && c[o] < bc) { bc = c[o]; bg = g; }
+          }
+          if (bg == ~0u) return;
+          uint32_t o = two[bg] != ~0u ? two[bg] : (occ[2*bg] != ~0u ? occ[2*bg] : occ[2*bg+1]);
+          occ[2*bg] = occ[2*bg+1] = ~0u; two[bg] = item; item = o;
+          continue;
+        }
+        if (nf(g2) > nf(g1)) std::swap(g1, g2);
+        if (nf(g1) > 0) { occ[2*g1 + (occ[2*g1] == ~0u ? 0 : 1)] = item; return; }
+        if (!getenv("SIM_NO_MOVE")) {  // a one-slot occupant with room in its other group moves there (nothing lost)
+          bool moved = false;
+          for (uint32_t g : {g1, g2}) {
+            if (moved || two[g] != ~0u) continue;
+            for (int h = 0; h < 2 && !moved; ++h) {
+              uint32_t o = occ[2*g+h], alt = other(o, g);
+              if (nf(alt) == 0) continue;
+              occ[2*alt + (occ[2*alt] == ~0u ? 0 : 1)] = o; occ[2*g+h] = item; moved = true;
+            }
+          }
+          if (moved) return;
+        }
+        // evict the lowest-count lower occupant: a one-slot word, or a two-word owner (its group then has a free half)
+        uint32_t bs = ~0u, bc = ~0u; bool btwo = false;
+        for (uint32_t g : {g1, g2}) {
+          if (two[g] != ~0u) { if (c[two[g]] < c[item] && c[two[g]] < bc) { bc = c[two[g]]; bs = g; btwo = true; } continue; }
+          for (int h = 0; h < 2; ++h) { uint32_t o = occ[2*g+h]; if (c[o] < c[item] && c[o] < bc) { bc = c[o]; bs = 2*g+h; btwo = false; } }
+        }
+        if (bs == ~0u) return;
+        if (btwo) { uint32_t o = two[bs]; two[bs] = ~0u; occ[2*bs] = item; item = o; }
+        else { uint32_t o = occ[bs]; occ[bs] = item; item = o; }
+      }
+    };
+    for (int pass = 0; pass < 3; ++pass)
+      for (int phase = 0; phase < 2; ++phase) {
+        std::vector<uint32_t> tier;
+        for (auto i : take) {
+          int tr = c[i] >= big ? 0 : (c[i] >= mid ? 1 : 2);
+          if (tr == pass && (slots(i) == 2) == (phase == 0)) tier.push_back(i);
+        }
+        std::shuffle(tier.begin(), tier.end(), rng);
+        for (auto i0 : tier) walk(i0);
+      }
+    uint32_t n2 = 0, n1 = 0;
+    for (uint32_t s = 0; s < 2 * NG; ++s) if (occ[s] != ~0u) { placed[occ[s]] = 1; ++n1; }
+    for (uint32_t g = 0; g < NG; ++g) if (two[g] != ~0u) { placed[two[g]] = 1; ++n2; }
+    if (getenv("SIM_DEBUG")) printf("two-word groups %u, one-slot words %u\n", n2, n1);
+    ord.clear();
+    (void)other;
   }
   if (mode == 3) {
     std::vector<uint32_t> o = take;
