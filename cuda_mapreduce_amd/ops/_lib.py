@@ -106,7 +106,8 @@ def _load() -> ctypes.CDLL:
         "wc_comm_destroy": (None, [c_void_p]),
         "wc_comm_barrier": (c_int, [c_void_p]),
         "wc_comm_allgather_host": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
-        "wc_loopback_count": (c_void_p, [P8, c_uint64, c_int, POINTER(c_int), POINTER(Options), c_int, c_int]),
+        "wc_loopback_count": (c_void_p, [P8, c_uint64, c_int, POINTER(c_int), POINTER(Options), c_int, c_int, P8,
+                                         c_uint64]),
         "wc_virtual_bench": (c_void_p, [POINTER(Options), c_int, c_int, c_uint64, c_uint64, c_uint32, c_double, c_double,
                                         c_int, c_int, POINTER(c_double)]),
     }

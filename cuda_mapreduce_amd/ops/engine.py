@@ -362,15 +362,19 @@ def virtual_bench(ranks: int, nbytes: int, seed: int = 1, vocab: int = 100000, z
 
 
 def loopback_count(data: bytes, ranks: int, devices: Optional[Sequence[int]] = None, all_ranks: bool = False,
-                   resident: bool = False, **opts) -> Result:
+                   resident: bool = False, warm: Optional[bytes] = None, **opts) -> Result:
     """`ranks` virtual ranks (threads) on `devices` count shards and merge in-process.
 
     Returns rank 0's table; with ``all_ranks`` every rank receives the merged
     table and the native side checks that they all equal rank 0's.  With
     ``resident`` each shard is counted from HBM and the merge runs behind the
-    pending last pass (the bench's speculative merged finalize)."""
+    pending last pass (the bench's speculative merged finalize).  ``warm``: a
+    first job on that text (its result dropped), so the merge of ``data``
+    plans from the caps it learned."""
     ptr, keep = _u8ptr(data)
+    wptr, wkeep = _u8ptr(warm) if warm is not None else (None, b"")
     devs = (ctypes.c_int * ranks)(*(devices if devices is not None else [0] * ranks))
     o = default_options(**opts)
     return Result._from_native(
-        check_ptr(lib.wc_loopback_count(ptr, len(keep), ranks, devs, ctypes.byref(o), int(all_ranks), int(resident))))
+        check_ptr(lib.wc_loopback_count(ptr, len(keep), ranks, devs, ctypes.byref(o), int(all_ranks), int(resident),
+                                        wptr, len(wkeep))))

@@ -125,7 +125,9 @@ int wc_comm_allgather_host(wc_comm* c, const void* send, uint64_t bytes, void* r
  * resident: shards are copied to HBM first and counted in place (the last
  * pass stays pending: the speculative merged finalize). */
 wc_result* wc_loopback_count(const uint8_t* text, uint64_t n, int ranks, const int* devices, const wc_options* o,
-                             int all_ranks, int resident);
+                             int all_ranks, int resident, const uint8_t* warm, uint64_t warm_n);
+/* warm (nullable): every rank first runs a job on its shard of `warm` (the merge
+ * learns its caps there), then the job on `text` — a planned merge. */
 
 #ifdef __cplusplus
 }

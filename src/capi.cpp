@@ -827,7 +827,7 @@ wc_result* wc_virtual_bench(const wc_options* o, int ranks, int device, uint64_t
 }
 
 wc_result* wc_loopback_count(const uint8_t* text, uint64_t n, int ranks, const int* devices, const wc_options* o,
-                             int all_ranks, int resident) {
+                             int all_ranks, int resident, const uint8_t* warm, uint64_t warm_n) {
   wc_result* out = new wc_result;
   std::vector<std::string> errs(ranks);
   std::vector<wc::KeyTable> tables(ranks);
@@ -847,21 +847,30 @@ wc_result* wc_loopback_count(const uint8_t* text, uint64_t n, int ranks, const i
         wc::Options opt = to_opts(o);
         opt.device = devices ? devices[r] : 0;
         wc::Engine eng(opt);
-        const wc::ShardRange sr = wc::shard_range_mem(text, n, r, ranks);
-        uint8_t* d = nullptr;
-        if (sr.end > sr.begin && resident) {
-          // HBM-resident shard: the last pass stays pending and the merge runs
-          // speculatively behind it (merge_cols_speculative)
-          const uint64_t len = sr.end - sr.begin;
-          WC_HIP_CHECK(hipSetDevice(opt.device));
-          wc::dev_malloc(&d, len + 64);
-          WC_HIP_CHECK(hipMemcpy(d, text + sr.begin, len, hipMemcpyHostToDevice));
-          eng.count_device(d, len, len, sr.begin, sr.begin ? text[sr.begin - 1] : ' ');
-        } else if (sr.end > sr.begin) {
-          eng.count_host(text + sr.begin, sr.end - sr.begin, sr.begin);
-        }
-        wc::KeyTable t = eng.result(comms[r].get(), all_ranks != 0);
-        if (d) (void)hipFree(d);
+        // one job on (tx, nn): this rank's shard, counted and merged
+        auto job = [&](const uint8_t* tx, uint64_t nn) {
+          eng.reset();
+          const wc::ShardRange sr = wc::shard_range_mem(tx, nn, r, ranks);
+          uint8_t* d = nullptr;
+          if (sr.end > sr.begin && resident) {
+            // HBM-resident shard: the last pass stays pending and the merge runs
+            // speculatively behind it (merge_cols_speculative / the planned merge)
+            const uint64_t len = sr.end - sr.begin;
+            WC_HIP_CHECK(hipSetDevice(opt.device));
+            wc::dev_malloc(&d, len + 64);
+            WC_HIP_CHECK(hipMemcpy(d, tx + sr.begin, len, hipMemcpyHostToDevice));
+            eng.count_device(d, len, len, sr.begin, sr.begin ? tx[sr.begin - 1] : ' ');
+          } else if (sr.end > sr.begin) {
+            eng.count_host(tx + sr.begin, sr.end - sr.begin, sr.begin);
+          }
+          wc::KeyTable kt = eng.result(comms[r].get(), all_ranks != 0);
+          if (d) (void)hipFree(d);
+          return kt;
+        };
+        // warm (nullable): a first job on other text — the merge learns its caps
+        // from it, so the job on `text` runs the planned merge
+        if (warm) (void)job(warm, warm_n);
+        wc::KeyTable t = job(text, n);
         if (r == 0) {
           out->t = std::move(t);
         } else if (all_ranks) {

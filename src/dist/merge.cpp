@@ -559,8 +559,13 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
 
   DeviceArena& A = im.merge_mem;
   const uint64_t RR = (uint64_t)W * Cr, RB = (uint64_t)W * Cb, GR = (uint64_t)W * Gr;
+  // the owner table: twice the learned merged-row cap (not the rows received:
+  // at W ranks an owner receives ~W x its distinct keys, so 2 RR slots made the
+  // zeroing and the compaction's scan W times larger than the keys need).  A
+  // job with more distinct keys fills it: the insert's probes are bounded and
+  // the compaction's count > Gr makes every rank redo the merge exactly.
   uint64_t T = 1024;
-  while (T < 2 * RR) T <<= 1;
+  while (T < 2 * std::min(RR, Gr)) T <<= 1;
   const bool have = R == 0 || all_ranks;
   A.reserve(2 * RR * sizeof(MRow) + 2 * RB + T * (4 + 16) + RR * sizeof(MRow) + (size_t)GR * sizeof(MRow) +
             (size_t)W * RB + (have ? GR * (5 * 8 + 4) : 0) + (4 * (size_t)W + 8) * 8 + 64 * 1024 +

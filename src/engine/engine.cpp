@@ -142,7 +142,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
 
   const size_t stage_n = (size_t)HOT_PARTS * map_blocks;
   hot_mem.reserve(stage_n * HOT_STAGE_CAP * sizeof(HotEnt) + stage_n * 4 +
-                  (size_t)HOT_PARTS * HOT_PART_TOP * (20 + 64) + HOT_PARTS * 4 + 8192);
+                  (size_t)HOT_PARTS * HOT_PART_TOP * (20 + 64) + HOT_PARTS * 4 + MAP_SLOTS * 8 + 8192);
   hot.stage = hot_mem.take_n<HotEnt>(stage_n * HOT_STAGE_CAP);
   hot.stage_n = hot_mem.take_n<uint32_t>(stage_n);
   hot.cand_sig = hot_mem.take_n<uint64_t>((size_t)HOT_PARTS * HOT_PART_TOP);
@@ -151,6 +151,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   hot.cand_n = hot_mem.take_n<uint32_t>(HOT_PARTS);
   hot.maxb = map_blocks;
   hot.long_bytes = hot_mem.take_n<uint8_t>((size_t)HOT_PARTS * HOT_PART_TOP * 64);
+  hot.image = hot_mem.take_n<uint64_t>(MAP_SLOTS);
   dev_malloc(&d_ctr, sizeof(DevCounters));
   WC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_ctr), sizeof(DevCounters), hipHostMallocDefault));
   h_pass_seq.resize(256);

@@ -159,9 +159,13 @@ struct HotArgs {
   // are reused)
   uint8_t* long_bytes;     // [HOT_PARTS * HOT_PART_TOP * 64]
   const uint8_t* text;     // the sampling pass's chunk text (the merge reads the sampled occurrence)
+  // The hot table image, built ONCE per sampled pass — each wc_hot_merge block
+  // places its partition's words into its partition's groups — and copied
+  // into every map block's LDS; persists while the candidates are reused.
+  uint64_t* image;         // [MAP_SLOTS] signatures (0 = empty slot)
 };
 constexpr uint32_t HOT_LONG_MAX = 64;
-constexpr int HOT_PARTS = 256;       // fingerprint partitions (one wc_hot_merge block each)
+constexpr int HOT_PARTS = 256;       // table partitions (one wc_hot_merge block each; a fingerprint's top byte)
 #ifndef WC_HOT_STAGE_CAP
 #define WC_HOT_STAGE_CAP 8
 #endif

@@ -8,16 +8,19 @@
 //
 //  wc_hot_sample  every map block tokenizes HOT_SAMPLE units spread over its
 //                 range, counts their words in an LDS table and writes them,
-//                 split into fingerprint partitions, to its own stage cells;
-//  wc_hot_merge   one block per partition sums the cells in LDS and keeps the
-//                 partition's most frequent words as candidates;
+//                 split by table partition (GPP = 8 groups each), to its own
+//                 stage cells;
+//  wc_hot_merge   one block per partition sums the cells in LDS, keeps the
+//                 partition's most frequent words as candidates and places
+//                 them into ITS groups of the pass's table image
+//                 (place_partition): a 2-choice table of 2-slot groups (4096
+//                 slots of 64-bit signatures, a two-word word's side word in
+//                 its group's second slot), both groups of a word in its
+//                 partition;
 //  wc_map         persistent, ONE 1024-thread block (16 waves) per CU over a
-//                 contiguous range of 2 KiB text units.  The block selects
-//                 the HOT_K most frequent candidates and places them in a
-//                 2-choice table of 2-slot groups in its LDS (4096 slots of
-//                 64-bit signatures, a two-word word's side word in its
-//                 group's second slot; blocks need not agree: each flushes
-//                 its slots with full keys).  Each wave grabs its
+//                 contiguous range of 2 KiB text units.  The block copies
+//                 the image into its LDS (every block flushes its slots with
+//                 full keys, so exactness never rests on it).  Each wave grabs its
 //                 next unit from an LDS cursor and prefetches it into registers (32 B per lane) while
 //                 tokenizing the current one from its private LDS copy:
 //                 SWAR delimiter masks -> token starts `~d & (d << 1 | c)` ->
@@ -65,20 +68,19 @@ constexpr int MAP_DEF_CAP_Q = 256;     // the same, queue layout (no LONG cursor
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr int GS = HOT_GROUP_SLOTS;    // slots per group
 constexpr int NG = HOT_GROUPS;         // groups
-#ifndef WC_HOT_K
-#define WC_HOT_K (HOT_GROUP_SLOTS == 2 ? MAP_SLOTS * 7 / 8 : MAP_SLOTS * 3 / 4)
-#endif
 #ifndef WC_HOT_SAMPLE
 #define WC_HOT_SAMPLE 4  // 8: +0.3-1 % at v100k but long30_v1m 388 -> 245 GB/s (profiles/r4_session3.md §13)
 #endif
-constexpr uint32_t HOT_K = WC_HOT_K;            // words placed in the hot table
 constexpr uint32_t HOT_SAMPLE = WC_HOT_SAMPLE;  // units sampled per map block
 constexpr int SAMPLE_PROBES = 8;
-// A power-of-two group count takes its groups from hash bit fields; any
-// other (e.g. 3072 groups: the 6144-slot table of 512-thread blocks) scales a
-// 12-bit field by NG (g1) and steps g2 a nonzero distance below NG from it.
-constexpr bool NG_POW2 = (NG & (NG - 1)) == 0;
-static_assert(NG_POW2 || (NG > 2048 && NG <= 4096), "table geometry: 2^k groups, or 2049..4096");
+// The table's groups come in HOT_PARTS partitions of GPP consecutive groups
+// (a partition = the top bits of g1); a word's two groups lie in ONE partition
+// (g2 = g1 ^ 1..GPP-1), and the partition's wc_hot_merge block, which holds
+// all of that partition's sampled words, places them itself (place_partition).
+static_assert((NG & (NG - 1)) == 0, "table geometry: 2^k groups");
+constexpr uint32_t GPP = NG / HOT_PARTS;  // groups per partition
+static_assert(GPP >= 2 && GPP <= 16 && (GPP & (GPP - 1)) == 0 && GPP * HOT_PARTS == NG,
+              "table geometry: 2..16 groups per hot-word partition");
 // The sampling table keeps 4096 slots whatever the map table holds.
 constexpr int SAMPLE_SLOTS = 4096, SNG = SAMPLE_SLOTS / GS;
 static_assert(UNIT <= 2048, "list entries hold 11-bit unit-relative positions");
@@ -143,29 +145,18 @@ __device__ __forceinline__ uint32_t slot_of(uint32_t g, uint32_t i) {
 }
 
 // The two candidate groups of a key (2-choice placement; g2 != g1: the xor
-// term is odd).
+// term is odd; both in g1's partition: the xor term is < GPP).
 __device__ __forceinline__ void hot_groups(uint32_t ph, uint32_t& g1, uint32_t& g2) {
-  if constexpr (NG_POW2) {
-    g1 = (ph >> 20) & (NG - 1);
-    g2 = g1 ^ (((ph >> 8) & (NG - 1)) | 1u);
-  } else {
-    g1 = __umul24(ph >> 20, (uint32_t)NG) >> 12;
-    g2 = g1 + ((ph >> 8) & 2047u) + 1u;  // 1..2048 groups on, < NG
-    g2 = min(g2, g2 - (uint32_t)NG);     // mod NG (unsigned: wraps high below NG)
-  }
+  g1 = (ph >> 20) & (NG - 1);
+  g2 = g1 ^ (((ph >> 8) & (GPP - 1)) | 1u);
 }
+__device__ __forceinline__ uint32_t hot_partition(uint32_t ph) { return ((ph >> 20) & (NG - 1)) / GPP; }
 // The same as byte offsets of the groups in the signature image (16 * g):
 // right shifts, ands and one bitop3 — all full-rate VALU on gfx950, where the
 // left shifts / max / shift-or forms are half rate (profiles/r4_session3.md §2).
 __device__ __forceinline__ void hot_group_offs(uint32_t ph, uint32_t& o1, uint32_t& o2) {
-  if constexpr (NG_POW2) {
-    o1 = (ph >> 16) & ((NG - 1) << 4);
-    o2 = o1 ^ (((ph >> 4) & ((NG - 1) << 4)) | 16u);
-  } else {  // hot_groups' g1 / g2 times 16
-    o1 = (__umul24(ph >> 20, (uint32_t)NG) >> 8) & ~15u;
-    o2 = o1 + ((ph >> 4) & (2047u << 4)) + 16u;
-    o2 = min(o2, o2 - 16u * (uint32_t)NG);
-  }
+  o1 = (ph >> 16) & ((NG - 1) << 4);
+  o2 = o1 ^ (((ph >> 4) & ((GPP - 1) << 4)) | 16u);
 }
 
 // 64-bit fingerprint of a sampled word (never 0): keys the global sample table.
@@ -368,13 +359,15 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs 
         window16(buf, p, w0, w1);
         inline_key(w0, w1, len, k0, k1, sg);
         sd = two_word(sg) ? k0 : 0ull;
-        f = sample_fp(sg, sd);
-        g = (place_hash(k0, k1) >> 20) & (SNG - 1);
+        const uint32_t ph = place_hash(k0, k1);
+        // the fingerprint's top byte is the word's table partition: its merge block places it
+        f = (sample_fp(sg, sd) & ~(0xFFull << 56)) | ((uint64_t)hot_partition(ph) << 56);
+        g = (ph >> 20) & (SNG - 1);
       } else {  // LONG: side = this occurrence's chunk offset | length (the placement copies its bytes)
         key_long_len(buf, p, len, a.k1_mask, k0, k1);
         sg = long_signature(k0, k1);
         sd = (u0 + p) | ((uint64_t)len << 32);
-        f = sample_fp(sg, k0);
+        f = (sample_fp(sg, k0) & ~(0xFFull << 56)) | ((uint64_t)hot_partition(long_group_hash(sg)) << 56);
         g = (uint32_t)(f >> 20) & (SNG - 1);
       }
       for (int st = 0; st < SAMPLE_PROBES * GS; ++st) {
@@ -403,7 +396,7 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs 
     const uint32_t c = L.cnt[s];
     if (!c) continue;
     const uint64_t f = L.fp[s];
-    const uint32_t part = (uint32_t)(f >> 56);
+    const uint32_t part = (uint32_t)(f >> 56);  // the word's table partition (HOT_PARTS = 256)
     const uint32_t at = atomicAdd(&L.pn[part], 1u);
     if (at >= (uint32_t)HOT_STAGE_CAP) continue;
     HotEnt e;
@@ -426,6 +419,18 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs 
 // (bins past the histogram count 0); a reverse block scan gives the words
 // counted >= each bin.  sc: 18 words of LDS scratch.
 constexpr int SEL_BINS = HOT_SEL_BINS;
+// hist[bin] += 1 for every lane with `valid`, one LDS atomic per distinct bin
+// of the wave: sampled counts crowd the low bins, and 64 lanes adding to one
+// LDS word serialise on its bank (called by whole waves, lanes converged).
+__device__ __forceinline__ void hist_add_wave(uint32_t* hist, uint32_t bin, bool valid) {
+  uint64_t todo = __ballot(valid);
+  while (todo) {
+    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)bin, (int)(__ffsll((unsigned long long)todo) - 1));
+    const uint64_t same = __ballot(valid && bin == b) & todo;
+    if (__lane_id() == (uint32_t)(__ffsll((unsigned long long)todo) - 1)) atomicAdd(&hist[b], (uint32_t)__popcll(same));
+    todo &= ~same;
+  }
+}
 template <int NT>
 __device__ void count_threshold(const uint32_t* hist, uint32_t limit, uint32_t* sc, uint32_t& t_out,
                                 uint32_t& cum_out) {
@@ -466,6 +471,102 @@ __device__ void count_threshold(const uint32_t* hist, uint32_t limit, uint32_t* 
   __syncthreads();  // sc is reusable
 }
 
+// ------------------------------------------------------------------ hot-table image
+// The partition's words into its GPP groups (2 GPP slots) of the table image,
+// by ONE wave of the partition's wc_hot_merge block: lane i holds candidate i;
+// in count order (ties by index) each word takes a free slot of the emptier of
+// its two groups (a two-slot word — two-word inline or LONG: signature + side
+// word — an empty group), else moves a one-slot occupant of one of its groups
+// to that occupant's other group when it has room and takes its slot, else
+// stays out.  Uniform control flow, the group states in one scalar word (2
+// bits per group: 0..2 occupants, 3 = a two-slot word), the slot owners one
+// per lane.  Every map block copies the finished image (no per-block build);
+// CPU model: tools/hot_place_sim.cpp mode 11 (SIM_REPAIR=1): 29.5 % of v100k
+// tokens missed vs 31.2 % for the per-block placement it replaces
+// (profiles/r6_session.md).
+static_assert(HOT_PART_TOP <= 64 && 2 * GPP <= 64, "partition placement: one wave");
+static_assert(HOT_PARTS == 256, "a sampled word's partition rides in its fingerprint's top byte");
+__device__ void place_partition(const HotArgs& h, uint32_t part, uint32_t n, const uint32_t* oc, const uint64_t* osig,
+                                const uint64_t* oside) {
+  const uint32_t lane = __lane_id();
+  const bool have = lane < n;
+  const uint32_t c = have ? oc[lane] : 0u;
+  const uint64_t sg = have ? osig[lane] : 0ull, sd = have ? oside[lane] : 0ull;
+  // local groups (0..GPP-1) and kind; a two-word word whose side word k0 has a
+  // top byte < 8 could equal a short signature in the image: it stays out
+  uint32_t g1 = 0, g2 = 0;
+  const bool lng = is_long_sig(sg);
+  bool ok = have && c != 0;
+  if (ok) {
+    if (lng) {
+      hot_groups(long_group_hash(sg), g1, g2);
+    } else {
+      uint64_t k0, k1;
+      sig_key(sg, sd, k0, k1);
+      hot_groups(place_hash(k0, k1), g1, g2);
+      if (two_word(sg) && (sd >> 59) == 0) ok = false;
+    }
+  }
+  const uint32_t a = g1 & (GPP - 1), b = g2 & (GPP - 1);
+  const bool two = lng || two_word(sg);
+  // rank in count order (ties: lower index first)
+  uint32_t rank = 0;
+  for (uint32_t j = 0; j < n; ++j) {
+    const uint32_t cj = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)j);
+    rank += (cj > c || (cj == c && j < lane)) ? 1u : 0u;
+  }
+  uint32_t st = 0;           // group states, 2 bits each (uniform)
+  uint32_t owner = 0xFFu;    // lane s < 2 GPP: the candidate in slot s (0xFF: empty)
+  auto gst = [&](uint32_t g) { return (st >> (2 * g)) & 3u; };
+  auto set_owner = [&](uint32_t slot, uint32_t who) { if (lane == slot) owner = who; };
+  for (uint32_t r = 0; r < n; ++r) {
+    const uint64_t m = __ballot(have && rank == r);
+    const uint32_t i = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+    if (!__builtin_amdgcn_readlane((int)ok, (int)i)) continue;
+    const uint32_t ai = (uint32_t)__builtin_amdgcn_readlane((int)a, (int)i);
+    const uint32_t bi = (uint32_t)__builtin_amdgcn_readlane((int)b, (int)i);
+    if (__builtin_amdgcn_readlane((int)two, (int)i)) {  // an empty group, g1 first
+      const uint32_t g = gst(ai) == 0 ? ai : (gst(bi) == 0 ? bi : 0xFFu);
+      if (g == 0xFFu) continue;
+      st |= 3u << (2 * g);
+      set_owner(2 * g, i);
+      set_owner(2 * g + 1, i);
+      continue;
+    }
+    const uint32_t sa = gst(ai), sb = gst(bi);
+    const uint32_t fa = sa == 3 ? 0u : 2u - sa, fb = sb == 3 ? 0u : 2u - sb;
+    if (fa | fb) {  // a free slot of the emptier group (slots fill first, then second)
+      const uint32_t g = fb > fa ? bi : ai, sg0 = gst(g);
+      set_owner(2 * g + sg0, i);
+      st += 1u << (2 * g);
+      continue;
+    }
+    // both full: move a one-slot occupant to its other group if that has room
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t g = k < 2 ? ai : bi, slot = 2 * g + (k & 1);
+      if (gst(g) == 3) continue;
+      const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)owner, (int)slot);
+      const uint32_t oa = (uint32_t)__builtin_amdgcn_readlane((int)a, (int)o);
+      const uint32_t ob = (uint32_t)__builtin_amdgcn_readlane((int)b, (int)o);
+      const uint32_t alt = oa == g ? ob : oa, salt = gst(alt);
+      if (salt >= 2) continue;
+      set_owner(2 * alt + salt, o);
+      st += 1u << (2 * alt);
+      set_owner(slot, i);
+      break;
+    }
+  }
+  // the partition's 2 GPP image slots: a two-slot word's signature and side
+  // word, one-slot words' signatures, 0 = empty
+  const uint32_t o = owner & 63u;  // (the whole wave shuffles: every source lane active)
+  const uint64_t osg = __shfl(sg, (int)o), osd = __shfl(sd, (int)o);
+  if (lane < 2 * GPP) {
+    const uint32_t g = lane >> 1;
+    const uint64_t v = owner == 0xFFu ? 0ull : ((gst(g) == 3 && (lane & 1)) ? osd : osg);
+    h.image[slot_of(part * GPP + g, lane & 1)] = v;
+  }
+}
+
 // One block per fingerprint partition: every map block's stage cell of the
 // partition is summed into an LDS table, then the HOT_PART_TOP most frequent
 // words (ties at the threshold while room remains) become the partition's
@@ -483,6 +584,9 @@ struct HotMergeLds {
   uint32_t hist[SEL_BINS];
   uint32_t sc[18];
   uint32_t nout, nties;
+  // the partition's candidates (place_partition): count, signature, side word
+  uint32_t oc[HOT_PART_TOP];
+  uint64_t osig[HOT_PART_TOP], oside[HOT_PART_TOP];
 };
 __device__ __forceinline__ void merge_insert(HotMergeLds& L, const HotEnt& e) {
   uint32_t s = (uint32_t)(e.fp >> 20) & (MERGE_SLOTS - 1);
@@ -535,8 +639,7 @@ __global__ void __launch_bounds__(1024) wc_hot_merge(HotArgs h) {
       if (e < n[k]) merge_insert(L, x[k]);
   }
   __syncthreads();
-  for (int s = tid; s < MERGE_SLOTS; s += 1024)
-    if (L.cnt[s]) atomicAdd(&L.hist[min(L.cnt[s], (uint32_t)SEL_BINS - 1)], 1u);
+  for (int s = tid; s < MERGE_SLOTS; s += 1024) hist_add_wave(L.hist, min(L.cnt[s], (uint32_t)SEL_BINS - 1), L.cnt[s] != 0);
   __syncthreads();
   uint32_t t, cum;
   count_threshold<1024>(L.hist, HOT_PART_TOP, L.sc, t, cum);
@@ -548,144 +651,28 @@ __global__ void __launch_bounds__(1024) wc_hot_merge(HotArgs h) {
     const uint32_t o = atomicAdd(&L.nout, 1u);
     if (o >= (uint32_t)HOT_PART_TOP) continue;
     const size_t at = (size_t)part * HOT_PART_TOP + o;
-    const uint64_t sg = L.sig[s], sd = L.side[s];
-    h.cand_cnt[at] = c;
-    h.cand_sig[at] = sg;
+    const uint64_t sg = L.sig[s];
+    uint64_t sd = L.side[s];
     if (is_long_sig(sg)) {  // the sampled occurrence's bytes (zero-padded) -> the candidate's line
       const uint32_t len = (uint32_t)(sd >> 32), from = (uint32_t)sd;
-      h.cand_side[at] = len | ((uint64_t)at << 32);
+      sd = len | ((uint64_t)at << 32);
       uint64_t* line = reinterpret_cast<uint64_t*>(h.long_bytes + at * 64);
       for (uint32_t c8 = 0; c8 < 64; c8 += 8) {
         uint64_t x = 0;
         for (uint32_t j = 0; j < 8 && c8 + j < len; ++j) x |= (uint64_t)h.text[(size_t)from + c8 + j] << (8 * j);
         line[c8 / 8] = x;
       }
-    } else {
-      h.cand_side[at] = sd;
     }
+    h.cand_cnt[at] = c;
+    h.cand_sig[at] = sg;
+    h.cand_side[at] = sd;
+    L.oc[o] = c;
+    L.osig[o] = sg;
+    L.oside[o] = sd;
   }
   __syncthreads();
   if (tid == 0) h.cand_n[part] = min(L.nout, (uint32_t)HOT_PART_TOP);
-}
-
-// Placement in count tiers, most frequent first: pass 0 places the words
-// counted >= HOT_FIRST_MUL * t (their tokens must never flood one shuffle
-// bucket: placed into a nearly empty image), pass 1 those >= HOT_MID_MUL * t,
-// pass 2 the rest — greedy 2-choice placement into 2-slot groups loses words
-// late in its order, so the order follows the counts (HOT_PLACE_PASSES).
-#ifndef WC_HOT_FIRST_MUL
-#define WC_HOT_FIRST_MUL 8
-#endif
-#ifndef WC_HOT_MID_MUL
-#define WC_HOT_MID_MUL 2
-#endif
-#ifndef WC_HOT_PLACE_PASSES
-#define WC_HOT_PLACE_PASSES 3
-#endif
-constexpr uint32_t HOT_FIRST_MUL = WC_HOT_FIRST_MUL, HOT_MID_MUL = WC_HOT_MID_MUL;
-constexpr int HOT_PLACE_PASSES = WC_HOT_PLACE_PASSES;
-static_assert(HOT_PLACE_PASSES == 2 || HOT_PLACE_PASSES == 3, "2 or 3 placement tiers");
-
-// candidates per map thread: candidate tid + k MAP_THREADS, k < CAND_PER_THREAD
-constexpr uint32_t CAND_PER_THREAD = (HOT_PARTS * HOT_PART_TOP + MAP_THREADS - 1) / MAP_THREADS;
-
-// One word into an LDS table image.  A one-slot word (<= 7 bytes): 2-choice,
-// the emptier group, else the other.  A two-word or LONG word: a whole empty
-// group (g1, else g2), signature in its first slot and side word in its second
-// (a two-word word whose side word k0 has a top byte < 8 could equal a short
-// signature: it stays out).  Both choices full: the word stays out.
-__device__ __forceinline__ void place_hot(uint64_t* isig, uint32_t* gocc, uint64_t sg, uint64_t sd) {
-  uint32_t g1, g2;
-  const bool lng = is_long_sig(sg);
-  if (lng) {
-    hot_groups(long_group_hash(sg), g1, g2);
-  } else {
-    uint64_t k0, k1;
-    sig_key(sg, sd, k0, k1);
-    hot_groups(place_hash(k0, k1), g1, g2);
-  }
-  if (lng || two_word(sg)) {
-    if (!lng && (sd >> 59) == 0) return;
-    uint32_t g = g1;
-    if (atomicCAS(&gocc[g1], 0u, 2u) != 0u) {
-      g = g2;
-      if (atomicCAS(&gocc[g2], 0u, 2u) != 0u) return;
-    }
-    isig[2 * g] = sg;
-    isig[2 * g + 1] = sd;
-    return;
-  }
-  if (gocc[g2] < gocc[g1]) {
-    const uint32_t x = g1;
-    g1 = g2;
-    g2 = x;
-  }
-  uint32_t g = g1, o = atomicAdd(&gocc[g1], 1u);
-  if (o >= GS) {
-    g = g2;
-    o = atomicAdd(&gocc[g2], 1u);
-  }
-  if (o >= GS) return;
-  isig[slot_of(g, o)] = sg;
-}
-
-// A map block's table image from the candidates (the block's prologue): the
-// HOT_K most frequent (threshold over every partition's candidates, ties while
-// room remains), placed tier by tier into the LDS image isig (cleared by the
-// caller).  Each thread holds CAND_PER_THREAD candidates in registers:
-// two dependent global steps (counts, then the taken candidates' keys).
-// scratch: >= SEL_BINS + 20 words, gocc: NG words (LDS the main loop reuses).
-__device__ void build_image(const HotArgs& h, uint64_t* isig, uint32_t* scratch, uint32_t* gocc) {
-  const int tid = threadIdx.x;
-  uint32_t* hist = scratch;
-  uint32_t* sc = scratch + SEL_BINS;  // 18 words + the tie counter
-  for (int i = tid; i < SEL_BINS; i += MAP_THREADS) hist[i] = 0;
-  for (int g = tid; g < NG; g += MAP_THREADS) gocc[g] = 0;
-  if (tid == 0) sc[18] = 0;
-  constexpr uint32_t NCAND = HOT_PARTS * HOT_PART_TOP;
-  uint32_t c[CAND_PER_THREAD], n[CAND_PER_THREAD];
-#pragma unroll
-  for (uint32_t i = 0; i < CAND_PER_THREAD; ++i) {
-    const uint32_t at = tid + i * MAP_THREADS;
-    n[i] = at < NCAND ? h.cand_n[at / HOT_PART_TOP] : 0u;
-    c[i] = at < NCAND ? h.cand_cnt[at] : 0u;
-  }
-#pragma unroll
-  for (uint32_t i = 0; i < CAND_PER_THREAD; ++i)  // stale past the row's count
-    c[i] = (tid + i * MAP_THREADS) % HOT_PART_TOP < n[i] ? c[i] : 0u;
-  __syncthreads();  // scratch cleared
-#pragma unroll
-  for (uint32_t i = 0; i < CAND_PER_THREAD; ++i)
-    if (c[i]) atomicAdd(&hist[min(c[i], (uint32_t)SEL_BINS - 1)], 1u);
-  __syncthreads();
-  uint32_t t, cum;
-  count_threshold<MAP_THREADS>(hist, HOT_K, sc, t, cum);
-  const uint32_t ties = t > 1 ? HOT_K - min(cum, HOT_K) : 0u;
-  uint64_t sg[CAND_PER_THREAD], sd[CAND_PER_THREAD];
-#pragma unroll
-  for (uint32_t i = 0; i < CAND_PER_THREAD; ++i) {
-    bool take = c[i] != 0 && c[i] + 1 >= t;
-    if (take && c[i] < t) take = atomicAdd(&sc[18], 1u) < ties;
-    if (!take) c[i] = 0;
-  }
-#pragma unroll
-  for (uint32_t i = 0; i < CAND_PER_THREAD; ++i) {
-    sg[i] = c[i] ? h.cand_sig[tid + i * MAP_THREADS] : 0ull;
-    sd[i] = c[i] ? h.cand_side[tid + i * MAP_THREADS] : 0ull;
-  }
-  const uint32_t big = min(HOT_FIRST_MUL * t, (uint32_t)SEL_BINS - 1);
-  const uint32_t mid = HOT_PLACE_PASSES == 3 ? min(HOT_MID_MUL * t, big) : big;
-  for (int pass = 0; pass < HOT_PLACE_PASSES; ++pass) {
-#pragma unroll
-    for (uint32_t i = 0; i < CAND_PER_THREAD; ++i) {
-      if (!c[i]) continue;
-      const uint32_t cc = min(c[i], (uint32_t)SEL_BINS - 1);
-      const int tier = cc >= big ? 0 : (cc >= mid ? 1 : 2);
-      if (tier != (pass == HOT_PLACE_PASSES - 1 ? 2 : pass)) continue;
-      place_hot(isig, gocc, sg[i], sd[i]);
-    }
-    __syncthreads();
-  }
+  if (tid < 64) place_partition(h, part, min(L.nout, (uint32_t)HOT_PART_TOP), L.oc, L.osig, L.oside);
 }
 
 // ------------------------------------------------------------------ map
@@ -753,21 +740,15 @@ __global__ void __launch_bounds__(MAP_THREADS, MAP_WAVES / 4) wc_map(MapArgs a, 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: per-wave LDS bases in SGPRs
   if (ST && tid < MAP_STAMP_N) st_acc[tid] = 0;
+  // the pass's hot table image (wc_hot_merge built it once for every block)
+  static_assert(MAP_SLOTS % 2 == 0, "image copy: 16-byte pieces");
+  for (int i = tid; i < MAP_SLOTS / 2; i += MAP_THREADS)
+    reinterpret_cast<u64x2*>(L.sig)[i] = reinterpret_cast<const u64x2*>(h.image)[i];
   for (int s = tid; s < MAP_SLOTS; s += MAP_THREADS) {
-    L.sig[s] = 0;
     L.cnt[s] = 0;
     L.off[s] = 0xFFFFFFFFu;
   }
   cursors_init(L.bcur, LD ? L.lcur : nullptr, 1u << a.log2_rec_buckets, a.rec.subcap);
-  // the table image, built in this block's LDS (the unit buffers and token
-  // lists are its scratch until the first unit)
-  // (group occupancy in the token lists, or after the histogram in the unit
-  // buffers when the lists are too small: 512-thread blocks of a 6144-slot table)
-  constexpr bool GOCC_IN_LIST = sizeof(L.list) >= 4 * NG;
-  static_assert(sizeof(L.buf) >= 4 * (SEL_BINS + 20 + (GOCC_IN_LIST ? 0 : NG)), "image scratch");
-  uint32_t* const img_scratch = reinterpret_cast<uint32_t*>(&L.buf[0][0][0]);
-  build_image(h, L.sig, img_scratch,
-              GOCC_IN_LIST ? reinterpret_cast<uint32_t*>(&L.list[0][0]) : img_scratch + SEL_BINS + 20);
   uint64_t u_begin, u_end;
   unit_range(a.chunk_len, gridDim.x, blockIdx.x, u_begin, u_end);
   if (tid == 0) {

@@ -287,7 +287,14 @@ __global__ void __launch_bounds__(256) wc_mrow_insert(const MRow* rows, uint64_t
     const uint8_t* mb = hashed ? bytes + bbase[source_of(rbase, W, r)] + me.aoff : nullptr;
     uint64_t slot = place_hash(me.k0, me.k1) & (T - 1);
     bool claimed = false;
-    for (;;) {
+    // bounded: a planned merge sizes T from the learned merged-row cap, so a
+    // job with more distinct keys than T can fill it; the compaction then
+    // counts > cap merged rows and every rank redoes the merge exactly
+    for (uint64_t probes = 0;; ++probes) {
+      if (probes >= T) {
+        slot = ~0ull;
+        break;
+      }
       // CAS first: most probes find their slot empty, and a load before the CAS
       // would add a round trip to every claim
       const uint32_t s = atomicCAS(&state[slot], 0u, (uint32_t)r + 1u);
@@ -300,6 +307,10 @@ __global__ void __launch_bounds__(256) wc_mrow_insert(const MRow* rows, uint64_t
           (!hashed || (o.alen == me.alen && mem_equal(bytes + bbase[source_of(rbase, W, s - 1)] + o.aoff, mb, me.alen))))
         break;  // same word
       slot = (slot + 1) & (T - 1);
+    }
+    if (slot == ~0ull) {  // table full (see above): the row is dropped, the merge redone
+      if (row_slot) row_slot[r] = 0xFFFFFFFFu;
+      continue;
     }
     if (!claimed) {
       atomicAdd(&cnt[slot], (unsigned long long)me.cnt);

@@ -404,6 +404,21 @@ def test_rccl_merge_protocol_world1(merge_mode):
     assert out.returncode == 0 and b"ok" in out.stdout, out.stderr.decode()[-2000:]
 
 
+@pytest.mark.parametrize("merge_mode", [0, 1])
+def test_planned_merge_outgrown_owner_table_redoes(merge_mode):
+    """The planned merge sizes each owner's table from the learned merged-row
+    cap (2 x cap, not 2 x rows received).  Caps learned on a shared vocabulary
+    (every owner sees each word from every rank: ~V / W distinct keys), then a
+    job whose four ranks hold DISJOINT vocabularies (~V distinct per owner, the
+    rows per sender unchanged, so no fixed region overflows): the owner table
+    fills, the insert's bounded probes end instead of spinning, the compaction
+    counts more merged rows than the cap and the merge is redone exactly."""
+    warm = ops.synth_host(4 << 20, seed=11, vocab=3000)
+    data = b"".join(ops.synth_host(1 << 20, seed=21 + r, vocab=3000) for r in range(4))
+    got = ops.loopback_count(data, 4, resident=True, warm=warm, chunk_bytes=1 << 20, merge_mode=merge_mode)
+    assert_same(got, ops.cpu_count(data))
+
+
 @pytest.mark.parametrize("fault", ["1:1", "2:3", "0:2"])
 @pytest.mark.parametrize("merge_mode", [0, 1])
 def test_loopback_injected_comm_fault(fault, merge_mode, monkeypatch):

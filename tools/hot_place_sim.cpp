@@ -105,7 +105,7 @@ int main(int argc, char** argv) {
   };
   std::vector<uint32_t> towner(NG, ~0u);
   if (mode == 4) { for (auto i : take) placed[i] = 1; ord.clear(); }
-  if (mode >= 5 && mode != 10) {
+  if (mode >= 5 && mode != 10 && mode != 11) {
     // thresholds as the GPU: t from counts; tiers big=8t, mid=2t
     uint32_t mn = ~0u; for (auto i : take) mn = std::min(mn, c[i]);
     const uint32_t t = mn + 1, big = 8 * t, mid = 2 * t;
@@ -165,6 +165,49 @@ int main(int argc, char** argv) {
     }
     for (uint32_t s = 0; s < 2 * NG; ++s) if (occ1[s] != ~0u) placed[occ1[s]] = 1;
     for (uint32_t g = 0; g < NG; ++g) if (towner[g] != ~0u) placed[towner[g]] = 1;
+    ord.clear();
+  }
+  if (mode == 11) {
+    // partition-local placement (round 6): group g1 = ph bits [20, 31), g2 = g1 ^
+    // (bits [8, 11) | 1) — both in g1's partition of 8 groups (ph bits [23, 31)),
+    // so each partition's 16 slots are placed by its own merge block: its
+    // sampled words by count (value per slot with SIM_VALUE=1), greedy 2-choice
+    take.clear();
+    std::vector<std::vector<uint32_t>> part(256);
+    for (auto i : cand) part[(ph[i] >> 23) & 255].push_back(i);
+    auto g2of = [&](uint32_t i) { uint32_t g1 = (ph[i] >> 20) & (NG - 1); return g1 ^ (((ph[i] >> 8) & 7u) | 1u); };
+    std::vector<uint32_t> occ(NG, 0);
+    std::vector<std::vector<uint32_t>> who(NG);  // one-slot occupants
+    const bool value = getenv("SIM_VALUE") != nullptr;
+    const uint32_t TOP = getenv("SIM_TOP") ? atoi(getenv("SIM_TOP")) : 32;
+    for (auto& P : part) {
+      std::stable_sort(P.begin(), P.end(), [&](uint32_t a, uint32_t b) {
+        if (value) return (double)c[a] / slots(a) > (double)c[b] / slots(b);
+        return c[a] > c[b]; });
+      if (P.size() > TOP) P.resize(TOP);
+      for (auto i : P) {
+        take.push_back(i);
+        uint32_t g1 = (ph[i] >> 20) & (NG - 1), g2 = g2of(i);
+        if (slots(i) == 2) {
+          if (occ[g1] == 0) { occ[g1] = 2; placed[i] = 1; }
+          else if (occ[g2] == 0) { occ[g2] = 2; placed[i] = 1; }
+          continue;
+        }
+        if (occ[g2] < occ[g1]) std::swap(g1, g2);
+        if (occ[g1] < 2) { occ[g1]++; placed[i] = 1; who[g1].push_back(i); }
+        else if (occ[g2] < 2) { occ[g2]++; placed[i] = 1; who[g2].push_back(i); }
+        else if (getenv("SIM_REPAIR")) {  // move a one-slot occupant of g1 / g2 to its other group
+          bool done = false;
+          for (uint32_t g : {g1, g2}) {
+            if (done) break;
+            for (size_t q = 0; q < who[g].size() && !done; ++q) {
+              uint32_t o = who[g][q]; uint32_t a1 = (ph[o] >> 20) & (NG - 1), a2 = g2of(o), alt = a1 == g ? a2 : a1;
+              if (occ[alt] < 2) { occ[alt]++; who[alt].push_back(o); who[g][q] = i; placed[i] = 1; done = true; }
+            }
+          }
+        }
+      }
+    }
     ord.clear();
   }
   if (mode == 10) {
