@@ -507,8 +507,9 @@ __device__ void place_partition(const HotArgs& h, uint32_t part, uint32_t n, con
       if (two_word(sg) && (sd >> 59) == 0) ok = false;
     }
   }
-  const uint32_t a = g1 & (GPP - 1), b = g2 & (GPP - 1);
-  const bool two = lng || two_word(sg);
+  // one word per lane for the scalar loop: a | b << 4 | two-slot << 8 | placeable << 9
+  const uint32_t info = (g1 & (GPP - 1)) | ((g2 & (GPP - 1)) << 4) | ((lng || two_word(sg)) ? 1u << 8 : 0u) |
+                        (ok ? 1u << 9 : 0u);
   // rank in count order (ties: lower index first)
   uint32_t rank = 0;
   for (uint32_t j = 0; j < n; ++j) {
@@ -517,15 +518,17 @@ __device__ void place_partition(const HotArgs& h, uint32_t part, uint32_t n, con
   }
   uint32_t st = 0;           // group states, 2 bits each (uniform)
   uint32_t owner = 0xFFu;    // lane s < 2 GPP: the candidate in slot s (0xFF: empty)
+  constexpr uint32_t FULL = (uint32_t)(0xAAAAAAAAull & ((1ull << (2 * GPP)) - 1ull));  // every group at 2 or 3: bit 1 of each field
   auto gst = [&](uint32_t g) { return (st >> (2 * g)) & 3u; };
   auto set_owner = [&](uint32_t slot, uint32_t who) { if (lane == slot) owner = who; };
   for (uint32_t r = 0; r < n; ++r) {
+    if ((st & FULL) == FULL) break;  // no free slot left: no word (or move) can be placed any more
     const uint64_t m = __ballot(have && rank == r);
     const uint32_t i = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-    if (!__builtin_amdgcn_readlane((int)ok, (int)i)) continue;
-    const uint32_t ai = (uint32_t)__builtin_amdgcn_readlane((int)a, (int)i);
-    const uint32_t bi = (uint32_t)__builtin_amdgcn_readlane((int)b, (int)i);
-    if (__builtin_amdgcn_readlane((int)two, (int)i)) {  // an empty group, g1 first
+    const uint32_t ii = (uint32_t)__builtin_amdgcn_readlane((int)info, (int)i);
+    if (!(ii & (1u << 9))) continue;
+    const uint32_t ai = ii & 15u, bi = (ii >> 4) & 15u;
+    if (ii & (1u << 8)) {  // an empty group, g1 first
       const uint32_t g = gst(ai) == 0 ? ai : (gst(bi) == 0 ? bi : 0xFFu);
       if (g == 0xFFu) continue;
       st |= 3u << (2 * g);
@@ -546,9 +549,8 @@ __device__ void place_partition(const HotArgs& h, uint32_t part, uint32_t n, con
       const uint32_t g = k < 2 ? ai : bi, slot = 2 * g + (k & 1);
       if (gst(g) == 3) continue;
       const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)owner, (int)slot);
-      const uint32_t oa = (uint32_t)__builtin_amdgcn_readlane((int)a, (int)o);
-      const uint32_t ob = (uint32_t)__builtin_amdgcn_readlane((int)b, (int)o);
-      const uint32_t alt = oa == g ? ob : oa, salt = gst(alt);
+      const uint32_t oi = (uint32_t)__builtin_amdgcn_readlane((int)info, (int)o);
+      const uint32_t alt = (oi & 15u) == g ? (oi >> 4) & 15u : oi & 15u, salt = gst(alt);
       if (salt >= 2) continue;
       set_owner(2 * alt + salt, o);
       st += 1u << (2 * alt);
@@ -672,6 +674,13 @@ __global__ void __launch_bounds__(1024) wc_hot_merge(HotArgs h) {
   }
   __syncthreads();
   if (tid == 0) h.cand_n[part] = min(L.nout, (uint32_t)HOT_PART_TOP);
+#ifndef WC_PLACE_ABLATE
+#define WC_PLACE_ABLATE 0  // profiling builds only (results invalid): 1 = no placement (empty image)
+#endif
+  if (WC_PLACE_ABLATE) {
+    if (tid < 2 * GPP) h.image[slot_of(part * GPP + tid / 2, tid & 1)] = 0;
+    return;
+  }
   if (tid < 64) place_partition(h, part, min(L.nout, (uint32_t)HOT_PART_TOP), L.oc, L.osig, L.oside);
 }
 
