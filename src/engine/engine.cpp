@@ -77,6 +77,9 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
     WC_HIP_CHECK(hipMemset(d_stamps, 0, MAP_STAMP_N * 8));
     dev_malloc(&d_red_stamps, RED_STAMP_N * 8);
     WC_HIP_CHECK(hipMemset(d_red_stamps, 0, RED_STAMP_N * 8));
+    dev_malloc(&d_hot_stamps, 32 * 8);
+    WC_HIP_CHECK(hipMemset(d_hot_stamps, 0, 32 * 8));
+    hot_setup_stamps(d_hot_stamps);
     red_blk_n = 16384;  // reduce grids up to this many blocks are profiled
     dev_malloc(&d_red_blk, red_blk_n * RED_BLK_WORDS * 8);
     WC_HIP_CHECK(hipMemset(d_red_blk, 0, red_blk_n * RED_BLK_WORDS * 8));
@@ -239,6 +242,17 @@ Engine::Impl::~Impl() {
       }
     }
     (void)hipFree(d_blk);
+  }
+  if (d_hot_stamps) {  // the per-job setup kernels' phases (max over blocks and jobs, us from block start)
+    unsigned long long h[32];
+    hot_setup_stamps(nullptr);
+    if (hipMemcpy(h, d_hot_stamps, sizeof h, hipMemcpyDeviceToHost) == hipSuccess) {
+      fprintf(stderr, "[wc] hot setup phases (us, max over blocks): sample init %.2f counted %.2f staged %.2f | "
+              "merge init %.2f summed %.2f hist %.2f threshold %.2f candidates %.2f placed %.2f\n",
+              h[1] / 100.0, h[2] / 100.0, h[3] / 100.0, h[17] / 100.0, h[18] / 100.0, h[19] / 100.0, h[20] / 100.0,
+              h[21] / 100.0, h[22] / 100.0);
+    }
+    (void)hipFree(d_hot_stamps);
   }
   if (d_red_stamps) {
     unsigned long long h[RED_STAMP_N];

@@ -58,6 +58,7 @@ struct Engine::Impl {
   unsigned long long* d_stamps = nullptr;  // WC_MAP_STAMPS: map phase clock sums
   unsigned long long* d_blk = nullptr;     // WC_MAP_STAMPS: per-block timing of the last map pass
   unsigned long long* d_red_stamps = nullptr;  // WC_MAP_STAMPS: reduce counters (WC_RED_STAMPS builds)
+  unsigned long long* d_hot_stamps = nullptr;  // WC_MAP_STAMPS: setup kernels' phase clock (hot_setup_stamps)
   unsigned long long* d_red_blk = nullptr;     // WC_MAP_STAMPS: per reduce block profile (RED_BLK_WORDS each)
   size_t red_blk_n = 0;
   // the profile buffer when the next reduce grid fits it (its last launch's blocks are printed at teardown)

@@ -263,6 +263,8 @@ struct ZeroList;
 // z: the pass's zeroing, applied before the map (inside the sampling launch when `sample`)
 void launch_map(const MapArgs& a, const HotArgs& h, uint32_t map_blocks, hipStream_t s, bool sample,
                 const ZeroList& z);
+// diagnostic: phase clock of wc_hot_sample / wc_hot_merge into d (32 words, nullptr: off)
+void hot_setup_stamps(unsigned long long* d);
 // extra: with ReduceArgs::bucket_w, blocks past one per bucket for the dispatch
 // plan's split heavy buckets (reduce.hip lpt_piece)
 // Bounds guard on the finalize's row writers (profiles/r5_fault_hunt.md): a

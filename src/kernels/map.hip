@@ -51,6 +51,7 @@
 
 #include <type_traits>
 
+#include "common/hip_util.hpp"
 #include "map_common.hpp"
 #include "zero_list.hpp"
 
@@ -281,6 +282,20 @@ __device__ __forceinline__ void unit_range(uint64_t chunk_len, uint32_t grid, ui
   ue = min(ub + per, nunits);
 }
 
+// Diagnostic phase clock of the two per-job setup kernels (WC_MAP_STAMPS=1:
+// hot_setup_stamps): [16 k + p] = the max over blocks of the 100 MHz wall time
+// from the block's start to its phase p (k 0: wc_hot_sample, 1: wc_hot_merge).
+__device__ unsigned long long* hot_stamps = nullptr;
+struct HotClock {
+  uint64_t t0;
+  int k;
+  __device__ HotClock(int kernel) : t0(hot_stamps ? __builtin_amdgcn_s_memrealtime() : 0), k(kernel) {}
+  __device__ void at(int p) {
+    if (hot_stamps && threadIdx.x == 0)
+      atomicMax(&hot_stamps[16 * k + p], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - t0));
+  }
+};
+
 // ------------------------------------------------------------------ sampling
 struct SampleLds {
   uint64_t fp[SAMPLE_SLOTS];  // 0 empty, else the word's fingerprint
@@ -302,6 +317,7 @@ static_assert(sizeof(SampleLds) <= 160 * 1024, "one sample block per CU");
 // of the 256 blocks in turn, two thirds of a 35 us launch.
 __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs h, ZeroList z) {
   __shared__ SampleLds L;
+  HotClock clk(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // the pass's zeroing (counters, table occupancy after a reset, ...): nothing
   // here or in wc_hot_merge touches those regions; the map and reduce that read
@@ -314,6 +330,7 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs 
   }
   if (tid < HOT_PARTS) L.pn[tid] = 0;
   __syncthreads();
+  clk.at(1);  // zero list + LDS init
   uint64_t ub, ue;
   unit_range(a.chunk_len, gridDim.x, blockIdx.x, ub, ue);
   const uint64_t nu = ue - ub;
@@ -391,6 +408,7 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs 
     wave_sync();
   }
   __syncthreads();
+  clk.at(2);  // the sampled units counted
   const size_t cell0 = (size_t)blockIdx.x * HOT_STAGE_CAP;  // + partition * maxb * HOT_STAGE_CAP
   for (int s = tid; s < SAMPLE_SLOTS; s += MAP_THREADS) {
     const uint32_t c = L.cnt[s];
@@ -409,6 +427,7 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs 
   }
   __syncthreads();
   if (tid < HOT_PARTS) h.stage_n[(size_t)tid * h.maxb + blockIdx.x] = min(L.pn[tid], (uint32_t)HOT_STAGE_CAP);
+  clk.at(3);  // stage cells written
 }
 
 // ------------------------------------------------------------------ selection
@@ -611,6 +630,7 @@ __device__ __forceinline__ void merge_insert(HotMergeLds& L, const HotEnt& e) {
 }
 __global__ void __launch_bounds__(1024) wc_hot_merge(HotArgs h) {
   __shared__ HotMergeLds L;
+  HotClock clk(1);
   const int tid = threadIdx.x;
   const uint32_t part = blockIdx.x;
   for (int s = tid; s < MERGE_SLOTS; s += 1024) {
@@ -620,6 +640,7 @@ __global__ void __launch_bounds__(1024) wc_hot_merge(HotArgs h) {
   for (int i = tid; i < SEL_BINS; i += 1024) L.hist[i] = 0;
   if (tid == 0) L.nout = L.nties = 0;
   __syncthreads();
+  clk.at(1);  // LDS init
   const size_t row = (size_t)part * h.maxb;
   // thread tid: entry (tid % CAP) of the cells tid / CAP + k * CELLS (all loads of a thread issued together)
   const uint32_t e = tid % HOT_STAGE_CAP, c0 = tid / HOT_STAGE_CAP;
@@ -641,10 +662,13 @@ __global__ void __launch_bounds__(1024) wc_hot_merge(HotArgs h) {
       if (e < n[k]) merge_insert(L, x[k]);
   }
   __syncthreads();
+  clk.at(2);  // stage cells summed
   for (int s = tid; s < MERGE_SLOTS; s += 1024) hist_add_wave(L.hist, min(L.cnt[s], (uint32_t)SEL_BINS - 1), L.cnt[s] != 0);
   __syncthreads();
   uint32_t t, cum;
+  clk.at(3);  // histogram
   count_threshold<1024>(L.hist, HOT_PART_TOP, L.sc, t, cum);
+  clk.at(4);  // threshold
   const uint32_t ties = t > 1 ? HOT_PART_TOP - min(cum, (uint32_t)HOT_PART_TOP) : 0u;
   for (int s = tid; s < MERGE_SLOTS; s += 1024) {
     const uint32_t c = L.cnt[s];
@@ -673,6 +697,7 @@ __global__ void __launch_bounds__(1024) wc_hot_merge(HotArgs h) {
     L.oside[o] = sd;
   }
   __syncthreads();
+  clk.at(5);  // candidates written
   if (tid == 0) h.cand_n[part] = min(L.nout, (uint32_t)HOT_PART_TOP);
 #ifndef WC_PLACE_ABLATE
 #define WC_PLACE_ABLATE 0  // profiling builds only (results invalid): 1 = no placement (empty image)
@@ -682,6 +707,7 @@ __global__ void __launch_bounds__(1024) wc_hot_merge(HotArgs h) {
     return;
   }
   if (tid < 64) place_partition(h, part, min(L.nout, (uint32_t)HOT_PART_TOP), L.oc, L.osig, L.oside);
+  clk.at(6);  // placed
 }
 
 // ------------------------------------------------------------------ map
@@ -1261,6 +1287,10 @@ __global__ void __launch_bounds__(MAP_THREADS, MAP_WAVES / 4) wc_map(MapArgs a, 
 }
 
 }  // namespace dev
+
+void hot_setup_stamps(unsigned long long* d) {
+  WC_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(dev::hot_stamps), &d, sizeof d));
+}
 
 void launch_map(const MapArgs& a, const HotArgs& h, uint32_t map_blocks, hipStream_t s, bool sample,
                 const ZeroList& z) {

@@ -10,7 +10,11 @@
 // bound), 5 / 6 tiered greedy + one- / two-level displacement repairs,
 // 7 the kernel: BUDGET words by sampled count (not slots), tiered greedy,
 // 8 slot-valued selection, 9 = 7 with two-word words first in each tier,
-// 10 the round-6 image builder (priority random-walk cuckoo, one block per job).
+// 10 one image builder per job (greedy tiers + priority-eviction walks; built
+// on the GPU in round 6 and dropped: its single block cost more than it saved),
+// 11 the shipped round-6 placement: each of 256 partitions (8 groups; a
+// word's two groups in its partition) places its own sampled words by count
+// (SIM_REPAIR=1: + the one-level move of map.hip place_partition).
 // SIM_ONE_SLOT8=1: 8-byte words as one-slot words; SIM_FIRST_SLOT8=1: only in
 // an empty group's first slot.
 // profiles/r5_session.md §12.
