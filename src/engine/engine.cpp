@@ -247,9 +247,9 @@ Engine::Impl::~Impl() {
     unsigned long long h[32];
     hot_setup_stamps(nullptr);
     if (hipMemcpy(h, d_hot_stamps, sizeof h, hipMemcpyDeviceToHost) == hipSuccess) {
-      fprintf(stderr, "[wc] hot setup phases (us, max over blocks): sample init %.2f counted %.2f staged %.2f | "
+      fprintf(stderr, "[wc] hot setup phases (us, max over blocks): sample init %.2f (unit loaded %.2f, counted %.2f) counted %.2f staged %.2f | "
               "merge init %.2f summed %.2f hist %.2f threshold %.2f candidates %.2f placed %.2f\n",
-              h[1] / 100.0, h[2] / 100.0, h[3] / 100.0, h[17] / 100.0, h[18] / 100.0, h[19] / 100.0, h[20] / 100.0,
+              h[1] / 100.0, h[4] / 100.0, h[5] / 100.0, h[2] / 100.0, h[3] / 100.0, h[17] / 100.0, h[18] / 100.0, h[19] / 100.0, h[20] / 100.0,
               h[21] / 100.0, h[22] / 100.0);
     }
     (void)hipFree(d_hot_stamps);

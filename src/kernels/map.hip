@@ -315,10 +315,33 @@ static_assert(sizeof(SampleLds) <= 160 * 1024, "one sample block per CU");
 // The round-2 form added every block's words into one global fingerprint table
 // with device CAS + add: the Zipf head's slots took one atomic pair from each
 // of the 256 blocks in turn, two thirds of a 35 us launch.
+// SUBW waves share each sampled unit, each counting every SUBW-th word of
+// every lane (a lane holds ~5 words of its 32 bytes and counts them one after
+// another: one wave per unit took 8 us for that loop, with 12 of 16 waves idle).
+constexpr int SUBW = MAP_WAVES / (int)HOT_SAMPLE;
+static_assert(SUBW >= 1 && MAP_WAVES % (int)HOT_SAMPLE == 0, "sampling: whole waves per sampled unit");
 __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs h, ZeroList z) {
   __shared__ SampleLds L;
   HotClock clk(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t sub = (uint32_t)wave % SUBW;
+  uint64_t ub, ue;
+  unit_range(a.chunk_len, gridDim.x, blockIdx.x, ub, ue);
+  const uint64_t nu = ue - ub;
+  const uint64_t ns = min<uint64_t>(nu, HOT_SAMPLE);
+  uint8_t* buf = L.buf[wave];
+  const uint32_t pbase = lane * MAP_BPL;
+  // this wave's unit loaded first: its HBM latency overlaps the zeroing below
+  const uint64_t i = (uint64_t)wave / SUBW;  // < HOT_SAMPLE: one unit per wave group
+  const bool act = i < ns;
+  const uint64_t u0 = act ? (ub + i * nu / ns) * UNIT : 0;
+  uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0, h16 = make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
+  uint32_t pv = 0x20;
+  if (act) {
+    load32(a, u0 + pbase, p0, p1);
+    if (lane < HALO / 16) h16 = load16(a, u0 + UNIT + lane * 16);
+    pv = (u0 == 0 && a.prev_byte >= 0) ? (uint32_t)a.prev_byte : a.text[(int64_t)u0 - 1];
+  }
   // the pass's zeroing (counters, table occupancy after a reset, ...): nothing
   // here or in wc_hot_merge touches those regions; the map and reduce that read
   // them run after both launches
@@ -331,32 +354,19 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs 
   if (tid < HOT_PARTS) L.pn[tid] = 0;
   __syncthreads();
   clk.at(1);  // zero list + LDS init
-  uint64_t ub, ue;
-  unit_range(a.chunk_len, gridDim.x, blockIdx.x, ub, ue);
-  const uint64_t nu = ue - ub;
-  const uint64_t ns = min<uint64_t>(nu, HOT_SAMPLE);
-  uint8_t* buf = L.buf[wave];
-  const uint32_t pbase = lane * MAP_BPL;
-  for (uint64_t i = wave; i < ns; i += MAP_WAVES) {
-    const uint64_t u = ub + i * nu / ns;
-    const uint64_t u0 = u * UNIT;
-    uint4 p0, p1;
-    load32(a, u0 + pbase, p0, p1);
+  if (act) {
     reinterpret_cast<uint4*>(&buf[pbase])[0] = p0;
     reinterpret_cast<uint4*>(&buf[pbase])[1] = p1;
-    uint4 h16 = make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
-    if (lane < HALO / 16) {
-      h16 = load16(a, u0 + UNIT + lane * 16);
-      *reinterpret_cast<uint4*>(&buf[UNIT + lane * 16]) = h16;
-    }
-    const uint32_t pv = (u0 == 0 && a.prev_byte >= 0) ? (uint32_t)a.prev_byte : a.text[(int64_t)u0 - 1];
+    if (lane < HALO / 16) *reinterpret_cast<uint4*>(&buf[UNIT + lane * 16]) = h16;
     wave_sync();
     uint64_t dm;
     uint32_t bits;
     unit_masks(p0, p1, halo_bits(h16), pv, u0, pbase, a.chunk_len, dm, bits);
-    while (bits) {
+    clk.at(4);  // diagnostic: wave 0's unit loaded and masked
+    for (uint32_t k = 0; bits; ++k) {
       const uint32_t b = __ffs(bits) - 1;
       bits &= bits - 1;
+      if (k % SUBW != sub) continue;  // another wave of the group counts this word
       const uint64_t rest = dm >> b;
       const uint32_t p = pbase + b;
       uint32_t len;
@@ -406,6 +416,7 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs 
       }
     }
     wave_sync();
+    clk.at(5);  // diagnostic: wave 0's unit's words counted
   }
   __syncthreads();
   clk.at(2);  // the sampled units counted
