@@ -41,11 +41,15 @@ void DeviceArena::reserve(size_t bytes) {
     used_ = 0;
     return;
   }
+  // work already launched may still write the old store (the engine's merge
+  // zeroing rides in a job's first launch): drained before it is freed
+  if (base_) WC_HIP_CHECK(hipDeviceSynchronize());
   if (base_) WC_HIP_CHECK(hipFree(base_));
   base_ = nullptr;
   cap_ = used_ = 0;
   dev_malloc(&base_, bytes);
   cap_ = bytes;
+  ++gen_;
 }
 
 void DeviceArena::reset() {

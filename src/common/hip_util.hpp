@@ -66,10 +66,12 @@ class DeviceArena {
   void reset();  // WC_POISON=2: the regions handed out so far are poisoned
   size_t capacity() const { return cap_; }
   size_t used() const { return used_; }
+  uint64_t generation() const { return gen_; }  // bumped by every reallocation
 
  private:
   uint8_t* base_ = nullptr;
   size_t cap_ = 0, used_ = 0;
+  uint64_t gen_ = 0;
 };
 
 // Pinned host buffer (hipHostMalloc) RAII.

@@ -567,10 +567,12 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
   uint64_t T = 1024;
   while (T < 2 * std::min(RR, Gr)) T <<= 1;
   const bool have = R == 0 || all_ranks;
-  A.reserve(2 * RR * sizeof(MRow) + 2 * RB + T * (4 + 16) + RR * sizeof(MRow) + (size_t)GR * sizeof(MRow) +
+  // send + receive rows and bytes, the owner table (state + index), the
+  // merged rows, the gathered rows and bytes, rank 0's columns, small words
+  A.reserve(2 * RR * sizeof(MRow) + 2 * RB + T * (4 + 4) + Gr * sizeof(MRow) + (size_t)GR * sizeof(MRow) +
             (size_t)W * RB + (have ? GR * (5 * 8 + 4) : 0) + (4 * (size_t)W + 8) * 8 + 64 * 1024 +
-            // dense: send_pos, row_slot, ids, ids_back, slot_id (u32); vc, vf, dcnt, dfirst, scnt, sfirst (u64)
-            (dense ? (nb + 3 * RR + T) * 4 + (4 * GR + 2 * (uint64_t)Gr) * 8 + 16 * 256 : 0));
+            // dense: send_pos, ids, ids_back (u32); the padded vectors vc, vf (u64)
+            (dense ? (nb + 2 * RR) * 4 + 2 * GR * 8 + 16 * 256 : 0));
   A.reset();
   // Nothing travels from a rank to itself: the scatter writes this rank's own
   // rows and bytes straight into its receive regions, rank 0's compaction
@@ -582,17 +584,17 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
   uint8_t* send_bytes = take_aligned<uint8_t>(A, RB);
   MRow* recv_rows = take_aligned<MRow>(A, RR);
   uint8_t* recv_bytes = R == 0 ? gbytes : take_aligned<uint8_t>(A, RB);
-  uint32_t* state = take_aligned<uint32_t>(A, T);
-  unsigned long long* tcnt = take_aligned<unsigned long long>(A, T);
-  unsigned long long* tfirst = take_aligned<unsigned long long>(A, T);
-  // compaction writes up to RR rows (more than Gr: flagged, the merge is redone); the first Gr are sent
-  MRow* merged = R == 0 ? grows : take_aligned<MRow>(A, RR);
-  const uint64_t merged_cap = R == 0 ? GR : RR;
+  uint32_t* state = take_aligned<uint32_t>(A, T);     // claiming row + 1 per slot
+  uint32_t* slot_idx = take_aligned<uint32_t>(A, T);  // its merged-row index + 1, once published
+  // the owner's merged rows: the first Gr (more: counted, flagged, the merge is
+  // redone) — count and (inverted) first offset words zeroed, added to by atomics
+  MRow* merged = R == 0 ? grows : take_aligned<MRow>(A, Gr);
   uint64_t* d_base = take_aligned<uint64_t>(A, 2 * (size_t)W + 2);
   uint64_t* d_seg = take_aligned<uint64_t>(A, (size_t)W + 1);
   uint32_t* send_pos = dense ? take_aligned<uint32_t>(A, nb) : nullptr;
-  uint32_t* row_slot = dense ? take_aligned<uint32_t>(A, RR) : nullptr;
-  uint32_t* slot_id = dense ? take_aligned<uint32_t>(A, T) : nullptr;
+  // dense: each received row's owner-local id (written by the insert) and the ids that come back
+  uint32_t* ids = dense ? take_aligned<uint32_t>(A, RR) : nullptr;
+  uint32_t* ids_back = dense ? take_aligned<uint32_t>(A, RR) : nullptr;
   // dense: padded count / first-offset vectors (zeroed with everything else)
   uint64_t* vc = dense ? take_aligned<uint64_t>(A, GR) : nullptr;
   uint64_t* vf = dense ? take_aligned<uint64_t>(A, GR) : nullptr;
@@ -605,15 +607,23 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
     if (R + 1 < W) z.add(send_rows + (uint64_t)(R + 1) * Cr, (uint64_t)(W - R - 1) * Cr * sizeof(MRow));
     z.add(recv_rows + (uint64_t)R * Cr, Cr * sizeof(MRow));
     z.add(state, T * 4);
-    z.add(tcnt, T * 8);
-    z.add(tfirst, T * 8, 0xFFFFFFFFu);
-    z.add(d_own, 16);  // merged rows (wc_mrow_compact adds), flags (the scatter ORs)
+    z.add(slot_idx, T * 4);
+    z.add(merged, Gr * sizeof(MRow));
+    z.add(d_own, 16);  // merged rows (wc_mrow_insert_emit adds), flags (the scatter ORs)
     if (im.cols.occ) z.add(reinterpret_cast<uint32_t*>(im.d_local_n), 8);  // the scatter counts the table's keys
     if (dense) {
       z.add(vc, GR * 8);
       z.add(vf, GR * 8, 0xFFFFFFFFu);
     }
-    launch_zero_regions(z, s);  // (region bases and the max offset: written by the scatter's block 0)
+    // (region bases and the max offset: written by the scatter's block 0).  The
+    // same list as the last planned merge's was already applied by this job's
+    // sampling launch (launch_pass): nothing since has touched these regions
+    if (!(im.merge_zero_pre && same_fills(z, im.merge_zero_last) && im.merge_zero_gen == im.merge_arena_gen()))
+      launch_zero_regions(z, s);
+    im.merge_zero_last = z;
+    im.merge_zero_last_valid = true;
+    im.merge_zero_gen = im.merge_arena_gen();
+    im.merge_zero_pre = false;
   }
   // 1. pack into the fixed regions (this rank's pass flags and region overflow
   // into its flag word) and exchange them whole
@@ -641,18 +651,10 @@ void merge_cols_planned(Engine::Impl& im, Comm& comm, bool all_ranks, bool dense
     account(im, R, per);  // the owner exchange (rows + LONG bytes, one grouped launch)
   }
   // 2. owner merge (padding rows skipped), merged rows counted on the device into the quad
-  launch_mrow_insert(recv_rows, RR, recv_bytes, d_base, d_base + W + 1, (uint32_t)W, state, tcnt, tfirst, T, row_slot,
-                     s);
-  launch_mrow_compact(recv_rows, state, tcnt, tfirst, T, d_base, d_base + W + 1, (uint32_t)W, merged, d_own, slot_id,
-                      s, merged_cap);
+  // (+ dense: each row's owner-local id, this rank's own region straight into the returned ids)
+  launch_mrow_insert_emit(recv_rows, RR, recv_bytes, d_base, d_base + W + 1, (uint32_t)W, state, slot_idx, T, merged,
+                          d_own, Gr, ids, ids_back, (uint32_t)R, Cr, s);
   // 3. every rank's quad (+ dense: the owner-local ids back to the senders), the decision
-  uint32_t* ids = nullptr;
-  uint32_t* ids_back = nullptr;
-  if (dense) {
-    ids = take_aligned<uint32_t>(A, RR);
-    ids_back = take_aligned<uint32_t>(A, RR);
-    launch_row_ids(row_slot, slot_id, RR, d_owns, 0u, ids, s, ids_back, (uint32_t)R, Cr);  // own region in place
-  }
   comm.group_begin();
   comm.allgather(d_own, d_owns, 32, s);
   if (dense) {

@@ -66,6 +66,7 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   if (const char* e = std::getenv("WC_NO_SPECULATE")) speculate = std::atoi(e) == 0;
   if (const char* e = std::getenv("WC_SPIN_WAIT")) spin_wait = std::atoi(e) != 0;
   if (const char* e = std::getenv("WC_STAGE_EVENTS")) stage_events = std::atoi(e) != 0;
+  if (const char* e = std::getenv("WC_HOST_CLOCK")) host_clock = std::atoi(e) != 0;
   if (const char* e = std::getenv("WC_FIRST_ORDER")) {
     order_radix = std::string(e) == "radix";
     order_bitmap = std::string(e) == "bitmap";
@@ -180,8 +181,27 @@ Engine::Impl::Impl(const Options& o) : opt(o) {
   WC_HIP_CHECK(hipStreamSynchronize(s));
 }
 
+void Engine::Impl::hc_mark(int i) {
+  if (!host_clock) return;
+  const double t = now_seconds();
+  // the interval since the previous milestone is credited to this one; a job's
+  // start closes the caller's own turnaround since the previous job's end
+  if (hc_prev > 0) hc_sum[i] += t - hc_prev;
+  if (i == HC_DONE) ++hc_jobs;
+  hc_prev = t;
+}
+
 Engine::Impl::~Impl() {
   (void)hipSetDevice(dev);
+  if (host_clock && hc_jobs > 1) {
+    const double n = (double)hc_jobs;
+    fprintf(stderr,
+            "[wc] host clock (us per job, %llu jobs): caller gap %.2f | reset %.2f | ->prelaunch %.2f | "
+            "sample+merge+map launches %.2f | ->wait %.2f | wait %.2f | waited->done %.2f\n",
+            (unsigned long long)hc_jobs, hc_sum[HC_START] / (n - 1) * 1e6, hc_sum[HC_RESET] / n * 1e6,
+            hc_sum[HC_PRELAUNCH] / n * 1e6, hc_sum[HC_MAPPED] / n * 1e6, hc_sum[HC_WAIT] / n * 1e6,
+            hc_sum[HC_WAITED] / n * 1e6, hc_sum[HC_DONE] / n * 1e6);
+  }
   if (s) (void)hipStreamSynchronize(s);
   if (copy_s) (void)hipStreamSynchronize(copy_s);
   for (int i = 0; i < 2; ++i) {
@@ -398,6 +418,16 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
     z.add(d_arena_cursor, sizeof(unsigned long long));
     reset_pending = false;
   }
+  // the last pass of a job whose finalize will likely run the planned merge
+  // again: its zeroing rides here (merge_cols_planned skips its launch if the
+  // list it needs is this one)
+  // (not under WC_POISON=2: the arenas' reset poisons the regions after this)
+  merge_zero_pre = false;
+  if (defer_publish && merge_zero_last_valid && merge_caps.valid && merge_zero_gen == merge_arena_gen() &&
+      poison_level() < 2) {
+    z.append_fills(merge_zero_last);
+    merge_zero_pre = true;
+  }
   pass_rec = rec;
   pass_rec.cursor = &d_ctr->records;
   pass_rec.subcap = (uint32_t)std::min<uint64_t>(rec.cap / ((uint64_t)blocks << log2_rb), 0xFFFFull);
@@ -410,7 +440,9 @@ void Engine::Impl::launch_pass(const uint8_t* text, uint64_t len, uint64_t avail
   if (d_stamps) blocks_stamped += blocks;
   hot.text = text;
   hot.nblk = blocks;
+  hc_mark(HC_PRELAUNCH);
   launch_map(m, hot, blocks, s, sample, z);  // z applied first (inside the sampling launch)
+  hc_mark(HC_MAPPED);
   mark(EV_MAP);
   if (sync_debug) {  // WC_SYNC_DEBUG: attribute a device fault to a kernel and a chunk
     const hipError_t e = hipStreamSynchronize(s);
@@ -853,8 +885,10 @@ bool Engine::Impl::finalize_local_speculative() {
     pc.seq = ++spec_seq;
   }
   launch_publish(pc, s);
+  hc_mark(HC_WAIT);
   if (spin_wait) wait_published(seq, spec_seq);
   else WC_HIP_CHECK(hipStreamSynchronize(s));
+  hc_mark(HC_WAITED);
   // the pass's counters arrived with this sync: check it (stats, recovery).  A
   // discarded attempt re-arms the bounds word: whatever it recorded belongs to
   // output that is thrown away, not to the redo that publishes it next
@@ -1109,6 +1143,7 @@ void Engine::set_stage_events(bool on) { p_->stage_events = on; }
 
 void Engine::reset() {
   Impl& im = *p_;
+  im.hc_mark(Impl::HC_START);
   WC_HIP_CHECK(hipSetDevice(im.dev));
   // zero only the occupancy: a bucket with occupancy 0 is empty whatever its
   // slice holds (reduce / compact / split never read such a slice)
@@ -1153,6 +1188,8 @@ void Engine::reset() {
   im.max_end = 0;
   im.ev_n = 0;
   im.hot_valid = false;  // each job samples its own hot words
+  im.merge_zero_pre = false;
+  im.hc_mark(Impl::HC_RESET);
 }
 
 void Engine::count_device(const uint8_t* d_text, uint64_t n, uint64_t avail, uint64_t global_base, int prev_byte) {
@@ -1425,6 +1462,7 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
   im.order_redo = false;
   bool drained = false;
   im.planned_active = false;
+  if (!merged) im.merge_zero_last_valid = false;  // a local job: the next pass does not pre-zero merge regions
   if (merged) {
     im.drop_reduce_bits();  // the merged order runs on merged columns
     // planned (no host round trip) when the last exact merge of this shape
@@ -1477,7 +1515,9 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
       launch_publish(pc, im.s);
       // the merge's last collectives are still in flight: wait under the comm watchdog
       if (merged && im.spin_wait) {
+        im.hc_mark(HC_WAIT);
         comm->wait_word(reinterpret_cast<const uint32_t*>(im.h_fin.data() + 32), im.fin_seq, im.s);
+        im.hc_mark(HC_WAITED);
         return;
       }
     }
@@ -1548,6 +1588,7 @@ uint64_t Engine::Impl::finalize(Comm* comm, bool all_ranks) {
     im.cols.dn = nullptr;
   }
   im.st.host_finalize_ms += (now_seconds() - t0) * 1e3;
+  im.hc_mark(HC_DONE);
   WC_LOG(LOG_INFO, "dev %d: finalize %.3f ms (host), %llu keys, %u chunk(s), %llu records, %u re-run(s)", im.dev,
          (now_seconds() - t0) * 1e3, (unsigned long long)im.cols.n, im.st.chunks, (unsigned long long)im.st.records,
          im.st.map_reruns);

@@ -214,6 +214,25 @@ struct Engine::Impl {
     uint64_t rows = 0, bytes = 0, merged = 0;  // per (rank -> owner) region / per owner in the gather
     uint64_t gmax_end = 0;                     // the sort key width of the last exact merge
   } merge_caps;
+  // WC_HOST_CLOCK=1 (diagnostics): host time between a job's milestones
+  // (each credited with the time since the previous milestone), summed over
+  // jobs and printed at teardown — where the GPU's idle gap between jobs goes
+  enum { HC_START, HC_RESET, HC_PRELAUNCH, HC_MAPPED, HC_WAIT, HC_WAITED, HC_DONE, HC_N };
+  bool host_clock = false;
+  double hc_prev = 0, hc_sum[HC_N] = {};
+  uint64_t hc_jobs = 0;
+  void hc_mark(int i);
+  // The last planned merge's zeroing list: the next job's last pass applies it
+  // inside its sampling launch (merge_zero_pre), and the planned merge skips
+  // its own zeroing launch when its list is the same (one launch fewer per job)
+  ZeroList merge_zero_last{};
+  bool merge_zero_last_valid = false;
+  bool merge_zero_pre = false;
+  uint64_t merge_zero_gen = 0;  // the arenas' generations the list points into (a reallocation voids it)
+  uint64_t merge_arena_gen() const {
+    return merge_mem.generation() * 0x9E3779B97F4A7C15ull ^ merge_small.generation() * 0xC2B2AE3D27D4EB4Full ^
+           fin_mem.generation();
+  }
   bool planned_active = false;      // a planned merge is in flight: check its flags after the last wait
   PendingPass planned_pass;         // the pass it ran behind (completed after the last wait)
   uint32_t* d_merge_flags = nullptr;  // device word of the planned merge's flags (merge_small)

@@ -392,7 +392,9 @@ void launch_iota_u32(uint32_t* v, uint64_t n, hipStream_t s);
 // util.hip: fill several device regions (+ a few small copies, e.g. host words
 // from page-locked memory into device buffers) / copy several small device
 // regions into page-locked host memory, one launch each (sizes in 32-bit words).
-constexpr int ZERO_MAX_REGIONS = 12, ZERO_MAX_COPIES = 4, PUB_MAX_REGIONS = 8;
+// (18 fills: a pass's own <= 5 + a planned merge's <= 12, folded into the
+// job's sampling launch — dist/merge.cpp merge_cols_planned)
+constexpr int ZERO_MAX_REGIONS = 18, ZERO_MAX_COPIES = 4, PUB_MAX_REGIONS = 8;
 [[noreturn]] void launch_list_overflow(const char* what);  // util.hip: fails the job (a caller bug)
 struct ZeroList {
   uint32_t* ptr[ZERO_MAX_REGIONS];
@@ -415,7 +417,17 @@ struct ZeroList {
     csrc[nc] = static_cast<const uint32_t*>(src);
     cwords[nc++] = (uint32_t)(bytes / 4);
   }
+  void append_fills(const ZeroList& o) {
+    for (int i = 0; i < o.n; ++i) add(o.ptr[i], o.words[i] * 4, o.val[i]);
+  }
 };
+// the same fills (regions, sizes, patterns, in order) and no copies in either
+inline bool same_fills(const ZeroList& a, const ZeroList& b) {
+  if (a.n != b.n || a.nc != 0 || b.nc != 0) return false;
+  for (int i = 0; i < a.n; ++i)
+    if (a.ptr[i] != b.ptr[i] || a.words[i] != b.words[i] || a.val[i] != b.val[i]) return false;
+  return true;
+}
 struct PubList {
   const uint32_t* src[PUB_MAX_REGIONS];
   uint32_t* dst[PUB_MAX_REGIONS];
@@ -504,6 +516,15 @@ void launch_mrow_compact(const MRow* rows, const uint32_t* state, const unsigned
                          const unsigned long long* first, uint64_t T, const uint64_t* rbase, const uint64_t* bbase,
                          uint32_t W, MRow* out, unsigned long long* out_n, uint32_t* slot_id, hipStream_t s,
                          uint64_t out_cap = ~0ull);  // slot_id nullable; rows past out_cap are counted, not written
+// Planned merge, owner side: insert + emit of the merged rows in one launch
+// (no compaction).  `out` rows [0, cap) must read count 0 / first word 0 (the
+// first offset is stored inverted: atomicMax of ~first); rows past cap are
+// counted in *out_n, not written.  ids (dense, nullable): each received row's
+// owner-local id (rows of region `self` of `reg` rows -> ids_self).
+void launch_mrow_insert_emit(const MRow* rows, uint64_t R, const uint8_t* bytes, const uint64_t* rbase,
+                             const uint64_t* bbase, uint32_t W, uint32_t* state, uint32_t* slot_idx, uint64_t T,
+                             MRow* out, unsigned long long* out_n, uint64_t cap, uint32_t* ids, uint32_t* ids_self,
+                             uint32_t self, uint64_t reg, hipStream_t s);
 void launch_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rbase, const uint64_t* bbase, uint32_t W,
                          uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first, uint64_t* soff, uint32_t* slen,
                          hipStream_t s, const uint64_t* dn = nullptr);  // dn: device-side row count (n a bound)

@@ -367,6 +367,106 @@ __global__ void __launch_bounds__(256) wc_mrow_compact(const MRow* rows, const u
   }
 }
 
+// Planned merge (dist/merge.cpp merge_cols_planned), owner side: the insert
+// and the compaction in one launch.  A slot belongs to the first row that
+// CAS-es its id in (as wc_mrow_insert); the claiming rows of a block take
+// their merged-row indices with one device atomic, write their key and
+// long-word reference there, and publish the index in slot_idx.  Every row —
+// claimer or a later row of the same key, which waits for the published index
+// — adds its count and its inverted first offset (atomicMax of ~first) to the
+// merged row with device atomics: the caller zeroed both words, so no order is
+// needed between a claimer's stores and another row's adds, and no fence.
+// A waiting row's claimer published before its own wave could wait (claim,
+// publish, then wait, in that order per wave), so the waits cannot cycle.
+// Indices past `cap` are counted in *out_n (the merge is redone), not written.
+__global__ void __launch_bounds__(256) wc_mrow_insert_emit(const MRow* rows, uint64_t R, const uint8_t* bytes,
+                                                           const uint64_t* rbase, const uint64_t* bbase, uint32_t W,
+                                                           uint32_t* state, uint32_t* slot_idx, uint64_t T, MRow* out,
+                                                           unsigned long long* out_n, uint64_t cap, uint32_t* ids,
+                                                           uint32_t* ids_self, uint32_t self, uint64_t reg) {
+  __shared__ uint32_t bcount;
+  __shared__ unsigned long long bbase_idx;
+  const int lane = (int)__lane_id();
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t r0 = blockIdx.x * (uint64_t)blockDim.x; r0 < R; r0 += stride) {  // whole blocks iterate together
+    const uint64_t r = r0 + threadIdx.x;
+    if (threadIdx.x == 0) bcount = 0;
+    MRow me{};
+    bool live = false;
+    if (r < R) {
+      me = rows[r];
+      live = me.k1 != K1_EMPTY;  // else padding of a fixed region
+    }
+    uint64_t slot = ~0ull;
+    bool claimed = false;
+    uint32_t src = 0;
+    if (live) {
+      const bool hashed = key_is_hashed(me.k1);
+      src = source_of(rbase, W, r);
+      const uint8_t* mb = hashed ? bytes + bbase[src] + me.aoff : nullptr;
+      slot = place_hash(me.k0, me.k1) & (T - 1);
+      for (uint64_t probes = 0;; ++probes) {
+        if (probes >= T) {  // table full: the row is dropped, the count past cap redoes the merge
+          slot = ~0ull;
+          break;
+        }
+        const uint32_t s = atomicCAS(&state[slot], 0u, (uint32_t)r + 1u);
+        if (s == 0) {
+          claimed = true;
+          break;
+        }
+        const MRow& o = rows[s - 1];
+        if (o.k0 == me.k0 && o.k1 == me.k1 &&
+            (!hashed || (o.alen == me.alen && mem_equal(bytes + bbase[source_of(rbase, W, s - 1)] + o.aoff, mb, me.alen))))
+          break;  // same word
+        slot = (slot + 1) & (T - 1);
+      }
+    }
+    __syncthreads();  // bcount reset seen
+    const uint64_t cm = __ballot(claimed);
+    uint32_t wb = 0;
+    if (lane == 0 && cm) wb = atomicAdd(&bcount, (uint32_t)__popcll(cm));
+    wb = (uint32_t)__shfl((int)wb, 0);
+    __syncthreads();
+    if (threadIdx.x == 0) bbase_idx = bcount ? atomicAdd(out_n, (unsigned long long)bcount) : 0;
+    __syncthreads();
+    uint64_t idx = ~0ull;
+    if (claimed) {
+      idx = bbase_idx + wb + (uint64_t)__popcll(cm & lt);
+      if (idx < cap) {
+        MRow* o = out + idx;
+        o->k0 = me.k0;
+        o->k1 = me.k1;
+        o->aoff = me.alen ? (uint32_t)(bbase[src] + me.aoff) : 0u;
+        o->alen = me.alen;
+      }
+      __hip_atomic_store(&slot_idx[slot], (uint32_t)idx + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // every claim of the block published before any of its rows waits: as an
+    // if / else the compiler may run the waiting lanes of a wave first, with the
+    // claiming lanes of the same wave (a region boundary: two sources) masked off
+    __syncthreads();
+    if (!claimed && slot != ~0ull) {  // a later row of a claimed key: wait for its index
+      uint32_t v;
+      while ((v = __hip_atomic_load(&slot_idx[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u)
+        __builtin_amdgcn_s_sleep(1);
+      idx = v - 1u;
+    }
+    if (idx < cap) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(&out[idx].cnt), (unsigned long long)me.cnt);
+      atomicMax(reinterpret_cast<unsigned long long*>(&out[idx].first), (unsigned long long)~me.first);
+    }
+    if (ids && r < R) {
+      uint32_t* d = ids_self && r / reg == self ? ids_self : ids;
+      d[r] = idx == ~0ull ? 0xFFFFFFFFu : (uint32_t)idx;
+    }
+    // no wave claims in the next round before every wave of this one is done
+    // waiting: a claim made behind a waiting wave's barrier could be the one it waits for
+    __syncthreads();
+  }
+}
+
 // Dense merge: global id of received row r = this owner's id base + the compact
 // index of the slot the row merged into.
 // id base = the merged rows of the owners before this one, from the all-gathered
@@ -470,7 +570,8 @@ __global__ void wc_merge_check(const unsigned long long* owns, uint32_t W, uint6
 // they become dense key columns at the exclusive prefix of the owners' counts,
 // the long-word references made absolute in the gathered byte buffer (owner o's
 // payload at o * byte_stride); dense merge: counts / first offsets from the
-// reduced padded vectors (id o * reg_merged + j), else from the rows.
+// reduced padded vectors (id o * reg_merged + j), else from the rows (first
+// offset inverted, as wc_mrow_insert_emit leaves it).
 // *out_n = the key count.
 // HIST: one 1024-thread block per CU, an LDS histogram per block flushed with
 // one global add per nonzero bin (a device atomic per row measured 16 us at
@@ -516,7 +617,7 @@ __global__ void __launch_bounds__(HIST ? 1024 : 256) wc_mrow_regions_to_cols(con
     k0[at] = m.k0;
     k1[at] = m.k1;
     cnt[at] = dcnt ? dcnt[i] : m.cnt;
-    const uint64_t f = dfirst ? dfirst[i] : m.first;
+    const uint64_t f = dfirst ? dfirst[i] : ~m.first;  // stored inverted by wc_mrow_insert_emit
     first[at] = f;
     soff[at] = m.alen ? o * byte_stride + m.aoff : 0;
     slen[at] = m.alen;
@@ -589,6 +690,16 @@ void launch_mrow_compact(const MRow* rows, const uint32_t* state, const unsigned
   const uint64_t blocks = (T + 256 * dev::MCOMPACT_PER - 1) / (256 * dev::MCOMPACT_PER);
   hipLaunchKernelGGL(dev::wc_mrow_compact, dim3((unsigned)blocks), dim3(256), 0, s, rows, state, cnt, first, T, rbase,
                      bbase, W, out, out_n, slot_id, out_cap);
+}
+void launch_mrow_insert_emit(const MRow* rows, uint64_t R, const uint8_t* bytes, const uint64_t* rbase,
+                             const uint64_t* bbase, uint32_t W, uint32_t* state, uint32_t* slot_idx, uint64_t T,
+                             MRow* out, unsigned long long* out_n, uint64_t cap, uint32_t* ids, uint32_t* ids_self,
+                             uint32_t self, uint64_t reg, hipStream_t s) {
+  WC_CHECK(R < 0xFFFFFFFFull && T <= 0xFFFFFFFFull && (T & (T - 1)) == 0, "insert_emit: 32-bit row ids, T a power of two");
+  WC_CHECK(!ids_self || reg > 0, "insert_emit: a region size with ids_self");
+  if (R)
+    hipLaunchKernelGGL(dev::wc_mrow_insert_emit, dev::mgrid(R), dim3(256), 0, s, rows, R, bytes, rbase, bbase, W, state,
+                       slot_idx, T, out, out_n, cap, ids, ids_self, self, reg);
 }
 void launch_mrow_to_cols(const MRow* rows, uint64_t n, const uint64_t* rbase, const uint64_t* bbase, uint32_t W,
                          uint64_t* k0, uint64_t* k1, uint64_t* cnt, uint64_t* first, uint64_t* soff, uint32_t* slen,
