@@ -182,7 +182,7 @@ constexpr int HOT_PART_TOP = 32;     // candidates kept per partition (the HOT_K
 constexpr int HOT_GROUP_SLOTS = WC_HOT_GS;
 constexpr int HOT_GROUPS = MAP_SLOTS / HOT_GROUP_SLOTS;
 static_assert(HOT_GROUP_SLOTS == 2 || HOT_GROUP_SLOTS == 4, "hot-table groups of 2 or 4 slots");
-constexpr int HOT_SEL_BINS = 4096;  // sampled-count histogram bins (counts clamp to the last)
+constexpr int HOT_SEL_BINS = 256;  // sampled-count histogram bins (counts clamp to the last: a partition holds < 1 word sampled 255+ times on Zipf(1.0) at 100k words)
 
 // In-kernel phase stamps of the map (diagnostic build, WC_MAP_STAMPS=1): shares
 // of wave lifetime per phase, then counters.

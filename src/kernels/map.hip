@@ -442,12 +442,10 @@ __global__ void __launch_bounds__(MAP_THREADS) wc_hot_sample(MapArgs a, HotArgs 
 }
 
 // ------------------------------------------------------------------ selection
-// Block-wide (NT threads) selection threshold over a count histogram of
-// HOT_SEL_BINS bins in LDS: t = the smallest count >= 1 whose words (counted
-// >= t) number <= limit (the last bin when even that holds more), cum = the
-// words counted >= t.  Thread i owns bins [B i, B i + B), B = ceil(bins / NT)
-// (bins past the histogram count 0); a reverse block scan gives the words
-// counted >= each bin.  sc: 18 words of LDS scratch.
+// Selection threshold over a count histogram of HOT_SEL_BINS bins in LDS:
+// t = the smallest count >= 1 whose words (counted >= t) number <= limit (the
+// last bin when even that holds more), cum = the words counted >= t
+// (wave_count_threshold below).
 constexpr int SEL_BINS = HOT_SEL_BINS;
 // hist[bin] += 1 for every lane with `valid`, one LDS atomic per distinct bin
 // of the wave: sampled counts crowd the low bins, and 64 lanes adding to one
@@ -461,46 +459,6 @@ __device__ __forceinline__ void hist_add_wave(uint32_t* hist, uint32_t bin, bool
     todo &= ~same;
   }
 }
-template <int NT>
-__device__ void count_threshold(const uint32_t* hist, uint32_t limit, uint32_t* sc, uint32_t& t_out,
-                                uint32_t& cum_out) {
-  constexpr int B = (SEL_BINS + NT - 1) / NT, NW = NT / 64;
-  static_assert(NT % 64 == 0 && NW <= 16, "threshold: whole waves, <= 16");
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  uint32_t b[B], own = 0;
-#pragma unroll
-  for (int i = 0; i < B; ++i) own += b[i] = B * tid + i < SEL_BINS ? hist[B * tid + i] : 0u;
-  uint32_t x = own;  // inclusive scan from the top: words in bins >= 4 tid within the wave
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_down(x, o);
-    if (lane + o < 64) x += y;
-  }
-  if (lane == 0) sc[wave] = x;
-  if (tid == 0) sc[16] = SEL_BINS;
-  __syncthreads();
-  uint32_t above = 0;  // words in the waves above this one
-  for (int w = wave + 1; w < NW; ++w) above += sc[w];
-  const uint32_t suf0 = x + above;  // words counted >= B tid
-  uint32_t suf = suf0, t = SEL_BINS;
-#pragma unroll
-  for (int i = 0; i < B; ++i) {  // words counted >= bin B tid + i
-    if (t == SEL_BINS && suf <= limit && B * tid + i >= 1 && B * tid + i < SEL_BINS) t = B * tid + i;
-    suf -= b[i];
-  }
-  if (t < SEL_BINS) atomicMin(&sc[16], t);
-  __syncthreads();
-  const uint32_t tt = sc[16] == SEL_BINS ? SEL_BINS - 1 : sc[16];
-  if ((uint32_t)tid == tt / B) {
-    uint32_t cum = suf0;
-    for (uint32_t i = 0; i < tt % B; ++i) cum -= b[i];
-    sc[17] = cum;
-  }
-  __syncthreads();
-  t_out = tt;
-  cum_out = sc[17];
-  __syncthreads();  // sc is reusable
-}
-
 // ------------------------------------------------------------------ hot-table image
 // The partition's words into its GPP groups (2 GPP slots) of the table image,
 // by ONE wave of the partition's wc_hot_merge block: lane i holds candidate i;
@@ -517,7 +475,7 @@ __device__ void count_threshold(const uint32_t* hist, uint32_t limit, uint32_t* 
 static_assert(HOT_PART_TOP <= 64 && 2 * GPP <= 64, "partition placement: one wave");
 static_assert(HOT_PARTS == 256, "a sampled word's partition rides in its fingerprint's top byte");
 __device__ void place_partition(const HotArgs& h, uint32_t part, uint32_t n, const uint32_t* oc, const uint64_t* osig,
-                                const uint64_t* oside) {
+                                const uint64_t* oside, uint32_t* ord) {
   const uint32_t lane = __lane_id();
   const bool have = lane < n;
   const uint32_t c = have ? oc[lane] : 0u;
@@ -537,54 +495,60 @@ __device__ void place_partition(const HotArgs& h, uint32_t part, uint32_t n, con
       if (two_word(sg) && (sd >> 59) == 0) ok = false;
     }
   }
-  // one word per lane for the scalar loop: a | b << 4 | two-slot << 8 | placeable << 9
+  // one word per candidate for the scalar loop: a | b << 4 | two-slot << 8 |
+  // placeable << 9 | its lane << 10
   const uint32_t info = (g1 & (GPP - 1)) | ((g2 & (GPP - 1)) << 4) | ((lng || two_word(sg)) ? 1u << 8 : 0u) |
-                        (ok ? 1u << 9 : 0u);
-  // rank in count order (ties: lower index first)
+                        (ok ? 1u << 9 : 0u) | (lane << 10);
+  // rank in count order (ties: lower index first); lane r of `sinfo` then
+  // holds the info of the rank-r candidate, so step r reads it with one readlane
   uint32_t rank = 0;
   for (uint32_t j = 0; j < n; ++j) {
     const uint32_t cj = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)j);
     rank += (cj > c || (cj == c && j < lane)) ? 1u : 0u;
   }
+  if (have) ord[rank] = info;
+  wave_sync();
+  const uint32_t sinfo = have ? ord[lane] : 0u;
   uint32_t st = 0;           // group states, 2 bits each (uniform)
-  uint32_t owner = 0xFFu;    // lane s < 2 GPP: the candidate in slot s (0xFF: empty)
+  uint64_t alt = 0;          // slot s: its one-slot occupant's other group (4 bits each, uniform)
+  uint32_t owner = 0xFFu;    // lane s < 2 GPP: the candidate (lane) in slot s (0xFF: empty)
+  static_assert(2 * GPP * 4 <= 64, "placement: 4 bits of `alt` per slot");
   constexpr uint32_t FULL = (uint32_t)(0xAAAAAAAAull & ((1ull << (2 * GPP)) - 1ull));  // every group at 2 or 3: bit 1 of each field
   auto gst = [&](uint32_t g) { return (st >> (2 * g)) & 3u; };
-  auto set_owner = [&](uint32_t slot, uint32_t who) { if (lane == slot) owner = who; };
+  auto set_alt = [&](uint32_t s, uint32_t g) { alt = (alt & ~(0xFull << (4 * s))) | ((uint64_t)g << (4 * s)); };
   for (uint32_t r = 0; r < n; ++r) {
     if ((st & FULL) == FULL) break;  // no free slot left: no word (or move) can be placed any more
-    const uint64_t m = __ballot(have && rank == r);
-    const uint32_t i = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-    const uint32_t ii = (uint32_t)__builtin_amdgcn_readlane((int)info, (int)i);
+    const uint32_t ii = (uint32_t)__builtin_amdgcn_readlane((int)sinfo, (int)r);
     if (!(ii & (1u << 9))) continue;
-    const uint32_t ai = ii & 15u, bi = (ii >> 4) & 15u;
+    const uint32_t i = ii >> 10, ai = ii & 15u, bi = (ii >> 4) & 15u;
+    const uint32_t sa = gst(ai), sb = gst(bi);
     if (ii & (1u << 8)) {  // an empty group, g1 first
-      const uint32_t g = gst(ai) == 0 ? ai : (gst(bi) == 0 ? bi : 0xFFu);
+      const uint32_t g = sa == 0 ? ai : (sb == 0 ? bi : 0xFFu);
       if (g == 0xFFu) continue;
       st |= 3u << (2 * g);
-      set_owner(2 * g, i);
-      set_owner(2 * g + 1, i);
+      if ((lane >> 1) == g) owner = i;
       continue;
     }
-    const uint32_t sa = gst(ai), sb = gst(bi);
     const uint32_t fa = sa == 3 ? 0u : 2u - sa, fb = sb == 3 ? 0u : 2u - sb;
     if (fa | fb) {  // a free slot of the emptier group (slots fill first, then second)
-      const uint32_t g = fb > fa ? bi : ai, sg0 = gst(g);
-      set_owner(2 * g + sg0, i);
+      const uint32_t g = fb > fa ? bi : ai, s = 2 * g + gst(g);
+      if (lane == s) owner = i;
+      set_alt(s, g == ai ? bi : ai);
       st += 1u << (2 * g);
       continue;
     }
     // both full: move a one-slot occupant to its other group if that has room
     for (int k = 0; k < 4; ++k) {
-      const uint32_t g = k < 2 ? ai : bi, slot = 2 * g + (k & 1);
+      const uint32_t g = k < 2 ? ai : bi, s = 2 * g + (k & 1);
       if (gst(g) == 3) continue;
-      const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)owner, (int)slot);
-      const uint32_t oi = (uint32_t)__builtin_amdgcn_readlane((int)info, (int)o);
-      const uint32_t alt = (oi & 15u) == g ? (oi >> 4) & 15u : oi & 15u, salt = gst(alt);
-      if (salt >= 2) continue;
-      set_owner(2 * alt + salt, o);
-      st += 1u << (2 * alt);
-      set_owner(slot, i);
+      const uint32_t ag = (uint32_t)(alt >> (4 * s)) & 15u, sag = gst(ag);
+      if (sag >= 2) continue;
+      const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)owner, (int)s), s2 = 2 * ag + sag;
+      if (lane == s2) owner = o;
+      set_alt(s2, g);
+      st += 1u << (2 * ag);
+      if (lane == s) owner = i;
+      set_alt(s, g == ai ? bi : ai);
       break;
     }
   }
@@ -613,12 +577,12 @@ struct HotMergeLds {
   uint64_t sig[MERGE_SLOTS];
   uint64_t side[MERGE_SLOTS];
   uint32_t cnt[MERGE_SLOTS];
-  uint32_t hist[SEL_BINS];
-  uint32_t sc[18];
+  alignas(16) uint32_t hist[SEL_BINS];
   uint32_t nout, nties;
   // the partition's candidates (place_partition): count, signature, side word
   uint32_t oc[HOT_PART_TOP];
   uint64_t osig[HOT_PART_TOP], oside[HOT_PART_TOP];
+  uint32_t ord[HOT_PART_TOP];  // place_partition: candidates' info in count order
 };
 __device__ __forceinline__ void merge_insert(HotMergeLds& L, const HotEnt& e) {
   uint32_t s = (uint32_t)(e.fp >> 20) & (MERGE_SLOTS - 1);
@@ -639,6 +603,40 @@ __device__ __forceinline__ void merge_insert(HotMergeLds& L, const HotEnt& e) {
     s = (s + 1) & (MERGE_SLOTS - 1);
   }
 }
+// The threshold by one wave, no block barrier (every wave may call it and gets
+// the same result): SEL_BINS = 4 bins per lane, a shuffle suffix scan.  (A
+// block-wide scan over 4096 bins took 4 us of the merge's ~20.)
+static_assert(SEL_BINS == 4 * 64, "wave threshold: 4 bins per lane");
+__device__ __forceinline__ void wave_count_threshold(const uint32_t* hist, uint32_t limit, uint32_t& t_out,
+                                                     uint32_t& cum_out) {
+  const uint32_t lane = __lane_id();
+  const uint4 b = reinterpret_cast<const uint4*>(hist)[lane];
+  const uint32_t own = b.x + b.y + b.z + b.w;
+  uint32_t x = own;  // words counted >= bin 4 lane (inclusive suffix over the lanes)
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_down(x, o);
+    if (lane + o < 64) x += y;
+  }
+  // words counted >= each of this lane's bins; the first bin >= 1 at or under the limit
+  const uint32_t s0 = x, s1 = s0 - b.x, s2 = s1 - b.y, s3 = s2 - b.z;
+  const uint32_t i0 = 4 * lane;
+  uint32_t t = SEL_BINS, cum = 0;
+  if (s3 <= limit && i0 + 3 >= 1) { t = i0 + 3; cum = s3; }
+  if (s2 <= limit && i0 + 2 >= 1) { t = i0 + 2; cum = s2; }
+  if (s1 <= limit && i0 + 1 >= 1) { t = i0 + 1; cum = s1; }
+  if (s0 <= limit && i0 >= 1) { t = i0; cum = s0; }
+  // the smallest such bin over the wave (suffixes only shrink with the bin)
+  const uint64_t has = __ballot(t < SEL_BINS);
+  if (has) {
+    const int l = __ffsll((unsigned long long)has) - 1;
+    t_out = (uint32_t)__builtin_amdgcn_readlane((int)t, l);
+    cum_out = (uint32_t)__builtin_amdgcn_readlane((int)cum, l);
+  } else {  // even the last bin holds more than the limit
+    t_out = SEL_BINS - 1;
+    cum_out = (uint32_t)__builtin_amdgcn_readlane((int)s3, 63);
+  }
+}
+
 __global__ void __launch_bounds__(1024) wc_hot_merge(HotArgs h) {
   __shared__ HotMergeLds L;
   HotClock clk(1);
@@ -678,7 +676,7 @@ __global__ void __launch_bounds__(1024) wc_hot_merge(HotArgs h) {
   __syncthreads();
   uint32_t t, cum;
   clk.at(3);  // histogram
-  count_threshold<1024>(L.hist, HOT_PART_TOP, L.sc, t, cum);
+  wave_count_threshold(L.hist, HOT_PART_TOP, t, cum);
   clk.at(4);  // threshold
   const uint32_t ties = t > 1 ? HOT_PART_TOP - min(cum, (uint32_t)HOT_PART_TOP) : 0u;
   for (int s = tid; s < MERGE_SLOTS; s += 1024) {
@@ -717,7 +715,7 @@ __global__ void __launch_bounds__(1024) wc_hot_merge(HotArgs h) {
     if (tid < 2 * GPP) h.image[slot_of(part * GPP + tid / 2, tid & 1)] = 0;
     return;
   }
-  if (tid < 64) place_partition(h, part, min(L.nout, (uint32_t)HOT_PART_TOP), L.oc, L.osig, L.oside);
+  if (tid < 64) place_partition(h, part, min(L.nout, (uint32_t)HOT_PART_TOP), L.oc, L.osig, L.oside, L.ord);
   clk.at(6);  // placed
 }
 
