@@ -58,7 +58,7 @@ int main(int argc, char** argv) {
     uint32_t t = 4095, suf = 0;
     for (int b = 4095; b >= 1; --b) { if (suf + hist[b] > BUDGET) { t = b + 1; break; } suf += hist[b]; t = b; }
     for (auto i : cand) if (c[i] / slots(i) >= t) take.push_back(i);
-  } else if (mode == 7 || mode == 9) {  // the kernel's selection (count_threshold): BUDGET words by sampled count, ties at t - 1 while room
+  } else if (mode == 7 || mode == 9) {  // the kernel's selection (map.hip wave_count_threshold): BUDGET words by sampled count, ties at t - 1 while room
     std::vector<uint32_t> hist(4096, 0);
     for (auto i : cand) hist[std::min(c[i], 4095u)]++;
     uint32_t t = 4095, suf = 0;
