@@ -361,12 +361,20 @@ __device__ void settle_new_long(RedLds& L, const ReduceArgs& a, uint32_t b) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   static_assert(TAB_SLOTS == 4 * RED_THREADS, "settle: 4 slots per thread");
   uint32_t need[4], mine = 0;
+  // the four slots' references loaded together (one device round trip, not one per slot)
+  uint64_t so[4];
+  uint32_t sl[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    so[j] = a.tab.sref_off[sbase + 4 * tid + j];
+    sl[j] = a.tab.sref_len[sbase + 4 * tid + j];
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int s = 4 * tid + j;
     need[j] = 0;
-    if (slot_tag(L.grp, s) > TAG_PENDING && key_is_hashed(slot_k1(L.grp, s)) && (a.tab.sref_off[sbase + s] & SREF_TEXT)) {
-      const uint32_t len = a.tab.sref_len[sbase + s];
+    if (slot_tag(L.grp, s) > TAG_PENDING && key_is_hashed(slot_k1(L.grp, s)) && (so[j] & SREF_TEXT)) {
+      const uint32_t len = sl[j];
       need[j] = len == SREF_POISON ? 0u : ((len + 7u) & ~7u) | 1u;  // | 1: a new word (even of length 0)
     }
     mine += need[j] & ~1u;
@@ -392,8 +400,8 @@ __device__ void settle_new_long(RedLds& L, const ReduceArgs& a, uint32_t b) {
   for (int j = 0; j < 4; ++j) {
     if (!need[j]) continue;
     const int s = 4 * tid + j;
-    const uint64_t to = a.tab.sref_off[sbase + s] & ~SREF_TEXT;
-    const uint32_t len = a.tab.sref_len[sbase + s];
+    const uint64_t to = so[j] & ~SREF_TEXT;
+    const uint32_t len = sl[j];
     if (ovf) {
       a.tab.sref_off[sbase + s] = 0;
       a.tab.sref_len[sbase + s] = SREF_POISON;
@@ -935,18 +943,31 @@ __device__ __forceinline__ void add_fo_hist(const RedLds& L, const ReduceArgs& a
 // without return, overlapped with the rest of the reduce) and their count.
 __device__ __forceinline__ void add_bm_bits(const RedLds& L, const ReduceArgs& a) {
   if (!a.bm) return;
+  // the thread's TAB_SLOTS / RED_THREADS slots: every returning OR issued before
+  // any result is looked at (one device round trip, not one per slot: in a
+  // loop that tested each OR before the next, the bits took ~33 us of a v1m /
+  // long30 bucket's ~450 us, profiles/r6_session.md §11)
+  constexpr int PER = TAB_SLOTS / RED_THREADS;
   bool range = false;
-  for (int s = threadIdx.x; s < TAB_SLOTS; s += RED_THREADS) {
+  unsigned long long m[PER], old[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int s = threadIdx.x + j * RED_THREADS;
+    m[j] = 0;
+    old[j] = 0;
     if (slot_tag(L.grp, s) <= TAG_PENDING) continue;
     const uint64_t p = L.first[s] >> a.bm_shift;
     if (p >= a.bm_pos_end) {
       range = true;
       continue;
     }
-    const unsigned long long m = 1ull << (p & 63);
-    if (__hip_atomic_fetch_or(&a.bm[p >> 6], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & m) range = true;
+    m[j] = 1ull << (p & 63);
+    old[j] = __hip_atomic_fetch_or(&a.bm[p >> 6], m[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_fetch_add(&a.bm_lines[p >> 9], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    if (old[j] & m[j]) range = true;
   if (range) atomicOr(a.bm_ctl, 1ull << 63);  // the order's redo flag (out of bounds, or a shared position)
   if (threadIdx.x == 0 && L.occupied) atomicAdd(a.bm_ctl, (unsigned long long)L.occupied);
 }
