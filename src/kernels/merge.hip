@@ -182,15 +182,27 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
   const bool live = !occ || occ[r0 >> TAB_SLOTS_LOG2] != 0;
   uint32_t own[PER], mine = 0;
   unsigned long long lr[PER], lb[PER];
+  // every row's key, count and first offset loaded at once (one round trip,
+  // not gated on the occupancy word or on k1; an empty bucket's slots hold
+  // stale values that are never used)
+  uint64_t rk0[PER], rk1[PER], rc[PER], rf[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint64_t i = min(r0 + threadIdx.x + (uint64_t)j * 256, n - 1);
+    rk0[j] = k0[i];
+    rk1[j] = k1[i];
+    rc[j] = cnt[i];
+    rf[j] = first[i];
+  }
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const uint64_t i = r0 + threadIdx.x + (uint64_t)j * 256;
     own[j] = OWN_MAX;
     uint32_t nb = 0;
     if (i < n) {
-      if (live && (!occ || k1[i] != K1_EMPTY)) {
-        own[j] = owner_of(place_hash(k0[i], k1[i]), W);
-        if (key_is_hashed(k1[i])) nb = (slen[i] + 7u) & ~7u;
+      if (live && (!occ || rk1[j] != K1_EMPTY)) {
+        own[j] = owner_of(place_hash(rk0[j], rk1[j]), W);
+        if (key_is_hashed(rk1[j])) nb = (slen[i] + 7u) & ~7u;
         ++mine;
       } else if (send_pos) {
         send_pos[i] = 0xFFFFFFFFu;  // an empty slot: no id comes back for it
@@ -228,7 +240,7 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
     if (fixed) {  // the row and its bytes must fit the owner's regions
       const uint64_t rp = base[2 * o] + lr[j] - o * reg_rows;
       const uint64_t bp = base[2 * o + 1] + lb[j] - o * reg_bytes;
-      const uint64_t nb = key_is_hashed(k1[i]) ? ((slen[i] + 7u) & ~7u) : 0u;
+      const uint64_t nb = key_is_hashed(rk1[j]) ? ((slen[i] + 7u) & ~7u) : 0u;
       if (rp >= reg_rows || bp + nb > reg_bytes) {
         atomicOr(ovf, 4u);  // wc_merge_check's capacity bit
         if (send_pos) send_pos[i] = 0xFFFFFFFFu;
@@ -236,10 +248,10 @@ __global__ void __launch_bounds__(256) wc_owner_scatter(const uint64_t* k0, cons
       }
     }
     MRow r;
-    r.k0 = k0[i];
-    r.k1 = k1[i];
-    r.cnt = cnt[i];
-    r.first = first[i];
+    r.k0 = rk0[j];
+    r.k1 = rk1[j];
+    r.cnt = rc[j];
+    r.first = rf[j];
     r.aoff = 0;
     r.alen = 0;
     const bool mine = o == self.rank;  // planned: straight into this rank's receive regions
