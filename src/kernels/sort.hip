@@ -864,7 +864,19 @@ __global__ void __launch_bounds__(256) wc_bm_place(OrderSrc src, uint64_t rows, 
   rows = bm_rows(src, rows);
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < rows; i += (uint64_t)gridDim.x * 256) {
     uint64_t f;
-    if (!bm_row(src, i, f)) continue;
+    // a table slot's words loaded at once, not behind its occupancy / k1 tests
+    // (one round trip; i < rows stays inside the table, stale slots go unused)
+    uint64_t tk0 = 0, tk1 = 0, tcnt = 0;
+    if (src.table) {
+      const uint32_t occ = src.t.occupancy[i >> TAB_SLOTS_LOG2];
+      tk1 = src.t.k1[i];
+      f = src.t.first[i];
+      tk0 = src.t.k0[i];
+      tcnt = src.t.cnt[i];
+      if (occ == 0 || tk1 == K1_EMPTY) continue;
+    } else {
+      f = src.first[i];
+    }
     const uint64_t p = f >> shift;
     if (p >= pos_end) continue;
     const uint64_t line = p / BM_LINE_BITS;
@@ -882,10 +894,9 @@ __global__ void __launch_bounds__(256) wc_bm_place(OrderSrc src, uint64_t rows, 
     if (!bounds_ok(bnd, BND_BM_PLACE, o)) continue;
     ulonglong2 w[4];
     if (src.table) {
-      const uint64_t k1 = src.t.k1[i];
-      const bool h = key_is_hashed(k1);
-      w[0] = make_ulonglong2(src.t.k0[i], k1);
-      w[1] = make_ulonglong2(src.t.cnt[i], f);
+      const bool h = key_is_hashed(tk1);
+      w[0] = make_ulonglong2(tk0, tk1);
+      w[1] = make_ulonglong2(tcnt, f);
       w[2] = make_ulonglong2(h ? src.t.sref_off[i] : 0, h ? src.t.sref_len[i] : 0);
     } else {
       w[0] = make_ulonglong2(src.k0[i], src.k1[i]);

@@ -10,3 +10,5 @@ for args in "--vocab 1000000" "--vocab 1000000 --long-frac 0.3" ""; do
 done
 bash tools/kstats_ab.sh --vocab 1000000 > gpurun_out/bm_ks.txt 2>&1 || exit 1
 grep -E "==|wc_reduce|wc_bm|wc_map" gpurun_out/bm_ks.txt
+bash tools/kstats_ab.sh > gpurun_out/bm_ks100k.txt 2>&1 || exit 1
+grep -E "==|wc_fo" gpurun_out/bm_ks100k.txt
