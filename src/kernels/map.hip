@@ -947,11 +947,13 @@ __global__ void __launch_bounds__(MAP_THREADS, MAP_WAVES / 4) wc_map(MapArgs a, 
     // trip; a tail of <= 64 entries takes the one-entry step.  General form:
     // any length (two-word signatures are confirmed by their group's side
     // word, LONG words deferred to the round end).
-    auto step = [&](uint32_t j, uint32_t hi, uint32_t cut, auto two_c, auto mixed_c, auto any_c) {
+    auto step = [&](uint32_t j, uint32_t hi, uint32_t cut, auto two_c, auto mixed_c, auto any_c, auto full_c) {
       // ANY: entries of any length (the > MAP_LIST rounds); otherwise the
       // other class only (8 bytes or longer: k0 is the first window as read)
       constexpr bool TWO = decltype(two_c)::value, MIXED = decltype(mixed_c)::value, ANY = decltype(any_c)::value;
-      const bool h1 = j + lane < hi, h2 = TWO && j + 64 + lane < hi;
+      constexpr bool FULL = decltype(full_c)::value;  // j + 128 <= hi: every lane holds two entries
+      static_assert(!FULL || TWO, "full steps take two entries per lane");
+      const bool h1 = FULL || j + lane < hi, h2 = TWO && (FULL || j + 64 + lane < hi);
       const uint32_t r1 = list[j + lane], r2 = TWO ? list[j + 64 + lane] : 0u;  // unconditional (see step_short)
       const uint32_t e1 = h1 ? r1 : 0u, e2 = h2 ? r2 : 0u;
       if (WC_MAP_ABLATE == 7) {
@@ -1036,9 +1038,11 @@ __global__ void __launch_bounds__(MAP_THREADS, MAP_WAVES / 4) wc_map(MapArgs a, 
     // key (bytes | len << 56): one 8-byte window (three LDS dwords, two
     // funnels), no tail, no side-word confirmation, and every miss a 16-byte
     // record candidate.  3 of 4 tokens of English-like text take it.
-    auto step_short = [&](uint32_t j, uint32_t hi, uint32_t cut, auto two_c, auto mixed_c) {
+    auto step_short = [&](uint32_t j, uint32_t hi, uint32_t cut, auto two_c, auto mixed_c, auto full_c) {
       constexpr bool TWO = decltype(two_c)::value, MIXED = decltype(mixed_c)::value;
-      const bool h1 = j + lane < hi, h2 = TWO && j + 64 + lane < hi;
+      constexpr bool FULL = decltype(full_c)::value;  // j + 128 <= hi
+      static_assert(!FULL || TWO, "full steps take two entries per lane");
+      const bool h1 = FULL || j + lane < hi, h2 = TWO && (FULL || j + 64 + lane < hi);
       // unconditional entry reads (no exec-mask branch): past `hi` they read a
       // later entry, the next wave's list or the deferred lists — inside MapLds, and masked by h1 / h2
       const uint32_t r1 = list[j + lane], r2 = TWO ? list[j + 64 + lane] : 0u;
@@ -1130,15 +1134,20 @@ __global__ void __launch_bounds__(MAP_THREADS, MAP_WAVES / 4) wc_map(MapArgs a, 
         if (lane + 64 < co) list[ob0 + 64 + lane] = (uint16_t)d1;
       }
       uint32_t ks = cs + ks0, ko = ob0 + co + ko0, sb = sbits, ob = obits;
+      // the lane's byte base, opaque: the entry's position q = base | i also
+      // feeds alignbit (which reads q's low 5 bits = i), so the entry is one
+      // lshl_or (known low zero bits would fold q back to i and add an or3)
+      uint32_t pb = pbase;
+      asm volatile("" : "+v"(pb));
       while (sb) {
-        const uint32_t i = __ffs(sb) - 1;
+        const uint32_t q = pb | (uint32_t)(__ffs(sb) - 1);
         sb &= sb - 1;
-        list[ks++] = (uint16_t)((pbase + i) | (ffbl_raw(__builtin_amdgcn_alignbit(dhi, dlo, i)) << 11));
+        list[ks++] = (uint16_t)(q | (ffbl_raw(__builtin_amdgcn_alignbit(dhi, dlo, q)) << 11));
       }
       while (ob) {
-        const uint32_t i = __ffs(ob) - 1;
+        const uint32_t q = pb | (uint32_t)(__ffs(ob) - 1);
         ob &= ob - 1;
-        list[ko++] = (uint16_t)((pbase + i) | (ffbl_raw(__builtin_amdgcn_alignbit(dhi, dlo, i)) << 11));
+        list[ko++] = (uint16_t)(q | (ffbl_raw(__builtin_amdgcn_alignbit(dhi, dlo, q)) << 11));
       }
       wave_sync();
       clk.lap(MS_LIST);
@@ -1159,14 +1168,14 @@ __global__ void __launch_bounds__(MAP_THREADS, MAP_WAVES / 4) wc_map(MapArgs a, 
       constexpr std::false_type F{}, P{};
       uint32_t j = 0;
       if (cs && ns >= 128) {
-        step_short(0u, ns, cs, T, M);
+        step_short(0u, ns, cs, T, M, T);
         j = 128;
       }
-      for (; j + 128 <= ns; j += 128) step_short(j, ns, 0u, T, P);
+      for (; j + 128 <= ns; j += 128) step_short(j, ns, 0u, T, P, T);
       if (j < ns && (j < cs || last)) {
-        if (j < cs) step_short(j, ns, cs, T, M);
-        else if (j + 64 < ns) step_short(j, ns, 0u, T, P);
-        else step_short(j, ns, 0u, F, P);
+        if (j < cs) step_short(j, ns, cs, T, M, F);
+        else if (j + 64 < ns) step_short(j, ns, 0u, T, P, F);
+        else step_short(j, ns, 0u, F, P, F);
         j = ns;
       }
       cs_from = j;
@@ -1174,14 +1183,14 @@ __global__ void __launch_bounds__(MAP_THREADS, MAP_WAVES / 4) wc_map(MapArgs a, 
       const uint32_t ocut = ob0 + co;
       j = ob0;
       if (co && no_end >= ob0 + 128) {
-        step(j, no_end, ocut, T, M, F);
+        step(j, no_end, ocut, T, M, F, T);
         j += 128;
       }
-      for (; j + 128 <= no_end; j += 128) step(j, no_end, 0u, T, P, F);
+      for (; j + 128 <= no_end; j += 128) step(j, no_end, 0u, T, P, F, T);
       if (j < no_end && (j < ocut || last)) {
-        if (j < ocut) step(j, no_end, ocut, T, M, F);
-        else if (j + 64 < no_end) step(j, no_end, 0u, T, P, F);
-        else step(j, no_end, 0u, F, P, F);
+        if (j < ocut) step(j, no_end, ocut, T, M, F, F);
+        else if (j + 64 < no_end) step(j, no_end, 0u, T, P, F, F);
+        else step(j, no_end, 0u, F, P, F, F);
         j = no_end;
       }
       co_from = j;
@@ -1196,8 +1205,8 @@ __global__ void __launch_bounds__(MAP_THREADS, MAP_WAVES / 4) wc_map(MapArgs a, 
       // words): the carried entries first, then rounds of MAP_LIST entries of
       // the unit in stream order, every entry on the general step
       // all carried: the cut past them (one general step per class, < 128 entries each)
-      if (cs) step_short(cs_from, cs_from + cs, MAP_LIST, std::true_type{}, std::true_type{});
-      if (co) step(co_from, co_from + co, MAP_LIST, std::true_type{}, std::true_type{}, std::false_type{});
+      if (cs) step_short(cs_from, cs_from + cs, MAP_LIST, std::true_type{}, std::true_type{}, std::false_type{});
+      if (co) step(co_from, co_from + co, MAP_LIST, std::true_type{}, std::true_type{}, std::false_type{}, std::false_type{});
       cs = co = 0;
       if (ndef) {
         run_deferred();
@@ -1218,8 +1227,8 @@ __global__ void __launch_bounds__(MAP_THREADS, MAP_WAVES / 4) wc_map(MapArgs a, 
         const uint32_t round_n = min(wave_total - base, (uint32_t)MAP_LIST);
         clk.lap(MS_LIST);
         uint32_t j = 0;
-        for (; j + 64 < round_n; j += 128) step(j, round_n, 0u, std::true_type{}, std::false_type{}, std::true_type{});
-        if (j < round_n) step(j, round_n, 0u, std::false_type{}, std::false_type{}, std::true_type{});
+        for (; j + 64 < round_n; j += 128) step(j, round_n, 0u, std::true_type{}, std::false_type{}, std::true_type{}, std::false_type{});
+        if (j < round_n) step(j, round_n, 0u, std::false_type{}, std::false_type{}, std::true_type{}, std::false_type{});
         if (ndef) {
           run_deferred();
           clk.lap(MS_SLOW);
