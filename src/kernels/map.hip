@@ -902,6 +902,7 @@ __global__ void __launch_bounds__(MAP_THREADS, MAP_WAVES / 4) wc_map(MapArgs a, 
   // class in the next list; an entry below a step's `cut` index reads the
   // previous slot and offsets.
   uint32_t cs = 0, cs_from = 0, co = 0, co_from = 0;  // carried short / other entries and where they wait
+  uint32_t pr1 = 0, pr2 = 0;  // a plain full step's entries, read one step ahead
   uint32_t u = grab();
   prefetch(u);
   uint32_t nu = u == NONE ? NONE : grab();
@@ -954,7 +955,9 @@ __global__ void __launch_bounds__(MAP_THREADS, MAP_WAVES / 4) wc_map(MapArgs a, 
       constexpr bool FULL = decltype(full_c)::value;  // j + 128 <= hi: every lane holds two entries
       static_assert(!FULL || TWO, "full steps take two entries per lane");
       const bool h1 = FULL || j + lane < hi, h2 = TWO && (FULL || j + 64 + lane < hi);
-      const uint32_t r1 = list[j + lane], r2 = TWO ? list[j + 64 + lane] : 0u;  // unconditional (see step_short)
+      // unconditional (see step_short); a plain full step's entries were read by the step before it
+      constexpr bool PRE = FULL && !MIXED;
+      const uint32_t r1 = PRE ? pr1 : list[j + lane], r2 = PRE ? pr2 : TWO ? list[j + 64 + lane] : 0u;
       const uint32_t e1 = h1 ? r1 : 0u, e2 = h2 ? r2 : 0u;
       if (WC_MAP_ABLATE == 7) {
         sink ^= e1 ^ e2;
@@ -965,6 +968,10 @@ __global__ void __launch_bounds__(MAP_THREADS, MAP_WAVES / 4) wc_map(MapArgs a, 
       uint64_t w10, w11, w20 = 0, w21 = 0;
       window16(bufw, q1 + (old1 ? pbo : cbo), w10, w11);
       if (TWO) window16(bufw, q2 + (old2 ? pbo : cbo), w20, w21);
+      if (PRE) {  // the next step's entries, beside this step's windows (past the list: inside MapLds, unused)
+        pr1 = list[j + 128 + lane];
+        pr2 = list[j + 192 + lane];
+      }
       if (WC_MAP_ABLATE == 1) {
         sink ^= w10 ^ w21;
         return;
@@ -1045,7 +1052,8 @@ __global__ void __launch_bounds__(MAP_THREADS, MAP_WAVES / 4) wc_map(MapArgs a, 
       const bool h1 = FULL || j + lane < hi, h2 = TWO && (FULL || j + 64 + lane < hi);
       // unconditional entry reads (no exec-mask branch): past `hi` they read a
       // later entry, the next wave's list or the deferred lists — inside MapLds, and masked by h1 / h2
-      const uint32_t r1 = list[j + lane], r2 = TWO ? list[j + 64 + lane] : 0u;
+      constexpr bool PRE = FULL && !MIXED;  // entries read by the step before (see step)
+      const uint32_t r1 = PRE ? pr1 : list[j + lane], r2 = PRE ? pr2 : TWO ? list[j + 64 + lane] : 0u;
       const uint32_t e1 = h1 ? r1 : 0u, e2 = h2 ? r2 : 0u;
       if (WC_MAP_ABLATE == 7) {
         sink ^= e1 ^ e2;
@@ -1054,6 +1062,10 @@ __global__ void __launch_bounds__(MAP_THREADS, MAP_WAVES / 4) wc_map(MapArgs a, 
       const uint32_t q1 = e1 & 0x7FFu, q2 = e2 & 0x7FFu, n1 = e1 >> 11, n2 = e2 >> 11;
       const bool old1 = MIXED && j + lane < cut, old2 = MIXED && TWO && j + 64 + lane < cut;  // carried entries
       const uint64_t w1 = window8(bufw, q1 + (old1 ? pbo : cbo)), w2 = TWO ? window8(bufw, q2 + (old2 ? pbo : cbo)) : 0ull;
+      if (PRE) {
+        pr1 = list[j + 128 + lane];
+        pr2 = list[j + 192 + lane];
+      }
       if (WC_MAP_ABLATE == 1) {
         sink ^= w1 ^ w2;
         return;
@@ -1171,6 +1183,8 @@ __global__ void __launch_bounds__(MAP_THREADS, MAP_WAVES / 4) wc_map(MapArgs a, 
         step_short(0u, ns, cs, T, M, T);
         j = 128;
       }
+      pr1 = list[j + lane];
+      pr2 = list[j + 64 + lane];
       for (; j + 128 <= ns; j += 128) step_short(j, ns, 0u, T, P, T);
       if (j < ns && (j < cs || last)) {
         if (j < cs) step_short(j, ns, cs, T, M, F);
@@ -1186,6 +1200,8 @@ __global__ void __launch_bounds__(MAP_THREADS, MAP_WAVES / 4) wc_map(MapArgs a, 
         step(j, no_end, ocut, T, M, F, T);
         j += 128;
       }
+      pr1 = list[j + lane];
+      pr2 = list[j + 64 + lane];
       for (; j + 128 <= no_end; j += 128) step(j, no_end, 0u, T, P, F, T);
       if (j < no_end && (j < ocut || last)) {
         if (j < ocut) step(j, no_end, ocut, T, M, F, F);
